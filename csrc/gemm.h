@@ -1,0 +1,189 @@
+// Generic LDS-staged MFMA GEMM core for gfx950 (bf16 in, fp32 accumulate).
+//
+// C[m][n] = sum_k A[m][k] * B[k][n], computed per workgroup tile BM x BN, K stepped by BK.
+// Operands are produced by *loader functors* so the same core serves plain GEMMs, implicit-GEMM
+// convolutions (im2col gather in the loader) and transposed operands:
+//
+//   struct Loader { static constexpr bool KC = ...;           // k-contiguous chunks?
+//                   __device__ uint4 operator()(int mn, int k) const; };
+//   KC = true : returns 8 bf16 {X[mn][k..k+7]}   -> LDS image [MN][BK+8], fragments by ds_read_b128
+//   KC = false: returns 8 bf16 {X[mn..mn+7][k]}  -> LDS image [BK][MN+16], fragments by two
+//               ds_read_b64_tr_b16 (hardware transpose read; no separate transposed weight copies)
+//   Loaders zero-fill out-of-range elements.
+//
+// Epilogue functor: epi(m4, n, f32x4 v) receives rows m4..m4+3 (m4 % 4 == 0) of column n: the
+// mfma_f32_16x16x32 C layout (row = 4*(lane>>4)+r, col = lane&15) gives each lane 4 consecutive
+// rows, which the fused pool epilogue uses as one 2x2 window.
+//
+// Pipeline: register-staged double-buffered LDS (global loads of tile t+1 are issued before the
+// MFMAs on tile t and written after them), one barrier per K-tile.
+#pragma once
+#include "common.h"
+
+namespace tfd {
+
+template <int MN, int BK, bool KC>
+struct LdsTile {
+  static constexpr int PAD = KC ? 8 : 16;                 // elements (16 B / 32 B: bank spread)
+  static constexpr int ROW = KC ? (BK + PAD) : (MN + PAD);
+  static constexpr int ELEMS = KC ? MN * ROW : BK * ROW;
+  static constexpr int CH_PER_ROW = KC ? BK / 8 : MN / 8; // 16-byte chunks per LDS row
+  static constexpr int CHUNKS = MN * BK / 8;
+};
+
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+template <int MN, int BK, bool KC>
+__device__ __forceinline__ bf16x8 read_frag(const bf16* lds, int r0, int kk, int lane) {
+  using L = LdsTile<MN, BK, KC>;
+  if constexpr (KC) {
+    const bf16* p = lds + (r0 + (lane & 15)) * L::ROW + kk + 8 * (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(p);
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p4 = i & 3;
+    const bf16* p0 = lds + (kk + 8 * g + q) * L::ROW + r0 + 4 * p4;
+    const bf16* p1 = p0 + 4 * L::ROW;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p1));
+    s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <int BM, int BN, int BK, class LA, class LB>
+struct GemmSmem {
+  using TA = LdsTile<BM, BK, LA::KC>;
+  using TB = LdsTile<BN, BK, LB::KC>;
+  static constexpr int BYTES = 2 * (TA::ELEMS + TB::ELEMS) * 2;
+};
+
+// One workgroup computes the BM x BN tile at (m0, n0) over k in [kbeg, kend).
+// WM x WN waves (64*WM*WN threads). kend - kbeg should be a multiple of BK except at the global
+// K tail (loaders zero-fill past K).
+template <int BM, int BN, int BK, int WM, int WN, class LA, class LB, class EPI>
+__device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI& epi, int m0, int n0,
+                                           int kbeg, int kend, bf16* smem) {
+  constexpr int NT = 64 * WM * WN;
+  using TA = LdsTile<BM, BK, LA::KC>;
+  using TB = LdsTile<BN, BK, LB::KC>;
+  static_assert(BK % 32 == 0, "BK multiple of 32");
+  static_assert(BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "tile/wave mismatch");
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+  constexpr int CA = (TA::CHUNKS + NT - 1) / NT;
+  constexpr int CB = (TB::CHUNKS + NT - 1) / NT;
+  bf16* As0 = smem;
+  bf16* As1 = smem + TA::ELEMS;
+  bf16* Bs0 = smem + 2 * TA::ELEMS;
+  bf16* Bs1 = Bs0 + TB::ELEMS;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  uint4 ra[CA], rb[CB];
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int c = 0; c < CA; ++c) {
+      const int idx = tid + c * NT;
+      if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
+        const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 8;
+        if constexpr (LA::KC) ra[c] = la(m0 + row, k0 + col);
+        else ra[c] = la(m0 + col, k0 + row);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const int idx = tid + c * NT;
+      if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
+        const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 8;
+        if constexpr (LB::KC) rb[c] = lb(n0 + row, k0 + col);
+        else rb[c] = lb(n0 + col, k0 + row);
+      }
+    }
+  };
+  auto sstore = [&](bf16* As, bf16* Bs) {
+#pragma unroll
+    for (int c = 0; c < CA; ++c) {
+      const int idx = tid + c * NT;
+      if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
+        const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 8;
+        *reinterpret_cast<uint4*>(As + row * TA::ROW + col) = ra[c];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const int idx = tid + c * NT;
+      if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
+        const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 8;
+        *reinterpret_cast<uint4*>(Bs + row * TB::ROW + col) = rb[c];
+      }
+    }
+  };
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
+    gload(kbeg);
+    sstore(As0, Bs0);
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      const bool odd = t & 1;
+      const bf16* As = odd ? As1 : As0;
+      const bf16* Bs = odd ? Bs1 : Bs0;
+      if (t + 1 < nk) gload(kbeg + (t + 1) * BK);
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 32) {
+        bf16x8 a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = read_frag<BM, BK, LA::KC>(As, wm * WTM + 16 * i, kk, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = read_frag<BN, BK, LB::KC>(Bs, wn * WTN + 16 * j, kk, lane);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+      }
+      if (t + 1 < nk) sstore(odd ? As0 : As1, odd ? Bs0 : Bs1);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      epi(m0 + wm * WTM + 16 * i + 4 * (lane >> 4), n0 + wn * WTN + 16 * j + (lane & 15), acc[i][j]);
+}
+
+// ---------------- common loaders ----------------
+__device__ __forceinline__ uint4 zero4() { return make_uint4(0u, 0u, 0u, 0u); }
+
+// Row-major X[rows][ld] bf16; chunk runs along the contiguous (column) dimension.
+//  KC=true : operand index (mn, k) = X[mn][k]   (A as [M][K] or B as [N][K])
+//  KC=false: operand index (mn, k) = X[k][mn]   (A as [K][M] or B as [K][N])
+template <bool KC_>
+struct DenseLoader {
+  static constexpr bool KC = KC_;
+  const uint16_t* __restrict__ x;
+  int ld, mn_lim, k_lim;  // logical bounds (mn < mn_lim, k < k_lim)
+  __device__ __forceinline__ uint4 operator()(int mn, int k) const {
+    if constexpr (KC) {
+      if (mn >= mn_lim || k >= k_lim) return zero4();
+      if (k + 8 <= k_lim) return *reinterpret_cast<const uint4*>(x + (size_t)mn * ld + k);
+      uint16_t t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = (k + j < k_lim) ? x[(size_t)mn * ld + k + j] : 0;
+      return *reinterpret_cast<uint4*>(t);
+    } else {
+      if (k >= k_lim || mn >= mn_lim) return zero4();
+      if (mn + 8 <= mn_lim) return *reinterpret_cast<const uint4*>(x + (size_t)k * ld + mn);
+      uint16_t t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = (mn + j < mn_lim) ? x[(size_t)k * ld + mn + j] : 0;
+      return *reinterpret_cast<uint4*>(t);
+    }
+  }
+};
+
+}  // namespace tfd

@@ -1,0 +1,514 @@
+// Fused CDNA4 kernels for one training step of the reference MNIST CNN
+// (conv5x5(32)+relu -> maxpool2 -> conv5x5(64)+relu -> maxpool2 -> FC1024+relu -> dropout -> FC10,
+//  softmax-xent mean loss; /root/reference/mnist_python_m.py:93-128, :205).
+//
+// Kernel map:
+//   conv1_pool_fwd   K1+K3 (+K18 batch gather): VALU direct conv (K=25, Cin=1 is MFMA-hostile),
+//                    bias+relu+2x2 pool+argmax fused; reads the device-resident dataset row
+//                    perm[(step*B+b) % n] so the whole step can be replayed from one hipGraph.
+//   conv2_pool_fwd   K2+K3: implicit GEMM on MFMA (M = B*196 in pool-window-major order, N=64,
+//                    K=800); each lane's 4 accumulator rows ARE one 2x2 pool window, so
+//                    bias+relu+maxpool+argmax happen in registers.
+//   fc1_fwd          K4 (split-K MFMA GEMM, fp32 slabs; the reducer is the head kernel).
+//   head             K4 finish + K5 dropout (Philox) + K6 + K7 + K8(dX) + K9 fused per batch row.
+//   fc1_dw / fc1_dx  K10: dW (+ bias row) and dX (with MaxPoolGrad+ReluGrad unpool epilogue, K11).
+//   conv2_dgrad      K13 with conv1 ReluGrad/pool-mask epilogue; conv2_wgrad K14 (+K12 bias row),
+//                    split-K slabs; out_grad K8 dW/db.
+//   conv1_wgrad      K15 (+K12): sparse wgrad straight from the pooled gradient and argmax (only the
+//                    1-of-4 argmax positions carry gradient), deterministic per-image slabs.
+#include "../common.h"
+#include "../gemm.h"
+#include "../mnist_layout.h"
+#include "../tfd_kernels.h"
+
+namespace tfd {
+using namespace mnist;
+
+namespace {
+
+__device__ __forceinline__ int data_row(const int* perm, const int64_t* step, int n_data, int B, int b) {
+  if (!perm) return b;
+  const int64_t s = *step;
+  return perm[(int)((s * (int64_t)B + b) % (int64_t)n_data)];
+}
+
+// ---------------- K1: conv1 + bias + relu + maxpool + argmax ----------------
+// thread = (pooled pixel, group of 8 output channels). 256 threads = 64 pooled pixels.
+__global__ __launch_bounds__(256) void conv1_pool_fwd(MnistStepArgs a) {
+  __shared__ float w[KTAPS * C1 + C1];
+  for (int i = threadIdx.x; i < KTAPS * C1 + C1; i += 256) w[i] = a.p32[OFF_WC1 + i];
+  __syncthreads();
+  const int gid = blockIdx.x * 256 + threadIdx.x;
+  const int gp = gid >> 2, cg = gid & 3;
+  if (gp >= a.B * 196) return;
+  const int b = gp / 196, pp = gp % 196, ph = pp / 14, pw = pp % 14;
+  const float* x = a.data + (size_t)data_row(a.perm, a.step, a.n_data, a.B, b) * 784;
+  float patch[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int ih = 2 * ph - 2 + i, iw = 2 * pw - 2 + j;
+      patch[i][j] = (ih >= 0 && ih < 28 && iw >= 0 && iw < 28) ? x[ih * 28 + iw] : 0.f;
+    }
+  uint32_t outw[4];
+  uint32_t idxw[2] = {0u, 0u};
+#pragma unroll
+  for (int cc = 0; cc < 8; ++cc) {
+    const int c = cg * 8 + cc;
+    const float bias = w[KTAPS * C1 + c];
+    float z[4];
+#pragma unroll
+    for (int win = 0; win < 4; ++win) {
+      const int dy = win >> 1, dx = win & 1;
+      float acc = bias;
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc = fmaf(patch[dy + kh][dx + kw], w[(kh * 5 + kw) * C1 + c], acc);
+      z[win] = acc;
+    }
+    float mx = z[0];
+    int am = 0;
+#pragma unroll
+    for (int win = 1; win < 4; ++win)
+      if (z[win] > mx) { mx = z[win]; am = win; }
+    mx = fmaxf(mx, 0.f);
+    const uint32_t hb = f2bf_bits(mx);
+    if (cc & 1) outw[cc >> 1] |= hb << 16; else outw[cc >> 1] = hb;
+    idxw[cc >> 2] |= (uint32_t)am << (8 * (cc & 3));
+  }
+  *reinterpret_cast<uint4*>(a.p1 + (size_t)gp * 32 + cg * 8) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+  *reinterpret_cast<uint2*>(a.idx1 + (size_t)gp * 32 + cg * 8) = make_uint2(idxw[0], idxw[1]);
+}
+
+// ---------------- K2: conv2 implicit GEMM, pooled epilogue ----------------
+// m = ((b*49 + pp)*4 + win); k = tap*32 + ci.
+struct Conv2FwdA {
+  static constexpr bool KC = true;
+  const uint16_t* __restrict__ p1;
+  int M;
+  __device__ __forceinline__ uint4 operator()(int m, int k) const {
+    if (m >= M || k >= 800) return zero4();
+    const int b = m / 196, r = m - b * 196, pp = r >> 2, win = r & 3;
+    const int ph = pp / 7, pw = pp - ph * 7;
+    const int tap = k >> 5, ci0 = k & 31, kh = tap / 5, kw = tap - kh * 5;
+    const int ih = 2 * ph + (win >> 1) + kh - 2, iw = 2 * pw + (win & 1) + kw - 2;
+    if ((unsigned)ih >= 14u || (unsigned)iw >= 14u) return zero4();
+    return *reinterpret_cast<const uint4*>(p1 + ((size_t)(b * 14 + ih) * 14 + iw) * 32 + ci0);
+  }
+};
+struct PoolEpi {
+  const float* __restrict__ bias;
+  uint16_t* __restrict__ p2;
+  uint8_t* __restrict__ idx2;
+  int M;
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+    if (m4 >= M) return;
+    const int b = m4 / 196, pp = (m4 - b * 196) >> 2;
+    const float bb = bias[n];
+    float mx = v[0] + bb;
+    int am = 0;
+#pragma unroll
+    for (int r = 1; r < 4; ++r) {
+      const float z = v[r] + bb;
+      if (z > mx) { mx = z; am = r; }
+    }
+    const size_t o = (size_t)b * FEAT + pp * 64 + n;
+    p2[o] = f2bf_bits(fmaxf(mx, 0.f));
+    idx2[o] = (uint8_t)am;
+  }
+};
+constexpr int C2F_BM = 64, C2F_BN = 64, C2F_BK = 160;
+using C2F_B = DenseLoader<false>;
+__global__ __launch_bounds__(256) void conv2_pool_fwd(MnistStepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int M = a.B * 196;
+  Conv2FwdA la{a.p1, M};
+  C2F_B lb{a.pbf + OFF_WC2, 64, 64, 800};
+  PoolEpi epi{a.p32 + OFF_BC2, a.p2, a.idx2, M};
+  gemm_block<C2F_BM, C2F_BN, C2F_BK, 2, 2>(la, lb, epi, blockIdx.x * C2F_BM, 0, 0, 800, (bf16*)smem_raw);
+}
+
+// ---------------- K3: fc1 forward, split-K slabs ----------------
+struct SlabEpi {
+  float* __restrict__ out;
+  int ld, M, N;
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+    if (n >= N) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (m4 + r < M) out[(size_t)(m4 + r) * ld + n] = v[r];
+  }
+};
+constexpr int FC1_BM = 64, FC1_BN = 64, FC1_BK = 64;
+__global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  DenseLoader<true> la{a.p2, FEAT, a.B, FEAT};
+  DenseLoader<false> lb{a.pbf + OFF_WD1, HID, HID, FEAT};
+  const int z = blockIdx.z;
+  SlabEpi epi{a.fc1_slab + (size_t)z * a.B * HID, HID, a.B, HID};
+  const int kb = z * kper, ke = min(FEAT, kb + kper);
+  gemm_block<FC1_BM, FC1_BN, FC1_BK, 2, 2>(la, lb, epi, blockIdx.y * FC1_BM, blockIdx.x * FC1_BN, kb, ke,
+                                           (bf16*)smem_raw);
+}
+
+// ---------------- K4-K9 head: reduce slabs, bias, relu, dropout, FC10, softmax-xent, bwd ----------
+// One 256-thread block per batch row; thread t owns hidden units 4t..4t+3.
+__global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
+  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int n0 = 4 * t;
+  f32x4 h = *reinterpret_cast<const f32x4*>(a.p32 + OFF_BD1 + n0);
+  for (int s = 0; s < a.fc1_splits; ++s) {
+    const f32x4 p = *reinterpret_cast<const f32x4*>(a.fc1_slab + ((size_t)s * a.B + row) * HID + n0);
+    h += p;
+  }
+  float hd[4], scale[4];
+  const float kp = train ? a.keep_prob : 1.0f;
+  if (kp < 1.0f) {
+    const int64_t st = *a.step;
+    Philox4 r = philox4x32_10((uint32_t)(row * 256 + t), (uint32_t)st, (uint32_t)(st >> 32), a.rank, a.seed,
+                              0x5EED1234u);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) scale[j] = (u01(r.v[j]) < kp) ? (1.0f / kp) : 0.f;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) scale[j] = 1.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) hd[j] = fmaxf(h[j], 0.f) * scale[j];
+  // logits partials
+  const float* wout = a.p32 + OFF_OUT;
+  float lp[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) lp[c] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float* wr = wout + (size_t)(n0 + j) * NCLS;
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) lp[c] = fmaf(hd[j], wr[c], lp[c]);
+  }
+  __shared__ float red[4][NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) {
+    const float v = wave_sum(lp[c]);
+    if (lane == 0) red[wv][c] = v;
+  }
+  __syncthreads();
+  const int lbl = a.labels[data_row(a.perm, a.step, a.n_data, a.B, row)];
+  float logit[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) logit[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + a.p32[OFF_BOUT + c];
+  float mx = logit[0];
+  int am = 0;
+#pragma unroll
+  for (int c = 1; c < NCLS; ++c)
+    if (logit[c] > mx) { mx = logit[c]; am = c; }
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) se += __expf(logit[c] - mx);
+  const float lse = mx + __logf(se);
+  if (t == 0) {
+    a.loss_row[row] = lse - logit[lbl];
+    a.correct_row[row] = (am == lbl) ? 1.f : 0.f;
+  }
+  if (!train) return;
+  const float invB = 1.0f / (float)a.B;
+  float dl[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) dl[c] = (__expf(logit[c] - lse) - (c == lbl ? 1.f : 0.f)) * invB;
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c)
+    if (t == c) a.dlogits[row * NCLS + c] = dl[c];
+  uint32_t hdw[2], dhw[2];
+  float dhv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float* wr = wout + (size_t)(n0 + j) * NCLS;
+    float d = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) d = fmaf(dl[c], wr[c], d);
+    dhv[j] = (h[j] > 0.f) ? d * scale[j] : 0.f;
+  }
+  hdw[0] = pack_bf2(hd[0], hd[1]); hdw[1] = pack_bf2(hd[2], hd[3]);
+  dhw[0] = pack_bf2(dhv[0], dhv[1]); dhw[1] = pack_bf2(dhv[2], dhv[3]);
+  *reinterpret_cast<uint2*>(a.hd + (size_t)row * HID + n0) = make_uint2(hdw[0], hdw[1]);
+  *reinterpret_cast<uint2*>(a.dh + (size_t)row * HID + n0) = make_uint2(dhw[0], dhw[1]);
+}
+
+// ---------------- K10 fc1 dW (+bias row): [3137][1024] = [P2;1]^T dH ----------------
+struct OnesRowMC {  // operand (mn, k) = X[k][mn] for mn < mn_real, 1 for mn == mn_real (k < k_lim)
+  static constexpr bool KC = false;
+  const uint16_t* __restrict__ x;
+  int ld, mn_real, k_lim;
+  __device__ __forceinline__ uint4 operator()(int mn, int k) const {
+    if (k >= k_lim) return zero4();
+    if (mn + 8 <= mn_real) return *reinterpret_cast<const uint4*>(x + (size_t)k * ld + mn);
+    uint16_t t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = mn + j;
+      t[j] = c < mn_real ? x[(size_t)k * ld + c] : (c == mn_real ? (uint16_t)0x3F80 : (uint16_t)0);
+    }
+    return *reinterpret_cast<uint4*>(t);
+  }
+};
+constexpr int FDW_BM = 64, FDW_BN = 64, FDW_BK = 64;
+__global__ __launch_bounds__(256) void fc1_dw(MnistStepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  OnesRowMC la{a.p2, FEAT, FEAT, a.B};
+  DenseLoader<false> lb{a.dh, HID, HID, a.B};
+  SlabEpi epi{a.grad + OFF_WD1, HID, FEAT + 1, HID};
+  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2>(la, lb, epi, blockIdx.y * FDW_BM, blockIdx.x * FDW_BN, 0, a.B,
+                                           (bf16*)smem_raw);
+}
+
+// ---------------- K10 fc1 dX + K11 MaxPoolGrad + ReluGrad -> dz2 (dense, conv2 pre-act grad) --------
+struct UnpoolEpi {
+  const uint16_t* __restrict__ p2;
+  const uint8_t* __restrict__ idx2;
+  uint16_t* __restrict__ dz2;
+  int B;
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+    if (n >= FEAT) return;
+    const int pp = n >> 6, c = n & 63, ph = pp / 7, pw = pp - ph * 7;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = m4 + r;
+      if (b >= B) continue;
+      const size_t o = (size_t)b * FEAT + n;
+      const float g = p2[o] != 0 ? v[r] : 0.f;  // relu output > 0
+      const int w = idx2[o];
+      const uint16_t gb = f2bf_bits(g);
+#pragma unroll
+      for (int wi = 0; wi < 4; ++wi) {
+        const int oh = 2 * ph + (wi >> 1), ow = 2 * pw + (wi & 1);
+        dz2[((size_t)(b * 14 + oh) * 14 + ow) * 64 + c] = (wi == w) ? gb : (uint16_t)0;
+      }
+    }
+  }
+};
+constexpr int FDX_BM = 32, FDX_BN = 64, FDX_BK = 64;
+__global__ __launch_bounds__(256) void fc1_dx(MnistStepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  DenseLoader<true> la{a.dh, HID, a.B, HID};
+  DenseLoader<true> lb{a.pbf + OFF_WD1, HID, FEAT, HID};
+  UnpoolEpi epi{a.p2, a.idx2, a.dz2, a.B};
+  gemm_block<FDX_BM, FDX_BN, FDX_BK, 2, 2>(la, lb, epi, blockIdx.y * FDX_BM, blockIdx.x * FDX_BN, 0, HID,
+                                           (bf16*)smem_raw);
+}
+
+// ---------------- K13 conv2 dgrad (+ conv1 relu/pool mask epilogue) ----------------
+struct Conv2DgradA {  // (m = (b,ih,iw), k = tap*64 + co)
+  static constexpr bool KC = true;
+  const uint16_t* __restrict__ dz2;
+  int M;
+  __device__ __forceinline__ uint4 operator()(int m, int k) const {
+    if (m >= M || k >= 1600) return zero4();
+    const int b = m / 196, r = m - b * 196, ih = r / 14, iw = r - ih * 14;
+    const int tap = k >> 6, co0 = k & 63, kh = tap / 5, kw = tap - kh * 5;
+    const int oh = ih - kh + 2, ow = iw - kw + 2;
+    if ((unsigned)oh >= 14u || (unsigned)ow >= 14u) return zero4();
+    return *reinterpret_cast<const uint4*>(dz2 + ((size_t)(b * 14 + oh) * 14 + ow) * 64 + co0);
+  }
+};
+struct Conv2DgradB {  // (n = ci, k = tap*64 + co) -> W2[tap][ci][co]
+  static constexpr bool KC = true;
+  const uint16_t* __restrict__ w2;
+  __device__ __forceinline__ uint4 operator()(int n, int k) const {
+    if (n >= 32 || k >= 1600) return zero4();
+    const int tap = k >> 6, co0 = k & 63;
+    return *reinterpret_cast<const uint4*>(w2 + (size_t)(tap * 32 + n) * 64 + co0);
+  }
+};
+struct MaskEpi {
+  const uint16_t* __restrict__ p1;
+  uint16_t* __restrict__ dp1m;
+  int M;
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m4 + r;
+      if (m >= M) return;
+      const size_t o = (size_t)m * 32 + n;
+      const uint16_t pv = p1[o];
+      dp1m[o] = pv != 0 ? f2bf_bits(v[r]) : (uint16_t)0;  // relu output > 0
+    }
+  }
+};
+constexpr int C2D_BM = 64, C2D_BN = 32, C2D_BK = 160;
+__global__ __launch_bounds__(256) void conv2_dgrad(MnistStepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int M = a.B * 196;
+  Conv2DgradA la{a.dz2, M};
+  Conv2DgradB lb{a.pbf + OFF_WC2};
+  MaskEpi epi{a.p1, a.dp1m, M};
+  gemm_block<C2D_BM, C2D_BN, C2D_BK, 2, 2>(la, lb, epi, blockIdx.x * C2D_BM, 0, 0, 1600, (bf16*)smem_raw);
+}
+
+// ---------------- K14 conv2 wgrad (+bias row), split-K slabs ----------------
+struct Conv2WgradA {  // (mn = tap*32+ci [800 = ones row], k = pixel (b,oh,ow))
+  static constexpr bool KC = false;
+  const uint16_t* __restrict__ p1;
+  int K;
+  __device__ __forceinline__ uint4 operator()(int mn, int k) const {
+    if (k >= K || mn > 800) return zero4();
+    if (mn == 800) return make_uint4(0x3F80u, 0u, 0u, 0u);
+    const int tap = mn >> 5, ci0 = mn & 31, kh = tap / 5, kw = tap - kh * 5;
+    const int b = k / 196, r = k - b * 196, oh = r / 14, ow = r - oh * 14;
+    const int ih = oh + kh - 2, iw = ow + kw - 2;
+    if ((unsigned)ih >= 14u || (unsigned)iw >= 14u) return zero4();
+    return *reinterpret_cast<const uint4*>(p1 + ((size_t)(b * 14 + ih) * 14 + iw) * 32 + ci0);
+  }
+};
+constexpr int C2W_BM = 64, C2W_BN = 64, C2W_BK = 64;
+__global__ __launch_bounds__(256) void conv2_wgrad(MnistStepArgs a, int kper) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int K = a.B * 196;
+  Conv2WgradA la{a.p1, K};
+  DenseLoader<false> lb{a.dz2, 64, 64, K};
+  const int z = blockIdx.y;
+  SlabEpi epi{a.wg2_slab + (size_t)z * 801 * 64, 64, 801, 64};
+  const int kb = z * kper, ke = min(K, kb + kper);
+  gemm_block<C2W_BM, C2W_BN, C2W_BK, 2, 2>(la, lb, epi, blockIdx.x * C2W_BM, 0, kb, ke, (bf16*)smem_raw);
+}
+
+// ---------------- K8 output layer dW/db: [1025][10] = [Hd;1]^T dlogits ----------------
+__global__ __launch_bounds__(256) void out_grad(MnistStepArgs a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= (HID + 1) * NCLS) return;
+  const int m = i / NCLS, c = i - m * NCLS;
+  float acc = 0.f;
+  if (m < HID) {
+    for (int b = 0; b < a.B; ++b) acc = fmaf(bf2f(a.hd[(size_t)b * HID + m]), a.dlogits[b * NCLS + c], acc);
+  } else {
+    for (int b = 0; b < a.B; ++b) acc += a.dlogits[b * NCLS + c];
+  }
+  a.grad[OFF_OUT + i] = acc;
+}
+
+// ---------------- K15 conv1 wgrad + bias grad (sparse, from pooled grad + argmax) ----------------
+// one block per image: thread (c = t & 31, sub = t >> 5); per-image slab [26][32].
+__global__ __launch_bounds__(256) void conv1_wgrad(MnistStepArgs a) {
+  __shared__ float img[32 * 32];
+  __shared__ float part[8][26 * 32 + 1];
+  const int b = blockIdx.x, t = threadIdx.x, c = t & 31, sub = t >> 5;
+  const float* x = a.data + (size_t)data_row(a.perm, a.step, a.n_data, a.B, b) * 784;
+  for (int i = t; i < 32 * 32; i += 256) {
+    const int r = i >> 5, q = i & 31, ih = r - 2, iw = q - 2;
+    img[i] = (ih >= 0 && ih < 28 && iw >= 0 && iw < 28) ? x[ih * 28 + iw] : 0.f;
+  }
+  __syncthreads();
+  float acc[26];
+#pragma unroll
+  for (int j = 0; j < 26; ++j) acc[j] = 0.f;
+  for (int pp = sub; pp < 196; pp += 8) {
+    const size_t o = ((size_t)b * 196 + pp) * 32 + c;
+    const float g = bf2f(a.dp1m[o]);
+    if (g != 0.f) {
+      const int w = a.idx1[o];
+      const int oh = 2 * (pp / 14) + (w >> 1), ow = 2 * (pp % 14) + (w & 1);
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] = fmaf(g, img[(oh + kh) * 32 + ow + kw], acc[kh * 5 + kw]);
+      acc[25] += g;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 26; ++j) part[sub][j * 32 + c] = acc[j];
+  __syncthreads();
+  for (int i = t; i < 26 * 32; i += 256) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += part[q][i];
+    a.wg1_slab[(size_t)b * 832 + i] = s;
+  }
+}
+
+// deterministic slab reductions into the flat gradient buffer
+__global__ __launch_bounds__(256) void reduce_slabs(const float* __restrict__ slab, int nslab, int64_t stride, int n,
+                                                    float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < nslab; ++k) s += slab[(size_t)k * stride + i];
+  out[i] = s;
+}
+
+template <auto K>
+inline void set_smem(int bytes) {
+  static bool done = false;
+  if (!done && bytes > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(K), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  done = true;
+}
+
+}  // namespace
+
+int mnist_fc1_splits(int B) { (void)B; return 7; }   // 3136 = 7 * 448 = 7 * 7 * 64
+int mnist_wg2_splits(int B) {
+  const int K = B * 196;
+  const int kper = 16 * C2W_BK;
+  return (K + kper - 1) / kper;
+}
+
+void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s) {
+  const int B = a.B;
+  {
+    const int threads = B * 196 * 4;
+    conv1_pool_fwd<<<(threads + 255) / 256, 256, 0, s>>>(a);
+  }
+  {
+    constexpr int sm = GemmSmem<C2F_BM, C2F_BN, C2F_BK, Conv2FwdA, C2F_B>::BYTES;
+    set_smem<conv2_pool_fwd>(sm);
+    conv2_pool_fwd<<<(B * 196 + C2F_BM - 1) / C2F_BM, 256, sm, s>>>(a);
+  }
+  {
+    constexpr int sm = GemmSmem<FC1_BM, FC1_BN, FC1_BK, DenseLoader<true>, DenseLoader<false>>::BYTES;
+    set_smem<fc1_fwd>(sm);
+    const int kper = (FEAT + a.fc1_splits - 1) / a.fc1_splits;
+    dim3 g(HID / FC1_BN, (B + FC1_BM - 1) / FC1_BM, a.fc1_splits);
+    fc1_fwd<<<g, 256, sm, s>>>(a, kper);
+  }
+  head_kernel<<<B, 256, 0, s>>>(a, train ? 1 : 0);
+}
+
+void mnist_backward_a(const MnistStepArgs& a, hipStream_t s) {
+  const int B = a.B;
+  {
+    constexpr int sm = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, DenseLoader<false>>::BYTES;
+    set_smem<fc1_dw>(sm);
+    dim3 g(HID / FDW_BN, (FEAT + 1 + FDW_BM - 1) / FDW_BM);
+    fc1_dw<<<g, 256, sm, s>>>(a);
+  }
+  out_grad<<<((HID + 1) * NCLS + 255) / 256, 256, 0, s>>>(a);
+  {
+    constexpr int sm = GemmSmem<FDX_BM, FDX_BN, FDX_BK, DenseLoader<true>, DenseLoader<true>>::BYTES;
+    set_smem<fc1_dx>(sm);
+    dim3 g(FEAT / FDX_BN, (B + FDX_BM - 1) / FDX_BM);
+    fc1_dx<<<g, 256, sm, s>>>(a);
+  }
+}
+
+void mnist_backward_b(const MnistStepArgs& a, hipStream_t s) {
+  const int B = a.B;
+  {
+    constexpr int sm = GemmSmem<C2D_BM, C2D_BN, C2D_BK, Conv2DgradA, Conv2DgradB>::BYTES;
+    set_smem<conv2_dgrad>(sm);
+    conv2_dgrad<<<(B * 196 + C2D_BM - 1) / C2D_BM, 256, sm, s>>>(a);
+  }
+  {
+    constexpr int sm = GemmSmem<C2W_BM, C2W_BN, C2W_BK, Conv2WgradA, DenseLoader<false>>::BYTES;
+    set_smem<conv2_wgrad>(sm);
+    const int K = B * 196;
+    const int kper = ((K + a.wg2_splits - 1) / a.wg2_splits + C2W_BK - 1) / C2W_BK * C2W_BK;
+    dim3 g((801 + C2W_BM - 1) / C2W_BM, a.wg2_splits);
+    conv2_wgrad<<<g, 256, sm, s>>>(a, kper);
+  }
+  conv1_wgrad<<<B, 256, 0, s>>>(a);
+  reduce_slabs<<<(801 * 64 + 255) / 256, 256, 0, s>>>(a.wg2_slab, a.wg2_splits, 801 * 64, 801 * 64, a.grad + OFF_WC2);
+  reduce_slabs<<<(832 + 255) / 256, 256, 0, s>>>(a.wg1_slab, B, 832, 832, a.grad + OFF_WC1);
+}
+
+}  // namespace tfd

@@ -1,0 +1,137 @@
+// Multi-tensor (flat-buffer) optimizer kernels: one launch updates every parameter of the model.
+// ApplyAdam semantics follow TF1 (training_ops ApplyAdam, reached from
+// /root/reference/mnist_python_m.py:208,222 and mnist_single.py:95):
+//   m_t = m + (g - m)(1 - b1);  v_t = v + (g^2 - v)(1 - b2)
+//   p  -= lr * sqrt(1 - b2^t) / (1 - b1^t) * m_t / (sqrt(v_t) + eps),   t = global_step + 1
+// The fp32 master is updated in place and its bf16 shadow (the operand every MFMA kernel reads)
+// is rewritten in the same pass. The device global_step is read by every block and incremented
+// by the last-arriving block (arrival counter, self-resetting) so a captured step graph needs no
+// host round trip.
+#include <math.h>
+#include "../common.h"
+#include "../tfd_kernels.h"
+
+namespace tfd {
+namespace {
+
+constexpr int kOptThreads = 256;
+constexpr int kOptMaxBlocks = 2048;
+
+__device__ __forceinline__ void bump_step(int64_t* step, unsigned* done) {
+  if (!step || !done) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned prev = atomicAdd(done, 1u);
+    if (prev == gridDim.x - 1) {
+      *step = *step + 1;
+      atomicExch(done, 0u);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kOptThreads) void adam_kernel(AdamArgs a) {
+  const int64_t t = (a.step ? *a.step : 0) + 1;
+  const float b1p = powf(a.beta1, (float)t), b2p = powf(a.beta2, (float)t);
+  const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  const float c1 = 1.f - a.beta1, c2 = 1.f - a.beta2;
+  const int64_t n4 = a.n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * kOptThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kOptThreads + threadIdx.x; i < n4; i += stride) {
+    f32x4 p = reinterpret_cast<f32x4*>(a.p)[i];
+    f32x4 m = reinterpret_cast<f32x4*>(a.m)[i];
+    f32x4 v = reinterpret_cast<f32x4*>(a.v)[i];
+    f32x4 g;
+    if (a.gbf) {
+      const uint2 gb = reinterpret_cast<const uint2*>(a.gbf)[i];
+      g = f32x4{bf2f((uint16_t)(gb.x & 0xFFFF)), bf2f((uint16_t)(gb.x >> 16)), bf2f((uint16_t)(gb.y & 0xFFFF)),
+                bf2f((uint16_t)(gb.y >> 16))};
+    } else {
+      g = reinterpret_cast<const f32x4*>(a.g)[i];
+    }
+    g *= a.grad_scale;
+    m = m + (g - m) * c1;
+    v = v + (g * g - v) * c2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] -= lr_t * m[j] / (sqrtf(v[j]) + a.eps);
+    reinterpret_cast<f32x4*>(a.p)[i] = p;
+    reinterpret_cast<f32x4*>(a.m)[i] = m;
+    reinterpret_cast<f32x4*>(a.v)[i] = v;
+    if (a.pbf) reinterpret_cast<uint2*>(a.pbf)[i] = make_uint2(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]));
+  }
+  // scalar tail (n % 4)
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * kOptThreads + threadIdx.x; i < a.n; i += stride) {
+    const float g = (a.gbf ? bf2f(a.gbf[i]) : a.g[i]) * a.grad_scale;
+    float m = a.m[i] + (g - a.m[i]) * c1;
+    float v = a.v[i] + (g * g - a.v[i]) * c2;
+    const float p = a.p[i] - lr_t * m / (sqrtf(v) + a.eps);
+    a.p[i] = p; a.m[i] = m; a.v[i] = v;
+    if (a.pbf) a.pbf[i] = f2bf_bits(p);
+  }
+  bump_step(a.step, a.done);
+}
+
+// GradientDescent / Momentum (TF ApplyMomentum: accum = accum*mu + g; p -= lr*accum,
+// nesterov: p -= lr*(g + mu*accum)); optional decoupled-from-nothing L2 weight decay folded in g.
+__global__ __launch_bounds__(kOptThreads) void sgd_kernel(SgdArgs a) {
+  const int64_t stride = (int64_t)gridDim.x * kOptThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kOptThreads + threadIdx.x; i < a.n; i += stride) {
+    float g = (a.gbf ? bf2f(a.gbf[i]) : a.g[i]) * a.grad_scale + a.weight_decay * a.p[i];
+    float p = a.p[i];
+    if (a.mom) {
+      const float acc = a.mom[i] * a.momentum + g;
+      a.mom[i] = acc;
+      p -= a.nesterov ? a.lr * (g + a.momentum * acc) : a.lr * acc;
+    } else {
+      p -= a.lr * g;
+    }
+    a.p[i] = p;
+    if (a.pbf) a.pbf[i] = f2bf_bits(p);
+  }
+  bump_step(a.step, a.done);
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = f2bf_bits(x[i]);
+}
+__global__ void cast_bf16_f32_kernel(const uint16_t* __restrict__ x, float* __restrict__ y, int64_t n, float sc) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = bf2f(x[i]) * sc;
+}
+__global__ void scale_kernel(float* __restrict__ x, int64_t n, float sc) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= sc;
+}
+__global__ void axpy_kernel(float* __restrict__ d, const float* __restrict__ s, int64_t n, float alpha) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) d[i] += alpha * s[i];
+}
+
+inline int blocks_for(int64_t n, int per_thread) {
+  const int64_t b = (n / per_thread + kOptThreads - 1) / kOptThreads;
+  return (int)(b < 1 ? 1 : (b > kOptMaxBlocks ? kOptMaxBlocks : b));
+}
+
+}  // namespace
+
+void adam_apply(const AdamArgs& a, hipStream_t s) {
+  adam_kernel<<<blocks_for(a.n, 4), kOptThreads, 0, s>>>(a);
+}
+void sgd_apply(const SgdArgs& a, hipStream_t s) {
+  sgd_kernel<<<blocks_for(a.n, 1), kOptThreads, 0, s>>>(a);
+}
+void cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s) {
+  cast_f32_bf16_kernel<<<blocks_for(n, 1), kOptThreads, 0, s>>>(x, y, n);
+}
+void cast_bf16_f32(const uint16_t* x, float* y, int64_t n, float scale, hipStream_t s) {
+  cast_bf16_f32_kernel<<<blocks_for(n, 1), kOptThreads, 0, s>>>(x, y, n, scale);
+}
+void scale_f32(float* x, int64_t n, float scale, hipStream_t s) {
+  scale_kernel<<<blocks_for(n, 1), kOptThreads, 0, s>>>(x, n, scale);
+}
+void vec_accumulate(float* dst, const float* src, int64_t n, float alpha, hipStream_t s) {
+  axpy_kernel<<<blocks_for(n, 1), kOptThreads, 0, s>>>(dst, src, n, alpha);
+}
+
+}  // namespace tfd

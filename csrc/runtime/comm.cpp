@@ -1,0 +1,110 @@
+#include "comm.h"
+
+#include <c10/hip/HIPStream.h>
+#include <c10/util/Exception.h>
+#include <cstring>
+
+namespace tfd {
+
+void rccl_check(ncclResult_t r, const char* what) {
+  TORCH_CHECK(r == ncclSuccess, "RCCL ", what, " failed: ", ncclGetErrorString(r));
+}
+
+ncclDataType_t rccl_dtype(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return ncclFloat32;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kHalf: return ncclFloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    case at::kByte: return ncclUint8;
+    case at::kChar: return ncclInt8;
+    default: TORCH_CHECK(false, "RcclComm: unsupported dtype ", t.scalar_type());
+  }
+}
+
+ncclRedOp_t rccl_op(const std::string& op) {
+  if (op == "sum") return ncclSum;
+  if (op == "avg" || op == "mean") return ncclAvg;
+  if (op == "max") return ncclMax;
+  if (op == "min") return ncclMin;
+  if (op == "prod") return ncclProd;
+  TORCH_CHECK(false, "RcclComm: unknown reduce op ", op);
+}
+
+at::Tensor RcclComm::unique_id() {
+  ncclUniqueId id;
+  rccl_check(ncclGetUniqueId(&id), "GetUniqueId");
+  auto t = at::empty({NCCL_UNIQUE_ID_BYTES}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(t.data_ptr(), &id, NCCL_UNIQUE_ID_BYTES);
+  return t;
+}
+
+RcclComm::RcclComm(const at::Tensor& uid, int64_t world, int64_t rank, int64_t device)
+    : world_(world), rank_(rank), device_(device) {
+  TORCH_CHECK(uid.numel() == NCCL_UNIQUE_ID_BYTES && uid.scalar_type() == at::kByte, "bad unique id");
+  ncclUniqueId id;
+  auto c = uid.contiguous().cpu();
+  std::memcpy(&id, c.data_ptr(), NCCL_UNIQUE_ID_BYTES);
+  TORCH_CHECK(hipSetDevice((int)device) == hipSuccess, "hipSetDevice failed");
+  rccl_check(ncclCommInitRank(&comm_, (int)world, id, (int)rank), "CommInitRank");
+}
+
+RcclComm::~RcclComm() {
+  if (comm_) {
+    ncclCommDestroy(comm_);
+    comm_ = nullptr;
+  }
+}
+
+void RcclComm::abort() {
+  if (comm_) {
+    ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
+}
+
+static hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void RcclComm::all_reduce_raw(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
+  TORCH_CHECK(comm_, "communicator aborted");
+  rccl_check(ncclAllReduce(buf, buf, count, dt, op, comm_, s), "AllReduce");
+}
+void RcclComm::reduce_scatter_raw(const void* in, void* out, size_t recvcount, ncclDataType_t dt, ncclRedOp_t op,
+                                  hipStream_t s) {
+  TORCH_CHECK(comm_, "communicator aborted");
+  rccl_check(ncclReduceScatter(in, out, recvcount, dt, op, comm_, s), "ReduceScatter");
+}
+void RcclComm::all_gather_raw(const void* in, void* out, size_t sendcount, ncclDataType_t dt, hipStream_t s) {
+  TORCH_CHECK(comm_, "communicator aborted");
+  rccl_check(ncclAllGather(in, out, sendcount, dt, comm_, s), "AllGather");
+}
+
+void RcclComm::all_reduce(const at::Tensor& t, const std::string& op) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "all_reduce: contiguous GPU tensor required");
+  all_reduce_raw(t.data_ptr(), t.numel(), rccl_dtype(t), rccl_op(op), cur_stream());
+}
+void RcclComm::reduce_scatter(const at::Tensor& in, const at::Tensor& out, const std::string& op) {
+  TORCH_CHECK(in.numel() == out.numel() * world_, "reduce_scatter: size mismatch");
+  reduce_scatter_raw(in.data_ptr(), out.data_ptr(), out.numel(), rccl_dtype(in), rccl_op(op), cur_stream());
+}
+void RcclComm::all_gather(const at::Tensor& in, const at::Tensor& out) {
+  TORCH_CHECK(out.numel() == in.numel() * world_, "all_gather: size mismatch");
+  all_gather_raw(in.data_ptr(), out.data_ptr(), in.numel(), rccl_dtype(in), cur_stream());
+}
+void RcclComm::broadcast(const at::Tensor& t, int64_t root) {
+  TORCH_CHECK(comm_, "communicator aborted");
+  rccl_check(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), rccl_dtype(t), (int)root, comm_, cur_stream()),
+             "Broadcast");
+}
+void RcclComm::send(const at::Tensor& t, int64_t peer) {
+  TORCH_CHECK(comm_, "communicator aborted");
+  rccl_check(ncclSend(t.data_ptr(), t.numel(), rccl_dtype(t), (int)peer, comm_, cur_stream()), "Send");
+}
+void RcclComm::recv(const at::Tensor& t, int64_t peer) {
+  TORCH_CHECK(comm_, "communicator aborted");
+  rccl_check(ncclRecv(t.data_ptr(), t.numel(), rccl_dtype(t), (int)peer, comm_, cur_stream()), "Recv");
+}
+
+}  // namespace tfd

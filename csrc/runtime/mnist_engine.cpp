@@ -1,0 +1,348 @@
+// Native train-step executor for the reference MNIST CNN.
+//
+// Plays the role of the TF1 graph executor + Session.run for the reference's hot loop
+// (/root/reference/mnist_python_m.py:289-302, mnist_single.py:109-117): it owns every device
+// buffer (flat fp32 master params, bf16 shadow, flat grads, Adam slots, activations), sequences
+// the fused HIP kernels of csrc/kernels/mnist.hip, overlaps the bucketed RCCL gradient all-reduce
+// with the conv backward on a second stream, applies the fused flat optimizer, and can capture the
+// whole step (both streams, collectives included) into one hipGraph that is replayed per step.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/custom_class.h>
+#include <torch/library.h>
+
+#include <map>
+#include <string>
+
+#include "../mnist_layout.h"
+#include "../tfd_kernels.h"
+#include "comm.h"
+
+namespace tfd {
+using namespace mnist;
+
+#define HIP_OK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    TORCH_CHECK(e_ == hipSuccess, #x, " failed: ", hipGetErrorString(e_));                 \
+  } while (0)
+
+class MnistEngine : public torch::CustomClassHolder {
+ public:
+  MnistEngine(int64_t batch, int64_t device, double keep_prob, int64_t seed, int64_t rank)
+      : B_(batch), device_(device), keep_prob_(keep_prob), seed_((uint32_t)seed), rank_((uint32_t)rank) {
+    TORCH_CHECK(batch > 0 && batch <= 65536, "bad batch");
+    auto f32 = at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device);
+    auto bf = at::TensorOptions().dtype(at::kBFloat16).device(at::kCUDA, device);
+    auto u8 = at::TensorOptions().dtype(at::kByte).device(at::kCUDA, device);
+    auto i64 = at::TensorOptions().dtype(at::kLong).device(at::kCUDA, device);
+    auto i32 = at::TensorOptions().dtype(at::kInt).device(at::kCUDA, device);
+    params_ = at::zeros({TOTAL}, f32);
+    pbf_ = at::zeros({TOTAL}, bf);
+    grad_ = at::zeros({TOTAL}, f32);
+    m_ = at::zeros({TOTAL}, f32);
+    v_ = at::zeros({TOTAL}, f32);
+    gbf_ = at::zeros({TOTAL}, bf);
+    step_ = at::zeros({1}, i64);
+    done_ = at::zeros({1}, i32);
+    fc1_splits_ = mnist_fc1_splits((int)B_);
+    wg2_splits_ = mnist_wg2_splits((int)B_);
+    p1_ = at::empty({B_, P1H, P1H, C1}, bf);
+    idx1_ = at::empty({B_, P1H, P1H, C1}, u8);
+    p2_ = at::empty({B_, FEAT}, bf);
+    idx2_ = at::empty({B_, FEAT}, u8);
+    fc1_slab_ = at::empty({fc1_splits_, B_, HID}, f32);
+    hd_ = at::empty({B_, HID}, bf);
+    dh_ = at::empty({B_, HID}, bf);
+    dlogits_ = at::empty({B_, NCLS}, f32);
+    loss_row_ = at::zeros({B_}, f32);
+    correct_row_ = at::zeros({B_}, f32);
+    dz2_ = at::empty({B_, P1H, P1H, C2}, bf);
+    dp1m_ = at::empty({B_, P1H, P1H, C1}, bf);
+    wg2_slab_ = at::empty({wg2_splits_, 801, C2}, f32);
+    wg1_slab_ = at::empty({B_, 832}, f32);
+    xbuf_ = at::zeros({B_, 784}, f32);
+    ybuf_ = at::zeros({B_}, i32);
+    HIP_OK(hipSetDevice((int)device));
+    HIP_OK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_b_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
+  }
+  ~MnistEngine() override {
+    for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
+    hipEventDestroy(ev_a_);
+    hipEventDestroy(ev_b_);
+    hipEventDestroy(ev_done_);
+    hipStreamDestroy(comm_stream_);
+  }
+
+  // ---- state accessors (views share storage with the engine) ----
+  at::Tensor params() { return params_; }
+  at::Tensor params_bf16() { return pbf_; }
+  at::Tensor grads() { return grad_; }
+  at::Tensor adam_m() { return m_; }
+  at::Tensor adam_v() { return v_; }
+  at::Tensor step_tensor() { return step_; }
+  at::Tensor loss_rows() { return loss_row_; }
+  at::Tensor correct_rows() { return correct_row_; }
+  at::Tensor hidden() { return hd_; }
+  at::Tensor pool2() { return p2_; }
+  at::Tensor pool1() { return p1_; }
+  at::Tensor feed_x() { return xbuf_; }
+  at::Tensor feed_y() { return ybuf_; }
+  int64_t batch() { return B_; }
+
+  void set_dataset(at::Tensor data, at::Tensor labels, at::Tensor perm) {
+    TORCH_CHECK(data.is_cuda() && data.scalar_type() == at::kFloat && data.dim() == 2 && data.size(1) == 784,
+                "dataset must be a [N,784] fp32 GPU tensor");
+    TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kInt && labels.numel() == data.size(0),
+                "labels must be [N] int32 GPU");
+    TORCH_CHECK(perm.is_cuda() && perm.scalar_type() == at::kInt && perm.numel() == data.size(0),
+                "perm must be [N] int32 GPU");
+    data_ = data.contiguous();
+    labels_ = labels.contiguous();
+    perm_ = perm.contiguous();
+  }
+  // mode 0 = feed buffers (feed_x/feed_y filled by the host each step), 1 = device dataset + perm
+  void set_input_mode(int64_t mode) {
+    TORCH_CHECK(mode == 0 || (mode == 1 && data_.defined()), "set_dataset first");
+    input_mode_ = mode;
+  }
+  void set_keep_prob(double kp) { keep_prob_ = kp; }
+  void sync_shadow() { cast_f32_bf16((const float*)params_.data_ptr(), (uint16_t*)pbf_.data_ptr(), TOTAL, stream()); }
+
+  void set_adam(double lr, double b1, double b2, double eps) {
+    opt_ = 0; lr_ = lr; b1_ = b1; b2_ = b2; eps_ = eps;
+  }
+  void set_momentum(double lr, double momentum, bool nesterov) {
+    opt_ = momentum > 0 ? 2 : 1; lr_ = lr; momentum_ = momentum; nesterov_ = nesterov;
+  }
+  void set_comm(c10::intrusive_ptr<RcclComm> comm, bool bf16_grads) {
+    comm_ = comm;
+    bf16_comm_ = bf16_grads;
+  }
+
+  // ---- step pieces (current HIP stream) ----
+  void forward(bool train) { mnist_forward(args(), train, stream()); }
+  void backward_a() { mnist_backward_a(args(), stream()); }
+  void backward_b() { mnist_backward_b(args(), stream()); }
+  void apply_optimizer(double grad_scale) {
+    const uint16_t* gbf = (comm_ && bf16_comm_ && comm_->world() > 1) ? (const uint16_t*)gbf_.data_ptr() : nullptr;
+    if (opt_ == 0) {
+      AdamArgs a{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(), (const float*)grad_.data_ptr(),
+                 (uint16_t*)pbf_.data_ptr(), gbf, TOTAL, (float)lr_, (float)b1_, (float)b2_, (float)eps_,
+                 (int64_t*)step_.data_ptr(), (unsigned*)done_.data_ptr(), (float)grad_scale};
+      adam_apply(a, stream());
+    } else {
+      SgdArgs a{(float*)params_.data_ptr(), opt_ == 2 ? (float*)m_.data_ptr() : nullptr, (const float*)grad_.data_ptr(),
+                (uint16_t*)pbf_.data_ptr(), gbf, TOTAL, (float)lr_, (float)momentum_, 0.f, (float)grad_scale,
+                nesterov_ ? 1 : 0, (int64_t*)step_.data_ptr(), (unsigned*)done_.data_ptr()};
+      sgd_apply(a, stream());
+    }
+  }
+
+  // Full synchronous data-parallel step: fwd -> bwd(fc) -> [bucket A all-reduce on comm stream]
+  // || bwd(conv) -> [bucket B all-reduce] -> join -> optimizer. Equivalent of the reference's
+  // SyncReplicasOptimizer global step with replicas_to_aggregate == num_workers (averaged grads,
+  // one ApplyAdam, global_step += 1).
+  void train_step() {
+    hipStream_t s = stream();
+    forward(true);
+    backward_a();
+    const bool dp = comm_ && comm_->world() > 1;
+    if (dp) {
+      HIP_OK(hipEventRecord(ev_a_, s));
+      HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
+      reduce_bucket(BUCKET_SPLIT, TOTAL);
+    }
+    backward_b();
+    if (dp) {
+      HIP_OK(hipEventRecord(ev_b_, s));
+      HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
+      reduce_bucket(0, BUCKET_SPLIT);
+      HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+      HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+    }
+    apply_optimizer(dp ? 1.0 / (double)comm_->world() : 1.0);
+  }
+
+  // Evaluate on an explicit batch (x [n,784] fp32, y [n] int32) in chunks of <= B.
+  // Returns a 2-element fp32 GPU tensor {sum of per-example loss, number correct}.
+  at::Tensor evaluate(at::Tensor x, at::Tensor y) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.size(1) == 784, "x: [n,784] fp32 GPU");
+    TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kInt, "y: [n] int32 GPU");
+    x = x.contiguous();
+    y = y.contiguous();
+    const int64_t n = x.size(0);
+    auto out = at::zeros({2}, x.options());
+    for (int64_t o = 0; o < n; o += B_) {
+      const int nb = (int)std::min<int64_t>(B_, n - o);
+      MnistStepArgs a = args();
+      a.B = nb;
+      a.data = (const float*)x.data_ptr() + o * 784;
+      a.labels = (const int*)y.data_ptr() + o;
+      a.perm = nullptr;
+      mnist_forward(a, false, stream());
+      out[0] += loss_row_.narrow(0, 0, nb).sum();
+      out[1] += correct_row_.narrow(0, 0, nb).sum();
+    }
+    return out;
+  }
+
+  // ---- hipGraph capture / replay of the whole step ----
+  void capture_train_step(const std::string& name) {
+    hipStream_t s = stream();
+    TORCH_CHECK(s != nullptr, "capture needs a non-default stream (use torch.cuda.stream(...))");
+    drop_graph(name);
+    HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+    try {
+      train_step();
+    } catch (...) {
+      hipGraph_t g;
+      hipStreamEndCapture(s, &g);
+      if (g) hipGraphDestroy(g);
+      throw;
+    }
+    hipGraph_t g = nullptr;
+    HIP_OK(hipStreamEndCapture(s, &g));
+    hipGraphExec_t ex = nullptr;
+    HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    HIP_OK(hipGraphDestroy(g));
+    graphs_[name] = ex;
+  }
+  void replay(const std::string& name, int64_t times) {
+    auto it = graphs_.find(name);
+    TORCH_CHECK(it != graphs_.end(), "no graph named ", name);
+    hipStream_t s = stream();
+    for (int64_t i = 0; i < times; ++i) HIP_OK(hipGraphLaunch(it->second, s));
+  }
+  void drop_graph(const std::string& name) {
+    auto it = graphs_.find(name);
+    if (it != graphs_.end()) {
+      hipGraphExecDestroy(it->second);
+      graphs_.erase(it);
+    }
+  }
+
+ private:
+  hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+  void reduce_bucket(int64_t beg, int64_t end) {
+    const size_t n = (size_t)(end - beg);
+    if (bf16_comm_) {
+      uint16_t* gb = (uint16_t*)gbf_.data_ptr() + beg;
+      cast_f32_bf16((const float*)grad_.data_ptr() + beg, gb, (int64_t)n, comm_stream_);
+      comm_->all_reduce_raw(gb, n, ncclBfloat16, ncclSum, comm_stream_);
+    } else {
+      comm_->all_reduce_raw((float*)grad_.data_ptr() + beg, n, ncclFloat32, ncclSum, comm_stream_);
+    }
+  }
+
+  MnistStepArgs args() {
+    MnistStepArgs a{};
+    a.B = (int)B_;
+    if (input_mode_ == 1) {
+      a.data = (const float*)data_.data_ptr();
+      a.labels = (const int*)labels_.data_ptr();
+      a.perm = (const int*)perm_.data_ptr();
+      a.n_data = (int)data_.size(0);
+    } else {
+      a.data = (const float*)xbuf_.data_ptr();
+      a.labels = (const int*)ybuf_.data_ptr();
+      a.perm = nullptr;
+      a.n_data = (int)B_;
+    }
+    a.step = (const int64_t*)step_.data_ptr();
+    a.p32 = (const float*)params_.data_ptr();
+    a.pbf = (const uint16_t*)pbf_.data_ptr();
+    a.grad = (float*)grad_.data_ptr();
+    a.p1 = (uint16_t*)p1_.data_ptr();
+    a.idx1 = (uint8_t*)idx1_.data_ptr();
+    a.p2 = (uint16_t*)p2_.data_ptr();
+    a.idx2 = (uint8_t*)idx2_.data_ptr();
+    a.fc1_slab = (float*)fc1_slab_.data_ptr();
+    a.hd = (uint16_t*)hd_.data_ptr();
+    a.dh = (uint16_t*)dh_.data_ptr();
+    a.dlogits = (float*)dlogits_.data_ptr();
+    a.loss_row = (float*)loss_row_.data_ptr();
+    a.correct_row = (float*)correct_row_.data_ptr();
+    a.dz2 = (uint16_t*)dz2_.data_ptr();
+    a.dp1m = (uint16_t*)dp1m_.data_ptr();
+    a.wg2_slab = (float*)wg2_slab_.data_ptr();
+    a.wg1_slab = (float*)wg1_slab_.data_ptr();
+    a.fc1_splits = fc1_splits_;
+    a.wg2_splits = wg2_splits_;
+    a.keep_prob = (float)keep_prob_;
+    a.seed = seed_;
+    a.rank = rank_;
+    return a;
+  }
+
+  int64_t B_, device_;
+  double keep_prob_;
+  uint32_t seed_, rank_;
+  int fc1_splits_, wg2_splits_;
+  int64_t input_mode_ = 0;
+  int opt_ = 0;
+  double lr_ = 0.01, b1_ = 0.9, b2_ = 0.999, eps_ = 1e-8, momentum_ = 0.0;
+  bool nesterov_ = false;
+  bool bf16_comm_ = true;
+  c10::intrusive_ptr<RcclComm> comm_;
+  at::Tensor params_, pbf_, grad_, m_, v_, gbf_, step_, done_;
+  at::Tensor p1_, idx1_, p2_, idx2_, fc1_slab_, hd_, dh_, dlogits_, loss_row_, correct_row_, dz2_, dp1m_, wg2_slab_,
+      wg1_slab_, xbuf_, ybuf_;
+  at::Tensor data_, labels_, perm_;
+  hipStream_t comm_stream_ = nullptr;
+  hipEvent_t ev_a_ = nullptr, ev_b_ = nullptr, ev_done_ = nullptr;
+  std::map<std::string, hipGraphExec_t> graphs_;
+};
+
+TORCH_LIBRARY_FRAGMENT(tfd, m) {
+  m.class_<RcclComm>("RcclComm")
+      .def(torch::init<at::Tensor, int64_t, int64_t, int64_t>())
+      .def_static("unique_id", &RcclComm::unique_id)
+      .def("world", &RcclComm::world)
+      .def("rank", &RcclComm::rank)
+      .def("all_reduce", &RcclComm::all_reduce)
+      .def("reduce_scatter", &RcclComm::reduce_scatter)
+      .def("all_gather", &RcclComm::all_gather)
+      .def("broadcast", &RcclComm::broadcast)
+      .def("send", &RcclComm::send)
+      .def("recv", &RcclComm::recv)
+      .def("abort", &RcclComm::abort);
+  m.class_<MnistEngine>("MnistEngine")
+      .def(torch::init<int64_t, int64_t, double, int64_t, int64_t>())
+      .def("params", &MnistEngine::params)
+      .def("params_bf16", &MnistEngine::params_bf16)
+      .def("grads", &MnistEngine::grads)
+      .def("adam_m", &MnistEngine::adam_m)
+      .def("adam_v", &MnistEngine::adam_v)
+      .def("step_tensor", &MnistEngine::step_tensor)
+      .def("loss_rows", &MnistEngine::loss_rows)
+      .def("correct_rows", &MnistEngine::correct_rows)
+      .def("hidden", &MnistEngine::hidden)
+      .def("pool1", &MnistEngine::pool1)
+      .def("pool2", &MnistEngine::pool2)
+      .def("feed_x", &MnistEngine::feed_x)
+      .def("feed_y", &MnistEngine::feed_y)
+      .def("batch", &MnistEngine::batch)
+      .def("set_dataset", &MnistEngine::set_dataset)
+      .def("set_input_mode", &MnistEngine::set_input_mode)
+      .def("set_keep_prob", &MnistEngine::set_keep_prob)
+      .def("sync_shadow", &MnistEngine::sync_shadow)
+      .def("set_adam", &MnistEngine::set_adam)
+      .def("set_momentum", &MnistEngine::set_momentum)
+      .def("set_comm", &MnistEngine::set_comm)
+      .def("forward", &MnistEngine::forward)
+      .def("backward_a", &MnistEngine::backward_a)
+      .def("backward_b", &MnistEngine::backward_b)
+      .def("apply_optimizer", &MnistEngine::apply_optimizer)
+      .def("train_step", &MnistEngine::train_step)
+      .def("evaluate", &MnistEngine::evaluate)
+      .def("capture_train_step", &MnistEngine::capture_train_step)
+      .def("replay", &MnistEngine::replay)
+      .def("drop_graph", &MnistEngine::drop_graph);
+}
+
+}  // namespace tfd

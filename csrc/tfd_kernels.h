@@ -1,0 +1,67 @@
+// Host-side launcher API of the HIP kernel library (no HIP kernel syntax here: this header is
+// included by the g++-compiled torch binding / runtime layer).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace tfd {
+
+// ---------------- fused MNIST CNN train step ----------------
+struct MnistStepArgs {
+  int B;                       // per-rank batch
+  // data: rows of `data` ([n_data][784] fp32) are taken as perm[(step*B + b) % n_data] when perm
+  // is non-null, else row b directly (a fed batch). labels likewise ([n_data] int32 class ids).
+  const float* data;
+  const int* labels;
+  const int* perm;
+  int n_data;
+  const int64_t* step;         // device global_step (read by every kernel, bumped by the optimizer)
+  // params
+  const float* p32;            // flat fp32 master params (mnist_layout.h)
+  const uint16_t* pbf;         // flat bf16 shadow of p32
+  float* grad;                 // flat fp32 gradient buffer
+  // activations / workspace (bf16 stored as uint16)
+  uint16_t* p1;  uint8_t* idx1;   // [B][14][14][32]
+  uint16_t* p2;  uint8_t* idx2;   // [B][3136]
+  float* fc1_slab;                // [fc1_splits][B][1024]
+  uint16_t* hd;  uint16_t* dh;    // [B][1024]
+  float* dlogits;                 // [B][10]
+  float* loss_row; float* correct_row;  // [B]
+  uint16_t* dz2;                  // [B][14][14][64]
+  uint16_t* dp1m;                 // [B][14][14][32]
+  float* wg2_slab;                // [wg2_splits][801][64]
+  float* wg1_slab;                // [B][832]
+  int fc1_splits, wg2_splits;
+  float keep_prob;
+  uint32_t seed, rank;
+};
+
+int mnist_fc1_splits(int B);
+int mnist_wg2_splits(int B);
+void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s);        // conv1, conv2, fc1, head
+void mnist_backward_a(const MnistStepArgs& a, hipStream_t s);                 // fc1 dW/dX -> bucket A done
+void mnist_backward_b(const MnistStepArgs& a, hipStream_t s);                 // conv2/conv1 grads -> bucket B done
+
+// ---------------- optimizers (flat, fp32 master + bf16 shadow) ----------------
+struct AdamArgs {
+  float* p; float* m; float* v; const float* g; uint16_t* pbf;
+  const uint16_t* gbf;         // if non-null, gradients are read from this bf16 buffer instead of g
+  int64_t n;
+  float lr, beta1, beta2, eps;
+  int64_t* step;               // device step; t = *step + 1; the last block increments it
+  unsigned* done;              // arrival counter (zero-initialised once; self-resetting)
+  float grad_scale;            // multiply g (e.g. 1/N for sum-all-reduce)
+};
+void adam_apply(const AdamArgs& a, hipStream_t s);
+struct SgdArgs {
+  float* p; float* mom; const float* g; uint16_t* pbf; const uint16_t* gbf; int64_t n;
+  float lr, momentum, weight_decay, grad_scale; int nesterov;
+  int64_t* step; unsigned* done;
+};
+void sgd_apply(const SgdArgs& a, hipStream_t s);
+void cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
+void cast_bf16_f32(const uint16_t* x, float* y, int64_t n, float scale, hipStream_t s);
+void scale_f32(float* x, int64_t n, float scale, hipStream_t s);
+void vec_accumulate(float* dst, const float* src, int64_t n, float alpha, hipStream_t s);
+
+}  // namespace tfd

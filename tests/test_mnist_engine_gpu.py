@@ -1,0 +1,138 @@
+"""Numerics of the native fused MNIST step (HIP kernels) against the PyTorch fp32 oracle.
+
+The oracle is ``models.mnist_cnn.conv_net`` in fp32 (optionally rounding to bf16 exactly where
+the native kernels store/consume bf16). Gradients come from torch autograd on the same params.
+"""
+import pytest
+import torch
+
+from tensorflow_distributed_amd.models import mnist_cnn as M
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(B, dev, keep=1.0):
+    from tensorflow_distributed_amd import _native
+    _native.require()
+    return torch.classes.tfd.MnistEngine(B, dev.index or 0, keep, 1234, 0)
+
+
+def _ref_grads(params, x, y, emulate):
+    p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    logits = M.conv_net(x, p, 1.0, emulate_bf16=emulate)
+    loss_rows = torch.nn.functional.cross_entropy(logits, y.long(), reduction="none")
+    loss_rows.mean().backward()
+    return logits.detach(), loss_rows.detach(), {k: v.grad for k, v in p.items()}
+
+
+def _relerr(a, b):
+    return (a - b).norm().item() / max(b.norm().item(), 1e-30)
+
+
+@pytest.mark.parametrize("scale,B", [(0.05, 128), (1.0, 128), (0.05, 40)])
+def test_step_grads_match_oracle(cuda, scale, B):
+    torch.manual_seed(0)
+    params = {k: v * scale for k, v in M.init_params(7).items()}
+    x = torch.rand(B, 784)
+    y = torch.randint(0, 10, (B,), dtype=torch.int32)
+    eng = _engine(B, cuda)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        eng.params().copy_(M.flat_from_dict(params).to(cuda))
+        eng.sync_shadow()
+        eng.feed_x().copy_(x.to(cuda))
+        eng.feed_y().copy_(y.to(cuda))
+        eng.forward(True)
+        eng.backward_a()
+        eng.backward_b()
+    torch.cuda.synchronize()
+    pd = {k: v.double() for k, v in params.items()}
+    _, loss_ref, g_ref = _ref_grads({k: v.float() for k, v in params.items()}, x, y, emulate=True)
+    loss = eng.loss_rows().cpu()
+    assert _relerr(loss, loss_ref) < 2e-2, (loss[:4], loss_ref[:4])
+    g = M.dict_from_flat(eng.grads().cpu())
+    for k in g_ref:
+        e = _relerr(g[k].float(), g_ref[k])
+        assert e < 5e-2, f"{k}: relerr {e}"
+    del pd
+
+
+def test_adam_step_and_counter(cuda):
+    B = 64
+    params = {k: v * 0.05 for k, v in M.init_params(3).items()}
+    x = torch.rand(B, 784)
+    y = torch.randint(0, 10, (B,), dtype=torch.int32)
+    eng = _engine(B, cuda)
+    eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        eng.params().copy_(M.flat_from_dict(params).to(cuda))
+        eng.sync_shadow()
+        eng.feed_x().copy_(x.to(cuda))
+        eng.feed_y().copy_(y.to(cuda))
+        p0 = eng.params().clone()
+        eng.forward(True); eng.backward_a(); eng.backward_b()
+        g = eng.grads().clone()
+        eng.apply_optimizer(1.0)
+    torch.cuda.synchronize()
+    assert int(eng.step_tensor().item()) == 1
+    # TF ApplyAdam first step: p -= lr * sqrt(1-b2)/(1-b1) * m/(sqrt(v)+eps), m=(1-b1)g, v=(1-b2)g^2
+    lr_t = 0.01 * (1 - 0.999) ** 0.5 / (1 - 0.9)
+    m = 0.1 * g
+    v = 0.001 * g * g
+    ref = p0 - lr_t * m / (v.sqrt() + 1e-8)
+    assert torch.allclose(eng.params(), ref, rtol=1e-5, atol=1e-6)
+    assert torch.equal(eng.params_bf16(), eng.params().to(torch.bfloat16))
+
+
+def test_graph_replay_matches_eager(cuda):
+    B = 128
+    params = M.flat_from_dict(M.init_params(11)).to(cuda)
+    n = 1024
+    data = torch.rand(n, 784, device=cuda)
+    labels = torch.randint(0, 10, (n,), dtype=torch.int32, device=cuda)
+    perm = torch.randperm(n, device=cuda).to(torch.int32)
+    engs = []
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            e = _engine(B, cuda, keep=0.75)
+            e.set_adam(0.01, 0.9, 0.999, 1e-8)
+            e.params().copy_(params)
+            e.sync_shadow()
+            e.set_dataset(data, labels, perm)
+            e.set_input_mode(1)
+            engs.append(e)
+        for _ in range(3):
+            engs[0].train_step()
+        engs[1].capture_train_step("g")
+        engs[1].replay("g", 3)
+    torch.cuda.synchronize()
+    assert int(engs[0].step_tensor().item()) == 3 and int(engs[1].step_tensor().item()) == 3
+    assert torch.equal(engs[0].params(), engs[1].params())
+
+
+def test_training_reduces_loss(cuda):
+    B = 128
+    n = 4096
+    torch.manual_seed(1)
+    # learnable synthetic task: class templates + noise
+    tmpl = torch.rand(10, 784)
+    yl = torch.randint(0, 10, (n,))
+    data = (0.7 * tmpl[yl] + 0.3 * torch.rand(n, 784)).to(cuda)
+    labels = yl.to(torch.int32).to(cuda)
+    perm = torch.randperm(n).to(torch.int32).to(cuda)
+    eng = _engine(B, cuda, keep=0.75)
+    eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        eng.params().copy_(M.flat_from_dict(M.init_params(5)).to(cuda))
+        eng.sync_shadow()
+        eng.set_dataset(data, labels, perm)
+        eng.set_input_mode(1)
+        r0 = eng.evaluate(data[:1000], labels[:1000]).cpu()
+        for _ in range(60):
+            eng.train_step()
+        r1 = eng.evaluate(data[:1000], labels[:1000]).cpu()
+    torch.cuda.synchronize()
+    assert r1[1] > r0[1] and r1[1] >= 800, (r0, r1)
