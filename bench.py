@@ -1,0 +1,124 @@
+"""Headline benchmark: images/sec (whole node) of the reference MNIST CNN training step, DP over
+N MI355X (BASELINE.json metric; reference config: per-worker batch 128, Adam lr 0.01,
+keep_prob 0.75 -- /root/reference/mnist_python_m.py:62-71,205-222).
+
+One process per GPU (torchrun env). Each step = fused HIP forward + backward + bucketed RCCL
+gradient all-reduce (sum, 1/N folded into Adam) + fused flat Adam, with every kernel and
+collective captured into ONE hipGraph that is replayed per step. Data is a device-resident
+synthetic MNIST-shaped split (55000 x 784 fp32 in [0,1], random labels) indexed by a per-rank
+permutation and the device global_step, so there is no host work inside the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch_size 128]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_IMG_PER_S = 52.1  # 120 global steps x 256 images / 590 s (performance:6)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--batch_size", type=int, default=128, help="per-GPU batch (reference --batch_size)")
+    ap.add_argument("--eager", action="store_true", help="launch kernels per step instead of hipGraph replay")
+    ap.add_argument("--fp32_grads", action="store_true", help="all-reduce fp32 grads (default bf16)")
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--seed", type=int, default=1)
+    a = ap.parse_args(argv)
+
+    import torch
+
+    from tensorflow_distributed_amd import _native
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+    from tensorflow_distributed_amd.parallel import dist as D
+
+    _native.require()
+    ctx = D.init_from_env(use_gpu=True)
+    world, rank = ctx.world, ctx.rank
+    if world != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    dev = ctx.device
+    B = a.batch_size
+    eng = torch.classes.tfd.MnistEngine(B, dev.index, 0.75, a.seed, rank)
+    eng.set_adam(a.lr, 0.9, 0.999, 1e-8)
+    if ctx.comm is not None:
+        eng.set_comm(ctx.comm, not a.fp32_grads)
+    s = torch.cuda.Stream(dev)
+    n_data = 55000
+    with torch.cuda.stream(s):
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        data = torch.rand(n_data, 784, device=dev, generator=g)
+        labels = torch.randint(0, 10, (n_data,), device=dev, generator=g, dtype=torch.int32)
+        perm = torch.randperm(n_data, device=dev, generator=g).to(torch.int32)
+        if rank == 0:
+            eng.params().copy_(M.flat_from_dict(M.init_params(a.seed)).to(dev))
+        if ctx.comm is not None:
+            ctx.comm.broadcast(eng.params(), 0)  # chief init -> everyone (reference M6)
+        eng.sync_shadow()
+        eng.set_dataset(data, labels, perm)
+        eng.set_input_mode(1)
+        if a.eager:
+            run = lambda k: [eng.train_step() for _ in range(k)]  # noqa: E731
+        else:
+            eng.train_step()  # one eager step first: sets kernel attributes outside capture
+            eng.capture_train_step("train")
+            run = lambda k: eng.replay("train", k)  # noqa: E731
+        run(a.warmup)
+    torch.cuda.synchronize(dev)
+    loss0 = float(eng.loss_rows().mean().item())
+
+    ctx.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s):
+        run(a.steps)
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    dt = time.perf_counter() - t0
+    dt = ctx.max_scalar(dt)
+    loss1 = float(eng.loss_rows().mean().item())
+    gstep = int(eng.step_tensor().item())
+    ms = dt * 1e3 / a.steps
+    img_s = world * B * a.steps / dt
+    if rank == 0:
+        print(f"# world={world} B/gpu={B} steps={a.steps} global_step={gstep} loss {loss0:.3f}->{loss1:.3f} "
+              f"{ms:.4f} ms/step", file=sys.stderr)
+        print(json.dumps({
+            "metric": "images/sec (whole node) MNIST CNN DP",
+            "value": round(img_s, 1),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(img_s / BASELINE_IMG_PER_S, 1),
+            "dtype": "bf16",
+            "data": "synthetic (device-resident MNIST-shaped 55000x784, random labels; random N(0,1) init)",
+            "config": {
+                "model": "mnist_cnn (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout0.75-fc10, Adam lr 0.01)",
+                "global_batch": world * B,
+                "per_gpu_batch": B,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "grad_allreduce": "fp32" if a.fp32_grads else "bf16",
+                "hipgraph": not a.eager,
+            },
+        }), flush=True)
+    ctx.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -21,6 +21,8 @@
 #include "../mnist_layout.h"
 #include "../tfd_kernels.h"
 
+#include <algorithm>
+
 namespace tfd {
 using namespace mnist;
 
@@ -119,7 +121,7 @@ struct PoolEpi {
     idx2[o] = (uint8_t)am;
   }
 };
-constexpr int C2F_BM = 64, C2F_BN = 64, C2F_BK = 160;
+constexpr int C2F_BM = 64, C2F_BN = 64, C2F_BK = 64;
 using C2F_B = DenseLoader<false>;
 __global__ __launch_bounds__(256) void conv2_pool_fwd(MnistStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -236,6 +238,44 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   *reinterpret_cast<uint2*>(a.dh + (size_t)row * HID + n0) = make_uint2(dhw[0], dhw[1]);
 }
 
+// ---------------- K8 output layer dW/db: [1025][10] = [Hd;1]^T dlogits ----------------
+// One 256-thread block owns 64 rows m (thread = row m0 + (t & 63), batch quarter t >> 6); dlogits
+// [B][10] staged in LDS; the 4 batch quarters are summed through LDS (deterministic).
+constexpr int OUTG_ROWS = 64;
+constexpr int OUTG_BLOCKS = (HID + 1 + OUTG_ROWS - 1) / OUTG_ROWS;  // 17 (last block: bias row)
+__device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, float* smem) {
+  float* dl = smem;                      // [B][10]
+  float* part = smem + a.B * NCLS;       // [4][64][10]
+  const int t = threadIdx.x, r = t & 63, q = t >> 6;
+  for (int i = t; i < a.B * NCLS; i += 256) dl[i] = a.dlogits[i];
+  __syncthreads();
+  const int m = blk * OUTG_ROWS + r;
+  float acc[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) acc[c] = 0.f;
+  const int bq = (a.B + 3) >> 2, b0 = q * bq, b1 = min(a.B, b0 + bq);
+  if (m < HID) {
+    for (int b = b0; b < b1; ++b) {
+      const float h = bf2f(a.hd[(size_t)b * HID + m]);
+#pragma unroll
+      for (int c = 0; c < NCLS; ++c) acc[c] = fmaf(h, dl[b * NCLS + c], acc[c]);
+    }
+  } else if (m == HID) {
+    for (int b = b0; b < b1; ++b)
+#pragma unroll
+      for (int c = 0; c < NCLS; ++c) acc[c] += dl[b * NCLS + c];
+  }
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) part[(q * 64 + r) * NCLS + c] = acc[c];
+  __syncthreads();
+  for (int i = t; i < OUTG_ROWS * NCLS; i += 256) {
+    const int rr = i / NCLS, mm = blk * OUTG_ROWS + rr;
+    if (mm <= HID)
+      a.grad[OFF_OUT + (size_t)mm * NCLS + (i - rr * NCLS)] =
+          part[i] + part[OUTG_ROWS * NCLS + i] + part[2 * OUTG_ROWS * NCLS + i] + part[3 * OUTG_ROWS * NCLS + i];
+  }
+}
+
 // ---------------- K10 fc1 dW (+bias row): [3137][1024] = [P2;1]^T dH ----------------
 struct OnesRowMC {  // operand (mn, k) = X[k][mn] for mn < mn_real, 1 for mn == mn_real (k < k_lim)
   static constexpr bool KC = false;
@@ -254,13 +294,11 @@ struct OnesRowMC {  // operand (mn, k) = X[k][mn] for mn < mn_real, 1 for mn == 
   }
 };
 constexpr int FDW_BM = 64, FDW_BN = 64, FDW_BK = 64;
-__global__ __launch_bounds__(256) void fc1_dw(MnistStepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+__device__ __forceinline__ void fc1_dw_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   OnesRowMC la{a.p2, FEAT, FEAT, a.B};
   DenseLoader<false> lb{a.dh, HID, HID, a.B};
   SlabEpi epi{a.grad + OFF_WD1, HID, FEAT + 1, HID};
-  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2>(la, lb, epi, blockIdx.y * FDW_BM, blockIdx.x * FDW_BN, 0, a.B,
-                                           (bf16*)smem_raw);
+  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2>(la, lb, epi, by * FDW_BM, bx * FDW_BN, 0, a.B, smem);
 }
 
 // ---------------- K10 fc1 dX + K11 MaxPoolGrad + ReluGrad -> dz2 (dense, conv2 pre-act grad) --------
@@ -289,13 +327,25 @@ struct UnpoolEpi {
   }
 };
 constexpr int FDX_BM = 32, FDX_BN = 64, FDX_BK = 64;
-__global__ __launch_bounds__(256) void fc1_dx(MnistStepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+__device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   DenseLoader<true> la{a.dh, HID, a.B, HID};
   DenseLoader<true> lb{a.pbf + OFF_WD1, HID, FEAT, HID};
   UnpoolEpi epi{a.p2, a.idx2, a.dz2, a.B};
-  gemm_block<FDX_BM, FDX_BN, FDX_BK, 2, 2>(la, lb, epi, blockIdx.y * FDX_BM, blockIdx.x * FDX_BN, 0, HID,
-                                           (bf16*)smem_raw);
+  gemm_block<FDX_BM, FDX_BN, FDX_BK, 2, 2>(la, lb, epi, by * FDX_BM, bx * FDX_BN, 0, HID, smem);
+}
+
+// K8 + K10: every fc-layer gradient in ONE launch (horizontal fusion of three independent
+// products that all consume dH / dlogits): [fc1 dW tiles | fc1 dX tiles | out dW/db blocks].
+constexpr int FDW_GX = HID / FDW_BN, FDW_GY = (FEAT + 1 + FDW_BM - 1) / FDW_BM;  // 16 x 50
+constexpr int FDX_GX = FEAT / FDX_BN;                                             // 49
+__global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  int id = blockIdx.x;
+  if (id < FDW_GX * FDW_GY) { fc1_dw_block(a, id % FDW_GX, id / FDW_GX, (bf16*)smem_raw); return; }
+  id -= FDW_GX * FDW_GY;
+  if (id < n_dx) { fc1_dx_block(a, id % FDX_GX, id / FDX_GX, (bf16*)smem_raw); return; }
+  id -= n_dx;
+  out_grad_block(a, id, (float*)smem_raw);
 }
 
 // ---------------- K13 conv2 dgrad (+ conv1 relu/pool mask epilogue) ----------------
@@ -336,14 +386,13 @@ struct MaskEpi {
     }
   }
 };
-constexpr int C2D_BM = 64, C2D_BN = 32, C2D_BK = 160;
-__global__ __launch_bounds__(256) void conv2_dgrad(MnistStepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+constexpr int C2D_BM = 64, C2D_BN = 32, C2D_BK = 64;
+__device__ __forceinline__ void conv2_dgrad_block(const MnistStepArgs& a, int bx, bf16* smem) {
   const int M = a.B * 196;
   Conv2DgradA la{a.dz2, M};
   Conv2DgradB lb{a.pbf + OFF_WC2};
   MaskEpi epi{a.p1, a.dp1m, M};
-  gemm_block<C2D_BM, C2D_BN, C2D_BK, 2, 2>(la, lb, epi, blockIdx.x * C2D_BM, 0, 0, 1600, (bf16*)smem_raw);
+  gemm_block<C2D_BM, C2D_BN, C2D_BK, 2, 2>(la, lb, epi, bx * C2D_BM, 0, 0, 1600, smem);
 }
 
 // ---------------- K14 conv2 wgrad (+bias row), split-K slabs ----------------
@@ -362,29 +411,22 @@ struct Conv2WgradA {  // (mn = tap*32+ci [800 = ones row], k = pixel (b,oh,ow))
   }
 };
 constexpr int C2W_BM = 64, C2W_BN = 64, C2W_BK = 64;
-__global__ __launch_bounds__(256) void conv2_wgrad(MnistStepArgs a, int kper) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+constexpr int C2W_GX = (801 + C2W_BM - 1) / C2W_BM;  // 13
+__device__ __forceinline__ void conv2_wgrad_block(const MnistStepArgs& a, int bx, int z, int kper, bf16* smem) {
   const int K = a.B * 196;
   Conv2WgradA la{a.p1, K};
   DenseLoader<false> lb{a.dz2, 64, 64, K};
-  const int z = blockIdx.y;
   SlabEpi epi{a.wg2_slab + (size_t)z * 801 * 64, 64, 801, 64};
   const int kb = z * kper, ke = min(K, kb + kper);
-  gemm_block<C2W_BM, C2W_BN, C2W_BK, 2, 2>(la, lb, epi, blockIdx.x * C2W_BM, 0, kb, ke, (bf16*)smem_raw);
+  gemm_block<C2W_BM, C2W_BN, C2W_BK, 2, 2>(la, lb, epi, bx * C2W_BM, 0, kb, ke, smem);
 }
-
-// ---------------- K8 output layer dW/db: [1025][10] = [Hd;1]^T dlogits ----------------
-__global__ __launch_bounds__(256) void out_grad(MnistStepArgs a) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= (HID + 1) * NCLS) return;
-  const int m = i / NCLS, c = i - m * NCLS;
-  float acc = 0.f;
-  if (m < HID) {
-    for (int b = 0; b < a.B; ++b) acc = fmaf(bf2f(a.hd[(size_t)b * HID + m]), a.dlogits[b * NCLS + c], acc);
-  } else {
-    for (int b = 0; b < a.B; ++b) acc += a.dlogits[b * NCLS + c];
-  }
-  a.grad[OFF_OUT + i] = acc;
+// K13 + K14 in one launch: conv2 dgrad and wgrad both consume dz2 only (independent).
+__global__ __launch_bounds__(256) void conv2_bwd(MnistStepArgs a, int n_dgrad, int kper) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int id = blockIdx.x;
+  if (id < n_dgrad) { conv2_dgrad_block(a, id, (bf16*)smem_raw); return; }
+  const int w = id - n_dgrad;
+  conv2_wgrad_block(a, w % C2W_GX, w / C2W_GX, kper, (bf16*)smem_raw);
 }
 
 // ---------------- K15 conv1 wgrad + bias grad (sparse, from pooled grad + argmax) ----------------
@@ -426,14 +468,27 @@ __global__ __launch_bounds__(256) void conv1_wgrad(MnistStepArgs a) {
   }
 }
 
-// deterministic slab reductions into the flat gradient buffer
-__global__ __launch_bounds__(256) void reduce_slabs(const float* __restrict__ slab, int nslab, int64_t stride, int n,
-                                                    float* __restrict__ out) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+// Deterministic slab reductions of both conv weight-gradient slab sets in ONE launch:
+// thread (x = output column of a 64-wide chunk, y = slab phase 0..3); fixed summation order.
+__device__ __forceinline__ void reduce_chunk(const float* __restrict__ slab, int nslab, int64_t stride, int n, int i0,
+                                             float* __restrict__ out, float* red) {
+  const int x = threadIdx.x & 63, y = threadIdx.x >> 6, i = i0 + x;
   float s = 0.f;
-  for (int k = 0; k < nslab; ++k) s += slab[(size_t)k * stride + i];
-  out[i] = s;
+  if (i < n)
+    for (int k = y; k < nslab; k += 4) s += slab[(size_t)k * stride + i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (y == 0 && i < n) out[i] = (red[x] + red[64 + x]) + (red[128 + x] + red[192 + x]);
+}
+constexpr int RED2_BLOCKS = (801 * 64 + 63) / 64;  // 801
+constexpr int RED1_BLOCKS = (832 + 63) / 64;       // 13
+__global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a) {
+  __shared__ float red[256];
+  const int id = blockIdx.x;
+  if (id < RED2_BLOCKS)
+    reduce_chunk(a.wg2_slab, a.wg2_splits, 801 * 64, 801 * 64, id * 64, a.grad + OFF_WC2, red);
+  else
+    reduce_chunk(a.wg1_slab, a.B, 832, 832, (id - RED2_BLOCKS) * 64, a.grad + OFF_WC1, red);
 }
 
 template <auto K>
@@ -476,39 +531,29 @@ void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s) {
 
 void mnist_backward_a(const MnistStepArgs& a, hipStream_t s) {
   const int B = a.B;
-  {
-    constexpr int sm = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, DenseLoader<false>>::BYTES;
-    set_smem<fc1_dw>(sm);
-    dim3 g(HID / FDW_BN, (FEAT + 1 + FDW_BM - 1) / FDW_BM);
-    fc1_dw<<<g, 256, sm, s>>>(a);
-  }
-  out_grad<<<((HID + 1) * NCLS + 255) / 256, 256, 0, s>>>(a);
-  {
-    constexpr int sm = GemmSmem<FDX_BM, FDX_BN, FDX_BK, DenseLoader<true>, DenseLoader<true>>::BYTES;
-    set_smem<fc1_dx>(sm);
-    dim3 g(FEAT / FDX_BN, (B + FDX_BM - 1) / FDX_BM);
-    fc1_dx<<<g, 256, sm, s>>>(a);
-  }
+  constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, DenseLoader<false>>::BYTES;
+  constexpr int sm_dx = GemmSmem<FDX_BM, FDX_BN, FDX_BK, DenseLoader<true>, DenseLoader<true>>::BYTES;
+  const int sm_og = (B * NCLS + 4 * OUTG_ROWS * NCLS) * 4;
+  const int sm = std::max(std::max(sm_dw, sm_dx), sm_og);
+  set_smem<fc1_bwd>(sm);
+  const int n_dx = FDX_GX * ((B + FDX_BM - 1) / FDX_BM);
+  fc1_bwd<<<FDW_GX * FDW_GY + n_dx + OUTG_BLOCKS, 256, sm, s>>>(a, n_dx);
 }
 
 void mnist_backward_b(const MnistStepArgs& a, hipStream_t s) {
   const int B = a.B;
   {
-    constexpr int sm = GemmSmem<C2D_BM, C2D_BN, C2D_BK, Conv2DgradA, Conv2DgradB>::BYTES;
-    set_smem<conv2_dgrad>(sm);
-    conv2_dgrad<<<(B * 196 + C2D_BM - 1) / C2D_BM, 256, sm, s>>>(a);
-  }
-  {
-    constexpr int sm = GemmSmem<C2W_BM, C2W_BN, C2W_BK, Conv2WgradA, DenseLoader<false>>::BYTES;
-    set_smem<conv2_wgrad>(sm);
+    constexpr int sm_d = GemmSmem<C2D_BM, C2D_BN, C2D_BK, Conv2DgradA, Conv2DgradB>::BYTES;
+    constexpr int sm_w = GemmSmem<C2W_BM, C2W_BN, C2W_BK, Conv2WgradA, DenseLoader<false>>::BYTES;
+    constexpr int sm = sm_d > sm_w ? sm_d : sm_w;
+    set_smem<conv2_bwd>(sm);
     const int K = B * 196;
     const int kper = ((K + a.wg2_splits - 1) / a.wg2_splits + C2W_BK - 1) / C2W_BK * C2W_BK;
-    dim3 g((801 + C2W_BM - 1) / C2W_BM, a.wg2_splits);
-    conv2_wgrad<<<g, 256, sm, s>>>(a, kper);
+    const int n_dgrad = (B * 196 + C2D_BM - 1) / C2D_BM;
+    conv2_bwd<<<n_dgrad + C2W_GX * a.wg2_splits, 256, sm, s>>>(a, n_dgrad, kper);
   }
   conv1_wgrad<<<B, 256, 0, s>>>(a);
-  reduce_slabs<<<(801 * 64 + 255) / 256, 256, 0, s>>>(a.wg2_slab, a.wg2_splits, 801 * 64, 801 * 64, a.grad + OFF_WC2);
-  reduce_slabs<<<(832 + 255) / 256, 256, 0, s>>>(a.wg1_slab, B, 832, 832, a.grad + OFF_WC1);
+  reduce_conv_grads<<<RED2_BLOCKS + RED1_BLOCKS, 256, 0, s>>>(a);
 }
 
 }  // namespace tfd

@@ -19,12 +19,14 @@ constexpr int kOptMaxBlocks = 2048;
 
 __device__ __forceinline__ void bump_step(int64_t* step, unsigned* done) {
   if (!step || !done) return;
+  // Every block has read *step (at entry) before it arrives here, so the last arriver may bump it
+  // without any data hand-off: no release/acquire fence is needed (a per-block __threadfence
+  // writes back the XCD L2 once per block, which serialised the 13 MB update).
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
     const unsigned prev = atomicAdd(done, 1u);
     if (prev == gridDim.x - 1) {
-      *step = *step + 1;
+      atomicAdd(reinterpret_cast<unsigned long long*>(step), 1ull);
       atomicExch(done, 0u);
     }
   }
