@@ -25,7 +25,7 @@ void adam_flat(at::Tensor p, at::Tensor m, at::Tensor v, at::Tensor g, c10::opti
   const bool gb = g.scalar_type() == at::kBFloat16;
   AdamArgs a{(float*)p.data_ptr(), (float*)m.data_ptr(), (float*)v.data_ptr(), gb ? nullptr : (const float*)g.data_ptr(),
              pbf ? (uint16_t*)pbf->data_ptr() : nullptr, gb ? (const uint16_t*)g.data_ptr() : nullptr, p.numel(),
-             (float)lr, (float)b1, (float)b2, (float)eps, (int64_t*)step.data_ptr(), nullptr, (float)grad_scale};
+             (float)lr, (float)b1, (float)b2, (float)eps, (const int64_t*)step.data_ptr(), 1, (float)grad_scale};
   adam_apply(a, cur());
 }
 
@@ -35,7 +35,7 @@ void momentum_flat(at::Tensor p, c10::optional<at::Tensor> mom, at::Tensor g, c1
   const bool gb = g.scalar_type() == at::kBFloat16;
   SgdArgs a{(float*)p.data_ptr(), mom ? (float*)mom->data_ptr() : nullptr, gb ? nullptr : (const float*)g.data_ptr(),
             pbf ? (uint16_t*)pbf->data_ptr() : nullptr, gb ? (const uint16_t*)g.data_ptr() : nullptr, p.numel(),
-            (float)lr, (float)momentum, (float)weight_decay, (float)grad_scale, nesterov ? 1 : 0, nullptr, nullptr};
+            (float)lr, (float)momentum, (float)weight_decay, (float)grad_scale, nesterov ? 1 : 0};
   sgd_apply(a, cur());
 }
 

@@ -50,6 +50,18 @@ __device__ __forceinline__ bf16x8 read_frag(const bf16* lds, int r0, int kk, int
   }
 }
 
+// Transposed operand fragment (mfma_f32_16x16x32_bf16 A or B) from an LDS image stored with
+// rows = k and columns = m/n (m/n contiguous, 16-B aligned rows). For lane l (g = l >> 4,
+// q = (l & 15) >> 2, p4 = l & 3) the caller passes p0 = &image[row(8g + q)][c0 + 4 p4] and
+// p1 = &image[row(8g + q + 4)][c0 + 4 p4]; rows may be arbitrary per lane (im2col gathers), the
+// result holds {X[k = 8g + j][c0 + (l & 15)] : j = 0..7}. EXEC must be all ones.
+__device__ __forceinline__ bf16x8 frag_tr16(const bf16* p0, const bf16* p1) {
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p1));
+  s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 template <int BM, int BN, int BK, class LA, class LB>
 struct GemmSmem {
   using TA = LdsTile<BM, BK, LA::KC>;

@@ -23,6 +23,46 @@
 
 #include <algorithm>
 
+#ifndef TFD_WROT
+#define TFD_WROT 1
+#endif
+
+#ifndef TFD_EXP_SKIP_MAIN
+#define TFD_EXP_SKIP_MAIN 0  // experiment: skip the MFMA main loops of the LDS conv kernels
+#endif
+
+#ifndef TFD_CONV2_LDS
+#define TFD_CONV2_LDS 1  // LDS-staged whole-image conv2 kernels (0 = im2col-through-L2 GEMM path)
+#endif
+
+#ifndef TFD_C2W_KPER
+#define TFD_C2W_KPER 1024  // conv2 wgrad split-K chunk (pixels per slab)
+#endif
+
+#ifndef TFD_C2W_BK
+#define TFD_C2W_BK 64
+#endif
+
+#ifndef TFD_C2D_BK
+#define TFD_C2D_BK 64
+#endif
+
+#ifndef TFD_FDX_BK
+#define TFD_FDX_BK 64
+#endif
+
+#ifndef TFD_FDW_BK
+#define TFD_FDW_BK 64
+#endif
+
+#ifndef TFD_FC1_BK
+#define TFD_FC1_BK 64
+#endif
+
+#ifndef TFD_C2F_BK
+#define TFD_C2F_BK 64
+#endif
+
 namespace tfd {
 using namespace mnist;
 
@@ -35,53 +75,67 @@ __device__ __forceinline__ int data_row(const int* perm, const int64_t* step, in
 }
 
 // ---------------- K1: conv1 + bias + relu + maxpool + argmax ----------------
-// thread = (pooled pixel, group of 8 output channels). 256 threads = 64 pooled pixels.
+// Block = (image b, output-channel group cg of 8): the 28x28 fp32 image is staged once into a
+// zero-bordered 32x32 LDS tile (coalesced 16 B loads), thread pp < 196 computes the 4 window
+// pre-activations of pooled pixel pp for 8 channels from a 6x6 LDS patch (fp32 VALU: K = 25 with
+// Cin = 1 is MFMA-hostile). Grid = 4B blocks (512 at B = 128: every CU busy).
 __global__ __launch_bounds__(256) void conv1_pool_fwd(MnistStepArgs a) {
-  __shared__ float w[KTAPS * C1 + C1];
-  for (int i = threadIdx.x; i < KTAPS * C1 + C1; i += 256) w[i] = a.p32[OFF_WC1 + i];
-  __syncthreads();
-  const int gid = blockIdx.x * 256 + threadIdx.x;
-  const int gp = gid >> 2, cg = gid & 3;
-  if (gp >= a.B * 196) return;
-  const int b = gp / 196, pp = gp % 196, ph = pp / 14, pw = pp % 14;
+  __shared__ float img[32 * 32];
+  __shared__ float w[KTAPS * 8 + 8];
+  const int b = blockIdx.x >> 2, cg = blockIdx.x & 3, t = threadIdx.x;
   const float* x = a.data + (size_t)data_row(a.perm, a.step, a.n_data, a.B, b) * 784;
+  for (int i = t; i < 32 * 32; i += 256) img[i] = 0.f;
+  if (t < KTAPS * 8) w[t] = a.p32[OFF_WC1 + (t >> 3) * C1 + cg * 8 + (t & 7)];
+  else if (t < KTAPS * 8 + 8) w[t] = a.p32[OFF_BC1 + cg * 8 + (t - KTAPS * 8)];
+  __syncthreads();
+  if (t < 196) {  // 196 float4 = one image
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[t];
+    const int r = (4 * t) / 28, c = (4 * t) % 28;
+    float* d = img + (r + 2) * 32 + c + 2;
+    d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+  }
+  __syncthreads();
+  if (t >= 196) return;
+  const int ph = t / 14, pw = t - ph * 14;
   float patch[6][6];
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int ih = 2 * ph - 2 + i, iw = 2 * pw - 2 + j;
-      patch[i][j] = (ih >= 0 && ih < 28 && iw >= 0 && iw < 28) ? x[ih * 28 + iw] : 0.f;
-    }
-  uint32_t outw[4];
-  uint32_t idxw[2] = {0u, 0u};
+    for (int j = 0; j < 6; ++j) patch[i][j] = img[(2 * ph + i) * 32 + 2 * pw + j];
+  // channel pairs in a rolled loop: keeps the live set at patch (36) + 2x4 accumulators, so the
+  // kernel runs at high occupancy instead of one wave per SIMD with AGPR spills.
+  const size_t gp = (size_t)b * 196 + t;
+  uint32_t* outp = reinterpret_cast<uint32_t*>(a.p1 + gp * 32 + cg * 8);
+  uint64_t idxw = 0;
+#pragma unroll 1
+  for (int cp = 0; cp < 4; ++cp) {
+    uint32_t word = 0;
 #pragma unroll
-  for (int cc = 0; cc < 8; ++cc) {
-    const int c = cg * 8 + cc;
-    const float bias = w[KTAPS * C1 + c];
-    float z[4];
-#pragma unroll
-    for (int win = 0; win < 4; ++win) {
-      const int dy = win >> 1, dx = win & 1;
-      float acc = bias;
+    for (int h = 0; h < 2; ++h) {
+      const int cc = 2 * cp + h;
+      const float bias = w[KTAPS * 8 + cc];
+      float z[4] = {bias, bias, bias, bias};
 #pragma unroll
       for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
-        for (int kw = 0; kw < 5; ++kw) acc = fmaf(patch[dy + kh][dx + kw], w[(kh * 5 + kw) * C1 + c], acc);
-      z[win] = acc;
-    }
-    float mx = z[0];
-    int am = 0;
+        for (int kw = 0; kw < 5; ++kw) {
+          const float wt = w[(kh * 5 + kw) * 8 + cc];
+          z[0] = fmaf(patch[kh][kw], wt, z[0]);
+          z[1] = fmaf(patch[kh][kw + 1], wt, z[1]);
+          z[2] = fmaf(patch[kh + 1][kw], wt, z[2]);
+          z[3] = fmaf(patch[kh + 1][kw + 1], wt, z[3]);
+        }
+      float mx = z[0];
+      int am = 0;
 #pragma unroll
-    for (int win = 1; win < 4; ++win)
-      if (z[win] > mx) { mx = z[win]; am = win; }
-    mx = fmaxf(mx, 0.f);
-    const uint32_t hb = f2bf_bits(mx);
-    if (cc & 1) outw[cc >> 1] |= hb << 16; else outw[cc >> 1] = hb;
-    idxw[cc >> 2] |= (uint32_t)am << (8 * (cc & 3));
+      for (int win = 1; win < 4; ++win)
+        if (z[win] > mx) { mx = z[win]; am = win; }
+      word |= f2bf_bits(fmaxf(mx, 0.f)) << (16 * h);
+      idxw |= (uint64_t)am << (8 * cc);
+    }
+    outp[cp] = word;
   }
-  *reinterpret_cast<uint4*>(a.p1 + (size_t)gp * 32 + cg * 8) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
-  *reinterpret_cast<uint2*>(a.idx1 + (size_t)gp * 32 + cg * 8) = make_uint2(idxw[0], idxw[1]);
+  *reinterpret_cast<uint2*>(a.idx1 + gp * 32 + cg * 8) = make_uint2((uint32_t)idxw, (uint32_t)(idxw >> 32));
 }
 
 // ---------------- K2: conv2 implicit GEMM, pooled epilogue ----------------
@@ -121,7 +175,7 @@ struct PoolEpi {
     idx2[o] = (uint8_t)am;
   }
 };
-constexpr int C2F_BM = 64, C2F_BN = 64, C2F_BK = 64;
+constexpr int C2F_BM = 64, C2F_BN = 64, C2F_BK = TFD_C2F_BK;
 using C2F_B = DenseLoader<false>;
 __global__ __launch_bounds__(256) void conv2_pool_fwd(MnistStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -130,6 +184,117 @@ __global__ __launch_bounds__(256) void conv2_pool_fwd(MnistStepArgs a) {
   C2F_B lb{a.pbf + OFF_WC2, 64, 64, 800};
   PoolEpi epi{a.p32 + OFF_BC2, a.p2, a.idx2, M};
   gemm_block<C2F_BM, C2F_BN, C2F_BK, 2, 2>(la, lb, epi, blockIdx.x * C2F_BM, 0, 0, 800, (bf16*)smem_raw);
+}
+
+// ---------------- K2 (LDS-staged): whole-image implicit GEMM ----------------
+// Block = image b, 512 threads (8 waves), 152 KiB LDS. The image's 14x14x32 bf16 activations are
+// staged ONCE into a zero-bordered, channel-chunk-major LDS image [4 chunks][18 rows][24 cols]
+// x 16 B, and W2 as [800 k][64 n + 16] rows; every im2col A fragment is then one ds_read_b128 at
+// (pixel(m) + tap offset) -- no global re-reads of the 25x-expanded im2col matrix. Row stride
+// 24 px = 8 (mod 16) 16-B slots and 256-B-multiple chunk planes make the pool-window-ordered A
+// reads of a 16-lane group hit 16 distinct slots. M = 196 rows in pool-window-major order
+// (13 tiles), N = 64 (4 tiles), K = 800 (25 taps x 32 ci = one MFMA k-step per tap). Wave w owns
+// N-tiles {2(w & 1), 2(w & 1) + 1} and M-tiles {w >> 1, +4, +8, +12}: per tap 2 B + <=4 A fragment
+// reads feed <=8 MFMAs. Each lane's 4 accumulator rows are one 2x2 pool window, so bias + relu +
+// maxpool + argmax happen in registers.
+constexpr int C2F_W = 24, C2F_PLANE = 18 * C2F_W, C2F_WLD = 80;
+constexpr int C2L_FWD_SMEM = (4 * C2F_PLANE * 8 + 800 * C2F_WLD) * 2;  // 155648 B
+static_assert(C2F_PLANE * 16 % 256 == 0, "chunk planes must be bank-row aligned");
+__global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16* img = (bf16*)smem_raw;                        // [4][18*24][8]
+  bf16* wt = img + 4 * C2F_PLANE * 8;                 // [800][80]
+  const int b = blockIdx.x, t = threadIdx.x;
+  // Staging: every thread issues ALL of its 16-B loads before its first LDS store (a load->store
+  // loop serialises one global latency per iteration).
+  const uint16_t* src = a.p1 + (size_t)b * 196 * 32;
+  const uint16_t* wsrc = a.pbf + OFF_WC2;
+  const int rot = TFD_WROT ? (int)((blockIdx.x * 1031u) % 6400u) : 0;  // per-block start: spread L2 channels
+  {
+    constexpr int CI = 4 * C2F_PLANE, NI = (CI + 511) / 512;  // 1728 chunks -> 4 per thread
+    uint4 vi[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int i = t + 512 * j, ch = i / C2F_PLANE, px = i - ch * C2F_PLANE;
+      const int r = px / C2F_W - 2, c = px % C2F_W - 2;
+      vi[j] = (i < CI && (unsigned)r < 14u && (unsigned)c < 14u)
+                  ? *reinterpret_cast<const uint4*>(src + (r * 14 + c) * 32 + ch * 8) : zero4();
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      constexpr int NH = (3200 + 511) / 512;  // 800 rows x 8 chunks, two passes of 3200
+      uint4 vw[NH];
+#pragma unroll
+      for (int j = 0; j < NH; ++j) {
+        const int i = (half * 3200 + t + 512 * j + rot) % 6400;
+        vw[j] = (t + 512 * j < 3200) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 3) * 64 + (i & 7) * 8) : zero4();
+      }
+#pragma unroll
+      for (int j = 0; j < NH; ++j) {
+        const int i = (half * 3200 + t + 512 * j + rot) % 6400;
+        if (t + 512 * j < 3200) *reinterpret_cast<uint4*>(wt + (i >> 3) * C2F_WLD + (i & 7) * 8) = vw[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int i = t + 512 * j;
+      if (i < CI) *reinterpret_cast<uint4*>(img + i * 8) = vi[j];
+    }
+  }
+  __syncthreads();
+  const int lane = t & 63, w = t >> 6, np = w & 1, g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  const int mt0 = w >> 1, njt = (mt0 + 12 < 13) ? 4 : 3;
+  int base[4];
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int m = (mt0 + 4 * j) * 16 + (lane & 15);
+    int px = 0;
+    if (m < 196) {
+      const int pp = m >> 2, win = m & 3;
+      px = (2 * (pp / 7) + (win >> 1)) * C2F_W + 2 * (pp % 7) + (win & 1);  // + (kh*24 + kw) per tap
+    }
+    base[j] = (g * C2F_PLANE + px) * 8;
+  }
+  const bf16* wcol = wt + (8 * g + q) * C2F_WLD + np * 32 + 4 * p4;
+#pragma unroll
+  for (int kh = 0; kh < (TFD_EXP_SKIP_MAIN ? 0 : 5); ++kh) {
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) {
+      const int tap = kh * 5 + kw, toff = (kh * C2F_W + kw) * 8;
+      const bf16* wr = wcol + tap * 32 * C2F_WLD;
+      const bf16x8 b0 = frag_tr16(wr, wr + 4 * C2F_WLD);
+      const bf16x8 b1 = frag_tr16(wr + 16, wr + 16 + 4 * C2F_WLD);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j < njt) {
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + base[j] + toff);
+          acc[j][0] = mfma16x16x32(af, b0, acc[j][0]);
+          acc[j][1] = mfma16x16x32(af, b1, acc[j][1]);
+        }
+    }
+  }
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n = np * 32 + nt * 16 + (lane & 15);
+    const float bb = a.p32[OFF_BC2 + n];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m4 = (mt0 + 4 * j) * 16 + 4 * g;
+      if (j >= njt || m4 >= 196) continue;
+      float mx = acc[j][nt][0] + bb;
+      int am = 0;
+#pragma unroll
+      for (int r = 1; r < 4; ++r) {
+        const float z = acc[j][nt][r] + bb;
+        if (z > mx) { mx = z; am = r; }
+      }
+      const size_t o = (size_t)b * FEAT + (m4 >> 2) * 64 + n;
+      a.p2[o] = f2bf_bits(fmaxf(mx, 0.f));
+      a.idx2[o] = (uint8_t)am;
+    }
+  }
 }
 
 // ---------------- K3: fc1 forward, split-K slabs ----------------
@@ -143,7 +308,8 @@ struct SlabEpi {
       if (m4 + r < M) out[(size_t)(m4 + r) * ld + n] = v[r];
   }
 };
-constexpr int FC1_BM = 64, FC1_BN = 64, FC1_BK = 64;
+constexpr int FC1_BM = 64, FC1_BN = 64, FC1_BK = TFD_FC1_BK;
+constexpr int FC1_SPLITS = 7;  // 3136 = 7 * 448 = 7 * 7 * 64
 __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DenseLoader<true> la{a.p2, FEAT, a.B, FEAT};
@@ -161,9 +327,12 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n0 = 4 * t;
   f32x4 h = *reinterpret_cast<const f32x4*>(a.p32 + OFF_BD1 + n0);
-  for (int s = 0; s < a.fc1_splits; ++s) {
-    const f32x4 p = *reinterpret_cast<const f32x4*>(a.fc1_slab + ((size_t)s * a.B + row) * HID + n0);
-    h += p;
+  {  // all split-K slab loads in flight together (compile-time count: no per-load branches)
+    f32x4 p[FC1_SPLITS];
+#pragma unroll
+    for (int s = 0; s < FC1_SPLITS; ++s) p[s] = *reinterpret_cast<const f32x4*>(a.fc1_slab + ((size_t)s * a.B + row) * HID + n0);
+#pragma unroll
+    for (int s = 0; s < FC1_SPLITS; ++s) h += p[s];
   }
   float hd[4], scale[4];
   const float kp = train ? a.keep_prob : 1.0f;
@@ -293,7 +462,7 @@ struct OnesRowMC {  // operand (mn, k) = X[k][mn] for mn < mn_real, 1 for mn == 
     return *reinterpret_cast<uint4*>(t);
   }
 };
-constexpr int FDW_BM = 64, FDW_BN = 64, FDW_BK = 64;
+constexpr int FDW_BM = 64, FDW_BN = 64, FDW_BK = TFD_FDW_BK;
 __device__ __forceinline__ void fc1_dw_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   OnesRowMC la{a.p2, FEAT, FEAT, a.B};
   DenseLoader<false> lb{a.dh, HID, HID, a.B};
@@ -326,7 +495,7 @@ struct UnpoolEpi {
     }
   }
 };
-constexpr int FDX_BM = 32, FDX_BN = 64, FDX_BK = 64;
+constexpr int FDX_BM = 32, FDX_BN = 64, FDX_BK = TFD_FDX_BK;
 __device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   DenseLoader<true> la{a.dh, HID, a.B, HID};
   DenseLoader<true> lb{a.pbf + OFF_WD1, HID, FEAT, HID};
@@ -386,13 +555,124 @@ struct MaskEpi {
     }
   }
 };
-constexpr int C2D_BM = 64, C2D_BN = 32, C2D_BK = 64;
+constexpr int C2D_BM = 64, C2D_BN = 32, C2D_BK = TFD_C2D_BK;
 __device__ __forceinline__ void conv2_dgrad_block(const MnistStepArgs& a, int bx, bf16* smem) {
   const int M = a.B * 196;
   Conv2DgradA la{a.dz2, M};
   Conv2DgradB lb{a.pbf + OFF_WC2};
   MaskEpi epi{a.p1, a.dp1m, M};
   gemm_block<C2D_BM, C2D_BN, C2D_BK, 2, 2>(la, lb, epi, bx * C2D_BM, 0, 0, 1600, smem);
+}
+
+// ---------------- K13 (LDS-staged): conv2 dgrad + conv1 relu/pool-mask epilogue ----------------
+// Block = (image b, half h: input rows ih in [7h, 7h + 7)), 512 threads, 140.5 KiB LDS. dz2 rows oh
+// in [7h - 2, 7h + 9) are staged into a zero-bordered channel-chunk-major LDS image
+// [8 chunks][11 rows][20 cols] x 16 B (planes padded to 224 px = 256-B multiple) and the whole W2
+// as [tap*32 + ci][co] rows (stride 72): both once, no im2col traffic. dX[p][ci] = sum_{tap,co}
+// dz2[p - tap][co] W2[tap][ci][co]. M-tile = one input row (16 lanes = iw 0..15, 14 valid) so the 16
+// A-fragment lanes read 16 consecutive 16-B slots (conflict-free); N = 32 (2 tiles); K = 1600.
+// Wave w owns M-tiles {w & 3, (w & 3) + 4}, both N-tiles, and taps [0,13) (w < 4) or [13,25):
+// 2 A + 2 B fragment reads per 4 MFMAs; the two K halves are summed through LDS at the end.
+constexpr int C2D_ROWS = 11, C2D_COLS = 20, C2D_PLANE = 224, C2D_WLD = 72;
+constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 800 * C2D_WLD) * 2;  // 143872 B
+static_assert(C2D_PLANE * 16 % 256 == 0 && C2D_PLANE >= C2D_ROWS * C2D_COLS, "dz2 plane");
+__global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16* img = (bf16*)smem_raw;                           // [8][224][8]
+  bf16* wt = img + 8 * C2D_PLANE * 8;                    // [800][72]
+  const int b = blockIdx.x >> 1, h = blockIdx.x & 1, t = threadIdx.x;
+  const uint16_t* src = a.dz2 + (size_t)b * 196 * 64;
+  const uint16_t* wsrc = a.pbf + OFF_WC2;
+  const int rot = TFD_WROT ? (int)((blockIdx.x * 1031u) % 6400u) : 0;  // per-block start: spread L2 channels
+  {
+    constexpr int CI = 8 * C2D_PLANE, NI = (CI + 511) / 512;  // 1792 chunks -> 4 per thread
+    uint4 vi[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int i = t + 512 * j, ch = i / C2D_PLANE, px = i - ch * C2D_PLANE;
+      const int r = px / C2D_COLS + 7 * h - 2, c = px % C2D_COLS - 2;
+      vi[j] = (i < CI && px < C2D_ROWS * C2D_COLS && (unsigned)r < 14u && (unsigned)c < 14u)
+                  ? *reinterpret_cast<const uint4*>(src + (r * 14 + c) * 64 + ch * 8) : zero4();
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      constexpr int NH = (3200 + 511) / 512;
+      uint4 vw[NH];
+#pragma unroll
+      for (int j = 0; j < NH; ++j) {
+        const int i = (half * 3200 + t + 512 * j + rot) % 6400;
+        vw[j] = (t + 512 * j < 3200) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 3) * 64 + (i & 7) * 8) : zero4();
+      }
+#pragma unroll
+      for (int j = 0; j < NH; ++j) {
+        const int i = (half * 3200 + t + 512 * j + rot) % 6400;
+        if (t + 512 * j < 3200) *reinterpret_cast<uint4*>(wt + (i >> 3) * C2D_WLD + (i & 7) * 8) = vw[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int i = t + 512 * j;
+      if (i < CI) *reinterpret_cast<uint4*>(img + i * 8) = vi[j];
+    }
+  }
+  __syncthreads();
+  const int lane = t & 63, w = t >> 6, g = lane >> 4, mt0 = w & 3, kq = w >> 2;
+  const int two = (mt0 + 4 < 7);
+  const int iw = lane & 15;
+  int base[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) base[j] = ((mt0 + 4 * j + 4) * C2D_COLS + iw + 4) * 8 + g * C2D_PLANE * 8;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16* wrow = wt + (lane & 15) * C2D_WLD + 8 * g;
+  const int tap0 = kq ? 13 : 0, tap1 = TFD_EXP_SKIP_MAIN ? tap0 : (kq ? 25 : 13);
+#pragma unroll 1
+  for (int tap = tap0; tap < tap1; ++tap) {
+    const int kh = tap / 5, kw = tap - kh * 5, toff = -(kh * C2D_COLS + kw) * 8;
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk) {
+      const bf16* wr = wrow + tap * 32 * C2D_WLD + sk * 32;
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(wr);
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(wr + 16 * C2D_WLD);
+      const int coff = toff + sk * 4 * C2D_PLANE * 8;  // co chunk 4sk + g
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(img + base[0] + coff);
+      acc[0][0] = mfma16x16x32(a0, b0, acc[0][0]);
+      acc[0][1] = mfma16x16x32(a0, b1, acc[0][1]);
+      if (two) {
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(img + base[1] + coff);
+        acc[1][0] = mfma16x16x32(a1, b0, acc[1][0]);
+        acc[1][1] = mfma16x16x32(a1, b1, acc[1][1]);
+      }
+    }
+  }
+  // sum the two K halves: waves 4..7 park their accumulators in LDS (image region is dead now)
+  __syncthreads();
+  f32x4* park = reinterpret_cast<f32x4*>(smem_raw);  // [4 waves][4 tiles][64 lanes]
+  if (kq) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) park[(mt0 * 4 + j * 2 + nt) * 64 + lane] = acc[j][nt];
+  }
+  __syncthreads();
+  if (kq) return;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (j == 1 && !two) break;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const f32x4 v = acc[j][nt] + park[(mt0 * 4 + j * 2 + nt) * 64 + lane];
+      const int n = nt * 16 + (lane & 15), ih = 7 * h + mt0 + 4 * j;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int x = 4 * g + r;  // C row = input column iw
+        if (x >= 14) break;
+        const size_t o = ((size_t)b * 196 + ih * 14 + x) * 32 + n;
+        a.dp1m[o] = a.p1[o] != 0 ? f2bf_bits(v[r]) : (uint16_t)0;  // conv1 relu output > 0
+      }
+    }
+  }
 }
 
 // ---------------- K14 conv2 wgrad (+bias row), split-K slabs ----------------
@@ -410,7 +690,7 @@ struct Conv2WgradA {  // (mn = tap*32+ci [800 = ones row], k = pixel (b,oh,ow))
     return *reinterpret_cast<const uint4*>(p1 + ((size_t)(b * 14 + ih) * 14 + iw) * 32 + ci0);
   }
 };
-constexpr int C2W_BM = 64, C2W_BN = 64, C2W_BK = 64;
+constexpr int C2W_BM = 64, C2W_BN = 64, C2W_BK = TFD_C2W_BK;
 constexpr int C2W_GX = (801 + C2W_BM - 1) / C2W_BM;  // 13
 __device__ __forceinline__ void conv2_wgrad_block(const MnistStepArgs& a, int bx, int z, int kper, bf16* smem) {
   const int K = a.B * 196;
@@ -419,6 +699,10 @@ __device__ __forceinline__ void conv2_wgrad_block(const MnistStepArgs& a, int bx
   SlabEpi epi{a.wg2_slab + (size_t)z * 801 * 64, 64, 801, 64};
   const int kb = z * kper, ke = min(K, kb + kper);
   gemm_block<C2W_BM, C2W_BN, C2W_BK, 2, 2>(la, lb, epi, bx * C2W_BM, 0, kb, ke, smem);
+}
+__global__ __launch_bounds__(256) void conv2_wgrad_k(MnistStepArgs a, int kper) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  conv2_wgrad_block(a, blockIdx.x % C2W_GX, blockIdx.x / C2W_GX, kper, (bf16*)smem_raw);
 }
 // K13 + K14 in one launch: conv2 dgrad and wgrad both consume dz2 only (independent).
 __global__ __launch_bounds__(256) void conv2_bwd(MnistStepArgs a, int n_dgrad, int kper) {
@@ -430,25 +714,40 @@ __global__ __launch_bounds__(256) void conv2_bwd(MnistStepArgs a, int n_dgrad, i
 }
 
 // ---------------- K15 conv1 wgrad + bias grad (sparse, from pooled grad + argmax) ----------------
-// one block per image: thread (c = t & 31, sub = t >> 5); per-image slab [26][32].
+// Only the argmax position of each 2x2 window carries gradient, so dW1[tap][c] =
+// sum_{b,pp} g[b,pp,c] * x[b, argmax-pixel(pp,c) + tap]. Block = (image, half of the 196 pooled
+// pixels): the padded image and the block's dp1m / argmax rows are staged in LDS with 16-B loads
+// (no dependent global loads in the loop), thread (c = t & 31, sub = t >> 5) accumulates 26
+// partials (25 taps + bias), then the 8 subs are summed in LDS into one deterministic slab per block.
+constexpr int C1W_HALF = 98;
 __global__ __launch_bounds__(256) void conv1_wgrad(MnistStepArgs a) {
   __shared__ float img[32 * 32];
+  __shared__ __attribute__((aligned(16))) uint16_t gs[C1W_HALF * 32];
+  __shared__ __attribute__((aligned(16))) uint8_t is[C1W_HALF * 32];
   __shared__ float part[8][26 * 32 + 1];
-  const int b = blockIdx.x, t = threadIdx.x, c = t & 31, sub = t >> 5;
+  const int b = blockIdx.x >> 1, half = blockIdx.x & 1, t = threadIdx.x, c = t & 31, sub = t >> 5;
   const float* x = a.data + (size_t)data_row(a.perm, a.step, a.n_data, a.B, b) * 784;
-  for (int i = t; i < 32 * 32; i += 256) {
-    const int r = i >> 5, q = i & 31, ih = r - 2, iw = q - 2;
-    img[i] = (ih >= 0 && ih < 28 && iw >= 0 && iw < 28) ? x[ih * 28 + iw] : 0.f;
+  for (int i = t; i < 32 * 32; i += 256) img[i] = 0.f;
+  const size_t base = ((size_t)b * 196 + half * C1W_HALF) * 32;
+  for (int i = t; i < C1W_HALF * 32 / 8; i += 256)   // 392 x 16 B of bf16 grads
+    reinterpret_cast<uint4*>(gs)[i] = reinterpret_cast<const uint4*>(a.dp1m + base)[i];
+  for (int i = t; i < C1W_HALF * 32 / 16; i += 256)  // 196 x 16 B of argmax bytes
+    reinterpret_cast<uint4*>(is)[i] = reinterpret_cast<const uint4*>(a.idx1 + base)[i];
+  __syncthreads();
+  if (t < 196) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[t];
+    const int r = (4 * t) / 28, q = (4 * t) % 28;
+    float* d = img + (r + 2) * 32 + q + 2;
+    d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
   }
   __syncthreads();
   float acc[26];
 #pragma unroll
   for (int j = 0; j < 26; ++j) acc[j] = 0.f;
-  for (int pp = sub; pp < 196; pp += 8) {
-    const size_t o = ((size_t)b * 196 + pp) * 32 + c;
-    const float g = bf2f(a.dp1m[o]);
+  for (int lp = sub; lp < C1W_HALF; lp += 8) {
+    const float g = bf2f(gs[lp * 32 + c]);
     if (g != 0.f) {
-      const int w = a.idx1[o];
+      const int pp = half * C1W_HALF + lp, w = is[lp * 32 + c];
       const int oh = 2 * (pp / 14) + (w >> 1), ow = 2 * (pp % 14) + (w & 1);
 #pragma unroll
       for (int kh = 0; kh < 5; ++kh)
@@ -464,31 +763,46 @@ __global__ __launch_bounds__(256) void conv1_wgrad(MnistStepArgs a) {
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < 8; ++q) s += part[q][i];
-    a.wg1_slab[(size_t)b * 832 + i] = s;
+    a.wg1_slab[(size_t)blockIdx.x * 832 + i] = s;
   }
 }
 
 // Deterministic slab reductions of both conv weight-gradient slab sets in ONE launch:
 // thread (x = output column of a 64-wide chunk, y = slab phase 0..3); fixed summation order.
+template <int XW>  // XW outputs per block row, 256/XW slab phases
 __device__ __forceinline__ void reduce_chunk(const float* __restrict__ slab, int nslab, int64_t stride, int n, int i0,
                                              float* __restrict__ out, float* red) {
-  const int x = threadIdx.x & 63, y = threadIdx.x >> 6, i = i0 + x;
+  constexpr int NY = 256 / XW;
+  const int x = threadIdx.x % XW, y = threadIdx.x / XW, i = i0 + x;
   float s = 0.f;
-  if (i < n)
-    for (int k = y; k < nslab; k += 4) s += slab[(size_t)k * stride + i];
+  if (i < n) {
+    int k = y;
+    for (; k + 3 * NY < nslab; k += 4 * NY) {  // 4 independent loads in flight per thread
+      const float v0 = slab[(size_t)k * stride + i], v1 = slab[(size_t)(k + NY) * stride + i];
+      const float v2 = slab[(size_t)(k + 2 * NY) * stride + i], v3 = slab[(size_t)(k + 3 * NY) * stride + i];
+      s += (v0 + v1) + (v2 + v3);
+    }
+    for (; k < nslab; k += NY) s += slab[(size_t)k * stride + i];
+  }
   red[threadIdx.x] = s;
   __syncthreads();
-  if (y == 0 && i < n) out[i] = (red[x] + red[64 + x]) + (red[128 + x] + red[192 + x]);
+  if (y == 0 && i < n) {
+    float r = 0.f;
+#pragma unroll
+    for (int q = 0; q < NY; ++q) r += red[q * XW + x];
+    out[i] = r;
+  }
 }
-constexpr int RED2_BLOCKS = (801 * 64 + 63) / 64;  // 801
-constexpr int RED1_BLOCKS = (832 + 63) / 64;       // 13
+constexpr int RED2_BLOCKS = (801 * 64 + 63) / 64;  // 801 blocks x 64 outputs (4 phases over ~25 slabs)
+constexpr int RED1_BLOCKS = (832 + 15) / 16;       // 52 blocks x 16 outputs (16 phases over 2B slabs)
 __global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a) {
   __shared__ float red[256];
   const int id = blockIdx.x;
   if (id < RED2_BLOCKS)
-    reduce_chunk(a.wg2_slab, a.wg2_splits, 801 * 64, 801 * 64, id * 64, a.grad + OFF_WC2, red);
+    reduce_chunk<64>(a.wg2_slab, a.wg2_splits, 801 * 64, 801 * 64, id * 64, a.grad + OFF_WC2, red);
   else
-    reduce_chunk(a.wg1_slab, a.B, 832, 832, (id - RED2_BLOCKS) * 64, a.grad + OFF_WC1, red);
+    reduce_chunk<16>(a.wg1_slab, 2 * a.B, 832, 832, (id - RED2_BLOCKS) * 16, a.grad + OFF_WC1, red);
+  if (id == 0 && threadIdx.x == 0 && a.step_bump) *a.step_bump += 1;  // see MnistStepArgs::step_bump
 }
 
 template <auto K>
@@ -501,24 +815,26 @@ inline void set_smem(int bytes) {
 
 }  // namespace
 
-int mnist_fc1_splits(int B) { (void)B; return 7; }   // 3136 = 7 * 448 = 7 * 7 * 64
+int mnist_fc1_splits(int B) { (void)B; return FC1_SPLITS; }
 int mnist_wg2_splits(int B) {
   const int K = B * 196;
-  const int kper = 16 * C2W_BK;
+  const int kper = TFD_C2W_KPER;
   return (K + kper - 1) / kper;
 }
 
 void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s) {
   const int B = a.B;
-  {
-    const int threads = B * 196 * 4;
-    conv1_pool_fwd<<<(threads + 255) / 256, 256, 0, s>>>(a);
-  }
+  conv1_pool_fwd<<<4 * B, 256, 0, s>>>(a);
+#if TFD_CONV2_LDS
+  set_smem<conv2_fwd_lds>(C2L_FWD_SMEM);
+  conv2_fwd_lds<<<B, 512, C2L_FWD_SMEM, s>>>(a);
+#else
   {
     constexpr int sm = GemmSmem<C2F_BM, C2F_BN, C2F_BK, Conv2FwdA, C2F_B>::BYTES;
     set_smem<conv2_pool_fwd>(sm);
     conv2_pool_fwd<<<(B * 196 + C2F_BM - 1) / C2F_BM, 256, sm, s>>>(a);
   }
+#endif
   {
     constexpr int sm = GemmSmem<FC1_BM, FC1_BN, FC1_BK, DenseLoader<true>, DenseLoader<false>>::BYTES;
     set_smem<fc1_fwd>(sm);
@@ -540,19 +856,33 @@ void mnist_backward_a(const MnistStepArgs& a, hipStream_t s) {
   fc1_bwd<<<FDW_GX * FDW_GY + n_dx + OUTG_BLOCKS, 256, sm, s>>>(a, n_dx);
 }
 
-void mnist_backward_b(const MnistStepArgs& a, hipStream_t s) {
+void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
   const int B = a.B;
+  const int K = B * 196;
+  const int kper = ((K + a.wg2_splits - 1) / a.wg2_splits + C2W_BK - 1) / C2W_BK * C2W_BK;
+#if TFD_CONV2_LDS
+  // conv2 wgrad (slabs) runs on the aux stream beside dgrad -> conv1 wgrad (both only need dz2/p1)
+  constexpr int sm_w = GemmSmem<C2W_BM, C2W_BN, C2W_BK, Conv2WgradA, DenseLoader<false>>::BYTES;
+  set_smem<conv2_wgrad_k>(sm_w);
+  hipStream_t ws = aux ? aux : s;
+  if (aux) { (void)hipEventRecord(fork, s); (void)hipStreamWaitEvent(aux, fork, 0); }
+  conv2_wgrad_k<<<C2W_GX * a.wg2_splits, 256, sm_w, ws>>>(a, kper);
+  set_smem<conv2_dgrad_lds>(C2D_SMEM);
+  conv2_dgrad_lds<<<2 * B, 512, C2D_SMEM, s>>>(a);
+  conv1_wgrad<<<2 * B, 256, 0, s>>>(a);
+  if (aux) { (void)hipEventRecord(join, aux); (void)hipStreamWaitEvent(s, join, 0); }
+#else
+  (void)aux; (void)fork; (void)join;
   {
     constexpr int sm_d = GemmSmem<C2D_BM, C2D_BN, C2D_BK, Conv2DgradA, Conv2DgradB>::BYTES;
     constexpr int sm_w = GemmSmem<C2W_BM, C2W_BN, C2W_BK, Conv2WgradA, DenseLoader<false>>::BYTES;
     constexpr int sm = sm_d > sm_w ? sm_d : sm_w;
     set_smem<conv2_bwd>(sm);
-    const int K = B * 196;
-    const int kper = ((K + a.wg2_splits - 1) / a.wg2_splits + C2W_BK - 1) / C2W_BK * C2W_BK;
     const int n_dgrad = (B * 196 + C2D_BM - 1) / C2D_BM;
     conv2_bwd<<<n_dgrad + C2W_GX * a.wg2_splits, 256, sm, s>>>(a, n_dgrad, kper);
   }
-  conv1_wgrad<<<B, 256, 0, s>>>(a);
+  conv1_wgrad<<<2 * B, 256, 0, s>>>(a);
+#endif
   reduce_conv_grads<<<RED2_BLOCKS + RED1_BLOCKS, 256, 0, s>>>(a);
 }
 

@@ -4,9 +4,9 @@
 //   m_t = m + (g - m)(1 - b1);  v_t = v + (g^2 - v)(1 - b2)
 //   p  -= lr * sqrt(1 - b2^t) / (1 - b1^t) * m_t / (sqrt(v_t) + eps),   t = global_step + 1
 // The fp32 master is updated in place and its bf16 shadow (the operand every MFMA kernel reads)
-// is rewritten in the same pass. The device global_step is read by every block and incremented
-// by the last-arriving block (arrival counter, self-resetting) so a captured step graph needs no
-// host round trip.
+// is rewritten in the same pass. t comes from the device global_step (read-only here: the step's
+// last conv-grad reduce kernel bumps it), so a captured step graph needs no host round trip and
+// the optimizer needs no cross-block arrival counter (a 2048-way fan-in on one word).
 #include <math.h>
 #include "../common.h"
 #include "../tfd_kernels.h"
@@ -17,23 +17,8 @@ namespace {
 constexpr int kOptThreads = 256;
 constexpr int kOptMaxBlocks = 2048;
 
-__device__ __forceinline__ void bump_step(int64_t* step, unsigned* done) {
-  if (!step || !done) return;
-  // Every block has read *step (at entry) before it arrives here, so the last arriver may bump it
-  // without any data hand-off: no release/acquire fence is needed (a per-block __threadfence
-  // writes back the XCD L2 once per block, which serialised the 13 MB update).
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev = atomicAdd(done, 1u);
-    if (prev == gridDim.x - 1) {
-      atomicAdd(reinterpret_cast<unsigned long long*>(step), 1ull);
-      atomicExch(done, 0u);
-    }
-  }
-}
-
 __global__ __launch_bounds__(kOptThreads) void adam_kernel(AdamArgs a) {
-  const int64_t t = (a.step ? *a.step : 0) + 1;
+  const int64_t t = (a.step ? *a.step : 0) + a.t_offset;
   const float b1p = powf(a.beta1, (float)t), b2p = powf(a.beta2, (float)t);
   const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float c1 = 1.f - a.beta1, c2 = 1.f - a.beta2;
@@ -70,7 +55,6 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(AdamArgs a) {
     a.p[i] = p; a.m[i] = m; a.v[i] = v;
     if (a.pbf) a.pbf[i] = f2bf_bits(p);
   }
-  bump_step(a.step, a.done);
 }
 
 // GradientDescent / Momentum (TF ApplyMomentum: accum = accum*mu + g; p -= lr*accum,
@@ -90,7 +74,6 @@ __global__ __launch_bounds__(kOptThreads) void sgd_kernel(SgdArgs a) {
     a.p[i] = p;
     if (a.pbf) a.pbf[i] = f2bf_bits(p);
   }
-  bump_step(a.step, a.done);
 }
 
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, int64_t n) {

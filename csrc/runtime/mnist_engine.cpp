@@ -44,7 +44,6 @@ class MnistEngine : public torch::CustomClassHolder {
     v_ = at::zeros({TOTAL}, f32);
     gbf_ = at::zeros({TOTAL}, bf);
     step_ = at::zeros({1}, i64);
-    done_ = at::zeros({1}, i32);
     fc1_splits_ = mnist_fc1_splits((int)B_);
     wg2_splits_ = mnist_wg2_splits((int)B_);
     p1_ = at::empty({B_, P1H, P1H, C1}, bf);
@@ -60,7 +59,7 @@ class MnistEngine : public torch::CustomClassHolder {
     dz2_ = at::empty({B_, P1H, P1H, C2}, bf);
     dp1m_ = at::empty({B_, P1H, P1H, C1}, bf);
     wg2_slab_ = at::empty({wg2_splits_, 801, C2}, f32);
-    wg1_slab_ = at::empty({B_, 832}, f32);
+    wg1_slab_ = at::empty({2 * B_, 832}, f32);
     xbuf_ = at::zeros({B_, 784}, f32);
     ybuf_ = at::zeros({B_}, i32);
     HIP_OK(hipSetDevice((int)device));
@@ -68,6 +67,9 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_b_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
+    HIP_OK(hipStreamCreateWithFlags(&aux_stream_, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
   }
   ~MnistEngine() override {
     for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
@@ -75,6 +77,9 @@ class MnistEngine : public torch::CustomClassHolder {
     hipEventDestroy(ev_b_);
     hipEventDestroy(ev_done_);
     hipStreamDestroy(comm_stream_);
+    hipEventDestroy(ev_fork_);
+    hipEventDestroy(ev_join_);
+    hipStreamDestroy(aux_stream_);
   }
 
   // ---- state accessors (views share storage with the engine) ----
@@ -126,18 +131,24 @@ class MnistEngine : public torch::CustomClassHolder {
   // ---- step pieces (current HIP stream) ----
   void forward(bool train) { mnist_forward(args(), train, stream()); }
   void backward_a() { mnist_backward_a(args(), stream()); }
-  void backward_b() { mnist_backward_b(args(), stream()); }
+  // backward_b ends with the conv-grad reduce kernel, which also bumps global_step (see
+  // MnistStepArgs::step_bump): apply_optimizer() after it therefore uses t = global_step.
+  void backward_b() {
+    MnistStepArgs a = args();
+    a.step_bump = (int64_t*)step_.data_ptr();
+    mnist_backward_b(a, stream(), aux_stream_, ev_fork_, ev_join_);
+  }
   void apply_optimizer(double grad_scale) {
     const uint16_t* gbf = (comm_ && bf16_comm_ && comm_->world() > 1) ? (const uint16_t*)gbf_.data_ptr() : nullptr;
     if (opt_ == 0) {
       AdamArgs a{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(), (const float*)grad_.data_ptr(),
                  (uint16_t*)pbf_.data_ptr(), gbf, TOTAL, (float)lr_, (float)b1_, (float)b2_, (float)eps_,
-                 (int64_t*)step_.data_ptr(), (unsigned*)done_.data_ptr(), (float)grad_scale};
+                 (const int64_t*)step_.data_ptr(), 0, (float)grad_scale};
       adam_apply(a, stream());
     } else {
       SgdArgs a{(float*)params_.data_ptr(), opt_ == 2 ? (float*)m_.data_ptr() : nullptr, (const float*)grad_.data_ptr(),
                 (uint16_t*)pbf_.data_ptr(), gbf, TOTAL, (float)lr_, (float)momentum_, 0.f, (float)grad_scale,
-                nesterov_ ? 1 : 0, (int64_t*)step_.data_ptr(), (unsigned*)done_.data_ptr()};
+                nesterov_ ? 1 : 0};
       sgd_apply(a, stream());
     }
   }
@@ -289,12 +300,13 @@ class MnistEngine : public torch::CustomClassHolder {
   bool nesterov_ = false;
   bool bf16_comm_ = true;
   c10::intrusive_ptr<RcclComm> comm_;
-  at::Tensor params_, pbf_, grad_, m_, v_, gbf_, step_, done_;
+  at::Tensor params_, pbf_, grad_, m_, v_, gbf_, step_;
   at::Tensor p1_, idx1_, p2_, idx2_, fc1_slab_, hd_, dh_, dlogits_, loss_row_, correct_row_, dz2_, dp1m_, wg2_slab_,
       wg1_slab_, xbuf_, ybuf_;
   at::Tensor data_, labels_, perm_;
   hipStream_t comm_stream_ = nullptr;
-  hipEvent_t ev_a_ = nullptr, ev_b_ = nullptr, ev_done_ = nullptr;
+  hipEvent_t ev_a_ = nullptr, ev_b_ = nullptr, ev_done_ = nullptr, ev_fork_ = nullptr, ev_join_ = nullptr;
+  hipStream_t aux_stream_ = nullptr;
   std::map<std::string, hipGraphExec_t> graphs_;
 };
 

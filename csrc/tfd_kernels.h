@@ -15,7 +15,10 @@ struct MnistStepArgs {
   const int* labels;
   const int* perm;
   int n_data;
-  const int64_t* step;         // device global_step (read by every kernel, bumped by the optimizer)
+  const int64_t* step;         // device global_step (read by every kernel of the step)
+  int64_t* step_bump;          // if set, the last conv-grad reduce kernel increments *step (it is the
+                               // first kernel of the step that no longer reads it; the optimizer after it
+                               // then sees t = global_step + 1 directly)
   // params
   const float* p32;            // flat fp32 master params (mnist_layout.h)
   const uint16_t* pbf;         // flat bf16 shadow of p32
@@ -30,7 +33,7 @@ struct MnistStepArgs {
   uint16_t* dz2;                  // [B][14][14][64]
   uint16_t* dp1m;                 // [B][14][14][32]
   float* wg2_slab;                // [wg2_splits][801][64]
-  float* wg1_slab;                // [B][832]
+  float* wg1_slab;                // [2B][832] (one slab per half image)
   int fc1_splits, wg2_splits;
   float keep_prob;
   uint32_t seed, rank;
@@ -40,7 +43,10 @@ int mnist_fc1_splits(int B);
 int mnist_wg2_splits(int B);
 void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s);        // conv1, conv2, fc1, head
 void mnist_backward_a(const MnistStepArgs& a, hipStream_t s);                 // fc1 dW/dX -> bucket A done
-void mnist_backward_b(const MnistStepArgs& a, hipStream_t s);                 // conv2/conv1 grads -> bucket B done
+// conv2/conv1 grads -> bucket B done. With `aux` set, independent kernels fork onto it (fork/join
+// events recorded on s/aux; both are captured into the step graph as parallel branches).
+void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux = nullptr, hipEvent_t fork = nullptr,
+                      hipEvent_t join = nullptr);
 
 // ---------------- optimizers (flat, fp32 master + bf16 shadow) ----------------
 struct AdamArgs {
@@ -48,15 +54,14 @@ struct AdamArgs {
   const uint16_t* gbf;         // if non-null, gradients are read from this bf16 buffer instead of g
   int64_t n;
   float lr, beta1, beta2, eps;
-  int64_t* step;               // device step; t = *step + 1; the last block increments it
-  unsigned* done;              // arrival counter (zero-initialised once; self-resetting)
+  const int64_t* step;         // device step counter; Adam's t = *step + t_offset (read-only here)
+  int t_offset;
   float grad_scale;            // multiply g (e.g. 1/N for sum-all-reduce)
 };
 void adam_apply(const AdamArgs& a, hipStream_t s);
 struct SgdArgs {
   float* p; float* mom; const float* g; uint16_t* pbf; const uint16_t* gbf; int64_t n;
   float lr, momentum, weight_decay, grad_scale; int nesterov;
-  int64_t* step; unsigned* done;
 };
 void sgd_apply(const SgdArgs& a, hipStream_t s);
 void cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);

@@ -21,8 +21,13 @@ import sysconfig
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "csrc")
 PKG = os.path.join(ROOT, "tensorflow_distributed_amd")
-BUILD = os.path.join(ROOT, "build", "native")
-OUT = os.path.join(PKG, "_C.so")
+# Variant builds for A/B kernel experiments: TFD_VARIANT=name + TFD_EXTRA_FLAGS="-DX=1 ..." build
+# into build/native-<name>/ and link tensorflow_distributed_amd/_C_<name>.so; load it with
+# TFD_NATIVE_LIB=<path>.
+VARIANT = os.environ.get("TFD_VARIANT", "")
+EXTRA_FLAGS = os.environ.get("TFD_EXTRA_FLAGS", "").split()
+BUILD = os.path.join(ROOT, "build", "native" + (f"-{VARIANT}" if VARIANT else ""))
+OUT = os.path.join(PKG, f"_C_{VARIANT}.so" if VARIANT else "_C.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("TFD_OFFLOAD_ARCH", "gfx950")
 
@@ -61,7 +66,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     hip_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")) + glob.glob(os.path.join(CSRC, "comm", "*.hip")))
     cpp_srcs = sorted(glob.glob(os.path.join(CSRC, "bindings", "*.cpp")) + glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     hdr_mtime = max([os.path.getmtime(h) for h in _headers()] + [0])
-    common = ["-O3", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={int(abi)}", "-I", CSRC]
+    common = ["-O3", "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={int(abi)}", "-I", CSRC] + EXTRA_FLAGS
     hip_flags = common + [
         "-x", "hip", f"--offload-arch={ARCH}", "-D__HIP_PLATFORM_AMD__=1",
         "-ffp-contract=fast", "-munsafe-fp-atomics", "-Wno-unused-result",

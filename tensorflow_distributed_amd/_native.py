@@ -12,7 +12,7 @@ import threading
 
 import torch
 
-_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_C.so")
+_LIB = os.environ.get("TFD_NATIVE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_C.so")
 _lock = threading.Lock()
 _loaded = False
 _error: Exception | None = None
