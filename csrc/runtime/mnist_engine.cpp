@@ -178,6 +178,20 @@ class MnistEngine : public torch::CustomClassHolder {
     apply_optimizer(dp ? 1.0 / (double)comm_->world() : 1.0);
   }
 
+  // Backup-worker path (SyncReplicas with replicas_to_aggregate < workers): sum-all-reduce of
+  // weight * local grads over the whole flat buffer (no optimizer). weight is 1 for the chosen
+  // replicas and 0 for the dropped stragglers; apply_optimizer(1/R) follows.
+  void reduce_grads(double weight) {
+    hipStream_t s = stream();
+    if (weight != 1.0) scale_f32((float*)grad_.data_ptr(), TOTAL, (float)weight, s);
+    if (!comm_ || comm_->world() <= 1) return;
+    HIP_OK(hipEventRecord(ev_a_, s));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
+    reduce_bucket(0, TOTAL);
+    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+  }
+
   // Evaluate on an explicit batch (x [n,784] fp32, y [n] int32) in chunks of <= B.
   // Returns a 2-element fp32 GPU tensor {sum of per-example loss, number correct}.
   at::Tensor evaluate(at::Tensor x, at::Tensor y) {
@@ -350,6 +364,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("backward_a", &MnistEngine::backward_a)
       .def("backward_b", &MnistEngine::backward_b)
       .def("apply_optimizer", &MnistEngine::apply_optimizer)
+      .def("reduce_grads", &MnistEngine::reduce_grads)
       .def("train_step", &MnistEngine::train_step)
       .def("evaluate", &MnistEngine::evaluate)
       .def("capture_train_step", &MnistEngine::capture_train_step)

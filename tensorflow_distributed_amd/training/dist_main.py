@@ -1,0 +1,325 @@
+"""The distributed trainer behind ``mnist_python_m.py`` / ``mnist_python_w1.py`` / ``mnist_python_w2.py``
+(``/root/reference/mnist_python_m.py:49-326``): same 14 flags and defaults, same roles, same stdout.
+
+Roles:
+  * ``--job_name=ps``: hosts the rendezvous store at ``--ps_hosts[task_index]`` (task 0), joins the
+    control group and runs ``server.join()`` -- the async parameter-server service when
+    ``--sync_replicas=False``, otherwise it just waits for the workers' completion signal.
+  * ``--job_name=worker``: task 0 is the chief. GPU ``task_index % num_gpus`` (``--num_gpus>0``)
+    or CPU. Chief initialises (or restores) and broadcasts; the loop runs until the GLOBAL step
+    reaches ``--train_steps``; then a 5 x 1000 validation pass.
+
+Sync mode = all-reduce DP with SyncReplicasOptimizer semantics (parallel/sync_replicas.py); async
+mode = Hogwild PS over Gloo point-to-point (parallel/async_ps.py).
+"""
+from __future__ import annotations
+
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+from ..utils import flags as flags_mod
+from ..utils.flags import FLAGS
+
+_DEFINED = False
+
+
+def define_flags(task_index_default: int = 0, job_name_default: str = "ps") -> None:
+    """The reference's 14 flags (mnist_python_m.py:49-87) + framework extras."""
+    global _DEFINED
+    f = flags_mod
+    if _DEFINED:
+        FLAGS._flags["task_index"].default = task_index_default
+        FLAGS._flags["job_name"].default = job_name_default
+        FLAGS.reset()
+        return
+    _DEFINED = True
+    f.DEFINE_string("data_dir", "/tmp/mnist-data", "Directory for storing mnist data")
+    f.DEFINE_boolean("download_only", False, "Only perform downloading of data; Do not proceed to "
+                     "session preparation, model definition or training")
+    f.DEFINE_integer("task_index", task_index_default, "Worker task index, should be >= 0. task_index=0 is "
+                     "the master worker task the performs the variable initialization ")
+    f.DEFINE_integer("num_gpus", 0, "Total number of gpus for each machine. If you don't use GPU, please set it to '0'")
+    f.DEFINE_integer("replicas_to_aggregate", 2, "Number of replicas to aggregate before parameter update"
+                     "is applied (For sync_replicas mode only; default: num_workers)")
+    f.DEFINE_integer("hidden_units", 100, "Number of units in the hidden layer of the NN (unused by the CNN, "
+                     "kept for flag compatibility)")
+    f.DEFINE_integer("train_steps", 4, "Number of (global) training steps to perform")
+    f.DEFINE_integer("batch_size", 128, "Training batch size")
+    f.DEFINE_float("learning_rate", 0.01, "Learning rate")
+    f.DEFINE_boolean("sync_replicas", True, "Use the sync_replicas (synchronized replicas) mode, "
+                     "wherein the parameter updates from workers are aggregated before applied to "
+                     "avoid stale gradients")
+    f.DEFINE_boolean("existing_servers", False, "Whether servers already exists. If True, will use "
+                     "the worker hosts via their GRPC URLs (one client process per worker host). "
+                     "Otherwise, will create an in-process TensorFlow server.")
+    f.DEFINE_string("ps_hosts", "10.0.1.3:2222", "Comma-separated list of hostname:port pairs")
+    f.DEFINE_string("worker_hosts", "10.0.1.6:2223,10.0.1.2:2224", "Comma-separated list of hostname:port pairs")
+    f.DEFINE_string("job_name", job_name_default, "job name: worker or ps")
+    # ---- framework extras ----
+    f.DEFINE_string("logdir", "", "Supervisor logdir (checkpoints, events). Empty = tempfile.mkdtemp() "
+                    "like the reference; set it to a stable path to enable resume")
+    f.DEFINE_float("save_model_secs", 600.0, "Checkpoint period (chief)")
+    f.DEFINE_float("save_summaries_secs", 120.0, "Summary (global_step/sec) period (chief)")
+    f.DEFINE_integer("seed", 0, "Init seed (normal(0,1) params, chief)")
+    f.DEFINE_float("keep_prob", 0.75, "Dropout keep probability during training")
+    f.DEFINE_enum("optimizer", "adam", ["adam", "sgd", "momentum"], "Optimizer (reference: adam)")
+    f.DEFINE_float("momentum", 0.9, "Momentum for --optimizer=momentum")
+    f.DEFINE_boolean("synthetic_data", False, "Use the synthetic MNIST-shaped dataset even if IDX files exist")
+    f.DEFINE_boolean("bf16_grads", True, "All-reduce gradients in bf16 (GPU)")
+    f.DEFINE_boolean("use_graph", True, "Replay the captured hipGraph of the train step (GPU)")
+    f.DEFINE_integer("eval_batches", 5, "Validation batches after training")
+    f.DEFINE_integer("eval_batch_size", 1000, "Validation batch size")
+    f.DEFINE_string("metrics_file", "", "Chief: JSONL metrics per step")
+    f.DEFINE_string("trace_file", "", "Chrome-trace JSON of host step phases")
+    f.DEFINE_integer("check_consistency_every", 0, "Every N steps all-reduce a param checksum and "
+                     "fail on cross-worker desync (sync mode)")
+    f.DEFINE_integer("fault_inject_step", -1, "Test hook: the worker --fault_inject_task exits abruptly "
+                     "when its global step reaches this value (first attempt only)")
+    f.DEFINE_integer("fault_inject_task", -1, "Worker task index for --fault_inject_step")
+    f.DEFINE_string("straggler_delay", "", "Test hook: 'task:seconds,...' artificial per-step delay "
+                    "(backup-worker tests)")
+    f.DEFINE_float("rendezvous_timeout", 600.0, "Seconds to wait for the cluster to assemble")
+    f.DEFINE_boolean("quiet", False, "Suppress per-step prints")
+
+
+def _make_optimizer():
+    from .optimizers import AdamOptimizer, GradientDescentOptimizer, MomentumOptimizer
+
+    if FLAGS.optimizer == "sgd":
+        return GradientDescentOptimizer(FLAGS.learning_rate)
+    if FLAGS.optimizer == "momentum":
+        return MomentumOptimizer(FLAGS.learning_rate, FLAGS.momentum)
+    return AdamOptimizer(FLAGS.learning_rate)
+
+
+def _worker_rccl_comm(server, device):
+    import torch.distributed as dist
+
+    from .. import _native
+
+    _native.require()
+    c = server.cluster
+    src = c.num_ps  # global rank of worker 0
+    if server.rank == src:
+        uid = torch.classes.tfd.RcclComm.unique_id()
+    else:
+        uid = torch.zeros(128, dtype=torch.uint8)
+    dist.broadcast(uid, src, group=server.worker_group)
+    return torch.classes.tfd.RcclComm(uid, c.num_workers, server.task_index, device.index)
+
+
+def main(argv=None) -> int:
+    from ..models import mnist_cnn as M
+    from ..models.mnist_runner import make_runner
+    from ..parallel import async_ps, sync_replicas
+    from ..parallel.cluster import ClusterSpec, Server
+    from ..utils import input_data
+    from ..utils.metrics import MetricsLogger, StepTimer
+    from .optimizers import SyncReplicasOptimizer
+    from .supervisor import Supervisor
+
+    if FLAGS.download_only:
+        # no network on MI355X boxes: materialise the IDX files (synthetic if absent) and stop
+        print("MNIST data in %s: %s" % (FLAGS.data_dir, input_data.maybe_download(FLAGS.data_dir)))
+        sys.exit(0)
+    mnist = input_data.read_data_sets(FLAGS.data_dir, one_hot=True, fake_data=FLAGS.synthetic_data,
+                                      seed=FLAGS.seed * 1000 + max(FLAGS.task_index, 0) + 17)
+
+    if FLAGS.job_name is None or FLAGS.job_name == "":
+        raise ValueError("Must specify an explicit `job_name`")
+    if FLAGS.task_index is None or FLAGS.task_index == "":
+        raise ValueError("Must specify an explicit `task_index`")
+
+    print("job name = %s" % FLAGS.job_name)
+    print("task index = %d" % FLAGS.task_index)
+
+    ps_spec = FLAGS.ps_hosts.split(",")
+    worker_spec = FLAGS.worker_hosts.split(",")
+    num_workers = len(worker_spec)
+    cluster = ClusterSpec({"ps": ps_spec, "worker": worker_spec})
+
+    server = Server(cluster, job_name=FLAGS.job_name, task_index=FLAGS.task_index,
+                    existing_servers=FLAGS.existing_servers, timeout_s=FLAGS.rendezvous_timeout)
+    opt = _make_optimizer()
+    layout = async_ps.mnist_layout(cluster.num_ps) if cluster.num_ps else None
+    if not FLAGS.sync_replicas and layout is None:
+        raise ValueError("--sync_replicas=False (async parameter-server mode) needs at least one --ps_hosts task")
+
+    if FLAGS.job_name == "ps":
+        # (reference quirk Q9: ps + existing_servers fell through to the worker code; a PS here
+        #  always serves and then exits once every worker has finished)
+        service = None
+        if not FLAGS.sync_replicas:
+            service = async_ps.ParameterServerService(FLAGS.task_index, cluster.num_ps, num_workers, layout, opt)
+        server.join(service)
+        server.shutdown()
+        return 0
+
+    is_chief = FLAGS.task_index == 0
+    if FLAGS.num_gpus > 0:
+        gpu = FLAGS.task_index % FLAGS.num_gpus
+        torch.cuda.set_device(gpu)
+        device = torch.device("cuda", gpu)
+    else:
+        device = torch.device("cpu")
+
+    sync = FLAGS.sync_replicas
+    sopt = None
+    if sync:
+        r2a = FLAGS.replicas_to_aggregate if FLAGS.replicas_to_aggregate is not None else num_workers
+        sopt = SyncReplicasOptimizer(opt, replicas_to_aggregate=r2a, total_num_replicas=num_workers).resolve(num_workers)
+
+    comm = None
+    if device.type == "cuda" and sync and num_workers > 1:
+        comm = _worker_rccl_comm(server, device)
+    runner = make_runner(FLAGS.batch_size, opt, device, keep_prob=FLAGS.keep_prob, seed=FLAGS.seed,
+                         rank=FLAGS.task_index, comm=comm, bf16_grads=FLAGS.bf16_grads,
+                         use_graph=FLAGS.use_graph and (sopt is None or not sopt.has_backup_workers))
+
+    def init_fn():
+        flat = M.flat_from_dict(M.init_params(FLAGS.seed))
+        runner.load_flat(flat, {}, 0)
+
+    client = None
+    if sync:
+        def broadcast_fn():
+            if num_workers > 1:
+                sync_replicas.broadcast_state(runner, 0, group=server.worker_group, group_src_rank=cluster.num_ps)
+    else:
+        client = async_ps.AsyncPSClient(FLAGS.task_index, layout)
+
+        def broadcast_fn():
+            flat = runner.params().detach().float().cpu()
+            if is_chief:
+                client.init(flat, step=runner.global_step(), t=runner.global_step())
+            gs = client.pull(flat)
+            runner.set_params(flat)
+            runner.set_global_step(gs)
+
+    logdir = FLAGS.logdir or tempfile.mkdtemp()
+    sv = Supervisor(is_chief=is_chief, logdir=logdir, runner=runner, init_fn=init_fn, broadcast_fn=broadcast_fn,
+                    save_model_secs=FLAGS.save_model_secs, save_summaries_secs=FLAGS.save_summaries_secs,
+                    recovery_wait_secs=1)
+
+    if is_chief:
+        print("Worker %d: Initializing session..." % FLAGS.task_index)
+    else:
+        print("Worker %d: Waiting for session to be initialized..." % FLAGS.task_index)
+    if FLAGS.existing_servers:
+        server_grpc_url = "grpc://" + worker_spec[FLAGS.task_index]
+        print("Using existing server at: %s" % server_grpc_url)
+    sys.stdout.flush()
+    sv.prepare_or_wait_for_session()
+    print("Worker %d: Session initialization complete." % FLAGS.task_index)
+
+    delays = {}
+    if FLAGS.straggler_delay:
+        for item in FLAGS.straggler_delay.split(","):
+            k, v = item.split(":")
+            delays[int(k)] = float(v)
+    stepper = None
+    if sync:
+        stepper = sync_replicas.SyncReplicasStepper(runner, FLAGS.task_index, num_workers, sopt.replicas_to_aggregate,
+                                                    group=server.worker_group, straggler_delay_s=delays)
+    metrics = MetricsLogger(FLAGS.metrics_file if is_chief else "")
+    timer = StepTimer(pid=FLAGS.task_index, enabled=bool(FLAGS.trace_file))
+    restart_attempt = int(os.environ.get("TFD_RESTART_COUNT", "0"))
+
+    time_begin = time.time()
+    print("Training begins @ %f" % time_begin)
+    local_step = 0
+    step = runner.global_step()
+    grad_cpu = None
+    while True:
+        if step >= FLAGS.train_steps:
+            break
+        with timer.phase("input"):
+            batch_xs, batch_ys = mnist.train.next_batch(FLAGS.batch_size)
+        t0 = time.time()
+        with timer.phase("step"):
+            if sync:
+                stepper.step(batch_xs, batch_ys)
+                step = runner.global_step()
+            else:
+                g, _ = runner.compute_grads(batch_xs, batch_ys)
+                if grad_cpu is None:
+                    grad_cpu = torch.zeros(M.TOTAL)
+                grad_cpu.copy_(g.detach().float().cpu())
+                flat = runner.params().detach().float().cpu()
+                step = client.push_pull(flat, grad_cpu)
+                runner.set_params(flat)
+                runner.set_global_step(step)
+        local_step += 1
+        now = time.time()
+        if not FLAGS.quiet:
+            print("%f: Worker %d: training step %d done (global step: %d)" % (now, FLAGS.task_index, local_step, step))
+        metrics.log(step=local_step, global_step=step, step_ms=1e3 * (now - t0),
+                    images_per_sec=FLAGS.batch_size * (num_workers if sync else 1) / max(now - t0, 1e-9))
+        if FLAGS.check_consistency_every and sync and local_step % FLAGS.check_consistency_every == 0:
+            _check_consistency(runner, server, num_workers)
+        sv.on_step(step)
+        if (FLAGS.fault_inject_step >= 0 and FLAGS.task_index == FLAGS.fault_inject_task and restart_attempt == 0
+                and step >= FLAGS.fault_inject_step):
+            print("Worker %d: fault injection at global step %d" % (FLAGS.task_index, step), flush=True)
+            os._exit(17)
+
+    time_end = time.time()
+    print("Training ends @ %f" % time_end)
+    training_time = time_end - time_begin
+    print("Training elapsed time: %f s" % training_time)
+
+    accuracy_arr = []
+    nt = FLAGS.eval_batches
+    for counter in range(1, nt + 1):
+        val_x, val_y = mnist.validation.next_batch(FLAGS.eval_batch_size)
+        _, correct = runner.evaluate(val_x, val_y)
+        val_xent = correct / float(len(val_x))
+        print("After %d training step(s)", FLAGS.train_steps)  # verbatim reference line (quirk Q3)
+        print("Accuracy : %f" % val_xent)
+        accuracy_arr.append(val_xent)
+    mean_accuracy = sum(accuracy_arr) / len(accuracy_arr) if accuracy_arr else float("nan")
+    print("Mean Accuracy : %f" % mean_accuracy)
+    sys.stdout.flush()
+
+    metrics.log(event="final", global_step=step, training_time_s=training_time, mean_accuracy=mean_accuracy)
+    metrics.close()
+    if FLAGS.trace_file:
+        timer.write_chrome_trace(FLAGS.trace_file.replace("{task}", str(FLAGS.task_index)))
+    sv.stop(save=True)
+    if client is not None:
+        client.stop()
+    server.mark_done()
+    if sync and num_workers > 1:
+        import torch.distributed as dist
+
+        dist.barrier(group=server.worker_group)
+    server.shutdown()
+    return 0
+
+
+def _check_consistency(runner, server, num_workers):
+    """Race/desync detector: max |checksum_i - checksum_0| across workers."""
+    import torch.distributed as dist
+
+    p = runner.params().detach().double()
+    cs = torch.tensor([float(p.sum().item()), float((p * p).sum().item())], dtype=torch.float64)
+    mx, mn = cs.clone(), cs.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=server.worker_group)
+    dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=server.worker_group)
+    if not torch.equal(mx, mn):
+        raise RuntimeError(f"worker parameter desync detected: checksum range {mn.tolist()} .. {mx.tolist()}")
+
+
+def run_script(task_index_default: int, job_name_default: str, argv=None) -> int:
+    define_flags(task_index_default, job_name_default)
+    argv = list(sys.argv if argv is None else argv)
+    if "--help" in argv or "-h" in argv:
+        print(f"usage: {argv[0]} [flags]\n{FLAGS.help_text()}")
+        return 0
+    FLAGS.parse(argv)
+    return main(argv) or 0

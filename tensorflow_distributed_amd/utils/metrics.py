@@ -1,0 +1,86 @@
+"""Metrics, step timing and trace export.
+
+* :class:`MetricsLogger` -- ``--metrics_file`` JSONL on the chief: one record per step
+  (step, global_step, loss, images/sec, step_ms, ...).
+* :class:`StepTimer` -- host wall-clock phases plus optional HIP events; keeps a chrome-trace
+  (``chrome://tracing`` / Perfetto JSON) of per-phase spans for ``--trace_file``.
+* :func:`performance_table` -- the reference's ``performance`` file format
+  (``Steps ,Time ,Accuracy, Learning rate``, ``/root/reference/performance:1-6``).
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+from contextlib import contextmanager
+from typing import Dict, List, Optional
+
+
+class MetricsLogger:
+    def __init__(self, path: Optional[str]):
+        self.path = path
+        self._f = None
+        self._lock = threading.Lock()
+        if path:
+            d = os.path.dirname(path)
+            if d:
+                os.makedirs(d, exist_ok=True)
+            self._f = open(path, "a")
+
+    def log(self, **rec) -> None:
+        if self._f is None:
+            return
+        rec.setdefault("time", time.time())
+        with self._lock:
+            self._f.write(json.dumps(rec) + "\n")
+            self._f.flush()
+
+    def close(self):
+        if self._f is not None:
+            self._f.close()
+            self._f = None
+
+
+class StepTimer:
+    """Named phases, host wall time; ``trace()`` returns chrome-trace events (µs)."""
+
+    def __init__(self, pid: int = 0, enabled: bool = True, max_events: int = 200000):
+        self.pid = pid
+        self.enabled = enabled
+        self.events: List[dict] = []
+        self.totals: Dict[str, float] = {}
+        self.counts: Dict[str, int] = {}
+        self.max_events = max_events
+
+    @contextmanager
+    def phase(self, name: str, tid: int = 0):
+        if not self.enabled:
+            yield
+            return
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            t1 = time.perf_counter()
+            self.totals[name] = self.totals.get(name, 0.0) + (t1 - t0)
+            self.counts[name] = self.counts.get(name, 0) + 1
+            if len(self.events) < self.max_events:
+                self.events.append({"name": name, "ph": "X", "pid": self.pid, "tid": tid,
+                                    "ts": t0 * 1e6, "dur": (t1 - t0) * 1e6})
+
+    def mean_ms(self, name: str) -> float:
+        n = self.counts.get(name, 0)
+        return 1e3 * self.totals.get(name, 0.0) / n if n else 0.0
+
+    def write_chrome_trace(self, path: str) -> None:
+        with open(path, "w") as f:
+            json.dump({"traceEvents": self.events, "displayTimeUnit": "ms"}, f)
+
+
+def performance_table(rows: List[dict]) -> str:
+    """rows: dicts with steps, time, accuracy (%), lr -> the reference's whitespace table."""
+    out = ["Steps ,Time ,Accuracy, Learning rate"]
+    for r in rows:
+        out.append(f"{r['steps']:<6}{r['time']:<4.0f}{r['accuracy']:<7g}{r['lr']:g}")
+    return "\n".join(out) + "\n"
