@@ -172,6 +172,11 @@ def main(argv=None) -> int:
     sopt = None
     if sync:
         r2a = FLAGS.replicas_to_aggregate if FLAGS.replicas_to_aggregate is not None else num_workers
+        if r2a > num_workers:
+            # TF1 would wait forever for gradients that never come; clamp instead (and say so)
+            print("Worker %d: replicas_to_aggregate=%d > %d workers; aggregating %d" %
+                  (FLAGS.task_index, r2a, num_workers, num_workers))
+            r2a = num_workers
         sopt = SyncReplicasOptimizer(opt, replicas_to_aggregate=r2a, total_num_replicas=num_workers).resolve(num_workers)
 
     comm = None

@@ -1,0 +1,148 @@
+"""Multi-process data parallelism on Gloo/CPU: sync DP equivalence,
+bit-identical replicas, backup workers (replicas_to_aggregate < N), async parameter server."""
+import numpy as np
+import pytest
+import torch
+
+from dist_util import run_ranks
+
+pytestmark = pytest.mark.slow
+
+
+def _data(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(n, 784, generator=g), torch.randint(0, 10, (n,), generator=g)
+
+
+def _dp_worker(rank, world, steps, B):
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+    from tensorflow_distributed_amd.models.mnist_runner import TorchMnistRunner
+    from tensorflow_distributed_amd.parallel.sync_replicas import SyncReplicasStepper, broadcast_state
+    from tensorflow_distributed_amd.training.optimizers import AdamOptimizer
+
+    r = TorchMnistRunner(B, AdamOptimizer(0.01), keep_prob=1.0, rank=rank)
+    if rank == 0:
+        r.load_flat(M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(4).items()}), {}, 0)
+    broadcast_state(r, 0)
+    st = SyncReplicasStepper(r, rank, world, world)
+    x, y = _data(B * world * steps, 11)
+    for s in range(steps):
+        lo = (s * world + rank) * B
+        st.step(x[lo:lo + B], y[lo:lo + B])
+    return r.params().clone(), r.global_step()
+
+
+def test_sync_dp_equals_big_batch_single_process():
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+    from tensorflow_distributed_amd.models.mnist_runner import TorchMnistRunner
+    from tensorflow_distributed_amd.training.optimizers import AdamOptimizer
+
+    steps, B, world = 3, 8, 2
+    outs = run_ranks(_dp_worker, world, steps, B)
+    assert torch.equal(outs[0][0], outs[1][0]), "replicas diverged"
+    assert outs[0][1] == outs[1][1] == steps
+    ref = TorchMnistRunner(B * world, AdamOptimizer(0.01), keep_prob=1.0)
+    ref.load_flat(M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(4).items()}), {}, 0)
+    x, y = _data(B * world * steps, 11)
+    for s in range(steps):
+        lo = s * world * B
+        ref.train_step(x[lo:lo + world * B], y[lo:lo + world * B])
+    # Adam amplifies summation-order differences where v ~ 0 (a handful of elements): bound them
+    torch.testing.assert_close(outs[0][0], ref.params(), rtol=1e-3, atol=1e-4)
+
+
+def _backup_worker(rank, world, r2a, slow_rank):
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+    from tensorflow_distributed_amd.models.mnist_runner import TorchMnistRunner
+    from tensorflow_distributed_amd.parallel.sync_replicas import SyncReplicasStepper, broadcast_state
+    from tensorflow_distributed_amd.training.optimizers import AdamOptimizer
+
+    B = 8
+    r = TorchMnistRunner(B, AdamOptimizer(0.01), keep_prob=1.0, rank=rank)
+    if rank == 0:
+        r.load_flat(M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(9).items()}), {}, 0)
+    broadcast_state(r, 0)
+    st = SyncReplicasStepper(r, rank, world, r2a, straggler_delay_s={slow_rank: 0.5})
+    x, y = _data(B * world, 3)
+    st.step(x[rank * B:(rank + 1) * B], y[rank * B:(rank + 1) * B])
+    return r.params().clone(), st.last_contributors
+
+
+def test_backup_workers_drop_the_straggler():
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+    from tensorflow_distributed_amd.models.mnist_runner import TorchMnistRunner
+    from tensorflow_distributed_amd.training.optimizers import AdamOptimizer
+
+    world, r2a, slow = 3, 2, 1
+    outs = run_ranks(_backup_worker, world, r2a, slow)
+    for p, contrib in outs:
+        assert contrib == [0, 2]
+        assert torch.equal(p, outs[0][0])
+    # reference: average of the two fast workers' gradients, one Adam step
+    B = 8
+    x, y = _data(B * world, 3)
+    grads = []
+    for rk in (0, 2):
+        r = TorchMnistRunner(B, AdamOptimizer(0.01), keep_prob=1.0)
+        r.load_flat(M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(9).items()}), {}, 0)
+        g, _ = r.compute_grads(x[rk * B:(rk + 1) * B], y[rk * B:(rk + 1) * B])
+        grads.append(g.clone())
+    r.apply_grads((grads[0] + grads[1]), 0.5)
+    torch.testing.assert_close(outs[0][0], r.params(), rtol=1e-4, atol=1e-6)
+
+
+def _async_role(rank, world, steps, num_ps):
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+    from tensorflow_distributed_amd.models.mnist_runner import TorchMnistRunner
+    from tensorflow_distributed_amd.parallel import async_ps
+    from tensorflow_distributed_amd.training.optimizers import AdamOptimizer
+
+    layout = async_ps.mnist_layout(num_ps)
+    nw = world - num_ps
+    if rank < num_ps:
+        svc = async_ps.ParameterServerService(rank, num_ps, nw, layout, AdamOptimizer(0.01))
+        svc.serve()
+        return ("ps", svc.updates, svc.global_step)
+    wk = rank - num_ps
+    r = TorchMnistRunner(8, AdamOptimizer(0.01), keep_prob=1.0, rank=wk)
+    client = async_ps.AsyncPSClient(wk, layout)
+    flat = torch.zeros(M.TOTAL)
+    if wk == 0:
+        client.init(M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(5).items()}))
+    client.pull(flat)
+    r.set_params(flat)
+    x, y = _data(8 * steps, 20 + wk)
+    gsteps = []
+    for s in range(steps):
+        g, _ = r.compute_grads(x[s * 8:(s + 1) * 8], y[s * 8:(s + 1) * 8])
+        gs = client.push_pull(flat, g.clone())
+        r.set_params(flat)
+        gsteps.append(gs)
+    client.stop()
+    return ("worker", gsteps, flat.clone())
+
+
+@pytest.mark.parametrize("num_ps", [1, 2])
+def test_async_parameter_server(num_ps):
+    steps, nw = 3, 2
+    outs = run_ranks(_async_role, num_ps + nw, steps, num_ps)
+    ps = [o for o in outs if o[0] == "ps"]
+    wk = [o for o in outs if o[0] == "worker"]
+    assert all(o[1] == steps * nw for o in ps), "every PS shard applies every worker's update"
+    assert ps[0][2] == steps * nw, "global_step counts every worker step (async)"
+    allsteps = sorted(s for o in wk for s in o[1])
+    assert allsteps == list(range(1, steps * nw + 1))
+
+
+def test_round_robin_placement():
+    from tensorflow_distributed_amd.parallel import async_ps
+    from tensorflow_distributed_amd.parallel.cluster import ClusterSpec, replica_device_setter
+
+    c = ClusterSpec({"ps": ["h:1", "h:2"], "worker": ["h:3"]})
+    names = ["global_step", "Variable", "Variable_1", "Variable_2"]
+    pl = replica_device_setter(c, names)
+    assert pl == {"global_step": "/job:ps/task:0/cpu:0", "Variable": "/job:ps/task:1/cpu:0",
+                  "Variable_1": "/job:ps/task:0/cpu:0", "Variable_2": "/job:ps/task:1/cpu:0"}
+    lay = async_ps.mnist_layout(2)
+    assert [n for n, _, _ in lay.ranges[1]] == ["Variable", "Variable_2", "Variable_4", "Variable_6"]
+    assert c.rank("ps", 1) == 1 and c.rank("worker", 0) == 2 and c.world_size == 3

@@ -1,0 +1,97 @@
+"""End-to-end launcher / script smoke tests on CPU: the three reference
+roles on localhost, sync and async modes, fault injection + restart + resume, mnist_single.py,
+--download_only and --existing_servers."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from tensorflow_distributed_amd import launch
+from tensorflow_distributed_amd.training.checkpoint import latest_checkpoint
+
+pytestmark = pytest.mark.slow
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COMMON = ["--synthetic_data", "--eval_batches=1", "--data_dir=/nonexistent"]
+
+
+def _out(r, name):
+    return "".join(v for k, v in r["outputs"].items() if k.startswith(name + "#"))
+
+
+def test_sync_cluster_reference_lines(tmp_path):
+    r = launch.launch(1, 2, ["--train_steps=3", f"--logdir={tmp_path}"] + COMMON, echo=False, timeout_s=300)
+    assert r["ok"], r["outputs"]
+    w0, w1, ps = _out(r, "worker:0"), _out(r, "worker:1"), _out(r, "ps:0")
+    assert "job name = ps" in ps and "task index = 0" in ps
+    assert "Worker 0: Initializing session..." in w0 and "Worker 1: Waiting for session to be initialized..." in w1
+    for w, i in ((w0, 0), (w1, 1)):
+        assert f"Worker {i}: Session initialization complete." in w
+        assert "Training begins @" in w and "Training elapsed time:" in w and "Mean Accuracy :" in w
+        assert f"Worker {i}: training step 3 done (global step: 3)" in w
+    assert latest_checkpoint(str(tmp_path)).endswith("model.ckpt-3")
+    assert any(f.startswith("events.out.tfevents.") for f in os.listdir(tmp_path))
+
+
+def test_async_cluster_two_ps(tmp_path):
+    r = launch.launch(2, 2, ["--train_steps=4", "--sync_replicas=False", f"--logdir={tmp_path}"] + COMMON,
+                      echo=False, timeout_s=300)
+    assert r["ok"], r["outputs"]
+    out = _out(r, "worker:0") + _out(r, "worker:1")
+    assert out.count("training step") >= 4  # global step advances once per worker step
+
+
+def test_fault_injection_restart_resumes(tmp_path):
+    args = ["--train_steps=6", f"--logdir={tmp_path}", "--save_model_secs=0.3", "--fault_inject_step=4",
+            "--fault_inject_task=1"] + COMMON
+    r = launch.launch(1, 2, args, max_restarts=1, echo=False, timeout_s=300)
+    assert r["ok"] and r["attempts"] == 2, r["outputs"]
+    first = r["outputs"]["worker:1#0"]
+    assert "fault injection at global step 4" in first
+    second = r["outputs"]["worker:0#1"]
+    assert "Restored from checkpoint" in second
+    assert latest_checkpoint(str(tmp_path)).endswith("model.ckpt-6")
+
+
+def test_fault_without_restart_fails(tmp_path):
+    args = ["--train_steps=5", f"--logdir={tmp_path}", "--fault_inject_step=2", "--fault_inject_task=0"] + COMMON
+    r = launch.launch(1, 2, args, max_restarts=0, echo=False, timeout_s=300)
+    assert not r["ok"] and r["failed"] == "worker:0"
+
+
+def test_mnist_single_cpu(tmp_path):
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "mnist_single.py"), "--cpu", "--training_iters=1400",
+                        "--eval_batches=5", f"--data_dir={tmp_path}/none"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    assert "Iter 1280, Minibatch Loss= " in p.stdout and "Optimization Finished!" in p.stdout
+    assert "Mean Accuracy :" in p.stdout and "seconds Time for Inference ---" in p.stdout
+
+
+def test_download_only(tmp_path):
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "mnist_python_w1.py"), "--download_only",
+                        f"--data_dir={tmp_path}"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    assert sorted(os.listdir(tmp_path)) == sorted(f + ".gz" for f in (
+        "train-images-idx3-ubyte", "train-labels-idx1-ubyte", "t10k-images-idx3-ubyte", "t10k-labels-idx1-ubyte"))
+
+
+def test_existing_servers_mode(tmp_path):
+    port = launch.free_port()
+    addr = f"127.0.0.1:{port}"
+    srv = subprocess.Popen([sys.executable, "-m", "tensorflow_distributed_amd.server", "--address", addr,
+                            "--num_workers", "1"], cwd=ROOT, stdout=subprocess.PIPE, text=True)
+    try:
+        base = [sys.executable, os.path.join(ROOT, "mnist_python_w1.py"), f"--ps_hosts={addr}",
+                f"--worker_hosts=127.0.0.1:{launch.free_port()}", "--existing_servers=True", "--train_steps=2",
+                f"--logdir={tmp_path}"] + COMMON
+        ps = subprocess.Popen(base[:1] + [os.path.join(ROOT, "mnist_python_m.py")] + base[2:], cwd=ROOT,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        w = subprocess.run(base, cwd=ROOT, capture_output=True, text=True, timeout=300)
+        assert w.returncode == 0, w.stdout + w.stderr
+        assert "Using existing server at: grpc://" in w.stdout
+        assert ps.wait(60) == 0
+        assert srv.wait(60) == 0
+    finally:
+        for p in (srv,):
+            if p.poll() is None:
+                p.kill()

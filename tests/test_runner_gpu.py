@@ -1,0 +1,128 @@
+"""GPU runner / framework paths on one MI355X: native runner vs CPU runner, checkpoint state,
+backup-worker primitives, RCCL communicator (world 1), launcher with a GPU worker."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from tensorflow_distributed_amd.models import mnist_cnn as M
+from tensorflow_distributed_amd.models.mnist_runner import NativeMnistRunner, TorchMnistRunner
+from tensorflow_distributed_amd.training.optimizers import AdamOptimizer, MomentumOptimizer
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _params(scale=0.05, seed=2):
+    return M.flat_from_dict({k: v * scale for k, v in M.init_params(seed).items()})
+
+
+def test_native_runner_tracks_cpu_runner(cuda):
+    B = 64
+    g = torch.Generator().manual_seed(0)
+    xs = torch.rand(4, B, 784, generator=g)
+    ys = torch.randint(0, 10, (4, B), generator=g)
+    nat = NativeMnistRunner(B, AdamOptimizer(0.01), keep_prob=1.0, device=cuda)
+    cpu = TorchMnistRunner(B, AdamOptimizer(0.01), keep_prob=1.0)
+    for r in (nat, cpu):
+        r.load_flat(_params(), {}, 0)
+    for i in range(4):
+        nat.train_step(xs[i], ys[i])
+        cpu.train_step(xs[i], ys[i])
+    assert nat.global_step() == 4
+    # bf16 MFMA operands vs fp32 oracle: compare the update direction, not bits
+    d_nat = nat.params().cpu() - _params()
+    d_cpu = cpu.params() - _params()
+    cos = torch.nn.functional.cosine_similarity(d_nat, d_cpu, dim=0).item()
+    assert cos > 0.95, cos
+    l_nat, c_nat = nat.evaluate(xs[0], ys[0])
+    l_cpu, c_cpu = cpu.evaluate(xs[0], ys[0])
+    assert abs(l_nat - l_cpu) / l_cpu < 0.05 and abs(c_nat - c_cpu) <= 3
+
+
+def test_native_runner_eager_equals_graph(cuda):
+    B = 32
+    x, y = torch.rand(B, 784), torch.randint(0, 10, (B,))
+    rs = [NativeMnistRunner(B, AdamOptimizer(0.01), keep_prob=0.75, device=cuda, use_graph=ug) for ug in (False, True)]
+    for r in rs:
+        r.load_flat(_params(1.0), {}, 0)
+        for _ in range(3):
+            r.train_step(x, y)
+    assert torch.equal(rs[0].params(), rs[1].params())
+
+
+def test_native_checkpoint_roundtrip_and_momentum(cuda, tmp_path):
+    from tensorflow_distributed_amd.training.checkpoint import load_bundle, save_bundle
+
+    B = 32
+    x, y = torch.rand(B, 784), torch.randint(0, 10, (B,))
+    r = NativeMnistRunner(B, AdamOptimizer(0.01), keep_prob=1.0, device=cuda)
+    r.load_flat(_params(), {}, 0)
+    r.train_step(x, y)
+    sd = r.state_dict_tf()
+    assert int(sd["global_step"]) == 1 and np.abs(sd["Variable_2/Adam"]).sum() > 0
+    save_bundle(str(tmp_path / "c"), sd)
+    r2 = NativeMnistRunner(B, AdamOptimizer(0.01), keep_prob=1.0, device=cuda)
+    r2.load_state_dict_tf(load_bundle(str(tmp_path / "c")))
+    r.train_step(x, y)
+    r2.train_step(x, y)
+    assert torch.equal(r.params(), r2.params())
+    m = NativeMnistRunner(B, MomentumOptimizer(0.01, 0.9), keep_prob=1.0, device=cuda)
+    m.load_flat(_params(), {}, 0)
+    p0 = m.params().clone()
+    m.train_step(x, y)
+    assert not torch.equal(p0, m.params())
+
+
+def test_backup_worker_primitives_world1(cuda):
+    """compute_grads -> reduce_grads(w) -> apply_grads(1/R) on one GPU equals w-scaled Adam input."""
+    B = 32
+    x, y = torch.rand(B, 784), torch.randint(0, 10, (B,))
+    a = NativeMnistRunner(B, AdamOptimizer(0.01), keep_prob=1.0, device=cuda, use_graph=False)
+    b = NativeMnistRunner(B, AdamOptimizer(0.01), keep_prob=1.0, device=cuda, use_graph=False)
+    for r in (a, b):
+        r.load_flat(_params(), {}, 0)
+    a.train_step(x, y)
+    g, _ = b.compute_grads(x, y)
+    b.reduce_grads(2.0)
+    b.apply_grads(None, 0.5)
+    torch.testing.assert_close(a.params(), b.params(), rtol=1e-5, atol=1e-6)
+    assert a.global_step() == b.global_step() == 1
+
+
+def test_rccl_comm_world1(cuda):
+    from tensorflow_distributed_amd import _native
+
+    _native.require()
+    uid = torch.classes.tfd.RcclComm.unique_id()
+    comm = torch.classes.tfd.RcclComm(uid, 1, 0, cuda.index)
+    t = torch.arange(1000, dtype=torch.float32, device=cuda)
+    comm.all_reduce(t, "sum")
+    comm.broadcast(t, 0)
+    out = torch.empty_like(t)
+    comm.all_gather(t, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, torch.arange(1000, dtype=torch.float32, device=cuda))
+    assert comm.world() == 1 and comm.rank() == 0
+
+
+def test_gpu_worker_cluster(cuda, tmp_path):
+    from tensorflow_distributed_amd import launch
+
+    args = ["--num_gpus=1", "--train_steps=5", f"--logdir={tmp_path}", "--synthetic_data", "--eval_batches=1",
+            "--data_dir=/nonexistent"]
+    r = launch.launch(1, 1, args, echo=False, timeout_s=300)
+    assert r["ok"], r["outputs"]
+    out = "".join(v for k, v in r["outputs"].items() if k.startswith("worker:0#"))
+    assert "training step 5 done (global step: 5)" in out
+
+
+def test_mnist_single_gpu(cuda, tmp_path):
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "mnist_single.py"), f"--data_dir={tmp_path}/none"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    acc = float(p.stdout.split("Mean Accuracy : ")[1].split()[0])
+    assert "Iter 1280, Minibatch Loss= " in p.stdout and acc > 0.5, p.stdout
