@@ -21,6 +21,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+METRIC = "images/sec (whole node) MNIST CNN DP at 1/2/4/8 MI355X; step-time scaling"  # BASELINE.json
 BASELINE_IMG_PER_S = 52.1  # 120 global steps x 256 images / 590 s (performance:6)
 
 
@@ -34,7 +35,11 @@ def main(argv=None):
     ap.add_argument("--fp32_grads", action="store_true", help="all-reduce fp32 grads (default bf16)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu", action="store_true", help="plumbing dry-run: fp32 PyTorch CPU runner + Gloo "
+                    "(exercises the launcher/barrier/JSON contract without a GPU; not a performance number)")
     a = ap.parse_args(argv)
+    if a.cpu:
+        return _cpu_dry_run(a)
 
     import torch
 
@@ -94,7 +99,7 @@ def main(argv=None):
         print(f"# world={world} B/gpu={B} steps={a.steps} global_step={gstep} loss {loss0:.3f}->{loss1:.3f} "
               f"{ms:.4f} ms/step", file=sys.stderr)
         print(json.dumps({
-            "metric": "images/sec (whole node) MNIST CNN DP",
+            "metric": METRIC,
             "value": round(img_s, 1),
             "unit": "images/s",
             "n_gpus": world,
@@ -107,7 +112,8 @@ def main(argv=None):
             "dtype": "bf16",
             "data": "synthetic (device-resident MNIST-shaped 55000x784, random labels; random N(0,1) init)",
             "config": {
-                "model": "mnist_cnn (conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout0.75-fc10, Adam lr 0.01)",
+                "model": "MNIST 2-conv CNN (reference conv_net: conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout0.75-fc10), "
+                         "Adam lr 0.01",
                 "global_batch": world * B,
                 "per_gpu_batch": B,
                 "seq_len": None,
@@ -116,6 +122,45 @@ def main(argv=None):
                 "hipgraph": not a.eager,
             },
         }), flush=True)
+    ctx.shutdown()
+    return 0
+
+
+def _cpu_dry_run(a):
+    import torch
+
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+    from tensorflow_distributed_amd.models.mnist_runner import TorchMnistRunner
+    from tensorflow_distributed_amd.parallel import dist as D
+    from tensorflow_distributed_amd.parallel.sync_replicas import SyncReplicasStepper, broadcast_state
+    from tensorflow_distributed_amd.training.optimizers import AdamOptimizer
+
+    ctx = D.init_from_env(use_gpu=False)
+    world, rank = ctx.world, ctx.rank
+    r = TorchMnistRunner(a.batch_size, AdamOptimizer(a.lr), keep_prob=0.75, seed=a.seed, rank=rank)
+    if rank == 0:
+        r.load_flat(M.flat_from_dict(M.init_params(a.seed)), {}, 0)
+    if world > 1:
+        broadcast_state(r, 0)
+    st = SyncReplicasStepper(r, rank, world, world)
+    g = torch.Generator().manual_seed(1000 + rank)
+    x = torch.rand(a.batch_size, 784, generator=g)
+    y = torch.randint(0, 10, (a.batch_size,), generator=g)
+    for _ in range(a.warmup):
+        st.step(x, y)
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        st.step(x, y)
+    ctx.barrier()
+    dt = ctx.max_scalar(time.perf_counter() - t0)
+    if rank == 0:
+        print(json.dumps({"metric": "images/sec (whole node) MNIST CNN DP [CPU dry-run]", "value": world * a.batch_size * a.steps / dt,
+                          "unit": "images/s", "n_gpus": 0, "n_ranks": world, "steps": a.steps, "warmup": a.warmup,
+                          "ms_per_step": dt * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+                          "config": {"model": "mnist_cnn", "global_batch": world * a.batch_size, "seq_len": None,
+                                     "parallelism": f"dp{world}", "device": "cpu"}}), flush=True)
     ctx.shutdown()
     return 0
 

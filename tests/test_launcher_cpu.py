@@ -95,3 +95,19 @@ def test_existing_servers_mode(tmp_path):
         for p in (srv,):
             if p.poll() is None:
                 p.kill()
+
+
+def test_bench_torchrun_cpu_dry_run():
+    """bench.py's multi-rank contract (torchrun env, barrier, max over ranks, one JSON line on rank 0)."""
+    import json
+
+    port = launch.free_port()
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu", "--batch_size", "16"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["n_ranks"] == 2 and rec["config"]["global_batch"] == 32 and rec["value"] > 0
