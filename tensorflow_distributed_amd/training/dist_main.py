@@ -85,6 +85,14 @@ def define_flags(task_index_default: int = 0, job_name_default: str = "ps") -> N
                     "(backup-worker tests)")
     f.DEFINE_float("rendezvous_timeout", 600.0, "Seconds to wait for the cluster to assemble")
     f.DEFINE_boolean("quiet", False, "Suppress per-step prints")
+    f.DEFINE_boolean("debug_sync", False, "Serialise every HIP launch/copy (AMD_SERIALIZE_KERNEL=3, "
+                     "HIP_LAUNCH_BLOCKING=1): race-hunting mode")
+    f.DEFINE_float("step_timeout_secs", 0.0, "Watchdog: abort the communicator and exit non-zero when no step "
+                   "completes for this long (0 = off); the launcher then restarts from the last checkpoint")
+    f.DEFINE_string("eval_at_steps", "", "Chief: comma-separated global steps at which to run the validation "
+                    "pass and print a 'performance' table row (steps, training seconds, accuracy %, lr)")
+    f.DEFINE_boolean("log_device_placement", False, "Print where every variable and the compute live "
+                     "(ConfigProto.log_device_placement, mnist_python_m.py:257)")
 
 
 def _make_optimizer():
@@ -127,6 +135,10 @@ def main(argv=None) -> int:
         # no network on MI355X boxes: materialise the IDX files (synthetic if absent) and stop
         print("MNIST data in %s: %s" % (FLAGS.data_dir, input_data.maybe_download(FLAGS.data_dir)))
         sys.exit(0)
+    if FLAGS.debug_sync:
+        from ..utils.tracing import enable_debug_sync
+
+        enable_debug_sync()
     mnist = input_data.read_data_sets(FLAGS.data_dir, one_hot=True, fake_data=FLAGS.synthetic_data,
                                       seed=FLAGS.seed * 1000 + max(FLAGS.task_index, 0) + 17)
 
@@ -222,6 +234,22 @@ def main(argv=None) -> int:
     sv.prepare_or_wait_for_session()
     print("Worker %d: Session initialization complete." % FLAGS.task_index)
 
+    if FLAGS.log_device_placement:
+        from ..parallel.cluster import replica_device_setter
+
+        names = ["global_step"] + [tf for _, tf, _ in M.PARAM_SPECS]
+        wdev = "/job:worker/task:%d/%s:%d" % (FLAGS.task_index, "gpu" if device.type == "cuda" else "cpu",
+                                              device.index or 0)
+        placed = replica_device_setter(cluster, names, wdev) if not sync else {n: wdev + " (replicated)" for n in names}
+        for n in names:
+            print("%s: %s" % (n, placed[n]))
+        print("compute (conv_net, loss, gradients): %s; gradient sync: %s" % (
+            wdev, ("RCCL all-reduce" if comm is not None else "Gloo all-reduce") if sync else "async PS push/pull"))
+
+    eval_at = sorted(int(v) for v in FLAGS.eval_at_steps.split(",") if v.strip()) if FLAGS.eval_at_steps else []
+    eval_time = 0.0
+    perf_rows = []
+
     delays = {}
     if FLAGS.straggler_delay:
         for item in FLAGS.straggler_delay.split(","):
@@ -235,6 +263,9 @@ def main(argv=None) -> int:
     timer = StepTimer(pid=FLAGS.task_index, enabled=bool(FLAGS.trace_file))
     restart_attempt = int(os.environ.get("TFD_RESTART_COUNT", "0"))
 
+    from ..utils.tracing import Watchdog, trace_range
+
+    watchdog = Watchdog(FLAGS.step_timeout_secs, on_timeout=(comm.abort if comm is not None else None))
     time_begin = time.time()
     print("Training begins @ %f" % time_begin)
     local_step = 0
@@ -246,7 +277,7 @@ def main(argv=None) -> int:
         with timer.phase("input"):
             batch_xs, batch_ys = mnist.train.next_batch(FLAGS.batch_size)
         t0 = time.time()
-        with timer.phase("step"):
+        with timer.phase("step"), trace_range("train_step"):
             if sync:
                 stepper.step(batch_xs, batch_ys)
                 step = runner.global_step()
@@ -260,6 +291,7 @@ def main(argv=None) -> int:
                 runner.set_params(flat)
                 runner.set_global_step(step)
         local_step += 1
+        watchdog.kick()
         now = time.time()
         if not FLAGS.quiet:
             print("%f: Worker %d: training step %d done (global step: %d)" % (now, FLAGS.task_index, local_step, step))
@@ -268,14 +300,28 @@ def main(argv=None) -> int:
         if FLAGS.check_consistency_every and sync and local_step % FLAGS.check_consistency_every == 0:
             _check_consistency(runner, server, num_workers)
         sv.on_step(step)
+        while is_chief and eval_at and step >= eval_at[0]:
+            te = time.time()
+            accs = []
+            for _ in range(FLAGS.eval_batches):
+                vx, vy = mnist.validation.next_batch(FLAGS.eval_batch_size)
+                accs.append(runner.evaluate(vx, vy)[1] / float(len(vx)))
+            acc = 100.0 * sum(accs) / len(accs)
+            eval_time += time.time() - te
+            row = dict(steps=eval_at.pop(0), time=time.time() - time_begin - eval_time, accuracy=round(acc, 2),
+                       lr=FLAGS.learning_rate)
+            perf_rows.append(row)
+            print("Performance row: %d %.1f %.2f %g" % (row["steps"], row["time"], row["accuracy"], row["lr"]))
+            metrics.log(event="performance", **row)
         if (FLAGS.fault_inject_step >= 0 and FLAGS.task_index == FLAGS.fault_inject_task and restart_attempt == 0
                 and step >= FLAGS.fault_inject_step):
             print("Worker %d: fault injection at global step %d" % (FLAGS.task_index, step), flush=True)
             os._exit(17)
 
+    watchdog.stop()
     time_end = time.time()
     print("Training ends @ %f" % time_end)
-    training_time = time_end - time_begin
+    training_time = time_end - time_begin - eval_time
     print("Training elapsed time: %f s" % training_time)
 
     accuracy_arr = []
@@ -292,6 +338,10 @@ def main(argv=None) -> int:
     sys.stdout.flush()
 
     metrics.log(event="final", global_step=step, training_time_s=training_time, mean_accuracy=mean_accuracy)
+    if perf_rows:
+        from ..utils.metrics import performance_table
+
+        print(performance_table(perf_rows), end="")
     metrics.close()
     if FLAGS.trace_file:
         timer.write_chrome_trace(FLAGS.trace_file.replace("{task}", str(FLAGS.task_index)))

@@ -111,3 +111,29 @@ def test_bench_torchrun_cpu_dry_run():
     assert len(lines) == 1
     rec = json.loads(lines[0])
     assert rec["n_ranks"] == 2 and rec["config"]["global_batch"] == 32 and rec["value"] > 0
+
+
+def test_performance_table_tool(tmp_path):
+    out = tmp_path / "performance"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "performance.py"), "--steps", "2,4",
+                        "--out", str(out), "--", "--synthetic_data", "--eval_batches=1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stdout + p.stderr
+    lines = out.read_text().splitlines()
+    assert lines[0] == "Steps ,Time ,Accuracy, Learning rate" and lines[1].split()[0] == "2" and len(lines) == 3
+
+
+def test_watchdog_exits_nonzero():
+    code = ("import time,sys; sys.path.insert(0, %r)\n"
+            "from tensorflow_distributed_amd.utils.tracing import Watchdog\n"
+            "w = Watchdog(0.5)\ntime.sleep(5)\n" % ROOT)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 3 and "watchdog" in p.stderr
+
+
+def test_log_device_placement_round_robin():
+    r = launch.launch(2, 1, ["--train_steps=1", "--sync_replicas=False", "--log_device_placement"] + COMMON,
+                      echo=False, timeout_s=300)
+    assert r["ok"]
+    w = _out(r, "worker:0")
+    assert "global_step: /job:ps/task:0/cpu:0" in w and "Variable: /job:ps/task:1/cpu:0" in w
