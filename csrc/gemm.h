@@ -72,7 +72,10 @@ struct GemmSmem {
 // One workgroup computes the BM x BN tile at (m0, n0) over k in [kbeg, kend).
 // WM x WN waves (64*WM*WN threads). kend - kbeg should be a multiple of BK except at the global
 // K tail (loaders zero-fill past K).
-template <int BM, int BN, int BK, int WM, int WN, class LA, class LB, class EPI>
+// RS = register stages: with RS = 2 the global loads of tile t+2 are issued while tile t+1 still
+// sits in registers, so every load has ~2 K-iterations of latency cover (twice the bytes in flight
+// per CU -- these small GEMMs are bound by bytes-in-flight / memory latency, not by MFMA rate).
+template <int BM, int BN, int BK, int WM, int WN, class LA, class LB, class EPI, int RS = 1>
 __device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI& epi, int m0, int n0,
                                            int kbeg, int kend, bf16* smem) {
   constexpr int NT = 64 * WM * WN;
@@ -80,6 +83,7 @@ __device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI
   using TB = LdsTile<BN, BK, LB::KC>;
   static_assert(BK % 32 == 0, "BK multiple of 32");
   static_assert(BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "tile/wave mismatch");
+  static_assert(RS == 1 || RS == 2, "register stages");
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
   constexpr int CA = (TA::CHUNKS + NT - 1) / NT;
   constexpr int CB = (TB::CHUNKS + NT - 1) / NT;
@@ -89,21 +93,21 @@ __device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI
   bf16* Bs1 = Bs0 + TB::ELEMS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  uint4 ra[CA], rb[CB];
+  uint4 ra[RS][CA], rb[RS][CB];
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto gload = [&](int k0) {
+  auto gload = [&](int k0, uint4 (&xa)[CA], uint4 (&xb)[CB]) {
 #pragma unroll
     for (int c = 0; c < CA; ++c) {
       const int idx = tid + c * NT;
       if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
         const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 8;
-        if constexpr (LA::KC) ra[c] = la(m0 + row, k0 + col);
-        else ra[c] = la(m0 + col, k0 + row);
+        if constexpr (LA::KC) xa[c] = la(m0 + row, k0 + col);
+        else xa[c] = la(m0 + col, k0 + row);
       }
     }
 #pragma unroll
@@ -111,18 +115,18 @@ __device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI
       const int idx = tid + c * NT;
       if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
         const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 8;
-        if constexpr (LB::KC) rb[c] = lb(n0 + row, k0 + col);
-        else rb[c] = lb(n0 + col, k0 + row);
+        if constexpr (LB::KC) xb[c] = lb(n0 + row, k0 + col);
+        else xb[c] = lb(n0 + col, k0 + row);
       }
     }
   };
-  auto sstore = [&](bf16* As, bf16* Bs) {
+  auto sstore = [&](bf16* As, bf16* Bs, const uint4 (&xa)[CA], const uint4 (&xb)[CB]) {
 #pragma unroll
     for (int c = 0; c < CA; ++c) {
       const int idx = tid + c * NT;
       if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
         const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 8;
-        *reinterpret_cast<uint4*>(As + row * TA::ROW + col) = ra[c];
+        *reinterpret_cast<uint4*>(As + row * TA::ROW + col) = xa[c];
       }
     }
 #pragma unroll
@@ -130,35 +134,59 @@ __device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI
       const int idx = tid + c * NT;
       if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
         const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 8;
-        *reinterpret_cast<uint4*>(Bs + row * TB::ROW + col) = rb[c];
+        *reinterpret_cast<uint4*>(Bs + row * TB::ROW + col) = xb[c];
       }
+    }
+  };
+  auto compute = [&](const bf16* As, const bf16* Bs) {
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = read_frag<BM, BK, LA::KC>(As, wm * WTM + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = read_frag<BN, BK, LB::KC>(Bs, wn * WTN + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
     }
   };
 
   const int nk = (kend - kbeg + BK - 1) / BK;
-  if (nk > 0) {
-    gload(kbeg);
-    sstore(As0, Bs0);
-    __syncthreads();
-    for (int t = 0; t < nk; ++t) {
-      const bool odd = t & 1;
-      const bf16* As = odd ? As1 : As0;
-      const bf16* Bs = odd ? Bs1 : Bs0;
-      if (t + 1 < nk) gload(kbeg + (t + 1) * BK);
-#pragma unroll
-      for (int kk = 0; kk < BK; kk += 32) {
-        bf16x8 a[TM], b[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = read_frag<BM, BK, LA::KC>(As, wm * WTM + 16 * i, kk, lane);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = read_frag<BN, BK, LB::KC>(Bs, wn * WTN + 16 * j, kk, lane);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
-      }
-      if (t + 1 < nk) sstore(odd ? As0 : As1, odd ? Bs0 : Bs1);
+  if constexpr (RS == 1) {
+    if (nk > 0) {
+      gload(kbeg, ra[0], rb[0]);
+      sstore(As0, Bs0, ra[0], rb[0]);
       __syncthreads();
+      for (int t = 0; t < nk; ++t) {
+        const bool odd = t & 1;
+        if (t + 1 < nk) gload(kbeg + (t + 1) * BK, ra[0], rb[0]);
+        compute(odd ? As1 : As0, odd ? Bs1 : Bs0);
+        if (t + 1 < nk) sstore(odd ? As0 : As1, odd ? Bs0 : Bs1, ra[0], rb[0]);
+        __syncthreads();
+      }
+    }
+  } else {
+    // LDS[t&1] holds tile t; register set (t+1)&1 holds tile t+1; tile t+2 loads into set t&1.
+    if (nk > 0) {
+      gload(kbeg, ra[0], rb[0]);
+      if (nk > 1) gload(kbeg + BK, ra[1], rb[1]);
+      sstore(As0, Bs0, ra[0], rb[0]);
+      __syncthreads();
+      for (int t = 0; t < nk; t += 2) {
+        // even step: compute LDS0 (tile t), regs1 = tile t+1, refill regs0 with tile t+2
+        if (t + 2 < nk) gload(kbeg + (t + 2) * BK, ra[0], rb[0]);
+        compute(As0, Bs0);
+        if (t + 1 < nk) sstore(As1, Bs1, ra[1], rb[1]);
+        __syncthreads();
+        if (t + 1 >= nk) break;
+        // odd step: compute LDS1 (tile t+1), regs0 = tile t+2, refill regs1 with tile t+3
+        if (t + 3 < nk) gload(kbeg + (t + 3) * BK, ra[1], rb[1]);
+        compute(As1, Bs1);
+        if (t + 2 < nk) sstore(As0, Bs0, ra[0], rb[0]);
+        __syncthreads();
+      }
     }
   }
 #pragma unroll

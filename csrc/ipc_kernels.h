@@ -1,0 +1,35 @@
+// Host-side API of the one-shot peer-to-peer (IPC) all-reduce (csrc/comm/ipc_allreduce.hip).
+//
+// for small gradient buckets the latency of a ring dominates, so
+// every rank's kernel reads its slice from ALL peers' staging buffers at once (on MI355X: over all
+// 7 xGMI links in parallel), reduces in fp32 registers and writes the result locally. Cross-rank
+// ordering uses per-block START/END flag barriers in uncached (fine-grained) signal memory with
+// system-scope release/acquire; every spin is time-bounded (error flag instead of a hang).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace tfd {
+
+constexpr int kIpcMaxRanks = 8;
+constexpr int kIpcMaxBlocks = 64;
+// signal region layout (int32): [2 phases][kIpcMaxBlocks][kIpcMaxRanks] flags, then
+// [kIpcMaxBlocks] per-block epochs (local), then 1 error word.
+constexpr int kIpcSigFlags = 2 * kIpcMaxBlocks * kIpcMaxRanks;
+constexpr int kIpcSigInts = kIpcSigFlags + kIpcMaxBlocks + 4;
+
+struct IpcAllReduceArgs {
+  const void* in;               // local input (fp32 or bf16)
+  void* out;                    // local output (may alias in)
+  void* stage[kIpcMaxRanks];    // fp32 staging buffer of every rank, mapped here
+  int* sig[kIpcMaxRanks];       // signal region of every rank, mapped here
+  int64_t n;                    // elements
+  int rank, world;
+  int in_bf16, out_bf16;
+  float scale;                  // applied to the reduced sum
+  int64_t spin_limit_ticks;     // s_memrealtime (100 MHz) ticks before a barrier gives up
+};
+
+void ipc_allreduce(const IpcAllReduceArgs& a, int blocks, hipStream_t s);
+
+}  // namespace tfd

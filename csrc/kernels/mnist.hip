@@ -23,6 +23,10 @@
 
 #include <algorithm>
 
+#ifndef TFD_GEMM_RS
+#define TFD_GEMM_RS 2  // register stages of the LDS-staged GEMM core (csrc/gemm.h)
+#endif
+
 #ifndef TFD_WROT
 #define TFD_WROT 1
 #endif
@@ -183,7 +187,7 @@ __global__ __launch_bounds__(256) void conv2_pool_fwd(MnistStepArgs a) {
   Conv2FwdA la{a.p1, M};
   C2F_B lb{a.pbf + OFF_WC2, 64, 64, 800};
   PoolEpi epi{a.p32 + OFF_BC2, a.p2, a.idx2, M};
-  gemm_block<C2F_BM, C2F_BN, C2F_BK, 2, 2>(la, lb, epi, blockIdx.x * C2F_BM, 0, 0, 800, (bf16*)smem_raw);
+  gemm_block<C2F_BM, C2F_BN, C2F_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, blockIdx.x * C2F_BM, 0, 0, 800, (bf16*)smem_raw);
 }
 
 // ---------------- K2 (LDS-staged): whole-image implicit GEMM ----------------
@@ -317,7 +321,7 @@ __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   const int z = blockIdx.z;
   SlabEpi epi{a.fc1_slab + (size_t)z * a.B * HID, HID, a.B, HID};
   const int kb = z * kper, ke = min(FEAT, kb + kper);
-  gemm_block<FC1_BM, FC1_BN, FC1_BK, 2, 2>(la, lb, epi, blockIdx.y * FC1_BM, blockIdx.x * FC1_BN, kb, ke,
+  gemm_block<FC1_BM, FC1_BN, FC1_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, blockIdx.y * FC1_BM, blockIdx.x * FC1_BN, kb, ke,
                                            (bf16*)smem_raw);
 }
 
@@ -467,7 +471,7 @@ __device__ __forceinline__ void fc1_dw_block(const MnistStepArgs& a, int bx, int
   OnesRowMC la{a.p2, FEAT, FEAT, a.B};
   DenseLoader<false> lb{a.dh, HID, HID, a.B};
   SlabEpi epi{a.grad + OFF_WD1, HID, FEAT + 1, HID};
-  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2>(la, lb, epi, by * FDW_BM, bx * FDW_BN, 0, a.B, smem);
+  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, by * FDW_BM, bx * FDW_BN, 0, a.B, smem);
 }
 
 // ---------------- K10 fc1 dX + K11 MaxPoolGrad + ReluGrad -> dz2 (dense, conv2 pre-act grad) --------
@@ -500,7 +504,7 @@ __device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int
   DenseLoader<true> la{a.dh, HID, a.B, HID};
   DenseLoader<true> lb{a.pbf + OFF_WD1, HID, FEAT, HID};
   UnpoolEpi epi{a.p2, a.idx2, a.dz2, a.B};
-  gemm_block<FDX_BM, FDX_BN, FDX_BK, 2, 2>(la, lb, epi, by * FDX_BM, bx * FDX_BN, 0, HID, smem);
+  gemm_block<FDX_BM, FDX_BN, FDX_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, by * FDX_BM, bx * FDX_BN, 0, HID, smem);
 }
 
 // K8 + K10: every fc-layer gradient in ONE launch (horizontal fusion of three independent
@@ -561,7 +565,7 @@ __device__ __forceinline__ void conv2_dgrad_block(const MnistStepArgs& a, int bx
   Conv2DgradA la{a.dz2, M};
   Conv2DgradB lb{a.pbf + OFF_WC2};
   MaskEpi epi{a.p1, a.dp1m, M};
-  gemm_block<C2D_BM, C2D_BN, C2D_BK, 2, 2>(la, lb, epi, bx * C2D_BM, 0, 0, 1600, smem);
+  gemm_block<C2D_BM, C2D_BN, C2D_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, bx * C2D_BM, 0, 0, 1600, smem);
 }
 
 // ---------------- K13 (LDS-staged): conv2 dgrad + conv1 relu/pool-mask epilogue ----------------
@@ -698,7 +702,7 @@ __device__ __forceinline__ void conv2_wgrad_block(const MnistStepArgs& a, int bx
   DenseLoader<false> lb{a.dz2, 64, 64, K};
   SlabEpi epi{a.wg2_slab + (size_t)z * 801 * 64, 64, 801, 64};
   const int kb = z * kper, ke = min(K, kb + kper);
-  gemm_block<C2W_BM, C2W_BN, C2W_BK, 2, 2>(la, lb, epi, bx * C2W_BM, 0, kb, ke, smem);
+  gemm_block<C2W_BM, C2W_BN, C2W_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, bx * C2W_BM, 0, kb, ke, smem);
 }
 __global__ __launch_bounds__(256) void conv2_wgrad_k(MnistStepArgs a, int kper) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];

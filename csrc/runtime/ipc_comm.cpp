@@ -1,0 +1,146 @@
+// IpcComm: peer-to-peer (IPC-mapped) communicator for latency-bound small collectives
+// (SURVEY.md §2.2 N3, §5.8 item 3). One process per GPU; each rank exports a staging buffer
+// (coarse-grained device memory) and an uncached signal region with hipIpcGetMemHandle; the
+// 2 x 64-byte handles are exchanged over the control plane (Gloo) and opened in every peer.
+// all_reduce() is one kernel (csrc/comm/ipc_allreduce.hip) and can be captured into a hipGraph.
+// Ranks may share one GPU (two processes, same device): that is how the protocol is tested on a
+// one-GPU box, where RCCL refuses duplicate devices.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/custom_class.h>
+#include <torch/library.h>
+
+#include <cstring>
+
+#include "../ipc_kernels.h"
+#include "ipc_comm.h"
+
+namespace tfd {
+
+#define HIP_OK2(x)                                                                         \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    TORCH_CHECK(e_ == hipSuccess, #x, " failed: ", hipGetErrorString(e_));                 \
+  } while (0)
+
+IpcComm::IpcComm(int64_t world, int64_t rank, int64_t device, int64_t capacity_elems)
+    : world_(world), rank_(rank), device_(device), cap_(capacity_elems) {
+  TORCH_CHECK(world >= 1 && world <= kIpcMaxRanks, "IpcComm: world must be in [1, ", kIpcMaxRanks, "]");
+  TORCH_CHECK(rank >= 0 && rank < world, "IpcComm: bad rank");
+  TORCH_CHECK(capacity_elems > 0, "IpcComm: capacity");
+  HIP_OK2(hipSetDevice((int)device));
+  HIP_OK2(hipMalloc(&stage_, (size_t)cap_ * sizeof(float)));
+  HIP_OK2(hipExtMallocWithFlags(&sig_, kIpcSigInts * sizeof(int), hipDeviceMallocUncached));
+  HIP_OK2(hipMemset(sig_, 0, kIpcSigInts * sizeof(int)));
+  HIP_OK2(hipMemset(stage_, 0, (size_t)cap_ * sizeof(float)));
+  HIP_OK2(hipDeviceSynchronize());
+  for (int i = 0; i < kIpcMaxRanks; ++i) {
+    peer_stage_[i] = nullptr;
+    peer_sig_[i] = nullptr;
+  }
+  peer_stage_[rank] = stage_;
+  peer_sig_[rank] = (int*)sig_;
+}
+
+IpcComm::~IpcComm() { close(); }
+
+at::Tensor IpcComm::handle() {
+  hipIpcMemHandle_t h[2];
+  HIP_OK2(hipIpcGetMemHandle(&h[0], stage_));
+  HIP_OK2(hipIpcGetMemHandle(&h[1], sig_));
+  auto t = at::empty({2 * (int64_t)sizeof(hipIpcMemHandle_t)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(t.data_ptr(), h, sizeof(h));
+  return t;
+}
+
+void IpcComm::open(const at::Tensor& all) {
+  TORCH_CHECK(!opened_, "IpcComm: already opened");
+  const int64_t hb = 2 * (int64_t)sizeof(hipIpcMemHandle_t);
+  TORCH_CHECK(all.numel() == world_ * hb && all.scalar_type() == at::kByte, "IpcComm.open: [world, 128] uint8");
+  auto c = all.contiguous().cpu();
+  const uint8_t* base = c.data_ptr<uint8_t>();
+  HIP_OK2(hipSetDevice((int)device_));
+  for (int p = 0; p < world_; ++p) {
+    if (p == rank_) continue;
+    hipIpcMemHandle_t h[2];
+    std::memcpy(h, base + p * hb, sizeof(h));
+    HIP_OK2(hipIpcOpenMemHandle(&peer_stage_[p], h[0], hipIpcMemLazyEnablePeerAccess));
+    HIP_OK2(hipIpcOpenMemHandle((void**)&peer_sig_[p], h[1], hipIpcMemLazyEnablePeerAccess));
+  }
+  opened_ = true;
+}
+
+void IpcComm::close() {
+  if (opened_) {
+    for (int p = 0; p < world_; ++p) {
+      if (p == rank_) continue;
+      if (peer_stage_[p]) hipIpcCloseMemHandle(peer_stage_[p]);
+      if (peer_sig_[p]) hipIpcCloseMemHandle(peer_sig_[p]);
+      peer_stage_[p] = nullptr;
+      peer_sig_[p] = nullptr;
+    }
+    opened_ = false;
+  }
+  if (stage_) {
+    hipFree(stage_);
+    stage_ = nullptr;
+  }
+  if (sig_) {
+    hipFree(sig_);
+    sig_ = nullptr;
+  }
+}
+
+void IpcComm::all_reduce_raw(const void* in, bool in_bf16, void* out, bool out_bf16, int64_t n, double scale,
+                             hipStream_t s) {
+  TORCH_CHECK(opened_ || world_ == 1, "IpcComm: open() the peer handles first");
+  TORCH_CHECK(n <= cap_, "IpcComm: ", n, " elements exceed the staging capacity ", cap_);
+  IpcAllReduceArgs a{};
+  a.in = in;
+  a.out = out;
+  for (int p = 0; p < world_; ++p) {
+    a.stage[p] = peer_stage_[p];
+    a.sig[p] = peer_sig_[p];
+  }
+  a.n = n;
+  a.rank = (int)rank_;
+  a.world = (int)world_;
+  a.in_bf16 = in_bf16 ? 1 : 0;
+  a.out_bf16 = out_bf16 ? 1 : 0;
+  a.scale = (float)scale;
+  a.spin_limit_ticks = spin_ticks_;
+  // ~8K elements per block keeps the per-rank slice reads wide; never more blocks than the
+  // signal layout holds
+  int blocks = (int)std::min<int64_t>(kIpcMaxBlocks, std::max<int64_t>(1, (n + 8191) / 8192));
+  ipc_allreduce(a, blocks, s);
+}
+
+void IpcComm::all_reduce(const at::Tensor& t, double scale) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "IpcComm.all_reduce: contiguous GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, "IpcComm: fp32/bf16 only");
+  const bool bf = t.scalar_type() == at::kBFloat16;
+  all_reduce_raw(t.data_ptr(), bf, t.data_ptr(), bf, t.numel(), scale, c10::hip::getCurrentHIPStream().stream());
+}
+
+int64_t IpcComm::error() {
+  int v = 0;
+  HIP_OK2(hipMemcpy(&v, (int*)sig_ + kIpcSigFlags + kIpcMaxBlocks, sizeof(int), hipMemcpyDeviceToHost));
+  return v;
+}
+
+void IpcComm::set_spin_limit_ms(double ms) { spin_ticks_ = (int64_t)(ms * 1e5); }  // 100 MHz clock
+
+TORCH_LIBRARY_FRAGMENT(tfd, m) {
+  m.class_<IpcComm>("IpcComm")
+      .def(torch::init<int64_t, int64_t, int64_t, int64_t>())
+      .def("handle", &IpcComm::handle)
+      .def("open", &IpcComm::open)
+      .def("close", &IpcComm::close)
+      .def("all_reduce", &IpcComm::all_reduce)
+      .def("error", &IpcComm::error)
+      .def("set_spin_limit_ms", &IpcComm::set_spin_limit_ms)
+      .def("world", &IpcComm::world)
+      .def("rank", &IpcComm::rank);
+}
+
+}  // namespace tfd

@@ -1,0 +1,36 @@
+// IpcComm class declaration (see ipc_comm.cpp).
+#pragma once
+#include <ATen/ATen.h>
+#include <hip/hip_runtime_api.h>
+#include <torch/custom_class.h>
+
+namespace tfd {
+
+class IpcComm : public torch::CustomClassHolder {
+ public:
+  IpcComm(int64_t world, int64_t rank, int64_t device, int64_t capacity_elems);
+  ~IpcComm() override;
+  at::Tensor handle();                       // this rank's [128] uint8 export (staging + signals)
+  void open(const at::Tensor& all_handles);  // [world, 128]: open every peer's export
+  void close();
+  void all_reduce(const at::Tensor& t, double scale);  // in place, current HIP stream
+  // in: fp32/bf16 -> fp32 staging -> reduced sum * scale -> out (fp32/bf16); n <= capacity
+  void all_reduce_raw(const void* in, bool in_bf16, void* out, bool out_bf16, int64_t n, double scale,
+                      hipStream_t s);
+  int64_t error();                           // 1 once a barrier timed out (sticky)
+  void set_spin_limit_ms(double ms);
+  int64_t world() const { return world_; }
+  int64_t rank() const { return rank_; }
+  int64_t capacity() const { return cap_; }
+
+ private:
+  int64_t world_, rank_, device_, cap_;
+  void* stage_ = nullptr;
+  void* sig_ = nullptr;
+  void* peer_stage_[8];
+  int* peer_sig_[8];
+  bool opened_ = false;
+  int64_t spin_ticks_ = 200000000;  // 2 s at 100 MHz
+};
+
+}  // namespace tfd

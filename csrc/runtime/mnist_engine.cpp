@@ -17,6 +17,7 @@
 #include "../mnist_layout.h"
 #include "../tfd_kernels.h"
 #include "comm.h"
+#include "ipc_comm.h"
 
 namespace tfd {
 using namespace mnist;
@@ -127,6 +128,18 @@ class MnistEngine : public torch::CustomClassHolder {
     comm_ = comm;
     bf16_comm_ = bf16_grads;
   }
+  // Peer-to-peer IPC all-reduce for latency-bound buckets (<= small_max elements, e.g. the conv
+  // bucket B); without an RCCL communicator it carries every bucket (one-GPU multi-process tests).
+  void set_ipc(c10::intrusive_ptr<IpcComm> ipc, int64_t small_max, bool bf16_grads) {
+    ipc_ = ipc;
+    ipc_small_ = small_max;
+    if (!comm_) bf16_comm_ = bf16_grads;
+  }
+  int64_t world() const {
+    if (comm_) return comm_->world();
+    if (ipc_) return ipc_->world();
+    return 1;
+  }
 
   // ---- step pieces (current HIP stream) ----
   void forward(bool train) { mnist_forward(args(), train, stream()); }
@@ -139,7 +152,7 @@ class MnistEngine : public torch::CustomClassHolder {
     mnist_backward_b(a, stream(), aux_stream_, ev_fork_, ev_join_);
   }
   void apply_optimizer(double grad_scale) {
-    const uint16_t* gbf = (comm_ && bf16_comm_ && comm_->world() > 1) ? (const uint16_t*)gbf_.data_ptr() : nullptr;
+    const uint16_t* gbf = (bf16_comm_ && world() > 1) ? (const uint16_t*)gbf_.data_ptr() : nullptr;
     if (opt_ == 0) {
       AdamArgs a{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(), (const float*)grad_.data_ptr(),
                  (uint16_t*)pbf_.data_ptr(), gbf, TOTAL, (float)lr_, (float)b1_, (float)b2_, (float)eps_,
@@ -161,7 +174,7 @@ class MnistEngine : public torch::CustomClassHolder {
     hipStream_t s = stream();
     forward(true);
     backward_a();
-    const bool dp = comm_ && comm_->world() > 1;
+    const bool dp = world() > 1;
     if (dp) {
       HIP_OK(hipEventRecord(ev_a_, s));
       HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
@@ -175,7 +188,7 @@ class MnistEngine : public torch::CustomClassHolder {
       HIP_OK(hipEventRecord(ev_done_, comm_stream_));
       HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
     }
-    apply_optimizer(dp ? 1.0 / (double)comm_->world() : 1.0);
+    apply_optimizer(dp ? 1.0 / (double)world() : 1.0);
   }
 
   // Backup-worker path (SyncReplicas with replicas_to_aggregate < workers): sum-all-reduce of
@@ -184,7 +197,7 @@ class MnistEngine : public torch::CustomClassHolder {
   void reduce_grads(double weight) {
     hipStream_t s = stream();
     if (weight != 1.0) scale_f32((float*)grad_.data_ptr(), TOTAL, (float)weight, s);
-    if (!comm_ || comm_->world() <= 1) return;
+    if (world() <= 1) return;
     HIP_OK(hipEventRecord(ev_a_, s));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
     reduce_bucket(0, TOTAL);
@@ -255,6 +268,14 @@ class MnistEngine : public torch::CustomClassHolder {
 
   void reduce_bucket(int64_t beg, int64_t end) {
     const size_t n = (size_t)(end - beg);
+    if (ipc_ && (!comm_ || (int64_t)n <= ipc_small_)) {
+      // fp32 grads in, exact fp32 sum, written where the optimizer reads (bf16 gbf or fp32 grad)
+      void* out = bf16_comm_ ? (void*)((uint16_t*)gbf_.data_ptr() + beg) : (void*)((float*)grad_.data_ptr() + beg);
+      ipc_->all_reduce_raw((const float*)grad_.data_ptr() + beg, false, out, bf16_comm_, (int64_t)n, 1.0,
+                           comm_stream_);
+      return;
+    }
+    TORCH_CHECK(comm_, "no communicator for a ", n, "-element bucket");
     if (bf16_comm_) {
       uint16_t* gb = (uint16_t*)gbf_.data_ptr() + beg;
       cast_f32_bf16((const float*)grad_.data_ptr() + beg, gb, (int64_t)n, comm_stream_);
@@ -314,6 +335,8 @@ class MnistEngine : public torch::CustomClassHolder {
   bool nesterov_ = false;
   bool bf16_comm_ = true;
   c10::intrusive_ptr<RcclComm> comm_;
+  c10::intrusive_ptr<IpcComm> ipc_;
+  int64_t ipc_small_ = 0;
   at::Tensor params_, pbf_, grad_, m_, v_, gbf_, step_;
   at::Tensor p1_, idx1_, p2_, idx2_, fc1_slab_, hd_, dh_, dlogits_, loss_row_, correct_row_, dz2_, dp1m_, wg2_slab_,
       wg1_slab_, xbuf_, ybuf_;
@@ -360,6 +383,8 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_adam", &MnistEngine::set_adam)
       .def("set_momentum", &MnistEngine::set_momentum)
       .def("set_comm", &MnistEngine::set_comm)
+      .def("set_ipc", &MnistEngine::set_ipc)
+      .def("world", &MnistEngine::world)
       .def("forward", &MnistEngine::forward)
       .def("backward_a", &MnistEngine::backward_a)
       .def("backward_b", &MnistEngine::backward_b)

@@ -1,0 +1,28 @@
+"""Peer-to-peer IPC communicator bootstrap (native ``IpcComm``, csrc/runtime/ipc_comm.cpp).
+
+Every rank exports its staging + signal buffers (``hipIpcGetMemHandle``), the 128-byte handles
+are all-gathered over the Gloo control group, and every rank opens its peers' exports. Used for
+latency-bound buckets (the conv-gradient bucket B, ~200 KB) next to RCCL,
+or alone (every bucket) when RCCL is unavailable -- e.g. several ranks sharing one GPU in tests.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def make_ipc_comm(rank: int, world: int, device_index: int, capacity_elems: int, group=None,
+                  spin_limit_ms: float = 2000.0):
+    from .. import _native
+
+    _native.require()
+    comm = torch.classes.tfd.IpcComm(world, rank, device_index, capacity_elems)
+    comm.set_spin_limit_ms(spin_limit_ms)
+    h = comm.handle()
+    if world > 1:
+        allh = [torch.zeros_like(h) for _ in range(world)]
+        dist.all_gather(allh, h, group=group)
+        comm.open(torch.stack(allh))
+    else:
+        comm.open(h.reshape(1, -1))
+    return comm

@@ -1,0 +1,123 @@
+"""Peer-to-peer IPC all-reduce and the engine's data-parallel step with several ranks on ONE GPU
+(RCCL refuses duplicate devices; the IPC transport does not), so the multi-rank orchestration --
+buckets on the comm stream, events, hipGraph capture of collectives, 1/N in Adam -- is exercised
+on the single-GPU box."""
+import pytest
+import torch
+
+from dist_util import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+
+def _ar_worker(rank, world, n):
+    from tensorflow_distributed_amd.parallel.ipc import make_ipc_comm
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    comm = make_ipc_comm(rank, world, 0, n)
+    outs = []
+    base = torch.arange(n, dtype=torch.float32, device=dev) % 97
+    t = base * (rank + 1)
+    comm.all_reduce(t, 1.0)
+    torch.cuda.synchronize()
+    outs.append(t.cpu())
+    # bf16 + scale, and hipGraph capture/replay of the collective
+    tb = (base * (rank + 1)).to(torch.bfloat16)
+    comm.all_reduce(tb, 0.5)
+    torch.cuda.synchronize()
+    outs.append(tb.float().cpu())
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    x = torch.ones(n, device=dev) * (rank + 1)
+    with torch.cuda.stream(s):
+        comm.all_reduce(x, 1.0)  # warm
+        x.fill_(rank + 1)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            comm.all_reduce(x, 1.0)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    outs.append(x.cpu())
+    err = comm.error()
+    comm.close()
+    return outs, err
+
+
+@pytest.mark.parametrize("world,n", [(2, 52096), (3, 1000), (4, 200000)])
+def test_ipc_allreduce_multiprocess_one_gpu(cuda, world, n):
+    res = run_ranks(_ar_worker, world, n, timeout=300)
+    base = torch.arange(n, dtype=torch.float32) % 97
+    tot = sum(range(1, world + 1))
+    for outs, err in res:
+        assert err == 0
+        assert torch.equal(outs[0], base * tot)
+        ref_bf = sum((base * (r + 1)).to(torch.bfloat16).float() for r in range(world)) * 0.5
+        torch.testing.assert_close(outs[1], ref_bf.to(torch.bfloat16).float(), rtol=1e-2, atol=1e-2)
+        # three replays of an in-place all-reduce: x -> x * tot each time, starting from rank+1 per rank
+        # (first replay sums (1..world), later replays multiply the identical value by world)
+        assert torch.allclose(outs[2], torch.full((n,), float(tot * world ** 2)))
+
+
+def _engine_dp_worker(rank, world, B, steps):
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+    from tensorflow_distributed_amd.parallel.ipc import make_ipc_comm
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    comm = make_ipc_comm(rank, world, 0, M.TOTAL)
+    eng = torch.classes.tfd.MnistEngine(B, 0, 1.0, 5, rank)
+    eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+    eng.set_ipc(comm, 1 << 30, True)
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand(steps, world * B, 784, generator=g)
+    y = torch.randint(0, 10, (steps, world * B), generator=g, dtype=torch.int32)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        eng.params().copy_(M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()}).to(dev))
+        eng.sync_shadow()
+        for i in range(steps):
+            eng.feed_x().copy_(x[i, rank * B:(rank + 1) * B].to(dev))
+            eng.feed_y().copy_(y[i, rank * B:(rank + 1) * B].to(dev))
+            if i == 0:
+                eng.train_step()
+                eng.capture_train_step("t")
+            else:
+                eng.replay("t", 1)
+            torch.cuda.current_stream().synchronize()
+    torch.cuda.synchronize()
+    out = eng.params().cpu(), int(eng.step_tensor().item()), comm.error(), eng.world()
+    comm.close()
+    return out
+
+
+def test_engine_dp_over_ipc_matches_single_rank_big_batch(cuda):
+    """DP=2 (two processes sharing the GPU, IPC transport, captured graph) == DP=1 with 2B."""
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+
+    B, steps, world = 32, 3, 2
+    res = run_ranks(_engine_dp_worker, world, B, steps, timeout=300)
+    p0, s0, e0, w0 = res[0]
+    p1, s1, e1, w1 = res[1]
+    assert e0 == e1 == 0 and w0 == w1 == 2 and s0 == s1 == steps
+    assert torch.equal(p0, p1), "replicas diverged"
+    eng = torch.classes.tfd.MnistEngine(world * B, 0, 1.0, 5, 0)
+    eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand(steps, world * B, 784, generator=g)
+    y = torch.randint(0, 10, (steps, world * B), generator=g, dtype=torch.int32)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        eng.params().copy_(M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()}).to(cuda))
+        eng.sync_shadow()
+        for i in range(steps):
+            eng.feed_x().copy_(x[i].to(cuda))
+            eng.feed_y().copy_(y[i].to(cuda))
+            eng.train_step()
+    torch.cuda.synchronize()
+    ref = eng.params().cpu()
+    d = p0 - M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()})
+    dr = ref - M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()})
+    cos = torch.nn.functional.cosine_similarity(d, dr, dim=0).item()
+    assert cos > 0.99, cos  # bf16 gradient all-reduce vs one big-batch step: same update direction
