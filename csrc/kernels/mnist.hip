@@ -887,6 +887,9 @@ void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux, hi
   }
   conv1_wgrad<<<2 * B, 256, 0, s>>>(a);
 #endif
+}
+
+void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s) {
   reduce_conv_grads<<<RED2_BLOCKS + RED1_BLOCKS, 256, 0, s>>>(a);
 }
 

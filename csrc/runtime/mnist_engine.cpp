@@ -69,6 +69,8 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipEventCreateWithFlags(&ev_b_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
     HIP_OK(hipStreamCreateWithFlags(&aux_stream_, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&opt_stream_, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&ev_opt_a_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
   }
@@ -81,6 +83,8 @@ class MnistEngine : public torch::CustomClassHolder {
     hipEventDestroy(ev_fork_);
     hipEventDestroy(ev_join_);
     hipStreamDestroy(aux_stream_);
+    hipStreamDestroy(opt_stream_);
+    hipEventDestroy(ev_opt_a_);
   }
 
   // ---- state accessors (views share storage with the engine) ----
@@ -150,19 +154,25 @@ class MnistEngine : public torch::CustomClassHolder {
     MnistStepArgs a = args();
     a.step_bump = (int64_t*)step_.data_ptr();
     mnist_backward_b(a, stream(), aux_stream_, ev_fork_, ev_join_);
+    mnist_conv_grad_reduce(a, stream());
   }
   void apply_optimizer(double grad_scale) {
-    const uint16_t* gbf = (bf16_comm_ && world() > 1) ? (const uint16_t*)gbf_.data_ptr() : nullptr;
+    apply_optimizer_range(0, TOTAL, grad_scale, 0, stream());
+  }
+  // Optimizer over the flat range [beg, end) on stream s; t = global_step + t_offset.
+  void apply_optimizer_range(int64_t beg, int64_t end, double grad_scale, int t_offset, hipStream_t s) {
+    const uint16_t* gbf = (bf16_comm_ && world() > 1) ? (const uint16_t*)gbf_.data_ptr() + beg : nullptr;
+    const int64_t n = end - beg;
     if (opt_ == 0) {
-      AdamArgs a{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(), (const float*)grad_.data_ptr(),
-                 (uint16_t*)pbf_.data_ptr(), gbf, TOTAL, (float)lr_, (float)b1_, (float)b2_, (float)eps_,
-                 (const int64_t*)step_.data_ptr(), 0, (float)grad_scale};
-      adam_apply(a, stream());
+      AdamArgs a{(float*)params_.data_ptr() + beg, (float*)m_.data_ptr() + beg, (float*)v_.data_ptr() + beg,
+                 (const float*)grad_.data_ptr() + beg, (uint16_t*)pbf_.data_ptr() + beg, gbf, n, (float)lr_,
+                 (float)b1_, (float)b2_, (float)eps_, (const int64_t*)step_.data_ptr(), t_offset, (float)grad_scale};
+      adam_apply(a, s);
     } else {
-      SgdArgs a{(float*)params_.data_ptr(), opt_ == 2 ? (float*)m_.data_ptr() : nullptr, (const float*)grad_.data_ptr(),
-                (uint16_t*)pbf_.data_ptr(), gbf, TOTAL, (float)lr_, (float)momentum_, 0.f, (float)grad_scale,
-                nesterov_ ? 1 : 0};
-      sgd_apply(a, stream());
+      SgdArgs a{(float*)params_.data_ptr() + beg, opt_ == 2 ? (float*)m_.data_ptr() + beg : nullptr,
+                (const float*)grad_.data_ptr() + beg, (uint16_t*)pbf_.data_ptr() + beg, gbf, n, (float)lr_,
+                (float)momentum_, 0.f, (float)grad_scale, nesterov_ ? 1 : 0};
+      sgd_apply(a, s);
     }
   }
 
@@ -171,16 +181,26 @@ class MnistEngine : public torch::CustomClassHolder {
   // SyncReplicasOptimizer global step with replicas_to_aggregate == num_workers (averaged grads,
   // one ApplyAdam, global_step += 1).
   void train_step() {
+    // fwd -> fc bwd (bucket A ready) -> [bucket A all-reduce ->] optimizer on region A, on a side
+    // stream, overlapping the conv backward on the main stream (the fc params are not read again
+    // this step) -> conv grads -> slab reduce + step bump (after region A's optimizer has read
+    // the step) -> [bucket B all-reduce ->] optimizer on region B.
     hipStream_t s = stream();
+    const bool dp = world() > 1;
+    const double scale = dp ? 1.0 / (double)world() : 1.0;
     forward(true);
     backward_a();
-    const bool dp = world() > 1;
-    if (dp) {
-      HIP_OK(hipEventRecord(ev_a_, s));
-      HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
-      reduce_bucket(BUCKET_SPLIT, TOTAL);
-    }
-    backward_b();
+    HIP_OK(hipEventRecord(ev_a_, s));
+    hipStream_t os = dp ? comm_stream_ : opt_stream_;
+    HIP_OK(hipStreamWaitEvent(os, ev_a_, 0));
+    if (dp) reduce_bucket(BUCKET_SPLIT, TOTAL);
+    apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 1, os);
+    HIP_OK(hipEventRecord(ev_opt_a_, os));
+    MnistStepArgs a = args();
+    a.step_bump = (int64_t*)step_.data_ptr();
+    mnist_backward_b(a, s, aux_stream_, ev_fork_, ev_join_);
+    HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+    mnist_conv_grad_reduce(a, s);
     if (dp) {
       HIP_OK(hipEventRecord(ev_b_, s));
       HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
@@ -188,7 +208,7 @@ class MnistEngine : public torch::CustomClassHolder {
       HIP_OK(hipEventRecord(ev_done_, comm_stream_));
       HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
     }
-    apply_optimizer(dp ? 1.0 / (double)world() : 1.0);
+    apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s);
   }
 
   // Backup-worker path (SyncReplicas with replicas_to_aggregate < workers): sum-all-reduce of
@@ -343,7 +363,8 @@ class MnistEngine : public torch::CustomClassHolder {
   at::Tensor data_, labels_, perm_;
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t ev_a_ = nullptr, ev_b_ = nullptr, ev_done_ = nullptr, ev_fork_ = nullptr, ev_join_ = nullptr;
-  hipStream_t aux_stream_ = nullptr;
+  hipStream_t aux_stream_ = nullptr, opt_stream_ = nullptr;
+  hipEvent_t ev_opt_a_ = nullptr;
   std::map<std::string, hipGraphExec_t> graphs_;
 };
 

@@ -47,6 +47,8 @@ void mnist_backward_a(const MnistStepArgs& a, hipStream_t s);                 //
 // events recorded on s/aux; both are captured into the step graph as parallel branches).
 void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux = nullptr, hipEvent_t fork = nullptr,
                       hipEvent_t join = nullptr);
+// deterministic conv weight-gradient slab reduction (+ the global_step bump, MnistStepArgs::step_bump)
+void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s);
 
 // ---------------- optimizers (flat, fp32 master + bf16 shadow) ----------------
 struct AdamArgs {

@@ -12,6 +12,31 @@ def free_port():
         return s.getsockname()[1]
 
 
+def _to_plain(x):
+    """Tensors -> numpy (plain pickles): avoids torch's fd-passing, which races with child exit."""
+    import torch
+
+    if isinstance(x, torch.Tensor):
+        return ("__tensor__", x.detach().cpu().numpy())
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_plain(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _to_plain(v) for k, v in x.items()}
+    return x
+
+
+def _from_plain(x):
+    import torch
+
+    if isinstance(x, tuple) and len(x) == 2 and isinstance(x[0], str) and x[0] == "__tensor__":
+        return torch.from_numpy(x[1])
+    if isinstance(x, (list, tuple)):
+        return type(x)(_from_plain(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _from_plain(v) for k, v in x.items()}
+    return x
+
+
 def _entry(rank, world, port, fn, args, q):
     import torch.distributed as dist
 
@@ -20,7 +45,7 @@ def _entry(rank, world, port, fn, args, q):
     try:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         out = fn(rank, world, *args)
-        q.put((rank, "ok", out))
+        q.put((rank, "ok", _to_plain(out)))
     except Exception:
         q.put((rank, "err", traceback.format_exc()))
     finally:
@@ -41,7 +66,7 @@ def run_ranks(fn, world, *args, timeout=240):
             rank, status, out = q.get(timeout=timeout)
             if status != "ok":
                 raise AssertionError(f"rank {rank} failed:\n{out}")
-            res[rank] = out
+            res[rank] = _from_plain(out)
     finally:
         for p in procs:
             p.join(timeout=30)
