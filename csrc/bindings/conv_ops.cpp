@@ -1,0 +1,246 @@
+// Torch op bindings (torch.ops.tfd.*) of the NHWC conv / dense / batch-norm / pooling kernel library
+// (csrc/conv_kernels.h). All ops run on the caller's current HIP stream (graph-capturable); shapes
+// are checked on the host before any launch (the kernels assume C % 8 == 0 etc.).
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <tuple>
+
+#include "../conv_kernels.h"
+
+namespace tfd {
+namespace {
+
+hipStream_t cur() { return c10::hip::getCurrentHIPStream().stream(); }
+uint16_t* bp(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+float* fp(const at::Tensor& t) { return t.defined() ? reinterpret_cast<float*>(t.data_ptr()) : nullptr; }
+
+void check_bf16(const at::Tensor& t, const char* name, int dim) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous(), name,
+              ": contiguous bf16 GPU tensor required");
+  TORCH_CHECK(dim < 0 || t.dim() == dim, name, ": expected ", dim, " dims");
+}
+void check_f32(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), name, ": contiguous fp32 GPU tensor");
+}
+
+ConvShape shape_of(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad) {
+  ConvShape c;
+  c.N = (int)x.size(0); c.H = (int)x.size(1); c.W = (int)x.size(2); c.C = (int)x.size(3);
+  c.R = (int)w.size(0); c.S = (int)w.size(1); c.K = (int)w.size(3);
+  c.stride = (int)stride; c.pad = (int)pad;
+  TORCH_CHECK(w.size(2) == c.C, "conv: filter C ", w.size(2), " != input C ", c.C);
+  TORCH_CHECK(c.C % 8 == 0 && c.K % 8 == 0, "conv: C and K must be multiples of 8 (pad the input channels)");
+  TORCH_CHECK(c.Ho() > 0 && c.Wo() > 0 && stride >= 1 && pad >= 0, "conv: bad geometry");
+  TORCH_CHECK((int64_t)c.N * c.H * c.W * c.C < (1ll << 31), "conv: tensor too large for 32-bit indexing");
+  return c;
+}
+
+at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad) {
+  check_bf16(x, "x", 4);
+  check_bf16(w, "w", 4);
+  const ConvShape c = shape_of(x, w, stride, pad);
+  auto y = at::empty({c.N, c.Ho(), c.Wo(), c.K}, x.options());
+  conv_fwd(c, bp(x), bp(w), bp(y), cur());
+  return y;
+}
+
+at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, at::IntArrayRef xshape, int64_t stride, int64_t pad) {
+  check_bf16(dy, "dy", 4);
+  check_bf16(w, "w", 4);
+  TORCH_CHECK(xshape.size() == 4, "xshape [N,H,W,C]");
+  auto x = at::empty(xshape, dy.options());
+  const ConvShape c = shape_of(x, w, stride, pad);
+  TORCH_CHECK(dy.size(1) == c.Ho() && dy.size(2) == c.Wo() && dy.size(3) == c.K, "dgrad: dy shape mismatch");
+  conv_dgrad(c, bp(dy), bp(w), bp(x), cur());
+  return x;
+}
+
+void conv2d_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, int64_t stride, int64_t pad) {
+  check_bf16(x, "x", 4);
+  check_bf16(dy, "dy", 4);
+  check_f32(dw, "dw");
+  TORCH_CHECK(dw.dim() == 4, "dw [R,S,C,K]");
+  auto wfake = at::empty({dw.size(0), dw.size(1), dw.size(2), dw.size(3)}, x.options().device(at::kCPU));
+  const ConvShape c = shape_of(x, wfake, stride, pad);
+  TORCH_CHECK(dy.size(0) == c.N && dy.size(1) == c.Ho() && dy.size(2) == c.Wo() && dy.size(3) == c.K,
+              "wgrad: dy shape mismatch");
+  conv_wgrad(c, bp(x), bp(dy), fp(dw), conv_wgrad_splits(c), cur());
+}
+
+at::Tensor linear_fwd_op(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias) {
+  check_bf16(x, "x", 2);
+  check_bf16(w, "w", 2);
+  TORCH_CHECK(x.size(1) == w.size(0) && x.size(1) % 8 == 0 && w.size(1) % 8 == 0, "linear: shapes / multiples of 8");
+  if (bias) check_f32(*bias, "bias");
+  auto y = at::empty({x.size(0), w.size(1)}, x.options().dtype(at::kFloat));
+  linear_fwd(bp(x), bp(w), bias ? fp(*bias) : nullptr, fp(y), (int)x.size(0), (int)x.size(1), (int)w.size(1), cur());
+  return y;
+}
+
+at::Tensor linear_dgrad_op(const at::Tensor& dy, const at::Tensor& w) {
+  check_bf16(dy, "dy", 2);
+  check_bf16(w, "w", 2);
+  TORCH_CHECK(dy.size(1) == w.size(1), "linear_dgrad: shapes");
+  auto dx = at::empty({dy.size(0), w.size(0)}, dy.options());
+  linear_dgrad(bp(dy), bp(w), bp(dx), (int)dy.size(0), (int)w.size(0), (int)w.size(1), cur());
+  return dx;
+}
+
+void linear_wgrad_op(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw) {
+  check_bf16(x, "x", 2);
+  check_bf16(dy, "dy", 2);
+  check_f32(dw, "dw");
+  TORCH_CHECK(dw.size(0) == x.size(1) && dw.size(1) == dy.size(1) && x.size(0) == dy.size(0), "linear_wgrad: shapes");
+  linear_wgrad(bp(x), bp(dy), fp(dw), (int)x.size(0), (int)x.size(1), (int)dy.size(1), cur());
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& y, const at::Tensor& gamma,
+                                                      const at::Tensor& beta, const c10::optional<at::Tensor>& res,
+                                                      bool relu, at::Tensor running_mean, at::Tensor running_var,
+                                                      double momentum, double eps) {
+  check_bf16(y, "y", -1);
+  const int C = (int)y.size(-1);
+  const int M = (int)(y.numel() / C);
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn: C must be a multiple of 8 and <= 2048");
+  check_f32(gamma, "gamma");
+  check_f32(beta, "beta");
+  if (res) {
+    check_bf16(*res, "residual", -1);
+    TORCH_CHECK(res->numel() == y.numel(), "bn: residual shape");
+  }
+  auto out = at::empty_like(y);
+  auto f = y.options().dtype(at::kFloat);
+  auto mean = at::empty({C}, f), invstd = at::empty({C}, f);
+  auto part = at::empty({bn_partials_size(M, C)}, f);
+  bn_forward(bp(y), fp(gamma), fp(beta), res ? bp(*res) : nullptr, relu ? 1 : 0, bp(out), fp(mean), fp(invstd),
+             running_mean.defined() && running_mean.numel() ? fp(running_mean) : nullptr,
+             running_var.defined() && running_var.numel() ? fp(running_var) : nullptr, (float)momentum, (float)eps, M,
+             C, fp(part), cur());
+  return {out, mean, invstd};
+}
+
+std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tensor& out, const at::Tensor& y,
+                                          const at::Tensor& gamma, const at::Tensor& mean, const at::Tensor& invstd,
+                                          bool relu, bool want_dres, at::Tensor dgamma, at::Tensor dbeta) {
+  check_bf16(dout, "dout", -1);
+  check_bf16(out, "out", -1);
+  check_bf16(y, "y", -1);
+  check_f32(dgamma, "dgamma");
+  check_f32(dbeta, "dbeta");
+  const int C = (int)y.size(-1);
+  const int M = (int)(y.numel() / C);
+  auto dy = at::empty_like(y);
+  at::Tensor dres = want_dres ? at::empty_like(y) : at::Tensor();
+  auto part = at::empty({bn_partials_size(M, C)}, y.options().dtype(at::kFloat));
+  bn_backward(bp(dout), bp(out), bp(y), fp(gamma), fp(mean), fp(invstd), relu ? 1 : 0, bp(dy),
+              want_dres ? bp(dres) : nullptr, fp(dgamma), fp(dbeta), M, C, fp(part), cur());
+  return {dy, dres};
+}
+
+at::Tensor bn_infer_op(const at::Tensor& y, const at::Tensor& gamma, const at::Tensor& beta, const at::Tensor& rm,
+                       const at::Tensor& rv, double eps, bool relu) {
+  check_bf16(y, "y", -1);
+  const int C = (int)y.size(-1);
+  auto out = at::empty_like(y);
+  bn_infer(bp(y), fp(gamma), fp(beta), fp(rm), fp(rv), (float)eps, relu ? 1 : 0, bp(out), (int)(y.numel() / C), C,
+           cur());
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t st, int64_t pad) {
+  check_bf16(x, "x", 4);
+  const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), C = (int)x.size(3);
+  TORCH_CHECK(C % 8 == 0 && k <= 15, "maxpool: C % 8, k <= 15");
+  const int Ho = (H + 2 * (int)pad - (int)k) / (int)st + 1, Wo = (W + 2 * (int)pad - (int)k) / (int)st + 1;
+  auto y = at::empty({N, Ho, Wo, C}, x.options());
+  auto am = at::empty({N, Ho, Wo, C}, x.options().dtype(at::kByte));
+  maxpool_fwd(bp(x), bp(y), am.data_ptr<uint8_t>(), N, H, W, C, (int)k, (int)st, (int)pad, Ho, Wo, cur());
+  return {y, am};
+}
+
+at::Tensor maxpool2d_bwd(const at::Tensor& dy, const at::Tensor& am, at::IntArrayRef xshape, int64_t k, int64_t st,
+                         int64_t pad) {
+  check_bf16(dy, "dy", 4);
+  auto dx = at::empty(xshape, dy.options());
+  maxpool_bwd(bp(dy), am.data_ptr<uint8_t>(), bp(dx), (int)xshape[0], (int)xshape[1], (int)xshape[2], (int)xshape[3],
+              (int)k, (int)st, (int)pad, (int)dy.size(1), (int)dy.size(2), cur());
+  return dx;
+}
+
+at::Tensor avgpool_fwd_op(const at::Tensor& x) {
+  check_bf16(x, "x", 4);
+  const int N = (int)x.size(0), HW = (int)(x.size(1) * x.size(2)), C = (int)x.size(3);
+  auto y = at::empty({N, C}, x.options());
+  avgpool_fwd(bp(x), bp(y), N, HW, C, cur());
+  return y;
+}
+
+at::Tensor avgpool_bwd_op(const at::Tensor& dy, at::IntArrayRef xshape) {
+  check_bf16(dy, "dy", 2);
+  auto dx = at::empty(xshape, dy.options());
+  avgpool_bwd(bp(dy), bp(dx), (int)xshape[0], (int)(xshape[1] * xshape[2]), (int)xshape[3], cur());
+  return dx;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> softmax_xent_op(const at::Tensor& logits, const at::Tensor& labels) {
+  check_f32(logits, "logits");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kInt && labels.numel() == logits.size(0), "labels int32");
+  const int N = (int)logits.size(0), K = (int)logits.size(1);
+  auto loss = at::empty({N}, logits.options());
+  auto corr = at::empty({N}, logits.options());
+  auto dl = at::empty({N, K}, logits.options().dtype(at::kBFloat16));
+  softmax_xent(fp(logits), labels.data_ptr<int>(), fp(loss), fp(corr), bp(dl), N, K, cur());
+  return {loss, corr, dl};
+}
+
+at::Tensor pad_channels_op(const at::Tensor& x, int64_t cout) {
+  check_f32(x, "x");
+  const int cin = (int)x.size(-1);
+  TORCH_CHECK(cout >= cin, "pad_channels: cout < cin");
+  std::vector<int64_t> sh(x.sizes().begin(), x.sizes().end());
+  sh.back() = cout;
+  auto y = at::empty(sh, x.options().dtype(at::kBFloat16));
+  pad_channels(fp(x), bp(y), (int)(x.numel() / cin), cin, (int)cout, cur());
+  return y;
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(tfd, m) {
+  m.def("conv2d_fwd(Tensor x, Tensor w, int stride, int pad) -> Tensor");
+  m.impl("conv2d_fwd", c10::DispatchKey::CUDA, &conv2d_fwd);
+  m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad) -> Tensor");
+  m.impl("conv2d_dgrad", c10::DispatchKey::CUDA, &conv2d_dgrad);
+  m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad) -> ()");
+  m.impl("conv2d_wgrad", c10::DispatchKey::CUDA, &conv2d_wgrad);
+  m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias) -> Tensor");
+  m.impl("linear_fwd", c10::DispatchKey::CUDA, &linear_fwd_op);
+  m.def("linear_dgrad(Tensor dy, Tensor w) -> Tensor");
+  m.impl("linear_dgrad", c10::DispatchKey::CUDA, &linear_dgrad_op);
+  m.def("linear_wgrad(Tensor x, Tensor dy, Tensor(a!) dw) -> ()");
+  m.impl("linear_wgrad", c10::DispatchKey::CUDA, &linear_wgrad_op);
+  m.def("bn_fwd(Tensor y, Tensor gamma, Tensor beta, Tensor? residual, bool relu, Tensor(a!) running_mean, "
+        "Tensor(b!) running_var, float momentum, float eps) -> (Tensor, Tensor, Tensor)");
+  m.impl("bn_fwd", c10::DispatchKey::CUDA, &bn_fwd);
+  m.def("bn_bwd(Tensor dout, Tensor out, Tensor y, Tensor gamma, Tensor mean, Tensor invstd, bool relu, "
+        "bool want_dres, Tensor(a!) dgamma, Tensor(b!) dbeta) -> (Tensor, Tensor)");
+  m.impl("bn_bwd", c10::DispatchKey::CUDA, &bn_bwd);
+  m.def("bn_infer(Tensor y, Tensor gamma, Tensor beta, Tensor rm, Tensor rv, float eps, bool relu) -> Tensor");
+  m.impl("bn_infer", c10::DispatchKey::CUDA, &bn_infer_op);
+  m.def("maxpool2d_fwd(Tensor x, int k, int stride, int pad) -> (Tensor, Tensor)");
+  m.impl("maxpool2d_fwd", c10::DispatchKey::CUDA, &maxpool2d_fwd);
+  m.def("maxpool2d_bwd(Tensor dy, Tensor argmax, int[] xshape, int k, int stride, int pad) -> Tensor");
+  m.impl("maxpool2d_bwd", c10::DispatchKey::CUDA, &maxpool2d_bwd);
+  m.def("avgpool_fwd(Tensor x) -> Tensor");
+  m.impl("avgpool_fwd", c10::DispatchKey::CUDA, &avgpool_fwd_op);
+  m.def("avgpool_bwd(Tensor dy, int[] xshape) -> Tensor");
+  m.impl("avgpool_bwd", c10::DispatchKey::CUDA, &avgpool_bwd_op);
+  m.def("softmax_xent(Tensor logits, Tensor labels) -> (Tensor, Tensor, Tensor)");
+  m.impl("softmax_xent", c10::DispatchKey::CUDA, &softmax_xent_op);
+  m.def("pad_channels(Tensor x, int cout) -> Tensor");
+  m.impl("pad_channels", c10::DispatchKey::CUDA, &pad_channels_op);
+}
+
+}  // namespace tfd

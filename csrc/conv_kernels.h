@@ -1,0 +1,59 @@
+// Host API of the generic NHWC convolution / dense / normalisation kernel library
+// (csrc/kernels/conv_nhwc.hip, csrc/kernels/norm.hip) used by the ResNet-style models.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+namespace tfd {
+
+struct ConvShape {
+  int N, H, W, C;   // input NHWC
+  int K, R, S;      // output channels, filter rows/cols (HWIO filter [R][S][C][K])
+  int stride, pad;  // symmetric zero padding
+  int Ho() const { return (H + 2 * pad - R) / stride + 1; }
+  int Wo() const { return (W + 2 * pad - S) / stride + 1; }
+};
+
+void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, hipStream_t st);
+void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st);
+// dw: fp32 [R*S*C][K]; overwritten (zeroed first when split)
+void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float* dw, int splits, hipStream_t st);
+int conv_wgrad_splits(const ConvShape& c);
+
+void linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, float* y, int M, int Kin, int N,
+                hipStream_t st);
+void linear_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int Kin, int N, hipStream_t st);
+void linear_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int Kin, int N, hipStream_t st);
+
+// ---- batch norm (training mode, per-channel over the M = N*H*W rows of a [M][C] bf16 tensor) ----
+// partials: fp32 workspace of bn_partials_size(M, C) floats.
+int bn_partials_size(int M, int C);
+// mean/invstd [C]; running stats updated with `momentum` (TF decay semantics: r = r*m + x*(1-m)).
+void bn_forward(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
+                uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var, float momentum,
+                float eps, int M, int C, float* partials, hipStream_t st);
+// dout -> dy (through relu/bn), writes dgamma/dbeta (fp32, overwritten) and, when dres != null, the
+// gradient of the residual input (== gradient after the relu mask).
+void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* mean,
+                 const float* invstd, int relu, uint16_t* dy, uint16_t* dres, float* dgamma, float* dbeta, int M,
+                 int C, float* partials, hipStream_t st);
+// inference-mode BN (running statistics), optional relu
+void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,
+              float eps, int relu, uint16_t* out, int M, int C, hipStream_t st);
+
+// ---- pooling / head ----
+void maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* argmax, int N, int H, int W, int C, int k, int st, int pad,
+                 int Ho, int Wo, hipStream_t s);
+void maxpool_bwd(const uint16_t* dy, const uint8_t* argmax, uint16_t* dx, int N, int H, int W, int C, int k, int st,
+                 int pad, int Ho, int Wo, hipStream_t s);
+void avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s);   // global average
+void avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t s);
+// softmax cross-entropy over fp32 logits [N][K], int labels: loss_rows [N], dlogits bf16 [N][K] (mean
+// over N folded in), correct [N]
+void softmax_xent(const float* logits, const int* labels, float* loss_rows, float* correct, uint16_t* dlogits, int N,
+                  int K, hipStream_t s);
+void pad_channels(const float* x, uint16_t* y, int P, int Cin, int Cout, hipStream_t s);  // fp32 NHWC -> bf16, zero-pad C
+
+}  // namespace tfd

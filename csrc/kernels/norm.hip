@@ -1,0 +1,409 @@
+// Batch normalisation (training + inference), pooling and the softmax-cross-entropy head for the
+// NHWC ResNet-style models (see csrc/conv_kernels.h). Activations are bf16 [M = N*H*W][C]; all
+// statistics and parameter gradients are fp32. Reductions are two-level and deterministic:
+// per-block partials over a row chunk (8 channels per thread, 16-B loads), then a per-channel
+// finalize kernel in a fixed order.
+#include "../common.h"
+#include "../conv_kernels.h"
+
+namespace tfd {
+namespace {
+
+constexpr int NT = 256;
+
+struct RowSplit {
+  int tpr;   // threads per row (one 8-channel chunk each, C/8 <= 256)
+  int rg;    // row groups per block
+  int nblk;  // blocks
+  int rb;    // rows per block
+};
+RowSplit row_split(int M, int C) {
+  RowSplit r;
+  r.tpr = C / 8;
+  r.rg = NT / r.tpr;
+  r.nblk = std::max(1, std::min(1024, (M + 63) / 64));
+  r.rb = (M + r.nblk - 1) / r.nblk;
+  r.nblk = (M + r.rb - 1) / r.rb;
+  return r;
+}
+
+__device__ __forceinline__ void unpack8(const uint4& u, float (&f)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
+}
+
+// partial sums of (a, b) per channel over a row chunk; mode 0: a = y, b = y^2 ; mode 1 (backward):
+// a = dz, b = dz * xhat with dz = relu-masked dout
+__global__ __launch_bounds__(NT) void bn_partial_kernel(int mode, const uint16_t* __restrict__ y,
+                                                        const uint16_t* __restrict__ dout,
+                                                        const uint16_t* __restrict__ out, int relu,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd, int M, int C, int tpr,
+                                                        int rg, int rb, float* __restrict__ part) {
+  __shared__ float red[2][NT][8];
+  const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
+  float sa[8], sb[8], mu[8], is[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sa[j] = 0.f; sb[j] = 0.f; }
+  if (mode == 1 && g < rg) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j]; }
+  }
+  const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
+  if (g < rg) {
+    for (int r = r0 + g; r < r1; r += rg) {
+      const size_t o = (size_t)r * C + c0;
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(y + o), v);
+      if (mode == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { sa[j] += v[j]; sb[j] = fmaf(v[j], v[j], sb[j]); }
+      } else {
+        float d[8];
+        unpack8(*reinterpret_cast<const uint4*>(dout + o), d);
+        if (relu) {
+          float ov[8];
+          unpack8(*reinterpret_cast<const uint4*>(out + o), ov);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d[j] = ov[j] > 0.f ? d[j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { sa[j] += d[j]; sb[j] = fmaf(d[j], (v[j] - mu[j]) * is[j], sb[j]); }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[0][t][j] = sa[j]; red[1][t][j] = sb[j]; }
+  __syncthreads();
+  if (g == 0) {
+    for (int q = 1; q < rg; ++q) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { sa[j] += red[0][q * tpr + ch][j]; sb[j] += red[1][q * tpr + ch][j]; }
+    }
+    float* pa = part + (size_t)blockIdx.x * 2 * C;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { pa[c0 + j] = sa[j]; pa[C + c0 + j] = sb[j]; }
+  }
+}
+
+// per-channel finalize. mode 0: mean/invstd (+running stats); mode 1: dbeta/dgamma.
+__global__ __launch_bounds__(NT) void bn_final_kernel(int mode, const float* __restrict__ part, int nblk, int M,
+                                                      int C, float eps, float momentum, float* __restrict__ o0,
+                                                      float* __restrict__ o1, float* __restrict__ rmean,
+                                                      float* __restrict__ rvar) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < nblk; ++k) {
+    a += part[(size_t)k * 2 * C + c];
+    b += part[(size_t)k * 2 * C + C + c];
+  }
+  if (mode == 0) {
+    const float mu = a / (float)M;
+    const float var = fmaxf(b / (float)M - mu * mu, 0.f);
+    o0[c] = mu;
+    o1[c] = rsqrtf(var + eps);
+    if (rmean) {
+      rmean[c] = rmean[c] * momentum + mu * (1.f - momentum);
+      rvar[c] = rvar[c] * momentum + var * ((float)M / (float)max(M - 1, 1)) * (1.f - momentum);
+    }
+  } else {
+    o0[c] = a;  // dbeta
+    o1[c] = b;  // dgamma
+  }
+}
+
+__global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, const float* __restrict__ mean,
+                                                      const float* __restrict__ invstd,
+                                                      const uint16_t* __restrict__ res, int relu,
+                                                      uint16_t* __restrict__ out, int64_t nchunks, int C) {
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < nchunks; i += stride) {
+    const int c0 = (int)((i * 8) % C);
+    float v[8];
+    unpack8(reinterpret_cast<const uint4*>(y)[i], v);
+    float r[8];
+    if (res) unpack8(reinterpret_cast<const uint4*>(res)[i], r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float z = (v[j] - mean[c0 + j]) * invstd[c0 + j] * gamma[c0 + j] + beta[c0 + j];
+      if (res) z += r[j];
+      v[j] = relu ? fmaxf(z, 0.f) : z;
+    }
+    reinterpret_cast<uint4*>(out)[i] = pack8(v);
+  }
+}
+
+__global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout,
+                                                          const uint16_t* __restrict__ out, const uint16_t* __restrict__ y,
+                                                          const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, const float* __restrict__ dbeta,
+                                                          const float* __restrict__ dgamma, int relu,
+                                                          uint16_t* __restrict__ dy, uint16_t* __restrict__ dres,
+                                                          int64_t nchunks, int C, float invM) {
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < nchunks; i += stride) {
+    const int c0 = (int)((i * 8) % C);
+    float d[8], v[8];
+    unpack8(reinterpret_cast<const uint4*>(dout)[i], d);
+    unpack8(reinterpret_cast<const uint4*>(y)[i], v);
+    if (relu) {
+      float ov[8];
+      unpack8(reinterpret_cast<const uint4*>(out)[i], ov);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = ov[j] > 0.f ? d[j] : 0.f;
+    }
+    if (dres) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      const float xh = (v[j] - mean[c]) * invstd[c];
+      o[j] = gamma[c] * invstd[c] * (d[j] - (dbeta[c] + xh * dgamma[c]) * invM);
+    }
+    reinterpret_cast<uint4*>(dy)[i] = pack8(o);
+  }
+}
+
+__global__ __launch_bounds__(NT) void bn_infer_kernel(const uint16_t* __restrict__ y, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, const float* __restrict__ rm,
+                                                      const float* __restrict__ rv, float eps, int relu,
+                                                      uint16_t* __restrict__ out, int64_t nchunks, int C) {
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < nchunks; i += stride) {
+    const int c0 = (int)((i * 8) % C);
+    float v[8];
+    unpack8(reinterpret_cast<const uint4*>(y)[i], v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      const float z = (v[j] - rm[c]) * rsqrtf(rv[c] + eps) * gamma[c] + beta[c];
+      v[j] = relu ? fmaxf(z, 0.f) : z;
+    }
+    reinterpret_cast<uint4*>(out)[i] = pack8(v);
+  }
+}
+
+// ---- pooling ----
+__global__ __launch_bounds__(NT) void maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                         uint8_t* __restrict__ am, int N, int H, int W, int C, int k,
+                                                         int st, int pad, int Ho, int Wo) {
+  const int64_t total = (int64_t)N * Ho * Wo * (C / 8);
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= total) return;
+  const int cc = (int)(i % (C / 8));
+  int64_t p = i / (C / 8);
+  const int wo = (int)(p % Wo);
+  p /= Wo;
+  const int ho = (int)(p % Ho);
+  const int n = (int)(p / Ho);
+  float best[8];
+  uint8_t arg[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; }
+  for (int r = 0; r < k; ++r) {
+    const int h = ho * st - pad + r;
+    if ((unsigned)h >= (unsigned)H) continue;
+    for (int s = 0; s < k; ++s) {
+      const int w = wo * st - pad + s;
+      if ((unsigned)w >= (unsigned)W) continue;
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + ((size_t)(n * H + h) * W + w) * C + cc * 8), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (v[j] > best[j]) { best[j] = v[j]; arg[j] = (uint8_t)(r * k + s); }
+    }
+  }
+  reinterpret_cast<uint4*>(y)[i] = pack8(best);
+  uint32_t lo = arg[0] | arg[1] << 8 | arg[2] << 16 | (uint32_t)arg[3] << 24;
+  uint32_t hi = arg[4] | arg[5] << 8 | arg[6] << 16 | (uint32_t)arg[7] << 24;
+  reinterpret_cast<uint2*>(am)[i] = make_uint2(lo, hi);
+}
+
+// gather form: every input element sums the output windows whose argmax points at it
+__global__ __launch_bounds__(NT) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ am,
+                                                         uint16_t* __restrict__ dx, int N, int H, int W, int C, int k,
+                                                         int st, int pad, int Ho, int Wo) {
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= total) return;
+  const int cc = (int)(i % (C / 8));
+  int64_t p = i / (C / 8);
+  const int w = (int)(p % W);
+  p /= W;
+  const int h = (int)(p % H);
+  const int n = (int)(p / H);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  const int ho_lo = max(0, (h + pad - k + st) / st), ho_hi = min(Ho - 1, (h + pad) / st);
+  const int wo_lo = max(0, (w + pad - k + st) / st), wo_hi = min(Wo - 1, (w + pad) / st);
+  for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+    const int r = h + pad - ho * st;
+    if (r < 0 || r >= k) continue;
+    for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+      const int s = w + pad - wo * st;
+      if (s < 0 || s >= k) continue;
+      const size_t o = ((size_t)(n * Ho + ho) * Wo + wo) * C + cc * 8;
+      float g[8];
+      unpack8(*reinterpret_cast<const uint4*>(dy + o), g);
+      const uint2 a = *reinterpret_cast<const uint2*>(am + o);
+      const uint8_t* ab = reinterpret_cast<const uint8_t*>(&a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (ab[j] == (uint8_t)(r * k + s)) acc[j] += g[j];
+    }
+  }
+  reinterpret_cast<uint4*>(dx)[i] = pack8(acc);
+}
+
+__global__ __launch_bounds__(NT) void avgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                         int N, int HW, int C) {
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i - n * C;
+  float s = 0.f;
+  for (int p = 0; p < HW; ++p) s += bf2f(x[((size_t)n * HW + p) * C + c]);
+  y[i] = f2bf_bits(s / (float)HW);
+}
+
+__global__ __launch_bounds__(NT) void avgpool_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx,
+                                                         int N, int HW, int C) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= (int64_t)N * HW * C) return;
+  const int c = (int)(i % C);
+  const int n = (int)(i / ((int64_t)HW * C));
+  dx[i] = f2bf_bits(bf2f(dy[(size_t)n * C + c]) / (float)HW);
+}
+
+__global__ __launch_bounds__(NT) void softmax_xent_kernel(const float* __restrict__ logits, const int* __restrict__ labels,
+                                                          float* __restrict__ loss, float* __restrict__ correct,
+                                                          uint16_t* __restrict__ dl, int N, int K) {
+  __shared__ float red[NT / 64];
+  __shared__ int redi[NT / 64];
+  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const float* z = logits + (size_t)row * K;
+  float mx = -INFINITY;
+  int am = 0;
+  for (int k = t; k < K; k += NT)
+    if (z[k] > mx) { mx = z[k]; am = k; }
+  // argmax (first index on ties) and max
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(am, o, 64);
+    if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+  }
+  if (lane == 0) { red[wv] = mx; redi[wv] = am; }
+  __syncthreads();
+  mx = red[0];
+  am = redi[0];
+  for (int q = 1; q < NT / 64; ++q)
+    if (red[q] > mx || (red[q] == mx && redi[q] < am)) { mx = red[q]; am = redi[q]; }
+  __syncthreads();
+  float se = 0.f;
+  for (int k = t; k < K; k += NT) se += __expf(z[k] - mx);
+  se = wave_sum(se);
+  if (lane == 0) red[wv] = se;
+  __syncthreads();
+  se = 0.f;
+  for (int q = 0; q < NT / 64; ++q) se += red[q];
+  const float lse = mx + __logf(se);
+  const int lbl = labels[row];
+  if (t == 0) {
+    loss[row] = lse - z[lbl];
+    correct[row] = (am == lbl) ? 1.f : 0.f;
+  }
+  const float invN = 1.f / (float)N;
+  for (int k = t; k < K; k += NT)
+    dl[(size_t)row * K + k] = f2bf_bits((__expf(z[k] - lse) - (k == lbl ? 1.f : 0.f)) * invN);
+}
+
+__global__ __launch_bounds__(NT) void pad_channels_kernel(const float* __restrict__ x, uint16_t* __restrict__ y,
+                                                          int64_t P, int Cin, int Cout) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= P * Cout) return;
+  const int c = (int)(i % Cout);
+  const int64_t p = i / Cout;
+  y[i] = c < Cin ? f2bf_bits(x[p * Cin + c]) : (uint16_t)0;
+}
+
+inline int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + NT - 1) / NT)); }
+
+}  // namespace
+
+int bn_partials_size(int M, int C) {
+  const RowSplit r = row_split(M, C);
+  return r.nblk * 2 * C;
+}
+
+void bn_forward(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
+                uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var, float momentum,
+                float eps, int M, int C, float* partials, hipStream_t st) {
+  const RowSplit r = row_split(M, C);
+  bn_partial_kernel<<<r.nblk, NT, 0, st>>>(0, y, nullptr, nullptr, 0, nullptr, nullptr, M, C, r.tpr, r.rg, r.rb,
+                                           partials);
+  bn_final_kernel<<<(C + NT - 1) / NT, NT, 0, st>>>(0, partials, r.nblk, M, C, eps, momentum, mean, invstd,
+                                                    running_mean, running_var);
+  const int64_t nch = (int64_t)M * C / 8;
+  bn_apply_kernel<<<grid_for(nch), NT, 0, st>>>(y, gamma, beta, mean, invstd, residual, relu, out, nch, C);
+}
+
+void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* mean,
+                 const float* invstd, int relu, uint16_t* dy, uint16_t* dres, float* dgamma, float* dbeta, int M,
+                 int C, float* partials, hipStream_t st) {
+  const RowSplit r = row_split(M, C);
+  bn_partial_kernel<<<r.nblk, NT, 0, st>>>(1, y, dout, out, relu, mean, invstd, M, C, r.tpr, r.rg, r.rb, partials);
+  bn_final_kernel<<<(C + NT - 1) / NT, NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,
+                                                    nullptr);
+  const int64_t nch = (int64_t)M * C / 8;
+  bn_bwd_apply_kernel<<<grid_for(nch), NT, 0, st>>>(dout, out, y, gamma, mean, invstd, dbeta, dgamma, relu, dy, dres,
+                                                    nch, C, 1.f / (float)M);
+}
+
+void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,
+              float eps, int relu, uint16_t* out, int M, int C, hipStream_t st) {
+  const int64_t nch = (int64_t)M * C / 8;
+  bn_infer_kernel<<<grid_for(nch), NT, 0, st>>>(y, gamma, beta, rmean, rvar, eps, relu, out, nch, C);
+}
+
+void maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* argmax, int N, int H, int W, int C, int k, int st, int pad,
+                 int Ho, int Wo, hipStream_t s) {
+  const int64_t total = (int64_t)N * Ho * Wo * (C / 8);
+  maxpool_fwd_kernel<<<(int)((total + NT - 1) / NT), NT, 0, s>>>(x, y, argmax, N, H, W, C, k, st, pad, Ho, Wo);
+}
+
+void maxpool_bwd(const uint16_t* dy, const uint8_t* argmax, uint16_t* dx, int N, int H, int W, int C, int k, int st,
+                 int pad, int Ho, int Wo, hipStream_t s) {
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  maxpool_bwd_kernel<<<(int)((total + NT - 1) / NT), NT, 0, s>>>(dy, argmax, dx, N, H, W, C, k, st, pad, Ho, Wo);
+}
+
+void avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s) {
+  avgpool_fwd_kernel<<<(N * C + NT - 1) / NT, NT, 0, s>>>(x, y, N, HW, C);
+}
+
+void avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t s) {
+  const int64_t total = (int64_t)N * HW * C;
+  avgpool_bwd_kernel<<<(int)((total + NT - 1) / NT), NT, 0, s>>>(dy, dx, N, HW, C);
+}
+
+void softmax_xent(const float* logits, const int* labels, float* loss_rows, float* correct, uint16_t* dlogits, int N,
+                  int K, hipStream_t s) {
+  softmax_xent_kernel<<<N, NT, 0, s>>>(logits, labels, loss_rows, correct, dlogits, N, K);
+}
+
+void pad_channels(const float* x, uint16_t* y, int P, int Cin, int Cout, hipStream_t s) {
+  const int64_t total = (int64_t)P * Cout;
+  pad_channels_kernel<<<(int)((total + NT - 1) / NT), NT, 0, s>>>(x, y, P, Cin, Cout);
+}
+
+}  // namespace tfd

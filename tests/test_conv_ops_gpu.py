@@ -1,0 +1,133 @@
+"""Numerics of the generic NHWC HIP kernel library (conv fwd/dgrad/wgrad, dense, batch norm,
+pooling, softmax-xent) against plain PyTorch fp32 references of the same ops."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+ops = None
+
+
+@pytest.fixture(autouse=True)
+def _ops(cuda):
+    global ops
+    ops = torch.ops.tfd
+
+
+def rb(t):  # round to bf16 and back (the kernels' operand precision)
+    return t.to(torch.bfloat16).float()
+
+
+def relerr(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+CONVS = [  # N, H, W, C, K, R, stride, pad
+    (2, 9, 7, 16, 24, 3, 1, 1),
+    (2, 10, 10, 16, 32, 3, 2, 1),
+    (3, 8, 8, 32, 16, 1, 1, 0),
+    (2, 9, 9, 16, 32, 1, 2, 0),
+    (2, 16, 16, 8, 16, 7, 2, 3),
+    (4, 14, 14, 64, 64, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS)
+def test_conv_fwd_dgrad_wgrad(cuda, N, H, W, C, K, R, st, pad):
+    torch.manual_seed(0)
+    x = rb(torch.randn(N, H, W, C))
+    w = rb(torch.randn(R, R, C, K) * 0.2)
+    xr = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    wr = w.permute(3, 2, 0, 1).clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=st, padding=pad)
+    dy = rb(torch.randn_like(yr))
+    yr.backward(dy)
+    y = ops.conv2d_fwd(x.to(cuda, torch.bfloat16), w.to(cuda, torch.bfloat16), st, pad)
+    assert relerr(y.cpu().permute(0, 3, 1, 2), yr.detach()) < 1e-2
+    dyn = dy.permute(0, 2, 3, 1).contiguous().to(cuda, torch.bfloat16)
+    dx = ops.conv2d_dgrad(dyn, w.to(cuda, torch.bfloat16), [N, H, W, C], st, pad)
+    assert relerr(dx.cpu().permute(0, 3, 1, 2), xr.grad) < 1e-2
+    dw = torch.zeros(R, R, C, K, device=cuda)
+    ops.conv2d_wgrad(x.to(cuda, torch.bfloat16), dyn, dw, st, pad)
+    assert relerr(dw.cpu(), wr.grad.permute(2, 3, 1, 0)) < 1e-3
+
+
+def test_linear(cuda):
+    torch.manual_seed(1)
+    M, Kin, N = 24, 64, 40
+    x, w, b = rb(torch.randn(M, Kin)), rb(torch.randn(Kin, N) * 0.1), torch.randn(N)
+    y = ops.linear_fwd(x.to(cuda, torch.bfloat16), w.to(cuda, torch.bfloat16), b.to(cuda))
+    assert relerr(y.cpu(), x @ w + b) < 1e-4
+    dy = rb(torch.randn(M, N))
+    dx = ops.linear_dgrad(dy.to(cuda, torch.bfloat16), w.to(cuda, torch.bfloat16))
+    assert relerr(dx.cpu(), dy @ w.t()) < 1e-2
+    dw = torch.empty(Kin, N, device=cuda)
+    ops.linear_wgrad(x.to(cuda, torch.bfloat16), dy.to(cuda, torch.bfloat16), dw)
+    assert relerr(dw.cpu(), x.t() @ dy) < 1e-4
+
+
+@pytest.mark.parametrize("relu,res", [(True, False), (False, True), (True, True)])
+def test_batchnorm_train(cuda, relu, res):
+    torch.manual_seed(2)
+    M, C = 300, 64
+    y = rb(torch.randn(M, C) * 3 + 1)
+    g, b = torch.rand(C) + 0.5, torch.randn(C)
+    r = rb(torch.randn(M, C)) if res else None
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    out, mean, invstd = ops.bn_fwd(y.to(cuda, torch.bfloat16), g.to(cuda), b.to(cuda),
+                                   r.to(cuda, torch.bfloat16) if res else None, relu, rm, rv, 0.9, 1e-5)
+    yr = y.clone().requires_grad_(True)
+    z = F.batch_norm(yr, None, None, g, b, training=True, eps=1e-5)
+    if res:
+        z = z + r
+    if relu:
+        z = torch.relu(z)
+    assert relerr(out.cpu(), z.detach()) < 1e-2
+    torch.testing.assert_close(mean.cpu(), y.mean(0), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rm.cpu(), 0.1 * y.mean(0), rtol=1e-4, atol=1e-4)
+    dout = rb(torch.randn(M, C))
+    dg, db = torch.empty(C, device=cuda), torch.empty(C, device=cuda)
+    dy, dres = ops.bn_bwd(dout.to(cuda, torch.bfloat16), out, y.to(cuda, torch.bfloat16), g.to(cuda), mean, invstd,
+                          relu, res, dg, db)
+    gr = torch.autograd.grad(z, [yr], dout)[0]
+    # dgamma / dbeta reference
+    yh = (y - y.mean(0)) / torch.sqrt(y.var(0, unbiased=False) + 1e-5)
+    mask = (z.detach() > 0).float() if relu else torch.ones_like(y)
+    dz = dout * mask
+    assert relerr(dy.cpu(), gr) < 2e-2
+    assert relerr(db.cpu(), dz.sum(0)) < 1e-3 and relerr(dg.cpu(), (dz * yh).sum(0)) < 1e-2
+    if res:
+        assert relerr(dres.cpu(), dz) < 1e-2
+
+
+def test_maxpool_avgpool(cuda):
+    torch.manual_seed(3)
+    x = rb(torch.randn(2, 11, 9, 16))
+    y, am = ops.maxpool2d_fwd(x.to(cuda, torch.bfloat16), 3, 2, 1)
+    xr = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert torch.equal(y.cpu().float().permute(0, 3, 1, 2), yr.detach())
+    dy = rb(torch.randn_like(yr))
+    yr.backward(dy)
+    dx = ops.maxpool2d_bwd(dy.permute(0, 2, 3, 1).contiguous().to(cuda, torch.bfloat16), am, [2, 11, 9, 16], 3, 2, 1)
+    assert relerr(dx.cpu().permute(0, 3, 1, 2), xr.grad) < 1e-2
+    a = ops.avgpool_fwd(x.to(cuda, torch.bfloat16))
+    assert relerr(a.cpu(), x.mean((1, 2))) < 1e-2
+    da = ops.avgpool_bwd(rb(torch.ones(2, 16)).to(cuda, torch.bfloat16), [2, 11, 9, 16])
+    assert torch.allclose(da.cpu().float(), torch.full((2, 11, 9, 16), 1 / 99.0), rtol=1e-2)
+
+
+def test_softmax_xent_and_pad(cuda):
+    torch.manual_seed(4)
+    z = torch.randn(5, 1000) * 3
+    lab = torch.randint(0, 1000, (5,), dtype=torch.int32)
+    loss, corr, dl = ops.softmax_xent(z.to(cuda), lab.to(cuda))
+    zr = z.clone().requires_grad_(True)
+    lr = F.cross_entropy(zr, lab.long(), reduction="none")
+    lr.mean().backward()
+    torch.testing.assert_close(loss.cpu(), lr.detach(), rtol=1e-4, atol=1e-4)
+    assert relerr(dl.cpu().float(), zr.grad) < 1e-2
+    assert torch.equal(corr.cpu(), (z.argmax(1) == lab.long()).float())
+    x = torch.randn(2, 4, 4, 3)
+    p = ops.pad_channels(x.to(cuda), 8)
+    assert p.shape == (2, 4, 4, 8) and torch.equal(p.cpu()[..., :3].float(), rb(x)) and p[..., 3:].abs().sum() == 0
