@@ -1,0 +1,394 @@
+"""ResNet-18 / ResNet-50 (v1.5, NHWC, bf16) on the native HIP kernel library -- the convnet
+configs of BASELINE.json (4: synthetic 224x224x3 ResNet-18-style DP=8; 5: synthetic-ImageNet
+ResNet-50 bf16 DP=8 with bucketed gradient all-reduce overlapped with backward).
+
+Execution model (MI355X-first, not a framework-module port):
+
+* Every trainable tensor lives in ONE flat fp32 master buffer with a bf16 shadow (the MFMA
+  operand) and ONE flat fp32 gradient buffer, laid out in *reverse* forward order, so the backward
+  pass fills the gradient buffer front to back and gradient buckets are contiguous ranges.
+* Activations flow through ``torch.autograd`` only for bookkeeping; every op is a native kernel
+  (``torch.ops.tfd.conv2d_* / bn_* / maxpool2d_* / linear_* / softmax_xent``). Weight gradients
+  are written straight into their slice of the flat gradient buffer from inside the backward, and
+  each write marks the parameter ready in the :class:`BucketReducer`, which launches that bucket's
+  all-reduce on a dedicated communication stream as soon as the bucket is complete (overlap with
+  the rest of the backward), exactly the bucket/backward overlap of config 5.
+* One fused flat optimizer kernel (SGD-momentum by default, Adam available) updates master +
+  shadow. The whole step can be captured into a hipGraph with ``torch.cuda.graph``.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+ops = None
+
+
+def _ops():
+    global ops
+    if ops is None:
+        from .. import _native
+
+        _native.require()
+        ops = torch.ops.tfd
+    return ops
+
+
+# ----------------------------------------------------------------------------- parameters
+@dataclass
+class PSpec:
+    name: str
+    shape: Tuple[int, ...]
+    init: str  # "he" (conv/linear weight), "ones", "zeros"
+    fan_in: int = 1
+    offset: int = 0
+
+    @property
+    def numel(self) -> int:
+        return int(math.prod(self.shape))
+
+
+class FlatParams:
+    """Flat master/shadow/grad buffers; slots padded to 64 elements (256-B aligned views)."""
+
+    def __init__(self, specs: List[PSpec], device, seed: int = 0):
+        self.specs = specs
+        off = 0
+        for s in reversed(specs):  # reverse forward order == backward production order
+            s.offset = off
+            off += (s.numel + 63) // 64 * 64
+        self.total = off
+        self.device = device
+        self.master = torch.zeros(off, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=device)
+        self.momentum = torch.zeros(off, dtype=torch.float32, device=device)
+        self.by_name: Dict[str, PSpec] = {s.name: s for s in specs}
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        for s in specs:
+            v = self.view(self.master, s)
+            if s.init == "he":
+                v.copy_((torch.randn(s.shape, generator=g) * math.sqrt(2.0 / s.fan_in)).to(device))
+            elif s.init == "ones":
+                v.fill_(1.0)
+            else:
+                v.zero_()
+        self.shadow = self.master.to(torch.bfloat16)
+
+    def view(self, buf: torch.Tensor, s: PSpec) -> torch.Tensor:
+        return buf[s.offset:s.offset + s.numel].view(s.shape)
+
+    def w(self, name: str) -> torch.Tensor:  # bf16 operand
+        return self.view(self.shadow, self.by_name[name])
+
+    def p(self, name: str) -> torch.Tensor:  # fp32 master
+        return self.view(self.master, self.by_name[name])
+
+    def g(self, name: str) -> torch.Tensor:  # fp32 grad slot
+        return self.view(self.grad, self.by_name[name])
+
+
+# ----------------------------------------------------------------------------- bucketed reducer
+class BucketReducer:
+    """Contiguous gradient buckets of ~``bucket_bytes``; a bucket's all-reduce is launched on the
+    comm stream the moment its last parameter gradient has been written (backward overlap)."""
+
+    def __init__(self, fp: FlatParams, comm=None, bucket_bytes: int = 8 << 20, bf16: bool = False):
+        self.fp = fp
+        self.comm = comm
+        self.world = comm.world() if comm is not None else 1
+        self.buckets: List[Tuple[int, int]] = []
+        self.bucket_of: Dict[str, int] = {}
+        cur_lo, cur_n = 0, 0
+        order = list(reversed(fp.specs))  # flat-buffer order
+        for s in order:
+            if cur_n and (s.offset + s.numel - cur_lo) * 4 > bucket_bytes:
+                self.buckets.append((cur_lo, s.offset))
+                cur_lo, cur_n = s.offset, 0
+            self.bucket_of[s.name] = len(self.buckets)
+            cur_n += 1
+        self.buckets.append((cur_lo, fp.total))
+        self.need = [0] * len(self.buckets)
+        for s in fp.specs:
+            self.need[self.bucket_of[s.name]] += 1
+        self.count = [0] * len(self.buckets)
+        self.stream = torch.cuda.Stream(fp.device) if (comm is not None and self.world > 1) else None
+        self.events = []
+        self.launched = 0
+
+    def reset(self):
+        self.count = [0] * len(self.buckets)
+        self.events = []
+        self.launched = 0
+
+    def mark_ready(self, name: str):
+        b = self.bucket_of[name]
+        self.count[b] += 1
+        if self.count[b] == self.need[b] and self.stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.fp.device))
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(ev)
+                lo, hi = self.buckets[b]
+                self.comm.all_reduce(self.fp.grad[lo:hi], "sum")
+            self.launched += 1
+
+    def finish(self):
+        if self.stream is not None:
+            torch.cuda.current_stream(self.fp.device).wait_stream(self.stream)
+
+
+# ----------------------------------------------------------------------------- autograd ops
+class _Conv(torch.autograd.Function):
+    # `token` is a 0-d tensor that requires grad: weights are not autograd leaves (their gradients
+    # go straight into the flat buffer), so the stem needs it to put the graph on the tape.
+    @staticmethod
+    def forward(ctx, x, token, layer):
+        ctx.layer = layer
+        ctx.save_for_backward(x)
+        return _ops().conv2d_fwd(x, layer.w(), layer.stride, layer.pad)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        L = ctx.layer
+        dy = dy.contiguous()
+        _ops().conv2d_wgrad(x, dy, L.g(), L.stride, L.pad)
+        L.model.reducer.mark_ready(L.name)
+        dx = _ops().conv2d_dgrad(dy, L.w(), list(x.shape), L.stride, L.pad) if ctx.needs_input_grad[0] else None
+        return dx, None, None
+
+
+class _BN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, res, layer, relu):
+        out, mean, invstd = _ops().bn_fwd(y, layer.gamma(), layer.beta(), res, relu, layer.rmean, layer.rvar,
+                                          layer.momentum, layer.eps)
+        ctx.layer, ctx.relu, ctx.has_res = layer, relu, res is not None
+        ctx.save_for_backward(y, out, mean, invstd)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, out, mean, invstd = ctx.saved_tensors
+        L = ctx.layer
+        dy, dres = _ops().bn_bwd(dout.contiguous(), out, y, L.gamma(), mean, invstd, ctx.relu, ctx.has_res,
+                                 L.g_gamma(), L.g_beta())
+        L.model.reducer.mark_ready(L.name + "/gamma")
+        L.model.reducer.mark_ready(L.name + "/beta")
+        return dy, (dres if ctx.has_res else None), None, None
+
+
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, st, pad):
+        y, am = _ops().maxpool2d_fwd(x, k, st, pad)
+        ctx.save_for_backward(am)
+        ctx.cfg = (list(x.shape), k, st, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (am,) = ctx.saved_tensors
+        xs, k, st, pad = ctx.cfg
+        return _ops().maxpool2d_bwd(dy.contiguous(), am, xs, k, st, pad), None, None, None
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.xs = list(x.shape)
+        return _ops().avgpool_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _ops().avgpool_bwd(dy.contiguous(), ctx.xs)
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, layer):
+        ctx.layer = layer
+        ctx.save_for_backward(x)
+        return _ops().linear_fwd(x, layer.w(), layer.bias())
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        (x,) = ctx.saved_tensors
+        L = ctx.layer
+        dl = dlogits.to(torch.bfloat16).contiguous()
+        _ops().linear_wgrad(x, dl, L.g())
+        torch.sum(dlogits.float(), 0, out=L.g_bias())
+        L.model.reducer.mark_ready(L.name)
+        L.model.reducer.mark_ready(L.name + "/bias")
+        return _ops().linear_dgrad(dl, L.w()), None
+
+
+class _SoftmaxXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels):
+        loss_rows, correct, dl = _ops().softmax_xent(logits.contiguous(), labels)
+        ctx.save_for_backward(dl)
+        ctx.mark_non_differentiable(correct)
+        return loss_rows.mean(), correct
+
+    @staticmethod
+    def backward(ctx, dloss, _dcorrect):
+        (dl,) = ctx.saved_tensors
+        return dl.float() * dloss, None  # dl already carries the 1/N of the mean
+
+
+# ----------------------------------------------------------------------------- layers
+class ConvLayer:
+    def __init__(self, model, name, cin, cout, k, stride, pad):
+        self.model, self.name, self.stride, self.pad = model, name, stride, pad
+        model.specs.append(PSpec(name, (k, k, cin, cout), "he", fan_in=k * k * cin))
+
+    def w(self):
+        return self.model.fp.w(self.name)
+
+    def g(self):
+        return self.model.fp.g(self.name)
+
+    def __call__(self, x):
+        return _Conv.apply(x, self.model.token, self)
+
+
+class BNLayer:
+    def __init__(self, model, name, c, zero_init=False):
+        self.model, self.name, self.c = model, name, c
+        self.momentum, self.eps = 0.9, 1e-5
+        model.specs.append(PSpec(name + "/gamma", (c,), "zeros" if zero_init else "ones"))
+        model.specs.append(PSpec(name + "/beta", (c,), "zeros"))
+        model.bns.append(self)
+
+    def gamma(self):
+        return self.model.fp.p(self.name + "/gamma")
+
+    def beta(self):
+        return self.model.fp.p(self.name + "/beta")
+
+    def g_gamma(self):
+        return self.model.fp.g(self.name + "/gamma")
+
+    def g_beta(self):
+        return self.model.fp.g(self.name + "/beta")
+
+    def __call__(self, y, relu=True, res=None):
+        return _BN.apply(y, res, self, relu)
+
+
+class LinearLayer:
+    def __init__(self, model, name, cin, cout):
+        self.model, self.name = model, name
+        model.specs.append(PSpec(name, (cin, cout), "he", fan_in=cin))
+        model.specs.append(PSpec(name + "/bias", (cout,), "zeros"))
+
+    def w(self):
+        return self.model.fp.w(self.name)
+
+    def bias(self):
+        return self.model.fp.p(self.name + "/bias")
+
+    def g(self):
+        return self.model.fp.g(self.name)
+
+    def g_bias(self):
+        return self.model.fp.g(self.name + "/bias")
+
+    def __call__(self, x):
+        return _Linear.apply(x, self)
+
+
+# ----------------------------------------------------------------------------- model
+class ResNet:
+    """ResNet-{18,34,50,101} v1.5, NHWC, input fp32 [N,H,W,3] (padded to 8 channels on device)."""
+
+    CFG = {18: ("basic", [2, 2, 2, 2]), 34: ("basic", [3, 4, 6, 3]), 50: ("bottleneck", [3, 4, 6, 3]),
+           101: ("bottleneck", [3, 4, 23, 3])}
+
+    def __init__(self, depth: int = 50, num_classes: int = 1000, device=None, seed: int = 0, width: int = 64,
+                 zero_init_residual: bool = True):
+        kind, blocks = self.CFG[depth]
+        if num_classes % 8 or width % 8:
+            raise ValueError("num_classes and width must be multiples of 8 (16-byte MFMA operand chunks)")
+        self.depth, self.kind, self.num_classes = depth, kind, num_classes
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.specs: List[PSpec] = []
+        self.bns: List[BNLayer] = []
+        self.stem = ConvLayer(self, "conv1", 8, width, 7, 2, 3)
+        self.stem_bn = BNLayer(self, "bn1", width)
+        self.blocks = []
+        cin = width
+        exp = 4 if kind == "bottleneck" else 1
+        for li, nb in enumerate(blocks):
+            w = width * (2 ** li)
+            for bi in range(nb):
+                st = 2 if (bi == 0 and li > 0) else 1
+                nm = f"layer{li + 1}.{bi}"
+                blk = {}
+                if kind == "basic":
+                    blk["c1"], blk["b1"] = ConvLayer(self, nm + ".conv1", cin, w, 3, st, 1), BNLayer(self, nm + ".bn1", w)
+                    blk["c2"], blk["b2"] = ConvLayer(self, nm + ".conv2", w, w, 3, 1, 1), BNLayer(self, nm + ".bn2", w, zero_init_residual)
+                    cout = w
+                else:
+                    blk["c1"], blk["b1"] = ConvLayer(self, nm + ".conv1", cin, w, 1, 1, 0), BNLayer(self, nm + ".bn1", w)
+                    blk["c2"], blk["b2"] = ConvLayer(self, nm + ".conv2", w, w, 3, st, 1), BNLayer(self, nm + ".bn2", w)
+                    blk["c3"], blk["b3"] = (ConvLayer(self, nm + ".conv3", w, w * exp, 1, 1, 0),
+                                            BNLayer(self, nm + ".bn3", w * exp, zero_init_residual))
+                    cout = w * exp
+                if st != 1 or cin != cout:
+                    blk["cd"] = ConvLayer(self, nm + ".downsample", cin, cout, 1, st, 0)
+                    blk["bd"] = BNLayer(self, nm + ".downsample_bn", cout)
+                self.blocks.append(blk)
+                cin = cout
+        self.fc = LinearLayer(self, "fc", cin, num_classes)
+        self.fp = FlatParams(self.specs, self.device, seed)
+        for bn in self.bns:
+            bn.rmean = torch.zeros(bn.c, device=self.device)
+            bn.rvar = torch.ones(bn.c, device=self.device)
+        self.reducer = BucketReducer(self.fp)
+        self.token = torch.zeros((), device=self.device, requires_grad=True)
+
+    @property
+    def num_params(self) -> int:
+        return sum(s.numel for s in self.specs)
+
+    def set_comm(self, comm, bucket_mb: float = 8.0):
+        self.reducer = BucketReducer(self.fp, comm, int(bucket_mb * (1 << 20)))
+
+    def forward(self, x_nhwc_f32: torch.Tensor) -> torch.Tensor:
+        x = _ops().pad_channels(x_nhwc_f32, 8)
+        x = self.stem_bn(self.stem(x))
+        x = _MaxPool.apply(x, 3, 2, 1)
+        for blk in self.blocks:
+            sc = x
+            if "cd" in blk:
+                sc = blk["bd"](blk["cd"](x), relu=False)
+            if self.kind == "basic":
+                h = blk["b1"](blk["c1"](x))
+                x = blk["b2"](blk["c2"](h), relu=True, res=sc)
+            else:
+                h = blk["b1"](blk["c1"](x))
+                h = blk["b2"](blk["c2"](h))
+                x = blk["b3"](blk["c3"](h), relu=True, res=sc)
+        x = _AvgPool.apply(x)
+        return self.fc(x)
+
+    def loss(self, x, labels):
+        logits = self.forward(x)
+        loss, correct = _SoftmaxXent.apply(logits, labels)
+        return loss, correct
+
+    def train_step(self, x, labels, lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 1e-4):
+        """fwd + bwd (bucketed all-reduce overlapped) + fused flat SGD-momentum. Returns loss tensor."""
+        self.reducer.reset()
+        loss, _ = self.loss(x, labels)
+        loss.backward()
+        self.reducer.finish()
+        scale = 1.0 / self.reducer.world
+        _ops().momentum_flat(self.fp.master, self.fp.momentum, self.fp.grad, self.fp.shadow, lr, momentum,
+                             weight_decay, False, scale)
+        return loss.detach()

@@ -1,0 +1,171 @@
+"""ResNet on the native kernel library: forward/backward against a pure-PyTorch fp32 reference
+with the same weights (bf16-rounded), and a few SGD steps reduce the loss."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+class _RB(torch.autograd.Function):
+    """Round to bf16 in forward AND backward: where the native kernels store bf16 tensors."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+def _ref_forward(model, x, labels):
+    """Pure PyTorch fp32 ResNet with the model's weights (NCHW), training-mode BN."""
+    fp = model.fp
+    P = {}
+
+    def W(name):  # HWIO bf16 -> OIHW fp32 leaf
+        if name not in P:
+            P[name] = fp.w(name).float().cpu().permute(3, 2, 0, 1).contiguous().requires_grad_(True)
+        return P[name]
+
+    def V(name):
+        if name not in P:
+            P[name] = fp.p(name).float().cpu().clone().requires_grad_(True)
+        return P[name]
+
+    def conv(x, L):
+        return _RB.apply(F.conv2d(x, W(L.name), stride=L.stride, padding=L.pad))
+
+    def bn(y, L, relu=True, res=None):
+        z = F.batch_norm(y, None, None, V(L.name + "/gamma"), V(L.name + "/beta"), training=True, eps=1e-5)
+        if res is not None:
+            z = z + res
+        return _RB.apply(torch.relu(z) if relu else z)
+
+    h = F.pad(x.permute(0, 3, 1, 2), (0, 0, 0, 0, 0, 5))  # 3 -> 8 channels
+    h = bn(conv(h, model.stem), model.stem_bn)
+    h = F.max_pool2d(h, 3, 2, 1)
+    for blk in model.blocks:
+        sc = h
+        if "cd" in blk:
+            sc = bn(conv(h, blk["cd"]), blk["bd"], relu=False)
+        if model.kind == "basic":
+            t = bn(conv(h, blk["c1"]), blk["b1"])
+            h = bn(conv(t, blk["c2"]), blk["b2"], True, sc)
+        else:
+            t = bn(conv(h, blk["c1"]), blk["b1"])
+            t = bn(conv(t, blk["c2"]), blk["b2"])
+            h = bn(conv(t, blk["c3"]), blk["b3"], True, sc)
+    h = _RB.apply(h.mean((2, 3)))
+    wfc = fp.w("fc").float().cpu().requires_grad_(True)
+    P["fc"] = wfc
+    logits = h @ wfc + V("fc/bias")
+    return F.cross_entropy(logits, labels.long()), P
+
+
+@pytest.mark.parametrize("depth", [18, 50])
+def test_resnet_end_to_end_loss_and_head(cuda, depth):
+    """Whole network: loss and the fc gradient agree with the fp32 reference. (Deep gradients are
+    checked block by block below: end to end, train-mode BN over tiny M amplifies bf16 rounding.)"""
+    from tensorflow_distributed_amd.models.resnet import ResNet
+
+    torch.manual_seed(0)
+    m = ResNet(depth, num_classes=16, device=cuda, seed=1, width=16, zero_init_residual=False)
+    x = torch.randn(4, 64, 64, 3)
+    lab = torch.randint(0, 16, (4,), dtype=torch.int32)
+    loss, _ = m.loss(x.to(cuda), lab.to(cuda))
+    loss.backward()
+    torch.cuda.synchronize()
+    lref, P = _ref_forward(m, x.to(torch.bfloat16).float(), lab)
+    lref.backward()
+    assert abs(loss.item() - lref.item()) / lref.item() < 3e-2, (loss.item(), lref.item())
+    cos = torch.nn.functional.cosine_similarity(m.fp.g("fc").cpu().flatten(), P["fc"].grad.flatten(), dim=0).item()
+    assert cos > 0.99, cos
+
+
+@pytest.mark.parametrize("depth,bi,hw", [(50, 0, 16), (50, 1, 16), (50, 3, 16), (50, 13, 4), (18, 0, 16), (18, 2, 16)])
+def test_resnet_block_forward_backward(cuda, depth, bi, hw):
+    """One residual block from identical inputs: output, dX and every weight/BN gradient."""
+    from tensorflow_distributed_amd.models.resnet import ResNet
+
+    torch.manual_seed(bi)
+    m = ResNet(depth, num_classes=16, device=cuda, seed=1, width=16, zero_init_residual=False)
+    blk = m.blocks[bi]
+    cin = m.fp.by_name[blk["c1"].name].shape[2]
+    x = torch.randn(4, hw, hw, cin).to(torch.bfloat16).float()
+    xn = x.to(cuda, torch.bfloat16).requires_grad_(True)
+    sc = blk["bd"](blk["cd"](xn), relu=False) if "cd" in blk else xn
+    if m.kind == "basic":
+        out = blk["b2"](blk["c2"](blk["b1"](blk["c1"](xn))), relu=True, res=sc)
+    else:
+        t = blk["b2"](blk["c2"](blk["b1"](blk["c1"](xn))))
+        out = blk["b3"](blk["c3"](t), relu=True, res=sc)
+    g = torch.randn(out.shape).to(torch.bfloat16).float()
+    out.backward(g.to(cuda, torch.bfloat16))
+    torch.cuda.synchronize()
+    Ws = {k: m.fp.w(L.name).float().cpu().permute(3, 2, 0, 1).clone().requires_grad_(True)
+          for k, L in blk.items() if k.startswith("c")}
+    Gs = {k: [m.fp.p(L.name + s).cpu().clone().requires_grad_(True) for s in ("/gamma", "/beta")]
+          for k, L in blk.items() if k.startswith("b")}
+
+    def conv(h, k):
+        return _RB.apply(F.conv2d(h, Ws[k], stride=blk[k].stride, padding=blk[k].pad))
+
+    def bn(y, k, relu=True, res=None):
+        z = F.batch_norm(y, None, None, Gs[k][0], Gs[k][1], training=True, eps=1e-5)
+        z = z + res if res is not None else z
+        return _RB.apply(torch.relu(z) if relu else z)
+
+    xr = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    scr = bn(conv(xr, "cd"), "bd", relu=False) if "cd" in blk else xr
+    if m.kind == "basic":
+        outr = bn(conv(bn(conv(xr, "c1"), "b1"), "c2"), "b2", True, scr)
+    else:
+        outr = bn(conv(bn(conv(bn(conv(xr, "c1"), "b1"), "c2"), "b2"), "c3"), "b3", True, scr)
+    outr.backward(g.permute(0, 3, 1, 2))
+
+    def cos(a, b):
+        return torch.nn.functional.cosine_similarity(a.flatten().float(), b.flatten().float(), dim=0).item()
+
+    checks = {"out": cos(out.detach().cpu().permute(0, 3, 1, 2), outr), "dx": cos(xn.grad.cpu().permute(0, 3, 1, 2), xr.grad)}
+    for k, L in blk.items():
+        if k.startswith("c"):
+            checks[k] = cos(m.fp.g(L.name).cpu(), Ws[k].grad.permute(2, 3, 1, 0))
+        else:
+            checks[k + "/gamma"] = cos(m.fp.g(L.name + "/gamma").cpu(), Gs[k][0].grad)
+            checks[k + "/beta"] = cos(m.fp.g(L.name + "/beta").cpu(), Gs[k][1].grad)
+    assert all(v > 0.999 for v in checks.values()), checks
+
+
+def test_resnet_training_reduces_loss(cuda):
+    from tensorflow_distributed_amd.models.resnet import ResNet
+
+    torch.manual_seed(0)
+    m = ResNet(18, num_classes=16, device=cuda, seed=2, width=16)
+    x = torch.randn(16, 32, 32, 3, device=cuda)
+    lab = torch.randint(0, 16, (16,), dtype=torch.int32, device=cuda)
+    losses = [m.train_step(x, lab, lr=0.05).item() for _ in range(15)]
+    assert losses[-1] < 0.5 * losses[0], losses
+
+
+def test_resnet_graph_capture(cuda):
+    from tensorflow_distributed_amd.models.resnet import ResNet
+
+    m = ResNet(18, num_classes=16, device=cuda, seed=3, width=16)
+    x = torch.randn(8, 32, 32, 3, device=cuda)
+    lab = torch.randint(0, 16, (8,), dtype=torch.int32, device=cuda)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            m.train_step(x, lab, lr=0.01)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = m.train_step(x, lab, lr=0.01)
+    vals = []
+    for _ in range(3):
+        g.replay()
+        vals.append(out.item())
+    assert all(v == v for v in vals) and vals[-1] < vals[0] + 1.0
