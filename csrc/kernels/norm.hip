@@ -21,7 +21,7 @@ RowSplit row_split(int M, int C) {
   RowSplit r;
   r.tpr = C / 8;
   r.rg = NT / r.tpr;
-  r.nblk = std::max(1, std::min(1024, (M + 63) / 64));
+  r.nblk = std::max(1, std::min(1024, (M + 31) / 32));
   r.rb = (M + r.nblk - 1) / r.nblk;
   r.nblk = (M + r.rb - 1) / r.rb;
   return r;
@@ -93,18 +93,35 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(int mode, const uint16_t
   }
 }
 
-// per-channel finalize. mode 0: mean/invstd (+running stats); mode 1: dbeta/dgamma.
+// per-channel finalize, block = 32 channels x 8 partial-row groups (coalesced 128-B rows, fixed
+// summation order). mode 0: mean/invstd (+running stats); mode 1: dbeta/dgamma.
 __global__ __launch_bounds__(NT) void bn_final_kernel(int mode, const float* __restrict__ part, int nblk, int M,
                                                       int C, float eps, float momentum, float* __restrict__ o0,
                                                       float* __restrict__ o1, float* __restrict__ rmean,
                                                       float* __restrict__ rvar) {
-  const int c = blockIdx.x * NT + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float red[2][8][33];
+  const int cl = threadIdx.x & 31, q = threadIdx.x >> 5, c = blockIdx.x * 32 + cl;
   float a = 0.f, b = 0.f;
-  for (int k = 0; k < nblk; ++k) {
-    a += part[(size_t)k * 2 * C + c];
-    b += part[(size_t)k * 2 * C + C + c];
+  if (c < C) {
+    int k = q;
+    for (; k + 24 < nblk; k += 32) {
+      const float* p0 = part + (size_t)k * 2 * C + c;
+      a += (p0[0] + p0[(size_t)8 * 2 * C]) + (p0[(size_t)16 * 2 * C] + p0[(size_t)24 * 2 * C]);
+      b += (p0[C] + p0[(size_t)8 * 2 * C + C]) + (p0[(size_t)16 * 2 * C + C] + p0[(size_t)24 * 2 * C + C]);
+    }
+    for (; k < nblk; k += 8) {
+      a += part[(size_t)k * 2 * C + c];
+      b += part[(size_t)k * 2 * C + C + c];
+    }
   }
+  red[0][q][cl] = a;
+  red[1][q][cl] = b;
+  __syncthreads();
+  if (q != 0 || c >= C) return;
+  a = 0.f;
+  b = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { a += red[0][j][cl]; b += red[1][j][cl]; }
   if (mode == 0) {
     const float mu = a / (float)M;
     const float var = fmaxf(b / (float)M - mu * mu, 0.f);
@@ -120,25 +137,35 @@ __global__ __launch_bounds__(NT) void bn_final_kernel(int mode, const float* __r
   }
 }
 
+// Elementwise passes walk the same row split as the partial kernel: thread = (8-channel chunk,
+// row group); its 8 channels' constants stay in registers for every row it touches.
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, const float* __restrict__ mean,
                                                       const float* __restrict__ invstd,
                                                       const uint16_t* __restrict__ res, int relu,
-                                                      uint16_t* __restrict__ out, int64_t nchunks, int C) {
-  const int64_t stride = (int64_t)gridDim.x * NT;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < nchunks; i += stride) {
-    const int c0 = (int)((i * 8) % C);
+                                                      uint16_t* __restrict__ out, int M, int C, int tpr, int rg, int rb) {
+  const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
+  if (g >= rg) return;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = invstd[c0 + j] * gamma[c0 + j];
+    sh[j] = beta[c0 + j] - mean[c0 + j] * sc[j];
+  }
+  const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
+  for (int r = r0 + g; r < r1; r += rg) {
+    const size_t o = (size_t)r * C + c0;
     float v[8];
-    unpack8(reinterpret_cast<const uint4*>(y)[i], v);
-    float r[8];
-    if (res) unpack8(reinterpret_cast<const uint4*>(res)[i], r);
+    unpack8(*reinterpret_cast<const uint4*>(y + o), v);
+    float q[8];
+    if (res) unpack8(*reinterpret_cast<const uint4*>(res + o), q);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float z = (v[j] - mean[c0 + j]) * invstd[c0 + j] * gamma[c0 + j] + beta[c0 + j];
-      if (res) z += r[j];
+      float z = fmaf(v[j], sc[j], sh[j]);
+      if (res) z += q[j];
       v[j] = relu ? fmaxf(z, 0.f) : z;
     }
-    reinterpret_cast<uint4*>(out)[i] = pack8(v);
+    *reinterpret_cast<uint4*>(out + o) = pack8(v);
   }
 }
 
@@ -148,28 +175,37 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __rest
                                                           const float* __restrict__ invstd, const float* __restrict__ dbeta,
                                                           const float* __restrict__ dgamma, int relu,
                                                           uint16_t* __restrict__ dy, uint16_t* __restrict__ dres,
-                                                          int64_t nchunks, int C, float invM) {
-  const int64_t stride = (int64_t)gridDim.x * NT;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < nchunks; i += stride) {
-    const int c0 = (int)((i * 8) % C);
+                                                          int M, int C, int tpr, int rg, int rb, float invM) {
+  const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
+  if (g >= rg) return;
+  // dy = k1 * dz + k2 * y + k3 with k1 = gamma*invstd, k2 = -k1*invstd*dgamma/M,
+  // k3 = -k1*(dbeta/M - mean*invstd^2*dgamma/M)
+  float k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    const float is = invstd[c];
+    k1[j] = gamma[c] * is;
+    k2[j] = -k1[j] * is * dgamma[c] * invM;
+    k3[j] = -k1[j] * (dbeta[c] * invM - mean[c] * is * dgamma[c] * invM);
+  }
+  const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
+  for (int r = r0 + g; r < r1; r += rg) {
+    const size_t o = (size_t)r * C + c0;
     float d[8], v[8];
-    unpack8(reinterpret_cast<const uint4*>(dout)[i], d);
-    unpack8(reinterpret_cast<const uint4*>(y)[i], v);
+    unpack8(*reinterpret_cast<const uint4*>(dout + o), d);
+    unpack8(*reinterpret_cast<const uint4*>(y + o), v);
     if (relu) {
       float ov[8];
-      unpack8(reinterpret_cast<const uint4*>(out)[i], ov);
+      unpack8(*reinterpret_cast<const uint4*>(out + o), ov);
 #pragma unroll
       for (int j = 0; j < 8; ++j) d[j] = ov[j] > 0.f ? d[j] : 0.f;
     }
-    if (dres) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
-    float o[8];
+    if (dres) *reinterpret_cast<uint4*>(dres + o) = pack8(d);
+    float w[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      const float xh = (v[j] - mean[c]) * invstd[c];
-      o[j] = gamma[c] * invstd[c] * (d[j] - (dbeta[c] + xh * dgamma[c]) * invM);
-    }
-    reinterpret_cast<uint4*>(dy)[i] = pack8(o);
+    for (int j = 0; j < 8; ++j) w[j] = fmaf(k1[j], d[j], fmaf(k2[j], v[j], k3[j]));
+    *reinterpret_cast<uint4*>(dy + o) = pack8(w);
   }
 }
 
@@ -351,10 +387,9 @@ void bn_forward(const uint16_t* y, const float* gamma, const float* beta, const 
   const RowSplit r = row_split(M, C);
   bn_partial_kernel<<<r.nblk, NT, 0, st>>>(0, y, nullptr, nullptr, 0, nullptr, nullptr, M, C, r.tpr, r.rg, r.rb,
                                            partials);
-  bn_final_kernel<<<(C + NT - 1) / NT, NT, 0, st>>>(0, partials, r.nblk, M, C, eps, momentum, mean, invstd,
-                                                    running_mean, running_var);
-  const int64_t nch = (int64_t)M * C / 8;
-  bn_apply_kernel<<<grid_for(nch), NT, 0, st>>>(y, gamma, beta, mean, invstd, residual, relu, out, nch, C);
+  bn_final_kernel<<<(C + 31) / 32, NT, 0, st>>>(0, partials, r.nblk, M, C, eps, momentum, mean, invstd,
+                                                running_mean, running_var);
+  bn_apply_kernel<<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r.tpr, r.rg, r.rb);
 }
 
 void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* mean,
@@ -362,11 +397,10 @@ void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, c
                  int C, float* partials, hipStream_t st) {
   const RowSplit r = row_split(M, C);
   bn_partial_kernel<<<r.nblk, NT, 0, st>>>(1, y, dout, out, relu, mean, invstd, M, C, r.tpr, r.rg, r.rb, partials);
-  bn_final_kernel<<<(C + NT - 1) / NT, NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,
-                                                    nullptr);
-  const int64_t nch = (int64_t)M * C / 8;
-  bn_bwd_apply_kernel<<<grid_for(nch), NT, 0, st>>>(dout, out, y, gamma, mean, invstd, dbeta, dgamma, relu, dy, dres,
-                                                    nch, C, 1.f / (float)M);
+  bn_final_kernel<<<(C + 31) / 32, NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,
+                                                nullptr);
+  bn_bwd_apply_kernel<<<r.nblk, NT, 0, st>>>(dout, out, y, gamma, mean, invstd, dbeta, dgamma, relu, dy, dres, M, C,
+                                             r.tpr, r.rg, r.rb, 1.f / (float)M);
 }
 
 void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,

@@ -102,9 +102,10 @@ class BucketReducer:
         self.buckets: List[Tuple[int, int]] = []
         self.bucket_of: Dict[str, int] = {}
         cur_lo, cur_n = 0, 0
+        elt = 2 if (bf16 and comm is not None and self.world > 1) else 4  # wire bytes per gradient
         order = list(reversed(fp.specs))  # flat-buffer order
         for s in order:
-            if cur_n and (s.offset + s.numel - cur_lo) * 4 > bucket_bytes:
+            if cur_n and (s.offset + s.numel - cur_lo) * elt > bucket_bytes:
                 self.buckets.append((cur_lo, s.offset))
                 cur_lo, cur_n = s.offset, 0
             self.bucket_of[s.name] = len(self.buckets)
@@ -117,6 +118,9 @@ class BucketReducer:
         self.stream = torch.cuda.Stream(fp.device) if (comm is not None and self.world > 1) else None
         self.events = []
         self.launched = 0
+        # bf16 wire format halves the all-reduce bytes; the optimizer reads the bf16 sums directly
+        self.bf16 = bf16 and self.stream is not None
+        self.gbf = torch.empty(fp.total, dtype=torch.bfloat16, device=fp.device) if self.bf16 else None
 
     def reset(self):
         self.count = [0] * len(self.buckets)
@@ -132,12 +136,19 @@ class BucketReducer:
             with torch.cuda.stream(self.stream):
                 self.stream.wait_event(ev)
                 lo, hi = self.buckets[b]
-                self.comm.all_reduce(self.fp.grad[lo:hi], "sum")
+                if self.bf16:
+                    self.gbf[lo:hi].copy_(self.fp.grad[lo:hi])
+                    self.comm.all_reduce(self.gbf[lo:hi], "sum")
+                else:
+                    self.comm.all_reduce(self.fp.grad[lo:hi], "sum")
             self.launched += 1
 
     def finish(self):
         if self.stream is not None:
             torch.cuda.current_stream(self.fp.device).wait_stream(self.stream)
+
+    def reduced_grads(self) -> torch.Tensor:
+        return self.gbf if self.bf16 else self.fp.grad
 
 
 # ----------------------------------------------------------------------------- autograd ops
@@ -356,8 +367,8 @@ class ResNet:
     def num_params(self) -> int:
         return sum(s.numel for s in self.specs)
 
-    def set_comm(self, comm, bucket_mb: float = 8.0):
-        self.reducer = BucketReducer(self.fp, comm, int(bucket_mb * (1 << 20)))
+    def set_comm(self, comm, bucket_mb: float = 8.0, bf16_grads: bool = True):
+        self.reducer = BucketReducer(self.fp, comm, int(bucket_mb * (1 << 20)), bf16=bf16_grads)
 
     def forward(self, x_nhwc_f32: torch.Tensor) -> torch.Tensor:
         x = _ops().pad_channels(x_nhwc_f32, 8)
@@ -389,6 +400,6 @@ class ResNet:
         loss.backward()
         self.reducer.finish()
         scale = 1.0 / self.reducer.world
-        _ops().momentum_flat(self.fp.master, self.fp.momentum, self.fp.grad, self.fp.shadow, lr, momentum,
-                             weight_decay, False, scale)
+        _ops().momentum_flat(self.fp.master, self.fp.momentum, self.reducer.reduced_grads(), self.fp.shadow, lr,
+                             momentum, weight_decay, False, scale)
         return loss.detach()
