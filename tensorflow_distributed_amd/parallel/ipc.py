@@ -26,3 +26,22 @@ def make_ipc_comm(rank: int, world: int, device_index: int, capacity_elems: int,
     else:
         comm.open(h.reshape(1, -1))
     return comm
+
+
+class IpcCollectives:
+    """RcclComm-shaped facade over IpcComm (``all_reduce(t, op)``, ``world()``, ``broadcast``) so
+    bucket reducers can run on the IPC transport, e.g. several ranks sharing one GPU in tests."""
+
+    def __init__(self, ipc):
+        self.ipc = ipc
+
+    def world(self) -> int:
+        return self.ipc.world()
+
+    def rank(self) -> int:
+        return self.ipc.rank()
+
+    def all_reduce(self, t, op: str = "sum") -> None:
+        if op not in ("sum", "avg", "mean"):
+            raise ValueError(f"IpcCollectives: unsupported op {op}")
+        self.ipc.all_reduce(t, 1.0 if op == "sum" else 1.0 / self.ipc.world())

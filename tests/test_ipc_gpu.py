@@ -121,3 +121,52 @@ def test_engine_dp_over_ipc_matches_single_rank_big_batch(cuda):
     dr = ref - M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()})
     cos = torch.nn.functional.cosine_similarity(d, dr, dim=0).item()
     assert cos > 0.99, cos  # bf16 gradient all-reduce vs one big-batch step: same update direction
+
+
+def _resnet_dp_worker(rank, world, steps):
+    from tensorflow_distributed_amd.models.resnet import ResNet
+    from tensorflow_distributed_amd.parallel.ipc import IpcCollectives, make_ipc_comm
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    m = ResNet(18, num_classes=16, device=dev, seed=5, width=16)
+    comm = make_ipc_comm(rank, world, 0, m.fp.total)
+    m.set_comm(IpcCollectives(comm), bucket_mb=0.25, bf16_grads=False)
+    nb = len(m.reducer.buckets)
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(steps, world * 4, 32, 32, 3, generator=g)
+    y = torch.randint(0, 16, (steps, world * 4), generator=g, dtype=torch.int32)
+    losses = []
+    for i in range(steps):
+        losses.append(m.train_step(x[i, rank * 4:(rank + 1) * 4].to(dev), y[i, rank * 4:(rank + 1) * 4].to(dev),
+                                   lr=0.05).item())
+    torch.cuda.synchronize()
+    out = m.fp.master.cpu(), losses, comm.error(), nb, m.reducer.launched
+    comm.close()
+    return out
+
+
+def test_resnet_bucketed_dp_over_ipc(cuda):
+    """Two ranks on one GPU: bucketed all-reduce overlapped with the backward keeps replicas
+    identical and equals manual averaging of the two half-batch gradients."""
+    from tensorflow_distributed_amd.models.resnet import ResNet
+
+    steps, world = 3, 2
+    res = run_ranks(_resnet_dp_worker, world, steps, timeout=300)
+    (p0, l0, e0, nb, launched), (p1, l1, e1, _, _) = res
+    assert e0 == e1 == 0 and nb > 2 and launched == nb
+    assert torch.equal(p0, p1)
+    m = ResNet(18, num_classes=16, device=cuda, seed=5, width=16)
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(steps, world * 4, 32, 32, 3, generator=g)
+    y = torch.randint(0, 16, (steps, world * 4), generator=g, dtype=torch.int32)
+    for i in range(steps):
+        acc = torch.zeros_like(m.fp.grad)
+        for r in range(world):
+            m.reducer.reset()
+            loss, _ = m.loss(x[i, r * 4:(r + 1) * 4].to(cuda), y[i, r * 4:(r + 1) * 4].to(cuda))
+            loss.backward()
+            acc += m.fp.grad
+        torch.ops.tfd.momentum_flat(m.fp.master, m.fp.momentum, acc, m.fp.shadow, 0.05, 0.9, 1e-4, False, 0.5)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(p0, m.fp.master.cpu(), rtol=1e-4, atol=1e-5)
