@@ -14,7 +14,7 @@ namespace tfd {
 constexpr int kIpcMaxRanks = 8;
 constexpr int kIpcMaxBlocks = 64;
 // signal region layout (int32): [2 phases][kIpcMaxBlocks][kIpcMaxRanks] flags, then
-// [kIpcMaxBlocks] per-block epochs (local), then 1 error word.
+// [kIpcMaxBlocks] reserved words, then the sticky error word and the call counter.
 constexpr int kIpcSigFlags = 2 * kIpcMaxBlocks * kIpcMaxRanks;
 constexpr int kIpcSigInts = kIpcSigFlags + kIpcMaxBlocks + 4;
 
@@ -31,5 +31,9 @@ struct IpcAllReduceArgs {
 };
 
 void ipc_allreduce(const IpcAllReduceArgs& a, int blocks, hipStream_t s);
+// n = shard size S. reduce-scatter: in = N*S local elements, out = this rank's S-element shard.
+void ipc_reduce_scatter(const IpcAllReduceArgs& a, int blocks, hipStream_t s);
+// all-gather in place: out = N*S elements of elem_bytes (2 or 4) with this rank's shard at rank*S.
+void ipc_all_gather(const IpcAllReduceArgs& a, int elem_bytes, int blocks, hipStream_t s);
 
 }  // namespace tfd

@@ -827,6 +827,11 @@ int mnist_wg2_splits(int B) {
 }
 
 void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s) {
+  mnist_forward_conv(a, s);
+  mnist_forward_fc(a, train, s);
+}
+
+void mnist_forward_conv(const MnistStepArgs& a, hipStream_t s) {
   const int B = a.B;
   conv1_pool_fwd<<<4 * B, 256, 0, s>>>(a);
 #if TFD_CONV2_LDS
@@ -839,6 +844,10 @@ void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s) {
     conv2_pool_fwd<<<(B * 196 + C2F_BM - 1) / C2F_BM, 256, sm, s>>>(a);
   }
 #endif
+}
+
+void mnist_forward_fc(const MnistStepArgs& a, bool train, hipStream_t s) {
+  const int B = a.B;
   {
     constexpr int sm = GemmSmem<FC1_BM, FC1_BN, FC1_BK, DenseLoader<true>, DenseLoader<false>>::BYTES;
     set_smem<fc1_fwd>(sm);

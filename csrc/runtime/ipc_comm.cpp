@@ -91,6 +91,10 @@ void IpcComm::close() {
   }
 }
 
+static int ipc_blocks(int64_t n) {
+  return (int)std::min<int64_t>(kIpcMaxBlocks, std::max<int64_t>(1, (n + 8191) / 8192));
+}
+
 void IpcComm::all_reduce_raw(const void* in, bool in_bf16, void* out, bool out_bf16, int64_t n, double scale,
                              hipStream_t s) {
   TORCH_CHECK(opened_ || world_ == 1, "IpcComm: open() the peer handles first");
@@ -111,8 +115,7 @@ void IpcComm::all_reduce_raw(const void* in, bool in_bf16, void* out, bool out_b
   a.spin_limit_ticks = spin_ticks_;
   // ~8K elements per block keeps the per-rank slice reads wide; never more blocks than the
   // signal layout holds
-  int blocks = (int)std::min<int64_t>(kIpcMaxBlocks, std::max<int64_t>(1, (n + 8191) / 8192));
-  ipc_allreduce(a, blocks, s);
+  ipc_allreduce(a, ipc_blocks(n), s);
 }
 
 void IpcComm::all_reduce(const at::Tensor& t, double scale) {
@@ -120,6 +123,57 @@ void IpcComm::all_reduce(const at::Tensor& t, double scale) {
   TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, "IpcComm: fp32/bf16 only");
   const bool bf = t.scalar_type() == at::kBFloat16;
   all_reduce_raw(t.data_ptr(), bf, t.data_ptr(), bf, t.numel(), scale, c10::hip::getCurrentHIPStream().stream());
+}
+
+void IpcComm::reduce_scatter_raw(const void* in, bool in_bf16, void* out, bool out_bf16, int64_t shard, double scale,
+                                 hipStream_t s) {
+  TORCH_CHECK(opened_ || world_ == 1, "IpcComm: open() the peer handles first");
+  TORCH_CHECK(shard * world_ <= cap_, "IpcComm.reduce_scatter: ", shard * world_, " elements exceed capacity ", cap_);
+  IpcAllReduceArgs a{};
+  a.in = in;
+  a.out = out;
+  for (int p = 0; p < world_; ++p) {
+    a.stage[p] = peer_stage_[p];
+    a.sig[p] = peer_sig_[p];
+  }
+  a.n = shard;
+  a.rank = (int)rank_;
+  a.world = (int)world_;
+  a.in_bf16 = in_bf16 ? 1 : 0;
+  a.out_bf16 = out_bf16 ? 1 : 0;
+  a.scale = (float)scale;
+  a.spin_limit_ticks = spin_ticks_;
+  ipc_reduce_scatter(a, ipc_blocks(shard), s);
+}
+
+void IpcComm::all_gather_raw(void* buf, int elem_bytes, int64_t shard, hipStream_t s) {
+  TORCH_CHECK(opened_ || world_ == 1, "IpcComm: open() the peer handles first");
+  TORCH_CHECK(elem_bytes == 2 || elem_bytes == 4, "IpcComm.all_gather: 2- or 4-byte elements");
+  TORCH_CHECK(shard * elem_bytes <= cap_ * 4, "IpcComm.all_gather: shard exceeds staging capacity");
+  IpcAllReduceArgs a{};
+  a.out = buf;
+  for (int p = 0; p < world_; ++p) {
+    a.stage[p] = peer_stage_[p];
+    a.sig[p] = peer_sig_[p];
+  }
+  a.n = shard;
+  a.rank = (int)rank_;
+  a.world = (int)world_;
+  a.spin_limit_ticks = spin_ticks_;
+  ipc_all_gather(a, elem_bytes, ipc_blocks(shard), s);
+}
+
+void IpcComm::reduce_scatter(const at::Tensor& in, const at::Tensor& out, double scale) {
+  TORCH_CHECK(in.is_cuda() && out.is_cuda() && in.is_contiguous() && out.is_contiguous(), "reduce_scatter: GPU");
+  TORCH_CHECK(in.numel() == out.numel() * world_, "reduce_scatter: in must be world * out elements");
+  reduce_scatter_raw(in.data_ptr(), in.scalar_type() == at::kBFloat16, out.data_ptr(),
+                     out.scalar_type() == at::kBFloat16, out.numel(), scale, c10::hip::getCurrentHIPStream().stream());
+}
+
+void IpcComm::all_gather(const at::Tensor& buf) {
+  TORCH_CHECK(buf.is_cuda() && buf.is_contiguous() && buf.numel() % world_ == 0, "all_gather: GPU, divisible");
+  all_gather_raw(buf.data_ptr(), (int)buf.element_size(), buf.numel() / world_,
+                 c10::hip::getCurrentHIPStream().stream());
 }
 
 int64_t IpcComm::error() {
@@ -137,6 +191,8 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("open", &IpcComm::open)
       .def("close", &IpcComm::close)
       .def("all_reduce", &IpcComm::all_reduce)
+      .def("reduce_scatter", &IpcComm::reduce_scatter)
+      .def("all_gather", &IpcComm::all_gather)
       .def("error", &IpcComm::error)
       .def("set_spin_limit_ms", &IpcComm::set_spin_limit_ms)
       .def("world", &IpcComm::world)

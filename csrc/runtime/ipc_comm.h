@@ -17,6 +17,13 @@ class IpcComm : public torch::CustomClassHolder {
   // in: fp32/bf16 -> fp32 staging -> reduced sum * scale -> out (fp32/bf16); n <= capacity
   void all_reduce_raw(const void* in, bool in_bf16, void* out, bool out_bf16, int64_t n, double scale,
                       hipStream_t s);
+  // reduce-scatter of N*S elements (fp32/bf16 in) into this rank's S-element shard (fp32/bf16 out)
+  void reduce_scatter_raw(const void* in, bool in_bf16, void* out, bool out_bf16, int64_t shard, double scale,
+                          hipStream_t s);
+  // in-place all-gather of N*S elements (2- or 4-byte) with this rank's shard at rank*S
+  void all_gather_raw(void* buf, int elem_bytes, int64_t shard, hipStream_t s);
+  void reduce_scatter(const at::Tensor& in, const at::Tensor& out, double scale);
+  void all_gather(const at::Tensor& buf);
   int64_t error();                           // 1 once a barrier timed out (sticky)
   void set_spin_limit_ms(double ms);
   int64_t world() const { return world_; }

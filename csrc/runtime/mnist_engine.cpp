@@ -71,6 +71,8 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipStreamCreateWithFlags(&aux_stream_, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&opt_stream_, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&ev_opt_a_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_start_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_ag_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
   }
@@ -85,6 +87,8 @@ class MnistEngine : public torch::CustomClassHolder {
     hipStreamDestroy(aux_stream_);
     hipStreamDestroy(opt_stream_);
     hipEventDestroy(ev_opt_a_);
+    hipEventDestroy(ev_start_);
+    hipEventDestroy(ev_ag_);
   }
 
   // ---- state accessors (views share storage with the engine) ----
@@ -144,6 +148,30 @@ class MnistEngine : public torch::CustomClassHolder {
     if (ipc_) return ipc_->world();
     return 1;
   }
+  int64_t rank_in_comm() const {
+    if (comm_) return comm_->rank();
+    if (ipc_) return ipc_->rank();
+    return 0;
+  }
+  // ZeRO-1 for the fc1 weight (98% of the parameters): its gradient is reduce-scattered, each rank
+  // runs the optimizer on its 1/N shard (fp32 master + m + v), and the updated bf16 shadow is
+  // all-gathered at the start of the next step, overlapping the conv forward. The re-expression of
+  // the reference's round-robin parameter sharding across PS tasks.
+  void set_zero(bool on) {
+    if (!on) { zero_ = false; return; }
+    const int64_t W = world();
+    TORCH_CHECK(W > 1, "set_zero: needs a communicator with world > 1");
+    TORCH_CHECK((OFF_BD1 - OFF_WD1) % (W * 64) == 0, "set_zero: fc1 weight not divisible into ", W, " shards");
+    zshard_ = (OFF_BD1 - OFF_WD1) / W;
+    zero_ = true;
+  }
+  bool zero() const { return zero_; }
+  // make every rank's bf16 shadow whole again (after the last zero step, before eval/checkpoint)
+  void sync_params() {
+    if (!zero_) return;
+    hipStream_t s = stream();
+    ag_w(s);
+  }
 
   // ---- step pieces (current HIP stream) ----
   void forward(bool train) { mnist_forward(args(), train, stream()); }
@@ -181,6 +209,10 @@ class MnistEngine : public torch::CustomClassHolder {
   // SyncReplicasOptimizer global step with replicas_to_aggregate == num_workers (averaged grads,
   // one ApplyAdam, global_step += 1).
   void train_step() {
+    if (zero_) {
+      train_step_zero();
+      return;
+    }
     // fwd -> fc bwd (bucket A ready) -> [bucket A all-reduce ->] optimizer on region A, on a side
     // stream, overlapping the conv backward on the main stream (the fc params are not read again
     // this step) -> conv grads -> slab reduce + step bump (after region A's optimizer has read
@@ -208,6 +240,39 @@ class MnistEngine : public torch::CustomClassHolder {
       HIP_OK(hipEventRecord(ev_done_, comm_stream_));
       HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
     }
+    apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s);
+  }
+
+  void train_step_zero() {
+    hipStream_t s = stream();
+    const double scale = 1.0 / (double)world();
+    const int64_t r = rank_in_comm();
+    MnistStepArgs a = args();
+    // all-gather last step's updated fc1 shadow shards, overlapping the conv forward
+    HIP_OK(hipEventRecord(ev_start_, s));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_start_, 0));
+    ag_w(comm_stream_);
+    HIP_OK(hipEventRecord(ev_ag_, comm_stream_));
+    mnist_forward_conv(a, s);
+    HIP_OK(hipStreamWaitEvent(s, ev_ag_, 0));
+    mnist_forward_fc(a, true, s);
+    backward_a();
+    HIP_OK(hipEventRecord(ev_a_, s));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
+    rs_w(comm_stream_);
+    reduce_bucket(OFF_BD1, TOTAL);
+    apply_optimizer_range(OFF_WD1 + r * zshard_, OFF_WD1 + (r + 1) * zshard_, scale, 1, comm_stream_);
+    apply_optimizer_range(OFF_BD1, TOTAL, scale, 1, comm_stream_);
+    HIP_OK(hipEventRecord(ev_opt_a_, comm_stream_));
+    a.step_bump = (int64_t*)step_.data_ptr();
+    mnist_backward_b(a, s, aux_stream_, ev_fork_, ev_join_);
+    HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+    mnist_conv_grad_reduce(a, s);
+    HIP_OK(hipEventRecord(ev_b_, s));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
+    reduce_bucket(0, BUCKET_SPLIT);
+    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
     apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s);
   }
 
@@ -285,6 +350,33 @@ class MnistEngine : public torch::CustomClassHolder {
 
  private:
   hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+  // ZeRO helpers (fc1 weight region W = [OFF_WD1, OFF_BD1))
+  void rs_w(hipStream_t st) {
+    const int64_t r = rank_in_comm();
+    const int64_t S = zshard_;
+    if (comm_) {
+      if (bf16_comm_) {
+        uint16_t* gb = (uint16_t*)gbf_.data_ptr() + OFF_WD1;
+        cast_f32_bf16((const float*)grad_.data_ptr() + OFF_WD1, gb, OFF_BD1 - OFF_WD1, st);
+        comm_->reduce_scatter_raw(gb, gb + r * S, (size_t)S, ncclBfloat16, ncclSum, st);
+      } else {
+        float* g = (float*)grad_.data_ptr() + OFF_WD1;
+        comm_->reduce_scatter_raw(g, g + r * S, (size_t)S, ncclFloat32, ncclSum, st);
+      }
+    } else {
+      void* out = bf16_comm_ ? (void*)((uint16_t*)gbf_.data_ptr() + OFF_WD1 + r * S)
+                             : (void*)((float*)grad_.data_ptr() + OFF_WD1 + r * S);
+      ipc_->reduce_scatter_raw((const float*)grad_.data_ptr() + OFF_WD1, false, out, bf16_comm_, S, 1.0, st);
+    }
+  }
+  void ag_w(hipStream_t st) {
+    const int64_t r = rank_in_comm();
+    const int64_t S = zshard_;
+    uint16_t* pb = (uint16_t*)pbf_.data_ptr() + OFF_WD1;
+    if (comm_) comm_->all_gather_raw(pb + r * S, pb, (size_t)S, ncclBfloat16, st);
+    else ipc_->all_gather_raw(pb, 2, S, st);
+  }
 
   void reduce_bucket(int64_t beg, int64_t end) {
     const size_t n = (size_t)(end - beg);
@@ -364,7 +456,9 @@ class MnistEngine : public torch::CustomClassHolder {
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t ev_a_ = nullptr, ev_b_ = nullptr, ev_done_ = nullptr, ev_fork_ = nullptr, ev_join_ = nullptr;
   hipStream_t aux_stream_ = nullptr, opt_stream_ = nullptr;
-  hipEvent_t ev_opt_a_ = nullptr;
+  hipEvent_t ev_opt_a_ = nullptr, ev_start_ = nullptr, ev_ag_ = nullptr;
+  bool zero_ = false;
+  int64_t zshard_ = 0;
   std::map<std::string, hipGraphExec_t> graphs_;
 };
 
@@ -405,6 +499,9 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_momentum", &MnistEngine::set_momentum)
       .def("set_comm", &MnistEngine::set_comm)
       .def("set_ipc", &MnistEngine::set_ipc)
+      .def("set_zero", &MnistEngine::set_zero)
+      .def("zero", &MnistEngine::zero)
+      .def("sync_params", &MnistEngine::sync_params)
       .def("world", &MnistEngine::world)
       .def("forward", &MnistEngine::forward)
       .def("backward_a", &MnistEngine::backward_a)

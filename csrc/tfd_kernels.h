@@ -42,6 +42,8 @@ struct MnistStepArgs {
 int mnist_fc1_splits(int B);
 int mnist_wg2_splits(int B);
 void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s);        // conv1, conv2, fc1, head
+void mnist_forward_conv(const MnistStepArgs& a, hipStream_t s);               // conv1, conv2 (read region B)
+void mnist_forward_fc(const MnistStepArgs& a, bool train, hipStream_t s);     // fc1, head (read region A)
 void mnist_backward_a(const MnistStepArgs& a, hipStream_t s);                 // fc1 dW/dX -> bucket A done
 // conv2/conv1 grads -> bucket B done. With `aux` set, independent kernels fork onto it (fork/join
 // events recorded on s/aux; both are captured into the step graph as parallel branches).

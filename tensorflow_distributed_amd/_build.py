@@ -26,6 +26,7 @@ PKG = os.path.join(ROOT, "tensorflow_distributed_amd")
 # TFD_NATIVE_LIB=<path>.
 VARIANT = os.environ.get("TFD_VARIANT", "")
 EXTRA_FLAGS = os.environ.get("TFD_EXTRA_FLAGS", "").split()
+HIP_EXTRA_FLAGS = os.environ.get("TFD_HIP_FLAGS", "").split()  # device-compiler-only flags
 BUILD = os.path.join(ROOT, "build", "native" + (f"-{VARIANT}" if VARIANT else ""))
 OUT = os.path.join(PKG, f"_C_{VARIANT}.so" if VARIANT else "_C.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
@@ -70,7 +71,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     hip_flags = common + [
         "-x", "hip", f"--offload-arch={ARCH}", "-D__HIP_PLATFORM_AMD__=1",
         "-ffp-contract=fast", "-munsafe-fp-atomics", "-Wno-unused-result",
-    ]
+    ] + HIP_EXTRA_FLAGS
     cpp_flags = common + [
         "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-I", os.path.join(ROCM, "include"),
     ] + sum([["-I", i] for i in incs], []) + ["-Wno-deprecated-declarations"]
