@@ -35,6 +35,8 @@ def main(argv=None):
     ap.add_argument("--fp32_grads", action="store_true", help="all-reduce fp32 grads (default bf16)")
     ap.add_argument("--ipc_small", type=int, default=1, help="1: peer-to-peer IPC one-shot all-reduce for the "
                     "small conv-gradient bucket (self-checked against RCCL at startup; falls back if it disagrees)")
+    ap.add_argument("--opt_overlap", type=int, default=0, help="1: run the fc-region optimizer on a side "
+                    "stream overlapping the conv backward (0: on the main stream after it)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu", action="store_true", help="plumbing dry-run: fp32 PyTorch CPU runner + Gloo "
@@ -58,6 +60,7 @@ def main(argv=None):
     B = a.batch_size
     eng = torch.classes.tfd.MnistEngine(B, dev.index, 0.75, a.seed, rank)
     eng.set_adam(a.lr, 0.9, 0.999, 1e-8)
+    eng.set_opt_overlap(a.opt_overlap)
     ipc_state = "off"
     if ctx.comm is not None:
         eng.set_comm(ctx.comm, not a.fp32_grads)

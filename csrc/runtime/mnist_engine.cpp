@@ -166,6 +166,7 @@ class MnistEngine : public torch::CustomClassHolder {
     zero_ = true;
   }
   bool zero() const { return zero_; }
+  void set_opt_overlap(int64_t on) { opt_overlap_ = on; }
   // make every rank's bf16 shadow whole again (after the last zero step, before eval/checkpoint)
   void sync_params() {
     if (!zero_) return;
@@ -222,16 +223,19 @@ class MnistEngine : public torch::CustomClassHolder {
     const double scale = dp ? 1.0 / (double)world() : 1.0;
     forward(true);
     backward_a();
-    HIP_OK(hipEventRecord(ev_a_, s));
-    hipStream_t os = dp ? comm_stream_ : opt_stream_;
-    HIP_OK(hipStreamWaitEvent(os, ev_a_, 0));
-    if (dp) reduce_bucket(BUCKET_SPLIT, TOTAL);
-    apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 1, os);
-    HIP_OK(hipEventRecord(ev_opt_a_, os));
     MnistStepArgs a = args();
     a.step_bump = (int64_t*)step_.data_ptr();
+    if (dp || opt_overlap_) {
+      HIP_OK(hipEventRecord(ev_a_, s));
+      hipStream_t os = dp ? comm_stream_ : opt_stream_;
+      HIP_OK(hipStreamWaitEvent(os, ev_a_, 0));
+      if (dp) reduce_bucket(BUCKET_SPLIT, TOTAL);
+      if (opt_overlap_) apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 1, os);
+      HIP_OK(hipEventRecord(ev_opt_a_, os));
+    }
     mnist_backward_b(a, s, aux_stream_, ev_fork_, ev_join_);
-    HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+    if (dp || opt_overlap_) HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+    if (!opt_overlap_) apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 1, s);
     mnist_conv_grad_reduce(a, s);
     if (dp) {
       HIP_OK(hipEventRecord(ev_b_, s));
@@ -459,6 +463,9 @@ class MnistEngine : public torch::CustomClassHolder {
   hipEvent_t ev_opt_a_ = nullptr, ev_start_ = nullptr, ev_ag_ = nullptr;
   bool zero_ = false;
   int64_t zshard_ = 0;
+  // where region A's optimizer runs: 0 = main stream after the conv backward (no HBM contention
+  // with the conv kernels), 1 = side stream overlapping the conv backward
+  int64_t opt_overlap_ = 0;
   std::map<std::string, hipGraphExec_t> graphs_;
 };
 
@@ -500,6 +507,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_comm", &MnistEngine::set_comm)
       .def("set_ipc", &MnistEngine::set_ipc)
       .def("set_zero", &MnistEngine::set_zero)
+      .def("set_opt_overlap", &MnistEngine::set_opt_overlap)
       .def("zero", &MnistEngine::zero)
       .def("sync_params", &MnistEngine::sync_params)
       .def("world", &MnistEngine::world)

@@ -71,10 +71,20 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     hip_flags = common + [
         "-x", "hip", f"--offload-arch={ARCH}", "-D__HIP_PLATFORM_AMD__=1",
         "-ffp-contract=fast", "-munsafe-fp-atomics", "-Wno-unused-result",
+        # No packed-fp32 VALU ops (v_pk_fma/mul/add_f32): with them, the SLP-vectorised VALU
+        # kernels (conv1, head, wgrad) gave sporadically different results for the same inputs
+        # when several processes shared the GPU; without them every stage is bit-reproducible
+        # (scripts/debug/determinism.py, docs/DESIGN.md section 6).
+        "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
     ] + HIP_EXTRA_FLAGS
     cpp_flags = common + [
         "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-I", os.path.join(ROCM, "include"),
     ] + sum([["-I", i] for i in incs], []) + ["-Wno-deprecated-declarations"]
+    # a flag change (build options, torch headers) invalidates every object of this variant
+    stamp = os.path.join(BUILD, "flags.stamp")
+    sig = repr((hip_flags, cpp_flags))
+    if not os.path.exists(stamp) or open(stamp).read() != sig:
+        force = True
     jobs_list = []
     objs = []
     for s in hip_srcs:
@@ -95,6 +105,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
                 s = f.result()
                 if verbose:
                     print("compiled", os.path.relpath(s, ROOT), flush=True)
+    with open(stamp, "w") as f:
+        f.write(sig)
     newest = max([os.path.getmtime(o) for o in objs] + [0])
     if force or jobs_list or not os.path.exists(OUT) or os.path.getmtime(OUT) < newest:
         link = [os.path.join(ROCM, "bin", "hipcc"), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", OUT] + objs + [
