@@ -443,9 +443,13 @@ __device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, 
   __syncthreads();
   for (int i = t; i < OUTG_ROWS * NCLS; i += 256) {
     const int rr = i / NCLS, mm = blk * OUTG_ROWS + rr;
-    if (mm <= HID)
-      a.grad[OFF_OUT + (size_t)mm * NCLS + (i - rr * NCLS)] =
+    if (mm <= HID) {
+      const size_t o = OFF_OUT + (size_t)mm * NCLS + (i - rr * NCLS);
+      const float g =
           part[i] + part[OUTG_ROWS * NCLS + i] + part[2 * OUTG_ROWS * NCLS + i] + part[3 * OUTG_ROWS * NCLS + i];
+      if (a.gbf_a) a.gbf_a[o] = f2bf_bits(g);
+      else a.grad[o] = g;
+    }
   }
 }
 
@@ -466,11 +470,28 @@ struct OnesRowMC {  // operand (mn, k) = X[k][mn] for mn < mn_real, 1 for mn == 
     return *reinterpret_cast<uint4*>(t);
   }
 };
+// fc1 dW rows [3137][1024]: fp32 into the flat gradient buffer, or (DP, bf16 wire format) bf16
+// straight into the all-reduce operand -- the rounding the separate cast pass used to do.
+struct GradEpi {
+  float* __restrict__ out;
+  uint16_t* __restrict__ outbf;
+  int ld, M, N;
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+    if (n >= N) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (m4 + r >= M) continue;
+      const size_t o = (size_t)(m4 + r) * ld + n;
+      if (outbf) outbf[o] = f2bf_bits(v[r]);
+      else out[o] = v[r];
+    }
+  }
+};
 constexpr int FDW_BM = 64, FDW_BN = 64, FDW_BK = TFD_FDW_BK;
 __device__ __forceinline__ void fc1_dw_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   OnesRowMC la{a.p2, FEAT, FEAT, a.B};
   DenseLoader<false> lb{a.dh, HID, HID, a.B};
-  SlabEpi epi{a.grad + OFF_WD1, HID, FEAT + 1, HID};
+  GradEpi epi{a.grad + OFF_WD1, a.gbf_a ? a.gbf_a + OFF_WD1 : nullptr, HID, FEAT + 1, HID};
   gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, by * FDW_BM, bx * FDW_BN, 0, a.B, smem);
 }
 

@@ -222,8 +222,9 @@ class MnistEngine : public torch::CustomClassHolder {
     const bool dp = world() > 1;
     const double scale = dp ? 1.0 / (double)world() : 1.0;
     forward(true);
-    backward_a();
     MnistStepArgs a = args();
+    if (fused_bf16_a()) a.gbf_a = (uint16_t*)gbf_.data_ptr();
+    mnist_backward_a(a, s);
     a.step_bump = (int64_t*)step_.data_ptr();
     if (dp || opt_overlap_) {
       HIP_OK(hipEventRecord(ev_a_, s));
@@ -260,7 +261,8 @@ class MnistEngine : public torch::CustomClassHolder {
     mnist_forward_conv(a, s);
     HIP_OK(hipStreamWaitEvent(s, ev_ag_, 0));
     mnist_forward_fc(a, true, s);
-    backward_a();
+    if (fused_bf16_a()) a.gbf_a = (uint16_t*)gbf_.data_ptr();
+    mnist_backward_a(a, s);
     HIP_OK(hipEventRecord(ev_a_, s));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
     rs_w(comm_stream_);
@@ -359,10 +361,11 @@ class MnistEngine : public torch::CustomClassHolder {
   void rs_w(hipStream_t st) {
     const int64_t r = rank_in_comm();
     const int64_t S = zshard_;
+    const bool pre = in_gbf(OFF_WD1);
     if (comm_) {
       if (bf16_comm_) {
         uint16_t* gb = (uint16_t*)gbf_.data_ptr() + OFF_WD1;
-        cast_f32_bf16((const float*)grad_.data_ptr() + OFF_WD1, gb, OFF_BD1 - OFF_WD1, st);
+        if (!pre) cast_f32_bf16((const float*)grad_.data_ptr() + OFF_WD1, gb, OFF_BD1 - OFF_WD1, st);
         comm_->reduce_scatter_raw(gb, gb + r * S, (size_t)S, ncclBfloat16, ncclSum, st);
       } else {
         float* g = (float*)grad_.data_ptr() + OFF_WD1;
@@ -371,7 +374,9 @@ class MnistEngine : public torch::CustomClassHolder {
     } else {
       void* out = bf16_comm_ ? (void*)((uint16_t*)gbf_.data_ptr() + OFF_WD1 + r * S)
                              : (void*)((float*)grad_.data_ptr() + OFF_WD1 + r * S);
-      ipc_->reduce_scatter_raw((const float*)grad_.data_ptr() + OFF_WD1, false, out, bf16_comm_, S, 1.0, st);
+      const void* in = pre ? (const void*)((const uint16_t*)gbf_.data_ptr() + OFF_WD1)
+                           : (const void*)((const float*)grad_.data_ptr() + OFF_WD1);
+      ipc_->reduce_scatter_raw(in, pre, out, bf16_comm_, S, 1.0, st);
     }
   }
   void ag_w(hipStream_t st) {
@@ -382,19 +387,26 @@ class MnistEngine : public torch::CustomClassHolder {
     else ipc_->all_gather_raw(pb, 2, S, st);
   }
 
+  // bucket A's gradients come out of the fc backward as bf16 in gbf_ (MnistStepArgs::gbf_a)
+  bool fused_bf16_a() const { return bf16_comm_ && world() > 1; }
+  bool in_gbf(int64_t beg) const { return fused_bf16_a() && beg >= BUCKET_SPLIT; }
+
   void reduce_bucket(int64_t beg, int64_t end) {
     const size_t n = (size_t)(end - beg);
+    const bool pre = in_gbf(beg);
     if (ipc_ && (!comm_ || (int64_t)n <= ipc_small_)) {
-      // fp32 grads in, exact fp32 sum, written where the optimizer reads (bf16 gbf or fp32 grad)
+      // fp32 (or fused bf16) grads in, fp32 sum in rank order, written where the optimizer reads
+      // (bf16 gbf or fp32 grad)
       void* out = bf16_comm_ ? (void*)((uint16_t*)gbf_.data_ptr() + beg) : (void*)((float*)grad_.data_ptr() + beg);
-      ipc_->all_reduce_raw((const float*)grad_.data_ptr() + beg, false, out, bf16_comm_, (int64_t)n, 1.0,
-                           comm_stream_);
+      const void* in = pre ? (const void*)((const uint16_t*)gbf_.data_ptr() + beg)
+                           : (const void*)((const float*)grad_.data_ptr() + beg);
+      ipc_->all_reduce_raw(in, pre, out, bf16_comm_, (int64_t)n, 1.0, comm_stream_);
       return;
     }
     TORCH_CHECK(comm_, "no communicator for a ", n, "-element bucket");
     if (bf16_comm_) {
       uint16_t* gb = (uint16_t*)gbf_.data_ptr() + beg;
-      cast_f32_bf16((const float*)grad_.data_ptr() + beg, gb, (int64_t)n, comm_stream_);
+      if (!pre) cast_f32_bf16((const float*)grad_.data_ptr() + beg, gb, (int64_t)n, comm_stream_);
       comm_->all_reduce_raw(gb, n, ncclBfloat16, ncclSum, comm_stream_);
     } else {
       comm_->all_reduce_raw((float*)grad_.data_ptr() + beg, n, ncclFloat32, ncclSum, comm_stream_);

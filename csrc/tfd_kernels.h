@@ -23,6 +23,9 @@ struct MnistStepArgs {
   const float* p32;            // flat fp32 master params (mnist_layout.h)
   const uint16_t* pbf;         // flat bf16 shadow of p32
   float* grad;                 // flat fp32 gradient buffer
+  uint16_t* gbf_a;             // if set (DP with a bf16 wire format): the fc backward writes bucket A's
+                               // gradients [OFF_WD1, TOTAL) as bf16 straight into this flat buffer (the
+                               // all-reduce operand) instead of fp32 into `grad` -- no separate cast pass
   // activations / workspace (bf16 stored as uint16)
   uint16_t* p1;  uint8_t* idx1;   // [B][14][14][32]
   uint16_t* p2;  uint8_t* idx2;   // [B][3136]
