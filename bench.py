@@ -37,6 +37,8 @@ def main(argv=None):
                     "small conv-gradient bucket (self-checked against RCCL at startup; falls back if it disagrees)")
     ap.add_argument("--opt_overlap", type=int, default=0, help="1: run the fc-region optimizer on a side "
                     "stream overlapping the conv backward (0: on the main stream after it)")
+    ap.add_argument("--conv_fork", type=int, default=0, help="1: conv2 wgrad on a forked stream beside dgrad")
+    ap.add_argument("--zero", type=int, default=0, help="1: ZeRO-1 sharding of the fc1 weight (N > 1)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu", action="store_true", help="plumbing dry-run: fp32 PyTorch CPU runner + Gloo "
@@ -61,11 +63,14 @@ def main(argv=None):
     eng = torch.classes.tfd.MnistEngine(B, dev.index, 0.75, a.seed, rank)
     eng.set_adam(a.lr, 0.9, 0.999, 1e-8)
     eng.set_opt_overlap(a.opt_overlap)
+    eng.set_conv_fork(a.conv_fork)
     ipc_state = "off"
     if ctx.comm is not None:
         eng.set_comm(ctx.comm, not a.fp32_grads)
         if a.ipc_small:
             ipc_state = _setup_ipc(eng, ctx, M)
+        if a.zero:
+            eng.set_zero(True)
     s = torch.cuda.Stream(dev)
     n_data = 55000
     with torch.cuda.stream(s):
@@ -104,6 +109,9 @@ def main(argv=None):
     torch.cuda.synchronize(dev)
     ctx.barrier()
     dt = time.perf_counter() - t0
+    if a.zero:
+        with torch.cuda.stream(s):
+            eng.sync_params()
     dt = ctx.max_scalar(dt)
     loss1 = float(eng.loss_rows().mean().item())
     gstep = int(eng.step_tensor().item())
@@ -135,6 +143,7 @@ def main(argv=None):
                 "grad_allreduce": "fp32" if a.fp32_grads else "bf16",
                 "hipgraph": graph_mode,
                 "small_bucket_allreduce": ipc_state,
+                "zero1_fc1": bool(a.zero),
             },
         }), flush=True)
     ctx.shutdown()

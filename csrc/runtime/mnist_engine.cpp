@@ -167,6 +167,8 @@ class MnistEngine : public torch::CustomClassHolder {
   }
   bool zero() const { return zero_; }
   void set_opt_overlap(int64_t on) { opt_overlap_ = on; }
+  // conv2 wgrad on a forked stream beside dgrad -> conv1 wgrad (1) or all on the main stream (0)
+  void set_conv_fork(int64_t on) { conv_fork_ = on != 0; }
   // make every rank's bf16 shadow whole again (after the last zero step, before eval/checkpoint)
   void sync_params() {
     if (!zero_) return;
@@ -182,7 +184,7 @@ class MnistEngine : public torch::CustomClassHolder {
   void backward_b() {
     MnistStepArgs a = args();
     a.step_bump = (int64_t*)step_.data_ptr();
-    mnist_backward_b(a, stream(), aux_stream_, ev_fork_, ev_join_);
+    mnist_backward_b(a, stream(), conv_fork_ ? aux_stream_ : nullptr, ev_fork_, ev_join_);
     mnist_conv_grad_reduce(a, stream());
   }
   void apply_optimizer(double grad_scale) {
@@ -205,19 +207,20 @@ class MnistEngine : public torch::CustomClassHolder {
     }
   }
 
-  // Full synchronous data-parallel step: fwd -> bwd(fc) -> [bucket A all-reduce on comm stream]
-  // || bwd(conv) -> [bucket B all-reduce] -> join -> optimizer. Equivalent of the reference's
-  // SyncReplicasOptimizer global step with replicas_to_aggregate == num_workers (averaged grads,
-  // one ApplyAdam, global_step += 1).
+  // Full synchronous data-parallel step (the reference's SyncReplicasOptimizer global step with
+  // replicas_to_aggregate == num_workers: averaged grads, one ApplyAdam, global_step += 1):
+  //   main: fwd -> fc bwd (bucket A ready) -> conv bwd -> conv-grad reduce + step bump (bucket B
+  //         ready) -> [wait A] optimizer on A -> [wait B] optimizer on B
+  //   comm:                     all-reduce A (overlaps the conv bwd)  -> all-reduce B (overlaps the
+  //                                                                       optimizer on A)
+  // One GPU: one optimizer launch over the whole buffer after the reduce. opt_overlap_: region A's
+  // optimizer runs on a side stream right after its bucket, beside the conv backward (the fc params
+  // are not read again this step; the reduce waits for it, so it reads the pre-bump step).
   void train_step() {
     if (zero_) {
       train_step_zero();
       return;
     }
-    // fwd -> fc bwd (bucket A ready) -> [bucket A all-reduce ->] optimizer on region A, on a side
-    // stream, overlapping the conv backward on the main stream (the fc params are not read again
-    // this step) -> conv grads -> slab reduce + step bump (after region A's optimizer has read
-    // the step) -> [bucket B all-reduce ->] optimizer on region B.
     hipStream_t s = stream();
     const bool dp = world() > 1;
     const double scale = dp ? 1.0 / (double)world() : 1.0;
@@ -226,25 +229,33 @@ class MnistEngine : public torch::CustomClassHolder {
     if (fused_bf16_a()) a.gbf_a = (uint16_t*)gbf_.data_ptr();
     mnist_backward_a(a, s);
     a.step_bump = (int64_t*)step_.data_ptr();
-    if (dp || opt_overlap_) {
-      HIP_OK(hipEventRecord(ev_a_, s));
-      hipStream_t os = dp ? comm_stream_ : opt_stream_;
-      HIP_OK(hipStreamWaitEvent(os, ev_a_, 0));
-      if (dp) reduce_bucket(BUCKET_SPLIT, TOTAL);
-      if (opt_overlap_) apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 1, os);
-      HIP_OK(hipEventRecord(ev_opt_a_, os));
+    hipStream_t ws = conv_fork_ ? aux_stream_ : nullptr;
+    if (!dp && !opt_overlap_) {
+      mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
+      mnist_conv_grad_reduce(a, s);
+      apply_optimizer_range(0, TOTAL, scale, 0, s);
+      return;
     }
-    mnist_backward_b(a, s, aux_stream_, ev_fork_, ev_join_);
-    if (dp || opt_overlap_) HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
-    if (!opt_overlap_) apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 1, s);
+    HIP_OK(hipEventRecord(ev_a_, s));
+    hipStream_t os = dp ? comm_stream_ : opt_stream_;
+    HIP_OK(hipStreamWaitEvent(os, ev_a_, 0));
+    if (dp) reduce_bucket(BUCKET_SPLIT, TOTAL);
+    if (opt_overlap_) apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 1, os);
+    HIP_OK(hipEventRecord(ev_opt_a_, os));
+    mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
+    if (opt_overlap_) HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
     mnist_conv_grad_reduce(a, s);
     if (dp) {
       HIP_OK(hipEventRecord(ev_b_, s));
       HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
       reduce_bucket(0, BUCKET_SPLIT);
       HIP_OK(hipEventRecord(ev_done_, comm_stream_));
-      HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
     }
+    if (!opt_overlap_) {
+      HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+      apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 0, s);
+    }
+    if (dp) HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
     apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s);
   }
 
@@ -271,7 +282,7 @@ class MnistEngine : public torch::CustomClassHolder {
     apply_optimizer_range(OFF_BD1, TOTAL, scale, 1, comm_stream_);
     HIP_OK(hipEventRecord(ev_opt_a_, comm_stream_));
     a.step_bump = (int64_t*)step_.data_ptr();
-    mnist_backward_b(a, s, aux_stream_, ev_fork_, ev_join_);
+    mnist_backward_b(a, s, conv_fork_ ? aux_stream_ : nullptr, ev_fork_, ev_join_);
     HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
     mnist_conv_grad_reduce(a, s);
     HIP_OK(hipEventRecord(ev_b_, s));
@@ -478,6 +489,8 @@ class MnistEngine : public torch::CustomClassHolder {
   // where region A's optimizer runs: 0 = main stream after the conv backward (no HBM contention
   // with the conv kernels), 1 = side stream overlapping the conv backward
   int64_t opt_overlap_ = 0;
+  // measured on one MI355X: the forked conv2 wgrad only contends with dgrad for CUs (110 vs 100 us/step)
+  bool conv_fork_ = false;
   std::map<std::string, hipGraphExec_t> graphs_;
 };
 
@@ -520,6 +533,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_ipc", &MnistEngine::set_ipc)
       .def("set_zero", &MnistEngine::set_zero)
       .def("set_opt_overlap", &MnistEngine::set_opt_overlap)
+      .def("set_conv_fork", &MnistEngine::set_conv_fork)
       .def("zero", &MnistEngine::zero)
       .def("sync_params", &MnistEngine::sync_params)
       .def("world", &MnistEngine::world)
