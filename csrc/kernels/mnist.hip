@@ -15,7 +15,8 @@
 //   conv2_dgrad      K13 with conv1 ReluGrad/pool-mask epilogue; conv2_wgrad K14 (+K12 bias row),
 //                    split-K slabs; out_grad K8 dW/db.
 //   conv1_wgrad      K15 (+K12): sparse wgrad straight from the pooled gradient and argmax (only the
-//                    1-of-4 argmax positions carry gradient), deterministic per-image slabs.
+//                    1-of-4 argmax positions carry gradient), deterministic per-image slabs. In the
+//                    LDS path it is the tail of conv2_dgrad_lds (same half-image rows, from LDS).
 #include "../common.h"
 #include "../gemm.h"
 #include "../mnist_layout.h"
@@ -601,6 +602,15 @@ __device__ __forceinline__ void conv2_dgrad_block(const MnistStepArgs& a, int bx
 constexpr int C2D_ROWS = 11, C2D_COLS = 20, C2D_PLANE = 224, C2D_WLD = 72;
 constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 800 * C2D_WLD) * 2;  // 143872 B
 static_assert(C2D_PLANE * 16 % 256 == 0 && C2D_PLANE >= C2D_ROWS * C2D_COLS, "dz2 plane");
+constexpr int C1W_HALF = 98;  // pooled conv1 pixels per half image (7 rows of 14)
+// fused conv1-wgrad tail: buffers carved from the (dead) weight region
+constexpr int C2D_X_OFF = 8 * C2D_PLANE * 8 * 2;          // 28672
+constexpr int C2D_G_OFF = C2D_X_OFF + 32 * 32 * 4;
+constexpr int C2D_I_OFF = C2D_G_OFF + C1W_HALF * 32 * 4;
+constexpr int C2D_P_OFF = C2D_I_OFF + C1W_HALF * 32;
+static_assert(C2D_I_OFF % 16 == 0 && C2D_P_OFF % 16 == 0, "LDS carve alignment");
+static_assert(C2D_P_OFF + 16 * 833 * 4 <= C2D_SMEM, "fused conv1-wgrad tail exceeds the dgrad LDS");
+static_assert(4 * 4 * 64 * 16 <= C2D_X_OFF, "park region overlaps the fused tail");
 __global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* img = (bf16*)smem_raw;                           // [8][224][8]
@@ -681,22 +691,70 @@ __global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) {
       for (int nt = 0; nt < 2; ++nt) park[(mt0 * 4 + j * 2 + nt) * 64 + lane] = acc[j][nt];
   }
   __syncthreads();
-  if (kq) return;
+  // K15 + K12 fused: this block's dX rows ARE conv1's pooled-gradient rows [7h, 7h + 7) of image b,
+  // so conv1's weight/bias gradient partial for them is computed here from LDS (no dp1m round trip,
+  // no separate launch). The weight region of LDS is dead now: x image, masked gradient, argmax.
+  float* xs = reinterpret_cast<float*>(smem_raw + C2D_X_OFF);     // [32][32] zero-bordered input
+  float* gsl = reinterpret_cast<float*>(smem_raw + C2D_G_OFF);    // [98][32] conv1 pre-act grad
+  uint8_t* isl = reinterpret_cast<uint8_t*>(smem_raw + C2D_I_OFF);  // [98][32] pool argmax
+  float* part = reinterpret_cast<float*>(smem_raw + C2D_P_OFF);   // [16][833] partials
+  if (!kq) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    if (j == 1 && !two) break;
+    for (int j = 0; j < 2; ++j) {
+      if (j == 1 && !two) break;
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const f32x4 v = acc[j][nt] + park[(mt0 * 4 + j * 2 + nt) * 64 + lane];
-      const int n = nt * 16 + (lane & 15), ih = 7 * h + mt0 + 4 * j;
+      for (int nt = 0; nt < 2; ++nt) {
+        const f32x4 v = acc[j][nt] + park[(mt0 * 4 + j * 2 + nt) * 64 + lane];
+        const int n = nt * 16 + (lane & 15), lr = mt0 + 4 * j, ih = 7 * h + lr;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int x = 4 * g + r;  // C row = input column iw
-        if (x >= 14) break;
-        const size_t o = ((size_t)b * 196 + ih * 14 + x) * 32 + n;
-        a.dp1m[o] = a.p1[o] != 0 ? f2bf_bits(v[r]) : (uint16_t)0;  // conv1 relu output > 0
+        for (int r = 0; r < 4; ++r) {
+          const int x = 4 * g + r;  // C row = input column iw
+          if (x >= 14) break;
+          const size_t o = ((size_t)b * 196 + ih * 14 + x) * 32 + n;
+          // conv1 relu output > 0; rounded to bf16 like the stored activation gradients
+          gsl[(lr * 14 + x) * 32 + n] = a.p1[o] != 0 ? bf2f(f2bf_bits(v[r])) : 0.f;
+        }
       }
     }
+  } else {
+    const int u = t - 256;
+    const float* xrow = a.data + (size_t)data_row(a.perm, a.step, a.n_data, a.B, b) * 784;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = 4 * u + q, r = i >> 5, c = i & 31;
+      xs[i] = (r >= 2 && r < 30 && c >= 2 && c < 30) ? xrow[(r - 2) * 28 + c - 2] : 0.f;
+    }
+    if (u < C1W_HALF * 32 / 16)
+      reinterpret_cast<uint4*>(isl)[u] = reinterpret_cast<const uint4*>(a.idx1 + ((size_t)b * 196 + h * C1W_HALF) * 32)[u];
+  }
+  __syncthreads();
+  {
+    // only the argmax position of each 2x2 window carries gradient: dW1[tap][c] += g * x[argmax + tap]
+    const int c = t & 31, sub = t >> 5;
+    float acc1[26];
+#pragma unroll
+    for (int j = 0; j < 26; ++j) acc1[j] = 0.f;
+    for (int lp = sub; lp < C1W_HALF; lp += 16) {
+      const float gv = gsl[lp * 32 + c];
+      if (gv != 0.f) {
+        const int pp = h * C1W_HALF + lp, w = isl[lp * 32 + c];
+        const int oh = 2 * (pp / 14) + (w >> 1), ow = 2 * (pp % 14) + (w & 1);
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) acc1[kh * 5 + kw] = fmaf(gv, xs[(oh + kh) * 32 + ow + kw], acc1[kh * 5 + kw]);
+        acc1[25] += gv;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 26; ++j) part[sub * 833 + j * 32 + c] = acc1[j];
+  }
+  __syncthreads();
+  for (int i = t; i < 26 * 32; i += 512) {
+    float sm = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sm += part[q * 833 + i];
+    a.wg1_slab[(size_t)blockIdx.x * 832 + i] = sm;
   }
 }
 
@@ -744,7 +802,6 @@ __global__ __launch_bounds__(256) void conv2_bwd(MnistStepArgs a, int n_dgrad, i
 // pixels): the padded image and the block's dp1m / argmax rows are staged in LDS with 16-B loads
 // (no dependent global loads in the loop), thread (c = t & 31, sub = t >> 5) accumulates 26
 // partials (25 taps + bias), then the 8 subs are summed in LDS into one deterministic slab per block.
-constexpr int C1W_HALF = 98;
 __global__ __launch_bounds__(256) void conv1_wgrad(MnistStepArgs a) {
   __shared__ float img[32 * 32];
   __shared__ __attribute__((aligned(16))) uint16_t gs[C1W_HALF * 32];
@@ -902,8 +959,7 @@ void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux, hi
   if (aux) { (void)hipEventRecord(fork, s); (void)hipStreamWaitEvent(aux, fork, 0); }
   conv2_wgrad_k<<<C2W_GX * a.wg2_splits, 256, sm_w, ws>>>(a, kper);
   set_smem<conv2_dgrad_lds>(C2D_SMEM);
-  conv2_dgrad_lds<<<2 * B, 512, C2D_SMEM, s>>>(a);
-  conv1_wgrad<<<2 * B, 256, 0, s>>>(a);
+  conv2_dgrad_lds<<<2 * B, 512, C2D_SMEM, s>>>(a);  // + conv1 wgrad (fused tail)
   if (aux) { (void)hipEventRecord(join, aux); (void)hipStreamWaitEvent(s, join, 0); }
 #else
   (void)aux; (void)fork; (void)join;
