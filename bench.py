@@ -39,6 +39,8 @@ def main(argv=None):
                     "stream overlapping the conv backward (0: on the main stream after it)")
     ap.add_argument("--conv_fork", type=int, default=0, help="1: conv2 wgrad on a forked stream beside dgrad")
     ap.add_argument("--zero", type=int, default=0, help="1: ZeRO-1 sharding of the fc1 weight (N > 1)")
+    ap.add_argument("--fused_tail", type=int, default=1, help="1: on one GPU the Adam kernel also reduces the "
+                    "conv weight-gradient slabs and bumps the step (one kernel less)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu", action="store_true", help="plumbing dry-run: fp32 PyTorch CPU runner + Gloo "
@@ -64,6 +66,7 @@ def main(argv=None):
     eng.set_adam(a.lr, 0.9, 0.999, 1e-8)
     eng.set_opt_overlap(a.opt_overlap)
     eng.set_conv_fork(a.conv_fork)
+    eng.set_fused_tail(a.fused_tail)
     ipc_state = "off"
     if ctx.comm is not None:
         eng.set_comm(ctx.comm, not a.fp32_grads)

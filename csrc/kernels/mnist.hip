@@ -331,6 +331,7 @@ __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
 __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n0 = 4 * t;
+  if (a.t_out && row == 0 && t == 0) *a.t_out = *a.step + 1;
   f32x4 h = *reinterpret_cast<const f32x4*>(a.p32 + OFF_BD1 + n0);
   {  // all split-K slab loads in flight together (compile-time count: no per-load branches)
     f32x4 p[FC1_SPLITS];
@@ -533,13 +534,17 @@ __device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int
 // products that all consume dH / dlogits): [fc1 dW tiles | fc1 dX tiles | out dW/db blocks].
 constexpr int FDW_GX = HID / FDW_BN, FDW_GY = (FEAT + 1 + FDW_BM - 1) / FDW_BM;  // 16 x 50
 constexpr int FDX_GX = FEAT / FDX_BN;                                             // 49
-__global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx) {
+// part 0: all three products; part 1: dW + out-layer grads (bucket A complete); part 2: dX only.
+__global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int part) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   int id = blockIdx.x;
+  if (part == 2) { fc1_dx_block(a, id % FDX_GX, id / FDX_GX, (bf16*)smem_raw); return; }
   if (id < FDW_GX * FDW_GY) { fc1_dw_block(a, id % FDW_GX, id / FDW_GX, (bf16*)smem_raw); return; }
   id -= FDW_GX * FDW_GY;
-  if (id < n_dx) { fc1_dx_block(a, id % FDX_GX, id / FDX_GX, (bf16*)smem_raw); return; }
-  id -= n_dx;
+  if (part == 0) {
+    if (id < n_dx) { fc1_dx_block(a, id % FDX_GX, id / FDX_GX, (bf16*)smem_raw); return; }
+    id -= n_dx;
+  }
   out_grad_block(a, id, (float*)smem_raw);
 }
 
@@ -787,6 +792,120 @@ __global__ __launch_bounds__(256) void conv2_wgrad_k(MnistStepArgs a, int kper) 
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   conv2_wgrad_block(a, blockIdx.x % C2W_GX, blockIdx.x / C2W_GX, kper, (bf16*)smem_raw);
 }
+// ---------------- K14 (LDS-staged): conv2 wgrad (+ K12 bias row) ----------------
+// Block = (tap group tg, image pair ip), 512 threads; 4 x 64 = 256 blocks at B = 128 (one per CU).
+// Per image: p1 (14x14x32) goes into a zero-bordered LDS image [18][18] x 40 ch and dz2 (196 x 64)
+// into LDS rows [224][72] (pixel rows 196..223 zero); then dW[tap*32 + ci][co] += sum_px
+// p1[px + tap][ci] * dz2[px][co] on MFMA with BOTH fragments read by ds_read_b64_tr_b16 (rows =
+// pixels), so the im2col shift of a tap is just a per-lane row address. Wave w owns ci-tile
+// w >> 2, co-tile w & 3 and every tap of its group. One fp32 slab per image pair (rows of its tap
+// group; tap group 0 also the bias row 800), reduced by the optimizer tail / reduce_conv_grads.
+// Replaces the im2col GEMM that re-read p1 25x through L2 (83 MB -> 19 MB of staging).
+constexpr int C2WL_IMG = 2;                 // images per block
+constexpr int C2WL_NTG = 4;                 // tap groups: [0,6) [6,12) [12,18) [18,25)
+constexpr int C2WL_MAXT = 7;
+constexpr int C2WL_CS = 40, C2WL_PW = 18;   // padded image: 18 x 18 positions x 40-ch stride
+constexpr int C2WL_DS = 72, C2WL_KP = 224;  // dz2 rows: pixels padded to 7 k-steps of 32
+constexpr int C2WL_IMG_ELEMS = C2WL_PW * C2WL_PW * C2WL_CS;
+constexpr int C2WL_BRED_OFF = (C2WL_IMG_ELEMS + C2WL_KP * C2WL_DS) * 2;
+constexpr int C2WL_SMEM = C2WL_BRED_OFF + 8 * 64 * 4;  // 60224 B: two blocks per CU
+static_assert(C2WL_BRED_OFF % 16 == 0 && (C2WL_IMG_ELEMS * 2) % 16 == 0, "LDS carve alignment");
+__global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16* img = (bf16*)smem_raw;
+  bf16* dz = img + C2WL_IMG_ELEMS;
+  float* bred = reinterpret_cast<float*>(smem_raw + C2WL_BRED_OFF);  // [8][64]
+  const int tg = blockIdx.x % C2WL_NTG, ip = blockIdx.x / C2WL_NTG, t = threadIdx.x;
+  const int tap0 = tg * 6, ntaps = (tg == C2WL_NTG - 1) ? 25 - tap0 : 6;
+  const int lane = t & 63, w = t >> 6, h = w >> 2, n = w & 3, g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  // the image border and the dz2 pad rows stay zero for every image of the block
+  for (int i = t; i < C2WL_PW * C2WL_PW; i += 512) {
+    const int r = i / C2WL_PW, c = i - r * C2WL_PW;
+    if (r < 2 || r >= 16 || c < 2 || c >= 16) {
+      uint4* d = reinterpret_cast<uint4*>(img + i * C2WL_CS);
+      d[0] = zero4(); d[1] = zero4(); d[2] = zero4(); d[3] = zero4();
+    }
+  }
+  for (int i = t; i < (C2WL_KP - 196) * (C2WL_DS / 8); i += 512) reinterpret_cast<uint4*>(dz + 196 * C2WL_DS)[i] = zero4();
+  // padded-image positions of this lane's two tr-read rows (pixels 32s + 8g + q and +4) per k-step
+  int pos[7][2];
+#pragma unroll
+  for (int s = 0; s < 7; ++s)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = 32 * s + 8 * g + q + 4 * u;
+      pos[s][u] = k < 196 ? (k / 14) * C2WL_PW + (k % 14) : 0;  // pad pixels: dz2 rows are zero
+    }
+  f32x4 acc[C2WL_MAXT];
+#pragma unroll
+  for (int j = 0; j < C2WL_MAXT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  for (int ii = 0; ii < C2WL_IMG; ++ii) {
+    const int b = ip * C2WL_IMG + ii;
+    if (b >= a.B) break;
+    __syncthreads();  // the previous image's fragments are consumed
+    {
+      const uint4* s1 = reinterpret_cast<const uint4*>(a.p1 + (size_t)b * 196 * 32);
+      const uint4* s2 = reinterpret_cast<const uint4*>(a.dz2 + (size_t)b * 196 * 64);
+      uint4 v1[2], v2[4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) { const int i = t + 512 * j; v1[j] = i < 784 ? s1[i] : zero4(); }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { const int i = t + 512 * j; v2[j] = i < 1568 ? s2[i] : zero4(); }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int i = t + 512 * j;
+        if (i < 784) {
+          const int px = i >> 2, ch = i & 3, r = px / 14, c = px - r * 14;
+          *reinterpret_cast<uint4*>(img + ((r + 2) * C2WL_PW + c + 2) * C2WL_CS + ch * 8) = v1[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = t + 512 * j;
+        if (i < 1568) *reinterpret_cast<uint4*>(dz + (i >> 3) * C2WL_DS + (i & 7) * 8) = v2[j];
+      }
+    }
+    __syncthreads();
+    if (tg == 0) {  // bias row: column sums of dz2 (pixel slice t >> 6 of 8)
+      for (int px = t >> 6; px < 196; px += 8) bsum += bf2f(dz[px * C2WL_DS + (t & 63)]);
+    }
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const bf16* bp0 = dz + (32 * s + 8 * g + q) * C2WL_DS + 16 * n + 4 * p4;
+      const bf16x8 bfr = frag_tr16(bp0, bp0 + 4 * C2WL_DS);
+#pragma unroll
+      for (int j = 0; j < C2WL_MAXT; ++j) {
+        if (j < ntaps) {
+          const int tap = tap0 + j, toff = (tap / 5) * C2WL_PW + (tap % 5);
+          const bf16* a0 = img + (pos[s][0] + toff) * C2WL_CS + 16 * h + 4 * p4;
+          const bf16* a1 = img + (pos[s][1] + toff) * C2WL_CS + 16 * h + 4 * p4;
+          acc[j] = mfma16x16x32(frag_tr16(a0, a1), bfr, acc[j]);
+        }
+      }
+    }
+  }
+  float* slab = a.wg2_slab + (size_t)ip * 801 * 64;
+#pragma unroll
+  for (int j = 0; j < C2WL_MAXT; ++j) {
+    if (j < ntaps) {
+      const int tap = tap0 + j;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) slab[(size_t)(tap * 32 + 16 * h + 4 * g + r) * 64 + 16 * n + (lane & 15)] = acc[j][r];
+    }
+  }
+  if (tg == 0) {
+    bred[(t >> 6) * 64 + (t & 63)] = bsum;
+    __syncthreads();
+    if (t < 64) {
+      float sm = 0.f;
+#pragma unroll
+      for (int sl = 0; sl < 8; ++sl) sm += bred[sl * 64 + t];
+      slab[800 * 64 + t] = sm;
+    }
+  }
+}
+
 // K13 + K14 in one launch: conv2 dgrad and wgrad both consume dz2 only (independent).
 __global__ __launch_bounds__(256) void conv2_bwd(MnistStepArgs a, int n_dgrad, int kper) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -875,7 +994,7 @@ __device__ __forceinline__ void reduce_chunk(const float* __restrict__ slab, int
     out[i] = r;
   }
 }
-constexpr int RED2_BLOCKS = (801 * 64 + 63) / 64;  // 801 blocks x 64 outputs (4 phases over ~25 slabs)
+constexpr int RED2_BLOCKS = (801 * 64 + 63) / 64;  // 801 blocks x 64 outputs (4 phases over the B/2 slabs)
 constexpr int RED1_BLOCKS = (832 + 15) / 16;       // 52 blocks x 16 outputs (16 phases over 2B slabs)
 __global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a) {
   __shared__ float red[256];
@@ -885,6 +1004,76 @@ __global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a) {
   else
     reduce_chunk<16>(a.wg1_slab, 2 * a.B, 832, 832, (id - RED2_BLOCKS) * 16, a.grad + OFF_WC1, red);
   if (id == 0 && threadIdx.x == 0 && a.step_bump) *a.step_bump += 1;  // see MnistStepArgs::step_bump
+}
+
+// ---------------- one-GPU optimizer tail: K16 ApplyAdam with the K12/K14/K15 slab reduce fused ----------------
+// Grid = [208 conv1 blocks | 801 conv2 blocks | MAD_FC_BLOCKS grid-stride blocks]:
+//   conv1: block j owns float4 j of the 832 conv1 weight/bias gradients, one slab (of 2B) per thread;
+//   conv2: block owns 16 float4s, a 16-lane group per float4 sums slabs l, l + 16, ... (independent
+//          loads, fixed order) then a 16-lane butterfly;
+//   fc:    plain grid-stride Adam over the flat gradient buffer.
+// Every gradient reduction is deterministic. t comes from the head kernel (MnistStepArgs::t_out),
+// so nothing here reads the global_step that the last block bumps.
+constexpr int MAD_NT = 256;
+constexpr int MAD_C1F4 = (int)(OFF_WC2 / 4);   // 208
+constexpr int MAD_C2END = (int)(OFF_WD1 / 4);  // 13024
+constexpr int MAD_C2BLK = (MAD_C2END - MAD_C1F4 + 15) / 16;  // 801
+constexpr int MAD_FC_BLOCKS = 1024;
+constexpr int MAD_GRID = MAD_C1F4 + MAD_C2BLK + MAD_FC_BLOCKS;
+__device__ __forceinline__ void adam4(const MnistAdamArgs& o, int64_t i, f32x4 g, float lr_t, float c1, float c2) {
+  f32x4 p = reinterpret_cast<f32x4*>(o.p)[i];
+  f32x4 m = reinterpret_cast<f32x4*>(o.m)[i];
+  f32x4 v = reinterpret_cast<f32x4*>(o.v)[i];
+  m = m + (g - m) * c1;
+  v = v + (g * g - v) * c2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) p[j] -= lr_t * m[j] / (sqrtf(v[j]) + o.eps);
+  reinterpret_cast<f32x4*>(o.p)[i] = p;
+  reinterpret_cast<f32x4*>(o.m)[i] = m;
+  reinterpret_cast<f32x4*>(o.v)[i] = v;
+  reinterpret_cast<uint2*>(o.pbf)[i] = make_uint2(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]));
+}
+__global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, MnistAdamArgs o) {
+  const int64_t t = *o.t;
+  const float b1p = powf(o.beta1, (float)t), b2p = powf(o.beta2, (float)t);
+  const float lr_t = o.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  const float c1 = 1.f - o.beta1, c2 = 1.f - o.beta2;
+  const int bid = blockIdx.x, tid = threadIdx.x;
+  if (bid < MAD_C1F4) {
+    __shared__ f32x4 red[MAD_NT / 64];
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = tid; q < 2 * a.B; q += MAD_NT) s += reinterpret_cast<const f32x4*>(a.wg1_slab + (size_t)q * 832)[bid];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] = wave_sum(s[j]);
+    if ((tid & 63) == 0) red[tid >> 6] = s;
+    __syncthreads();
+    if (tid == 0) adam4(o, bid, (red[0] + red[1]) + (red[2] + red[3]), lr_t, c1, c2);
+  } else if (bid < MAD_C1F4 + MAD_C2BLK) {
+    constexpr int64_t SLAB4 = 801 * 64 / 4;
+    const int64_t i = MAD_C1F4 + (int64_t)(bid - MAD_C1F4) * 16 + (tid >> 4);
+    const int sl = tid & 15, ns = a.wg2_splits;
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(a.wg2_slab) + (i - MAD_C1F4);
+    f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f}, g1 = g0;
+    if (i < MAD_C2END) {
+      int k = sl;
+      for (; k + 16 < ns; k += 32) {  // two independent loads in flight per lane
+        g0 += s4[(size_t)k * SLAB4];
+        g1 += s4[(size_t)(k + 16) * SLAB4];
+      }
+      if (k < ns) g0 += s4[(size_t)k * SLAB4];
+    }
+    f32x4 g = g0 + g1;
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] += __shfl_xor(g[j], off, 16);
+    if (sl == 0 && i < MAD_C2END) adam4(o, i, g, lr_t, c1, c2);
+  } else {
+    for (int64_t i = MAD_C2END + (int64_t)(bid - MAD_C1F4 - MAD_C2BLK) * MAD_NT + tid; i < TOTAL / 4;
+         i += (int64_t)MAD_FC_BLOCKS * MAD_NT)
+      adam4(o, i, reinterpret_cast<const f32x4*>(a.grad)[i], lr_t, c1, c2);
+    if (bid == MAD_GRID - 1 && tid == 0) *o.step += 1;  // see MnistAdamArgs
+  }
 }
 
 template <auto K>
@@ -899,6 +1088,9 @@ inline void set_smem(int bytes) {
 
 int mnist_fc1_splits(int B) { (void)B; return FC1_SPLITS; }
 int mnist_wg2_splits(int B) {
+#if TFD_CONV2_LDS
+  return (B + C2WL_IMG - 1) / C2WL_IMG;  // one slab per image pair (conv2_wgrad_lds)
+#endif
   const int K = B * 196;
   const int kper = TFD_C2W_KPER;
   return (K + kper - 1) / kper;
@@ -936,7 +1128,7 @@ void mnist_forward_fc(const MnistStepArgs& a, bool train, hipStream_t s) {
   head_kernel<<<B, 256, 0, s>>>(a, train ? 1 : 0);
 }
 
-void mnist_backward_a(const MnistStepArgs& a, hipStream_t s) {
+void mnist_backward_a(const MnistStepArgs& a, hipStream_t s, int part) {
   const int B = a.B;
   constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, DenseLoader<false>>::BYTES;
   constexpr int sm_dx = GemmSmem<FDX_BM, FDX_BN, FDX_BK, DenseLoader<true>, DenseLoader<true>>::BYTES;
@@ -944,7 +1136,8 @@ void mnist_backward_a(const MnistStepArgs& a, hipStream_t s) {
   const int sm = std::max(std::max(sm_dw, sm_dx), sm_og);
   set_smem<fc1_bwd>(sm);
   const int n_dx = FDX_GX * ((B + FDX_BM - 1) / FDX_BM);
-  fc1_bwd<<<FDW_GX * FDW_GY + n_dx + OUTG_BLOCKS, 256, sm, s>>>(a, n_dx);
+  const int nb = part == 2 ? n_dx : FDW_GX * FDW_GY + (part == 0 ? n_dx : 0) + OUTG_BLOCKS;
+  fc1_bwd<<<nb, 256, sm, s>>>(a, n_dx, part);
 }
 
 void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
@@ -952,12 +1145,11 @@ void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux, hi
   const int K = B * 196;
   const int kper = ((K + a.wg2_splits - 1) / a.wg2_splits + C2W_BK - 1) / C2W_BK * C2W_BK;
 #if TFD_CONV2_LDS
-  // conv2 wgrad (slabs) runs on the aux stream beside dgrad -> conv1 wgrad (both only need dz2/p1)
-  constexpr int sm_w = GemmSmem<C2W_BM, C2W_BN, C2W_BK, Conv2WgradA, DenseLoader<false>>::BYTES;
-  set_smem<conv2_wgrad_k>(sm_w);
+  // conv2 wgrad (one slab per image pair) optionally on the aux stream beside dgrad + conv1 wgrad
+  (void)kper;
   hipStream_t ws = aux ? aux : s;
   if (aux) { (void)hipEventRecord(fork, s); (void)hipStreamWaitEvent(aux, fork, 0); }
-  conv2_wgrad_k<<<C2W_GX * a.wg2_splits, 256, sm_w, ws>>>(a, kper);
+  conv2_wgrad_lds<<<C2WL_NTG * a.wg2_splits, 512, C2WL_SMEM, ws>>>(a);
   set_smem<conv2_dgrad_lds>(C2D_SMEM);
   conv2_dgrad_lds<<<2 * B, 512, C2D_SMEM, s>>>(a);  // + conv1 wgrad (fused tail)
   if (aux) { (void)hipEventRecord(join, aux); (void)hipStreamWaitEvent(s, join, 0); }
@@ -977,6 +1169,10 @@ void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux, hi
 
 void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s) {
   reduce_conv_grads<<<RED2_BLOCKS + RED1_BLOCKS, 256, 0, s>>>(a);
+}
+
+void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s) {
+  mnist_adam_kernel<<<MAD_GRID, MAD_NT, 0, s>>>(a, o);
 }
 
 }  // namespace tfd

@@ -45,6 +45,7 @@ class MnistEngine : public torch::CustomClassHolder {
     v_ = at::zeros({TOTAL}, f32);
     gbf_ = at::zeros({TOTAL}, bf);
     step_ = at::zeros({1}, i64);
+    tnext_ = at::zeros({1}, i64);
     fc1_splits_ = mnist_fc1_splits((int)B_);
     wg2_splits_ = mnist_wg2_splits((int)B_);
     p1_ = at::empty({B_, P1H, P1H, C1}, bf);
@@ -169,6 +170,7 @@ class MnistEngine : public torch::CustomClassHolder {
   void set_opt_overlap(int64_t on) { opt_overlap_ = on; }
   // conv2 wgrad on a forked stream beside dgrad -> conv1 wgrad (1) or all on the main stream (0)
   void set_conv_fork(int64_t on) { conv_fork_ = on != 0; }
+  void set_fused_tail(int64_t on) { fuse_tail_ = on != 0; }
   // make every rank's bf16 shadow whole again (after the last zero step, before eval/checkpoint)
   void sync_params() {
     if (!zero_) return;
@@ -224,24 +226,42 @@ class MnistEngine : public torch::CustomClassHolder {
     hipStream_t s = stream();
     const bool dp = world() > 1;
     const double scale = dp ? 1.0 / (double)world() : 1.0;
-    forward(true);
-    MnistStepArgs a = args();
-    if (fused_bf16_a()) a.gbf_a = (uint16_t*)gbf_.data_ptr();
-    mnist_backward_a(a, s);
-    a.step_bump = (int64_t*)step_.data_ptr();
     hipStream_t ws = conv_fork_ ? aux_stream_ : nullptr;
+    MnistStepArgs a = args();
     if (!dp && !opt_overlap_) {
+      // one GPU: nothing to overlap with. With Adam ONE kernel ends the step: it reduces the conv
+      // weight-gradient slabs itself and bumps the step (its t was written by the head kernel).
+      const bool fused = opt_ == 0 && fuse_tail_;
+      if (fused) a.t_out = (int64_t*)tnext_.data_ptr();
+      mnist_forward(a, true, s);
+      mnist_backward_a(a, s);
+      a.step_bump = (int64_t*)step_.data_ptr();
       mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
-      mnist_conv_grad_reduce(a, s);
-      apply_optimizer_range(0, TOTAL, scale, 0, s);
+      if (fused) {
+        MnistAdamArgs o{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(),
+                        (uint16_t*)pbf_.data_ptr(), (float)lr_, (float)b1_, (float)b2_, (float)eps_,
+                        (const int64_t*)tnext_.data_ptr(), (int64_t*)step_.data_ptr()};
+        mnist_adam_fused(a, o, s);
+      } else {
+        mnist_conv_grad_reduce(a, s);
+        apply_optimizer_range(0, TOTAL, scale, 0, s);
+      }
       return;
     }
+    mnist_forward(a, true, s);
+    if (fused_bf16_a()) a.gbf_a = (uint16_t*)gbf_.data_ptr();
+    // DP: dW + out-layer grads first, so bucket A's all-reduce starts before the dX GEMM (not with
+    // opt_overlap_, whose region-A optimizer would rewrite the weights dX reads)
+    const bool split = dp && !opt_overlap_;
+    mnist_backward_a(a, s, split ? 1 : 0);
+    a.step_bump = (int64_t*)step_.data_ptr();
     HIP_OK(hipEventRecord(ev_a_, s));
     hipStream_t os = dp ? comm_stream_ : opt_stream_;
     HIP_OK(hipStreamWaitEvent(os, ev_a_, 0));
     if (dp) reduce_bucket(BUCKET_SPLIT, TOTAL);
     if (opt_overlap_) apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 1, os);
     HIP_OK(hipEventRecord(ev_opt_a_, os));
+    if (split) mnist_backward_a(a, s, 2);
     mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
     if (opt_overlap_) HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
     mnist_conv_grad_reduce(a, s);
@@ -476,7 +496,7 @@ class MnistEngine : public torch::CustomClassHolder {
   c10::intrusive_ptr<RcclComm> comm_;
   c10::intrusive_ptr<IpcComm> ipc_;
   int64_t ipc_small_ = 0;
-  at::Tensor params_, pbf_, grad_, m_, v_, gbf_, step_;
+  at::Tensor params_, pbf_, grad_, m_, v_, gbf_, step_, tnext_;
   at::Tensor p1_, idx1_, p2_, idx2_, fc1_slab_, hd_, dh_, dlogits_, loss_row_, correct_row_, dz2_, dp1m_, wg2_slab_,
       wg1_slab_, xbuf_, ybuf_;
   at::Tensor data_, labels_, perm_;
@@ -491,6 +511,8 @@ class MnistEngine : public torch::CustomClassHolder {
   int64_t opt_overlap_ = 0;
   // measured on one MI355X: the forked conv2 wgrad only contends with dgrad for CUs (110 vs 100 us/step)
   bool conv_fork_ = false;
+  // one GPU + Adam: the optimizer kernel also reduces the conv gradient slabs and bumps the step
+  bool fuse_tail_ = true;
   std::map<std::string, hipGraphExec_t> graphs_;
 };
 
@@ -534,6 +556,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_zero", &MnistEngine::set_zero)
       .def("set_opt_overlap", &MnistEngine::set_opt_overlap)
       .def("set_conv_fork", &MnistEngine::set_conv_fork)
+      .def("set_fused_tail", &MnistEngine::set_fused_tail)
       .def("zero", &MnistEngine::zero)
       .def("sync_params", &MnistEngine::sync_params)
       .def("world", &MnistEngine::world)

@@ -16,6 +16,8 @@ struct MnistStepArgs {
   const int* perm;
   int n_data;
   const int64_t* step;         // device global_step (read by every kernel of the step)
+  int64_t* t_out;              // if set, the head kernel writes *step + 1 here: Adam's t for the fused
+                               // one-GPU optimizer tail, which bumps *step itself (mnist_adam_fused)
   int64_t* step_bump;          // if set, the last conv-grad reduce kernel increments *step (it is the
                                // first kernel of the step that no longer reads it; the optimizer after it
                                // then sees t = global_step + 1 directly)
@@ -47,13 +49,26 @@ int mnist_wg2_splits(int B);
 void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s);        // conv1, conv2, fc1, head
 void mnist_forward_conv(const MnistStepArgs& a, hipStream_t s);               // conv1, conv2 (read region B)
 void mnist_forward_fc(const MnistStepArgs& a, bool train, hipStream_t s);     // fc1, head (read region A)
-void mnist_backward_a(const MnistStepArgs& a, hipStream_t s);                 // fc1 dW/dX -> bucket A done
+// fc1 dW/dX + out-layer grads. part 0: one launch; part 1: dW + out grads (bucket A complete);
+// part 2: dX (DP launches 1 then 2 so bucket A's all-reduce starts before the dX GEMM)
+void mnist_backward_a(const MnistStepArgs& a, hipStream_t s, int part = 0);
 // conv2/conv1 grads -> bucket B done. With `aux` set, independent kernels fork onto it (fork/join
 // events recorded on s/aux; both are captured into the step graph as parallel branches).
 void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux = nullptr, hipEvent_t fork = nullptr,
                       hipEvent_t join = nullptr);
 // deterministic conv weight-gradient slab reduction (+ the global_step bump, MnistStepArgs::step_bump)
 void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s);
+
+// One-GPU optimizer tail: TF ApplyAdam over the whole flat buffer with the conv weight-gradient
+// slab reduction fused in (the conv region takes its gradient straight from the per-block slabs),
+// t = *t (written by the head kernel, MnistStepArgs::t_out), *step bumped once by the kernel.
+struct MnistAdamArgs {
+  float* p; float* m; float* v; uint16_t* pbf;
+  float lr, beta1, beta2, eps;
+  const int64_t* t;
+  int64_t* step;
+};
+void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s);
 
 // ---------------- optimizers (flat, fp32 master + bf16 shadow) ----------------
 struct AdamArgs {

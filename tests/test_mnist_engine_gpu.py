@@ -136,3 +136,35 @@ def test_training_reduces_loss(cuda):
         r1 = eng.evaluate(data[:1000], labels[:1000]).cpu()
     torch.cuda.synchronize()
     assert r1[1] > r0[1] and r1[1] >= 800, (r0, r1)
+
+
+def test_fused_adam_tail_matches_unfused(cuda):
+    """One-GPU step whose Adam kernel also reduces the conv grad slabs (set_fused_tail) == the
+    reduce kernel + plain Adam path, up to the slab summation order."""
+    B = 128
+    params = M.flat_from_dict(M.init_params(13)).to(cuda) * 0.05
+    n = 1024
+    data = torch.rand(n, 784, device=cuda)
+    labels = torch.randint(0, 10, (n,), dtype=torch.int32, device=cuda)
+    perm = torch.randperm(n, device=cuda).to(torch.int32)
+    engs = []
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for fused in (1, 0):
+            e = _engine(B, cuda, keep=0.75)
+            e.set_adam(0.01, 0.9, 0.999, 1e-8)
+            e.set_fused_tail(fused)
+            e.params().copy_(params)
+            e.sync_shadow()
+            e.set_dataset(data, labels, perm)
+            e.set_input_mode(1)
+            engs.append(e)
+        for e in engs:
+            for _ in range(3):
+                e.train_step()
+    torch.cuda.synchronize()
+    assert [int(e.step_tensor().item()) for e in engs] == [3, 3]
+    d0 = engs[0].params() - params
+    d1 = engs[1].params() - params
+    assert _relerr(d0, d1) < 1e-2, _relerr(d0, d1)
+    assert torch.equal(engs[0].params_bf16(), engs[0].params().to(torch.bfloat16))

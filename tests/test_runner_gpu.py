@@ -85,6 +85,7 @@ def test_backup_worker_primitives_world1(cuda):
     b = NativeMnistRunner(B, AdamOptimizer(0.01), keep_prob=1.0, device=cuda, use_graph=False)
     for r in (a, b):
         r.load_flat(_params(), {}, 0)
+    a.eng.set_fused_tail(0)  # same conv-grad slab summation order as reduce_grads' path
     a.train_step(x, y)
     g, _ = b.compute_grads(x, y)
     b.reduce_grads(2.0)
