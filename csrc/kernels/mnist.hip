@@ -192,32 +192,35 @@ __global__ __launch_bounds__(256) void conv2_pool_fwd(MnistStepArgs a) {
 }
 
 // ---------------- K2 (LDS-staged): whole-image implicit GEMM ----------------
-// Block = image b, 512 threads (8 waves), 152 KiB LDS. The image's 14x14x32 bf16 activations are
-// staged ONCE into a zero-bordered, channel-chunk-major LDS image [4 chunks][18 rows][24 cols]
-// x 16 B, and W2 as [800 k][64 n + 16] rows; every im2col A fragment is then one ds_read_b128 at
+// Block = (image b, output-channel half nh), 512 threads (8 waves), 102 KiB LDS: 2B blocks (256 at
+// B = 128, every CU busy). The image's 14x14x32 bf16 activations are staged into a zero-bordered,
+// channel-chunk-major LDS image [4 chunks][18 rows][24 cols] x 16 B and the block's half of W2
+// as [800 k][32 n + 16] rows; every im2col A fragment is then one ds_read_b128 at
 // (pixel(m) + tap offset) -- no global re-reads of the 25x-expanded im2col matrix. Row stride
 // 24 px = 8 (mod 16) 16-B slots and 256-B-multiple chunk planes make the pool-window-ordered A
 // reads of a 16-lane group hit 16 distinct slots. M = 196 rows in pool-window-major order
-// (13 tiles), N = 64 (4 tiles), K = 800 (25 taps x 32 ci = one MFMA k-step per tap). Wave w owns
-// N-tiles {2(w & 1), 2(w & 1) + 1} and M-tiles {w >> 1, +4, +8, +12}: per tap 2 B + <=4 A fragment
-// reads feed <=8 MFMAs. Each lane's 4 accumulator rows are one 2x2 pool window, so bias + relu +
-// maxpool + argmax happen in registers.
-constexpr int C2F_W = 24, C2F_PLANE = 18 * C2F_W, C2F_WLD = 80;
-constexpr int C2L_FWD_SMEM = (4 * C2F_PLANE * 8 + 800 * C2F_WLD) * 2;  // 155648 B
+// (13 tiles), N = 32 (2 tiles), K = 800 (25 taps x 32 ci = one MFMA k-step per tap). Wave w owns
+// M-tiles {w, w + 8} and both N-tiles: per tap 2 B + <= 2 A fragment reads feed <= 4 MFMAs.
+// Each lane's 4 accumulator rows are one 2x2 pool window, so bias + relu + maxpool + argmax
+// happen in registers. (The per-image block of 64 channels used only 128 CUs at B = 128 and
+// staged 129 KB per CU; this split stages 78 KB per CU on all 256.)
+constexpr int C2F_W = 24, C2F_PLANE = 18 * C2F_W, C2F_WLD = 48;
+constexpr int C2L_FWD_SMEM = (4 * C2F_PLANE * 8 + 800 * C2F_WLD) * 2;  // 104448 B
 static_assert(C2F_PLANE * 16 % 256 == 0, "chunk planes must be bank-row aligned");
 __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* img = (bf16*)smem_raw;                        // [4][18*24][8]
-  bf16* wt = img + 4 * C2F_PLANE * 8;                 // [800][80]
-  const int b = blockIdx.x, t = threadIdx.x;
+  bf16* wt = img + 4 * C2F_PLANE * 8;                 // [800][48] (32 used)
+  const int b = blockIdx.x >> 1, nh = blockIdx.x & 1, t = threadIdx.x;
   // Staging: every thread issues ALL of its 16-B loads before its first LDS store (a load->store
   // loop serialises one global latency per iteration).
   const uint16_t* src = a.p1 + (size_t)b * 196 * 32;
-  const uint16_t* wsrc = a.pbf + OFF_WC2;
-  const int rot = TFD_WROT ? (int)((blockIdx.x * 1031u) % 6400u) : 0;  // per-block start: spread L2 channels
+  const uint16_t* wsrc = a.pbf + OFF_WC2 + nh * 32;
+  const int rot = TFD_WROT ? (int)((blockIdx.x * 1031u) % 3200u) : 0;  // per-block start: spread L2 channels
   {
     constexpr int CI = 4 * C2F_PLANE, NI = (CI + 511) / 512;  // 1728 chunks -> 4 per thread
-    uint4 vi[NI];
+    constexpr int NW = (3200 + 511) / 512;                    // 800 rows x 4 chunks -> 7 per thread
+    uint4 vi[NI], vw[NW];
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int i = t + 512 * j, ch = i / C2F_PLANE, px = i - ch * C2F_PLANE;
@@ -226,19 +229,14 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
                   ? *reinterpret_cast<const uint4*>(src + (r * 14 + c) * 32 + ch * 8) : zero4();
     }
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      constexpr int NH = (3200 + 511) / 512;  // 800 rows x 8 chunks, two passes of 3200
-      uint4 vw[NH];
+    for (int j = 0; j < NW; ++j) {
+      const int i = (t + 512 * j + rot) % 3200;
+      vw[j] = (t + 512 * j < 3200) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 2) * 64 + (i & 3) * 8) : zero4();
+    }
 #pragma unroll
-      for (int j = 0; j < NH; ++j) {
-        const int i = (half * 3200 + t + 512 * j + rot) % 6400;
-        vw[j] = (t + 512 * j < 3200) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 3) * 64 + (i & 7) * 8) : zero4();
-      }
-#pragma unroll
-      for (int j = 0; j < NH; ++j) {
-        const int i = (half * 3200 + t + 512 * j + rot) % 6400;
-        if (t + 512 * j < 3200) *reinterpret_cast<uint4*>(wt + (i >> 3) * C2F_WLD + (i & 7) * 8) = vw[j];
-      }
+    for (int j = 0; j < NW; ++j) {
+      const int i = (t + 512 * j + rot) % 3200;
+      if (t + 512 * j < 3200) *reinterpret_cast<uint4*>(wt + (i >> 2) * C2F_WLD + (i & 3) * 8) = vw[j];
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -247,14 +245,14 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
     }
   }
   __syncthreads();
-  const int lane = t & 63, w = t >> 6, np = w & 1, g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
-  const int mt0 = w >> 1, njt = (mt0 + 12 < 13) ? 4 : 3;
-  int base[4];
-  f32x4 acc[4][2];
+  const int lane = t & 63, w = t >> 6, g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  const int nmt = (w + 8 < 13) ? 2 : 1;
+  int base[2];
+  f32x4 acc[2][2];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < 2; ++j) {
     acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int m = (mt0 + 4 * j) * 16 + (lane & 15);
+    const int m = (w + 8 * j) * 16 + (lane & 15);
     int px = 0;
     if (m < 196) {
       const int pp = m >> 2, win = m & 3;
@@ -262,7 +260,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
     }
     base[j] = (g * C2F_PLANE + px) * 8;
   }
-  const bf16* wcol = wt + (8 * g + q) * C2F_WLD + np * 32 + 4 * p4;
+  const bf16* wcol = wt + (8 * g + q) * C2F_WLD + 4 * p4;
 #pragma unroll
   for (int kh = 0; kh < (TFD_EXP_SKIP_MAIN ? 0 : 5); ++kh) {
 #pragma unroll
@@ -272,8 +270,8 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
       const bf16x8 b0 = frag_tr16(wr, wr + 4 * C2F_WLD);
       const bf16x8 b1 = frag_tr16(wr + 16, wr + 16 + 4 * C2F_WLD);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (j < njt) {
+      for (int j = 0; j < 2; ++j)
+        if (j < nmt) {
           const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + base[j] + toff);
           acc[j][0] = mfma16x16x32(af, b0, acc[j][0]);
           acc[j][1] = mfma16x16x32(af, b1, acc[j][1]);
@@ -282,12 +280,12 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
   }
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
-    const int n = np * 32 + nt * 16 + (lane & 15);
+    const int n = nh * 32 + nt * 16 + (lane & 15);
     const float bb = a.p32[OFF_BC2 + n];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m4 = (mt0 + 4 * j) * 16 + 4 * g;
-      if (j >= njt || m4 >= 196) continue;
+    for (int j = 0; j < 2; ++j) {
+      const int m4 = (w + 8 * j) * 16 + 4 * g;
+      if (j >= nmt || m4 >= 196) continue;
       float mx = acc[j][nt][0] + bb;
       int am = 0;
 #pragma unroll
@@ -1106,7 +1104,7 @@ void mnist_forward_conv(const MnistStepArgs& a, hipStream_t s) {
   conv1_pool_fwd<<<4 * B, 256, 0, s>>>(a);
 #if TFD_CONV2_LDS
   set_smem<conv2_fwd_lds>(C2L_FWD_SMEM);
-  conv2_fwd_lds<<<B, 512, C2L_FWD_SMEM, s>>>(a);
+  conv2_fwd_lds<<<2 * B, 512, C2L_FWD_SMEM, s>>>(a);
 #else
   {
     constexpr int sm = GemmSmem<C2F_BM, C2F_BN, C2F_BK, Conv2FwdA, C2F_B>::BYTES;
