@@ -62,7 +62,7 @@ def _backup_worker(rank, world, r2a, slow_rank):
     if rank == 0:
         r.load_flat(M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(9).items()}), {}, 0)
     broadcast_state(r, 0)
-    st = SyncReplicasStepper(r, rank, world, r2a, straggler_delay_s={slow_rank: 0.5})
+    st = SyncReplicasStepper(r, rank, world, r2a, straggler_delay_s={slow_rank: 3.0})
     x, y = _data(B * world, 3)
     st.step(x[rank * B:(rank + 1) * B], y[rank * B:(rank + 1) * B])
     return r.params().clone(), st.last_contributors
