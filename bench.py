@@ -41,6 +41,8 @@ def main(argv=None):
     ap.add_argument("--zero", type=int, default=0, help="1: ZeRO-1 sharding of the fc1 weight (N > 1)")
     ap.add_argument("--fused_tail", type=int, default=1, help="1: on one GPU the Adam kernel also reduces the "
                     "conv weight-gradient slabs and bumps the step (one kernel less)")
+    ap.add_argument("--local_bf16_grads", type=int, default=1, help="1: on one GPU keep the fc-region gradients "
+                    "in bf16 (the DP all-reduce wire format): fc backward writes and Adam reads 2 B per gradient")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu", action="store_true", help="plumbing dry-run: fp32 PyTorch CPU runner + Gloo "
@@ -67,6 +69,7 @@ def main(argv=None):
     eng.set_opt_overlap(a.opt_overlap)
     eng.set_conv_fork(a.conv_fork)
     eng.set_fused_tail(a.fused_tail)
+    eng.set_local_bf16_grads(a.local_bf16_grads)
     ipc_state = "off"
     if ctx.comm is not None:
         eng.set_comm(ctx.comm, not a.fp32_grads)
@@ -147,6 +150,7 @@ def main(argv=None):
                 "hipgraph": graph_mode,
                 "small_bucket_allreduce": ipc_state,
                 "zero1_fc1": bool(a.zero),
+                "fc_grads": "bf16" if (a.local_bf16_grads or world > 1) and not a.fp32_grads else "fp32",
             },
         }), flush=True)
     ctx.shutdown()

@@ -46,18 +46,26 @@ at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
   return y;
 }
 
-at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, at::IntArrayRef xshape, int64_t stride, int64_t pad) {
+at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, at::IntArrayRef xshape, int64_t stride, int64_t pad,
+                        const c10::optional<at::Tensor>& acc) {
   check_bf16(dy, "dy", 4);
   check_bf16(w, "w", 4);
   TORCH_CHECK(xshape.size() == 4, "xshape [N,H,W,C]");
-  auto x = at::empty(xshape, dy.options());
+  at::Tensor x;
+  if (acc.has_value()) {  // dx = acc + dgrad, in place
+    x = *acc;
+    check_bf16(x, "acc", 4);
+    TORCH_CHECK(x.sizes() == xshape, "dgrad: acc shape must equal xshape");
+  } else {
+    x = at::empty(xshape, dy.options());
+  }
   const ConvShape c = shape_of(x, w, stride, pad);
   TORCH_CHECK(dy.size(1) == c.Ho() && dy.size(2) == c.Wo() && dy.size(3) == c.K, "dgrad: dy shape mismatch");
-  conv_dgrad(c, bp(dy), bp(w), bp(x), cur());
+  conv_dgrad(c, bp(dy), bp(w), bp(x), cur(), acc.has_value());
   return x;
 }
 
-void conv2d_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, int64_t stride, int64_t pad) {
+void conv2d_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, int64_t stride, int64_t pad, bool zeroed) {
   check_bf16(x, "x", 4);
   check_bf16(dy, "dy", 4);
   check_f32(dw, "dw");
@@ -66,7 +74,7 @@ void conv2d_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, int6
   const ConvShape c = shape_of(x, wfake, stride, pad);
   TORCH_CHECK(dy.size(0) == c.N && dy.size(1) == c.Ho() && dy.size(2) == c.Wo() && dy.size(3) == c.K,
               "wgrad: dy shape mismatch");
-  conv_wgrad(c, bp(x), bp(dy), fp(dw), conv_wgrad_splits(c), cur());
+  conv_wgrad(c, bp(x), bp(dy), fp(dw), conv_wgrad_splits(c), cur(), zeroed);
 }
 
 at::Tensor linear_fwd_op(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias) {
@@ -211,9 +219,9 @@ at::Tensor pad_channels_op(const at::Tensor& x, int64_t cout) {
 TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.def("conv2d_fwd(Tensor x, Tensor w, int stride, int pad) -> Tensor");
   m.impl("conv2d_fwd", c10::DispatchKey::CUDA, &conv2d_fwd);
-  m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad) -> Tensor");
+  m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor(a!)? acc=None) -> Tensor");
   m.impl("conv2d_dgrad", c10::DispatchKey::CUDA, &conv2d_dgrad);
-  m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad) -> ()");
+  m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad, bool zeroed=False) -> ()");
   m.impl("conv2d_wgrad", c10::DispatchKey::CUDA, &conv2d_wgrad);
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias) -> Tensor");
   m.impl("linear_fwd", c10::DispatchKey::CUDA, &linear_fwd_op);

@@ -17,9 +17,15 @@ struct ConvShape {
 };
 
 void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, hipStream_t st);
-void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st);
+// accumulate: dx += dgrad (read-modify-write of the bf16 dx; every element has one writer) -- the
+// residual-join sum of two gradient paths without a separate add kernel
+void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
+                bool accumulate = false);
 // dw: fp32 [R*S*C][K]; overwritten (zeroed first when split)
-void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float* dw, int splits, hipStream_t st);
+// zeroed: dw is known to be zero already (the model zeroes its flat gradient buffer once per
+// step), so split-K needs no per-layer memset
+void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float* dw, int splits, hipStream_t st,
+                bool zeroed = false);
 int conv_wgrad_splits(const ConvShape& c);
 
 void linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, float* y, int M, int Kin, int N,

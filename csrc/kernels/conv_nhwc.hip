@@ -115,6 +115,19 @@ struct StoreBf16 {  // Y[m][n] bf16, ld = N
       if (m4 + r < M) y[(size_t)(m4 + r) * N + n] = f2bf_bits(v[r]);
   }
 };
+struct AddStoreBf16 {  // Y[m][n] bf16 += v (fp32 add of the existing bf16 value, one rounding)
+  uint16_t* __restrict__ y;
+  int M, N;
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+    if (n >= N) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (m4 + r < M) {
+        const size_t o = (size_t)(m4 + r) * N + n;
+        y[o] = f2bf_bits(v[r] + bf2f(y[o]));
+      }
+  }
+};
 struct BiasStoreF32 {  // out[m][n] fp32 = v + bias[n] (dense layer logits)
   float* __restrict__ y;
   const float* __restrict__ bias;
@@ -206,9 +219,9 @@ void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t
   }
 }
 
-void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st) {
+template <class Epi>
+static void conv_dgrad_impl(const ConvShape& c, const uint16_t* dy, const uint16_t* w, Epi epi, hipStream_t st) {
   const int M = c.N * c.H * c.W, KD = c.R * c.S * c.K;
-  StoreBf16 epi{dx, M, c.C};
   if (is_pointwise(c)) {  // dX = dY W^T: W [C][K] read k-contiguous
     DenseLoader<true> la{dy, c.K, M, c.K};
     DenseLoader<true> lb{w, c.K, c.C, c.K};
@@ -221,9 +234,17 @@ void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint1
   }
 }
 
-void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float* dw, int splits, hipStream_t st) {
+void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
+                bool accumulate) {
+  const int M = c.N * c.H * c.W;
+  if (accumulate) conv_dgrad_impl(c, dy, w, AddStoreBf16{dx, M, c.C}, st);
+  else conv_dgrad_impl(c, dy, w, StoreBf16{dx, M, c.C}, st);
+}
+
+void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float* dw, int splits, hipStream_t st,
+                bool zeroed) {
   const int P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
-  if (splits > 1) (void)hipMemsetAsync(dw, 0, (size_t)MT * c.K * sizeof(float), st);
+  if (splits > 1 && !zeroed) (void)hipMemsetAsync(dw, 0, (size_t)MT * c.K * sizeof(float), st);
   AccF32 epi{dw, MT, c.K, splits > 1 ? 1 : 0};
   DenseLoader<false> lb{dy, c.K, c.K, P};
   if (is_pointwise(c)) {  // dW = X^T dY

@@ -1067,9 +1067,18 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
       for (int j = 0; j < 4; ++j) g[j] += __shfl_xor(g[j], off, 16);
     if (sl == 0 && i < MAD_C2END) adam4(o, i, g, lr_t, c1, c2);
   } else {
-    for (int64_t i = MAD_C2END + (int64_t)(bid - MAD_C1F4 - MAD_C2BLK) * MAD_NT + tid; i < TOTAL / 4;
-         i += (int64_t)MAD_FC_BLOCKS * MAD_NT)
-      adam4(o, i, reinterpret_cast<const f32x4*>(a.grad)[i], lr_t, c1, c2);
+    const int64_t i0 = MAD_C2END + (int64_t)(bid - MAD_C1F4 - MAD_C2BLK) * MAD_NT + tid;
+    constexpr int64_t STRIDE = (int64_t)MAD_FC_BLOCKS * MAD_NT;
+    if (o.gbf) {  // bf16 gradients: 8 B instead of 16 B per float4 of parameters
+      for (int64_t i = i0; i < TOTAL / 4; i += STRIDE) {
+        const uint2 h = reinterpret_cast<const uint2*>(o.gbf)[i];
+        const f32x4 g = f32x4{__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xFFFF0000u),
+                              __uint_as_float(h.y << 16), __uint_as_float(h.y & 0xFFFF0000u)};
+        adam4(o, i, g, lr_t, c1, c2);
+      }
+    } else {
+      for (int64_t i = i0; i < TOTAL / 4; i += STRIDE) adam4(o, i, reinterpret_cast<const f32x4*>(a.grad)[i], lr_t, c1, c2);
+    }
     if (bid == MAD_GRID - 1 && tid == 0) *o.step += 1;  // see MnistAdamArgs
   }
 }

@@ -82,34 +82,53 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(int mode, const uint16_t
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[0][t][j] = sa[j]; red[1][t][j] = sb[j]; }
   __syncthreads();
-  if (g == 0) {
+  if ((rg & (rg - 1)) == 0) {  // power-of-two row groups: log2(rg) tree levels instead of rg - 1 serial adds
+    for (int h = rg >> 1; h > 0; h >>= 1) {
+      if (g < h) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sa[j] += red[0][t + h * tpr][j];
+          sb[j] += red[1][t + h * tpr][j];
+          red[0][t][j] = sa[j];
+          red[1][t][j] = sb[j];
+        }
+      }
+      __syncthreads();
+    }
+  } else if (g == 0) {
     for (int q = 1; q < rg; ++q) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) { sa[j] += red[0][q * tpr + ch][j]; sb[j] += red[1][q * tpr + ch][j]; }
     }
+  }
+  if (g == 0) {
     float* pa = part + (size_t)blockIdx.x * 2 * C;
 #pragma unroll
     for (int j = 0; j < 8; ++j) { pa[c0 + j] = sa[j]; pa[C + c0 + j] = sb[j]; }
   }
 }
 
-// per-channel finalize, block = 32 channels x 8 partial-row groups (coalesced 128-B rows, fixed
-// summation order). mode 0: mean/invstd (+running stats); mode 1: dbeta/dgamma.
-__global__ __launch_bounds__(NT) void bn_final_kernel(int mode, const float* __restrict__ part, int nblk, int M,
-                                                      int C, float eps, float momentum, float* __restrict__ o0,
-                                                      float* __restrict__ o1, float* __restrict__ rmean,
-                                                      float* __restrict__ rvar) {
-  __shared__ float red[2][8][33];
+// per-channel finalize, block = 32 channels x 32 partial-row groups (1024 threads: coalesced 128-B
+// rows, 4 independent loads in flight per thread, fixed summation order, so deterministic).
+// mode 0: mean/invstd (+running stats); mode 1: dbeta/dgamma. It is one dependent chain between
+// the partial and apply kernels, so it is latency-bound: more rows in flight, fewer trips.
+constexpr int FIN_G = 32, FIN_NT = 32 * FIN_G;
+__global__ __launch_bounds__(FIN_NT) void bn_final_kernel(int mode, const float* __restrict__ part, int nblk, int M,
+                                                          int C, float eps, float momentum, float* __restrict__ o0,
+                                                          float* __restrict__ o1, float* __restrict__ rmean,
+                                                          float* __restrict__ rvar) {
+  __shared__ float red[2][FIN_G][33];
   const int cl = threadIdx.x & 31, q = threadIdx.x >> 5, c = blockIdx.x * 32 + cl;
   float a = 0.f, b = 0.f;
   if (c < C) {
+    const size_t st = (size_t)FIN_G * 2 * C;
     int k = q;
-    for (; k + 24 < nblk; k += 32) {
+    for (; k + 3 * FIN_G < nblk; k += 4 * FIN_G) {
       const float* p0 = part + (size_t)k * 2 * C + c;
-      a += (p0[0] + p0[(size_t)8 * 2 * C]) + (p0[(size_t)16 * 2 * C] + p0[(size_t)24 * 2 * C]);
-      b += (p0[C] + p0[(size_t)8 * 2 * C + C]) + (p0[(size_t)16 * 2 * C + C] + p0[(size_t)24 * 2 * C + C]);
+      a += (p0[0] + p0[st]) + (p0[2 * st] + p0[3 * st]);
+      b += (p0[C] + p0[st + C]) + (p0[2 * st + C] + p0[3 * st + C]);
     }
-    for (; k < nblk; k += 8) {
+    for (; k < nblk; k += FIN_G) {
       a += part[(size_t)k * 2 * C + c];
       b += part[(size_t)k * 2 * C + C + c];
     }
@@ -121,7 +140,7 @@ __global__ __launch_bounds__(NT) void bn_final_kernel(int mode, const float* __r
   a = 0.f;
   b = 0.f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { a += red[0][j][cl]; b += red[1][j][cl]; }
+  for (int j = 0; j < FIN_G; ++j) { a += red[0][j][cl]; b += red[1][j][cl]; }
   if (mode == 0) {
     const float mu = a / (float)M;
     const float var = fmaxf(b / (float)M - mu * mu, 0.f);
@@ -387,7 +406,7 @@ void bn_forward(const uint16_t* y, const float* gamma, const float* beta, const 
   const RowSplit r = row_split(M, C);
   bn_partial_kernel<<<r.nblk, NT, 0, st>>>(0, y, nullptr, nullptr, 0, nullptr, nullptr, M, C, r.tpr, r.rg, r.rb,
                                            partials);
-  bn_final_kernel<<<(C + 31) / 32, NT, 0, st>>>(0, partials, r.nblk, M, C, eps, momentum, mean, invstd,
+  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, r.nblk, M, C, eps, momentum, mean, invstd,
                                                 running_mean, running_var);
   bn_apply_kernel<<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r.tpr, r.rg, r.rb);
 }
@@ -397,7 +416,7 @@ void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, c
                  int C, float* partials, hipStream_t st) {
   const RowSplit r = row_split(M, C);
   bn_partial_kernel<<<r.nblk, NT, 0, st>>>(1, y, dout, out, relu, mean, invstd, M, C, r.tpr, r.rg, r.rb, partials);
-  bn_final_kernel<<<(C + 31) / 32, NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,
+  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,
                                                 nullptr);
   bn_bwd_apply_kernel<<<r.nblk, NT, 0, st>>>(dout, out, y, gamma, mean, invstd, dbeta, dgamma, relu, dy, dres, M, C,
                                              r.tpr, r.rg, r.rb, 1.f / (float)M);

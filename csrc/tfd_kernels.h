@@ -67,6 +67,7 @@ struct MnistAdamArgs {
   float lr, beta1, beta2, eps;
   const int64_t* t;
   int64_t* step;
+  const uint16_t* gbf;  // if non-null: the fc-region (bucket A) gradients are bf16 here (gbf_a)
 };
 void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s);
 

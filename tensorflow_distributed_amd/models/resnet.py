@@ -152,6 +152,40 @@ class BucketReducer:
 
 
 # ----------------------------------------------------------------------------- autograd ops
+class GradJoin:
+    """Sum of the gradients that reach one activation over several paths (a residual block's input
+    feeds the first conv and the shortcut), without autograd's separate elementwise add: the
+    first path to run parks its gradient here and hands autograd ``None``; the last one adds into
+    the parked tensor -- a conv adds in its dgrad epilogue (``conv2d_dgrad(acc=...)``), so the sum
+    costs no extra pass over the activation. Works for either execution order of the paths."""
+
+    def __init__(self, n: int):
+        self.n = n
+        self.reset()
+
+    def reset(self):
+        self.seen, self.acc = 0, None
+
+    def arrive(self, g=None, conv=None):
+        """``g``: a finished gradient; or ``conv=(dy, layer, xshape)``: compute it as a dgrad.
+        Returns the total for the last arrival, else None."""
+        self.seen += 1
+        last = self.seen == self.n
+        if conv is not None:
+            dy, L, xs = conv
+            if self.acc is not None:
+                g = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad, self.acc)
+            else:
+                g = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad)
+        elif self.acc is not None:
+            g = self.acc.add_(g)
+        self.acc = g
+        if last:
+            self.acc = None
+            return g
+        return None
+
+
 class _Conv(torch.autograd.Function):
     # `token` is a 0-d tensor that requires grad: weights are not autograd leaves (their gradients
     # go straight into the flat buffer), so the stem needs it to put the graph on the tape.
@@ -166,9 +200,14 @@ class _Conv(torch.autograd.Function):
         (x,) = ctx.saved_tensors
         L = ctx.layer
         dy = dy.contiguous()
-        _ops().conv2d_wgrad(x, dy, L.g(), L.stride, L.pad)
+        _ops().conv2d_wgrad(x, dy, L.g(), L.stride, L.pad, L.model.grads_zeroed)
         L.model.reducer.mark_ready(L.name)
-        dx = _ops().conv2d_dgrad(dy, L.w(), list(x.shape), L.stride, L.pad) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if L.in_join is not None:
+                dx = L.in_join.arrive(conv=(dy, L, list(x.shape)))
+            else:
+                dx = _ops().conv2d_dgrad(dy, L.w(), list(x.shape), L.stride, L.pad)
         return dx, None, None
 
 
@@ -189,6 +228,8 @@ class _BN(torch.autograd.Function):
                                  L.g_gamma(), L.g_beta())
         L.model.reducer.mark_ready(L.name + "/gamma")
         L.model.reducer.mark_ready(L.name + "/beta")
+        if ctx.has_res and L.res_join is not None:
+            dres = L.res_join.arrive(dres)
         return dy, (dres if ctx.has_res else None), None, None
 
 
@@ -255,6 +296,7 @@ class _SoftmaxXent(torch.autograd.Function):
 class ConvLayer:
     def __init__(self, model, name, cin, cout, k, stride, pad):
         self.model, self.name, self.stride, self.pad = model, name, stride, pad
+        self.in_join = None  # GradJoin of this conv's input (residual block inputs)
         model.specs.append(PSpec(name, (k, k, cin, cout), "he", fan_in=k * k * cin))
 
     def w(self):
@@ -271,6 +313,7 @@ class BNLayer:
     def __init__(self, model, name, c, zero_init=False):
         self.model, self.name, self.c = model, name, c
         self.momentum, self.eps = 0.9, 1e-5
+        self.res_join = None  # GradJoin of the residual input (identity shortcut)
         model.specs.append(PSpec(name + "/gamma", (c,), "zeros" if zero_init else "ones"))
         model.specs.append(PSpec(name + "/beta", (c,), "zeros"))
         model.bns.append(self)
@@ -332,6 +375,8 @@ class ResNet:
         self.stem = ConvLayer(self, "conv1", 8, width, 7, 2, 3)
         self.stem_bn = BNLayer(self, "bn1", width)
         self.blocks = []
+        self.joins: List[GradJoin] = []
+        self.grads_zeroed = False  # set by train_step: the flat grad buffer was zeroed this step
         cin = width
         exp = 4 if kind == "bottleneck" else 1
         for li, nb in enumerate(blocks):
@@ -353,6 +398,14 @@ class ResNet:
                 if st != 1 or cin != cout:
                     blk["cd"] = ConvLayer(self, nm + ".downsample", cin, cout, 1, st, 0)
                     blk["bd"] = BNLayer(self, nm + ".downsample_bn", cout)
+                # the block input feeds conv1 and the shortcut: join their gradients in place
+                j = GradJoin(2)
+                blk["c1"].in_join = j
+                if "cd" in blk:
+                    blk["cd"].in_join = j
+                else:
+                    blk["b2" if kind == "basic" else "b3"].res_join = j
+                self.joins.append(j)
                 self.blocks.append(blk)
                 cin = cout
         self.fc = LinearLayer(self, "fc", cin, num_classes)
@@ -371,6 +424,8 @@ class ResNet:
         self.reducer = BucketReducer(self.fp, comm, int(bucket_mb * (1 << 20)), bf16=bf16_grads)
 
     def forward(self, x_nhwc_f32: torch.Tensor) -> torch.Tensor:
+        for j in self.joins:
+            j.reset()
         x = _ops().pad_channels(x_nhwc_f32, 8)
         x = self.stem_bn(self.stem(x))
         x = _MaxPool.apply(x, 3, 2, 1)
@@ -396,8 +451,14 @@ class ResNet:
     def train_step(self, x, labels, lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 1e-4):
         """fwd + bwd (bucketed all-reduce overlapped) + fused flat SGD-momentum. Returns loss tensor."""
         self.reducer.reset()
-        loss, _ = self.loss(x, labels)
-        loss.backward()
+        # one fill of the flat fp32 grad buffer instead of a memset per split-K weight gradient
+        self.fp.grad.zero_()
+        self.grads_zeroed = True
+        try:
+            loss, _ = self.loss(x, labels)
+            loss.backward()
+        finally:
+            self.grads_zeroed = False
         self.reducer.finish()
         scale = 1.0 / self.reducer.world
         _ops().momentum_flat(self.fp.master, self.fp.momentum, self.reducer.reduced_grads(), self.fp.shadow, lr,

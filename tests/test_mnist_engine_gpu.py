@@ -168,3 +168,37 @@ def test_fused_adam_tail_matches_unfused(cuda):
     d1 = engs[1].params() - params
     assert _relerr(d0, d1) < 1e-2, _relerr(d0, d1)
     assert torch.equal(engs[0].params_bf16(), engs[0].params().to(torch.bfloat16))
+
+
+def test_local_bf16_fc_grads_match_fp32(cuda):
+    """One GPU, fused tail, fc-region gradients kept in bf16 (set_local_bf16_grads: fc backward
+    writes bf16, Adam reads bf16) == the fp32-gradient path, up to bf16 rounding of the grads."""
+    B = 128
+    params = M.flat_from_dict(M.init_params(17)).to(cuda) * 0.05
+    n = 1024
+    data = torch.rand(n, 784, device=cuda)
+    labels = torch.randint(0, 10, (n,), dtype=torch.int32, device=cuda)
+    perm = torch.randperm(n, device=cuda).to(torch.int32)
+    engs = []
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for bf in (1, 0):
+            e = _engine(B, cuda, keep=0.75)
+            e.set_adam(0.01, 0.9, 0.999, 1e-8)
+            e.set_local_bf16_grads(bf)
+            e.params().copy_(params)
+            e.sync_shadow()
+            e.set_dataset(data, labels, perm)
+            e.set_input_mode(1)
+            engs.append(e)
+        for e in engs:
+            for _ in range(3):
+                e.train_step()
+    torch.cuda.synchronize()
+    assert [int(e.step_tensor().item()) for e in engs] == [3, 3]
+    d0 = engs[0].params() - params
+    d1 = engs[1].params() - params
+    assert _relerr(d0, d1) < 2e-2, _relerr(d0, d1)
+    fc = slice(M.BUCKET_SPLIT, None)
+    assert _relerr(d0[fc], d1[fc]) < 2e-2
+    assert torch.equal(engs[0].params_bf16(), engs[0].params().to(torch.bfloat16))
