@@ -29,6 +29,8 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bucket_mb", type=float, default=8.0)
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--fuse_joins", type=int, default=1, help="1: residual-join gradient sums in the dgrad "
+                    "epilogue and one grad-buffer fill per step (0: autograd adds + per-layer split-K memsets)")
     ap.add_argument("--lr", type=float, default=0.1)
     a = ap.parse_args(argv)
 
@@ -41,7 +43,7 @@ def main(argv=None):
     _native.require()
     ctx = D.init_from_env(use_gpu=True)
     dev = ctx.device
-    m = ResNet(a.depth, num_classes=1000, device=dev, seed=0)
+    m = ResNet(a.depth, num_classes=1000, device=dev, seed=0, fuse_joins=bool(a.fuse_joins))
     if ctx.comm is not None:
         ctx.comm.broadcast(m.fp.master, 0)
         m.fp.shadow.copy_(m.fp.master)
@@ -93,7 +95,7 @@ def main(argv=None):
             "config": {"model": f"resnet{a.depth} v1.5 NHWC", "global_batch": ctx.world * a.batch_size,
                        "per_gpu_batch": a.batch_size, "seq_len": None, "parallelism": f"dp{ctx.world}",
                        "bucket_mb": a.bucket_mb, "optimizer": "sgd-momentum 0.9 wd 1e-4",
-                       "hipgraph": not a.eager}}), flush=True)
+                       "hipgraph": not a.eager, "fuse_joins": bool(a.fuse_joins)}}), flush=True)
     ctx.shutdown()
     return 0
 

@@ -51,17 +51,14 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, at::IntArrayR
   check_bf16(dy, "dy", 4);
   check_bf16(w, "w", 4);
   TORCH_CHECK(xshape.size() == 4, "xshape [N,H,W,C]");
-  at::Tensor x;
-  if (acc.has_value()) {  // dx = acc + dgrad, in place
-    x = *acc;
-    check_bf16(x, "acc", 4);
-    TORCH_CHECK(x.sizes() == xshape, "dgrad: acc shape must equal xshape");
-  } else {
-    x = at::empty(xshape, dy.options());
+  auto x = at::empty(xshape, dy.options());
+  if (acc.has_value()) {  // dx = acc + dgrad
+    check_bf16(*acc, "acc", 4);
+    TORCH_CHECK(acc->sizes() == xshape, "dgrad: acc shape must equal xshape");
   }
   const ConvShape c = shape_of(x, w, stride, pad);
   TORCH_CHECK(dy.size(1) == c.Ho() && dy.size(2) == c.Wo() && dy.size(3) == c.K, "dgrad: dy shape mismatch");
-  conv_dgrad(c, bp(dy), bp(w), bp(x), cur(), acc.has_value());
+  conv_dgrad(c, bp(dy), bp(w), bp(x), cur(), acc.has_value() ? bp(*acc) : nullptr);
   return x;
 }
 
@@ -219,7 +216,7 @@ at::Tensor pad_channels_op(const at::Tensor& x, int64_t cout) {
 TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.def("conv2d_fwd(Tensor x, Tensor w, int stride, int pad) -> Tensor");
   m.impl("conv2d_fwd", c10::DispatchKey::CUDA, &conv2d_fwd);
-  m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor(a!)? acc=None) -> Tensor");
+  m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc=None) -> Tensor");
   m.impl("conv2d_dgrad", c10::DispatchKey::CUDA, &conv2d_dgrad);
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad, bool zeroed=False) -> ()");
   m.impl("conv2d_wgrad", c10::DispatchKey::CUDA, &conv2d_wgrad);

@@ -17,10 +17,10 @@ struct ConvShape {
 };
 
 void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, hipStream_t st);
-// accumulate: dx += dgrad (read-modify-write of the bf16 dx; every element has one writer) -- the
-// residual-join sum of two gradient paths without a separate add kernel
+// add (optional, must not alias dx): dx = add + dgrad in the epilogue -- the residual-join sum of
+// two gradient paths without a separate add kernel
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                bool accumulate = false);
+                const uint16_t* add = nullptr);
 // dw: fp32 [R*S*C][K]; overwritten (zeroed first when split)
 // zeroed: dw is known to be zero already (the model zeroes its flat gradient buffer once per
 // step), so split-K needs no per-layer memset

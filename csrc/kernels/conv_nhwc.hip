@@ -115,17 +115,18 @@ struct StoreBf16 {  // Y[m][n] bf16, ld = N
       if (m4 + r < M) y[(size_t)(m4 + r) * N + n] = f2bf_bits(v[r]);
   }
 };
-struct AddStoreBf16 {  // Y[m][n] bf16 += v (fp32 add of the existing bf16 value, one rounding)
-  uint16_t* __restrict__ y;
+struct AddStoreBf16 {  // Y[m][n] bf16 = v + A[m][n] (fp32 add, one rounding). A and Y are distinct
+  uint16_t* __restrict__ y;  // buffers: no aliasing, so the unrolled epilogue issues every load of A
+  const uint16_t* __restrict__ add;  // before its stores instead of one load->store round trip each
   int M, N;
   __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
     if (n >= N) return;
+    float a[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[r] = m4 + r < M ? bf2f(add[(size_t)(m4 + r) * N + n]) : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (m4 + r < M) {
-        const size_t o = (size_t)(m4 + r) * N + n;
-        y[o] = f2bf_bits(v[r] + bf2f(y[o]));
-      }
+      if (m4 + r < M) y[(size_t)(m4 + r) * N + n] = f2bf_bits(v[r] + a[r]);
   }
 };
 struct BiasStoreF32 {  // out[m][n] fp32 = v + bias[n] (dense layer logits)
@@ -235,9 +236,9 @@ static void conv_dgrad_impl(const ConvShape& c, const uint16_t* dy, const uint16
 }
 
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                bool accumulate) {
+                const uint16_t* add) {
   const int M = c.N * c.H * c.W;
-  if (accumulate) conv_dgrad_impl(c, dy, w, AddStoreBf16{dx, M, c.C}, st);
+  if (add) conv_dgrad_impl(c, dy, w, AddStoreBf16{dx, add, M, c.C}, st);
   else conv_dgrad_impl(c, dy, w, StoreBf16{dx, M, c.C}, st);
 }
 

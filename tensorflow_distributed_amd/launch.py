@@ -81,10 +81,24 @@ class Proc:
             self._log.close()
 
 
+def profiler_prefix(out_dir: str, pmc: str = "") -> List[str]:
+    """rocprofv3 command prefix (SURVEY 5.1 ``--profile``): kernel trace + per-kernel stats, or one
+    PMC counter pass (counters of one pass only; see scripts/gpu_pmc.sh for the per-block limits)."""
+    if pmc:
+        return ["rocprofv3", "--kernel-trace", "--pmc", *pmc.split(","), "-d", out_dir, "-o", "run", "--"]
+    return ["rocprofv3", "--kernel-trace", "--stats", "-d", out_dir, "-o", "run", "--"]
+
+
 def launch(num_ps: int, num_workers: int, script_args: List[str], script: str = "mnist_python_m.py",
            max_restarts: int = 0, log_dir: Optional[str] = None, echo: bool = True, timeout_s: float = 3600.0,
-           python: str = sys.executable, extra_env: Optional[dict] = None) -> dict:
-    """Run the cluster to completion. Returns {"ok", "attempts", "outputs": {name: text}}."""
+           python: str = sys.executable, extra_env: Optional[dict] = None, profile_dir: Optional[str] = None,
+           profile_pmc: str = "") -> dict:
+    """Run the cluster to completion. Returns {"ok", "attempts", "outputs": {name: text}}.
+
+    ``profile_dir``: run every worker under ``rocprofv3 --kernel-trace --stats`` (or, with
+    ``profile_pmc``, a counter pass ``--pmc <counters>``; never combined with trace domains) into
+    ``<profile_dir>/worker<i>``. The worker program comes directly after ``--`` (no shell or
+    env hop: the profiler initialises the GPU before the program starts)."""
     attempt = 0
     outputs = {}
     while True:
@@ -104,8 +118,10 @@ def launch(num_ps: int, num_workers: int, script_args: List[str], script: str = 
             procs.append(Proc("ps", i, base + ["--job_name=ps", f"--task_index={i}"] + script_args, env, lp, echo))
         for i in range(num_workers):
             lp = os.path.join(log_dir, f"worker{i}.attempt{attempt}.log") if log_dir else None
-            procs.append(Proc("worker", i, base + ["--job_name=worker", f"--task_index={i}"] + script_args, env, lp,
-                              echo))
+            cmd = base + ["--job_name=worker", f"--task_index={i}"] + script_args
+            if profile_dir:
+                cmd = profiler_prefix(os.path.join(profile_dir, f"worker{i}"), profile_pmc) + cmd
+            procs.append(Proc("worker", i, cmd, env, lp, echo))
         t0 = time.time()
         failed = None
         while True:
@@ -157,8 +173,11 @@ def main(argv=None) -> int:
     ap.add_argument("--max_restarts", type=int, default=0)
     ap.add_argument("--log_dir", default=None)
     ap.add_argument("--timeout", type=float, default=3600.0)
+    ap.add_argument("--profile", default=None, metavar="DIR", help="run workers under rocprofv3 into DIR/worker<i>")
+    ap.add_argument("--profile_pmc", default="", help="comma-separated PMC counters for one --profile pass")
     a = ap.parse_args(ours)
-    r = launch(a.num_ps, a.num_workers, rest, a.script, a.max_restarts, a.log_dir, True, a.timeout)
+    r = launch(a.num_ps, a.num_workers, rest, a.script, a.max_restarts, a.log_dir, True, a.timeout,
+               profile_dir=a.profile, profile_pmc=a.profile_pmc)
     print(f"[launch] {'ok' if r['ok'] else 'FAILED'} after {r['attempts']} attempt(s)", flush=True)
     return 0 if r["ok"] else 1
 

@@ -155,8 +155,8 @@ class BucketReducer:
 class GradJoin:
     """Sum of the gradients that reach one activation over several paths (a residual block's input
     feeds the first conv and the shortcut), without autograd's separate elementwise add: the
-    first path to run parks its gradient here and hands autograd ``None``; the last one adds into
-    the parked tensor -- a conv adds in its dgrad epilogue (``conv2d_dgrad(acc=...)``), so the sum
+    first path to run parks its gradient here and hands autograd ``None``; the last one adds
+    the parked tensor -- a conv adds it in its dgrad epilogue (``conv2d_dgrad(acc=...)``), so the sum
     costs no extra pass over the activation. Works for either execution order of the paths."""
 
     def __init__(self, n: int):
@@ -364,7 +364,7 @@ class ResNet:
            101: ("bottleneck", [3, 4, 23, 3])}
 
     def __init__(self, depth: int = 50, num_classes: int = 1000, device=None, seed: int = 0, width: int = 64,
-                 zero_init_residual: bool = True):
+                 zero_init_residual: bool = True, fuse_joins: bool = True):
         kind, blocks = self.CFG[depth]
         if num_classes % 8 or width % 8:
             raise ValueError("num_classes and width must be multiples of 8 (16-byte MFMA operand chunks)")
@@ -377,6 +377,7 @@ class ResNet:
         self.blocks = []
         self.joins: List[GradJoin] = []
         self.grads_zeroed = False  # set by train_step: the flat grad buffer was zeroed this step
+        self.fuse_joins = fuse_joins
         cin = width
         exp = 4 if kind == "bottleneck" else 1
         for li, nb in enumerate(blocks):
@@ -400,12 +401,15 @@ class ResNet:
                     blk["bd"] = BNLayer(self, nm + ".downsample_bn", cout)
                 # the block input feeds conv1 and the shortcut: join their gradients in place
                 j = GradJoin(2)
+                if not fuse_joins:
+                    j = None
                 blk["c1"].in_join = j
                 if "cd" in blk:
                     blk["cd"].in_join = j
                 else:
                     blk["b2" if kind == "basic" else "b3"].res_join = j
-                self.joins.append(j)
+                if j is not None:
+                    self.joins.append(j)
                 self.blocks.append(blk)
                 cin = cout
         self.fc = LinearLayer(self, "fc", cin, num_classes)
@@ -452,8 +456,9 @@ class ResNet:
         """fwd + bwd (bucketed all-reduce overlapped) + fused flat SGD-momentum. Returns loss tensor."""
         self.reducer.reset()
         # one fill of the flat fp32 grad buffer instead of a memset per split-K weight gradient
-        self.fp.grad.zero_()
-        self.grads_zeroed = True
+        if self.fuse_joins:
+            self.fp.grad.zero_()
+            self.grads_zeroed = True
         try:
             loss, _ = self.loss(x, labels)
             loss.backward()

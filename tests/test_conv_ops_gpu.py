@@ -50,11 +50,11 @@ def test_conv_fwd_dgrad_wgrad(cuda, N, H, W, C, K, R, st, pad):
     dw = torch.zeros(R, R, C, K, device=cuda)
     ops.conv2d_wgrad(x.to(cuda, torch.bfloat16), dyn, dw, st, pad)
     assert relerr(dw.cpu(), wr.grad.permute(2, 3, 1, 0)) < 1e-3
-    # residual-join form: dx = acc + dgrad, in place in the dgrad epilogue
+    # residual-join form: dx = acc + dgrad in the dgrad epilogue
     acc0 = rb(torch.randn(N, H, W, C))
     acc = acc0.to(cuda, torch.bfloat16)
     dx2 = ops.conv2d_dgrad(dyn, w.to(cuda, torch.bfloat16), [N, H, W, C], st, pad, acc)
-    assert dx2.data_ptr() == acc.data_ptr()
+    assert dx2.data_ptr() != acc.data_ptr()
     assert relerr(dx2.cpu().float().permute(0, 3, 1, 2), xr.grad + acc0.permute(0, 3, 1, 2)) < 1e-2
     # pre-zeroed weight-gradient buffer: no per-call memset
     dw2 = torch.zeros(R, R, C, K, device=cuda)

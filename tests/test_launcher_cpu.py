@@ -137,3 +137,13 @@ def test_log_device_placement_round_robin():
     assert r["ok"]
     w = _out(r, "worker:0")
     assert "global_step: /job:ps/task:0/cpu:0" in w and "Variable: /job:ps/task:1/cpu:0" in w
+
+
+def test_profile_prefix_puts_program_right_after_dashdash():
+    from tensorflow_distributed_amd.launch import profiler_prefix
+
+    p = profiler_prefix("/tmp/prof/worker0")
+    assert p[0] == "rocprofv3" and p[-1] == "--" and "--stats" in p and "--pmc" not in p
+    q = profiler_prefix("/tmp/prof/worker1", "SQ_WAVES,SQ_INSTS_VALU_MFMA_MOPS_BF16")
+    assert q[q.index("--pmc") + 1:q.index("--pmc") + 3] == ["SQ_WAVES", "SQ_INSTS_VALU_MFMA_MOPS_BF16"]
+    assert "--stats" not in q and "--sys-trace" not in q
