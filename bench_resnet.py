@@ -29,8 +29,8 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bucket_mb", type=float, default=8.0)
     ap.add_argument("--eager", action="store_true")
-    ap.add_argument("--fuse_joins", type=int, default=1, help="1: residual-join gradient sums in the dgrad "
-                    "epilogue and one grad-buffer fill per step (0: autograd adds + per-layer split-K memsets)")
+    ap.add_argument("--fuse_joins", type=int, default=0, help="1: residual-join gradient sums in the dgrad "
+                    "epilogue (0: autograd adds; measured faster, see resnet.GradJoin)")
     ap.add_argument("--lr", type=float, default=0.1)
     a = ap.parse_args(argv)
 

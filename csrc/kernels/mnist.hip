@@ -330,6 +330,8 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n0 = 4 * t;
   if (a.t_out && row == 0 && t == 0) *a.t_out = *a.step + 1;
+  // the label's dependent chain (step -> perm -> label) starts first, hidden behind the fc1 math
+  const int lbl = a.labels[data_row(a.perm, a.step, a.n_data, a.B, row)];
   f32x4 h = *reinterpret_cast<const f32x4*>(a.p32 + OFF_BD1 + n0);
   {  // all split-K slab loads in flight together (compile-time count: no per-load branches)
     f32x4 p[FC1_SPLITS];
@@ -370,7 +372,6 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
     if (lane == 0) red[wv][c] = v;
   }
   __syncthreads();
-  const int lbl = a.labels[data_row(a.perm, a.step, a.n_data, a.B, row)];
   float logit[NCLS];
 #pragma unroll
   for (int c = 0; c < NCLS; ++c) logit[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + a.p32[OFF_BOUT + c];

@@ -157,7 +157,12 @@ class GradJoin:
     feeds the first conv and the shortcut), without autograd's separate elementwise add: the
     first path to run parks its gradient here and hands autograd ``None``; the last one adds
     the parked tensor -- a conv adds it in its dgrad epilogue (``conv2d_dgrad(acc=...)``), so the sum
-    costs no extra pass over the activation. Works for either execution order of the paths."""
+    costs no extra pass over the activation. Works for either execution order of the paths.
+
+    Off by default (``ResNet(fuse_joins=False)``): measured on MI355X (ResNet-50 b128) the add
+    epilogue's bf16 loads are issued after the K loop and serialise on memory latency, so the
+    pointwise dgrad got 3.6x slower (77 -> 277 us) -- more than the 40 us add kernels it removes.
+    Needs the add tile prefetched into registers before the K loop to pay off."""
 
     def __init__(self, n: int):
         self.n = n
@@ -364,7 +369,7 @@ class ResNet:
            101: ("bottleneck", [3, 4, 23, 3])}
 
     def __init__(self, depth: int = 50, num_classes: int = 1000, device=None, seed: int = 0, width: int = 64,
-                 zero_init_residual: bool = True, fuse_joins: bool = True):
+                 zero_init_residual: bool = True, fuse_joins: bool = False):
         kind, blocks = self.CFG[depth]
         if num_classes % 8 or width % 8:
             raise ValueError("num_classes and width must be multiples of 8 (16-byte MFMA operand chunks)")
@@ -456,9 +461,8 @@ class ResNet:
         """fwd + bwd (bucketed all-reduce overlapped) + fused flat SGD-momentum. Returns loss tensor."""
         self.reducer.reset()
         # one fill of the flat fp32 grad buffer instead of a memset per split-K weight gradient
-        if self.fuse_joins:
-            self.fp.grad.zero_()
-            self.grads_zeroed = True
+        self.fp.grad.zero_()
+        self.grads_zeroed = True
         try:
             loss, _ = self.loss(x, labels)
             loss.backward()
