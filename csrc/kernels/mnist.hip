@@ -312,7 +312,10 @@ struct SlabEpi {
   }
 };
 constexpr int FC1_BM = 64, FC1_BN = 64, FC1_BK = TFD_FC1_BK;
-constexpr int FC1_SPLITS = 7;  // 3136 = 7 * 448 = 7 * 7 * 64
+#ifndef TFD_FC1_SPLITS
+#define TFD_FC1_SPLITS 7
+#endif
+constexpr int FC1_SPLITS = TFD_FC1_SPLITS;  // 3136 = 7 * 448 = 7 * 7 * 64 (14 splits need FC1_BK 32)
 __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DenseLoader<true> la{a.p2, FEAT, a.B, FEAT};
@@ -538,12 +541,15 @@ __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int pa
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   int id = blockIdx.x;
   if (part == 2) { fc1_dx_block(a, id % FDX_GX, id / FDX_GX, (bf16*)smem_raw); return; }
-  if (id < FDW_GX * FDW_GY) { fc1_dw_block(a, id % FDW_GX, id / FDW_GX, (bf16*)smem_raw); return; }
-  id -= FDW_GX * FDW_GY;
+  // part 0: the dX blocks (K = 1024: 16 k-steps each) get the lowest block ids so they are
+  // dispatched first and the short dW blocks (K = B) fill in around them, instead of the long
+  // blocks starting last and forming the kernel's tail.
   if (part == 0) {
     if (id < n_dx) { fc1_dx_block(a, id % FDX_GX, id / FDX_GX, (bf16*)smem_raw); return; }
     id -= n_dx;
   }
+  if (id < FDW_GX * FDW_GY) { fc1_dw_block(a, id % FDW_GX, id / FDW_GX, (bf16*)smem_raw); return; }
+  id -= FDW_GX * FDW_GY;
   out_grad_block(a, id, (float*)smem_raw);
 }
 
