@@ -83,7 +83,7 @@ __device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI
   using TB = LdsTile<BN, BK, LB::KC>;
   static_assert(BK % 32 == 0, "BK multiple of 32");
   static_assert(BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "tile/wave mismatch");
-  static_assert(RS == 1 || RS == 2, "register stages");
+  static_assert(RS >= 1 && RS <= 8, "register stages");
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
   constexpr int CA = (TA::CHUNKS + NT - 1) / NT;
   constexpr int CB = (TB::CHUNKS + NT - 1) / NT;
@@ -167,6 +167,28 @@ __device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI
         __syncthreads();
       }
     }
+  } else if constexpr (RS > 2) {
+    // Register ring: set u = t % RS holds tile t until it is written to LDS at step t-1, then is
+    // refilled with tile t+RS -- RS tiles of loads in flight behind the MFMAs (long-K blocks).
+    if (nk > 0) {
+#pragma unroll
+      for (int u = 0; u < RS; ++u)
+        if (u < nk) gload(kbeg + u * BK, ra[u], rb[u]);
+      sstore(As0, Bs0, ra[0], rb[0]);
+      __syncthreads();
+      for (int t0 = 0; t0 < nk; t0 += RS) {
+#pragma unroll
+        for (int u = 0; u < RS; ++u) {
+          const int t = t0 + u;
+          if (t < nk) {
+            if (t + RS < nk) gload(kbeg + (t + RS) * BK, ra[u], rb[u]);
+            compute((t & 1) ? As1 : As0, (t & 1) ? Bs1 : Bs0);
+            if (t + 1 < nk) sstore((t & 1) ? As0 : As1, (t & 1) ? Bs0 : Bs1, ra[(u + 1) % RS], rb[(u + 1) % RS]);
+            __syncthreads();
+          }
+        }
+      }
+    }
   } else {
     // LDS[t&1] holds tile t; register set (t+1)&1 holds tile t+1; tile t+2 loads into set t&1.
     if (nk > 0) {
@@ -189,6 +211,98 @@ __device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI
       }
     }
   }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      epi(m0 + wm * WTM + 16 * i + 4 * (lane >> 4), n0 + wn * WTN + 16 * j + (lane & 15), acc[i][j]);
+}
+
+// Whole-K variant for short, latency-bound K ranges (split-K slabs): the global loads of ALL NKT
+// K-tiles are issued back to back (NKT x (CA + CB) x 16 B per lane in flight), each tile is written
+// to its own LDS slot as soon as its loads land (in-order vmcnt), then ONE barrier and the MFMA
+// sweep. Replaces the NKT-deep load -> barrier chain of gemm_block by a single memory round trip.
+// LDS: NKT x GemmSmem/2 bytes; K range [kbeg, kbeg + NKT*BK) (loaders zero-fill past K).
+template <int BM, int BN, int BK, int NKT, class LA, class LB>
+struct GemmSmemOneshot {
+  static constexpr int BYTES = NKT * (LdsTile<BM, BK, LA::KC>::ELEMS + LdsTile<BN, BK, LB::KC>::ELEMS) * 2;
+};
+template <int BM, int BN, int BK, int NKT, int WM, int WN, class LA, class LB, class EPI>
+__device__ __forceinline__ void gemm_block_oneshot(const LA& la, const LB& lb, const EPI& epi, int m0, int n0,
+                                                   int kbeg, bf16* smem) {
+  constexpr int NT = 64 * WM * WN;
+  using TA = LdsTile<BM, BK, LA::KC>;
+  using TB = LdsTile<BN, BK, LB::KC>;
+  static_assert(BK % 32 == 0 && BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "tile shape");
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+  constexpr int CA = (TA::CHUNKS + NT - 1) / NT;
+  constexpr int CB = (TB::CHUNKS + NT - 1) / NT;
+  bf16* As = smem;
+  bf16* Bs = smem + NKT * TA::ELEMS;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  uint4 ra[NKT][CA], rb[NKT][CB];
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+    const int k0 = kbeg + t * BK;
+#pragma unroll
+    for (int c = 0; c < CA; ++c) {
+      const int idx = tid + c * NT;
+      if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
+        const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 8;
+        if constexpr (LA::KC) ra[t][c] = la(m0 + row, k0 + col);
+        else ra[t][c] = la(m0 + col, k0 + row);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const int idx = tid + c * NT;
+      if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
+        const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 8;
+        if constexpr (LB::KC) rb[t][c] = lb(n0 + row, k0 + col);
+        else rb[t][c] = lb(n0 + col, k0 + row);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+#pragma unroll
+    for (int c = 0; c < CA; ++c) {
+      const int idx = tid + c * NT;
+      if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
+        const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 8;
+        *reinterpret_cast<uint4*>(As + t * TA::ELEMS + row * TA::ROW + col) = ra[t][c];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      const int idx = tid + c * NT;
+      if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
+        const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 8;
+        *reinterpret_cast<uint4*>(Bs + t * TB::ELEMS + row * TB::ROW + col) = rb[t][c];
+      }
+    }
+  }
+  __syncthreads();
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NKT; ++t)
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = read_frag<BM, BK, LA::KC>(As + t * TA::ELEMS, wm * WTM + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = read_frag<BN, BK, LB::KC>(Bs + t * TB::ELEMS, wn * WTN + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+    }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll

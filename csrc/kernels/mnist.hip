@@ -60,6 +60,10 @@
 #define TFD_FDW_BK 64
 #endif
 
+#ifndef TFD_ADAM_U  // fc-region Adam: strides per lane with all loads issued up front (1 = plain loop)
+#define TFD_ADAM_U 2
+#endif
+
 #ifndef TFD_FC1_BK
 #define TFD_FC1_BK 64
 #endif
@@ -316,6 +320,11 @@ constexpr int FC1_BM = 64, FC1_BN = 64, FC1_BK = TFD_FC1_BK;
 #define TFD_FC1_SPLITS 7
 #endif
 constexpr int FC1_SPLITS = TFD_FC1_SPLITS;  // 3136 = 7 * 448 = 7 * 7 * 64 (14 splits need FC1_BK 32)
+#ifndef TFD_FC1_ONESHOT  // 1: every split's whole K range staged in one memory round trip (gemm_block_oneshot)
+#define TFD_FC1_ONESHOT 1
+#endif
+constexpr int FC1_NKT = FEAT / FC1_SPLITS / FC1_BK;  // K-tiles per split
+static_assert(FC1_NKT * FC1_BK * FC1_SPLITS == FEAT, "fc1 split-K must tile K exactly");
 __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DenseLoader<true> la{a.p2, FEAT, a.B, FEAT};
@@ -323,8 +332,13 @@ __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   const int z = blockIdx.z;
   SlabEpi epi{a.fc1_slab + (size_t)z * a.B * HID, HID, a.B, HID};
   const int kb = z * kper, ke = min(FEAT, kb + kper);
+#if TFD_FC1_ONESHOT
+  (void)ke;
+  gemm_block_oneshot<FC1_BM, FC1_BN, FC1_BK, FC1_NKT, 2, 2>(la, lb, epi, blockIdx.y * FC1_BM, blockIdx.x * FC1_BN, kb, (bf16*)smem_raw);
+#else
   gemm_block<FC1_BM, FC1_BN, FC1_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, blockIdx.y * FC1_BM, blockIdx.x * FC1_BN, kb, ke,
                                            (bf16*)smem_raw);
+#endif
 }
 
 // ---------------- K4-K9 head: reduce slabs, bias, relu, dropout, FC10, softmax-xent, bwd ----------
@@ -524,12 +538,15 @@ struct UnpoolEpi {
     }
   }
 };
+#ifndef TFD_FDX_RS  // register stages of the long-K (1024) fc1 dX blocks
+#define TFD_FDX_RS TFD_GEMM_RS
+#endif
 constexpr int FDX_BM = 32, FDX_BN = 64, FDX_BK = TFD_FDX_BK;
 __device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   DenseLoader<true> la{a.dh, HID, a.B, HID};
   DenseLoader<true> lb{a.pbf + OFF_WD1, HID, FEAT, HID};
   UnpoolEpi epi{a.p2, a.idx2, a.dz2, a.B};
-  gemm_block<FDX_BM, FDX_BN, FDX_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, by * FDX_BM, bx * FDX_BN, 0, HID, smem);
+  gemm_block<FDX_BM, FDX_BN, FDX_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_FDX_RS>(la, lb, epi, by * FDX_BM, bx * FDX_BN, 0, HID, smem);
 }
 
 // K8 + K10: every fc-layer gradient in ONE launch (horizontal fusion of three independent
@@ -1076,6 +1093,43 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
   } else {
     const int64_t i0 = MAD_C2END + (int64_t)(bid - MAD_C1F4 - MAD_C2BLK) * MAD_NT + tid;
     constexpr int64_t STRIDE = (int64_t)MAD_FC_BLOCKS * MAD_NT;
+#if TFD_ADAM_U > 1
+    // All U strides' loads issued before any math/store, so U x 56 B per lane are in flight
+    // (the one-at-a-time loop leaves the compiler no room: p/m/v stores may alias the next loads).
+    if (o.gbf) {
+      constexpr int U = TFD_ADAM_U;
+      for (int64_t base = i0; base < TOTAL / 4; base += STRIDE * U) {
+        uint2 h[U];
+        f32x4 p[U], m[U], v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t i = base + (int64_t)u * STRIDE;
+          if (i < TOTAL / 4) {
+            h[u] = reinterpret_cast<const uint2*>(o.gbf)[i];
+            p[u] = reinterpret_cast<const f32x4*>(o.p)[i];
+            m[u] = reinterpret_cast<const f32x4*>(o.m)[i];
+            v[u] = reinterpret_cast<const f32x4*>(o.v)[i];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t i = base + (int64_t)u * STRIDE;
+          if (i < TOTAL / 4) {
+            const f32x4 g = f32x4{__uint_as_float(h[u].x << 16), __uint_as_float(h[u].x & 0xFFFF0000u),
+                                  __uint_as_float(h[u].y << 16), __uint_as_float(h[u].y & 0xFFFF0000u)};
+            m[u] = m[u] + (g - m[u]) * c1;
+            v[u] = v[u] + (g * g - v[u]) * c2;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) p[u][j] -= lr_t * m[u][j] / (sqrtf(v[u][j]) + o.eps);
+            reinterpret_cast<f32x4*>(o.p)[i] = p[u];
+            reinterpret_cast<f32x4*>(o.m)[i] = m[u];
+            reinterpret_cast<f32x4*>(o.v)[i] = v[u];
+            reinterpret_cast<uint2*>(o.pbf)[i] = make_uint2(pack_bf2(p[u][0], p[u][1]), pack_bf2(p[u][2], p[u][3]));
+          }
+        }
+      }
+    } else
+#endif
     if (o.gbf) {  // bf16 gradients: 8 B instead of 16 B per float4 of parameters
       for (int64_t i = i0; i < TOTAL / 4; i += STRIDE) {
         const uint2 h = reinterpret_cast<const uint2*>(o.gbf)[i];
@@ -1133,7 +1187,12 @@ void mnist_forward_conv(const MnistStepArgs& a, hipStream_t s) {
 void mnist_forward_fc(const MnistStepArgs& a, bool train, hipStream_t s) {
   const int B = a.B;
   {
+#if TFD_FC1_ONESHOT
+    constexpr int sm = GemmSmemOneshot<FC1_BM, FC1_BN, FC1_BK, FC1_NKT, DenseLoader<true>, DenseLoader<false>>::BYTES;
+    static_assert(sm <= 160 * 1024, "fc1 one-shot LDS");
+#else
     constexpr int sm = GemmSmem<FC1_BM, FC1_BN, FC1_BK, DenseLoader<true>, DenseLoader<false>>::BYTES;
+#endif
     set_smem<fc1_fwd>(sm);
     const int kper = (FEAT + a.fc1_splits - 1) / a.fc1_splits;
     dim3 g(HID / FC1_BN, (B + FC1_BM - 1) / FC1_BM, a.fc1_splits);
