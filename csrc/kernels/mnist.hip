@@ -434,6 +434,7 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
 // [B][10] staged in LDS; the 4 batch quarters are summed through LDS (deterministic).
 constexpr int OUTG_ROWS = 64;
 constexpr int OUTG_BLOCKS = (HID + 1 + OUTG_ROWS - 1) / OUTG_ROWS;  // 17 (last block: bias row)
+constexpr int OUTG_LB = 16;  // hd loads batched per thread (a one-at-a-time loop was a 32-deep latency chain)
 __device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, float* smem) {
   float* dl = smem;                      // [B][10]
   float* part = smem + a.B * NCLS;       // [4][64][10]
@@ -446,7 +447,17 @@ __device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, 
   for (int c = 0; c < NCLS; ++c) acc[c] = 0.f;
   const int bq = (a.B + 3) >> 2, b0 = q * bq, b1 = min(a.B, b0 + bq);
   if (m < HID) {
-    for (int b = b0; b < b1; ++b) {
+    int b = b0;
+    for (; b + OUTG_LB <= b1; b += OUTG_LB) {  // OUTG_LB independent loads in flight, then the FMAs
+      float hv[OUTG_LB];
+#pragma unroll
+      for (int u = 0; u < OUTG_LB; ++u) hv[u] = bf2f(a.hd[(size_t)(b + u) * HID + m]);
+#pragma unroll
+      for (int u = 0; u < OUTG_LB; ++u)
+#pragma unroll
+        for (int c = 0; c < NCLS; ++c) acc[c] = fmaf(hv[u], dl[(b + u) * NCLS + c], acc[c]);
+    }
+    for (; b < b1; ++b) {
       const float h = bf2f(a.hd[(size_t)b * HID + m]);
 #pragma unroll
       for (int c = 0; c < NCLS; ++c) acc[c] = fmaf(h, dl[b * NCLS + c], acc[c]);
@@ -538,6 +549,9 @@ struct UnpoolEpi {
     }
   }
 };
+#ifndef TFD_OUTG_FIRST  // 1: output-layer gradient blocks get the lowest block ids of fc1_bwd
+#define TFD_OUTG_FIRST 1
+#endif
 #ifndef TFD_FDX_RS  // register stages of the long-K (1024) fc1 dX blocks
 #define TFD_FDX_RS TFD_GEMM_RS
 #endif
@@ -558,16 +572,30 @@ __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int pa
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   int id = blockIdx.x;
   if (part == 2) { fc1_dx_block(a, id % FDX_GX, id / FDX_GX, (bf16*)smem_raw); return; }
+#if TFD_OUTG_FIRST
+  // the 17 output-layer blocks each walk the whole batch: dispatched first, their latency hides
+  // under the GEMM tiles instead of forming the kernel's tail.
+  if (id < OUTG_BLOCKS) { out_grad_block(a, id, (float*)smem_raw); return; }
+  id -= OUTG_BLOCKS;
+#endif
   // part 0: the dX blocks (K = 1024: 16 k-steps each) get the lowest block ids so they are
   // dispatched first and the short dW blocks (K = B) fill in around them, instead of the long
   // blocks starting last and forming the kernel's tail.
   if (part == 0) {
+#if TFD_DIAG_FC1BWD == 1  // timing diagnosis only (wrong gradients): drop the dX blocks
+    if (id < n_dx) return;
+#endif
     if (id < n_dx) { fc1_dx_block(a, id % FDX_GX, id / FDX_GX, (bf16*)smem_raw); return; }
     id -= n_dx;
   }
+#if TFD_DIAG_FC1BWD == 2  // timing diagnosis only (wrong gradients): drop the dW blocks
+  if (id < FDW_GX * FDW_GY) return;
+#endif
   if (id < FDW_GX * FDW_GY) { fc1_dw_block(a, id % FDW_GX, id / FDW_GX, (bf16*)smem_raw); return; }
+#if !TFD_OUTG_FIRST
   id -= FDW_GX * FDW_GY;
   out_grad_block(a, id, (float*)smem_raw);
+#endif
 }
 
 // ---------------- K13 conv2 dgrad (+ conv1 relu/pool mask epilogue) ----------------

@@ -8,6 +8,7 @@ mkdir -p gpurun_out
 TAG=${TAG:-vab}
 lib() { if [ "$1" = "base" ]; then echo $PWD/tensorflow_distributed_amd/_C.so; else echo $PWD/tensorflow_distributed_amd/_C_$1.so; fi; }
 for v in ${VARIANTS:-base}; do
+  [ "${SKIP_TESTS:-0}" = "1" ] && break
   TFD_NATIVE_LIB=$(lib $v) timeout -k 10 300 python -u -m pytest tests/test_mnist_engine_gpu.py -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/pytest_${TAG}_$v.log 2>&1 || { echo "pytest $v failed"; tail -30 gpurun_out/pytest_${TAG}_$v.log; exit 1; }
   echo "tests $v: $(tail -1 gpurun_out/pytest_${TAG}_$v.log)"
