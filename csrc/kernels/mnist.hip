@@ -53,7 +53,7 @@
 #endif
 
 #ifndef TFD_FDX_BK
-#define TFD_FDX_BK 64
+#define TFD_FDX_BK 128
 #endif
 
 #ifndef TFD_FDW_BK
@@ -434,7 +434,10 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
 // [B][10] staged in LDS; the 4 batch quarters are summed through LDS (deterministic).
 constexpr int OUTG_ROWS = 64;
 constexpr int OUTG_BLOCKS = (HID + 1 + OUTG_ROWS - 1) / OUTG_ROWS;  // 17 (last block: bias row)
-constexpr int OUTG_LB = 16;  // hd loads batched per thread (a one-at-a-time loop was a 32-deep latency chain)
+#ifndef TFD_OUTG_LB
+#define TFD_OUTG_LB 16
+#endif
+constexpr int OUTG_LB = TFD_OUTG_LB;  // hd loads batched per thread (a one-at-a-time loop was a 32-deep latency chain)
 __device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, float* smem) {
   float* dl = smem;                      // [B][10]
   float* part = smem + a.B * NCLS;       // [4][64][10]
@@ -516,11 +519,43 @@ struct GradEpi {
     }
   }
 };
+// Same output, one wide store per lane: a 4x4 transpose inside each 4-lane group (4 bpermute
+// rounds) turns "4 rows of one column" into "4 columns of one row", so each lane writes 8 B (bf16)
+// or 16 B (fp32) instead of four scattered 2/4-B stores. Needs every lane of the wave (no early
+// return before the shuffles) and N % 4 == 0.
+struct GradEpiT {
+  float* __restrict__ out;
+  uint16_t* __restrict__ outbf;
+  int ld, M, N;
+  __device__ __forceinline__ static float pick(f32x4 v, int i) {
+    return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
+  }
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+    const int lane = threadIdx.x & 63, j = lane & 3;
+    f32x4 r;  // r[k] = column ((j + k) & 3) of row j, from lane (j + k) & 3 of the group
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = __shfl(pick(v, (j - k) & 3), (lane & ~3) | ((j + k) & 3), 64);
+    const f32x4 w = f32x4{pick(r, (0 - j) & 3), pick(r, (1 - j) & 3), pick(r, (2 - j) & 3), pick(r, (3 - j) & 3)};
+    const int m = m4 + j, nb = n - j;
+    if (m >= M || nb >= N) return;
+    const size_t o = (size_t)m * ld + nb;
+    if (outbf) *reinterpret_cast<uint2*>(outbf + o) = make_uint2(pack_bf2(w[0], w[1]), pack_bf2(w[2], w[3]));
+    else *reinterpret_cast<f32x4*>(out + o) = w;
+  }
+};
+#ifndef TFD_DW_EPIT  // 1: fc1 dW epilogue through the 4-lane transpose (GradEpiT)
+#define TFD_DW_EPIT 0
+#endif
 constexpr int FDW_BM = 64, FDW_BN = 64, FDW_BK = TFD_FDW_BK;
 __device__ __forceinline__ void fc1_dw_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   OnesRowMC la{a.p2, FEAT, FEAT, a.B};
   DenseLoader<false> lb{a.dh, HID, HID, a.B};
+#if TFD_DW_EPIT
+  static_assert(OFF_WD1 % 4 == 0 && HID % 4 == 0, "wide dW stores");
+  GradEpiT epi{a.grad + OFF_WD1, a.gbf_a ? a.gbf_a + OFF_WD1 : nullptr, HID, FEAT + 1, HID};
+#else
   GradEpi epi{a.grad + OFF_WD1, a.gbf_a ? a.gbf_a + OFF_WD1 : nullptr, HID, FEAT + 1, HID};
+#endif
   gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, by * FDW_BM, bx * FDW_BN, 0, a.B, smem);
 }
 
@@ -553,7 +588,7 @@ struct UnpoolEpi {
 #define TFD_OUTG_FIRST 1
 #endif
 #ifndef TFD_FDX_RS  // register stages of the long-K (1024) fc1 dX blocks
-#define TFD_FDX_RS TFD_GEMM_RS
+#define TFD_FDX_RS 1  // with BK 128: 8 K-steps, A/B vs RS 2 -1.3 us/step
 #endif
 constexpr int FDX_BM = 32, FDX_BN = 64, FDX_BK = TFD_FDX_BK;
 __device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
