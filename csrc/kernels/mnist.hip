@@ -546,7 +546,10 @@ struct GradEpiT {
 #ifndef TFD_DW_EPIT  // 1: fc1 dW epilogue through the 4-lane transpose (GradEpiT)
 #define TFD_DW_EPIT 0
 #endif
-constexpr int FDW_BM = 64, FDW_BN = 64, FDW_BK = TFD_FDW_BK;
+#ifndef TFD_FDW_BM
+#define TFD_FDW_BM 64
+#endif
+constexpr int FDW_BM = TFD_FDW_BM, FDW_BN = 64, FDW_BK = TFD_FDW_BK;
 __device__ __forceinline__ void fc1_dw_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   OnesRowMC la{a.p2, FEAT, FEAT, a.B};
   DenseLoader<false> lb{a.dh, HID, HID, a.B};
@@ -1168,10 +1171,20 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
         for (int u = 0; u < U; ++u) {
           const int64_t i = base + (int64_t)u * STRIDE;
           if (i < TOTAL / 4) {
-            h[u] = reinterpret_cast<const uint2*>(o.gbf)[i];
             p[u] = reinterpret_cast<const f32x4*>(o.p)[i];
+#if TFD_ADAM_NT
+            {
+              typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+              const u32x2 hv = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(o.gbf) + i);
+              h[u] = make_uint2(hv[0], hv[1]);
+            }
+            m[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.m) + i);
+            v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.v) + i);
+#else
+            h[u] = reinterpret_cast<const uint2*>(o.gbf)[i];
             m[u] = reinterpret_cast<const f32x4*>(o.m)[i];
             v[u] = reinterpret_cast<const f32x4*>(o.v)[i];
+#endif
           }
         }
 #pragma unroll
@@ -1184,9 +1197,15 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
             v[u] = v[u] + (g * g - v[u]) * c2;
 #pragma unroll
             for (int j = 0; j < 4; ++j) p[u][j] -= lr_t * m[u][j] / (sqrtf(v[u][j]) + o.eps);
+#if TFD_ADAM_NT  // streaming stores for the optimizer state (m, v are not read again this step)
+            reinterpret_cast<f32x4*>(o.p)[i] = p[u];
+            __builtin_nontemporal_store(m[u], reinterpret_cast<f32x4*>(o.m) + i);
+            __builtin_nontemporal_store(v[u], reinterpret_cast<f32x4*>(o.v) + i);
+#else
             reinterpret_cast<f32x4*>(o.p)[i] = p[u];
             reinterpret_cast<f32x4*>(o.m)[i] = m[u];
             reinterpret_cast<f32x4*>(o.v)[i] = v[u];
+#endif
             reinterpret_cast<uint2*>(o.pbf)[i] = make_uint2(pack_bf2(p[u][0], p[u][1]), pack_bf2(p[u][2], p[u][3]));
           }
         }
