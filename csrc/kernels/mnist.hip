@@ -60,12 +60,16 @@
 #define TFD_FDW_BK 64
 #endif
 
+#ifndef TFD_C1_EARLY_X  // 1: conv1 forward issues its image load before the filter-staging barrier
+#define TFD_C1_EARLY_X 0
+#endif
+
 #ifndef TFD_ADAM_U  // fc-region Adam: strides per lane with all loads issued up front (1 = plain loop)
 #define TFD_ADAM_U 2
 #endif
 
 #ifndef TFD_FC1_BK
-#define TFD_FC1_BK 64
+#define TFD_FC1_BK 32  // one-shot fc1: 14 K-tiles of 32 (140 KiB LDS) measured 0.6 us/step faster than 7 of 64
 #endif
 
 #ifndef TFD_C2F_BK
@@ -93,12 +97,20 @@ __global__ __launch_bounds__(256) void conv1_pool_fwd(MnistStepArgs a) {
   __shared__ float w[KTAPS * 8 + 8];
   const int b = blockIdx.x >> 2, cg = blockIdx.x & 3, t = threadIdx.x;
   const float* x = a.data + (size_t)data_row(a.perm, a.step, a.n_data, a.B, b) * 784;
+#if TFD_C1_EARLY_X
+  // the image load is issued before the first barrier, so its step -> perm -> row chain overlaps
+  // the filter loads instead of starting after them
+  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (t < 196) v = reinterpret_cast<const f32x4*>(x)[t];
+#endif
   for (int i = t; i < 32 * 32; i += 256) img[i] = 0.f;
   if (t < KTAPS * 8) w[t] = a.p32[OFF_WC1 + (t >> 3) * C1 + cg * 8 + (t & 7)];
   else if (t < KTAPS * 8 + 8) w[t] = a.p32[OFF_BC1 + cg * 8 + (t - KTAPS * 8)];
   __syncthreads();
   if (t < 196) {  // 196 float4 = one image
+#if !TFD_C1_EARLY_X
     const f32x4 v = reinterpret_cast<const f32x4*>(x)[t];
+#endif
     const int r = (4 * t) / 28, c = (4 * t) % 28;
     float* d = img + (r + 2) * 32 + c + 2;
     d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
@@ -712,6 +724,10 @@ __global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) {
   const uint16_t* src = a.dz2 + (size_t)b * 196 * 64;
   const uint16_t* wsrc = a.pbf + OFF_WC2;
   const int rot = TFD_WROT ? (int)((blockIdx.x * 1031u) % 6400u) : 0;  // per-block start: spread L2 channels
+#if TFD_C1_EARLY_X
+  // the conv1-wgrad tail's step -> perm chain resolved now, behind the staging loads
+  const int xrow_idx = data_row(a.perm, a.step, a.n_data, a.B, b);
+#endif
   {
     constexpr int CI = 8 * C2D_PLANE, NI = (CI + 511) / 512;  // 1792 chunks -> 4 per thread
     uint4 vi[NI];
@@ -811,7 +827,11 @@ __global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) {
     }
   } else {
     const int u = t - 256;
+#if TFD_C1_EARLY_X
+    const float* xrow = a.data + (size_t)xrow_idx * 784;
+#else
     const float* xrow = a.data + (size_t)data_row(a.perm, a.step, a.n_data, a.B, b) * 784;
+#endif
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int i = 4 * u + q, r = i >> 5, c = i & 31;
