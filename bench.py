@@ -35,6 +35,16 @@ def main(argv=None):
     ap.add_argument("--fp32_grads", action="store_true", help="all-reduce fp32 grads (default bf16)")
     ap.add_argument("--ipc_small", type=int, default=1, help="1: peer-to-peer IPC one-shot all-reduce for the "
                     "small conv-gradient bucket (self-checked against RCCL at startup; falls back if it disagrees)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "ipc"],
+                    help="DP gradient transport: auto = IPC for every bucket when ranks share a GPU, else RCCL "
+                    "(+ IPC for the small bucket)")
+    ap.add_argument("--force_dp", type=int, default=0, help="1: run the full DP schedule (comm stream, captured "
+                    "collectives) even at world 1 -- one-GPU rehearsal of the multi-GPU path")
+    ap.add_argument("--min_warmup_ms", type=float, default=300.0, help="after --warmup steps, keep replaying "
+                    "untimed steps until this much warm-up time has passed (GPU clock ramp; reported in the JSON)")
+    ap.add_argument("--graph_steps", type=int, default=20, help="training steps captured per hipGraph "
+                    "(device-side step counter/data cursor/dropout key make step i+1 of a graph the next step)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16"], help="compute dtype of the MFMA operands")
     ap.add_argument("--opt_overlap", type=int, default=0, help="1: run the fc-region optimizer on a side "
                     "stream overlapping the conv backward (0: on the main stream after it)")
     ap.add_argument("--conv_fork", type=int, default=0, help="1: conv2 wgrad on a forked stream beside dgrad")
@@ -70,13 +80,15 @@ def main(argv=None):
     eng.set_conv_fork(a.conv_fork)
     eng.set_fused_tail(a.fused_tail)
     eng.set_local_bf16_grads(a.local_bf16_grads)
-    ipc_state = "off"
-    if ctx.comm is not None:
-        eng.set_comm(ctx.comm, not a.fp32_grads)
-        if a.ipc_small:
-            ipc_state = _setup_ipc(eng, ctx, M)
-        if a.zero:
-            eng.set_zero(True)
+    from tensorflow_distributed_amd.parallel.transport import attach_engine
+
+    mode = a.transport
+    if mode == "auto":
+        mode = "ipc" if ctx.shared_device else "rccl"
+    tr = attach_engine(eng, rank, world, dev, mode=mode, comm=ctx.comm, bf16=not a.fp32_grads,
+                       small_ipc=bool(a.ipc_small), force_dp=bool(a.force_dp))
+    if a.zero:
+        eng.set_zero(True)
     s = torch.cuda.Stream(dev)
     n_data = 55000
     with torch.cuda.stream(s):
@@ -86,25 +98,56 @@ def main(argv=None):
         perm = torch.randperm(n_data, device=dev, generator=g).to(torch.int32)
         if rank == 0:
             eng.params().copy_(M.flat_from_dict(M.init_params(a.seed)).to(dev))
-        if ctx.comm is not None:
-            ctx.comm.broadcast(eng.params(), 0)  # chief init -> everyone (reference M6)
+        if world > 1:  # chief init -> everyone (reference M6): RCCL, or Gloo when ranks share a GPU
+            if ctx.comm is not None:
+                ctx.comm.broadcast(eng.params(), 0)
+            else:
+                torch.cuda.synchronize(dev)
+                host = eng.params().cpu()
+                ctx.broadcast_tensor_cpu(host, 0)
+                eng.params().copy_(host.to(dev))
         eng.sync_shadow()
         eng.set_dataset(data, labels, perm)
         eng.set_input_mode(1)
         graph_mode = not a.eager
         eng.train_step()  # one eager step first: sets kernel attributes outside capture
+        gsteps = max(1, a.graph_steps)
         if graph_mode:
             try:
                 eng.capture_train_step("train")
+                if gsteps > 1:
+                    eng.capture_train_steps("trainN", gsteps)
             except Exception as e:  # pragma: no cover - capture support depends on the RCCL build
                 print(f"# hipGraph capture failed ({e!r}); timing eager launches", file=sys.stderr)
                 graph_mode = False
         if graph_mode:
-            run = lambda k: eng.replay("train", k)  # noqa: E731
+            def run(k):
+                if gsteps > 1 and k >= gsteps:
+                    eng.replay("trainN", k // gsteps)
+                if k % gsteps or gsteps == 1:
+                    eng.replay("train", k % gsteps if gsteps > 1 else k)
         else:
             run = lambda k: [eng.train_step() for _ in range(k)]  # noqa: E731
         run(a.warmup)
     torch.cuda.synchronize(dev)
+    # GPU clocks ramp over the first few hundred steps (profiles/warmup_ramp.log: 99 -> 92 us per
+    # replay over 400 steps, back to 99.6 us after 2 s idle), so a 20-step timed region right after a
+    # 5-step warm-up measures the ramp. Keep replaying untimed steps until --min_warmup_ms elapsed;
+    # every rank runs the same count (decided by rank 0), so collectives stay matched.
+    extra = 0
+    if a.min_warmup_ms > 0:
+        t_w = time.perf_counter()
+        chunk = 50
+        while True:
+            el = (time.perf_counter() - t_w) * 1e3
+            go = torch.tensor([1 if el < a.min_warmup_ms else 0], dtype=torch.int64)
+            ctx.broadcast_tensor_cpu(go, 0)
+            if not int(go.item()):
+                break
+            with torch.cuda.stream(s):
+                run(chunk)
+            torch.cuda.synchronize(dev)
+            extra += chunk
     loss0 = float(eng.loss_rows().mean().item())
 
     ctx.barrier()
@@ -119,6 +162,7 @@ def main(argv=None):
         with torch.cuda.stream(s):
             eng.sync_params()
     dt = ctx.max_scalar(dt)
+    tr.check("after the timed steps")
     loss1 = float(eng.loss_rows().mean().item())
     gstep = int(eng.step_tensor().item())
     ms = dt * 1e3 / a.steps
@@ -133,6 +177,7 @@ def main(argv=None):
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "warmup_extra_steps": extra,
             "ms_per_step": round(ms, 5),
             "higher_is_better": True,
             "scaling": "weak",
@@ -148,39 +193,16 @@ def main(argv=None):
                 "parallelism": f"dp{world}",
                 "grad_allreduce": "fp32" if a.fp32_grads else "bf16",
                 "hipgraph": graph_mode,
-                "small_bucket_allreduce": ipc_state,
+                "steps_per_graph": gsteps if graph_mode else 0,
+                "dp_transport": tr.kind,
+                "force_dp": bool(a.force_dp),
                 "zero1_fc1": bool(a.zero),
                 "fc_grads": "bf16" if (a.local_bf16_grads or world > 1) and not a.fp32_grads else "fp32",
             },
         }), flush=True)
+    tr.close()
     ctx.shutdown()
     return 0
-
-
-def _setup_ipc(eng, ctx, M):
-    """IPC one-shot all-reduce for bucket B, validated against RCCL on this node before use."""
-    import torch
-
-    from tensorflow_distributed_amd.parallel.ipc import make_ipc_comm
-
-    try:
-        ipc = make_ipc_comm(ctx.rank, ctx.world, ctx.device.index, M.BUCKET_SPLIT)
-        dev = ctx.device
-        g = torch.Generator(device=dev).manual_seed(77 + ctx.rank)
-        x = torch.randn(M.BUCKET_SPLIT, device=dev, generator=g)
-        y = x.clone()
-        ipc.all_reduce(x, 1.0)
-        ctx.comm.all_reduce(y, "sum")
-        torch.cuda.synchronize(dev)
-        ok = int(ipc.error() == 0 and torch.allclose(x, y, rtol=1e-4, atol=1e-4))
-    except Exception as e:  # pragma: no cover - depends on the node's IPC support
-        print(f"# ipc setup failed: {e!r}", file=sys.stderr)
-        ipc, ok = None, 0
-    ok = int(ctx.max_scalar(1 - ok) == 0)  # every rank must agree
-    if not ok:
-        return "rccl (ipc self-check failed)"
-    eng.set_ipc(ipc, M.BUCKET_SPLIT, True)
-    return "ipc-oneshot"
 
 
 def _cpu_dry_run(a):

@@ -96,6 +96,8 @@ class MnistEngine : public torch::CustomClassHolder {
   at::Tensor params() { return params_; }
   at::Tensor params_bf16() { return pbf_; }
   at::Tensor grads() { return grad_; }
+  // bf16 gradient buffer: the DP wire format (reduced in place by the bucket all-reduces)
+  at::Tensor grads_bf16() { return gbf_; }
   at::Tensor adam_m() { return m_; }
   at::Tensor adam_v() { return v_; }
   at::Tensor step_tensor() { return step_; }
@@ -149,6 +151,11 @@ class MnistEngine : public torch::CustomClassHolder {
     if (ipc_) return ipc_->world();
     return 1;
   }
+  // Force the data-parallel schedule (comm stream, bucket casts, captured collectives, 1/N scale)
+  // even at world 1: exercises the multi-rank orchestration -- RCCL or IPC -- on a one-GPU box
+  // with the exact code an 8-GPU node runs.
+  void set_force_dp(bool on) { force_dp_ = on; }
+  bool dp() const { return world() > 1 || (force_dp_ && (comm_ || ipc_)); }
   int64_t rank_in_comm() const {
     if (comm_) return comm_->rank();
     if (ipc_) return ipc_->rank();
@@ -196,7 +203,7 @@ class MnistEngine : public torch::CustomClassHolder {
   }
   // Optimizer over the flat range [beg, end) on stream s; t = global_step + t_offset.
   void apply_optimizer_range(int64_t beg, int64_t end, double grad_scale, int t_offset, hipStream_t s) {
-    const uint16_t* gbf = (bf16_comm_ && world() > 1) ? (const uint16_t*)gbf_.data_ptr() + beg : nullptr;
+    const uint16_t* gbf = (bf16_comm_ && dp()) ? (const uint16_t*)gbf_.data_ptr() + beg : nullptr;
     const int64_t n = end - beg;
     if (opt_ == 0) {
       AdamArgs a{(float*)params_.data_ptr() + beg, (float*)m_.data_ptr() + beg, (float*)v_.data_ptr() + beg,
@@ -226,8 +233,8 @@ class MnistEngine : public torch::CustomClassHolder {
       return;
     }
     hipStream_t s = stream();
-    const bool dp = world() > 1;
-    const double scale = dp ? 1.0 / (double)world() : 1.0;
+    const bool dp = this->dp();
+    const double scale = 1.0 / (double)world();
     hipStream_t ws = conv_fork_ ? aux_stream_ : nullptr;
     MnistStepArgs a = args();
     if (!dp && !opt_overlap_) {
@@ -326,7 +333,7 @@ class MnistEngine : public torch::CustomClassHolder {
   void reduce_grads(double weight) {
     hipStream_t s = stream();
     if (weight != 1.0) scale_f32((float*)grad_.data_ptr(), TOTAL, (float)weight, s);
-    if (world() <= 1) return;
+    if (!dp()) return;
     HIP_OK(hipEventRecord(ev_a_, s));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
     reduce_bucket(0, TOTAL);
@@ -358,13 +365,18 @@ class MnistEngine : public torch::CustomClassHolder {
   }
 
   // ---- hipGraph capture / replay of the whole step ----
-  void capture_train_step(const std::string& name) {
+  void capture_train_step(const std::string& name) { capture_train_steps(name, 1); }
+  // n consecutive steps in ONE graph: the step counter, the dataset cursor and the dropout key all
+  // live on the device, so step i+1 of the graph is exactly the next training step. One launch per
+  // n steps removes the host launch and the graph-to-graph boundary from n - 1 of them.
+  void capture_train_steps(const std::string& name, int64_t n) {
+    TORCH_CHECK(n >= 1 && n <= 1000, "capture_train_steps: 1 <= n <= 1000");
     hipStream_t s = stream();
     TORCH_CHECK(s != nullptr, "capture needs a non-default stream (use torch.cuda.stream(...))");
     drop_graph(name);
     HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
     try {
-      train_step();
+      for (int64_t i = 0; i < n; ++i) train_step();
     } catch (...) {
       hipGraph_t g;
       hipStreamEndCapture(s, &g);
@@ -426,7 +438,7 @@ class MnistEngine : public torch::CustomClassHolder {
   }
 
   // bucket A's gradients come out of the fc backward as bf16 in gbf_ (MnistStepArgs::gbf_a)
-  bool fused_bf16_a() const { return bf16_comm_ && world() > 1; }
+  bool fused_bf16_a() const { return bf16_comm_ && dp(); }
   bool in_gbf(int64_t beg) const { return fused_bf16_a() && beg >= BUCKET_SPLIT; }
 
   void reduce_bucket(int64_t beg, int64_t end) {
@@ -512,6 +524,7 @@ class MnistEngine : public torch::CustomClassHolder {
   hipStream_t aux_stream_ = nullptr, opt_stream_ = nullptr;
   hipEvent_t ev_opt_a_ = nullptr, ev_start_ = nullptr, ev_ag_ = nullptr;
   bool zero_ = false;
+  bool force_dp_ = false;
   int64_t zshard_ = 0;
   // where region A's optimizer runs: 0 = main stream after the conv backward (no HBM contention
   // with the conv kernels), 1 = side stream overlapping the conv backward
@@ -542,6 +555,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("params", &MnistEngine::params)
       .def("params_bf16", &MnistEngine::params_bf16)
       .def("grads", &MnistEngine::grads)
+      .def("grads_bf16", &MnistEngine::grads_bf16)
       .def("adam_m", &MnistEngine::adam_m)
       .def("adam_v", &MnistEngine::adam_v)
       .def("step_tensor", &MnistEngine::step_tensor)
@@ -562,6 +576,8 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_comm", &MnistEngine::set_comm)
       .def("set_ipc", &MnistEngine::set_ipc)
       .def("set_zero", &MnistEngine::set_zero)
+      .def("set_force_dp", &MnistEngine::set_force_dp)
+      .def("dp", &MnistEngine::dp)
       .def("set_opt_overlap", &MnistEngine::set_opt_overlap)
       .def("set_conv_fork", &MnistEngine::set_conv_fork)
       .def("set_fused_tail", &MnistEngine::set_fused_tail)
@@ -577,6 +593,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("train_step", &MnistEngine::train_step)
       .def("evaluate", &MnistEngine::evaluate)
       .def("capture_train_step", &MnistEngine::capture_train_step)
+      .def("capture_train_steps", &MnistEngine::capture_train_steps)
       .def("replay", &MnistEngine::replay)
       .def("drop_graph", &MnistEngine::drop_graph);
 }

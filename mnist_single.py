@@ -47,6 +47,8 @@ def main(argv=None):
     ap.add_argument("--no_graph", action="store_true", help="GPU: launch kernels per step (no hipGraph)")
     ap.add_argument("--eval_batches", type=int, default=50)
     ap.add_argument("--train_flag", type=int, default=1, help="1 = train, else evaluation only (mnist_single.py:103)")
+    ap.add_argument("--host_feed", action="store_true", help="GPU: feed every batch from the host (next_batch + "
+                    "H2D) instead of the device-resident split with a per-epoch device shuffle")
     a = ap.parse_args(argv)
 
     # Import MNIST data (mnist_single.py:14-15)
@@ -55,6 +57,9 @@ def main(argv=None):
     runner = make_runner(a.batch_size, AdamOptimizer(a.learning_rate), dev, keep_prob=dropout, seed=a.seed,
                          use_graph=not a.no_graph)
     runner.load_flat(M.flat_from_dict(M.init_params(a.seed)), {}, 0)  # init = initialize_all_variables()
+    device_input = dev.type == "cuda" and not a.host_feed
+    if device_input:  # upload the split once; batches are gathered on the GPU (no per-step feed)
+        runner.set_device_dataset(mnist.train.images, mnist.train.labels, seed=a.seed + 101)
 
     start_time = time.time()
     train_flag = a.train_flag
@@ -62,10 +67,15 @@ def main(argv=None):
     if train_flag == 1:
         # Keep training until reach max iterations
         while step * a.batch_size < a.training_iters:
-            batch_x, batch_y = mnist.train.next_batch(a.batch_size)
-            # Run optimization op (backprop)
-            runner.train_step(batch_x, batch_y)
+            if device_input:
+                runner.train_step(None, None)  # next_batch happens on the device
+            else:
+                batch_x, batch_y = mnist.train.next_batch(a.batch_size)
+                # Run optimization op (backprop)
+                runner.train_step(batch_x, batch_y)
             if step % a.display_step == 0:
+                if device_input:
+                    batch_x, batch_y = runner.last_device_batch()
                 # Calculate batch loss (keep_prob = 1)
                 loss_sum, _ = runner.evaluate(batch_x, batch_y)
                 loss = loss_sum / len(batch_x)

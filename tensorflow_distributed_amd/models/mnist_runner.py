@@ -197,6 +197,48 @@ class NativeMnistRunner(MnistRunnerBase):
         self._graph_ready = False
         self._x_stage = torch.empty(batch_size, 784, dtype=torch.float32).pin_memory()
         self._y_stage = torch.empty(batch_size, dtype=torch.int32).pin_memory()
+        self.transport = None  # parallel.transport.DPTransport when DP runs over RCCL/IPC
+        self._dev_data = None  # device-resident split (set_device_dataset)
+        self._hstep = 0        # host mirror of the device global_step (epoch bookkeeping, no sync)
+        self._epoch = -1
+
+    # ---- device-resident input (reference feed: mnist_python_m.py:291-294) ----
+    def set_device_dataset(self, images, labels, seed: int = 0) -> None:
+        """Upload a training split once; every later ``train_step(None, None)`` gathers its batch on
+        the device from ``perm[(global_step * B + b) % n]``. The permutation is redrawn at every
+        epoch boundary, which is ``DataSet.next_batch``'s per-epoch reshuffle without a host feed."""
+        x = _as_f32(images)
+        y = _labels_to_ids(labels)
+        n = x.shape[0]
+        self._perm_gen = torch.Generator().manual_seed(int(seed))
+        with torch.cuda.stream(self.stream):
+            self._dev_data = x.to(self.device, non_blocking=False).contiguous()
+            self._dev_labels = y.to(self.device).contiguous()
+            self._dev_perm = torch.randperm(n, generator=self._perm_gen).to(torch.int32).to(self.device)
+            self.eng.set_dataset(self._dev_data, self._dev_labels, self._dev_perm)
+            self.eng.set_input_mode(1)
+        self.stream.synchronize()
+        self._hstep = self.global_step()
+        self._epoch = (self._hstep * self.batch_size) // n
+
+    def last_device_batch(self):
+        """(x, y) device tensors of the batch the last device-input step trained on."""
+        n = self._dev_data.shape[0]
+        pos = ((self._hstep - 1) * self.batch_size + torch.arange(self.batch_size, device=self.device)) % n
+        with torch.cuda.stream(self.stream):
+            rows = self._dev_perm[pos].long()
+            out = self._dev_data[rows], self._dev_labels[rows]
+        self.stream.synchronize()
+        return out
+
+    def _device_batch(self) -> None:
+        n = self._dev_data.shape[0]
+        ep = (self._hstep * self.batch_size) // n
+        if ep != self._epoch:
+            self._epoch = ep
+            p = torch.randperm(n, generator=self._perm_gen).to(torch.int32)
+            with torch.cuda.stream(self.stream):
+                self._dev_perm.copy_(p.to(self.device))
 
     # ---- state ----
     def params(self) -> torch.Tensor:
@@ -209,6 +251,7 @@ class NativeMnistRunner(MnistRunnerBase):
     def set_global_step(self, s: int) -> None:
         with torch.cuda.stream(self.stream):
             self.eng.step_tensor().fill_(int(s))
+        self._hstep = int(s)
 
     def load_flat(self, flat, slots, step):
         with torch.cuda.stream(self.stream):
@@ -220,6 +263,7 @@ class NativeMnistRunner(MnistRunnerBase):
                 self.eng.adam_v().copy_(slots["v"].to(self.device))
             self.eng.step_tensor().fill_(int(step))
         self.stream.synchronize()
+        self._hstep = int(step)
 
     def slot_tensors(self):
         self.stream.synchronize()
@@ -252,9 +296,16 @@ class NativeMnistRunner(MnistRunnerBase):
             self.comm.broadcast(self.eng.step_tensor(), root)
             self.eng.sync_shadow()
         self.stream.synchronize()
+        self._hstep = int(self.eng.step_tensor().item())
 
     # ---- feeds ----
     def _feed(self, x, y) -> None:
+        if x is None:
+            assert self._dev_data is not None, "train_step(None, None) needs set_device_dataset() first"
+            self._device_batch()
+            return
+        if self._dev_data is not None:
+            raise ValueError("host batches fed to a runner in device-input mode")
         x = _as_f32(x)
         y = _labels_to_ids(y)
         assert x.shape[0] == self.batch_size, f"batch {x.shape[0]} != engine batch {self.batch_size}"
@@ -277,8 +328,10 @@ class NativeMnistRunner(MnistRunnerBase):
                     self.eng.replay("train", 1)
             else:
                 self.eng.train_step()
-        # the pinned staging buffers are reused next step: wait for the H2D copies to land
-        self.stream.synchronize()
+        self._hstep += 1
+        if x is not None:
+            # the pinned staging buffers are reused next step: wait for the H2D copies to land
+            self.stream.synchronize()
 
     def compute_grads(self, x, y) -> Tuple[torch.Tensor, float]:
         """Forward + backward only (no reduction / optimizer). Bumps the engine's local step."""
@@ -288,6 +341,7 @@ class NativeMnistRunner(MnistRunnerBase):
             self.eng.backward_a()
             self.eng.backward_b()
         self.stream.synchronize()
+        self._hstep += 1
         return self.eng.grads(), float(self.eng.loss_rows().mean().item())
 
     def reduce_grads(self, weight: float = 1.0) -> None:

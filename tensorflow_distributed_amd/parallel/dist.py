@@ -27,8 +27,9 @@ class DistContext:
     world: int = 1
     local_rank: int = 0
     device: Optional[torch.device] = None
-    comm: object = None  # torch.classes.tfd.RcclComm when world > 1 and on GPU
+    comm: object = None  # torch.classes.tfd.RcclComm when world > 1, on GPU, one rank per device
     initialized_pg: bool = False
+    shared_device: bool = False  # >= 2 ranks on one GPU: RCCL refuses that, the IPC transport carries DP
 
     @property
     def is_chief(self) -> bool:
@@ -111,7 +112,11 @@ def init_from_env(use_gpu: Optional[bool] = None, num_gpus: Optional[int] = None
         torch.cuda.set_device(idx)
         ctx.device = torch.device("cuda", idx)
         if rccl and world > 1:
-            ctx.comm = make_rccl_comm(rank, world, idx)
+            from .transport import devices_shared
+
+            ctx.shared_device = devices_shared(ctx.device, world)
+            if not ctx.shared_device:
+                ctx.comm = make_rccl_comm(rank, world, idx)
     else:
         ctx.device = torch.device("cpu")
     return ctx

@@ -93,6 +93,11 @@ def define_flags(task_index_default: int = 0, job_name_default: str = "ps") -> N
                     "pass and print a 'performance' table row (steps, training seconds, accuracy %, lr)")
     f.DEFINE_boolean("log_device_placement", False, "Print where every variable and the compute live "
                      "(ConfigProto.log_device_placement, mnist_python_m.py:257)")
+    f.DEFINE_enum("dp_transport", "auto", ["auto", "rccl", "ipc"], "GPU sync gradient transport: auto = "
+                  "peer-to-peer IPC when workers share a GPU (--num_gpus < workers; RCCL refuses that), else "
+                  "RCCL over xGMI (+ IPC one-shot for the small conv bucket)")
+    f.DEFINE_boolean("device_input", True, "GPU: upload the training split once and index it on the device "
+                     "by a per-epoch shuffle (no per-step host feed); False = host next_batch + H2D per step")
 
 
 def _make_optimizer():
@@ -103,22 +108,6 @@ def _make_optimizer():
     if FLAGS.optimizer == "momentum":
         return MomentumOptimizer(FLAGS.learning_rate, FLAGS.momentum)
     return AdamOptimizer(FLAGS.learning_rate)
-
-
-def _worker_rccl_comm(server, device):
-    import torch.distributed as dist
-
-    from .. import _native
-
-    _native.require()
-    c = server.cluster
-    src = c.num_ps  # global rank of worker 0
-    if server.rank == src:
-        uid = torch.classes.tfd.RcclComm.unique_id()
-    else:
-        uid = torch.zeros(128, dtype=torch.uint8)
-    dist.broadcast(uid, src, group=server.worker_group)
-    return torch.classes.tfd.RcclComm(uid, c.num_workers, server.task_index, device.index)
 
 
 def main(argv=None) -> int:
@@ -191,12 +180,23 @@ def main(argv=None) -> int:
             r2a = num_workers
         sopt = SyncReplicasOptimizer(opt, replicas_to_aggregate=r2a, total_num_replicas=num_workers).resolve(num_workers)
 
-    comm = None
-    if device.type == "cuda" and sync and num_workers > 1:
-        comm = _worker_rccl_comm(server, device)
     runner = make_runner(FLAGS.batch_size, opt, device, keep_prob=FLAGS.keep_prob, seed=FLAGS.seed,
-                         rank=FLAGS.task_index, comm=comm, bf16_grads=FLAGS.bf16_grads,
+                         rank=FLAGS.task_index, comm=None, bf16_grads=FLAGS.bf16_grads,
                          use_graph=FLAGS.use_graph and (sopt is None or not sopt.has_backup_workers))
+    comm = None
+    transport = None
+    if device.type == "cuda" and sync and num_workers > 1:
+        from ..parallel.transport import attach_engine
+
+        transport = attach_engine(runner.eng, FLAGS.task_index, num_workers, device, group=server.worker_group,
+                                  src=cluster.num_ps, mode=FLAGS.dp_transport, bf16=FLAGS.bf16_grads)
+        comm = transport.comm
+        runner.comm = comm
+        runner.transport = transport
+    device_input = device.type == "cuda" and FLAGS.device_input
+    if device_input:
+        runner.set_device_dataset(mnist.train.images, mnist.train.labels,
+                                  seed=FLAGS.seed * 1000 + FLAGS.task_index + 31)
 
     def init_fn():
         flat = M.flat_from_dict(M.init_params(FLAGS.seed))
@@ -244,7 +244,8 @@ def main(argv=None) -> int:
         for n in names:
             print("%s: %s" % (n, placed[n]))
         print("compute (conv_net, loss, gradients): %s; gradient sync: %s" % (
-            wdev, ("RCCL all-reduce" if comm is not None else "Gloo all-reduce") if sync else "async PS push/pull"))
+            wdev, (transport.kind + " all-reduce" if transport is not None else "Gloo all-reduce") if sync
+            else "async PS push/pull"))
 
     eval_at = sorted(int(v) for v in FLAGS.eval_at_steps.split(",") if v.strip()) if FLAGS.eval_at_steps else []
     eval_time = 0.0
@@ -275,7 +276,10 @@ def main(argv=None) -> int:
         if step >= FLAGS.train_steps:
             break
         with timer.phase("input"):
-            batch_xs, batch_ys = mnist.train.next_batch(FLAGS.batch_size)
+            if device_input:
+                batch_xs = batch_ys = None  # the engine gathers the batch on the device
+            else:
+                batch_xs, batch_ys = mnist.train.next_batch(FLAGS.batch_size)
         t0 = time.time()
         with timer.phase("step"), trace_range("train_step"):
             if sync:
@@ -319,6 +323,12 @@ def main(argv=None) -> int:
             os._exit(17)
 
     watchdog.stop()
+    if FLAGS.check_consistency_every and sync:
+        pp = runner.params().detach().double()
+        print("Worker %d: parameter checksum %.17g %.17g" % (FLAGS.task_index, float(pp.sum().item()),
+                                                             float((pp * pp).sum().item())))
+    if transport is not None:
+        transport.check("training")  # a timed-out IPC barrier must not pass as a finished run
     time_end = time.time()
     print("Training ends @ %f" % time_end)
     training_time = time_end - time_begin - eval_time
@@ -348,6 +358,8 @@ def main(argv=None) -> int:
     sv.stop(save=True)
     if client is not None:
         client.stop()
+    if transport is not None:
+        transport.close()
     server.mark_done()
     if sync and num_workers > 1:
         import torch.distributed as dist

@@ -146,3 +146,22 @@ def test_round_robin_placement():
     lay = async_ps.mnist_layout(2)
     assert [n for n, _, _ in lay.ranges[1]] == ["Variable", "Variable_2", "Variable_4", "Variable_6"]
     assert c.rank("ps", 1) == 1 and c.rank("worker", 0) == 2 and c.world_size == 3
+
+
+def _shared_worker(rank, world):
+    import torch
+
+    from tensorflow_distributed_amd.parallel.transport import device_key, devices_shared
+
+    same = devices_shared(torch.device("cuda", 0), world)
+    own = devices_shared(torch.device("cuda", rank), world)
+    return same, own, device_key(torch.device("cuda", rank))
+
+
+def test_transport_detects_shared_devices():
+    """Two ranks on 'gpu:0' share a device (IPC transport); gpu:0 + gpu:1 do not (RCCL)."""
+    from dist_util import run_ranks
+
+    res = run_ranks(_shared_worker, 2)
+    assert all(r[0] for r in res) and not any(r[1] for r in res)
+    assert res[0][2] != res[1][2]
