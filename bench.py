@@ -53,6 +53,10 @@ def main(argv=None):
                     "conv weight-gradient slabs and bumps the step (one kernel less)")
     ap.add_argument("--local_bf16_grads", type=int, default=1, help="1: on one GPU keep the fc-region gradients "
                     "in bf16 (the DP all-reduce wire format): fc backward writes and Adam reads 2 B per gradient")
+    ap.add_argument("--fc_adam", type=int, default=0, help="1: on one GPU, ApplyAdam of the fc region runs in "
+                    "the fc backward epilogues (the fc gradients never reach memory)")
+    ap.add_argument("--fc_adam_fork", type=int, default=0, help="1: that fused fc backward+Adam kernel on a side "
+                    "stream beside the conv backward")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu", action="store_true", help="plumbing dry-run: fp32 PyTorch CPU runner + Gloo "
@@ -80,6 +84,7 @@ def main(argv=None):
     eng.set_conv_fork(a.conv_fork)
     eng.set_fused_tail(a.fused_tail)
     eng.set_local_bf16_grads(a.local_bf16_grads)
+    eng.set_fc_adam(a.fc_adam, a.fc_adam_fork)
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     mode = a.transport
@@ -197,7 +202,8 @@ def main(argv=None):
                 "dp_transport": tr.kind,
                 "force_dp": bool(a.force_dp),
                 "zero1_fc1": bool(a.zero),
-                "fc_grads": "bf16" if (a.local_bf16_grads or world > 1) and not a.fp32_grads else "fp32",
+                "fc_grads": ("fused into Adam (fp32, in registers)" if world == 1 and a.fc_adam and not a.force_dp
+                             else "bf16" if (a.local_bf16_grads or world > 1) and not a.fp32_grads else "fp32"),
             },
         }), flush=True)
     tr.close()

@@ -18,9 +18,24 @@
 // Pipeline: register-staged double-buffered LDS (global loads of tile t+1 are issued before the
 // MFMAs on tile t and written after them), one barrier per K-tile.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace tfd {
+
+// Epilogues that declare `static constexpr bool WANTS_IJ = true` are called as
+// epi(m4, n, v, i, j) with the compile-time (after unrolling) tile indices of the lane's
+// accumulator, so they can consume per-tile values they prefetched before the K loop.
+template <class E, class = void>
+struct EpiWantsIJ : std::false_type {};
+template <class E>
+struct EpiWantsIJ<E, std::void_t<decltype(E::WANTS_IJ)>> : std::integral_constant<bool, E::WANTS_IJ> {};
+template <class EPI>
+__device__ __forceinline__ void epi_call(const EPI& epi, int m4, int n, const f32x4& v, int i, int j) {
+  if constexpr (EpiWantsIJ<EPI>::value) epi(m4, n, v, i, j);
+  else epi(m4, n, v);
+}
 
 template <int MN, int BK, bool KC>
 struct LdsTile {
@@ -215,7 +230,7 @@ __device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
-      epi(m0 + wm * WTM + 16 * i + 4 * (lane >> 4), n0 + wn * WTN + 16 * j + (lane & 15), acc[i][j]);
+      epi_call(epi, m0 + wm * WTM + 16 * i + 4 * (lane >> 4), n0 + wn * WTN + 16 * j + (lane & 15), acc[i][j], i, j);
 }
 
 // Whole-K variant for short, latency-bound K ranges (split-K slabs): the global loads of ALL NKT

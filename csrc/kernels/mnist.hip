@@ -450,7 +450,26 @@ constexpr int OUTG_BLOCKS = (HID + 1 + OUTG_ROWS - 1) / OUTG_ROWS;  // 17 (last 
 #define TFD_OUTG_LB 16
 #endif
 constexpr int OUTG_LB = TFD_OUTG_LB;  // hd loads batched per thread (a one-at-a-time loop was a 32-deep latency chain)
-__device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, float* smem) {
+__device__ __forceinline__ void adam1(const MnistAdamArgs& o, int64_t i, float g, float lr_t, float c1, float c2) {
+  float p = o.p[i], m = o.m[i], v = o.v[i];
+  m = m + (g - m) * c1;
+  v = v + (g * g - v) * c2;
+  p -= lr_t * m / (sqrtf(v) + o.eps);
+  o.p[i] = p;
+  o.m[i] = m;
+  o.v[i] = v;
+  o.pbf[i] = f2bf_bits(p);
+}
+struct AdamCoef {
+  float lr_t, c1, c2;
+};
+// TF ApplyAdam coefficients for step t (lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t))
+__device__ __forceinline__ AdamCoef adam_coef(const MnistAdamArgs& o, int64_t t) {
+  const float b1p = powf(o.beta1, (float)t), b2p = powf(o.beta2, (float)t);
+  return AdamCoef{o.lr * sqrtf(1.f - b2p) / (1.f - b1p), 1.f - o.beta1, 1.f - o.beta2};
+}
+__device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, float* smem,
+                                               const MnistAdamArgs* adam = nullptr) {
   float* dl = smem;                      // [B][10]
   float* part = smem + a.B * NCLS;       // [4][64][10]
   const int t = threadIdx.x, r = t & 63, q = t >> 6;
@@ -491,8 +510,14 @@ __device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, 
       const size_t o = OFF_OUT + (size_t)mm * NCLS + (i - rr * NCLS);
       const float g =
           part[i] + part[OUTG_ROWS * NCLS + i] + part[2 * OUTG_ROWS * NCLS + i] + part[3 * OUTG_ROWS * NCLS + i];
-      if (a.gbf_a) a.gbf_a[o] = f2bf_bits(g);
-      else a.grad[o] = g;
+      if (adam) {  // one GPU: the gradient goes straight into Adam (t = global_step + 1)
+        const AdamCoef c = adam_coef(*adam, *a.step + 1);
+        adam1(*adam, (int64_t)o, g, c.lr_t, c.c1, c.c2);
+      } else if (a.gbf_a) {
+        a.gbf_a[o] = f2bf_bits(g);
+      } else {
+        a.grad[o] = g;
+      }
     }
   }
 }
@@ -646,6 +671,75 @@ __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int pa
   id -= FDW_GX * FDW_GY;
   out_grad_block(a, id, (float*)smem_raw);
 #endif
+}
+
+// ---------------- K10 + K16 (one GPU): fc1 dW with ApplyAdam in the epilogue ----------------
+// The dW tile never reaches memory: every lane prefetches the fp32 master, m and v of the 16
+// parameters its accumulators will cover (4 tiles x one row x 4 columns, 16-B loads) BEFORE the
+// K loop, so their latency hides behind the GEMM; the epilogue turns "4 rows of one column" into
+// "4 columns of one row" with a 4-lane transpose (GradEpiT) and applies TF ApplyAdam in registers
+// (t = global_step + 1), writing p, m, v and the bf16 shadow once. Row 3136 (the ones row) is the
+// bias bd1, contiguous after the weights (mnist_layout.h), so the same indexing covers it.
+struct AdamDwEpi {
+  static constexpr bool WANTS_IJ = true;
+  const MnistAdamArgs& o;
+  const f32x4 (&P)[2][2];
+  const f32x4 (&Mm)[2][2];
+  const f32x4 (&V)[2][2];
+  AdamCoef c;
+  __device__ __forceinline__ static float pick(f32x4 v, int i) {
+    return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
+  }
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v, int i, int j) const {
+    const int lane = threadIdx.x & 63, q = lane & 3;
+    f32x4 r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = __shfl(pick(v, (q - k) & 3), (lane & ~3) | ((q + k) & 3), 64);
+    const f32x4 g = f32x4{pick(r, (0 - q) & 3), pick(r, (1 - q) & 3), pick(r, (2 - q) & 3), pick(r, (3 - q) & 3)};
+    const int m = m4 + q, nb = n - q;
+    if (m > FEAT) return;  // rows 0..3135 weights, 3136 bias
+    const int64_t e = OFF_WD1 + (int64_t)m * HID + nb;
+    f32x4 p = P[i][j], mm = Mm[i][j], vv = V[i][j];
+    mm = mm + (g - mm) * c.c1;
+    vv = vv + (g * g - vv) * c.c2;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) p[k] -= c.lr_t * mm[k] / (sqrtf(vv[k]) + o.eps);
+    *reinterpret_cast<f32x4*>(o.p + e) = p;
+    *reinterpret_cast<f32x4*>(o.m + e) = mm;
+    *reinterpret_cast<f32x4*>(o.v + e) = vv;
+    *reinterpret_cast<uint2*>(o.pbf + e) = make_uint2(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]));
+  }
+};
+static_assert(FDW_BM == 64 && FDW_BN == 64, "AdamDwEpi assumes 2x2 waves of 32x32");
+__device__ __forceinline__ void fc1_dw_adam_block(const MnistStepArgs& a, const MnistAdamArgs& o, int bx, int by,
+                                                  bf16* smem) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
+  const int m0 = by * FDW_BM, n0 = bx * FDW_BN;
+  f32x4 P[2][2], Mm[2][2], V[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int m = m0 + wm * 32 + 16 * i + 4 * (lane >> 4) + (lane & 3);
+      const int nb = n0 + wn * 32 + 16 * j + 4 * ((lane & 15) >> 2);
+      const int64_t e = OFF_WD1 + (int64_t)min(m, FEAT) * HID + nb;
+      P[i][j] = *reinterpret_cast<const f32x4*>(o.p + e);
+      Mm[i][j] = *reinterpret_cast<const f32x4*>(o.m + e);
+      V[i][j] = *reinterpret_cast<const f32x4*>(o.v + e);
+    }
+  OnesRowMC la{a.p2, FEAT, FEAT, a.B};
+  DenseLoader<false> lb{a.dh, HID, HID, a.B};
+  AdamDwEpi epi{o, P, Mm, V, adam_coef(o, *a.step + 1)};
+  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, m0, n0, 0, a.B, smem);
+}
+// [out-layer grad + Adam blocks | fc1 dW + Adam tiles]; the dX GEMM ran before (part 2), so the
+// fc1 weights it read are not yet updated.
+__global__ __launch_bounds__(256) void fc1_bwd_adam(MnistStepArgs a, MnistAdamArgs o) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  int id = blockIdx.x;
+  if (id < OUTG_BLOCKS) { out_grad_block(a, id, (float*)smem_raw, &o); return; }
+  id -= OUTG_BLOCKS;
+  fc1_dw_adam_block(a, o, id % FDW_GX, id / FDW_GX, (bf16*)smem_raw);
 }
 
 // ---------------- K13 conv2 dgrad (+ conv1 relu/pool mask epilogue) ----------------
@@ -1115,19 +1209,27 @@ __global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a) {
 }
 
 // ---------------- one-GPU optimizer tail: K16 ApplyAdam with the K12/K14/K15 slab reduce fused ----------------
-// Grid = [208 conv1 blocks | 801 conv2 blocks | MAD_FC_BLOCKS grid-stride blocks]:
-//   conv1: block j owns float4 j of the 832 conv1 weight/bias gradients, one slab (of 2B) per thread;
-//   conv2: block owns 16 float4s, a 16-lane group per float4 sums slabs l, l + 16, ... (independent
-//          loads, fixed order) then a 16-lane butterfly;
+// Grid = [13 conv1 blocks | 201 conv2 blocks | MAD_FC_BLOCKS grid-stride blocks]:
+//   conv1: block owns 16 float4 of the 832 conv1 weight/bias gradients; thread (q = t >> 4, x = t & 15)
+//          sums slabs q, q + 16, ... of float4 x (16-lane groups read 256 contiguous bytes per slab,
+//          every load issued before the first add), then the 16 partials are summed in LDS in q order;
+//   conv2: block owns 64 float4; thread (q = t >> 6, x = t & 63) sums slabs q, q + 4, ... (each wave
+//          reads 1 KiB contiguous per slab), then 4 partials in LDS in q order;
 //   fc:    plain grid-stride Adam over the flat gradient buffer.
-// Every gradient reduction is deterministic. t comes from the head kernel (MnistStepArgs::t_out),
-// so nothing here reads the global_step that the last block bumps.
+// Every gradient reduction is deterministic (fixed order). t comes from the head kernel
+// (MnistStepArgs::t_out), so nothing here reads the global_step that the last block bumps.
+// (The previous layout -- one 16-lane group per float4, each lane a different slab -- made every
+//  wave instruction touch 64 scattered 16-B pieces: 7.6 us for the conv region alone.)
 constexpr int MAD_NT = 256;
 constexpr int MAD_C1F4 = (int)(OFF_WC2 / 4);   // 208
 constexpr int MAD_C2END = (int)(OFF_WD1 / 4);  // 13024
-constexpr int MAD_C2BLK = (MAD_C2END - MAD_C1F4 + 15) / 16;  // 801
+constexpr int MAD_C1BLK = MAD_C1F4 / 16;       // 13
+constexpr int MAD_C2BLK = (MAD_C2END - MAD_C1F4 + 63) / 64;  // 201
 constexpr int MAD_FC_BLOCKS = 1024;
-constexpr int MAD_GRID = MAD_C1F4 + MAD_C2BLK + MAD_FC_BLOCKS;
+constexpr int MAD_CONV = MAD_C1BLK + MAD_C2BLK;
+constexpr int MAD_GRID = MAD_CONV + MAD_FC_BLOCKS;
+static_assert(MAD_C1F4 % 16 == 0, "conv1 region: whole blocks");
+constexpr int MAD_SL = 16;  // slab loads in flight per thread
 __device__ __forceinline__ void adam4(const MnistAdamArgs& o, int64_t i, f32x4 g, float lr_t, float c1, float c2) {
   f32x4 p = reinterpret_cast<f32x4*>(o.p)[i];
   f32x4 m = reinterpret_cast<f32x4*>(o.m)[i];
@@ -1141,43 +1243,53 @@ __device__ __forceinline__ void adam4(const MnistAdamArgs& o, int64_t i, f32x4 g
   reinterpret_cast<f32x4*>(o.v)[i] = v;
   reinterpret_cast<uint2*>(o.pbf)[i] = make_uint2(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]));
 }
+// sum over slabs q, q + QS, ... (< ns) of float4 column x of a [ns][stride4] slab array; MAD_SL loads
+// issued per batch before any add
+template <int QS>
+__device__ __forceinline__ f32x4 slab_sum(const f32x4* __restrict__ s4, int64_t stride4, int ns, int q, int x) {
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = q; k0 < ns; k0 += QS * MAD_SL) {
+    f32x4 v[MAD_SL];
+#pragma unroll
+    for (int u = 0; u < MAD_SL; ++u) {
+      const int k = k0 + u * QS;
+      v[u] = k < ns ? s4[(size_t)k * stride4 + x] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < MAD_SL; ++u) acc += v[u];
+  }
+  return acc;
+}
 __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, MnistAdamArgs o) {
+  // gridDim.x == MAD_CONV: the fc region was updated by fc1_bwd_adam; the last conv2 block bumps
+  // the step instead
+  if (gridDim.x == MAD_CONV && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *o.step += 1;
   const int64_t t = *o.t;
   const float b1p = powf(o.beta1, (float)t), b2p = powf(o.beta2, (float)t);
   const float lr_t = o.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float c1 = 1.f - o.beta1, c2 = 1.f - o.beta2;
   const int bid = blockIdx.x, tid = threadIdx.x;
-  if (bid < MAD_C1F4) {
-    __shared__ f32x4 red[MAD_NT / 64];
-    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int q = tid; q < 2 * a.B; q += MAD_NT) s += reinterpret_cast<const f32x4*>(a.wg1_slab + (size_t)q * 832)[bid];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) s[j] = wave_sum(s[j]);
-    if ((tid & 63) == 0) red[tid >> 6] = s;
-    __syncthreads();
-    if (tid == 0) adam4(o, bid, (red[0] + red[1]) + (red[2] + red[3]), lr_t, c1, c2);
-  } else if (bid < MAD_C1F4 + MAD_C2BLK) {
-    constexpr int64_t SLAB4 = 801 * 64 / 4;
-    const int64_t i = MAD_C1F4 + (int64_t)(bid - MAD_C1F4) * 16 + (tid >> 4);
-    const int sl = tid & 15, ns = a.wg2_splits;
-    const f32x4* s4 = reinterpret_cast<const f32x4*>(a.wg2_slab) + (i - MAD_C1F4);
-    f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f}, g1 = g0;
-    if (i < MAD_C2END) {
-      int k = sl;
-      for (; k + 16 < ns; k += 32) {  // two independent loads in flight per lane
-        g0 += s4[(size_t)k * SLAB4];
-        g1 += s4[(size_t)(k + 16) * SLAB4];
-      }
-      if (k < ns) g0 += s4[(size_t)k * SLAB4];
+  if (bid < MAD_CONV) {
+    __shared__ f32x4 red[MAD_NT];
+    const bool one = bid < MAD_C1BLK;
+    const int q = one ? tid >> 4 : tid >> 6, x = one ? tid & 15 : tid & 63;
+    const int64_t i = one ? (int64_t)bid * 16 + x : MAD_C1F4 + (int64_t)(bid - MAD_C1BLK) * 64 + x;
+    f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (one) {
+      g = slab_sum<16>(reinterpret_cast<const f32x4*>(a.wg1_slab) + i, 832 / 4, 2 * a.B, q, 0);
+    } else if (i < MAD_C2END) {
+      g = slab_sum<4>(reinterpret_cast<const f32x4*>(a.wg2_slab) + (i - MAD_C1F4), 801 * 64 / 4, a.wg2_splits, q, 0);
     }
-    f32x4 g = g0 + g1;
-#pragma unroll
-    for (int off = 8; off >= 1; off >>= 1)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) g[j] += __shfl_xor(g[j], off, 16);
-    if (sl == 0 && i < MAD_C2END) adam4(o, i, g, lr_t, c1, c2);
+    red[tid] = g;
+    __syncthreads();
+    if (q == 0 && i < MAD_C2END) {
+      const int nq = one ? 16 : 4, qs = one ? 16 : 64;
+      f32x4 s = red[x];
+      for (int k = 1; k < nq; ++k) s += red[k * qs + x];
+      adam4(o, i, s, lr_t, c1, c2);
+    }
   } else {
-    const int64_t i0 = MAD_C2END + (int64_t)(bid - MAD_C1F4 - MAD_C2BLK) * MAD_NT + tid;
+    const int64_t i0 = MAD_C2END + (int64_t)(bid - MAD_CONV) * MAD_NT + tid;
     constexpr int64_t STRIDE = (int64_t)MAD_FC_BLOCKS * MAD_NT;
 #if TFD_ADAM_U > 1
     // All U strides' loads issued before any math/store, so U x 56 B per lane are in flight
@@ -1346,8 +1458,16 @@ void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s) {
   reduce_conv_grads<<<RED2_BLOCKS + RED1_BLOCKS, 256, 0, s>>>(a);
 }
 
-void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s) {
-  mnist_adam_kernel<<<MAD_GRID, MAD_NT, 0, s>>>(a, o);
+void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region) {
+  mnist_adam_kernel<<<fc_region ? MAD_GRID : MAD_CONV, MAD_NT, 0, s>>>(a, o);
+}
+
+void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s) {
+  constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, DenseLoader<false>>::BYTES;
+  const int sm_og = (a.B * NCLS + 4 * OUTG_ROWS * NCLS) * 4;
+  const int sm = std::max(sm_dw, sm_og);
+  set_smem<fc1_bwd_adam>(sm);
+  fc1_bwd_adam<<<OUTG_BLOCKS + FDW_GX * FDW_GY, 256, sm, s>>>(a, o);
 }
 
 }  // namespace tfd

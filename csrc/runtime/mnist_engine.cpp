@@ -180,6 +180,9 @@ class MnistEngine : public torch::CustomClassHolder {
   void set_fused_tail(int64_t on) { fuse_tail_ = on != 0; }
   // one GPU, fused tail: keep the fc-region gradients in bf16 (as DP all-reduces them)
   void set_local_bf16_grads(int64_t on) { local_bf16_grads_ = on != 0; }
+  // one GPU + Adam: fc-region ApplyAdam fused into the fc backward (gradients never reach memory);
+  // fork = that kernel on a side stream beside the conv backward
+  void set_fc_adam(int64_t on, int64_t fork) { fc_adam_ = on != 0; fc_adam_fork_ = fork != 0; }
   // make every rank's bf16 shadow whole again (after the last zero step, before eval/checkpoint)
   void sync_params() {
     if (!zero_) return;
@@ -242,6 +245,28 @@ class MnistEngine : public torch::CustomClassHolder {
       // weight-gradient slabs itself and bumps the step (its t was written by the head kernel).
       const bool fused = opt_ == 0 && fuse_tail_;
       if (fused) a.t_out = (int64_t*)tnext_.data_ptr();
+      MnistAdamArgs o{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(),
+                      (uint16_t*)pbf_.data_ptr(), (float)lr_, (float)b1_, (float)b2_, (float)eps_,
+                      (const int64_t*)tnext_.data_ptr(), (int64_t*)step_.data_ptr(), nullptr};
+      if (fused && fc_adam_) {
+        // fc-region Adam inside the fc backward epilogues (dX first: it reads the old fc1 weights);
+        // optionally on a side stream beside the conv backward, which only needs dX
+        mnist_forward(a, true, s);
+        mnist_backward_a(a, s, 2);
+        hipStream_t fs = fc_adam_fork_ ? opt_stream_ : s;
+        if (fc_adam_fork_) {
+          HIP_OK(hipEventRecord(ev_a_, s));
+          HIP_OK(hipStreamWaitEvent(fs, ev_a_, 0));
+        }
+        mnist_backward_a_adam(a, o, fs);
+        mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
+        if (fc_adam_fork_) {
+          HIP_OK(hipEventRecord(ev_opt_a_, fs));
+          HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+        }
+        mnist_adam_fused(a, o, s, false);
+        return;
+      }
       // bf16 fc-region gradients (the DP wire format): the fc backward writes 2 B and Adam reads
       // 2 B per gradient instead of 4 + 4 (13 MB less HBM traffic per step)
       const bool gbf_local = fused && local_bf16_grads_;
@@ -251,10 +276,7 @@ class MnistEngine : public torch::CustomClassHolder {
       a.step_bump = (int64_t*)step_.data_ptr();
       mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
       if (fused) {
-        MnistAdamArgs o{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(),
-                        (uint16_t*)pbf_.data_ptr(), (float)lr_, (float)b1_, (float)b2_, (float)eps_,
-                        (const int64_t*)tnext_.data_ptr(), (int64_t*)step_.data_ptr(),
-                        gbf_local ? (const uint16_t*)gbf_.data_ptr() : nullptr};
+        o.gbf = gbf_local ? (const uint16_t*)gbf_.data_ptr() : nullptr;
         mnist_adam_fused(a, o, s);
       } else {
         mnist_conv_grad_reduce(a, s);
@@ -534,6 +556,7 @@ class MnistEngine : public torch::CustomClassHolder {
   // one GPU + Adam: the optimizer kernel also reduces the conv gradient slabs and bumps the step
   bool fuse_tail_ = true;
   bool local_bf16_grads_ = false;
+  bool fc_adam_ = false, fc_adam_fork_ = false;  // measured slower (docs/DESIGN.md)
   std::map<std::string, hipGraphExec_t> graphs_;
 };
 
@@ -582,6 +605,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_conv_fork", &MnistEngine::set_conv_fork)
       .def("set_fused_tail", &MnistEngine::set_fused_tail)
       .def("set_local_bf16_grads", &MnistEngine::set_local_bf16_grads)
+      .def("set_fc_adam", &MnistEngine::set_fc_adam)
       .def("zero", &MnistEngine::zero)
       .def("sync_params", &MnistEngine::sync_params)
       .def("world", &MnistEngine::world)

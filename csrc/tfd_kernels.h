@@ -69,7 +69,11 @@ struct MnistAdamArgs {
   int64_t* step;
   const uint16_t* gbf;  // if non-null: the fc-region (bucket A) gradients are bf16 here (gbf_a)
 };
-void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s);
+// fc_region = false: the conv region only (the fc region was updated by mnist_backward_a_adam)
+void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region = true);
+// One GPU: fc1 dW and the output-layer gradients with ApplyAdam fused into their epilogues (the fc
+// gradients never reach memory; t = global_step + 1). Launch after the dX GEMM (part 2).
+void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s);
 
 // ---------------- optimizers (flat, fp32 master + bf16 shadow) ----------------
 struct AdamArgs {

@@ -202,3 +202,42 @@ def test_local_bf16_fc_grads_match_fp32(cuda):
     fc = slice(M.BUCKET_SPLIT, None)
     assert _relerr(d0[fc], d1[fc]) < 2e-2
     assert torch.equal(engs[0].params_bf16(), engs[0].params().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("fork", [0, 1])
+def test_fc_adam_in_backward_epilogue_matches_separate_adam(cuda, fork):
+    """One GPU: ApplyAdam of the fc region inside the fc1 dW / out-layer gradient epilogues
+    (set_fc_adam) == the separate fused-tail Adam over fp32 gradients, up to the conv-slab
+    summation order; bf16 shadow stays the rounding of the fp32 master."""
+    B = 128
+    params = M.flat_from_dict(M.init_params(19)).to(cuda) * 0.05
+    n = 1024
+    data = torch.rand(n, 784, device=cuda)
+    labels = torch.randint(0, 10, (n,), dtype=torch.int32, device=cuda)
+    perm = torch.randperm(n, device=cuda).to(torch.int32)
+    engs = []
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for on in (1, 0):
+            e = _engine(B, cuda, keep=0.75)
+            e.set_adam(0.01, 0.9, 0.999, 1e-8)
+            e.set_local_bf16_grads(0)
+            e.set_fc_adam(on, fork)
+            e.params().copy_(params)
+            e.sync_shadow()
+            e.set_dataset(data, labels, perm)
+            e.set_input_mode(1)
+            engs.append(e)
+        for e in engs:
+            e.train_step()
+            e.capture_train_step("g")
+            e.replay("g", 2)
+    torch.cuda.synchronize()
+    assert [int(e.step_tensor().item()) for e in engs] == [3, 3]
+    d0 = engs[0].params() - params
+    d1 = engs[1].params() - params
+    fc = slice(M.BUCKET_SPLIT, None)
+    assert _relerr(d0[fc], d1[fc]) < 1e-3, _relerr(d0[fc], d1[fc])
+    assert _relerr(d0, d1) < 1e-3, _relerr(d0, d1)
+    assert torch.equal(engs[0].params_bf16(), engs[0].params().to(torch.bfloat16))
+    assert torch.allclose(engs[0].adam_v(), engs[1].adam_v(), rtol=1e-3, atol=1e-12)
