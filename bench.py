@@ -44,9 +44,9 @@ def main(argv=None):
                     "untimed steps until this much warm-up time has passed (GPU clock ramp; reported in the JSON)")
     ap.add_argument("--graph_steps", type=int, default=20, help="training steps captured per hipGraph "
                     "(device-side step counter/data cursor/dropout key make step i+1 of a graph the next step)")
+    ap.add_argument("--phases", type=int, default=1, help="after the timed steps, replay a few steps of a graph "
+                    "with HIP timing events at the phase boundaries and report the GPU phase breakdown (untimed)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16"], help="compute dtype of the MFMA operands")
-    ap.add_argument("--opt_overlap", type=int, default=0, help="1: run the fc-region optimizer on a side "
-                    "stream overlapping the conv backward (0: on the main stream after it)")
     ap.add_argument("--conv_fork", type=int, default=0, help="1: conv2 wgrad on a forked stream beside dgrad")
     ap.add_argument("--zero", type=int, default=0, help="1: ZeRO-1 sharding of the fc1 weight (N > 1)")
     ap.add_argument("--fused_tail", type=int, default=1, help="1: on one GPU the Adam kernel also reduces the "
@@ -80,7 +80,6 @@ def main(argv=None):
     B = a.batch_size
     eng = torch.classes.tfd.MnistEngine(B, dev.index, 0.75, a.seed, rank)
     eng.set_adam(a.lr, 0.9, 0.999, 1e-8)
-    eng.set_opt_overlap(a.opt_overlap)
     eng.set_conv_fork(a.conv_fork)
     eng.set_fused_tail(a.fused_tail)
     eng.set_local_bf16_grads(a.local_bf16_grads)
@@ -168,6 +167,7 @@ def main(argv=None):
             eng.sync_params()
     dt = ctx.max_scalar(dt)
     tr.check("after the timed steps")
+    phases = _phase_breakdown(eng, s, graph_mode, world, ctx) if a.phases else None
     loss1 = float(eng.loss_rows().mean().item())
     gstep = int(eng.step_tensor().item())
     ms = dt * 1e3 / a.steps
@@ -189,6 +189,7 @@ def main(argv=None):
             "vs_baseline": round(img_s / BASELINE_IMG_PER_S, 1),
             "dtype": "bf16",
             "data": "synthetic (device-resident MNIST-shaped 55000x784, random labels; random N(0,1) init)",
+            "phases_ms": phases,
             "config": {
                 "model": "MNIST 2-conv CNN (reference conv_net: conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout0.75-fc10), "
                          "Adam lr 0.01",
@@ -209,6 +210,36 @@ def main(argv=None):
     tr.close()
     ctx.shutdown()
     return 0
+
+
+def _phase_breakdown(eng, stream, graph_mode, world, ctx):
+    """GPU ms of fwd / fc bwd / conv bwd / optimizer / all-reduce of one step, from HIP timing
+    events inside a separately captured graph (outside the timed region; median of 5 steps)."""
+    import torch
+
+    names = ("fwd", "bwd_fc", "bwd_conv", "optim", "allreduce", "comm_wait", "step")
+    try:
+        eng.set_phase_timing(True)
+        rows = []
+        with torch.cuda.stream(stream):
+            eng.train_step()  # HIP needs an eager record of the timing events before graph replays time them
+            if graph_mode:
+                eng.capture_train_step("phases")
+            for _ in range(5):
+                if graph_mode:
+                    eng.replay("phases", 1)
+                else:
+                    eng.train_step()
+                rows.append(eng.phase_times().tolist())
+        eng.set_phase_timing(False)
+        if graph_mode:
+            eng.drop_graph("phases")
+        ctx.barrier()
+        med = [sorted(r[i] for r in rows)[len(rows) // 2] for i in range(len(names))]
+        return {k: round(v, 4) for k, v in zip(names, med)}
+    except Exception as e:  # pragma: no cover - event capture support depends on the HIP build
+        print(f"# phase timing unavailable: {e!r}", file=sys.stderr)
+        return None
 
 
 def _cpu_dry_run(a):

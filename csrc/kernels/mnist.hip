@@ -1174,7 +1174,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad(MnistStepArgs a) {
 // thread (x = output column of a 64-wide chunk, y = slab phase 0..3); fixed summation order.
 template <int XW>  // XW outputs per block row, 256/XW slab phases
 __device__ __forceinline__ void reduce_chunk(const float* __restrict__ slab, int nslab, int64_t stride, int n, int i0,
-                                             float* __restrict__ out, float* red) {
+                                             float* __restrict__ out, uint16_t* __restrict__ outbf, float* red) {
   constexpr int NY = 256 / XW;
   const int x = threadIdx.x % XW, y = threadIdx.x / XW, i = i0 + x;
   float s = 0.f;
@@ -1193,7 +1193,8 @@ __device__ __forceinline__ void reduce_chunk(const float* __restrict__ slab, int
     float r = 0.f;
 #pragma unroll
     for (int q = 0; q < NY; ++q) r += red[q * XW + x];
-    out[i] = r;
+    if (outbf) outbf[i] = f2bf_bits(r);  // DP bf16 wire format: no separate cast pass
+    else out[i] = r;
   }
 }
 constexpr int RED2_BLOCKS = (801 * 64 + 63) / 64;  // 801 blocks x 64 outputs (4 phases over the B/2 slabs)
@@ -1202,9 +1203,11 @@ __global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a) {
   __shared__ float red[256];
   const int id = blockIdx.x;
   if (id < RED2_BLOCKS)
-    reduce_chunk<64>(a.wg2_slab, a.wg2_splits, 801 * 64, 801 * 64, id * 64, a.grad + OFF_WC2, red);
+    reduce_chunk<64>(a.wg2_slab, a.wg2_splits, 801 * 64, 801 * 64, id * 64, a.grad + OFF_WC2,
+                     a.gbf_b ? a.gbf_b + OFF_WC2 : nullptr, red);
   else
-    reduce_chunk<16>(a.wg1_slab, 2 * a.B, 832, 832, (id - RED2_BLOCKS) * 16, a.grad + OFF_WC1, red);
+    reduce_chunk<16>(a.wg1_slab, 2 * a.B, 832, 832, (id - RED2_BLOCKS) * 16, a.grad + OFF_WC1,
+                     a.gbf_b ? a.gbf_b + OFF_WC1 : nullptr, red);
   if (id == 0 && threadIdx.x == 0 && a.step_bump) *a.step_bump += 1;  // see MnistStepArgs::step_bump
 }
 

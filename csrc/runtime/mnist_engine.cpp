@@ -76,6 +76,7 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipEventCreateWithFlags(&ev_ag_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    for (auto& e : pev_) HIP_OK(hipEventCreate(&e));  // timing events (phase timer)
   }
   ~MnistEngine() override {
     for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
@@ -90,6 +91,7 @@ class MnistEngine : public torch::CustomClassHolder {
     hipEventDestroy(ev_opt_a_);
     hipEventDestroy(ev_start_);
     hipEventDestroy(ev_ag_);
+    for (auto& e : pev_) hipEventDestroy(e);
   }
 
   // ---- state accessors (views share storage with the engine) ----
@@ -174,7 +176,6 @@ class MnistEngine : public torch::CustomClassHolder {
     zero_ = true;
   }
   bool zero() const { return zero_; }
-  void set_opt_overlap(int64_t on) { opt_overlap_ = on; }
   // conv2 wgrad on a forked stream beside dgrad -> conv1 wgrad (1) or all on the main stream (0)
   void set_conv_fork(int64_t on) { conv_fork_ = on != 0; }
   void set_fused_tail(int64_t on) { fuse_tail_ = on != 0; }
@@ -188,6 +189,35 @@ class MnistEngine : public torch::CustomClassHolder {
     if (!zero_) return;
     hipStream_t s = stream();
     ag_w(s);
+  }
+
+  // ---- per-phase GPU timing ----
+  // With timing on, train_step records HIP timing events at its phase boundaries -- also inside a
+  // captured graph (event-record nodes) -- and phase_times() returns the last step's
+  //   [forward, fc backward, conv backward, optimizer, allreduce (sum of the bucket collectives on
+  //    the comm stream; 0 on one GPU), exposed comm wait, step] in milliseconds.
+  void set_phase_timing(bool on) { timing_ = on; }
+  at::Tensor phase_times() {
+    auto out = at::zeros({7}, at::TensorOptions().dtype(at::kFloat));
+    if (!timing_ || !timed_) return out;
+    HIP_OK(hipEventSynchronize(pev_[P_OPT]));
+    float* o = out.data_ptr<float>();
+    auto el = [&](int a, int b) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, pev_[a], pev_[b]) == hipSuccess) return ms;
+      (void)hipGetLastError();  // not sticky: a pair that cannot be timed reports -1
+      return -1.f;
+    };
+    o[0] = el(P_START, P_FWD);
+    o[1] = el(P_FWD, P_BFC);
+    o[2] = el(P_BFC, P_BCONV);
+    o[3] = el(P_BCONV, P_OPT);
+    if (timed_dp_) {
+      o[4] = el(P_CA0, P_CA1) + el(P_CB0, P_CB1);
+      o[5] = el(P_BCONV, P_CB1);
+    }
+    o[6] = el(P_START, P_OPT);
+    return out;
   }
 
   // ---- step pieces (current HIP stream) ----
@@ -205,13 +235,15 @@ class MnistEngine : public torch::CustomClassHolder {
     apply_optimizer_range(0, TOTAL, grad_scale, 0, stream());
   }
   // Optimizer over the flat range [beg, end) on stream s; t = global_step + t_offset.
-  void apply_optimizer_range(int64_t beg, int64_t end, double grad_scale, int t_offset, hipStream_t s) {
+  void apply_optimizer_range(int64_t beg, int64_t end, double grad_scale, int t_offset, hipStream_t s,
+                             const int64_t* tsrc = nullptr) {
     const uint16_t* gbf = (bf16_comm_ && dp()) ? (const uint16_t*)gbf_.data_ptr() + beg : nullptr;
     const int64_t n = end - beg;
     if (opt_ == 0) {
       AdamArgs a{(float*)params_.data_ptr() + beg, (float*)m_.data_ptr() + beg, (float*)v_.data_ptr() + beg,
                  (const float*)grad_.data_ptr() + beg, (uint16_t*)pbf_.data_ptr() + beg, gbf, n, (float)lr_,
-                 (float)b1_, (float)b2_, (float)eps_, (const int64_t*)step_.data_ptr(), t_offset, (float)grad_scale};
+                 (float)b1_, (float)b2_, (float)eps_, tsrc ? tsrc : (const int64_t*)step_.data_ptr(), t_offset,
+                 (float)grad_scale};
       adam_apply(a, s);
     } else {
       SgdArgs a{(float*)params_.data_ptr() + beg, opt_ == 2 ? (float*)m_.data_ptr() + beg : nullptr,
@@ -222,100 +254,138 @@ class MnistEngine : public torch::CustomClassHolder {
   }
 
   // Full synchronous data-parallel step (the reference's SyncReplicasOptimizer global step with
-  // replicas_to_aggregate == num_workers: averaged grads, one ApplyAdam, global_step += 1):
-  //   main: fwd -> fc bwd (bucket A ready) -> conv bwd -> conv-grad reduce + step bump (bucket B
-  //         ready) -> [wait A] optimizer on A -> [wait B] optimizer on B
-  //   comm:                     all-reduce A (overlaps the conv bwd)  -> all-reduce B (overlaps the
-  //                                                                       optimizer on A)
-  // One GPU: one optimizer launch over the whole buffer after the reduce. opt_overlap_: region A's
-  // optimizer runs on a side stream right after its bucket, beside the conv backward (the fc params
-  // are not read again this step; the reduce waits for it, so it reads the pre-bump step).
-  void train_step() {
+  // replicas_to_aggregate == num_workers: averaged grads, one ApplyAdam, global_step += 1).
+  // One GPU: fused forward/backward and ONE optimizer kernel (it also reduces the conv slabs).
+  // DP (train_step_dp): three streams, the fc-region optimizer deferred into the next step.
+  void train_step() { train_step_impl(true); }
+
+  void train_step_impl(bool join_end) {
     if (zero_) {
       train_step_zero();
       return;
     }
     hipStream_t s = stream();
     const bool dp = this->dp();
-    const double scale = 1.0 / (double)world();
-    hipStream_t ws = conv_fork_ ? aux_stream_ : nullptr;
-    MnistStepArgs a = args();
-    if (!dp && !opt_overlap_) {
-      // one GPU: nothing to overlap with. With Adam ONE kernel ends the step: it reduces the conv
-      // weight-gradient slabs itself and bumps the step (its t was written by the head kernel).
-      const bool fused = opt_ == 0 && fuse_tail_;
-      if (fused) a.t_out = (int64_t*)tnext_.data_ptr();
-      MnistAdamArgs o{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(),
-                      (uint16_t*)pbf_.data_ptr(), (float)lr_, (float)b1_, (float)b2_, (float)eps_,
-                      (const int64_t*)tnext_.data_ptr(), (int64_t*)step_.data_ptr(), nullptr};
-      if (fused && fc_adam_) {
-        // fc-region Adam inside the fc backward epilogues (dX first: it reads the old fc1 weights);
-        // optionally on a side stream beside the conv backward, which only needs dX
-        mnist_forward(a, true, s);
-        mnist_backward_a(a, s, 2);
-        hipStream_t fs = fc_adam_fork_ ? opt_stream_ : s;
-        if (fc_adam_fork_) {
-          HIP_OK(hipEventRecord(ev_a_, s));
-          HIP_OK(hipStreamWaitEvent(fs, ev_a_, 0));
-        }
-        mnist_backward_a_adam(a, o, fs);
-        mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
-        if (fc_adam_fork_) {
-          HIP_OK(hipEventRecord(ev_opt_a_, fs));
-          HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
-        }
-        mnist_adam_fused(a, o, s, false);
-        return;
-      }
-      // bf16 fc-region gradients (the DP wire format): the fc backward writes 2 B and Adam reads
-      // 2 B per gradient instead of 4 + 4 (13 MB less HBM traffic per step)
-      const bool gbf_local = fused && local_bf16_grads_;
-      if (gbf_local) a.gbf_a = (uint16_t*)gbf_.data_ptr();
-      mnist_forward(a, true, s);
-      mnist_backward_a(a, s);
-      a.step_bump = (int64_t*)step_.data_ptr();
-      mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
-      if (fused) {
-        o.gbf = gbf_local ? (const uint16_t*)gbf_.data_ptr() : nullptr;
-        mnist_adam_fused(a, o, s);
-      } else {
-        mnist_conv_grad_reduce(a, s);
-        apply_optimizer_range(0, TOTAL, scale, 0, s);
-      }
+    timed_ = timing_;
+    timed_dp_ = timing_ && dp;
+    if (dp) {
+      train_step_dp(join_end);
       return;
     }
+    mark(P_START, s);
+    hipStream_t ws = conv_fork_ ? aux_stream_ : nullptr;
+    MnistStepArgs a = args();
+    // one GPU: nothing to overlap with. With Adam ONE kernel ends the step: it reduces the conv
+    // weight-gradient slabs itself and bumps the step (its t was written by the head kernel).
+    const bool fused = opt_ == 0 && fuse_tail_;
+    if (fused) a.t_out = (int64_t*)tnext_.data_ptr();
+    MnistAdamArgs o{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(),
+                    (uint16_t*)pbf_.data_ptr(), (float)lr_, (float)b1_, (float)b2_, (float)eps_,
+                    (const int64_t*)tnext_.data_ptr(), (int64_t*)step_.data_ptr(), nullptr};
+    if (fused && fc_adam_) {
+      // fc-region Adam inside the fc backward epilogues (dX first: it reads the old fc1 weights);
+      // optionally on a side stream beside the conv backward, which only needs dX
+      mnist_forward(a, true, s);
+      mark(P_FWD, s);
+      mnist_backward_a(a, s, 2);
+      mark(P_BFC, s);
+      hipStream_t fs = fc_adam_fork_ ? opt_stream_ : s;
+      if (fc_adam_fork_) {
+        HIP_OK(hipEventRecord(ev_a_, s));
+        HIP_OK(hipStreamWaitEvent(fs, ev_a_, 0));
+      }
+      mnist_backward_a_adam(a, o, fs);
+      mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
+      if (fc_adam_fork_) {
+        HIP_OK(hipEventRecord(ev_opt_a_, fs));
+        HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+      }
+      mark(P_BCONV, s);
+      mnist_adam_fused(a, o, s, false);
+      mark(P_OPT, s);
+      return;
+    }
+    // bf16 fc-region gradients (the DP wire format): the fc backward writes 2 B and Adam reads
+    // 2 B per gradient instead of 4 + 4 (13 MB less HBM traffic per step)
+    const bool gbf_local = fused && local_bf16_grads_;
+    if (gbf_local) a.gbf_a = (uint16_t*)gbf_.data_ptr();
     mnist_forward(a, true, s);
-    if (fused_bf16_a()) a.gbf_a = (uint16_t*)gbf_.data_ptr();
-    // DP: dW + out-layer grads first, so bucket A's all-reduce starts before the dX GEMM (not with
-    // opt_overlap_, whose region-A optimizer would rewrite the weights dX reads)
-    const bool split = dp && !opt_overlap_;
-    mnist_backward_a(a, s, split ? 1 : 0);
+    mark(P_FWD, s);
+    mnist_backward_a(a, s);
+    mark(P_BFC, s);
     a.step_bump = (int64_t*)step_.data_ptr();
-    HIP_OK(hipEventRecord(ev_a_, s));
-    hipStream_t os = dp ? comm_stream_ : opt_stream_;
-    HIP_OK(hipStreamWaitEvent(os, ev_a_, 0));
-    if (dp) reduce_bucket(BUCKET_SPLIT, TOTAL);
-    if (opt_overlap_) apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 1, os);
-    HIP_OK(hipEventRecord(ev_opt_a_, os));
-    if (split) mnist_backward_a(a, s, 2);
     mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
-    if (opt_overlap_) HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
-    mnist_conv_grad_reduce(a, s);
-    if (dp) {
-      HIP_OK(hipEventRecord(ev_b_, s));
-      HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
-      reduce_bucket(0, BUCKET_SPLIT);
-      HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    if (fused) {
+      mark(P_BCONV, s);
+      o.gbf = gbf_local ? (const uint16_t*)gbf_.data_ptr() : nullptr;
+      mnist_adam_fused(a, o, s);
+    } else {
+      mnist_conv_grad_reduce(a, s);
+      mark(P_BCONV, s);
+      apply_optimizer_range(0, TOTAL, 1.0, 0, s);
     }
-    if (!opt_overlap_) {
+    mark(P_OPT, s);
+  }
+
+  // DP step, three streams (main s, comm c, optimizer o):
+  //   s: conv fwd -> [wait o: previous step's fc optimizer] -> fc fwd + head -> fc bwd (bucket A as
+  //      bf16 in gbf) -> conv bwd -> conv-slab reduce (bucket B as bf16 in gbf, step bump)
+  //      -> [wait c: B reduced] -> optimizer on B (conv region)
+  //   c: [wait A] all-reduce A -> [wait B] all-reduce B
+  //   o: [wait A reduced] optimizer on A (fc region; t from the head kernel, so the step bump on s
+  //      does not race it)
+  // The fc optimizer overlaps the conv backward, bucket B's collective, the conv optimizer AND the
+  // next step's conv forward (which needs only conv params): the main stream waits for it just
+  // before the next fc forward. Captured multi-step graphs keep that cross-step overlap; the last
+  // step of a graph (and every eager step) joins o back into s at its end.
+  void train_step_dp(bool join_end) {
+    hipStream_t s = stream();
+    const double scale = 1.0 / (double)world();
+    const bool bf = bf16_comm_;
+    MnistStepArgs a = args();
+    a.t_out = (int64_t*)tnext_.data_ptr();
+    a.step_bump = (int64_t*)step_.data_ptr();
+    if (bf) {
+      a.gbf_a = (uint16_t*)gbf_.data_ptr();
+      a.gbf_b = (uint16_t*)gbf_.data_ptr();
+    }
+    mark(P_START, s);
+    mnist_forward_conv(a, s);
+    if (pending_opt_a_) {
       HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
-      apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 0, s);
+      pending_opt_a_ = false;
     }
-    if (dp) HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+    mnist_forward_fc(a, true, s);
+    mark(P_FWD, s);
+    mnist_backward_a(a, s, 0);
+    mark(P_BFC, s);
+    HIP_OK(hipEventRecord(ev_a_, s));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
+    mark(P_CA0, comm_stream_);
+    reduce_bucket(BUCKET_SPLIT, TOTAL, bf);
+    mark(P_CA1, comm_stream_);
+    HIP_OK(hipEventRecord(ev_ag_, comm_stream_));
+    HIP_OK(hipStreamWaitEvent(opt_stream_, ev_ag_, 0));
+    apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 0, opt_stream_, (const int64_t*)tnext_.data_ptr());
+    HIP_OK(hipEventRecord(ev_opt_a_, opt_stream_));
+    mnist_backward_b(a, s, conv_fork_ ? aux_stream_ : nullptr, ev_fork_, ev_join_);
+    mnist_conv_grad_reduce(a, s);
+    mark(P_BCONV, s);
+    HIP_OK(hipEventRecord(ev_b_, s));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
+    mark(P_CB0, comm_stream_);
+    reduce_bucket(0, BUCKET_SPLIT, bf);
+    mark(P_CB1, comm_stream_);
+    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
     apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s);
+    mark(P_OPT, s);
+    if (join_end) HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+    else pending_opt_a_ = true;
   }
 
   void train_step_zero() {
+    timed_ = false;
     hipStream_t s = stream();
     const double scale = 1.0 / (double)world();
     const int64_t r = rank_in_comm();
@@ -333,7 +403,7 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipEventRecord(ev_a_, s));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
     rs_w(comm_stream_);
-    reduce_bucket(OFF_BD1, TOTAL);
+    reduce_bucket(OFF_BD1, TOTAL, in_gbf(OFF_BD1));
     apply_optimizer_range(OFF_WD1 + r * zshard_, OFF_WD1 + (r + 1) * zshard_, scale, 1, comm_stream_);
     apply_optimizer_range(OFF_BD1, TOTAL, scale, 1, comm_stream_);
     HIP_OK(hipEventRecord(ev_opt_a_, comm_stream_));
@@ -343,7 +413,7 @@ class MnistEngine : public torch::CustomClassHolder {
     mnist_conv_grad_reduce(a, s);
     HIP_OK(hipEventRecord(ev_b_, s));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
-    reduce_bucket(0, BUCKET_SPLIT);
+    reduce_bucket(0, BUCKET_SPLIT, false);
     HIP_OK(hipEventRecord(ev_done_, comm_stream_));
     HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
     apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s);
@@ -358,7 +428,7 @@ class MnistEngine : public torch::CustomClassHolder {
     if (!dp()) return;
     HIP_OK(hipEventRecord(ev_a_, s));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
-    reduce_bucket(0, TOTAL);
+    reduce_bucket(0, TOTAL, false);
     HIP_OK(hipEventRecord(ev_done_, comm_stream_));
     HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
   }
@@ -398,7 +468,7 @@ class MnistEngine : public torch::CustomClassHolder {
     drop_graph(name);
     HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
     try {
-      for (int64_t i = 0; i < n; ++i) train_step();
+      for (int64_t i = 0; i < n; ++i) train_step_impl(i == n - 1);
     } catch (...) {
       hipGraph_t g;
       hipStreamEndCapture(s, &g);
@@ -428,6 +498,10 @@ class MnistEngine : public torch::CustomClassHolder {
 
  private:
   hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+  enum { P_START, P_FWD, P_BFC, P_BCONV, P_OPT, P_CA0, P_CA1, P_CB0, P_CB1, P_N };
+  void mark(int k, hipStream_t st) {
+    if (timing_) HIP_OK(hipEventRecord(pev_[k], st));
+  }
 
   // ZeRO helpers (fc1 weight region W = [OFF_WD1, OFF_BD1))
   void rs_w(hipStream_t st) {
@@ -463,9 +537,9 @@ class MnistEngine : public torch::CustomClassHolder {
   bool fused_bf16_a() const { return bf16_comm_ && dp(); }
   bool in_gbf(int64_t beg) const { return fused_bf16_a() && beg >= BUCKET_SPLIT; }
 
-  void reduce_bucket(int64_t beg, int64_t end) {
+  // pre: the bucket's gradients are already bf16 in gbf_ (written by the producing kernel)
+  void reduce_bucket(int64_t beg, int64_t end, bool pre) {
     const size_t n = (size_t)(end - beg);
-    const bool pre = in_gbf(beg);
     if (ipc_ && (!comm_ || (int64_t)n <= ipc_small_)) {
       // fp32 (or fused bf16) grads in, fp32 sum in rank order, written where the optimizer reads
       // (bf16 gbf or fp32 grad)
@@ -548,9 +622,7 @@ class MnistEngine : public torch::CustomClassHolder {
   bool zero_ = false;
   bool force_dp_ = false;
   int64_t zshard_ = 0;
-  // where region A's optimizer runs: 0 = main stream after the conv backward (no HBM contention
-  // with the conv kernels), 1 = side stream overlapping the conv backward
-  int64_t opt_overlap_ = 0;
+  bool pending_opt_a_ = false;  // DP: the main stream still has to wait for the fc optimizer
   // measured on one MI355X: the forked conv2 wgrad only contends with dgrad for CUs (110 vs 100 us/step)
   bool conv_fork_ = false;
   // one GPU + Adam: the optimizer kernel also reduces the conv gradient slabs and bumps the step
@@ -558,6 +630,8 @@ class MnistEngine : public torch::CustomClassHolder {
   bool local_bf16_grads_ = false;
   bool fc_adam_ = false, fc_adam_fork_ = false;  // measured slower (docs/DESIGN.md)
   std::map<std::string, hipGraphExec_t> graphs_;
+  hipEvent_t pev_[P_N] = {};
+  bool timing_ = false, timed_ = false, timed_dp_ = false;
 };
 
 TORCH_LIBRARY_FRAGMENT(tfd, m) {
@@ -601,11 +675,12 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_zero", &MnistEngine::set_zero)
       .def("set_force_dp", &MnistEngine::set_force_dp)
       .def("dp", &MnistEngine::dp)
-      .def("set_opt_overlap", &MnistEngine::set_opt_overlap)
       .def("set_conv_fork", &MnistEngine::set_conv_fork)
       .def("set_fused_tail", &MnistEngine::set_fused_tail)
       .def("set_local_bf16_grads", &MnistEngine::set_local_bf16_grads)
       .def("set_fc_adam", &MnistEngine::set_fc_adam)
+      .def("set_phase_timing", &MnistEngine::set_phase_timing)
+      .def("phase_times", &MnistEngine::phase_times)
       .def("zero", &MnistEngine::zero)
       .def("sync_params", &MnistEngine::sync_params)
       .def("world", &MnistEngine::world)

@@ -28,6 +28,7 @@ struct MnistStepArgs {
   uint16_t* gbf_a;             // if set (DP with a bf16 wire format): the fc backward writes bucket A's
                                // gradients [OFF_WD1, TOTAL) as bf16 straight into this flat buffer (the
                                // all-reduce operand) instead of fp32 into `grad` -- no separate cast pass
+  uint16_t* gbf_b;             // likewise for bucket B [0, OFF_WD1): the conv-slab reduce writes bf16 here
   // activations / workspace (bf16 stored as uint16)
   uint16_t* p1;  uint8_t* idx1;   // [B][14][14][32]
   uint16_t* p2;  uint8_t* idx2;   // [B][3136]

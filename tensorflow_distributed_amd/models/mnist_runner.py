@@ -155,10 +155,21 @@ class TorchMnistRunner(MnistRunnerBase):
         self._step += 1
 
     def train_step(self, x, y) -> None:
-        g, _ = self.compute_grads(x, y)
+        g, self._last_loss = self.compute_grads(x, y)
         if self.comm is not None:
             self.comm(g)
         self.apply_grads(g)
+
+    def last_loss(self) -> float:
+        return float(getattr(self, "_last_loss", float("nan")))
+
+    def set_phase_timing(self, on: bool = True) -> None:
+        pass
+
+    def phase_times(self) -> dict:
+        """CPU path: host time of the last Gloo gradient all-reduce (the only timed phase)."""
+        ms = getattr(self.comm, "last_ms", None)
+        return {"allreduce_ms": round(ms, 4)} if ms is not None else {}
 
     @torch.no_grad()
     def evaluate(self, x, y) -> Tuple[float, int]:
@@ -201,6 +212,25 @@ class NativeMnistRunner(MnistRunnerBase):
         self._dev_data = None  # device-resident split (set_device_dataset)
         self._hstep = 0        # host mirror of the device global_step (epoch bookkeeping, no sync)
         self._epoch = -1
+
+    # ---- observability ----
+    PHASES = ("fwd_ms", "bwd_fc_ms", "bwd_conv_ms", "optim_ms", "allreduce_ms", "comm_wait_ms", "step_ms_gpu")
+
+    def set_phase_timing(self, on: bool = True) -> None:
+        """HIP timing events at the step's phase boundaries (recorded inside the captured graph too).
+        Takes effect for graphs captured afterwards."""
+        self.eng.set_phase_timing(bool(on))
+        self._graph_ready = False
+
+    def phase_times(self) -> dict:
+        """GPU milliseconds of the last step's phases (all 0 when timing is off)."""
+        self.stream.synchronize()
+        return {k: round(float(v), 4) for k, v in zip(self.PHASES, self.eng.phase_times().tolist())}
+
+    def last_loss(self) -> float:
+        """Mean training loss of the last step's batch (with its dropout mask)."""
+        self.stream.synchronize()
+        return float(self.eng.loss_rows().mean().item())
 
     # ---- device-resident input (reference feed: mnist_python_m.py:291-294) ----
     def set_device_dataset(self, images, labels, seed: int = 0) -> None:

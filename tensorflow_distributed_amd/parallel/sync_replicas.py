@@ -30,11 +30,14 @@ class GlooGradAverager:
     def __init__(self, group=None, world: int = 1):
         self.group = group
         self.world = world
+        self.last_ms = 0.0  # host time of the last all-reduce (metrics JSONL: allreduce_ms)
 
     def __call__(self, flat_grad: torch.Tensor) -> None:
         if self.world > 1:
+            t0 = time.perf_counter()
             dist.all_reduce(flat_grad, group=self.group)
             flat_grad.div_(self.world)
+            self.last_ms = (time.perf_counter() - t0) * 1e3
 
 
 def select_contributors(finish_time: float, rank: int, world: int, replicas_to_aggregate: int, group=None):

@@ -96,6 +96,9 @@ def define_flags(task_index_default: int = 0, job_name_default: str = "ps") -> N
     f.DEFINE_enum("dp_transport", "auto", ["auto", "rccl", "ipc"], "GPU sync gradient transport: auto = "
                   "peer-to-peer IPC when workers share a GPU (--num_gpus < workers; RCCL refuses that), else "
                   "RCCL over xGMI (+ IPC one-shot for the small conv bucket)")
+    f.DEFINE_boolean("phase_timing", False, "GPU: HIP timing events at the step's phase boundaries (forward, fc "
+                     "backward, conv backward, optimizer, all-reduce), written to --metrics_file (always on when "
+                     "--metrics_file is set on the chief)")
     f.DEFINE_boolean("device_input", True, "GPU: upload the training split once and index it on the device "
                      "by a per-epoch shuffle (no per-step host feed); False = host next_batch + H2D per step")
 
@@ -261,6 +264,9 @@ def main(argv=None) -> int:
         stepper = sync_replicas.SyncReplicasStepper(runner, FLAGS.task_index, num_workers, sopt.replicas_to_aggregate,
                                                     group=server.worker_group, straggler_delay_s=delays)
     metrics = MetricsLogger(FLAGS.metrics_file if is_chief else "")
+    phase_timing = FLAGS.phase_timing or (is_chief and bool(FLAGS.metrics_file))
+    if phase_timing:
+        runner.set_phase_timing(True)
     timer = StepTimer(pid=FLAGS.task_index, enabled=bool(FLAGS.trace_file))
     restart_attempt = int(os.environ.get("TFD_RESTART_COUNT", "0"))
 
@@ -299,8 +305,15 @@ def main(argv=None) -> int:
         now = time.time()
         if not FLAGS.quiet:
             print("%f: Worker %d: training step %d done (global step: %d)" % (now, FLAGS.task_index, local_step, step))
-        metrics.log(step=local_step, global_step=step, step_ms=1e3 * (now - t0),
-                    images_per_sec=FLAGS.batch_size * (num_workers if sync else 1) / max(now - t0, 1e-9))
+        if metrics.path:
+            rec = dict(step=local_step, global_step=step, step_ms=1e3 * (now - t0), loss=runner.last_loss(),
+                       images_per_sec=FLAGS.batch_size * (num_workers if sync else 1) / max(now - t0, 1e-9))
+            if phase_timing:
+                ph = runner.phase_times()
+                rec.update(ph)
+                timer.add_gpu_phases(now, ph)
+            rec.setdefault("allreduce_ms", 0.0 if (not sync or num_workers == 1) else None)
+            metrics.log(**rec)
         if FLAGS.check_consistency_every and sync and local_step % FLAGS.check_consistency_every == 0:
             _check_consistency(runner, server, num_workers)
         sv.on_step(step)

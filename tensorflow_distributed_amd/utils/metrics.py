@@ -2,8 +2,10 @@
 
 * :class:`MetricsLogger` -- ``--metrics_file`` JSONL on the chief: one record per step
   (step, global_step, loss, images/sec, step_ms, ...).
-* :class:`StepTimer` -- host wall-clock phases plus optional HIP events; keeps a chrome-trace
-  (``chrome://tracing`` / Perfetto JSON) of per-phase spans for ``--trace_file``.
+* :class:`StepTimer` -- host wall-clock phases; keeps a chrome-trace (``chrome://tracing`` /
+  Perfetto JSON) of per-phase spans for ``--trace_file``. GPU phases (forward, fc/conv backward,
+  optimizer, all-reduce) come from the engine's HIP timing events (``runner.phase_times()``,
+  recorded inside the captured step graph) and are added to the same trace by :meth:`add_gpu_phases`.
 * :func:`performance_table` -- the reference's ``performance`` file format
   (``Steps ,Time ,Accuracy, Learning rate``, ``/root/reference/performance:1-6``).
 """
@@ -43,7 +45,7 @@ class MetricsLogger:
 
 
 class StepTimer:
-    """Named phases, host wall time; ``trace()`` returns chrome-trace events (µs)."""
+    """Named host wall-time phases + GPU phase spans; chrome-trace events in µs."""
 
     def __init__(self, pid: int = 0, enabled: bool = True, max_events: int = 200000):
         self.pid = pid
@@ -68,6 +70,24 @@ class StepTimer:
             if len(self.events) < self.max_events:
                 self.events.append({"name": name, "ph": "X", "pid": self.pid, "tid": tid,
                                     "ts": t0 * 1e6, "dur": (t1 - t0) * 1e6})
+
+    def add_gpu_phases(self, end_s: float, phases: Dict[str, float], tid: int = 1) -> None:
+        """Lay the GPU phase durations (ms, in step order) back to back ending at host time ``end_s``
+        on their own trace row."""
+        if not self.enabled:
+            return
+        order = ["fwd_ms", "bwd_fc_ms", "bwd_conv_ms", "optim_ms"]
+        total = sum(phases.get(k, 0.0) for k in order)
+        t = end_s * 1e6 - total * 1e3
+        for k in order:
+            d = phases.get(k, 0.0) * 1e3
+            if d > 0 and len(self.events) < self.max_events:
+                self.events.append({"name": "gpu:" + k[:-3], "ph": "X", "pid": self.pid, "tid": tid, "ts": t, "dur": d})
+            t += d
+        ar = phases.get("allreduce_ms", 0.0)
+        if ar and len(self.events) < self.max_events:
+            self.events.append({"name": "gpu:allreduce", "ph": "X", "pid": self.pid, "tid": tid + 1,
+                                "ts": end_s * 1e6 - ar * 1e3, "dur": ar * 1e3})
 
     def mean_ms(self, name: str) -> float:
         n = self.counts.get(name, 0)

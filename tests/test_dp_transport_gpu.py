@@ -104,7 +104,8 @@ def test_reference_quickstart_two_workers_share_one_gpu(cuda, tmp_path):
     from tensorflow_distributed_amd import launch
 
     args = ["--num_gpus=1", "--train_steps=12", f"--logdir={tmp_path}", "--synthetic_data", "--eval_batches=1",
-            "--data_dir=/nonexistent", "--check_consistency_every=1", "--log_device_placement"]
+            "--data_dir=/nonexistent", "--check_consistency_every=1", "--log_device_placement",
+            f"--metrics_file={tmp_path}/m.jsonl"]
     r = launch.launch(1, 2, args, echo=False, timeout_s=300)
     assert r["ok"], r["outputs"]
     outs = {k.split("#")[0]: v for k, v in r["outputs"].items()}
@@ -116,6 +117,11 @@ def test_reference_quickstart_two_workers_share_one_gpu(cuda, tmp_path):
         line = [ln for ln in out.splitlines() if "parameter checksum" in ln][-1]
         sums.append(line.split("checksum")[1].split())
     assert sums[0] == sums[1], sums
+    recs = [json.loads(ln) for ln in open(tmp_path / "m.jsonl")]
+    steps = [rec for rec in recs if "step" in rec and "event" not in rec]
+    assert len(steps) == 12
+    # GPU phase events: the IPC bucket collectives were timed on the comm stream
+    assert all(rec["allreduce_ms"] > 0 and rec["fwd_ms"] > 0 and rec["loss"] > 0 for rec in steps[1:]), steps
 
 
 def _bench(args, nproc=1, timeout=300):
@@ -138,6 +144,7 @@ def test_bench_two_ranks_one_gpu_over_ipc(cuda):
     r = _bench(["--gpus", "2", "--steps", "20", "--warmup", "5", "--min_warmup_ms", "50"], nproc=2)
     assert r["n_gpus"] == 2 and r["config"]["dp_transport"] == "ipc" and r["config"]["parallelism"] == "dp2"
     assert r["value"] > 0 and r["config"]["global_batch"] == 256
+    assert r["phases_ms"]["allreduce"] > 0, r["phases_ms"]
 
 
 def test_bench_forced_dp_world1_rccl(cuda):

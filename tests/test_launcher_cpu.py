@@ -20,7 +20,9 @@ def _out(r, name):
 
 
 def test_sync_cluster_reference_lines(tmp_path):
-    r = launch.launch(1, 2, ["--train_steps=3", f"--logdir={tmp_path}"] + COMMON, echo=False, timeout_s=300)
+    mf = tmp_path / "m.jsonl"
+    r = launch.launch(1, 2, ["--train_steps=3", f"--logdir={tmp_path}", f"--metrics_file={mf}",
+                             f"--trace_file={tmp_path}/trace{{task}}.json"] + COMMON, echo=False, timeout_s=300)
     assert r["ok"], r["outputs"]
     w0, w1, ps = _out(r, "worker:0"), _out(r, "worker:1"), _out(r, "ps:0")
     assert "job name = ps" in ps and "task index = 0" in ps
@@ -31,6 +33,11 @@ def test_sync_cluster_reference_lines(tmp_path):
         assert f"Worker {i}: training step 3 done (global step: 3)" in w
     assert latest_checkpoint(str(tmp_path)).endswith("model.ckpt-3")
     assert any(f.startswith("events.out.tfevents.") for f in os.listdir(tmp_path))
+    import json
+    recs = [json.loads(ln) for ln in open(mf)]
+    steps = [rec for rec in recs if "step" in rec and "event" not in rec]
+    assert len(steps) == 3 and all(rec["loss"] > 0 and rec["allreduce_ms"] > 0 for rec in steps), steps
+    assert os.path.exists(tmp_path / "trace0.json")
 
 
 def test_async_cluster_two_ps(tmp_path):

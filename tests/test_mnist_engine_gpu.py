@@ -241,3 +241,32 @@ def test_fc_adam_in_backward_epilogue_matches_separate_adam(cuda, fork):
     assert _relerr(d0, d1) < 1e-3, _relerr(d0, d1)
     assert torch.equal(engs[0].params_bf16(), engs[0].params().to(torch.bfloat16))
     assert torch.allclose(engs[0].adam_v(), engs[1].adam_v(), rtol=1e-3, atol=1e-12)
+
+
+def test_phase_timing_events_inside_graph(cuda):
+    """HIP timing events at the phase boundaries, recorded eagerly and as graph event nodes."""
+    B = 128
+    n = 1024
+    data = torch.rand(n, 784, device=cuda)
+    labels = torch.randint(0, 10, (n,), dtype=torch.int32, device=cuda)
+    perm = torch.randperm(n, device=cuda).to(torch.int32)
+    e = _engine(B, cuda, keep=0.75)
+    e.set_adam(0.01, 0.9, 0.999, 1e-8)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        e.params().copy_(M.flat_from_dict(M.init_params(1)).to(cuda))
+        e.sync_shadow()
+        e.set_dataset(data, labels, perm)
+        e.set_input_mode(1)
+        e.set_phase_timing(True)
+        e.train_step()
+        eager = e.phase_times().tolist()
+        e.capture_train_step("g")
+        e.replay("g", 3)
+        graph = e.phase_times().tolist()
+    torch.cuda.synchronize()
+    for ph in (eager, graph):
+        fwd, bfc, bconv, opt, ar, wait, step = ph
+        assert min(fwd, bfc, bconv, opt) > 0 and ar == 0 and step > 0, ph
+        assert abs(fwd + bfc + bconv + opt - step) < 1e-3 * max(step, 1), ph
+        assert step < 5.0, ph  # ms
