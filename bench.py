@@ -134,6 +134,8 @@ def main(argv=None):
             run = lambda k: [eng.train_step() for _ in range(k)]  # noqa: E731
         run(a.warmup)
     torch.cuda.synchronize(dev)
+    if os.environ.get("TFD_DEBUG_IPC"):
+        print(f"# rank {rank}: transport error after warmup = {tr.error()}", file=sys.stderr)
     # GPU clocks ramp over the first few hundred steps (profiles/warmup_ramp.log: 99 -> 92 us per
     # replay over 400 steps, back to 99.6 us after 2 s idle), so a 20-step timed region right after a
     # 5-step warm-up measures the ramp. Keep replaying untimed steps until --min_warmup_ms elapsed;

@@ -12,24 +12,26 @@
 namespace tfd {
 
 constexpr int kIpcMaxRanks = 8;
-constexpr int kIpcMaxBlocks = 64;
-// signal region layout (int32): [2 phases][kIpcMaxBlocks][kIpcMaxRanks] flags, then
-// [kIpcMaxBlocks] reserved words, then the sticky error word and the call counter.
-constexpr int kIpcSigFlags = 2 * kIpcMaxBlocks * kIpcMaxRanks;
-constexpr int kIpcSigInts = kIpcSigFlags + kIpcMaxBlocks + 4;
+constexpr int kIpcMaxBlocks = 256;
+// signal region layout (int32): [kIpcMaxBlocks][kIpcMaxRanks] START flags, then the sticky error
+// word, the call counter and the per-call block-arrival ticket.
+constexpr int kIpcSigFlags = kIpcMaxBlocks * kIpcMaxRanks;
+constexpr int kIpcSigInts = kIpcSigFlags + 8;
 
 struct IpcAllReduceArgs {
   const void* in;               // local input (fp32 or bf16)
   void* out;                    // local output (may alias in)
-  void* stage[kIpcMaxRanks];    // fp32 staging buffer of every rank, mapped here
+  void* stage[kIpcMaxRanks];    // staging buffer of every rank (two halves of half_bytes), mapped here
   int* sig[kIpcMaxRanks];       // signal region of every rank, mapped here
   int64_t n;                    // elements
   int rank, world;
   int in_bf16, out_bf16;
   float scale;                  // applied to the reduced sum
   int64_t spin_limit_ticks;     // s_memrealtime (100 MHz) ticks before a barrier gives up
+  int64_t half_bytes;           // bytes per staging half (call v uses half v & 1)
 };
 
+int ipc_blocks_for(int64_t n);  // grid size for an n-element collective
 void ipc_allreduce(const IpcAllReduceArgs& a, int blocks, hipStream_t s);
 // n = shard size S. reduce-scatter: in = N*S local elements, out = this rank's S-element shard.
 void ipc_reduce_scatter(const IpcAllReduceArgs& a, int blocks, hipStream_t s);

@@ -10,7 +10,9 @@
 #include <torch/custom_class.h>
 #include <torch/library.h>
 
+#include <cstdlib>
 #include <cstring>
+#include <algorithm>
 
 #include "../ipc_kernels.h"
 #include "ipc_comm.h"
@@ -29,10 +31,11 @@ IpcComm::IpcComm(int64_t world, int64_t rank, int64_t device, int64_t capacity_e
   TORCH_CHECK(rank >= 0 && rank < world, "IpcComm: bad rank");
   TORCH_CHECK(capacity_elems > 0, "IpcComm: capacity");
   HIP_OK2(hipSetDevice((int)device));
-  HIP_OK2(hipMalloc(&stage_, (size_t)cap_ * sizeof(float)));
+  // two halves of cap_ fp32 (call v stages into half v & 1: double buffering instead of an END barrier)
+  HIP_OK2(hipMalloc(&stage_, 2 * (size_t)cap_ * sizeof(float)));
   HIP_OK2(hipExtMallocWithFlags(&sig_, kIpcSigInts * sizeof(int), hipDeviceMallocUncached));
   HIP_OK2(hipMemset(sig_, 0, kIpcSigInts * sizeof(int)));
-  HIP_OK2(hipMemset(stage_, 0, (size_t)cap_ * sizeof(float)));
+  HIP_OK2(hipMemset(stage_, 0, 2 * (size_t)cap_ * sizeof(float)));
   HIP_OK2(hipDeviceSynchronize());
   for (int i = 0; i < kIpcMaxRanks; ++i) {
     peer_stage_[i] = nullptr;
@@ -91,9 +94,19 @@ void IpcComm::close() {
   }
 }
 
-static int ipc_blocks(int64_t n) {
-  return (int)std::min<int64_t>(kIpcMaxBlocks, std::max<int64_t>(1, (n + 8191) / 8192));
+// Grid of a spinning collective: every block of it must become resident while the peers' blocks
+// are resident too. Ranks that share one GPU compete for its CUs with two spinning kernels plus
+// their other streams' work; grids of up to 256 blocks there hung in 2 of 4 DP runs (a block
+// spinning for a peer block that could not be dispatched), 8-block grids in none
+// (scripts/gpu_diag_ipc.sh). set_max_blocks() caps it; TFD_IPC_MAX_BLOCKS overrides.
+int IpcComm::blocks(int64_t n) const {
+  static const int env_cap = [] {
+    const char* e = std::getenv("TFD_IPC_MAX_BLOCKS");
+    return e ? std::max(1, std::atoi(e)) : 0;
+  }();
+  return std::min(ipc_blocks_for(n), env_cap ? env_cap : max_blocks_);
 }
+void IpcComm::set_max_blocks(int64_t b) { max_blocks_ = (int)std::max<int64_t>(1, std::min<int64_t>(b, kIpcMaxBlocks)); }
 
 void IpcComm::all_reduce_raw(const void* in, bool in_bf16, void* out, bool out_bf16, int64_t n, double scale,
                              hipStream_t s) {
@@ -113,9 +126,8 @@ void IpcComm::all_reduce_raw(const void* in, bool in_bf16, void* out, bool out_b
   a.out_bf16 = out_bf16 ? 1 : 0;
   a.scale = (float)scale;
   a.spin_limit_ticks = spin_ticks_;
-  // ~8K elements per block keeps the per-rank slice reads wide; never more blocks than the
-  // signal layout holds
-  ipc_allreduce(a, ipc_blocks(n), s);
+  a.half_bytes = cap_ * (int64_t)sizeof(float);
+  ipc_allreduce(a, blocks(n), s);
 }
 
 void IpcComm::all_reduce(const at::Tensor& t, double scale) {
@@ -143,7 +155,9 @@ void IpcComm::reduce_scatter_raw(const void* in, bool in_bf16, void* out, bool o
   a.out_bf16 = out_bf16 ? 1 : 0;
   a.scale = (float)scale;
   a.spin_limit_ticks = spin_ticks_;
-  ipc_reduce_scatter(a, ipc_blocks(shard), s);
+  a.half_bytes = cap_ * (int64_t)sizeof(float);
+  TORCH_CHECK(shard % 8 == 0, "IpcComm.reduce_scatter: shard must be a multiple of 8 elements");
+  ipc_reduce_scatter(a, blocks(shard), s);
 }
 
 void IpcComm::all_gather_raw(void* buf, int elem_bytes, int64_t shard, hipStream_t s) {
@@ -160,7 +174,9 @@ void IpcComm::all_gather_raw(void* buf, int elem_bytes, int64_t shard, hipStream
   a.rank = (int)rank_;
   a.world = (int)world_;
   a.spin_limit_ticks = spin_ticks_;
-  ipc_all_gather(a, elem_bytes, ipc_blocks(shard), s);
+  a.half_bytes = cap_ * (int64_t)sizeof(float);
+  TORCH_CHECK(shard % 8 == 0, "IpcComm.all_gather: shard must be a multiple of 8 elements");
+  ipc_all_gather(a, elem_bytes, blocks(shard), s);
 }
 
 void IpcComm::reduce_scatter(const at::Tensor& in, const at::Tensor& out, double scale) {
@@ -178,7 +194,7 @@ void IpcComm::all_gather(const at::Tensor& buf) {
 
 int64_t IpcComm::error() {
   int v = 0;
-  HIP_OK2(hipMemcpy(&v, (int*)sig_ + kIpcSigFlags + kIpcMaxBlocks, sizeof(int), hipMemcpyDeviceToHost));
+  HIP_OK2(hipMemcpy(&v, (int*)sig_ + kIpcSigFlags, sizeof(int), hipMemcpyDeviceToHost));
   return v;
 }
 
@@ -195,6 +211,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("all_gather", &IpcComm::all_gather)
       .def("error", &IpcComm::error)
       .def("set_spin_limit_ms", &IpcComm::set_spin_limit_ms)
+      .def("set_max_blocks", &IpcComm::set_max_blocks)
       .def("world", &IpcComm::world)
       .def("rank", &IpcComm::rank);
 }

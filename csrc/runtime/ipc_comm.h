@@ -26,6 +26,8 @@ class IpcComm : public torch::CustomClassHolder {
   void all_gather(const at::Tensor& buf);
   int64_t error();                           // 1 once a barrier timed out (sticky)
   void set_spin_limit_ms(double ms);
+  void set_max_blocks(int64_t b);          // grid cap of the spinning collectives
+  int blocks(int64_t n) const;
   int64_t world() const { return world_; }
   int64_t rank() const { return rank_; }
   int64_t capacity() const { return cap_; }
@@ -38,6 +40,7 @@ class IpcComm : public torch::CustomClassHolder {
   int* peer_sig_[8];
   bool opened_ = false;
   int64_t spin_ticks_ = 200000000;  // 2 s at 100 MHz
+  int max_blocks_ = 64;
 };
 
 }  // namespace tfd

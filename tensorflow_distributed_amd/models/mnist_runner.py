@@ -43,15 +43,28 @@ class MnistRunnerBase:
     def params(self) -> torch.Tensor: ...
     def global_step(self) -> int: ...
 
+    ps_client = None  # parallel.async_ps.AsyncPSClient when the variables live on PS tasks
+
     def state_dict_tf(self) -> "dict":
-        """TF-named tensors for the checkpoint (mnist_python_m.py:178,185-196 creation order)."""
+        """TF-named tensors for the checkpoint (mnist_python_m.py:178,185-196 creation order).
+        With the variables on parameter servers (async / backup-worker modes) the values AND the
+        optimizer slots are pulled from the PS tasks -- what TF's Saver would save."""
         from collections import OrderedDict
 
-        flat = self.params().detach().float().cpu()
+        flat = self.params().detach().float().cpu().clone()
+        step = self.global_step()
+        slot_t = {k: v.detach().float().cpu() for k, v in self.slot_tensors().items()}
+        powers = self.powers()
+        if self.ps_client is not None:
+            got, t, step = self.ps_client.pull_state(flat)
+            kind = getattr(getattr(self, "opt", None), "kind", "adam")
+            slot_t = {("accum" if kind == "momentum" else k): v for k, v in got.items()}
+            o = self.opt
+            powers = {"beta1_power": o.beta1 ** t, "beta2_power": o.beta2 ** t} if kind == "adam" else {}
         out = OrderedDict()
-        out["global_step"] = np.array(self.global_step(), dtype=np.int64)
+        out["global_step"] = np.array(step, dtype=np.int64)
         views = M.dict_from_flat(flat)
-        slots = {k: M.dict_from_flat(v.detach().float().cpu()) for k, v in self.slot_tensors().items()}
+        slots = {k: M.dict_from_flat(v) for k, v in slot_t.items()}
         for key, tf_name, _ in M.PARAM_SPECS:
             out[tf_name] = views[key].numpy().copy()
             if "m" in slots:
@@ -60,7 +73,7 @@ class MnistRunnerBase:
                 out[tf_name + "/Adam_1"] = slots["v"][key].numpy().copy()
             if "accum" in slots:
                 out[tf_name + "/Momentum"] = slots["accum"][key].numpy().copy()
-        for k, v in self.powers().items():
+        for k, v in powers.items():
             out[k] = np.array(v, dtype=np.float32)
         return out
 
@@ -148,14 +161,15 @@ class TorchMnistRunner(MnistRunnerBase):
         g, = torch.autograd.grad(loss, self.flat)
         self.flat.requires_grad_(False)
         self.grad.copy_(g)
-        return self.grad, float(loss.item())
+        self._last_loss = float(loss.item())
+        return self.grad, self._last_loss
 
     def apply_grads(self, grad: torch.Tensor, scale: float = 1.0) -> None:
         self.applier.apply(self.flat, grad, scale)
         self._step += 1
 
     def train_step(self, x, y) -> None:
-        g, self._last_loss = self.compute_grads(x, y)
+        g, _ = self.compute_grads(x, y)
         if self.comm is not None:
             self.comm(g)
         self.apply_grads(g)

@@ -12,12 +12,22 @@ import torch.distributed as dist
 
 
 def make_ipc_comm(rank: int, world: int, device_index: int, capacity_elems: int, group=None,
-                  spin_limit_ms: float = 2000.0):
+                  spin_limit_ms: float = None, max_blocks: int = None):
+    """max_blocks: grid cap of the spinning collectives -- 64 with one rank per GPU, 8 (the default,
+    safe everywhere) when ranks share a GPU: both kernels' blocks must be co-resident, see
+    IpcComm::blocks."""
     from .. import _native
 
     _native.require()
+    import os
+
+    if spin_limit_ms is None:
+        # generous: a peer may still be loading code objects on its first call (observed > 2 s when
+        # ranks share a GPU); any finite limit keeps a missing peer from hanging the device
+        spin_limit_ms = float(os.environ.get("TFD_IPC_SPIN_MS", "30000"))
     comm = torch.classes.tfd.IpcComm(world, rank, device_index, capacity_elems)
     comm.set_spin_limit_ms(spin_limit_ms)
+    comm.set_max_blocks(int(max_blocks or 8))
     h = comm.handle()
     if world > 1:
         allh = [torch.zeros_like(h) for _ in range(world)]

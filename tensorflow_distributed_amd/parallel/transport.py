@@ -110,11 +110,12 @@ def attach_engine(eng, rank: int, world: int, device: torch.device, group=None, 
     log = log or (lambda m: print(m, file=sys.stderr))
     if world <= 1 and not force_dp:
         return DPTransport("none")
+    shared = devices_shared(device, world, group)
     if mode == "auto":
-        mode = "ipc" if devices_shared(device, world, group) else "rccl"
+        mode = "ipc" if shared else "rccl"
     cap = capacity or M.TOTAL
     if mode == "ipc":
-        ipc = make_ipc_comm(rank, world, device.index or 0, cap, group=group)
+        ipc = make_ipc_comm(rank, world, device.index or 0, cap, group=group, max_blocks=8 if shared else 64)
         eng.set_ipc(ipc, cap, bf16)
         if force_dp:
             eng.set_force_dp(True)

@@ -154,14 +154,32 @@ def main(argv=None) -> int:
     if not FLAGS.sync_replicas and layout is None:
         raise ValueError("--sync_replicas=False (async parameter-server mode) needs at least one --ps_hosts task")
 
+    sync = FLAGS.sync_replicas
+    r2a = num_workers
+    if sync:
+        r2a = FLAGS.replicas_to_aggregate if FLAGS.replicas_to_aggregate is not None else num_workers
+        if r2a > num_workers:
+            # TF1 would wait forever for gradients that never come; clamp instead (and say so)
+            print("Worker %d: replicas_to_aggregate=%d > %d workers; aggregating %d" %
+                  (FLAGS.task_index, r2a, num_workers, num_workers))
+            r2a = num_workers
+    # backup workers (R < N) with a ps task: TF's accumulator semantics on the PS (stale gradients of
+    # stragglers dropped, the first R fresh ones averaged); without a ps task: the all-gather stepper
+    backup_ps = sync and r2a < num_workers and layout is not None
+    ps_mode = (not sync) or backup_ps
+
     if FLAGS.job_name == "ps":
         # (reference quirk Q9: ps + existing_servers fell through to the worker code; a PS here
         #  always serves and then exits once every worker has finished)
         service = None
-        if not FLAGS.sync_replicas:
-            service = async_ps.ParameterServerService(FLAGS.task_index, cluster.num_ps, num_workers, layout, opt)
+        if ps_mode:
+            service = async_ps.ParameterServerService(FLAGS.task_index, cluster.num_ps, num_workers, layout, opt,
+                                                      sync=backup_ps, replicas_to_aggregate=r2a)
         server.join(service)
         server.shutdown()
+        if service is not None and backup_ps:
+            print("ps %d: %d synchronous updates, %d stale gradients dropped" % (FLAGS.task_index, service.updates,
+                                                                               service.dropped))
         return 0
 
     is_chief = FLAGS.task_index == 0
@@ -172,15 +190,8 @@ def main(argv=None) -> int:
     else:
         device = torch.device("cpu")
 
-    sync = FLAGS.sync_replicas
     sopt = None
     if sync:
-        r2a = FLAGS.replicas_to_aggregate if FLAGS.replicas_to_aggregate is not None else num_workers
-        if r2a > num_workers:
-            # TF1 would wait forever for gradients that never come; clamp instead (and say so)
-            print("Worker %d: replicas_to_aggregate=%d > %d workers; aggregating %d" %
-                  (FLAGS.task_index, r2a, num_workers, num_workers))
-            r2a = num_workers
         sopt = SyncReplicasOptimizer(opt, replicas_to_aggregate=r2a, total_num_replicas=num_workers).resolve(num_workers)
 
     runner = make_runner(FLAGS.batch_size, opt, device, keep_prob=FLAGS.keep_prob, seed=FLAGS.seed,
@@ -188,7 +199,7 @@ def main(argv=None) -> int:
                          use_graph=FLAGS.use_graph and (sopt is None or not sopt.has_backup_workers))
     comm = None
     transport = None
-    if device.type == "cuda" and sync and num_workers > 1:
+    if device.type == "cuda" and sync and num_workers > 1 and not backup_ps:
         from ..parallel.transport import attach_engine
 
         transport = attach_engine(runner.eng, FLAGS.task_index, num_workers, device, group=server.worker_group,
@@ -206,17 +217,23 @@ def main(argv=None) -> int:
         runner.load_flat(flat, {}, 0)
 
     client = None
-    if sync:
+    if not ps_mode:
         def broadcast_fn():
             if num_workers > 1:
                 sync_replicas.broadcast_state(runner, 0, group=server.worker_group, group_src_rank=cluster.num_ps)
     else:
-        client = async_ps.AsyncPSClient(FLAGS.task_index, layout)
+        from .optimizers import FlatApplier
+
+        client = async_ps.AsyncPSClient(FLAGS.task_index, layout, slot_names=list(FlatApplier(opt, 0).slots()))
+        runner.ps_client = client  # the chief's checkpoints read the PS-resident state (params + slots)
 
         def broadcast_fn():
             flat = runner.params().detach().float().cpu()
             if is_chief:
-                client.init(flat, step=runner.global_step(), t=runner.global_step())
+                # restored moments go back to the PS (fresh init: zeros); t = global_step
+                slots = {("m" if k == "accum" else k): v.detach().float().cpu()
+                         for k, v in runner.slot_tensors().items()} if sv.restored_from else None
+                client.init(flat, step=runner.global_step(), t=runner.global_step(), slots=slots)
             gs = client.pull(flat)
             runner.set_params(flat)
             runner.set_global_step(gs)
@@ -243,12 +260,13 @@ def main(argv=None) -> int:
         names = ["global_step"] + [tf for _, tf, _ in M.PARAM_SPECS]
         wdev = "/job:worker/task:%d/%s:%d" % (FLAGS.task_index, "gpu" if device.type == "cuda" else "cpu",
                                               device.index or 0)
-        placed = replica_device_setter(cluster, names, wdev) if not sync else {n: wdev + " (replicated)" for n in names}
+        placed = replica_device_setter(cluster, names, wdev) if ps_mode else {n: wdev + " (replicated)" for n in names}
         for n in names:
             print("%s: %s" % (n, placed[n]))
         print("compute (conv_net, loss, gradients): %s; gradient sync: %s" % (
-            wdev, (transport.kind + " all-reduce" if transport is not None else "Gloo all-reduce") if sync
-            else "async PS push/pull"))
+            wdev, ("async PS push/pull" if not sync else
+                   "PS accumulator (%d of %d replicas)" % (r2a, num_workers) if backup_ps else
+                   transport.kind + " all-reduce" if transport is not None else "Gloo all-reduce")))
 
     eval_at = sorted(int(v) for v in FLAGS.eval_at_steps.split(",") if v.strip()) if FLAGS.eval_at_steps else []
     eval_time = 0.0
@@ -260,7 +278,7 @@ def main(argv=None) -> int:
             k, v = item.split(":")
             delays[int(k)] = float(v)
     stepper = None
-    if sync:
+    if sync and not backup_ps:
         stepper = sync_replicas.SyncReplicasStepper(runner, FLAGS.task_index, num_workers, sopt.replicas_to_aggregate,
                                                     group=server.worker_group, straggler_delay_s=delays)
     metrics = MetricsLogger(FLAGS.metrics_file if is_chief else "")
@@ -288,7 +306,7 @@ def main(argv=None) -> int:
                 batch_xs, batch_ys = mnist.train.next_batch(FLAGS.batch_size)
         t0 = time.time()
         with timer.phase("step"), trace_range("train_step"):
-            if sync:
+            if not ps_mode:
                 stepper.step(batch_xs, batch_ys)
                 step = runner.global_step()
             else:
@@ -296,8 +314,12 @@ def main(argv=None) -> int:
                 if grad_cpu is None:
                     grad_cpu = torch.zeros(M.TOTAL)
                 grad_cpu.copy_(g.detach().float().cpu())
+                if FLAGS.task_index in delays:
+                    time.sleep(delays[FLAGS.task_index])  # test hook: a straggling worker
                 flat = runner.params().detach().float().cpu()
-                step = client.push_pull(flat, grad_cpu)
+                # sync: the gradient is tagged with the global step it was computed at (stale ones
+                # are dropped by the PS accumulator); async: applied as it comes
+                step = client.push_pull(flat, grad_cpu, local_step=step)
                 runner.set_params(flat)
                 runner.set_global_step(step)
         local_step += 1
@@ -305,6 +327,8 @@ def main(argv=None) -> int:
         now = time.time()
         if not FLAGS.quiet:
             print("%f: Worker %d: training step %d done (global step: %d)" % (now, FLAGS.task_index, local_step, step))
+            if backup_ps and client.last_dropped:
+                print("Worker %d: stale gradient dropped (a backup replica finished this step first)" % FLAGS.task_index)
         if metrics.path:
             rec = dict(step=local_step, global_step=step, step_ms=1e3 * (now - t0), loss=runner.last_loss(),
                        images_per_sec=FLAGS.batch_size * (num_workers if sync else 1) / max(now - t0, 1e-9))

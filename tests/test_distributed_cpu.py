@@ -165,3 +165,66 @@ def test_transport_detects_shared_devices():
     res = run_ranks(_shared_worker, 2)
     assert all(r[0] for r in res) and not any(r[1] for r in res)
     assert res[0][2] != res[1][2]
+
+
+def _ps_state_role(rank, world, sync):
+    """1 PS + 2 workers: PUSH/PULL_STATE/INIT-with-slots protocol (sync: R = 2 accumulator)."""
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+    from tensorflow_distributed_amd.parallel import async_ps
+    from tensorflow_distributed_amd.training.optimizers import AdamOptimizer, FlatApplier
+
+    layout = async_ps.mnist_layout(1)
+    if rank == 0:
+        svc = async_ps.ParameterServerService(0, 1, 2, layout, AdamOptimizer(0.01), sync=sync, replicas_to_aggregate=2)
+        svc.serve()
+        return ("ps", svc.updates, svc.global_step, svc.dropped)
+    wk = rank - 1
+    client = async_ps.AsyncPSClient(wk, layout, slot_names=["m", "v"])
+    flat = torch.zeros(M.TOTAL)
+    p0 = M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(5).items()})
+    if wk == 0:
+        client.init(p0.clone())
+    client.pull(flat)
+    g = torch.randn(M.TOTAL, generator=torch.Generator().manual_seed(100 + wk)) * 1e-2
+    step = client.push_pull(flat, g, local_step=0)
+    out = {"step": step, "flat": flat.clone(), "dropped": client.last_dropped}
+    if sync and wk == 1:
+        # a straggler's gradient for step 0 arriving after the step-0 update is stale: dropped
+        step2 = client.push_pull(flat, g, local_step=0)
+        out["stale_step"], out["stale_dropped"] = step2, client.last_dropped
+    slots, t, gs = client.pull_state(flat.clone())
+    out.update(slots=slots, t=t)
+    client.stop()
+    return ("worker", out)
+
+
+def test_sync_ps_accumulator_averages_r_fresh_gradients_and_drops_stale():
+    import torch.nn.functional as F  # noqa: F401
+
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+    from tensorflow_distributed_amd.training.optimizers import AdamOptimizer, FlatApplier
+
+    outs = run_ranks(_ps_state_role, 3, True)
+    ps = outs[0]
+    w0, w1 = outs[1][1], outs[2][1]
+    assert ps[1] == 1 and ps[2] == 1 and ps[3] == 1, ps  # one averaged update, one stale push dropped
+    assert w0["step"] == w1["step"] == 1 and not w0["dropped"] and not w1["dropped"]
+    assert w1["stale_dropped"] and w1["stale_step"] == 1
+    p = M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(5).items()})
+    gs = [torch.randn(M.TOTAL, generator=torch.Generator().manual_seed(100 + w)) * 1e-2 for w in (0, 1)]
+    ap = FlatApplier(AdamOptimizer(0.01), M.TOTAL)
+    ap.apply(p, gs[0] + gs[1], 0.5)
+    real = lambda t: torch.cat([v.reshape(-1) for v in M.dict_from_flat(t).values()])  # noqa: E731 (no padding)
+    torch.testing.assert_close(real(w0["flat"]), real(p), rtol=1e-6, atol=1e-7)
+    assert torch.equal(w0["flat"], w1["flat"])
+    torch.testing.assert_close(real(w0["slots"]["m"]), real(ap.m), rtol=1e-6, atol=1e-9)
+    torch.testing.assert_close(real(w0["slots"]["v"]), real(ap.v), rtol=1e-6, atol=1e-12)
+    assert w0["t"] == 1
+
+
+def test_async_ps_state_pull_has_the_optimizer_slots():
+    outs = run_ranks(_ps_state_role, 3, False)
+    ps = outs[0]
+    assert ps[1] == 2 and ps[2] == 2  # async: every push applied
+    for _, w in outs[1:]:
+        assert w["t"] == 2 and w["slots"]["m"].abs().sum() > 0 and w["slots"]["v"].abs().sum() > 0

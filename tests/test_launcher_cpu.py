@@ -154,3 +154,47 @@ def test_profile_prefix_puts_program_right_after_dashdash():
     q = profiler_prefix("/tmp/prof/worker1", "SQ_WAVES,SQ_INSTS_VALU_MFMA_MOPS_BF16")
     assert q[q.index("--pmc") + 1:q.index("--pmc") + 3] == ["SQ_WAVES", "SQ_INSTS_VALU_MFMA_MOPS_BF16"]
     assert "--stats" not in q and "--sys-trace" not in q
+
+
+def test_backup_workers_tolerate_a_straggler(tmp_path):
+    """1 ps + 3 workers, replicas_to_aggregate=2, worker 2 stalls 8 s per step: the fast workers
+    finish without waiting for it (TF accumulator semantics on the PS), its stale gradient is
+    dropped, and everyone exits (mnist_python_m.py:62-65,216-220)."""
+    import re
+
+    args = ["--train_steps=6", "--replicas_to_aggregate=2", "--straggler_delay=2:8", "--batch_size=16",
+            f"--logdir={tmp_path}"] + COMMON
+    r = launch.launch(1, 3, args, echo=False, timeout_s=300)
+    assert r["ok"], r["outputs"]
+    fast = [float(re.search(r"Training elapsed time: ([0-9.]+) s", _out(r, f"worker:{i}")).group(1)) for i in (0, 1)]
+    slow = float(re.search(r"Training elapsed time: ([0-9.]+) s", _out(r, "worker:2")).group(1))
+    assert max(fast) < 6.0 < slow, (fast, slow)
+    assert "stale gradient dropped" in _out(r, "worker:2")
+    m = re.search(r"(\d+) synchronous updates, (\d+) stale gradients dropped", _out(r, "ps:0"))
+    assert m and int(m.group(1)) == 6 and int(m.group(2)) >= 1, _out(r, "ps:0")
+    for i in range(3):
+        assert "global step: 6)" in _out(r, f"worker:{i}")
+
+
+def test_async_checkpoint_holds_ps_adam_slots(tmp_path):
+    """in async mode the optimizer state lives on the PS; the chief's checkpoint must
+    hold those moments (not the worker's zero slots) so a resume continues Adam correctly."""
+    import numpy as np
+
+    from tensorflow_distributed_amd.training.checkpoint import load_bundle
+
+    r = launch.launch(1, 2, ["--train_steps=4", "--sync_replicas=False", "--batch_size=16",
+                             f"--logdir={tmp_path}"] + COMMON, echo=False, timeout_s=300)
+    assert r["ok"], r["outputs"]
+    ck = load_bundle(latest_checkpoint(str(tmp_path)))
+    assert np.abs(ck["Variable_2/Adam"]).sum() > 0 and np.abs(ck["Variable_2/Adam_1"]).sum() > 0
+    assert int(ck["global_step"]) >= 4
+    assert abs(float(ck["beta1_power"]) - 0.9 ** int(ck["global_step"])) < 1e-6
+    # resume: the restored moments go back to the PS (no restart of Adam from zero)
+    r2 = launch.launch(1, 2, ["--train_steps=6", "--sync_replicas=False", "--batch_size=16",
+                              f"--logdir={tmp_path}"] + COMMON, echo=False, timeout_s=300)
+    assert r2["ok"], r2["outputs"]
+    assert "Restored from checkpoint" in _out(r2, "worker:0")
+    ck2 = load_bundle(latest_checkpoint(str(tmp_path)))
+    assert int(ck2["global_step"]) >= 6
+    assert abs(float(ck2["beta1_power"]) - 0.9 ** int(ck2["global_step"])) < 1e-6
