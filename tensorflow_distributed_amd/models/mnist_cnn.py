@@ -138,3 +138,43 @@ def softmax_xent_mean(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tenso
 def accuracy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     lab = labels.argmax(1) if labels.dim() == 2 else labels.long()
     return (logits.argmax(1) == lab).float().mean()
+
+
+# ------------------------------------------------------------------ native dropout mask (host replay)
+def _philox4x32_10(c, k0, k1):
+    """Philox4x32-10 on uint64 numpy arrays holding 32-bit lanes (csrc/common.h philox4x32_10)."""
+    import numpy as np
+
+    m32 = np.uint64(0xFFFFFFFF)
+    M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    W0, W1 = np.uint64(0x9E3779B9), np.uint64(0xBB67AE85)
+    c0, c1, c2, c3 = (x.astype(np.uint64) for x in c)
+    k0 = np.uint64(k0) & m32
+    k1 = np.uint64(k1) & m32
+    for _ in range(10):
+        p0 = M0 * c0
+        p1 = M1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & m32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & m32
+        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+        k0 = (k0 + W0) & m32
+        k1 = (k1 + W1) & m32
+    return c0, c1, c2, c3
+
+
+def native_dropout_mask(batch: int, step: int, rank: int, seed: int, keep_prob: float) -> torch.Tensor:
+    """The exact 0/1 dropout mask [batch, 1024] the native head kernel draws at global step ``step``
+    (counter = row * 256 + thread, (step lo, step hi, rank); key = (seed, 0x5EED1234); unit j of
+    thread t is hidden unit 4t + j; kept iff u01 < keep_prob), so the fp32 oracle can replay it."""
+    import numpy as np
+
+    rows = np.arange(batch, dtype=np.uint64)[:, None]
+    t = np.arange(256, dtype=np.uint64)[None, :]
+    c0 = (rows * np.uint64(256) + t) & np.uint64(0xFFFFFFFF)
+    shape = c0.shape
+    c1 = np.full(shape, step & 0xFFFFFFFF, dtype=np.uint64)
+    c2 = np.full(shape, (step >> 32) & 0xFFFFFFFF, dtype=np.uint64)
+    c3 = np.full(shape, rank & 0xFFFFFFFF, dtype=np.uint64)
+    out = _philox4x32_10((c0, c1, c2, c3), seed & 0xFFFFFFFF, 0x5EED1234)
+    u = np.stack([((v >> np.uint64(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)) for v in out], axis=-1)
+    return torch.from_numpy((u < np.float32(keep_prob)).reshape(batch, HID).astype(np.float32))
