@@ -46,7 +46,8 @@ def main(argv=None):
                     "(device-side step counter/data cursor/dropout key make step i+1 of a graph the next step)")
     ap.add_argument("--phases", type=int, default=1, help="after the timed steps, replay a few steps of a graph "
                     "with HIP timing events at the phase boundaries and report the GPU phase breakdown (untimed)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16"], help="compute dtype of the MFMA operands")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="compute dtype: bf16 MFMA operands "
+                    "(fp32 accumulate/master/optimizer), or fp32 everything (the reference's precision)")
     ap.add_argument("--conv_fork", type=int, default=0, help="1: conv2 wgrad on a forked stream beside dgrad")
     ap.add_argument("--zero", type=int, default=0, help="1: ZeRO-1 sharding of the fc1 weight (N > 1)")
     ap.add_argument("--fused_tail", type=int, default=1, help="1: on one GPU the Adam kernel also reduces the "
@@ -80,6 +81,7 @@ def main(argv=None):
     B = a.batch_size
     eng = torch.classes.tfd.MnistEngine(B, dev.index, 0.75, a.seed, rank)
     eng.set_adam(a.lr, 0.9, 0.999, 1e-8)
+    eng.set_dtype(a.dtype)
     eng.set_conv_fork(a.conv_fork)
     eng.set_fused_tail(a.fused_tail)
     eng.set_local_bf16_grads(a.local_bf16_grads)
@@ -189,7 +191,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(img_s / BASELINE_IMG_PER_S, 1),
-            "dtype": "bf16",
+            "dtype": a.dtype,
             "data": "synthetic (device-resident MNIST-shaped 55000x784, random labels; random N(0,1) init)",
             "phases_ms": phases,
             "config": {
@@ -199,13 +201,14 @@ def main(argv=None):
                 "per_gpu_batch": B,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
-                "grad_allreduce": "fp32" if a.fp32_grads else "bf16",
+                "grad_allreduce": "fp32" if (a.fp32_grads or a.dtype == "fp32") else "bf16",
                 "hipgraph": graph_mode,
                 "steps_per_graph": gsteps if graph_mode else 0,
                 "dp_transport": tr.kind,
                 "force_dp": bool(a.force_dp),
                 "zero1_fc1": bool(a.zero),
-                "fc_grads": ("fused into Adam (fp32, in registers)" if world == 1 and a.fc_adam and not a.force_dp
+                "fc_grads": ("fp32" if a.dtype == "fp32" else
+                             "fused into Adam (fp32, in registers)" if world == 1 and a.fc_adam and not a.force_dp
                              else "bf16" if (a.local_bf16_grads or world > 1) and not a.fp32_grads else "fp32"),
             },
         }), flush=True)

@@ -1,0 +1,524 @@
+// Reference-precision (fp32) kernels of the MNIST CNN training step: the reference trains in fp32
+// (tf.float32 placeholders, tf.random_normal params; /root/reference/mnist_python_m.py:185-200).
+// Same fusion structure as the bf16 step (csrc/kernels/mnist.hip) -- bias+relu+2x2 pool+argmax in
+// the conv epilogues, Philox dropout + FC10 + softmax-xent fused per batch row, MaxPoolGrad +
+// ReluGrad in the dX / dgrad epilogues, deterministic split-K slabs for the long-K weight
+// gradients -- but every activation is stored fp32 and every GEMM runs on the fp32 matrix core
+// (v_mfma_f32_16x16x4_f32, csrc/gemm_f32.h). No bf16 rounding anywhere: gradients match an fp32
+// PyTorch oracle to ~1e-5.
+//
+// Kernel map: f32_conv1_pool_fwd K1+K3; f32_conv2_fwd K2+K3; f32_fc1_fwd K4;
+// f32_head K4-finish+K5+K6+K7+K8(dX)+K9; f32_fc1_bwd K8 dW + K10 dW/dX (+K11 unpool epilogue);
+// f32_conv2_bwd K13 (+conv1 ReluGrad/pool-mask epilogue) + K14 (+K12 bias row) slabs;
+// f32_conv1_wgrad K15 (+K12). The slab reduce + optimizer are shared with the bf16 step.
+#include "../common.h"
+#include "../gemm_f32.h"
+#include "../mnist_layout.h"
+#include "../tfd_kernels.h"
+
+#include <algorithm>
+
+namespace tfd {
+using namespace mnist;
+
+namespace {
+
+__device__ __forceinline__ int data_row_f(const int* perm, const int64_t* step, int n_data, int B, int b) {
+  if (!perm) return b;
+  const int64_t s = *step;
+  return perm[(int)((s * (int64_t)B + b) % (int64_t)n_data)];
+}
+
+// ---------------- K1+K3: conv1 + bias + relu + maxpool + argmax (VALU, fp32 out) ----------------
+// Block = (image b, output-channel group of 8); the image is staged into a zero-bordered 32x32 LDS
+// tile; thread pp < 196 computes one pooled pixel's 2x2 window for 8 channels.
+__global__ __launch_bounds__(256) void f32_conv1_pool_fwd(MnistF32Args a) {
+  __shared__ float img[32 * 32];
+  __shared__ float w[KTAPS * 8 + 8];
+  const int b = blockIdx.x >> 2, cg = blockIdx.x & 3, t = threadIdx.x;
+  const float* x = a.data + (size_t)data_row_f(a.perm, a.step, a.n_data, a.B, b) * 784;
+  for (int i = t; i < 32 * 32; i += 256) img[i] = 0.f;
+  if (t < KTAPS * 8) w[t] = a.p32[OFF_WC1 + (t >> 3) * C1 + cg * 8 + (t & 7)];
+  else if (t < KTAPS * 8 + 8) w[t] = a.p32[OFF_BC1 + cg * 8 + (t - KTAPS * 8)];
+  __syncthreads();
+  if (t < 196) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[t];
+    const int r = (4 * t) / 28, c = (4 * t) % 28;
+    float* d = img + (r + 2) * 32 + c + 2;
+    d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+  }
+  __syncthreads();
+  if (t >= 196) return;
+  const int ph = t / 14, pw = t - ph * 14;
+  float patch[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) patch[i][j] = img[(2 * ph + i) * 32 + 2 * pw + j];
+  const size_t gp = (size_t)b * 196 + t;
+  float out[8];
+  uint64_t idxw = 0;
+#pragma unroll 2
+  for (int cc = 0; cc < 8; ++cc) {
+    const float bias = w[KTAPS * 8 + cc];
+    float z[4] = {bias, bias, bias, bias};
+#pragma unroll
+    for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) {
+        const float wt = w[(kh * 5 + kw) * 8 + cc];
+        z[0] = fmaf(patch[kh][kw], wt, z[0]);
+        z[1] = fmaf(patch[kh][kw + 1], wt, z[1]);
+        z[2] = fmaf(patch[kh + 1][kw], wt, z[2]);
+        z[3] = fmaf(patch[kh + 1][kw + 1], wt, z[3]);
+      }
+    float mx = z[0];
+    int am = 0;
+#pragma unroll
+    for (int win = 1; win < 4; ++win)
+      if (z[win] > mx) { mx = z[win]; am = win; }
+    out[cc] = fmaxf(mx, 0.f);
+    idxw |= (uint64_t)am << (8 * cc);
+  }
+  f32x4* op = reinterpret_cast<f32x4*>(a.p1 + gp * 32 + cg * 8);
+  op[0] = f32x4{out[0], out[1], out[2], out[3]};
+  op[1] = f32x4{out[4], out[5], out[6], out[7]};
+  *reinterpret_cast<uint2*>(a.idx1 + gp * 32 + cg * 8) = make_uint2((uint32_t)idxw, (uint32_t)(idxw >> 32));
+}
+
+// ---------------- K2+K3: conv2 implicit GEMM (pool-window-major M), pooled epilogue ----------------
+// m = ((b*49 + pp)*4 + win), k = tap*32 + ci: each lane's 4 accumulator rows are one 2x2 window.
+struct Conv2FwdAF {
+  static constexpr bool KC = true;
+  const float* __restrict__ p1;
+  int M;
+  __device__ __forceinline__ f32x4 operator()(int m, int k) const {
+    if (m >= M || k >= 800) return zero_f4();
+    const int b = m / 196, r = m - b * 196, pp = r >> 2, win = r & 3;
+    const int ph = pp / 7, pw = pp - ph * 7;
+    const int tap = k >> 5, ci0 = k & 31, kh = tap / 5, kw = tap - kh * 5;
+    const int ih = 2 * ph + (win >> 1) + kh - 2, iw = 2 * pw + (win & 1) + kw - 2;
+    if ((unsigned)ih >= 14u || (unsigned)iw >= 14u) return zero_f4();
+    return *reinterpret_cast<const f32x4*>(p1 + ((size_t)(b * 14 + ih) * 14 + iw) * 32 + ci0);
+  }
+};
+struct PoolEpiF {
+  const float* __restrict__ bias;
+  float* __restrict__ p2;
+  uint8_t* __restrict__ idx2;
+  int M;
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+    if (m4 >= M) return;
+    const int b = m4 / 196, pp = (m4 - b * 196) >> 2;
+    const float bb = bias[n];
+    float mx = v[0] + bb;
+    int am = 0;
+#pragma unroll
+    for (int r = 1; r < 4; ++r) {
+      const float z = v[r] + bb;
+      if (z > mx) { mx = z; am = r; }
+    }
+    const size_t o = (size_t)b * FEAT + pp * 64 + n;
+    a_store(o, fmaxf(mx, 0.f), am);
+  }
+  __device__ __forceinline__ void a_store(size_t o, float v, int am) const {
+    p2[o] = v;
+    idx2[o] = (uint8_t)am;
+  }
+};
+constexpr int F_BK = 32;
+__global__ __launch_bounds__(256) void f32_conv2_fwd(MnistF32Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int M = a.B * 196;
+  Conv2FwdAF la{a.p1, M};
+  DenseLoaderF<false> lb{a.p32 + OFF_WC2, 64, 64, 800};
+  PoolEpiF epi{a.p32 + OFF_BC2, a.p2, a.idx2, M};
+  gemm_block_f32<64, 64, F_BK, 2, 2>(la, lb, epi, blockIdx.x * 64, 0, 0, 800, (float*)smem_raw);
+}
+
+// ---------------- K4: fc1 forward, split-K slabs (reduced by the head) ----------------
+struct SlabEpiF {
+  float* __restrict__ out;
+  int ld, M, N;
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+    if (n >= N) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (m4 + r < M) out[(size_t)(m4 + r) * ld + n] = v[r];
+  }
+};
+constexpr int F_FC1_SPLITS = 7;  // 3136 = 7 x 448
+__global__ __launch_bounds__(256) void f32_fc1_fwd(MnistF32Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  DenseLoaderF<true> la{a.p2, FEAT, a.B, FEAT};
+  DenseLoaderF<false> lb{a.p32 + OFF_WD1, HID, HID, FEAT};
+  const int z = blockIdx.z, kper = FEAT / F_FC1_SPLITS;
+  SlabEpiF epi{a.fc1_slab + (size_t)z * a.B * HID, HID, a.B, HID};
+  gemm_block_f32<64, 64, F_BK, 2, 2>(la, lb, epi, blockIdx.y * 64, blockIdx.x * 64, z * kper, (z + 1) * kper,
+                                     (float*)smem_raw);
+}
+
+// ---------------- K4..K9 head: slabs + bias + relu + dropout + FC10 + softmax-xent + dlogits/dh -------
+// One block per batch row; thread t owns hidden units 4t..4t+3 (same Philox stream as the bf16 step).
+__global__ __launch_bounds__(256) void f32_head(MnistF32Args a, int train) {
+  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int n0 = 4 * t;
+  const int lbl = a.labels[data_row_f(a.perm, a.step, a.n_data, a.B, row)];
+  f32x4 h = *reinterpret_cast<const f32x4*>(a.p32 + OFF_BD1 + n0);
+  {
+    f32x4 p[F_FC1_SPLITS];
+#pragma unroll
+    for (int s = 0; s < F_FC1_SPLITS; ++s) p[s] = *reinterpret_cast<const f32x4*>(a.fc1_slab + ((size_t)s * a.B + row) * HID + n0);
+#pragma unroll
+    for (int s = 0; s < F_FC1_SPLITS; ++s) h += p[s];
+  }
+  float hd[4], scale[4];
+  const float kp = train ? a.keep_prob : 1.0f;
+  if (kp < 1.0f) {
+    const int64_t st = *a.step;
+    Philox4 r = philox4x32_10((uint32_t)(row * 256 + t), (uint32_t)st, (uint32_t)(st >> 32), a.rank, a.seed, 0x5EED1234u);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) scale[j] = (u01(r.v[j]) < kp) ? (1.0f / kp) : 0.f;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) scale[j] = 1.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) hd[j] = fmaxf(h[j], 0.f) * scale[j];
+  const float* wout = a.p32 + OFF_OUT;
+  float lp[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) lp[c] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float* wr = wout + (size_t)(n0 + j) * NCLS;
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) lp[c] = fmaf(hd[j], wr[c], lp[c]);
+  }
+  __shared__ float red[4][NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) {
+    const float v = wave_sum(lp[c]);
+    if (lane == 0) red[wv][c] = v;
+  }
+  __syncthreads();
+  float logit[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) logit[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + a.p32[OFF_BOUT + c];
+  float mx = logit[0];
+  int am = 0;
+#pragma unroll
+  for (int c = 1; c < NCLS; ++c)
+    if (logit[c] > mx) { mx = logit[c]; am = c; }
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) se += expf(logit[c] - mx);
+  const float lse = mx + logf(se);
+  if (t == 0) {
+    a.loss_row[row] = lse - logit[lbl];
+    a.correct_row[row] = (am == lbl) ? 1.f : 0.f;
+  }
+  if (!train) return;
+  const float invB = 1.0f / (float)a.B;
+  float dl[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) dl[c] = (expf(logit[c] - lse) - (c == lbl ? 1.f : 0.f)) * invB;
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c)
+    if (t == c) a.dlogits[row * NCLS + c] = dl[c];
+  float dhv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float* wr = wout + (size_t)(n0 + j) * NCLS;
+    float d = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) d = fmaf(dl[c], wr[c], d);
+    dhv[j] = (h[j] > 0.f) ? d * scale[j] : 0.f;
+  }
+  *reinterpret_cast<f32x4*>(a.hd + (size_t)row * HID + n0) = f32x4{hd[0], hd[1], hd[2], hd[3]};
+  *reinterpret_cast<f32x4*>(a.dh + (size_t)row * HID + n0) = f32x4{dhv[0], dhv[1], dhv[2], dhv[3]};
+}
+
+// ---------------- K8: output layer dW/db [1025][10] = [Hd;1]^T dlogits ----------------
+constexpr int F_OUTG_ROWS = 64;
+constexpr int F_OUTG_BLOCKS = (HID + 1 + F_OUTG_ROWS - 1) / F_OUTG_ROWS;  // 17
+__device__ __forceinline__ void f32_out_grad_block(const MnistF32Args& a, int blk, float* smem) {
+  float* dl = smem;                 // [B][10]
+  float* part = smem + a.B * NCLS;  // [4][64][10]
+  const int t = threadIdx.x, r = t & 63, q = t >> 6;
+  for (int i = t; i < a.B * NCLS; i += 256) dl[i] = a.dlogits[i];
+  __syncthreads();
+  const int m = blk * F_OUTG_ROWS + r;
+  float acc[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) acc[c] = 0.f;
+  const int bq = (a.B + 3) >> 2, b0 = q * bq, b1 = min(a.B, b0 + bq);
+  if (m < HID) {
+    for (int b = b0; b < b1; ++b) {
+      const float h = a.hd[(size_t)b * HID + m];
+#pragma unroll
+      for (int c = 0; c < NCLS; ++c) acc[c] = fmaf(h, dl[b * NCLS + c], acc[c]);
+    }
+  } else if (m == HID) {
+    for (int b = b0; b < b1; ++b)
+#pragma unroll
+      for (int c = 0; c < NCLS; ++c) acc[c] += dl[b * NCLS + c];
+  }
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) part[(q * 64 + r) * NCLS + c] = acc[c];
+  __syncthreads();
+  for (int i = t; i < F_OUTG_ROWS * NCLS; i += 256) {
+    const int rr = i / NCLS, mm = blk * F_OUTG_ROWS + rr;
+    if (mm <= HID)
+      a.grad[OFF_OUT + (size_t)mm * NCLS + (i - rr * NCLS)] =
+          part[i] + part[F_OUTG_ROWS * NCLS + i] + part[2 * F_OUTG_ROWS * NCLS + i] + part[3 * F_OUTG_ROWS * NCLS + i];
+  }
+}
+
+// ---------------- K10: fc1 dW [3137][1024] = [P2;1]^T dH, dX [B][3136] (+ unpool epilogue) ----------------
+struct OnesRowMCF {  // (mn, k) = X[k][mn] for mn < mn_real, 1 for mn == mn_real (k < k_lim); 4 along mn
+  static constexpr bool KC = false;
+  const float* __restrict__ x;
+  int ld, mn_real, k_lim;
+  __device__ __forceinline__ f32x4 operator()(int mn, int k) const {
+    if (k >= k_lim) return zero_f4();
+    if (mn + 4 <= mn_real) return *reinterpret_cast<const f32x4*>(x + (size_t)k * ld + mn);
+    f32x4 t;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = mn + j;
+      t[j] = c < mn_real ? x[(size_t)k * ld + c] : (c == mn_real ? 1.f : 0.f);
+    }
+    return t;
+  }
+};
+struct GradEpiF {
+  float* __restrict__ out;
+  int ld, M, N;
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+    if (n >= N) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (m4 + r < M) out[(size_t)(m4 + r) * ld + n] = v[r];
+  }
+};
+struct UnpoolEpiF {
+  const float* __restrict__ p2;
+  const uint8_t* __restrict__ idx2;
+  float* __restrict__ dz2;
+  int B;
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+    if (n >= FEAT) return;
+    const int pp = n >> 6, c = n & 63, ph = pp / 7, pw = pp - ph * 7;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = m4 + r;
+      if (b >= B) continue;
+      const size_t o = (size_t)b * FEAT + n;
+      const float g = p2[o] > 0.f ? v[r] : 0.f;  // relu output > 0
+      const int w = idx2[o];
+#pragma unroll
+      for (int wi = 0; wi < 4; ++wi) {
+        const int oh = 2 * ph + (wi >> 1), ow = 2 * pw + (wi & 1);
+        dz2[((size_t)(b * 14 + oh) * 14 + ow) * 64 + c] = (wi == w) ? g : 0.f;
+      }
+    }
+  }
+};
+constexpr int F_DW_GX = HID / 64, F_DW_GY = (FEAT + 1 + 63) / 64;  // 16 x 50
+constexpr int F_DX_GX = FEAT / 64;                                  // 49 (x ceil(B/32))
+// [out-layer grad blocks | dX tiles (long K first) | dW tiles]
+__global__ __launch_bounds__(256) void f32_fc1_bwd(MnistF32Args a, int n_dx) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  int id = blockIdx.x;
+  if (id < F_OUTG_BLOCKS) { f32_out_grad_block(a, id, (float*)smem_raw); return; }
+  id -= F_OUTG_BLOCKS;
+  if (id < n_dx) {
+    const int bx = id % F_DX_GX, by = id / F_DX_GX;
+    DenseLoaderF<true> la{a.dh, HID, a.B, HID};
+    DenseLoaderF<true> lb{a.p32 + OFF_WD1, HID, FEAT, HID};
+    UnpoolEpiF epi{a.p2, a.idx2, a.dz2, a.B};
+    gemm_block_f32<32, 64, F_BK, 2, 2>(la, lb, epi, by * 32, bx * 64, 0, HID, (float*)smem_raw);
+    return;
+  }
+  id -= n_dx;
+  const int bx = id % F_DW_GX, by = id / F_DW_GX;
+  OnesRowMCF la{a.p2, FEAT, FEAT, a.B};
+  DenseLoaderF<false> lb{a.dh, HID, HID, a.B};
+  GradEpiF epi{a.grad + OFF_WD1, HID, FEAT + 1, HID};
+  gemm_block_f32<64, 64, F_BK, 2, 2>(la, lb, epi, by * 64, bx * 64, 0, a.B, (float*)smem_raw);
+}
+
+// ---------------- K13: conv2 dgrad + conv1 relu/pool-mask epilogue; K14: conv2 wgrad slabs ----------
+struct Conv2DgradAF {  // (m = (b,ih,iw), k = tap*64 + co) = dz2[b][ih-kh+2][iw-kw+2][co]
+  static constexpr bool KC = true;
+  const float* __restrict__ dz2;
+  int M;
+  __device__ __forceinline__ f32x4 operator()(int m, int k) const {
+    if (m >= M || k >= 1600) return zero_f4();
+    const int b = m / 196, r = m - b * 196, ih = r / 14, iw = r - ih * 14;
+    const int tap = k >> 6, co0 = k & 63, kh = tap / 5, kw = tap - kh * 5;
+    const int oh = ih - kh + 2, ow = iw - kw + 2;
+    if ((unsigned)oh >= 14u || (unsigned)ow >= 14u) return zero_f4();
+    return *reinterpret_cast<const f32x4*>(dz2 + ((size_t)(b * 14 + oh) * 14 + ow) * 64 + co0);
+  }
+};
+struct Conv2DgradBF {  // (n = ci, k = tap*64 + co) -> W2[tap][ci][co]
+  static constexpr bool KC = true;
+  const float* __restrict__ w2;
+  __device__ __forceinline__ f32x4 operator()(int n, int k) const {
+    if (n >= 32 || k >= 1600) return zero_f4();
+    const int tap = k >> 6, co0 = k & 63;
+    return *reinterpret_cast<const f32x4*>(w2 + (size_t)(tap * 32 + n) * 64 + co0);
+  }
+};
+struct MaskEpiF {
+  const float* __restrict__ p1;
+  float* __restrict__ dp1m;
+  int M;
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m4 + r;
+      if (m >= M) return;
+      const size_t o = (size_t)m * 32 + n;
+      dp1m[o] = p1[o] > 0.f ? v[r] : 0.f;  // relu output > 0
+    }
+  }
+};
+struct Conv2WgradAF {  // (mn = tap*32+ci [800 = ones row], k = pixel): 4 consecutive ci
+  static constexpr bool KC = false;
+  const float* __restrict__ p1;
+  int K;
+  __device__ __forceinline__ f32x4 operator()(int mn, int k) const {
+    if (k >= K || mn > 800) return zero_f4();
+    if (mn == 800) return f32x4{1.f, 0.f, 0.f, 0.f};
+    const int tap = mn >> 5, ci0 = mn & 31, kh = tap / 5, kw = tap - kh * 5;
+    const int b = k / 196, r = k - b * 196, oh = r / 14, ow = r - oh * 14;
+    const int ih = oh + kh - 2, iw = ow + kw - 2;
+    if ((unsigned)ih >= 14u || (unsigned)iw >= 14u) return zero_f4();
+    return *reinterpret_cast<const f32x4*>(p1 + ((size_t)(b * 14 + ih) * 14 + iw) * 32 + ci0);
+  }
+};
+constexpr int F_C2W_GX = (801 + 63) / 64;  // 13
+constexpr int F_C2W_KPER = 1024;           // pixels per slab
+__global__ __launch_bounds__(256) void f32_conv2_bwd(MnistF32Args a, int n_dgrad) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int id = blockIdx.x;
+  const int M = a.B * 196;
+  if (id < n_dgrad) {
+    Conv2DgradAF la{a.dz2, M};
+    Conv2DgradBF lb{a.p32 + OFF_WC2};
+    MaskEpiF epi{a.p1, a.dp1m, M};
+    gemm_block_f32<64, 32, F_BK, 2, 2>(la, lb, epi, id * 64, 0, 0, 1600, (float*)smem_raw);
+    return;
+  }
+  const int w = id - n_dgrad, bx = w % F_C2W_GX, z = w / F_C2W_GX;
+  Conv2WgradAF la{a.p1, M};
+  DenseLoaderF<false> lb{a.dz2, 64, 64, M};
+  SlabEpiF epi{a.wg2_slab + (size_t)z * 801 * 64, 64, 801, 64};
+  const int kb = z * F_C2W_KPER, ke = min(M, kb + F_C2W_KPER);
+  gemm_block_f32<64, 64, F_BK, 2, 2>(la, lb, epi, bx * 64, 0, kb, ke, (float*)smem_raw);
+}
+
+// ---------------- K15 + K12: conv1 wgrad + bias grad (sparse: only the argmax pixel of a window) -------
+constexpr int F_C1W_HALF = 98;
+__global__ __launch_bounds__(256) void f32_conv1_wgrad(MnistF32Args a) {
+  __shared__ float img[32 * 32];
+  __shared__ __attribute__((aligned(16))) float gs[F_C1W_HALF * 32];
+  __shared__ __attribute__((aligned(16))) uint8_t is[F_C1W_HALF * 32];
+  __shared__ float part[8][26 * 32 + 1];
+  const int b = blockIdx.x >> 1, half = blockIdx.x & 1, t = threadIdx.x, c = t & 31, sub = t >> 5;
+  const float* x = a.data + (size_t)data_row_f(a.perm, a.step, a.n_data, a.B, b) * 784;
+  for (int i = t; i < 32 * 32; i += 256) img[i] = 0.f;
+  const size_t base = ((size_t)b * 196 + half * F_C1W_HALF) * 32;
+  for (int i = t; i < F_C1W_HALF * 32 / 4; i += 256)
+    reinterpret_cast<f32x4*>(gs)[i] = reinterpret_cast<const f32x4*>(a.dp1m + base)[i];
+  for (int i = t; i < F_C1W_HALF * 32 / 16; i += 256)
+    reinterpret_cast<uint4*>(is)[i] = reinterpret_cast<const uint4*>(a.idx1 + base)[i];
+  __syncthreads();
+  if (t < 196) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[t];
+    const int r = (4 * t) / 28, q = (4 * t) % 28;
+    float* d = img + (r + 2) * 32 + q + 2;
+    d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+  }
+  __syncthreads();
+  float acc[26];
+#pragma unroll
+  for (int j = 0; j < 26; ++j) acc[j] = 0.f;
+  for (int lp = sub; lp < F_C1W_HALF; lp += 8) {
+    const float g = gs[lp * 32 + c];
+    if (g != 0.f) {
+      const int pp = half * F_C1W_HALF + lp, w = is[lp * 32 + c];
+      const int oh = 2 * (pp / 14) + (w >> 1), ow = 2 * (pp % 14) + (w & 1);
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] = fmaf(g, img[(oh + kh) * 32 + ow + kw], acc[kh * 5 + kw]);
+      acc[25] += g;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 26; ++j) part[sub][j * 32 + c] = acc[j];
+  __syncthreads();
+  for (int i = t; i < 26 * 32; i += 256) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += part[q][i];
+    a.wg1_slab[(size_t)blockIdx.x * 832 + i] = s;
+  }
+}
+
+template <auto K>
+inline void set_smem_f(int bytes) {
+  static bool done = false;
+  if (!done && bytes > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(K), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  done = true;
+}
+
+}  // namespace
+
+int mnist_f32_fc1_splits() { return F_FC1_SPLITS; }
+int mnist_f32_wg2_splits(int B) { return (B * 196 + F_C2W_KPER - 1) / F_C2W_KPER; }
+
+void mnist_f32_forward(const MnistF32Args& a, bool train, hipStream_t s) {
+  const int B = a.B;
+  f32_conv1_pool_fwd<<<4 * B, 256, 0, s>>>(a);
+  {
+    constexpr int sm = GemmSmemF<64, 64, F_BK, Conv2FwdAF, DenseLoaderF<false>>::BYTES;
+    set_smem_f<f32_conv2_fwd>(sm);
+    f32_conv2_fwd<<<(B * 196 + 63) / 64, 256, sm, s>>>(a);
+  }
+  {
+    constexpr int sm = GemmSmemF<64, 64, F_BK, DenseLoaderF<true>, DenseLoaderF<false>>::BYTES;
+    set_smem_f<f32_fc1_fwd>(sm);
+    f32_fc1_fwd<<<dim3(HID / 64, (B + 63) / 64, F_FC1_SPLITS), 256, sm, s>>>(a);
+  }
+  f32_head<<<B, 256, 0, s>>>(a, train ? 1 : 0);
+}
+
+void mnist_f32_backward(const MnistF32Args& a, hipStream_t s) {
+  const int B = a.B;
+  {
+    constexpr int sm_dw = GemmSmemF<64, 64, F_BK, OnesRowMCF, DenseLoaderF<false>>::BYTES;
+    constexpr int sm_dx = GemmSmemF<32, 64, F_BK, DenseLoaderF<true>, DenseLoaderF<true>>::BYTES;
+    const int sm_og = (B * NCLS + 4 * F_OUTG_ROWS * NCLS) * 4;
+    const int sm = std::max(std::max(sm_dw, sm_dx), sm_og);
+    set_smem_f<f32_fc1_bwd>(sm);
+    const int n_dx = F_DX_GX * ((B + 31) / 32);
+    f32_fc1_bwd<<<F_OUTG_BLOCKS + n_dx + F_DW_GX * F_DW_GY, 256, sm, s>>>(a, n_dx);
+  }
+  {
+    constexpr int sm_d = GemmSmemF<64, 32, F_BK, Conv2DgradAF, Conv2DgradBF>::BYTES;
+    constexpr int sm_w = GemmSmemF<64, 64, F_BK, Conv2WgradAF, DenseLoaderF<false>>::BYTES;
+    constexpr int sm = sm_d > sm_w ? sm_d : sm_w;
+    set_smem_f<f32_conv2_bwd>(sm);
+    const int n_dgrad = (B * 196 + 63) / 64;
+    f32_conv2_bwd<<<n_dgrad + F_C2W_GX * a.wg2_splits, 256, sm, s>>>(a, n_dgrad);
+  }
+  f32_conv1_wgrad<<<2 * B, 256, 0, s>>>(a);
+}
+
+}  // namespace tfd

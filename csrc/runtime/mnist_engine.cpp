@@ -105,7 +105,7 @@ class MnistEngine : public torch::CustomClassHolder {
   at::Tensor step_tensor() { return step_; }
   at::Tensor loss_rows() { return loss_row_; }
   at::Tensor correct_rows() { return correct_row_; }
-  at::Tensor hidden() { return hd_; }
+  at::Tensor hidden() { return fp32_ ? fhd_ : hd_; }
   at::Tensor pool2() { return p2_; }
   at::Tensor pool1() { return p1_; }
   at::Tensor feed_x() { return xbuf_; }
@@ -139,14 +139,14 @@ class MnistEngine : public torch::CustomClassHolder {
   }
   void set_comm(c10::intrusive_ptr<RcclComm> comm, bool bf16_grads) {
     comm_ = comm;
-    bf16_comm_ = bf16_grads;
+    bf16_comm_ = bf16_grads && !fp32_;
   }
   // Peer-to-peer IPC all-reduce for latency-bound buckets (<= small_max elements, e.g. the conv
   // bucket B); without an RCCL communicator it carries every bucket (one-GPU multi-process tests).
   void set_ipc(c10::intrusive_ptr<IpcComm> ipc, int64_t small_max, bool bf16_grads) {
     ipc_ = ipc;
     ipc_small_ = small_max;
-    if (!comm_) bf16_comm_ = bf16_grads;
+    if (!comm_) bf16_comm_ = bf16_grads && !fp32_;
   }
   int64_t world() const {
     if (comm_) return comm_->world();
@@ -191,6 +191,29 @@ class MnistEngine : public torch::CustomClassHolder {
     ag_w(s);
   }
 
+  // ---- compute precision ----
+  // "bf16" (default): bf16 MFMA operands / activations, fp32 accumulation, master and optimizer.
+  // "fp32": the reference's precision -- every operand and activation fp32, GEMMs on the fp32
+  // matrix core (csrc/kernels/mnist_f32.hip); the gradient wire format becomes fp32 too.
+  void set_dtype(const std::string& dt) {
+    TORCH_CHECK(dt == "bf16" || dt == "fp32", "dtype must be bf16 or fp32");
+    const bool f = dt == "fp32";
+    if (f && !f1_.defined()) {
+      auto f32 = at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device_);
+      f1_ = at::empty({B_, P1H, P1H, C1}, f32);
+      f2_ = at::empty({B_, FEAT}, f32);
+      fhd_ = at::empty({B_, HID}, f32);
+      fdh_ = at::empty({B_, HID}, f32);
+      fdz2_ = at::empty({B_, P1H, P1H, C2}, f32);
+      fdp1m_ = at::empty({B_, P1H, P1H, C1}, f32);
+      fslab_ = at::empty({mnist_f32_fc1_splits(), B_, HID}, f32);
+      fwg2_ = at::empty({mnist_f32_wg2_splits((int)B_), 801, C2}, f32);
+    }
+    fp32_ = f;
+    if (f) bf16_comm_ = false;
+  }
+  std::string dtype() const { return fp32_ ? "fp32" : "bf16"; }
+
   // ---- per-phase GPU timing ----
   // With timing on, train_step records HIP timing events at its phase boundaries -- also inside a
   // captured graph (event-record nodes) -- and phase_times() returns the last step's
@@ -221,13 +244,26 @@ class MnistEngine : public torch::CustomClassHolder {
   }
 
   // ---- step pieces (current HIP stream) ----
-  void forward(bool train) { mnist_forward(args(), train, stream()); }
-  void backward_a() { mnist_backward_a(args(), stream()); }
+  void forward(bool train) {
+    if (fp32_) mnist_f32_forward(args_f32(), train, stream());
+    else mnist_forward(args(), train, stream());
+  }
+  // fp32 mode: backward_a runs the whole backward (fc + conv), backward_b the slab reduce
+  void backward_a() {
+    if (fp32_) mnist_f32_backward(args_f32(), stream());
+    else mnist_backward_a(args(), stream());
+  }
   // backward_b ends with the conv-grad reduce kernel, which also bumps global_step (see
   // MnistStepArgs::step_bump): apply_optimizer() after it therefore uses t = global_step.
   void backward_b() {
     MnistStepArgs a = args();
     a.step_bump = (int64_t*)step_.data_ptr();
+    if (fp32_) {
+      a.wg2_slab = (float*)fwg2_.data_ptr();
+      a.wg2_splits = mnist_f32_wg2_splits((int)B_);
+      mnist_conv_grad_reduce(a, stream());
+      return;
+    }
     mnist_backward_b(a, stream(), conv_fork_ ? aux_stream_ : nullptr, ev_fork_, ev_join_);
     mnist_conv_grad_reduce(a, stream());
   }
@@ -268,6 +304,10 @@ class MnistEngine : public torch::CustomClassHolder {
     const bool dp = this->dp();
     timed_ = timing_;
     timed_dp_ = timing_ && dp;
+    if (fp32_) {
+      train_step_f32(dp);
+      return;
+    }
     if (dp) {
       train_step_dp(join_end);
       return;
@@ -384,6 +424,38 @@ class MnistEngine : public torch::CustomClassHolder {
     else pending_opt_a_ = true;
   }
 
+  // fp32 step: forward, backward (fc grads + conv slabs), slab reduce + step bump, [fp32
+  // all-reduce of the whole buffer], optimizer (t = bumped step).
+  void train_step_f32(bool dp) {
+    TORCH_CHECK(!zero_, "ZeRO-1 is a bf16-path option");
+    hipStream_t s = stream();
+    MnistF32Args f = args_f32();
+    mark(P_START, s);
+    mnist_f32_forward(f, true, s);
+    mark(P_FWD, s);
+    mnist_f32_backward(f, s);
+    mark(P_BFC, s);
+    MnistStepArgs r = args();
+    r.wg2_slab = f.wg2_slab;
+    r.wg2_splits = f.wg2_splits;
+    r.step_bump = (int64_t*)step_.data_ptr();
+    mnist_conv_grad_reduce(r, s);
+    mark(P_BCONV, s);
+    if (dp) {
+      HIP_OK(hipEventRecord(ev_b_, s));
+      HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
+      mark(P_CA0, comm_stream_);
+      reduce_bucket(0, TOTAL, false);
+      mark(P_CA1, comm_stream_);
+      mark(P_CB0, comm_stream_);
+      mark(P_CB1, comm_stream_);
+      HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+      HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+    }
+    apply_optimizer_range(0, TOTAL, 1.0 / (double)world(), 0, s);
+    mark(P_OPT, s);
+  }
+
   void train_step_zero() {
     timed_ = false;
     hipStream_t s = stream();
@@ -444,12 +516,21 @@ class MnistEngine : public torch::CustomClassHolder {
     auto out = at::zeros({2}, x.options());
     for (int64_t o = 0; o < n; o += B_) {
       const int nb = (int)std::min<int64_t>(B_, n - o);
-      MnistStepArgs a = args();
-      a.B = nb;
-      a.data = (const float*)x.data_ptr() + o * 784;
-      a.labels = (const int*)y.data_ptr() + o;
-      a.perm = nullptr;
-      mnist_forward(a, false, stream());
+      if (fp32_) {
+        MnistF32Args f = args_f32();
+        f.B = nb;
+        f.data = (const float*)x.data_ptr() + o * 784;
+        f.labels = (const int*)y.data_ptr() + o;
+        f.perm = nullptr;
+        mnist_f32_forward(f, false, stream());
+      } else {
+        MnistStepArgs a = args();
+        a.B = nb;
+        a.data = (const float*)x.data_ptr() + o * 784;
+        a.labels = (const int*)y.data_ptr() + o;
+        a.perm = nullptr;
+        mnist_forward(a, false, stream());
+      }
       out[0] += loss_row_.narrow(0, 0, nb).sum();
       out[1] += correct_row_.narrow(0, 0, nb).sum();
     }
@@ -559,6 +640,40 @@ class MnistEngine : public torch::CustomClassHolder {
     }
   }
 
+  MnistF32Args args_f32() {
+    TORCH_CHECK(f1_.defined(), "set_dtype('fp32') first");
+    MnistStepArgs a = args();
+    MnistF32Args f{};
+    f.B = a.B;
+    f.data = a.data;
+    f.labels = a.labels;
+    f.perm = a.perm;
+    f.n_data = a.n_data;
+    f.step = a.step;
+    f.p32 = a.p32;
+    f.grad = a.grad;
+    f.p1 = (float*)f1_.data_ptr();
+    f.idx1 = a.idx1;
+    f.p2 = (float*)f2_.data_ptr();
+    f.idx2 = a.idx2;
+    f.fc1_slab = (float*)fslab_.data_ptr();
+    f.hd = (float*)fhd_.data_ptr();
+    f.dh = (float*)fdh_.data_ptr();
+    f.dlogits = a.dlogits;
+    f.loss_row = a.loss_row;
+    f.correct_row = a.correct_row;
+    f.dz2 = (float*)fdz2_.data_ptr();
+    f.dp1m = (float*)fdp1m_.data_ptr();
+    f.wg2_slab = (float*)fwg2_.data_ptr();
+    f.wg1_slab = a.wg1_slab;
+    f.fc1_splits = mnist_f32_fc1_splits();
+    f.wg2_splits = mnist_f32_wg2_splits((int)B_);
+    f.keep_prob = a.keep_prob;
+    f.seed = a.seed;
+    f.rank = a.rank;
+    return f;
+  }
+
   MnistStepArgs args() {
     MnistStepArgs a{};
     a.B = (int)B_;
@@ -615,6 +730,8 @@ class MnistEngine : public torch::CustomClassHolder {
   at::Tensor p1_, idx1_, p2_, idx2_, fc1_slab_, hd_, dh_, dlogits_, loss_row_, correct_row_, dz2_, dp1m_, wg2_slab_,
       wg1_slab_, xbuf_, ybuf_;
   at::Tensor data_, labels_, perm_;
+  at::Tensor f1_, f2_, fhd_, fdh_, fdz2_, fdp1m_, fslab_, fwg2_;  // fp32-mode activations / slabs
+  bool fp32_ = false;
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t ev_a_ = nullptr, ev_b_ = nullptr, ev_done_ = nullptr, ev_fork_ = nullptr, ev_join_ = nullptr;
   hipStream_t aux_stream_ = nullptr, opt_stream_ = nullptr;
@@ -679,6 +796,8 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_fused_tail", &MnistEngine::set_fused_tail)
       .def("set_local_bf16_grads", &MnistEngine::set_local_bf16_grads)
       .def("set_fc_adam", &MnistEngine::set_fc_adam)
+      .def("set_dtype", &MnistEngine::set_dtype)
+      .def("dtype", &MnistEngine::dtype)
       .def("set_phase_timing", &MnistEngine::set_phase_timing)
       .def("phase_times", &MnistEngine::phase_times)
       .def("zero", &MnistEngine::zero)

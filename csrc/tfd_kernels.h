@@ -76,6 +76,35 @@ void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_
 // gradients never reach memory; t = global_step + 1). Launch after the dX GEMM (part 2).
 void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s);
 
+// ---------------- reference-precision (fp32) MNIST step: csrc/kernels/mnist_f32.hip ----------------
+// Same dataflow and flat parameter layout as the bf16 step, every operand and activation fp32,
+// every GEMM on v_mfma_f32_16x16x4_f32 (csrc/gemm_f32.h). The conv-slab layouts match the bf16
+// step's, so mnist_conv_grad_reduce (MnistStepArgs view) finishes the conv gradients.
+struct MnistF32Args {
+  int B;
+  const float* data; const int* labels; const int* perm; int n_data;
+  const int64_t* step;
+  const float* p32;            // flat fp32 params
+  float* grad;                 // flat fp32 gradients
+  float* p1; uint8_t* idx1;    // [B][14][14][32]
+  float* p2; uint8_t* idx2;    // [B][3136]
+  float* fc1_slab;             // [splits][B][1024]
+  float* hd; float* dh;        // [B][1024]
+  float* dlogits;              // [B][10]
+  float* loss_row; float* correct_row;
+  float* dz2;                  // [B][14][14][64]
+  float* dp1m;                 // [B][14][14][32]
+  float* wg2_slab;             // [wg2_splits][801][64]
+  float* wg1_slab;             // [2B][832]
+  int fc1_splits, wg2_splits;
+  float keep_prob;
+  uint32_t seed, rank;
+};
+int mnist_f32_fc1_splits();
+int mnist_f32_wg2_splits(int B);
+void mnist_f32_forward(const MnistF32Args& a, bool train, hipStream_t s);
+void mnist_f32_backward(const MnistF32Args& a, hipStream_t s);  // fc + conv grads (slabs for conv)
+
 // ---------------- optimizers (flat, fp32 master + bf16 shadow) ----------------
 struct AdamArgs {
   float* p; float* m; float* v; const float* g; uint16_t* pbf;

@@ -47,6 +47,8 @@ def main(argv=None):
     ap.add_argument("--no_graph", action="store_true", help="GPU: launch kernels per step (no hipGraph)")
     ap.add_argument("--eval_batches", type=int, default=50)
     ap.add_argument("--train_flag", type=int, default=1, help="1 = train, else evaluation only (mnist_single.py:103)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="GPU compute precision (fp32 = the "
+                    "reference's)")
     ap.add_argument("--host_feed", action="store_true", help="GPU: feed every batch from the host (next_batch + "
                     "H2D) instead of the device-resident split with a per-epoch device shuffle")
     a = ap.parse_args(argv)
@@ -55,7 +57,7 @@ def main(argv=None):
     mnist = input_data.read_data_sets(a.data_dir, one_hot=True, seed=a.seed)
     dev = torch.device("cuda", 0) if (torch.cuda.is_available() and not a.cpu) else torch.device("cpu")
     runner = make_runner(a.batch_size, AdamOptimizer(a.learning_rate), dev, keep_prob=dropout, seed=a.seed,
-                         use_graph=not a.no_graph)
+                         use_graph=not a.no_graph, dtype=a.dtype)
     runner.load_flat(M.flat_from_dict(M.init_params(a.seed)), {}, 0)  # init = initialize_all_variables()
     device_input = dev.type == "cuda" and not a.host_feed
     if device_input:  # upload the split once; batches are gathered on the GPU (no per-step feed)

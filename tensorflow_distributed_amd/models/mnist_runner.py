@@ -198,7 +198,8 @@ class NativeMnistRunner(MnistRunnerBase):
     """GPU runner over the native MnistEngine (HIP kernels + RCCL + hipGraph)."""
 
     def __init__(self, batch_size: int, optimizer, keep_prob: float = 0.75, seed: int = 0, rank: int = 0,
-                 device: Optional[torch.device] = None, comm=None, bf16_grads: bool = True, use_graph: bool = True):
+                 device: Optional[torch.device] = None, comm=None, bf16_grads: bool = True, use_graph: bool = True,
+                 dtype: str = "bf16"):
         from .. import _native
 
         _native.require()
@@ -207,6 +208,7 @@ class NativeMnistRunner(MnistRunnerBase):
         self.keep_prob = keep_prob
         self.opt = base_optimizer(optimizer)
         self.eng = torch.classes.tfd.MnistEngine(batch_size, self.device.index, keep_prob, seed, rank)
+        self.eng.set_dtype(dtype)  # "bf16" MFMA operands, or "fp32" (the reference's precision)
         o = self.opt
         if o.kind == "adam":
             self.eng.set_adam(o.learning_rate, o.beta1, o.beta2, o.epsilon)
@@ -412,7 +414,9 @@ class NativeMnistRunner(MnistRunnerBase):
 
 
 def make_runner(batch_size: int, optimizer, device: torch.device, keep_prob: float = 0.75, seed: int = 0,
-                rank: int = 0, comm=None, bf16_grads: bool = True, use_graph: bool = True) -> MnistRunnerBase:
+                rank: int = 0, comm=None, bf16_grads: bool = True, use_graph: bool = True,
+                dtype: str = "bf16") -> MnistRunnerBase:
     if device.type == "cuda":
-        return NativeMnistRunner(batch_size, optimizer, keep_prob, seed, rank, device, comm, bf16_grads, use_graph)
+        return NativeMnistRunner(batch_size, optimizer, keep_prob, seed, rank, device, comm, bf16_grads, use_graph,
+                                 dtype)
     return TorchMnistRunner(batch_size, optimizer, keep_prob, seed, rank, device)

@@ -99,6 +99,14 @@ def define_flags(task_index_default: int = 0, job_name_default: str = "ps") -> N
     f.DEFINE_boolean("phase_timing", False, "GPU: HIP timing events at the step's phase boundaries (forward, fc "
                      "backward, conv backward, optimizer, all-reduce), written to --metrics_file (always on when "
                      "--metrics_file is set on the chief)")
+    f.DEFINE_enum("dtype", "bf16", ["bf16", "fp32"], "GPU compute precision: bf16 MFMA operands (fp32 accumulate, "
+                  "master weights and optimizer), or fp32 everywhere (the reference's precision, "
+                  "mnist_python_m.py:185-200)")
+    f.DEFINE_float("bucket_mb", 0.0, "Gradient all-reduce bucketing: 0 = the MNIST engine's two buckets (fc 12.9 "
+                   "MB over RCCL, conv 0.2 MB over the IPC one-shot kernel); > 0 = bucket size for the "
+                   "generic bucket reducer (--model resnet*)")
+    f.DEFINE_enum("model", "mnist_cnn", ["mnist_cnn", "resnet18", "resnet50"], "Model: the reference CNN, or the "
+                  "synthetic-ImageNet ResNet family (BASELINE configs 4-5; trained by bench_resnet.py)")
     f.DEFINE_boolean("device_input", True, "GPU: upload the training split once and index it on the device "
                      "by a per-epoch shuffle (no per-step host feed); False = host next_batch + H2D per step")
 
@@ -111,6 +119,67 @@ def _make_optimizer():
     if FLAGS.optimizer == "momentum":
         return MomentumOptimizer(FLAGS.learning_rate, FLAGS.momentum)
     return AdamOptimizer(FLAGS.learning_rate)
+
+
+def _resnet_worker(server, cluster, num_workers: int, is_chief: bool) -> int:
+    """``--model resnet18|resnet50``: the same cluster roles and stdout, training the synthetic-
+    ImageNet ResNet family (BASELINE configs 4-5) with synchronous DP -- bucketed bf16 gradient
+    all-reduce (``--bucket_mb``, default 8) overlapped with the backward, fused SGD-momentum (lr =
+    ``--learning_rate``). RCCL between GPUs; the IPC transport when workers share a GPU. Synthetic
+    data: one device-resident random 224x224x3 batch per worker. No checkpointing in this mode."""
+    import torch.distributed as dist
+
+    from ..models.resnet import ResNet
+    from ..parallel.ipc import IpcCollectives, make_ipc_comm
+    from ..parallel.transport import devices_shared, make_rccl
+
+    if not FLAGS.sync_replicas or FLAGS.num_gpus <= 0:
+        raise ValueError("--model %s: synchronous data parallelism on GPUs only (--num_gpus > 0)" % FLAGS.model)
+    gpu = FLAGS.task_index % FLAGS.num_gpus
+    torch.cuda.set_device(gpu)
+    device = torch.device("cuda", gpu)
+    depth = int(FLAGS.model.replace("resnet", ""))
+    m = ResNet(depth, num_classes=1000, device=device, seed=FLAGS.seed)
+    comm = None
+    if num_workers > 1:
+        grp = server.worker_group
+        if devices_shared(device, num_workers, grp):
+            comm = IpcCollectives(make_ipc_comm(FLAGS.task_index, num_workers, gpu, m.fp.total, group=grp))
+        else:
+            comm = make_rccl(FLAGS.task_index, num_workers, gpu, group=grp, src=cluster.num_ps)
+        host = m.fp.master.detach().cpu()
+        dist.broadcast(host, cluster.num_ps, group=grp)  # chief init -> every worker
+        m.fp.master.copy_(host.to(device))
+        m.fp.shadow.copy_(m.fp.master)
+    m.set_comm(comm, FLAGS.bucket_mb or 8.0)
+    g = torch.Generator(device=device).manual_seed(100 + FLAGS.task_index)
+    x = torch.randn(FLAGS.batch_size, 224, 224, 3, device=device, generator=g)
+    y = torch.randint(0, 1000, (FLAGS.batch_size,), device=device, generator=g, dtype=torch.int32)
+    print("Worker %d: Session initialization complete." % FLAGS.task_index)
+    time_begin = time.time()
+    print("Training begins @ %f" % time_begin)
+    step = 0
+    while step < FLAGS.train_steps:
+        loss = m.train_step(x, y, lr=FLAGS.learning_rate)
+        step += 1
+        if not FLAGS.quiet:
+            print("%f: Worker %d: training step %d done (global step: %d) loss %.4f" % (
+                time.time(), FLAGS.task_index, step, step, float(loss)))
+    torch.cuda.synchronize(device)
+    time_end = time.time()
+    print("Training ends @ %f" % time_end)
+    el = time_end - time_begin
+    print("Training elapsed time: %f s" % el)
+    print("Worker %d: %.1f images/sec (this worker)" % (FLAGS.task_index, FLAGS.batch_size * step / max(el, 1e-9)))
+    if num_workers > 1:
+        dist.barrier(group=server.worker_group)
+    if isinstance(comm, IpcCollectives):
+        if comm.ipc.error():
+            raise RuntimeError("IPC collective barrier timed out")
+        comm.ipc.close()
+    server.mark_done()
+    server.shutdown()
+    return 0
 
 
 def main(argv=None) -> int:
@@ -183,6 +252,8 @@ def main(argv=None) -> int:
         return 0
 
     is_chief = FLAGS.task_index == 0
+    if FLAGS.model != "mnist_cnn":
+        return _resnet_worker(server, cluster, num_workers, is_chief)
     if FLAGS.num_gpus > 0:
         gpu = FLAGS.task_index % FLAGS.num_gpus
         torch.cuda.set_device(gpu)
@@ -196,7 +267,8 @@ def main(argv=None) -> int:
 
     runner = make_runner(FLAGS.batch_size, opt, device, keep_prob=FLAGS.keep_prob, seed=FLAGS.seed,
                          rank=FLAGS.task_index, comm=None, bf16_grads=FLAGS.bf16_grads,
-                         use_graph=FLAGS.use_graph and (sopt is None or not sopt.has_backup_workers))
+                         use_graph=FLAGS.use_graph and (sopt is None or not sopt.has_backup_workers),
+                         dtype=FLAGS.dtype)
     comm = None
     transport = None
     if device.type == "cuda" and sync and num_workers > 1 and not backup_ps:

@@ -147,6 +147,25 @@ def test_bench_two_ranks_one_gpu_over_ipc(cuda):
     assert r["phases_ms"]["allreduce"] > 0, r["phases_ms"]
 
 
+def test_bench_fp32_dtype(cuda):
+    r = _bench(["--steps", "20", "--warmup", "5", "--dtype", "fp32", "--min_warmup_ms", "50"])
+    assert r["dtype"] == "fp32" and r["config"]["grad_allreduce"] == "fp32" and r["value"] > 0
+
+
 def test_bench_forced_dp_world1_rccl(cuda):
     r = _bench(["--steps", "20", "--warmup", "5", "--force_dp", "1", "--min_warmup_ms", "50"])
     assert r["config"]["dp_transport"] == "rccl" and r["config"]["force_dp"] and r["config"]["hipgraph"]
+
+
+def test_dist_main_resnet18_two_workers_one_gpu(tmp_path):
+    """--model resnet18 through the same cluster roles: sync DP (bucketed all-reduce over IPC,
+    both workers on gpu:0), reference step lines, clean exit."""
+    from tensorflow_distributed_amd import launch
+
+    args = ["--num_gpus=1", "--model=resnet18", "--train_steps=3", "--batch_size=8", "--bucket_mb=2",
+            "--synthetic_data", "--data_dir=/nonexistent", f"--logdir={tmp_path}"]
+    r = launch.launch(1, 2, args, echo=False, timeout_s=300)
+    assert r["ok"], r["outputs"]
+    for w in ("worker:0", "worker:1"):
+        out = "".join(v for k, v in r["outputs"].items() if k.startswith(w + "#"))
+        assert "training step 3 done (global step: 3)" in out and "images/sec" in out, out
