@@ -184,11 +184,20 @@ class MnistEngine : public torch::CustomClassHolder {
   // one GPU + Adam: fc-region ApplyAdam fused into the fc backward (gradients never reach memory);
   // fork = that kernel on a side stream beside the conv backward
   void set_fc_adam(int64_t on, int64_t fork) { fc_adam_ = on != 0; fc_adam_fork_ = fork != 0; }
-  // make every rank's bf16 shadow whole again (after the last zero step, before eval/checkpoint)
+  // Make every rank's state whole again after ZeRO-1 steps (before eval / checkpoint / broadcast):
+  // each rank updated the fp32 master, m and v of its own fc1 shard only, so all four are
+  // all-gathered -- the bf16 shadow (what the forward reads) and the fp32 master + Adam slots (what
+  // params() / a checkpoint read).
   void sync_params() {
     if (!zero_) return;
     hipStream_t s = stream();
     ag_w(s);
+    const int64_t r = rank_in_comm();
+    for (at::Tensor* t : {&params_, &m_, &v_}) {
+      float* base = (float*)t->data_ptr() + OFF_WD1;
+      if (comm_) comm_->all_gather_raw(base + r * zshard_, base, (size_t)zshard_, ncclFloat32, s);
+      else ipc_->all_gather_raw(base, 4, zshard_, s);
+    }
   }
 
   // ---- compute precision ----

@@ -235,7 +235,7 @@ def _engine_zero_worker(rank, world, B, steps, zero):
             torch.cuda.current_stream().synchronize()
         eng.sync_params()
     torch.cuda.synchronize()
-    out = eng.params_bf16().float().cpu(), comm.error()
+    out = eng.params_bf16().float().cpu(), comm.error(), eng.params().cpu(), eng.adam_v().cpu()
     comm.close()
     return out
 
@@ -247,9 +247,12 @@ def test_engine_zero1_matches_replicated_dp(cuda, world):
     B, steps = 16, 3
     zr = run_ranks(_engine_zero_worker, world, B, steps, True, timeout=300)
     rp = run_ranks(_engine_zero_worker, world, B, steps, False, timeout=300)
-    assert all(e == 0 for _, e in zr + rp)
-    for p, _ in zr[1:]:
-        assert torch.equal(p, zr[0][0]), "ZeRO replicas diverged"
+    assert all(r[1] == 0 for r in zr + rp)
+    for r in zr[1:]:
+        assert torch.equal(r[0], zr[0][0]), "ZeRO replicas diverged"
+        # sync_params also gathered the fp32 master and the Adam moments of every shard
+        assert torch.equal(r[2], zr[0][2]) and torch.equal(r[3], zr[0][3])
+    assert torch.equal(zr[0][2].to(torch.bfloat16).float(), zr[0][0])
     d = (zr[0][0] - rp[0][0]).abs()
     # identical math up to fp32 summation order in the reduction -> at most a bf16 ulp here and there
     assert (d > 1e-2).float().mean().item() < 1e-3, d.max().item()
