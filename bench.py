@@ -58,6 +58,8 @@ def main(argv=None):
                     "the fc backward epilogues (the fc gradients never reach memory)")
     ap.add_argument("--fc_adam_fork", type=int, default=0, help="1: that fused fc backward+Adam kernel on a side "
                     "stream beside the conv backward")
+    ap.add_argument("--conv_unfused", type=int, default=0, help="1: conv1 and conv2 forward as two kernels "
+                    "(A/B of the fused conv1->conv2 kernel)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu", action="store_true", help="plumbing dry-run: fp32 PyTorch CPU runner + Gloo "
@@ -86,6 +88,7 @@ def main(argv=None):
     eng.set_fused_tail(a.fused_tail)
     eng.set_local_bf16_grads(a.local_bf16_grads)
     eng.set_fc_adam(a.fc_adam, a.fc_adam_fork)
+    eng.set_conv_unfused(a.conv_unfused)
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     mode = a.transport

@@ -86,6 +86,41 @@ __device__ __forceinline__ int data_row(const int* perm, const int64_t* step, in
   const int64_t s = *step;
   return perm[(int)((s * (int64_t)B + b) % (int64_t)n_data)];
 }
+// the batch row b of this step: the prefetched rows[b] when their tag matches the step (the tag, the
+// row and the step are three independent loads), else the step -> perm chain
+__device__ __forceinline__ int data_row(const MnistStepArgs& a, int b) {
+  if (!a.perm) return b;
+  if (a.rows) {
+    const int tag = a.rows[a.B], r = a.rows[b];
+    const int64_t s = *a.step;
+    if (tag == (int)s) return r;
+    return a.perm[(int)((s * (int64_t)a.B + b) % (int64_t)a.n_data)];
+  }
+  return data_row(a.perm, a.step, a.n_data, a.B, b);
+}
+// gather block b: the batch row b of step `next` into rows / xpre / ypre; block 0 also writes the
+// tag (visibility to the next kernel is the kernel boundary)
+__device__ __forceinline__ void gather_next(const MnistStepArgs& a, int64_t next, int b) {
+  const int row = a.perm[(int)((next * (int64_t)a.B + b) % (int64_t)a.n_data)];
+  const f32x4* src = reinterpret_cast<const f32x4*>(a.data + (size_t)row * 784);
+  f32x4* dst = reinterpret_cast<f32x4*>(a.xpre + (size_t)b * 784);
+  for (int i = threadIdx.x; i < 196; i += blockDim.x) dst[i] = src[i];
+  if (threadIdx.x == 0) {
+    a.rows[b] = row;
+    a.ypre[b] = a.labels[row];
+    if (b == 0) a.rows[a.B] = (int)next;
+  }
+}
+__device__ __forceinline__ int gather_blocks(const MnistStepArgs& a) { return (a.perm && a.xpre) ? a.B : 0; }
+// the prefetched label of batch row b (speculative load beside the tag and the step)
+__device__ __forceinline__ int batch_label(const MnistStepArgs& a, int b) {
+  if (a.perm && a.xpre) {
+    const int tag = a.rows[a.B], y = a.ypre[b];
+    const int64_t s = *a.step;
+    if (tag == (int)s) return y;
+  }
+  return a.labels[data_row(a, b)];
+}
 
 // ---------------- K1: conv1 + bias + relu + maxpool + argmax ----------------
 // Block = (image b, output-channel group cg of 8): the 28x28 fp32 image is staged once into a
@@ -96,7 +131,7 @@ __global__ __launch_bounds__(256) void conv1_pool_fwd(MnistStepArgs a) {
   __shared__ float img[32 * 32];
   __shared__ float w[KTAPS * 8 + 8];
   const int b = blockIdx.x >> 2, cg = blockIdx.x & 3, t = threadIdx.x;
-  const float* x = a.data + (size_t)data_row(a.perm, a.step, a.n_data, a.B, b) * 784;
+  const float* x = a.data + (size_t)data_row(a, b) * 784;
 #if TFD_C1_EARLY_X
   // the image load is issued before the first barrier, so its step -> perm -> row chain overlaps
   // the filter loads instead of starting after them
@@ -316,6 +351,221 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
   }
 }
 
+// ---------------- K1+K3+K2+K3 fused: conv1 -> pool -> conv2 -> pool per image, p1 in LDS ----------------
+// Block = (image b, conv2 output-channel half nh), 512 threads. conv2 needs all 32 conv1 channels
+// of the image, so each half recomputes conv1 (fp32 VALU, exactly the K1 kernel's math) straight
+// into the zero-bordered, channel-chunk-major LDS image that conv2_fwd_lds used to stage from
+// global memory; p1 / idx1 still go to global (half 0 only) for the backward. The conv2 weight
+// half's loads are issued FIRST and stay in flight behind the conv1 arithmetic; they are written
+// to LDS after it. One launch and one activation round trip less than conv1_pool_fwd +
+// conv2_fwd_lds. LDS: p1 image 27 KiB + W2 half 75 KiB + x / W1 staging 7.5 KiB.
+constexpr int C12_XOFF = C2L_FWD_SMEM;                       // fp32 [32][32] zero-bordered x image
+constexpr int C12_WOFF = C12_XOFF + 32 * 32 * 4;             // fp32 [25][32] W1 + [32] bias
+constexpr int C12_IOFF = C12_WOFF + (KTAPS * C1 + C1) * 4;   // uint8 [196][32] conv1 argmax
+constexpr int C12_SMEM = C12_IOFF + 196 * 32;                // 118,400 B
+static_assert(C12_IOFF % 16 == 0, "LDS carve alignment");
+#ifndef TFD_STAMP
+#define TFD_STAMP 0  // 1: thread 0 of every conv12 block records s_memtime at its phase boundaries
+#endif
+#define C12_STAMP(k)                                                                       \
+  do {                                                                                     \
+    if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+__global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
+  C12_STAMP(0);
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  bf16* img = (bf16*)smem_raw;                        // [4][18*24][8]  (conv2 input = pooled conv1)
+  bf16* wt = img + 4 * C2F_PLANE * 8;                 // [800][48]
+  float* xs = reinterpret_cast<float*>(smem_raw + C12_XOFF);
+  float* w1 = reinterpret_cast<float*>(smem_raw + C12_WOFF);
+  const int b = blockIdx.x >> 1, nh = blockIdx.x & 1, t = threadIdx.x;
+  // 1. wave specialisation of the loads (a wave's vmcnt is in-order, so a load issued behind the
+  //    W2 loads could not be consumed before them): waves 0-3 issue the conv2 weight half (12.5 x
+  //    16 B per lane, written to LDS only after conv1); waves 4-7 the W1 / bias and the x image
+  //    (prefetched row -> x) that conv1 needs first. Both overlap the LDS zeroing.
+  const uint16_t* wsrc = a.pbf + OFF_WC2 + nh * 32;
+  const int rot = TFD_WROT ? (int)((blockIdx.x * 1031u) % 3200u) : 0;
+  constexpr int NW = (3200 + 255) / 256;
+  uint4 vw[NW];
+  f32x4 xv = f32x4{0.f, 0.f, 0.f, 0.f}, w1v = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int u = t - 256;
+  if (t < 256) {
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const int i = (t + 256 * j + rot) % 3200;
+      vw[j] = (t + 256 * j < 3200) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 2) * 64 + (i & 3) * 8) : zero4();
+    }
+  } else {
+    if (u < (KTAPS * C1 + C1) / 4) w1v = reinterpret_cast<const f32x4*>(a.p32 + OFF_WC1)[u];
+    // the prefetched image, loaded speculatively beside its tag and the step
+    bool hit = false;
+    if (a.perm && a.xpre) {
+      if (u < 196) xv = reinterpret_cast<const f32x4*>(a.xpre + (size_t)b * 784)[u];
+      hit = a.rows[a.B] == (int)*a.step;
+    }
+    if (!hit) {
+      const float* x = a.data + (size_t)data_row(a, b) * 784;
+      if (u < 196) xv = reinterpret_cast<const f32x4*>(x)[u];
+    }
+  }
+  C12_STAMP(1);
+  // 2. zero the x image border and the p1 image (its border is conv2's SAME padding), then x, W1
+  for (int i = t; i < 32 * 32; i += 512) xs[i] = 0.f;
+  for (int i = t; i < 4 * C2F_PLANE; i += 512) reinterpret_cast<uint4*>(img)[i] = zero4();
+  __syncthreads();
+  if (t >= 256) {
+    if (u < (KTAPS * C1 + C1) / 4) reinterpret_cast<f32x4*>(w1)[u] = w1v;
+    if (u < 196) {
+      const int r = (4 * u) / 28, c = (4 * u) % 28;
+      float* d = xs + (r + 2) * 32 + c + 2;
+      d[0] = xv[0]; d[1] = xv[1]; d[2] = xv[2]; d[3] = xv[3];
+    }
+  }
+  __syncthreads();
+  C12_STAMP(2);
+#ifndef TFD_EXP_C12
+#define TFD_EXP_C12 0  // timing experiments only (wrong results): 1 skip conv1, 2 skip conv2's MFMA loop
+#endif
+  if (!(TFD_EXP_C12 & 1))
+  // 3. conv1 on the matrix core: implicit GEMM M = 784 pixels (pool-window-major, m = pp*4 + win),
+  //    N = 32 channels, K = 25 taps padded to 32 -> one v_mfma_f32_16x16x32_bf16 per (M-tile, N-tile);
+  //    each lane's 4 accumulator rows are one 2x2 window, so bias + relu + max + argmax happen in
+  //    registers. Operands: the x image and W1 rounded to bf16 (the bf16 engine's operand precision;
+  //    --dtype fp32 keeps conv1 exact). Wave w owns M-tiles w, w + 8, ... (<= 7): all of its A
+  //    fragments are gathered first, then the MFMAs, then the epilogues (no per-tile
+  //    LDS -> MFMA -> epilogue latency chain). Pooled values go to the conv2 LDS image, argmax bytes
+  //    to an LDS array; both are copied out to global with 16-B stores afterwards (half 0 only).
+  {
+    const int lane = t & 63, w = t >> 6, g = lane >> 4, col = lane & 15;
+    uint8_t* idx_l = reinterpret_cast<uint8_t*>(smem_raw + C12_IOFF);  // [196][32]
+    bf16x8 bw[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int k = 8 * g + jj;
+        bw[nt][jj] = (bf16)(k < KTAPS ? w1[k * C1 + nt * 16 + col] : 0.f);
+      }
+    const float bias0 = w1[KTAPS * C1 + col], bias1 = w1[KTAPS * C1 + 16 + col];
+    constexpr int MT = 7;  // ceil(49 / 8)
+    bf16x8 af[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int mt = w + 8 * i;
+      const int m = min(mt, 48) * 16 + col, pp = m >> 2, win = m & 3;
+      const int oh = 2 * (pp / 14) + (win >> 1), ow = 2 * (pp % 14) + (win & 1);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int k = 8 * g + jj, kh = k / 5, kw = k - 5 * (k / 5);
+        af[i][jj] = (bf16)(k < KTAPS ? xs[(oh + kh) * 32 + ow + kw] : 0.f);
+      }
+    }
+    f32x4 z[MT][2];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) z[i][nt] = mfma16x16x32(af[i], bw[nt], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int mt = w + 8 * i;
+      if (mt >= 49) break;
+      const int pq = mt * 4 + g, ph = pq / 14, pw = pq - ph * 14;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int n = nt * 16 + col;
+        const float bias = nt ? bias1 : bias0;
+        float mx = z[i][nt][0] + bias;
+        int am = 0;
+#pragma unroll
+        for (int r = 1; r < 4; ++r) {
+          const float zz = z[i][nt][r] + bias;
+          if (zz > mx) { mx = zz; am = r; }
+        }
+        reinterpret_cast<uint16_t*>(img)[((n >> 3) * C2F_PLANE + (ph + 2) * C2F_W + pw + 2) * 8 + (n & 7)] =
+            f2bf_bits(fmaxf(mx, 0.f));
+        idx_l[pq * 32 + n] = (uint8_t)am;
+      }
+    }
+  }
+  C12_STAMP(3);
+  // 4. the W2 half (landed during conv1) into LDS
+  if (t < 256) {
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const int i = (t + 256 * j + rot) % 3200;
+      if (t + 256 * j < 3200) *reinterpret_cast<uint4*>(wt + (i >> 2) * C2F_WLD + (i & 3) * 8) = vw[j];
+    }
+  }
+  __syncthreads();
+  if (nh == 0) {  // p1 / idx1 for the backward: 16-B stores from the LDS image and argmax array
+    const uint8_t* idx_l = reinterpret_cast<const uint8_t*>(smem_raw + C12_IOFF);
+    for (int i = t; i < 196 * 4; i += 512) {
+      const int pq = i >> 2, cg = i & 3, ph = pq / 14, pw = pq - ph * 14;
+      *reinterpret_cast<uint4*>(a.p1 + ((size_t)b * 196 + pq) * 32 + cg * 8) =
+          *reinterpret_cast<const uint4*>(img + (cg * C2F_PLANE + (ph + 2) * C2F_W + pw + 2) * 8);
+    }
+    for (int i = t; i < 196 * 2; i += 512)
+      reinterpret_cast<uint4*>(a.idx1 + (size_t)b * 196 * 32)[i] = reinterpret_cast<const uint4*>(idx_l)[i];
+  }
+  C12_STAMP(4);
+  // 5. conv2 implicit GEMM + bias + relu + pool + argmax (conv2_fwd_lds's main loop and epilogue)
+  const int lane = t & 63, w = t >> 6, g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  const int nmt = (w + 8 < 13) ? 2 : 1;
+  int base[2];
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int m = (w + 8 * j) * 16 + (lane & 15);
+    int px = 0;
+    if (m < 196) {
+      const int pp = m >> 2, win = m & 3;
+      px = (2 * (pp / 7) + (win >> 1)) * C2F_W + 2 * (pp % 7) + (win & 1);
+    }
+    base[j] = (g * C2F_PLANE + px) * 8;
+  }
+  const bf16* wcol = wt + (8 * g + q) * C2F_WLD + 4 * p4;
+#pragma unroll
+  for (int kh = 0; kh < ((TFD_EXP_C12 & 2) ? 0 : 5); ++kh) {
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) {
+      const int tap = kh * 5 + kw, toff = (kh * C2F_W + kw) * 8;
+      const bf16* wr = wcol + tap * 32 * C2F_WLD;
+      const bf16x8 b0 = frag_tr16(wr, wr + 4 * C2F_WLD);
+      const bf16x8 b1 = frag_tr16(wr + 16, wr + 16 + 4 * C2F_WLD);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (j < nmt) {
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + base[j] + toff);
+          acc[j][0] = mfma16x16x32(af, b0, acc[j][0]);
+          acc[j][1] = mfma16x16x32(af, b1, acc[j][1]);
+        }
+    }
+  }
+  C12_STAMP(5);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n = nh * 32 + nt * 16 + (lane & 15);
+    const float bb = a.p32[OFF_BC2 + n];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int m4 = (w + 8 * j) * 16 + 4 * g;
+      if (j >= nmt || m4 >= 196) continue;
+      float mx = acc[j][nt][0] + bb;
+      int am = 0;
+#pragma unroll
+      for (int r = 1; r < 4; ++r) {
+        const float z = acc[j][nt][r] + bb;
+        if (z > mx) { mx = z; am = r; }
+      }
+      const size_t o = (size_t)b * FEAT + (m4 >> 2) * 64 + n;
+      a.p2[o] = f2bf_bits(fmaxf(mx, 0.f));
+      a.idx2[o] = (uint8_t)am;
+    }
+  }
+  C12_STAMP(6);
+}
+
 // ---------------- K3: fc1 forward, split-K slabs ----------------
 struct SlabEpi {
   float* __restrict__ out;
@@ -360,7 +610,7 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   const int n0 = 4 * t;
   if (a.t_out && row == 0 && t == 0) *a.t_out = *a.step + 1;
   // the label's dependent chain (step -> perm -> label) starts first, hidden behind the fc1 math
-  const int lbl = a.labels[data_row(a.perm, a.step, a.n_data, a.B, row)];
+  const int lbl = batch_label(a, row);
   f32x4 h = *reinterpret_cast<const f32x4*>(a.p32 + OFF_BD1 + n0);
   {  // all split-K slab loads in flight together (compile-time count: no per-load branches)
     f32x4 p[FC1_SPLITS];
@@ -820,7 +1070,7 @@ __global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) {
   const int rot = TFD_WROT ? (int)((blockIdx.x * 1031u) % 6400u) : 0;  // per-block start: spread L2 channels
 #if TFD_C1_EARLY_X
   // the conv1-wgrad tail's step -> perm chain resolved now, behind the staging loads
-  const int xrow_idx = data_row(a.perm, a.step, a.n_data, a.B, b);
+  const int xrow_idx = data_row(a, b);
 #endif
   {
     constexpr int CI = 8 * C2D_PLANE, NI = (CI + 511) / 512;  // 1792 chunks -> 4 per thread
@@ -924,7 +1174,7 @@ __global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) {
 #if TFD_C1_EARLY_X
     const float* xrow = a.data + (size_t)xrow_idx * 784;
 #else
-    const float* xrow = a.data + (size_t)data_row(a.perm, a.step, a.n_data, a.B, b) * 784;
+    const float* xrow = a.data + (size_t)data_row(a, b) * 784;
 #endif
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1129,7 +1379,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad(MnistStepArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t is[C1W_HALF * 32];
   __shared__ float part[8][26 * 32 + 1];
   const int b = blockIdx.x >> 1, half = blockIdx.x & 1, t = threadIdx.x, c = t & 31, sub = t >> 5;
-  const float* x = a.data + (size_t)data_row(a.perm, a.step, a.n_data, a.B, b) * 784;
+  const float* x = a.data + (size_t)data_row(a, b) * 784;
   for (int i = t; i < 32 * 32; i += 256) img[i] = 0.f;
   const size_t base = ((size_t)b * 196 + half * C1W_HALF) * 32;
   for (int i = t; i < C1W_HALF * 32 / 8; i += 256)   // 392 x 16 B of bf16 grads
@@ -1199,6 +1449,7 @@ __device__ __forceinline__ void reduce_chunk(const float* __restrict__ slab, int
 }
 constexpr int RED2_BLOCKS = (801 * 64 + 63) / 64;  // 801 blocks x 64 outputs (4 phases over the B/2 slabs)
 constexpr int RED1_BLOCKS = (832 + 15) / 16;       // 52 blocks x 16 outputs (16 phases over 2B slabs)
+__global__ __launch_bounds__(256) void gather_next_kernel(MnistStepArgs a) { gather_next(a, *a.step + 1, blockIdx.x); }
 __global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a) {
   __shared__ float red[256];
   const int id = blockIdx.x;
@@ -1264,14 +1515,19 @@ __device__ __forceinline__ f32x4 slab_sum(const f32x4* __restrict__ s4, int64_t 
   return acc;
 }
 __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, MnistAdamArgs o) {
-  // gridDim.x == MAD_CONV: the fc region was updated by fc1_bwd_adam; the last conv2 block bumps
-  // the step instead
-  if (gridDim.x == MAD_CONV && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *o.step += 1;
+  const int gb = gather_blocks(a);
+  if ((int)blockIdx.x < gb) {  // the next step's batch; t = the step started next
+    gather_next(a, *o.t, blockIdx.x);
+    return;
+  }
+  const int grid = (int)gridDim.x - gb;
+  // grid == MAD_CONV: the fc region was updated by fc1_bwd_adam; the last conv2 block bumps the step
+  if (grid == MAD_CONV && (int)blockIdx.x - gb == grid - 1 && threadIdx.x == 0) *o.step += 1;
   const int64_t t = *o.t;
   const float b1p = powf(o.beta1, (float)t), b2p = powf(o.beta2, (float)t);
   const float lr_t = o.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float c1 = 1.f - o.beta1, c2 = 1.f - o.beta2;
-  const int bid = blockIdx.x, tid = threadIdx.x;
+  const int bid = (int)blockIdx.x - gb, tid = threadIdx.x;
   if (bid < MAD_CONV) {
     __shared__ f32x4 red[MAD_NT];
     const bool one = bid < MAD_C1BLK;
@@ -1386,8 +1642,18 @@ void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s) {
   mnist_forward_fc(a, train, s);
 }
 
+#ifndef TFD_CONV12_FUSED  // 1: conv1 fused into the conv2 kernel (p1 stays in LDS)
+#define TFD_CONV12_FUSED 1
+#endif
 void mnist_forward_conv(const MnistStepArgs& a, hipStream_t s) {
   const int B = a.B;
+#if TFD_CONV12_FUSED && TFD_CONV2_LDS
+  if (!a.conv_unfused) {
+    set_smem<conv12_fwd_lds>(C12_SMEM);
+    conv12_fwd_lds<<<2 * B, 512, C12_SMEM, s>>>(a);
+    return;
+  }
+#endif
   conv1_pool_fwd<<<4 * B, 256, 0, s>>>(a);
 #if TFD_CONV2_LDS
   set_smem<conv2_fwd_lds>(C2L_FWD_SMEM);
@@ -1458,11 +1724,14 @@ void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux, hi
 }
 
 void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s) {
+  // the next step's batch first (this kernel bumps the step; the gather reads it unbumped)
+  if (a.step_bump && a.perm && a.xpre) gather_next_kernel<<<a.B, 256, 0, s>>>(a);
   reduce_conv_grads<<<RED2_BLOCKS + RED1_BLOCKS, 256, 0, s>>>(a);
 }
 
 void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region) {
-  mnist_adam_kernel<<<fc_region ? MAD_GRID : MAD_CONV, MAD_NT, 0, s>>>(a, o);
+  const int gb = (a.perm && a.xpre) ? a.B : 0;
+  mnist_adam_kernel<<<gb + (fc_region ? MAD_GRID : MAD_CONV), MAD_NT, 0, s>>>(a, o);
 }
 
 void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s) {

@@ -63,6 +63,9 @@ class MnistEngine : public torch::CustomClassHolder {
     wg2_slab_ = at::empty({wg2_splits_, 801, C2}, f32);
     wg1_slab_ = at::empty({2 * B_, 832}, f32);
     xbuf_ = at::zeros({B_, 784}, f32);
+    rows_ = at::full({B_ + 1}, -1, i32);  // prefetched batch rows + step tag (MnistStepArgs::rows)
+    xpre_ = at::zeros({B_, 784}, f32);    // prefetched next batch (MnistStepArgs::xpre / ypre)
+    ypre_ = at::zeros({B_}, i32);
     ybuf_ = at::zeros({B_}, i32);
     HIP_OK(hipSetDevice((int)device));
     HIP_OK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
@@ -122,7 +125,12 @@ class MnistEngine : public torch::CustomClassHolder {
     data_ = data.contiguous();
     labels_ = labels.contiguous();
     perm_ = perm.contiguous();
+    invalidate_prefetch();
   }
+  // the permutation changed (epoch reshuffle): drop the rows prefetched from the old one
+  void invalidate_prefetch() { rows_.narrow(0, B_, 1).fill_(-1); }
+  // timing-stamp builds (TFD_STAMP): kernels write per-block phase clocks here
+  void set_debug_buffer(at::Tensor t) { dbg_ = t; }
   // mode 0 = feed buffers (feed_x/feed_y filled by the host each step), 1 = device dataset + perm
   void set_input_mode(int64_t mode) {
     TORCH_CHECK(mode == 0 || (mode == 1 && data_.defined()), "set_dataset first");
@@ -184,6 +192,8 @@ class MnistEngine : public torch::CustomClassHolder {
   // one GPU + Adam: fc-region ApplyAdam fused into the fc backward (gradients never reach memory);
   // fork = that kernel on a side stream beside the conv backward
   void set_fc_adam(int64_t on, int64_t fork) { fc_adam_ = on != 0; fc_adam_fork_ = fork != 0; }
+  // 0 (default): conv1 fused into the conv2 forward kernel; 1: the two separate kernels (A/B)
+  void set_conv_unfused(int64_t on) { conv_unfused_ = on != 0; }
   // Make every rank's state whole again after ZeRO-1 steps (before eval / checkpoint / broadcast):
   // each rank updated the fp32 master, m and v of its own fc1 shard only, so all four are
   // all-gathered -- the bf16 shadow (what the forward reads) and the fp32 master + Adam slots (what
@@ -720,6 +730,11 @@ class MnistEngine : public torch::CustomClassHolder {
     a.keep_prob = (float)keep_prob_;
     a.seed = seed_;
     a.rank = rank_;
+    a.conv_unfused = conv_unfused_ ? 1 : 0;
+    a.rows = input_mode_ == 1 ? (int*)rows_.data_ptr() : nullptr;
+    a.xpre = input_mode_ == 1 ? (float*)xpre_.data_ptr() : nullptr;
+    a.ypre = input_mode_ == 1 ? (int*)ypre_.data_ptr() : nullptr;
+    a.dbg = dbg_.defined() ? (int64_t*)dbg_.data_ptr() : nullptr;
     return a;
   }
 
@@ -738,7 +753,7 @@ class MnistEngine : public torch::CustomClassHolder {
   at::Tensor params_, pbf_, grad_, m_, v_, gbf_, step_, tnext_;
   at::Tensor p1_, idx1_, p2_, idx2_, fc1_slab_, hd_, dh_, dlogits_, loss_row_, correct_row_, dz2_, dp1m_, wg2_slab_,
       wg1_slab_, xbuf_, ybuf_;
-  at::Tensor data_, labels_, perm_;
+  at::Tensor data_, labels_, perm_, rows_, xpre_, ypre_, dbg_;
   at::Tensor f1_, f2_, fhd_, fdh_, fdz2_, fdp1m_, fslab_, fwg2_;  // fp32-mode activations / slabs
   bool fp32_ = false;
   hipStream_t comm_stream_ = nullptr;
@@ -754,7 +769,8 @@ class MnistEngine : public torch::CustomClassHolder {
   // one GPU + Adam: the optimizer kernel also reduces the conv gradient slabs and bumps the step
   bool fuse_tail_ = true;
   bool local_bf16_grads_ = false;
-  bool fc_adam_ = false, fc_adam_fork_ = false;  // measured slower (docs/DESIGN.md)
+  bool fc_adam_ = false, fc_adam_fork_ = false;
+  bool conv_unfused_ = false;  // measured slower (docs/DESIGN.md)
   std::map<std::string, hipGraphExec_t> graphs_;
   hipEvent_t pev_[P_N] = {};
   bool timing_ = false, timed_ = false, timed_dp_ = false;
@@ -791,6 +807,8 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("feed_y", &MnistEngine::feed_y)
       .def("batch", &MnistEngine::batch)
       .def("set_dataset", &MnistEngine::set_dataset)
+      .def("invalidate_prefetch", &MnistEngine::invalidate_prefetch)
+      .def("set_debug_buffer", &MnistEngine::set_debug_buffer)
       .def("set_input_mode", &MnistEngine::set_input_mode)
       .def("set_keep_prob", &MnistEngine::set_keep_prob)
       .def("sync_shadow", &MnistEngine::sync_shadow)
@@ -805,6 +823,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_fused_tail", &MnistEngine::set_fused_tail)
       .def("set_local_bf16_grads", &MnistEngine::set_local_bf16_grads)
       .def("set_fc_adam", &MnistEngine::set_fc_adam)
+      .def("set_conv_unfused", &MnistEngine::set_conv_unfused)
       .def("set_dtype", &MnistEngine::set_dtype)
       .def("dtype", &MnistEngine::dtype)
       .def("set_phase_timing", &MnistEngine::set_phase_timing)

@@ -43,6 +43,17 @@ struct MnistStepArgs {
   int fc1_splits, wg2_splits;
   float keep_prob;
   uint32_t seed, rank;
+  int conv_unfused;            // 1: conv1 and conv2 forward as two kernels (A/B; default: one fused kernel)
+  // Next-batch prefetch (device dataset mode): the kernel that bumps the step also gathers the NEXT
+  // step's batch -- rows[b] = perm[...], xpre[b] = data[rows[b]] ([B][784] fp32), ypre[b] = its label
+  // -- and tags it with that step in rows[B]. Consumers load the prefetched value speculatively
+  // beside the tag and the step and fall back to the step -> perm -> row chain on a mismatch, so the
+  // forward starts with one memory round trip to an L2-resident buffer instead of three dependent
+  // loads ending in a random 3 KB row of a 172 MB array.
+  int* rows;
+  float* xpre;
+  int* ypre;
+  int64_t* dbg;                // timing-stamp builds only (TFD_STAMP): per-block phase clocks
 };
 
 int mnist_fc1_splits(int B);

@@ -1,0 +1,40 @@
+"""Per-phase clocks of the conv12 kernel from a TFD_STAMP build (TFD_NATIVE_LIB=..._C_stamp.so):
+median over blocks of the s_memtime deltas between consecutive stamps, after warm replays."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from tensorflow_distributed_amd import _native  # noqa: E402
+from tensorflow_distributed_amd.models import mnist_cnn as M  # noqa: E402
+
+_native.require()
+dev = torch.device("cuda", 0)
+B = 128
+eng = torch.classes.tfd.MnistEngine(B, 0, 0.75, 1, 0)
+eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+dbg = torch.zeros(2 * B * 8, dtype=torch.int64, device=dev)
+eng.set_debug_buffer(dbg)
+s = torch.cuda.Stream()
+with torch.cuda.stream(s):
+    data = torch.rand(55000, 784, device=dev)
+    labels = torch.randint(0, 10, (55000,), device=dev, dtype=torch.int32)
+    perm = torch.randperm(55000, device=dev).to(torch.int32)
+    eng.params().copy_(M.flat_from_dict(M.init_params(1)).to(dev))
+    eng.sync_shadow()
+    eng.set_dataset(data, labels, perm)
+    eng.set_input_mode(1)
+    eng.train_step()
+    eng.capture_train_steps("g", 20)
+    eng.replay("g", 50)
+torch.cuda.synchronize()
+d = dbg.view(-1, 8).cpu()
+names = ["issue loads", "zero+barrier", "x/W1 stage+barrier", "conv1", "W2 store+copyout+barrier", "conv2 loop", "epilogue"]
+base = d[:, 0].min()
+print("block span (cycles): median", (d[:, 6] - d[:, 0]).median().item(), "max", (d[:, 6] - d[:, 0]).max().item(),
+      "start spread", (d[:, 0] - base).max().item())
+for k in range(6):
+    dd = d[:, k + 1] - d[:, k]
+    print(f"{names[k]:28s} median {dd.median().item():8d}  p90 {dd.float().quantile(0.9).item():8.0f}")

@@ -109,13 +109,16 @@ def maxpool_same_nhwc(x: torch.Tensor, k: int = 2) -> torch.Tensor:
 
 
 def conv_net(x: torch.Tensor, p: Dict[str, torch.Tensor], keep_prob: float = 1.0,
-             dropout_mask: Optional[torch.Tensor] = None, emulate_bf16: bool = False) -> torch.Tensor:
+             dropout_mask: Optional[torch.Tensor] = None, emulate_bf16: bool = False,
+             bf16_conv1: bool = True) -> torch.Tensor:
     """Reference forward (mnist_python_m.py:104-128). ``dropout_mask`` (0/1, [B,1024]) overrides
     random dropout so the oracle can replay the native kernel's Philox mask. ``emulate_bf16``
-    rounds at exactly the points where the native kernels store/consume bf16."""
+    rounds at exactly the points where the native bf16 kernels store/consume bf16 (``bf16_conv1``:
+    conv1's operands too -- the fused conv1->conv2 kernel runs conv1 on the bf16 matrix core)."""
     r = (lambda t: t.to(torch.bfloat16).to(torch.float32)) if emulate_bf16 else (lambda t: t)
+    r1 = r if bf16_conv1 else (lambda t: t)
     x = x.reshape(-1, IMG, IMG, 1)
-    h = torch.relu(conv2d_same_nhwc(x, p["wc1"], p["bc1"]))
+    h = torch.relu(conv2d_same_nhwc(r1(x), r1(p["wc1"]), p["bc1"]))
     h = r(maxpool_same_nhwc(h, 2))
     h = torch.relu(conv2d_same_nhwc(h, r(p["wc2"]), p["bc2"]))
     h = r(maxpool_same_nhwc(h, 2))

@@ -285,6 +285,7 @@ class NativeMnistRunner(MnistRunnerBase):
             p = torch.randperm(n, generator=self._perm_gen).to(torch.int32)
             with torch.cuda.stream(self.stream):
                 self._dev_perm.copy_(p.to(self.device))
+                self.eng.invalidate_prefetch()  # rows prefetched from the old permutation
 
     # ---- state ----
     def params(self) -> torch.Tensor:

@@ -270,3 +270,70 @@ def test_phase_timing_events_inside_graph(cuda):
         assert min(fwd, bfc, bconv, opt) > 0 and ar == 0 and step > 0, ph
         assert abs(fwd + bfc + bconv + opt - step) < 1e-3 * max(step, 1), ph
         assert step < 5.0, ph  # ms
+
+
+def test_fused_conv12_forward_matches_oracle_and_two_kernel_path(cuda):
+    """conv1 fused into the conv2 kernel (bf16 MFMA, p1 computed into LDS) and the two-kernel path
+    (fp32 VALU conv1) each match the oracle that rounds their conv1 operands the same way."""
+    B = 128
+    params = {k: v * 0.05 for k, v in M.init_params(21).items()}
+    x = torch.rand(B, 784)
+    y = torch.randint(0, 10, (B,), dtype=torch.int32)
+    s = torch.cuda.Stream()
+    for unfused in (0, 1):
+        with torch.cuda.stream(s):
+            e = _engine(B, cuda, keep=1.0)
+            e.set_conv_unfused(unfused)
+            e.params().copy_(M.flat_from_dict(params).to(cuda))
+            e.sync_shadow()
+            e.feed_x().copy_(x.to(cuda))
+            e.feed_y().copy_(y.to(cuda))
+            e.forward(True)
+            e.backward_a()
+            e.backward_b()
+        torch.cuda.synchronize()
+        r = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
+        x4 = x.reshape(-1, 28, 28, 1)
+        xin, w1 = (x4, params["wc1"]) if unfused else (r(x4), r(params["wc1"]))
+        p1 = r(M.maxpool_same_nhwc(torch.relu(M.conv2d_same_nhwc(xin, w1, params["bc1"])), 2))
+        got = e.pool1().float().cpu()
+        assert _relerr(got, p1) < 4e-3, (unfused, _relerr(got, p1))
+        p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+        logits = M.conv_net(x, p, 1.0, emulate_bf16=True, bf16_conv1=not unfused)
+        torch.nn.functional.cross_entropy(logits, y.long()).backward()
+        g = M.dict_from_flat(e.grads().cpu())
+        for k in p:
+            assert _relerr(g[k], p[k].grad) < 3e-2, (unfused, k, _relerr(g[k], p[k].grad))
+
+
+def test_device_dataset_rows_equal_host_gathered_batches(cuda):
+    """Dataset mode (batch rows perm[(step*B + b) % n], prefetched for the next step by the kernel
+    that bumps the step) == feeding the same host-gathered batches, bit for bit, across an epoch
+    boundary and an invalidated prefetch (new permutation)."""
+    B, n, steps = 64, 200, 7  # 200 / 64: wraps around the dataset
+    g = torch.Generator(device=cuda).manual_seed(5)
+    data = torch.rand(n, 784, device=cuda, generator=g)
+    labels = torch.randint(0, 10, (n,), device=cuda, generator=g, dtype=torch.int32)
+    perm = torch.randperm(n, device=cuda, generator=g).to(torch.int32)
+    params = M.flat_from_dict(M.init_params(2)).to(cuda) * 0.05
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        a, b = _engine(B, cuda, keep=0.75), _engine(B, cuda, keep=0.75)
+        for e in (a, b):
+            e.set_adam(0.01, 0.9, 0.999, 1e-8)
+            e.params().copy_(params)
+            e.sync_shadow()
+        a.set_dataset(data, labels, perm)
+        a.set_input_mode(1)
+        for i in range(steps):
+            if i == 4:  # reshuffle mid-run: the prefetched rows must be dropped
+                perm.copy_(torch.randperm(n, device=cuda, generator=g).to(torch.int32))
+                a.invalidate_prefetch()
+            a.train_step()
+            idx = perm[(torch.arange(B, device=cuda) + i * B) % n].long()
+            b.feed_x().copy_(data[idx])
+            b.feed_y().copy_(labels[idx])
+            b.train_step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.params(), b.params())
+    assert torch.equal(a.loss_rows(), b.loss_rows())

@@ -109,7 +109,7 @@ def test_cpu_training_learns():
     r.load_flat(M.flat_from_dict(M.init_params(0)), {}, 0)
     x0, y0 = ds.images[:512], ds.labels[:512]
     _, c0 = r.evaluate(x0, y0)
-    for _ in range(25):
+    for _ in range(60):  # calibrated (MNIST-difficulty) synthetic data: ~75 % after 60 steps
         r.train_step(*ds.next_batch(64))
     _, c1 = r.evaluate(x0, y0)
     assert c1 > c0 + 100 and c1 / 512 > 0.5, (c0, c1)
