@@ -58,6 +58,8 @@ def main(argv=None):
                     "the fc backward epilogues (the fc gradients never reach memory)")
     ap.add_argument("--fc_adam_fork", type=int, default=0, help="1: that fused fc backward+Adam kernel on a side "
                     "stream beside the conv backward")
+    ap.add_argument("--fc_split", type=int, default=0, help="1: on one GPU, fc dW + the fc-region Adam on a "
+                    "second stream beside dX and the conv backward")
     ap.add_argument("--conv_unfused", type=int, default=0, help="1: conv1 and conv2 forward as two kernels "
                     "(A/B of the fused conv1->conv2 kernel)")
     ap.add_argument("--lr", type=float, default=0.01)
@@ -89,6 +91,7 @@ def main(argv=None):
     eng.set_local_bf16_grads(a.local_bf16_grads)
     eng.set_fc_adam(a.fc_adam, a.fc_adam_fork)
     eng.set_conv_unfused(a.conv_unfused)
+    eng.set_fc_split(a.fc_split)
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     mode = a.transport

@@ -605,7 +605,12 @@ __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
 
 // ---------------- K4-K9 head: reduce slabs, bias, relu, dropout, FC10, softmax-xent, bwd ----------
 // One 256-thread block per batch row; thread t owns hidden units 4t..4t+3.
+#define HEAD_STAMP(k)                                                                                    \
+  do {                                                                                                   \
+    if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[(2 * a.B + blockIdx.x) * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
+  } while (0)
 __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
+  HEAD_STAMP(0);
   const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n0 = 4 * t;
   if (a.t_out && row == 0 && t == 0) *a.t_out = *a.step + 1;
@@ -619,6 +624,7 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
 #pragma unroll
     for (int s = 0; s < FC1_SPLITS; ++s) h += p[s];
   }
+  HEAD_STAMP(1);
   float hd[4], scale[4];
   const float kp = train ? a.keep_prob : 1.0f;
   if (kp < 1.0f) {
@@ -644,6 +650,7 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
 #pragma unroll
     for (int c = 0; c < NCLS; ++c) lp[c] = fmaf(hd[j], wr[c], lp[c]);
   }
+  HEAD_STAMP(2);
   __shared__ float red[4][NCLS];
 #pragma unroll
   for (int c = 0; c < NCLS; ++c) {
@@ -663,6 +670,7 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
 #pragma unroll
   for (int c = 0; c < NCLS; ++c) se += __expf(logit[c] - mx);
   const float lse = mx + __logf(se);
+  HEAD_STAMP(3);
   if (t == 0) {
     a.loss_row[row] = lse - logit[lbl];
     a.correct_row[row] = (am == lbl) ? 1.f : 0.f;
@@ -689,6 +697,7 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   dhw[0] = pack_bf2(dhv[0], dhv[1]); dhw[1] = pack_bf2(dhv[2], dhv[3]);
   *reinterpret_cast<uint2*>(a.hd + (size_t)row * HID + n0) = make_uint2(hdw[0], hdw[1]);
   *reinterpret_cast<uint2*>(a.dh + (size_t)row * HID + n0) = make_uint2(dhw[0], dhw[1]);
+  HEAD_STAMP(4);
 }
 
 // ---------------- K8 output layer dW/db: [1025][10] = [Hd;1]^T dlogits ----------------
@@ -1515,19 +1524,19 @@ __device__ __forceinline__ f32x4 slab_sum(const f32x4* __restrict__ s4, int64_t 
   return acc;
 }
 __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, MnistAdamArgs o) {
-  const int gb = gather_blocks(a);
+  const int gb = o.fc_only ? 0 : gather_blocks(a);
   if ((int)blockIdx.x < gb) {  // the next step's batch; t = the step started next
     gather_next(a, *o.t, blockIdx.x);
     return;
   }
   const int grid = (int)gridDim.x - gb;
   // grid == MAD_CONV: the fc region was updated by fc1_bwd_adam; the last conv2 block bumps the step
-  if (grid == MAD_CONV && (int)blockIdx.x - gb == grid - 1 && threadIdx.x == 0) *o.step += 1;
+  if (!o.fc_only && grid == MAD_CONV && (int)blockIdx.x - gb == grid - 1 && threadIdx.x == 0) *o.step += 1;
   const int64_t t = *o.t;
   const float b1p = powf(o.beta1, (float)t), b2p = powf(o.beta2, (float)t);
   const float lr_t = o.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float c1 = 1.f - o.beta1, c2 = 1.f - o.beta2;
-  const int bid = (int)blockIdx.x - gb, tid = threadIdx.x;
+  const int bid = (int)blockIdx.x - gb + (o.fc_only ? MAD_CONV : 0), tid = threadIdx.x;
   if (bid < MAD_CONV) {
     __shared__ f32x4 red[MAD_NT];
     const bool one = bid < MAD_C1BLK;
@@ -1613,7 +1622,7 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
     } else {
       for (int64_t i = i0; i < TOTAL / 4; i += STRIDE) adam4(o, i, reinterpret_cast<const f32x4*>(a.grad)[i], lr_t, c1, c2);
     }
-    if (bid == MAD_GRID - 1 && tid == 0) *o.step += 1;  // see MnistAdamArgs
+    if (!o.fc_only && bid == MAD_GRID - 1 && tid == 0) *o.step += 1;  // see MnistAdamArgs
   }
 }
 
@@ -1732,6 +1741,11 @@ void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s) {
 void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region) {
   const int gb = (a.perm && a.xpre) ? a.B : 0;
   mnist_adam_kernel<<<gb + (fc_region ? MAD_GRID : MAD_CONV), MAD_NT, 0, s>>>(a, o);
+}
+
+void mnist_adam_fc(const MnistStepArgs& a, MnistAdamArgs o, hipStream_t s) {
+  o.fc_only = 1;
+  mnist_adam_kernel<<<MAD_FC_BLOCKS, MAD_NT, 0, s>>>(a, o);
 }
 
 void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s) {

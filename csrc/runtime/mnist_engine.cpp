@@ -192,6 +192,8 @@ class MnistEngine : public torch::CustomClassHolder {
   // one GPU + Adam: fc-region ApplyAdam fused into the fc backward (gradients never reach memory);
   // fork = that kernel on a side stream beside the conv backward
   void set_fc_adam(int64_t on, int64_t fork) { fc_adam_ = on != 0; fc_adam_fork_ = fork != 0; }
+  // one GPU: fc dW + fc Adam on the optimizer stream beside dX + the conv backward
+  void set_fc_split(int64_t on) { fc_split_ = on != 0; }
   // 0 (default): conv1 fused into the conv2 forward kernel; 1: the two separate kernels (A/B)
   void set_conv_unfused(int64_t on) { conv_unfused_ = on != 0; }
   // Make every rank's state whole again after ZeRO-1 steps (before eval / checkpoint / broadcast):
@@ -360,6 +362,30 @@ class MnistEngine : public torch::CustomClassHolder {
         HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
       }
       mark(P_BCONV, s);
+      mnist_adam_fused(a, o, s, false);
+      mark(P_OPT, s);
+      return;
+    }
+    if (fused && fc_split_) {
+      // fc dW + output-layer grads and then the fc-region Adam on the optimizer stream, beside the
+      // dX GEMM and the conv backward on the main stream (the fc Adam waits for dX, which reads the
+      // old fc1 weights); the conv-region Adam + slab reduce + step bump end the step after the join
+      a.gbf_a = (uint16_t*)gbf_.data_ptr();
+      o.gbf = (const uint16_t*)gbf_.data_ptr();
+      mnist_forward(a, true, s);
+      mark(P_FWD, s);
+      HIP_OK(hipEventRecord(ev_a_, s));
+      HIP_OK(hipStreamWaitEvent(opt_stream_, ev_a_, 0));
+      mnist_backward_a(a, opt_stream_, 1);
+      mnist_backward_a(a, s, 2);
+      mark(P_BFC, s);
+      HIP_OK(hipEventRecord(ev_b_, s));
+      HIP_OK(hipStreamWaitEvent(opt_stream_, ev_b_, 0));
+      mnist_adam_fc(a, o, opt_stream_);
+      mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
+      mark(P_BCONV, s);
+      HIP_OK(hipEventRecord(ev_opt_a_, opt_stream_));
+      HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
       mnist_adam_fused(a, o, s, false);
       mark(P_OPT, s);
       return;
@@ -769,7 +795,7 @@ class MnistEngine : public torch::CustomClassHolder {
   // one GPU + Adam: the optimizer kernel also reduces the conv gradient slabs and bumps the step
   bool fuse_tail_ = true;
   bool local_bf16_grads_ = false;
-  bool fc_adam_ = false, fc_adam_fork_ = false;
+  bool fc_adam_ = false, fc_adam_fork_ = false, fc_split_ = false;
   bool conv_unfused_ = false;  // measured slower (docs/DESIGN.md)
   std::map<std::string, hipGraphExec_t> graphs_;
   hipEvent_t pev_[P_N] = {};
@@ -820,6 +846,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_force_dp", &MnistEngine::set_force_dp)
       .def("dp", &MnistEngine::dp)
       .def("set_conv_fork", &MnistEngine::set_conv_fork)
+      .def("set_fc_split", &MnistEngine::set_fc_split)
       .def("set_fused_tail", &MnistEngine::set_fused_tail)
       .def("set_local_bf16_grads", &MnistEngine::set_local_bf16_grads)
       .def("set_fc_adam", &MnistEngine::set_fc_adam)

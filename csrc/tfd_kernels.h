@@ -80,9 +80,13 @@ struct MnistAdamArgs {
   const int64_t* t;
   int64_t* step;
   const uint16_t* gbf;  // if non-null: the fc-region (bucket A) gradients are bf16 here (gbf_a)
+  int fc_only;          // 1: the fc region only (no gather, no step bump; see mnist_adam_fc)
 };
 // fc_region = false: the conv region only (the fc region was updated by mnist_backward_a_adam)
 void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region = true);
+// The fc region alone (1024 grid-stride blocks), e.g. on a side stream beside the conv backward;
+// mnist_adam_fused(..., fc_region = false) then finishes the step.
+void mnist_adam_fc(const MnistStepArgs& a, MnistAdamArgs o, hipStream_t s);
 // One GPU: fc1 dW and the output-layer gradients with ApplyAdam fused into their epilogues (the fc
 // gradients never reach memory; t = global_step + 1). Launch after the dX GEMM (part 2).
 void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s);

@@ -15,7 +15,7 @@ dev = torch.device("cuda", 0)
 B = 128
 eng = torch.classes.tfd.MnistEngine(B, 0, 0.75, 1, 0)
 eng.set_adam(0.01, 0.9, 0.999, 1e-8)
-dbg = torch.zeros(2 * B * 8, dtype=torch.int64, device=dev)
+dbg = torch.zeros(3 * B * 8, dtype=torch.int64, device=dev)
 eng.set_debug_buffer(dbg)
 s = torch.cuda.Stream()
 with torch.cuda.stream(s):
@@ -31,6 +31,8 @@ with torch.cuda.stream(s):
     eng.replay("g", 50)
 torch.cuda.synchronize()
 d = dbg.view(-1, 8).cpu()
+h = d[2 * B:]
+d = d[:2 * B]
 names = ["issue loads", "zero+barrier", "x/W1 stage+barrier", "conv1", "W2 store+copyout+barrier", "conv2 loop", "epilogue"]
 base = d[:, 0].min()
 print("block span (cycles): median", (d[:, 6] - d[:, 0]).median().item(), "max", (d[:, 6] - d[:, 0]).max().item(),
@@ -38,3 +40,8 @@ print("block span (cycles): median", (d[:, 6] - d[:, 0]).median().item(), "max",
 for k in range(6):
     dd = d[:, k + 1] - d[:, k]
     print(f"{names[k]:28s} median {dd.median().item():8d}  p90 {dd.float().quantile(0.9).item():8.0f}")
+hn = ["bias+slab loads", "dropout+wout+lp", "reduce+softmax", "dl/dh+stores"]
+print("head block span: median", (h[:, 4] - h[:, 0]).median().item())
+for k in range(4):
+    dd = h[:, k + 1] - h[:, k]
+    print(f"head {hn[k]:23s} median {dd.median().item():8d}  p90 {dd.float().quantile(0.9).item():8.0f}")

@@ -243,6 +243,55 @@ def test_fc_adam_in_backward_epilogue_matches_separate_adam(cuda, fork):
     assert torch.allclose(engs[0].adam_v(), engs[1].adam_v(), rtol=1e-3, atol=1e-12)
 
 
+def _assert_same_regions(p0, p1, what):
+    bad = {}
+    for name, sl in (("conv1", slice(0, 832)), ("conv2", slice(832, M.BUCKET_SPLIT)),
+                     ("fc1", slice(M.BUCKET_SPLIT, M.OFFSETS["out"])), ("out", slice(M.OFFSETS["out"], None))):
+        d = (p0[sl] - p1[sl]).abs()
+        if d.max().item() > 0:
+            bad[name] = (int((d > 0).sum().item()), d.max().item())
+    assert not bad, f"{what}: differing elements per region {bad}"
+
+
+def test_fc_split_schedule_is_bitwise_the_fused_step(cuda):
+    """One GPU, set_fc_split: fc dW + the fc-region Adam on the optimizer stream beside dX and the
+    conv backward, the conv-region Adam after the join. Same kernels, same summation orders as the
+    one-stream fused step, so parameters, slots and the step counter are bitwise equal after
+    eager + captured steps (a missing stream dependency shows up as a mismatch)."""
+    B = 128
+    params = M.flat_from_dict(M.init_params(23)).to(cuda) * 0.05
+    n = 1024
+    data = torch.rand(n, 784, device=cuda)
+    labels = torch.randint(0, 10, (n,), dtype=torch.int32, device=cuda)
+    perm = torch.randperm(n, device=cuda).to(torch.int32)
+    engs = []
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for on in (1, 0):
+            e = _engine(B, cuda, keep=0.75)
+            e.set_adam(0.01, 0.9, 0.999, 1e-8)
+            e.set_fc_split(on)
+            e.set_local_bf16_grads(1)  # the split schedule always keeps the fc gradients in bf16
+            e.params().copy_(params)
+            e.sync_shadow()
+            e.set_dataset(data, labels, perm)
+            e.set_input_mode(1)
+            engs.append(e)
+        for e in engs:
+            e.train_step()
+        torch.cuda.synchronize()
+        _assert_same_regions(engs[0].params(), engs[1].params(), "eager step")
+        for e in engs:
+            e.capture_train_steps("g", 4)
+            e.replay("g", 3)
+    torch.cuda.synchronize()
+    assert [int(e.step_tensor().item()) for e in engs] == [13, 13]
+    _assert_same_regions(engs[0].params(), engs[1].params(), "captured steps")
+    assert torch.equal(engs[0].params(), engs[1].params())
+    assert torch.equal(engs[0].adam_v(), engs[1].adam_v())
+    assert torch.equal(engs[0].params_bf16(), engs[1].params_bf16())
+
+
 def test_phase_timing_events_inside_graph(cuda):
     """HIP timing events at the phase boundaries, recorded eagerly and as graph event nodes."""
     B = 128
