@@ -60,6 +60,8 @@ def main(argv=None):
                     "stream beside the conv backward")
     ap.add_argument("--fc_split", type=int, default=0, help="1: on one GPU, fc dW + the fc-region Adam on a "
                     "second stream beside dX and the conv backward")
+    ap.add_argument("--fc_defer", type=int, default=0, help="N > 0: on one GPU, the fc-region Adam on a second "
+                    "stream with N workgroups, overlapping the conv backward and the next conv forward")
     ap.add_argument("--conv_unfused", type=int, default=0, help="1: conv1 and conv2 forward as two kernels "
                     "(A/B of the fused conv1->conv2 kernel)")
     ap.add_argument("--lr", type=float, default=0.01)
@@ -92,6 +94,7 @@ def main(argv=None):
     eng.set_fc_adam(a.fc_adam, a.fc_adam_fork)
     eng.set_conv_unfused(a.conv_unfused)
     eng.set_fc_split(a.fc_split)
+    eng.set_fc_defer(a.fc_defer)
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     mode = a.transport

@@ -257,6 +257,37 @@ __global__ __launch_bounds__(256) void conv2_pool_fwd(MnistStepArgs a) {
 // staged 129 KB per CU; this split stages 78 KB per CU on all 256.)
 constexpr int C2F_W = 24, C2F_PLANE = 18 * C2F_W, C2F_WLD = 48;
 constexpr int C2L_FWD_SMEM = (4 * C2F_PLANE * 8 + 800 * C2F_WLD) * 2;  // 104448 B
+#ifndef TFD_C2_PIPE  // 1: conv2 forward tap loop software-pipelined, both M-tiles on every wave
+#define TFD_C2_PIPE 1
+#endif
+// conv2 forward main loop over the 25 taps: two M-tiles (rows base[0], base[1] of the LDS image) x
+// two 16-channel N-tiles. Every wave runs both M-tiles (a second tile past row 196 reads row 0's
+// valid LDS address; the epilogue drops it) so there is no exec-masked branch in the loop, and
+// tap t + 1's fragments are read while tap t's MFMAs run: with a branch per tile the compiler
+// waited lgkmcnt(0) twice per tap, 25 serial LDS round trips (6.2 K cycles of the 24 K-cycle
+// conv12 block, s_memtime stamps).
+__device__ __forceinline__ void conv2_taps(const bf16* img, const bf16* wcol, const int base[2], f32x4 acc[2][2]) {
+  bf16x8 a[2][2], b[2][2];
+  auto load = [&](int tap, int slot) {
+    const int kh = tap / 5, kw = tap - 5 * kh, toff = (kh * C2F_W + kw) * 8;
+    const bf16* wr = wcol + tap * 32 * C2F_WLD;
+    b[slot][0] = frag_tr16(wr, wr + 4 * C2F_WLD);
+    b[slot][1] = frag_tr16(wr + 16, wr + 16 + 4 * C2F_WLD);
+    a[slot][0] = *reinterpret_cast<const bf16x8*>(img + base[0] + toff);
+    a[slot][1] = *reinterpret_cast<const bf16x8*>(img + base[1] + toff);
+  };
+  load(0, 0);
+#pragma unroll
+  for (int tap = 0; tap < 25; ++tap) {
+    const int cur = tap & 1;
+    if (tap + 1 < 25) load(tap + 1, cur ^ 1);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      acc[j][0] = mfma16x16x32(a[cur][j], b[cur][0], acc[j][0]);
+      acc[j][1] = mfma16x16x32(a[cur][j], b[cur][1], acc[j][1]);
+    }
+  }
+}
 static_assert(C2F_PLANE * 16 % 256 == 0, "chunk planes must be bank-row aligned");
 __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -312,6 +343,9 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
     base[j] = (g * C2F_PLANE + px) * 8;
   }
   const bf16* wcol = wt + (8 * g + q) * C2F_WLD + 4 * p4;
+  if (TFD_C2_PIPE && !TFD_EXP_SKIP_MAIN) {
+    conv2_taps(img, wcol, base, acc);
+  } else {
 #pragma unroll
   for (int kh = 0; kh < (TFD_EXP_SKIP_MAIN ? 0 : 5); ++kh) {
 #pragma unroll
@@ -328,6 +362,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
           acc[j][1] = mfma16x16x32(af, b1, acc[j][1]);
         }
     }
+  }
   }
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
@@ -359,20 +394,29 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
 // half's loads are issued FIRST and stay in flight behind the conv1 arithmetic; they are written
 // to LDS after it. One launch and one activation round trip less than conv1_pool_fwd +
 // conv2_fwd_lds. LDS: p1 image 27 KiB + W2 half 75 KiB + x / W1 staging 7.5 KiB.
-constexpr int C12_XOFF = C2L_FWD_SMEM;                       // fp32 [32][32] zero-bordered x image
-constexpr int C12_WOFF = C12_XOFF + 32 * 32 * 4;             // fp32 [25][32] W1 + [32] bias
+constexpr int C12_XS = 36;                                   // x image row stride (floats): fewer bank conflicts than 32
+constexpr int C12_XR = 60;                                   // rows: 32 (zero-bordered 28 x 28) + 28 zero rows
+constexpr int C12_XZ = 32 * C12_XS;                          // a padded tap (k >= 25): lands in the zero rows for any pixel
+constexpr int C12_XOFF = C2L_FWD_SMEM;                       // fp32 [C12_XR][C12_XS] x image
+constexpr int C12_WOFF = C12_XOFF + C12_XR * C12_XS * 4;     // fp32 [25][32] W1 + [32] bias
 constexpr int C12_IOFF = C12_WOFF + (KTAPS * C1 + C1) * 4;   // uint8 [196][32] conv1 argmax
-constexpr int C12_SMEM = C12_IOFF + 196 * 32;                // 118,400 B
+constexpr int C12_SMEM = C12_IOFF + 196 * 32;                // 122,944 B
 static_assert(C12_IOFF % 16 == 0, "LDS carve alignment");
 #ifndef TFD_STAMP
 #define TFD_STAMP 0  // 1: thread 0 of every conv12 block records s_memtime at its phase boundaries
 #endif
 #define C12_STAMP(k)                                                                       \
   do {                                                                                     \
-    if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
+    if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[blockIdx.x * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+// the same from wave 4 (the x / W1 loader), slots 8..15
+#define C12_STAMPW(k)                                                                      \
+  do {                                                                                     \
+    if (TFD_STAMP && a.dbg && threadIdx.x == 256) a.dbg[blockIdx.x * 16 + 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
   } while (0)
 __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
   C12_STAMP(0);
+  C12_STAMPW(0);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* img = (bf16*)smem_raw;                        // [4][18*24][8]  (conv2 input = pooled conv1)
   bf16* wt = img + 4 * C2F_PLANE * 8;                 // [800][48]
@@ -389,12 +433,18 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
   uint4 vw[NW];
   f32x4 xv = f32x4{0.f, 0.f, 0.f, 0.f}, w1v = f32x4{0.f, 0.f, 0.f, 0.f};
   const int u = t - 256;
+#ifndef TFD_EXP_C12L
+#define TFD_EXP_C12L 0  // timing experiments only (wrong results): 1 no W2 loads, 2 x from a fixed row
+#endif
   if (t < 256) {
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
       const int i = (t + 256 * j + rot) % 3200;
-      vw[j] = (t + 256 * j < 3200) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 2) * 64 + (i & 3) * 8) : zero4();
+      vw[j] = (t + 256 * j < 3200 && !(TFD_EXP_C12L & 1)) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 2) * 64 + (i & 3) * 8) : zero4();
     }
+  } else if (TFD_EXP_C12L & 2) {
+    if (u < (KTAPS * C1 + C1) / 4) w1v = reinterpret_cast<const f32x4*>(a.p32 + OFF_WC1)[u];
+    if (u < 196) xv = reinterpret_cast<const f32x4*>(a.data)[u];
   } else {
     if (u < (KTAPS * C1 + C1) / 4) w1v = reinterpret_cast<const f32x4*>(a.p32 + OFF_WC1)[u];
     // the prefetched image, loaded speculatively beside its tag and the step
@@ -409,23 +459,40 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
     }
   }
   C12_STAMP(1);
+  C12_STAMPW(1);
+#if TFD_STAMP
+  if (t == 256) {  // when wave 4's loads have landed (stamp only; the data wait happens anyway below)
+    __builtin_amdgcn_s_waitcnt(0);
+    C12_STAMPW(2);
+  }
+#endif
   // 2. zero the x image border and the p1 image (its border is conv2's SAME padding), then x, W1
-  for (int i = t; i < 32 * 32; i += 512) xs[i] = 0.f;
+  for (int i = t; i < C12_XR * C12_XS / 4; i += 512) reinterpret_cast<f32x4*>(xs)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int i = t; i < 4 * C2F_PLANE; i += 512) reinterpret_cast<uint4*>(img)[i] = zero4();
+  C12_STAMPW(3);
   __syncthreads();
+  C12_STAMPW(4);
   if (t >= 256) {
     if (u < (KTAPS * C1 + C1) / 4) reinterpret_cast<f32x4*>(w1)[u] = w1v;
     if (u < 196) {
       const int r = (4 * u) / 28, c = (4 * u) % 28;
-      float* d = xs + (r + 2) * 32 + c + 2;
+      float* d = xs + (r + 2) * C12_XS + c + 2;
       d[0] = xv[0]; d[1] = xv[1]; d[2] = xv[2]; d[3] = xv[3];
     }
   }
+  C12_STAMPW(5);
   __syncthreads();
   C12_STAMP(2);
+  C12_STAMPW(6);
 #ifndef TFD_EXP_C12
 #define TFD_EXP_C12 0  // timing experiments only (wrong results): 1 skip conv1, 2 skip conv2's MFMA loop
 #endif
+#ifndef TFD_EXP_C12REP
+#define TFD_EXP_C12REP 1  // timing experiment only: >1 runs the conv1 section that many times (warm I-cache)
+#endif
+#pragma nounroll
+  for (int rep = 0; rep < TFD_EXP_C12REP; ++rep) {
+  if (rep == 1) C12_STAMP(7);
   if (!(TFD_EXP_C12 & 1))
   // 3. conv1 on the matrix core: implicit GEMM M = 784 pixels (pool-window-major, m = pp*4 + win),
   //    N = 32 channels, K = 25 taps padded to 32 -> one v_mfma_f32_16x16x32_bf16 per (M-tile, N-tile);
@@ -448,17 +515,24 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
       }
     const float bias0 = w1[KTAPS * C1 + col], bias1 = w1[KTAPS * C1 + 16 + col];
     constexpr int MT = 7;  // ceil(49 / 8)
+    // The A gather is VALU-bound (wave64 VALU = 4 cycles, 2 waves per SIMD): per-lane tap offsets
+    // are computed once, a padded tap (k >= 25) points into the zero rows (no select, no exec-masked
+    // read: a masked read per element made the compiler wait lgkmcnt(0) 56 times, 7.6 K cycles),
+    // so each element costs one add + the read.
+    int toff[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int k = 8 * g + jj;
+      toff[jj] = k < KTAPS ? (k / 5) * C12_XS + (k % 5) : C12_XZ;
+    }
     bf16x8 af[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       const int mt = w + 8 * i;
       const int m = min(mt, 48) * 16 + col, pp = m >> 2, win = m & 3;
-      const int oh = 2 * (pp / 14) + (win >> 1), ow = 2 * (pp % 14) + (win & 1);
+      const int pb = (2 * (pp / 14) + (win >> 1)) * C12_XS + 2 * (pp % 14) + (win & 1);
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int k = 8 * g + jj, kh = k / 5, kw = k - 5 * (k / 5);
-        af[i][jj] = (bf16)(k < KTAPS ? xs[(oh + kh) * 32 + ow + kw] : 0.f);
-      }
+      for (int jj = 0; jj < 8; ++jj) af[i][jj] = (bf16)xs[pb + toff[jj]];
     }
     f32x4 z[MT][2];
 #pragma unroll
@@ -487,6 +561,7 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
       }
     }
   }
+  }  // rep
   C12_STAMP(3);
   // 4. the W2 half (landed during conv1) into LDS
   if (t < 256) {
@@ -525,6 +600,9 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
     base[j] = (g * C2F_PLANE + px) * 8;
   }
   const bf16* wcol = wt + (8 * g + q) * C2F_WLD + 4 * p4;
+  if (TFD_C2_PIPE && !(TFD_EXP_C12 & 2)) {
+    conv2_taps(img, wcol, base, acc);
+  } else {
 #pragma unroll
   for (int kh = 0; kh < ((TFD_EXP_C12 & 2) ? 0 : 5); ++kh) {
 #pragma unroll
@@ -541,6 +619,7 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
           acc[j][1] = mfma16x16x32(af, b1, acc[j][1]);
         }
     }
+  }
   }
   C12_STAMP(5);
 #pragma unroll
@@ -607,7 +686,7 @@ __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
 // One 256-thread block per batch row; thread t owns hidden units 4t..4t+3.
 #define HEAD_STAMP(k)                                                                                    \
   do {                                                                                                   \
-    if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[(2 * a.B + blockIdx.x) * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
+    if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[4 * a.B * 8 + blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
   } while (0)
 __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   HEAD_STAMP(0);
@@ -1057,6 +1136,9 @@ __device__ __forceinline__ void conv2_dgrad_block(const MnistStepArgs& a, int bx
 // A-fragment lanes read 16 consecutive 16-B slots (conflict-free); N = 32 (2 tiles); K = 1600.
 // Wave w owns M-tiles {w & 3, (w & 3) + 4}, both N-tiles, and taps [0,13) (w < 4) or [13,25):
 // 2 A + 2 B fragment reads per 4 MFMAs; the two K halves are summed through LDS at the end.
+#ifndef TFD_C2D_PIPE  // 1: conv2 dgrad K loop unrolled + software-pipelined (see conv2_dgrad_lds)
+#define TFD_C2D_PIPE 1
+#endif
 constexpr int C2D_ROWS = 11, C2D_COLS = 20, C2D_PLANE = 224, C2D_WLD = 72;
 constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 800 * C2D_WLD) * 2;  // 143872 B
 static_assert(C2D_PLANE * 16 % 256 == 0 && C2D_PLANE >= C2D_ROWS * C2D_COLS, "dz2 plane");
@@ -1123,9 +1205,47 @@ __global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bf16* wrow = wt + (lane & 15) * C2D_WLD + 8 * g;
-  const int tap0 = kq ? 13 : 0, tap1 = TFD_EXP_SKIP_MAIN ? tap0 : (kq ? 25 : 13);
-#pragma unroll 1
-  for (int tap = tap0; tap < tap1; ++tap) {
+#if TFD_C2D_PIPE
+  // Fully unrolled, software-pipelined K loop: step st = (tap, co half sk), step st + 1's four
+  // fragments are read while step st's MFMAs run; both M-tiles on every wave (the second tile of
+  // wave 3 reads rows past the image, dropped by the epilogue), and the per-half step count is a
+  // wave-uniform (scalar) branch: the former exec-masked tile branch in a rolled loop waited
+  // lgkmcnt(0) twice per step.
+  {
+    const int kqu = __builtin_amdgcn_readfirstlane(kq);
+    const int tapb = kqu ? 13 : 0, ns = TFD_EXP_SKIP_MAIN ? 0 : (kqu ? 24 : 26);
+    bf16x8 fb[2][2], fa[2][2];
+    auto ld = [&](int st, int slot) {
+      const int tap = tapb + (st >> 1), sk = st & 1;
+      const int kh = tap / 5, kw = tap - kh * 5, coff = -(kh * C2D_COLS + kw) * 8 + sk * 4 * C2D_PLANE * 8;
+      const bf16* wr = wrow + tap * 32 * C2D_WLD + sk * 32;
+      fb[slot][0] = *reinterpret_cast<const bf16x8*>(wr);
+      fb[slot][1] = *reinterpret_cast<const bf16x8*>(wr + 16 * C2D_WLD);
+      fa[slot][0] = *reinterpret_cast<const bf16x8*>(img + base[0] + coff);
+      fa[slot][1] = *reinterpret_cast<const bf16x8*>(img + base[1] + coff);
+    };
+    // ns is 24 or 26 (wave-uniform): steps < 24 are unconditional, the last two a scalar branch;
+    // st is a compile-time constant after unrolling, so the fragment slots stay in registers
+    const bool full = ns == 26;
+    if (ns > 0) {
+      ld(0, 0);
+#pragma unroll
+      for (int st = 0; st < 26; ++st) {
+        const int cur = st & 1;
+        if (st + 1 < 24 || (st + 1 < 26 && full)) ld(st + 1, cur ^ 1);
+        if (st < 24 || full) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc[j][0] = mfma16x16x32(fa[cur][j], fb[cur][0], acc[j][0]);
+            acc[j][1] = mfma16x16x32(fa[cur][j], fb[cur][1], acc[j][1]);
+          }
+        }
+      }
+    }
+  }
+  if (false)
+#endif
+  for (int tap = (kq ? 13 : 0); tap < (TFD_EXP_SKIP_MAIN ? (kq ? 13 : 0) : (kq ? 25 : 13)); ++tap) {
     const int kh = tap / 5, kw = tap - kh * 5, toff = -(kh * C2D_COLS + kw) * 8;
 #pragma unroll
     for (int sk = 0; sk < 2; ++sk) {
@@ -1558,7 +1678,7 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
     }
   } else {
     const int64_t i0 = MAD_C2END + (int64_t)(bid - MAD_CONV) * MAD_NT + tid;
-    constexpr int64_t STRIDE = (int64_t)MAD_FC_BLOCKS * MAD_NT;
+    const int64_t STRIDE = (int64_t)(o.fc_only ? (int)gridDim.x : MAD_FC_BLOCKS) * MAD_NT;
 #if TFD_ADAM_U > 1
     // All U strides' loads issued before any math/store, so U x 56 B per lane are in flight
     // (the one-at-a-time loop leaves the compiler no room: p/m/v stores may alias the next loads).
@@ -1743,9 +1863,9 @@ void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_
   mnist_adam_kernel<<<gb + (fc_region ? MAD_GRID : MAD_CONV), MAD_NT, 0, s>>>(a, o);
 }
 
-void mnist_adam_fc(const MnistStepArgs& a, MnistAdamArgs o, hipStream_t s) {
+void mnist_adam_fc(const MnistStepArgs& a, MnistAdamArgs o, hipStream_t s, int blocks) {
   o.fc_only = 1;
-  mnist_adam_kernel<<<MAD_FC_BLOCKS, MAD_NT, 0, s>>>(a, o);
+  mnist_adam_kernel<<<blocks > 0 ? blocks : MAD_FC_BLOCKS, MAD_NT, 0, s>>>(a, o);
 }
 
 void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s) {

@@ -194,6 +194,8 @@ class MnistEngine : public torch::CustomClassHolder {
   void set_fc_adam(int64_t on, int64_t fork) { fc_adam_ = on != 0; fc_adam_fork_ = fork != 0; }
   // one GPU: fc dW + fc Adam on the optimizer stream beside dX + the conv backward
   void set_fc_split(int64_t on) { fc_split_ = on != 0; }
+  // one GPU: the fc-region Adam deferred onto the optimizer stream with `blocks` workgroups (0: off)
+  void set_fc_defer(int64_t blocks) { fc_defer_ = blocks; }
   // 0 (default): conv1 fused into the conv2 forward kernel; 1: the two separate kernels (A/B)
   void set_conv_unfused(int64_t on) { conv_unfused_ = on != 0; }
   // Make every rank's state whole again after ZeRO-1 steps (before eval / checkpoint / broadcast):
@@ -364,6 +366,34 @@ class MnistEngine : public torch::CustomClassHolder {
       mark(P_BCONV, s);
       mnist_adam_fused(a, o, s, false);
       mark(P_OPT, s);
+      return;
+    }
+    if (fused && fc_defer_ > 0) {
+      // fc-region Adam on the optimizer stream with a small grid (fc_defer_ blocks: it leaves the
+      // CUs' wave slots to the conv kernels), overlapping the conv backward, the conv Adam and the
+      // NEXT step's conv forward; the main stream waits for it just before the next fc forward
+      // (the same cross-step schedule as train_step_dp, without the collectives)
+      a.gbf_a = (uint16_t*)gbf_.data_ptr();
+      o.gbf = (const uint16_t*)gbf_.data_ptr();
+      mnist_forward_conv(a, s);
+      if (pending_opt_a_) {
+        HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+        pending_opt_a_ = false;
+      }
+      mnist_forward_fc(a, true, s);
+      mark(P_FWD, s);
+      mnist_backward_a(a, s, 0);
+      mark(P_BFC, s);
+      HIP_OK(hipEventRecord(ev_a_, s));
+      HIP_OK(hipStreamWaitEvent(opt_stream_, ev_a_, 0));
+      mnist_adam_fc(a, o, opt_stream_, (int)fc_defer_);
+      HIP_OK(hipEventRecord(ev_opt_a_, opt_stream_));
+      mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
+      mark(P_BCONV, s);
+      mnist_adam_fused(a, o, s, false);
+      mark(P_OPT, s);
+      if (join_end) HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+      else pending_opt_a_ = true;
       return;
     }
     if (fused && fc_split_) {
@@ -796,6 +826,7 @@ class MnistEngine : public torch::CustomClassHolder {
   bool fuse_tail_ = true;
   bool local_bf16_grads_ = false;
   bool fc_adam_ = false, fc_adam_fork_ = false, fc_split_ = false;
+  int64_t fc_defer_ = 0;
   bool conv_unfused_ = false;  // measured slower (docs/DESIGN.md)
   std::map<std::string, hipGraphExec_t> graphs_;
   hipEvent_t pev_[P_N] = {};
@@ -847,6 +878,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("dp", &MnistEngine::dp)
       .def("set_conv_fork", &MnistEngine::set_conv_fork)
       .def("set_fc_split", &MnistEngine::set_fc_split)
+      .def("set_fc_defer", &MnistEngine::set_fc_defer)
       .def("set_fused_tail", &MnistEngine::set_fused_tail)
       .def("set_local_bf16_grads", &MnistEngine::set_local_bf16_grads)
       .def("set_fc_adam", &MnistEngine::set_fc_adam)

@@ -84,9 +84,9 @@ struct MnistAdamArgs {
 };
 // fc_region = false: the conv region only (the fc region was updated by mnist_backward_a_adam)
 void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region = true);
-// The fc region alone (1024 grid-stride blocks), e.g. on a side stream beside the conv backward;
-// mnist_adam_fused(..., fc_region = false) then finishes the step.
-void mnist_adam_fc(const MnistStepArgs& a, MnistAdamArgs o, hipStream_t s);
+// The fc region alone (`blocks` grid-stride blocks, default 1024), e.g. on a side stream beside the
+// conv backward; mnist_adam_fused(..., fc_region = false) then finishes the step.
+void mnist_adam_fc(const MnistStepArgs& a, MnistAdamArgs o, hipStream_t s, int blocks = 0);
 // One GPU: fc1 dW and the output-layer gradients with ApplyAdam fused into their epilogues (the fc
 // gradients never reach memory; t = global_step + 1). Launch after the dX GEMM (part 2).
 void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s);

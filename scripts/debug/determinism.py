@@ -8,7 +8,7 @@ import torch
 from dist_util import run_ranks
 
 
-def _worker(rank, world, B, R):
+def _worker(rank, world, B, R, unfused):
     from tensorflow_distributed_amd.models import mnist_cnn as M
     from tensorflow_distributed_amd import _native
     _native.require()
@@ -16,6 +16,7 @@ def _worker(rank, world, B, R):
     dev = torch.device("cuda", 0)
     eng = torch.classes.tfd.MnistEngine(B, 0, 1.0, 5, 0)
     eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+    eng.set_conv_unfused(unfused)
     g = torch.Generator().manual_seed(7)
     x = torch.rand(B, 784, generator=g)
     y = torch.randint(0, 10, (B,), generator=g, dtype=torch.int32)
@@ -60,7 +61,8 @@ def _worker(rank, world, B, R):
 
 if __name__ == "__main__":
     world = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    res = run_ranks(_worker, world, 16, 60, timeout=400)
+    unfused = int(sys.argv[2]) if len(sys.argv) > 2 else 0  # 1: conv1_pool_fwd (VALU conv1) + conv2 kernels
+    res = run_ranks(_worker, world, 16, 60, unfused, timeout=400)
     for r, (bad, first) in enumerate(res):
         print("rank", r, "within-process max diff:", {k: f"{v:.3g}" for k, v in bad.items()})
         print("rank", r, "vs rank0:", {k: f"{(first[k] - res[0][1][k]).abs().max().item():.3g}" for k in first})

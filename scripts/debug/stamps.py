@@ -15,7 +15,7 @@ dev = torch.device("cuda", 0)
 B = 128
 eng = torch.classes.tfd.MnistEngine(B, 0, 0.75, 1, 0)
 eng.set_adam(0.01, 0.9, 0.999, 1e-8)
-dbg = torch.zeros(3 * B * 8, dtype=torch.int64, device=dev)
+dbg = torch.zeros(5 * B * 8, dtype=torch.int64, device=dev)
 eng.set_debug_buffer(dbg)
 s = torch.cuda.Stream()
 with torch.cuda.stream(s):
@@ -30,16 +30,39 @@ with torch.cuda.stream(s):
     eng.capture_train_steps("g", 20)
     eng.replay("g", 50)
 torch.cuda.synchronize()
+MODE = sys.argv[1] if len(sys.argv) > 1 else "train"
+if MODE == "fwd_after_idle":  # conv12 + head with no write-heavy kernel before them
+    import time
+    time.sleep(0.01)
+    with torch.cuda.stream(s):
+        eng.forward(True)
+    torch.cuda.synchronize()
+elif MODE == "fwd_after_fill":  # conv12 + head right after a 45 MB write-only fill
+    junk = torch.empty(45 * 2**20 // 4, device=dev)
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            junk.fill_(1.0)
+            eng.forward(True)
+    torch.cuda.synchronize()
+print("mode", MODE)
 d = dbg.view(-1, 8).cpu()
-h = d[2 * B:]
-d = d[:2 * B]
-names = ["issue loads", "zero+barrier", "x/W1 stage+barrier", "conv1", "W2 store+copyout+barrier", "conv2 loop", "epilogue"]
+h = d[4 * B:]
+w4 = d[1:4 * B:2]
+d = d[0:4 * B:2]
+names = ["issue loads", "zero+stage+2 barriers", "conv1", "W2 store+copyout+barrier", "conv2 loop", "epilogue"]
 base = d[:, 0].min()
 print("block span (cycles): median", (d[:, 6] - d[:, 0]).median().item(), "max", (d[:, 6] - d[:, 0]).max().item(),
       "start spread", (d[:, 0] - base).max().item())
 for k in range(6):
     dd = d[:, k + 1] - d[:, k]
     print(f"{names[k]:28s} median {dd.median().item():8d}  p90 {dd.float().quantile(0.9).item():8.0f}")
+wn = ["w4 issue loads", "w4 vmcnt(0) wait", "w4 zero LDS", "w4 barrier 1", "w4 x/W1 LDS stores", "w4 barrier 2"]
+for k in range(6):
+    dd = w4[:, k + 1] - w4[:, k]
+    print(f"{wn[k]:28s} median {dd.median().item():8d}  p90 {dd.float().quantile(0.9).item():8.0f}")
+print("wave4 start - wave0 start: median", (w4[:, 0] - d[:, 0]).median().item())
+if (d[:, 7] > 0).all():  # TFD_EXP_C12REP=2: conv1 section twice (second pass with a warm I-cache)
+    print("conv1 rep0", (d[:, 7] - d[:, 2]).median().item(), "rep1", (d[:, 3] - d[:, 7]).median().item())
 hn = ["bias+slab loads", "dropout+wout+lp", "reduce+softmax", "dl/dh+stores"]
 print("head block span: median", (h[:, 4] - h[:, 0]).median().item())
 for k in range(4):

@@ -1,13 +1,16 @@
 #!/bin/bash
-# Interleaved A/B of bench.py argument sets on one lease: ARGS_A / ARGS_B, REPS rounds, 20/5 and 1000/100.
+# Interleaved A/B/C/... of bench.py argument sets on one lease: ARGS_A, ARGS_B (and optional ARGS_C,
+# ARGS_D), REPS rounds, at 20/5 and 1000/100 (SWEEPS="20 5;1000 100" overrides).
 set -o pipefail
 export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
+IFS=';' read -ra SW <<< "${SWEEPS:-20 5;1000 100}"
 for r in $(seq 1 ${REPS:-2}); do
-  for v in A B; do
-    eval "args=\$ARGS_$v"
-    for sw in "20 5" "1000 100"; do
+  for v in A B C D; do
+    eval "args=\${ARGS_$v-__unset__}"
+    [ "$args" = "__unset__" ] && continue
+    for sw in "${SW[@]}"; do
       set -- $sw
       timeout -k 10 120 python bench.py --steps $1 --warmup $2 $args > gpurun_out/ab.log 2>&1 || { echo "bench failed"; cat gpurun_out/ab.log; exit 1; }
       echo "$v [$args] $1/$2: $(grep -o 'ms_per_step": [0-9.]*' gpurun_out/ab.log)"

@@ -253,11 +253,14 @@ def _assert_same_regions(p0, p1, what):
     assert not bad, f"{what}: differing elements per region {bad}"
 
 
-def test_fc_split_schedule_is_bitwise_the_fused_step(cuda):
-    """One GPU, set_fc_split: fc dW + the fc-region Adam on the optimizer stream beside dX and the
-    conv backward, the conv-region Adam after the join. Same kernels, same summation orders as the
-    one-stream fused step, so parameters, slots and the step counter are bitwise equal after
-    eager + captured steps (a missing stream dependency shows up as a mismatch)."""
+@pytest.mark.parametrize("mode", ["split", "defer"])
+def test_two_stream_schedules_are_bitwise_the_fused_step(cuda, mode):
+    """One GPU, two-stream schedules vs the one-stream fused step:
+    split: fc dW + the fc-region Adam on the optimizer stream beside dX and the conv backward;
+    defer: the fc-region Adam (small grid) on the optimizer stream across the step boundary, the
+    next fc forward waits for it. Same kernels, same summation orders, so parameters, slots and the
+    step counter are bitwise equal after eager + captured multi-step graphs (a missing stream
+    dependency shows up as a mismatch)."""
     B = 128
     params = M.flat_from_dict(M.init_params(23)).to(cuda) * 0.05
     n = 1024
@@ -270,7 +273,10 @@ def test_fc_split_schedule_is_bitwise_the_fused_step(cuda):
         for on in (1, 0):
             e = _engine(B, cuda, keep=0.75)
             e.set_adam(0.01, 0.9, 0.999, 1e-8)
-            e.set_fc_split(on)
+            if mode == "split":
+                e.set_fc_split(on)
+            else:
+                e.set_fc_defer(256 if on else 0)
             e.set_local_bf16_grads(1)  # the split schedule always keeps the fc gradients in bf16
             e.params().copy_(params)
             e.sync_shadow()
