@@ -256,6 +256,16 @@ __global__ __launch_bounds__(256) void conv2_pool_fwd(MnistStepArgs a) {
 // happen in registers. (The per-image block of 64 channels used only 128 CUs at B = 128 and
 // staged 129 KB per CU; this split stages 78 KB per CU on all 256.)
 constexpr int C2F_W = 24, C2F_PLANE = 18 * C2F_W, C2F_WLD = 48;
+// LDS weight rows r = tap*32 + ci (32 bf16 each): groups of 8 rows 384 elements apart, rows 32
+// apart inside a group, odd groups shifted by 16 elements. A B-fragment ds_read_b64_tr_b16 has the
+// lanes of K-chunks g = 0, 1 reading rows 8g + q (q < 4; the second read q + 4): with a plain
+// 96-B pitch rows r and r + 8 share banks (2-way, 3.2 K of the conv2 loop's 5.7 K LDS cycles per
+// block); with this layout the 8 rows cover 64 distinct banks (scripts/debug/lds_banks.py). Same
+// footprint as the plain [800][48] layout.
+__device__ __forceinline__ int c2f_wrow(int r) { return (r >> 3) * 384 + (r & 7) * 32 + ((r >> 3) & 1) * 16; }
+constexpr int C2F_WTAP = 4 * 384;  // one tap = 32 rows = 4 groups
+constexpr int C2F_WR4 = 4 * 32;    // + 4 rows inside a group
+static_assert(C2F_WTAP == 32 * C2F_WLD, "the layout keeps the [800][48] footprint");
 constexpr int C2L_FWD_SMEM = (4 * C2F_PLANE * 8 + 800 * C2F_WLD) * 2;  // 104448 B
 #ifndef TFD_C2_PIPE  // 1: conv2 forward tap loop software-pipelined, both M-tiles on every wave
 #define TFD_C2_PIPE 1
@@ -270,9 +280,9 @@ __device__ __forceinline__ void conv2_taps(const bf16* img, const bf16* wcol, co
   bf16x8 a[2][2], b[2][2];
   auto load = [&](int tap, int slot) {
     const int kh = tap / 5, kw = tap - 5 * kh, toff = (kh * C2F_W + kw) * 8;
-    const bf16* wr = wcol + tap * 32 * C2F_WLD;
-    b[slot][0] = frag_tr16(wr, wr + 4 * C2F_WLD);
-    b[slot][1] = frag_tr16(wr + 16, wr + 16 + 4 * C2F_WLD);
+    const bf16* wr = wcol + tap * C2F_WTAP;
+    b[slot][0] = frag_tr16(wr, wr + C2F_WR4);
+    b[slot][1] = frag_tr16(wr + 16, wr + 16 + C2F_WR4);
     a[slot][0] = *reinterpret_cast<const bf16x8*>(img + base[0] + toff);
     a[slot][1] = *reinterpret_cast<const bf16x8*>(img + base[1] + toff);
   };
@@ -318,7 +328,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
       const int i = (t + 512 * j + rot) % 3200;
-      if (t + 512 * j < 3200) *reinterpret_cast<uint4*>(wt + (i >> 2) * C2F_WLD + (i & 3) * 8) = vw[j];
+      if (t + 512 * j < 3200) *reinterpret_cast<uint4*>(wt + c2f_wrow(i >> 2) + (i & 3) * 8) = vw[j];
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -342,7 +352,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
     }
     base[j] = (g * C2F_PLANE + px) * 8;
   }
-  const bf16* wcol = wt + (8 * g + q) * C2F_WLD + 4 * p4;
+  const bf16* wcol = wt + c2f_wrow(8 * g + q) + 4 * p4;  // rows tap*32 + 8g + q (+4)
   if (TFD_C2_PIPE && !TFD_EXP_SKIP_MAIN) {
     conv2_taps(img, wcol, base, acc);
   } else {
@@ -351,9 +361,9 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
 #pragma unroll
     for (int kw = 0; kw < 5; ++kw) {
       const int tap = kh * 5 + kw, toff = (kh * C2F_W + kw) * 8;
-      const bf16* wr = wcol + tap * 32 * C2F_WLD;
-      const bf16x8 b0 = frag_tr16(wr, wr + 4 * C2F_WLD);
-      const bf16x8 b1 = frag_tr16(wr + 16, wr + 16 + 4 * C2F_WLD);
+      const bf16* wr = wcol + tap * C2F_WTAP;
+      const bf16x8 b0 = frag_tr16(wr, wr + C2F_WR4);
+      const bf16x8 b1 = frag_tr16(wr + 16, wr + 16 + C2F_WR4);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         if (j < nmt) {
@@ -436,12 +446,18 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
 #ifndef TFD_EXP_C12L
 #define TFD_EXP_C12L 0  // timing experiments only (wrong results): 1 no W2 loads, 2 x from a fixed row
 #endif
-  if (t < 256) {
+#ifndef TFD_C12_XFIRST  // 1: the x / W1 loads are issued before the W2 loads (a barrier orders them)
+#define TFD_C12_XFIRST 0  // measured: no gain (75.6 vs 75.4 us/step), kept as a switch
+#endif
+  auto load_w2 = [&]() {
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
       const int i = (t + 256 * j + rot) % 3200;
       vw[j] = (t + 256 * j < 3200 && !(TFD_EXP_C12L & 1)) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 2) * 64 + (i & 3) * 8) : zero4();
     }
+  };
+  if (t < 256) {
+    if (!TFD_C12_XFIRST) load_w2();
   } else if (TFD_EXP_C12L & 2) {
     if (u < (KTAPS * C1 + C1) / 4) w1v = reinterpret_cast<const f32x4*>(a.p32 + OFF_WC1)[u];
     if (u < 196) xv = reinterpret_cast<const f32x4*>(a.data)[u];
@@ -458,6 +474,13 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
       if (u < 196) xv = reinterpret_cast<const f32x4*>(x)[u];
     }
   }
+#if TFD_C12_XFIRST
+  // conv1 needs x / W1 first; the 51 KB W2 half is only needed after conv1. The CU's memory
+  // pipeline serves a block's loads at ~11 B/cycle, so W2 issued beside x delayed x by ~3.5 K
+  // cycles: waves 0-3 issue W2 only after waves 4-7 have issued x / W1 (plain s_barrier, no fence)
+  __builtin_amdgcn_s_barrier();
+  if (t < 256) load_w2();
+#endif
   C12_STAMP(1);
   C12_STAMPW(1);
 #if TFD_STAMP
@@ -568,7 +591,7 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
       const int i = (t + 256 * j + rot) % 3200;
-      if (t + 256 * j < 3200) *reinterpret_cast<uint4*>(wt + (i >> 2) * C2F_WLD + (i & 3) * 8) = vw[j];
+      if (t + 256 * j < 3200) *reinterpret_cast<uint4*>(wt + c2f_wrow(i >> 2) + (i & 3) * 8) = vw[j];
     }
   }
   __syncthreads();
@@ -599,7 +622,7 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
     }
     base[j] = (g * C2F_PLANE + px) * 8;
   }
-  const bf16* wcol = wt + (8 * g + q) * C2F_WLD + 4 * p4;
+  const bf16* wcol = wt + c2f_wrow(8 * g + q) + 4 * p4;  // rows tap*32 + 8g + q (+4)
   if (TFD_C2_PIPE && !(TFD_EXP_C12 & 2)) {
     conv2_taps(img, wcol, base, acc);
   } else {
@@ -608,9 +631,9 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
 #pragma unroll
     for (int kw = 0; kw < 5; ++kw) {
       const int tap = kh * 5 + kw, toff = (kh * C2F_W + kw) * 8;
-      const bf16* wr = wcol + tap * 32 * C2F_WLD;
-      const bf16x8 b0 = frag_tr16(wr, wr + 4 * C2F_WLD);
-      const bf16x8 b1 = frag_tr16(wr + 16, wr + 16 + 4 * C2F_WLD);
+      const bf16* wr = wcol + tap * C2F_WTAP;
+      const bf16x8 b0 = frag_tr16(wr, wr + C2F_WR4);
+      const bf16x8 b1 = frag_tr16(wr + 16, wr + 16 + C2F_WR4);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         if (j < nmt) {
