@@ -1162,8 +1162,11 @@ __device__ __forceinline__ void conv2_dgrad_block(const MnistStepArgs& a, int bx
 #ifndef TFD_C2D_PIPE  // 1: conv2 dgrad K loop unrolled + software-pipelined (see conv2_dgrad_lds)
 #define TFD_C2D_PIPE 1
 #endif
-constexpr int C2D_ROWS = 11, C2D_COLS = 20, C2D_PLANE = 224, C2D_WLD = 72;
-constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 800 * C2D_WLD) * 2;  // 143872 B
+constexpr int C2D_ROWS = 11, C2D_COLS = 20, C2D_PLANE = 224;
+// weight row pitch 80 (not 72): the B-fragment ds_read_b128 of rows co = lane & 15 is conflict-free
+// (72: 2-way, 3.2 K vs 1.6 K LDS cycles per block; scripts/debug/lds_banks.py)
+constexpr int C2D_WLD = 80;
+constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 800 * C2D_WLD) * 2;  // 156672 B
 static_assert(C2D_PLANE * 16 % 256 == 0 && C2D_PLANE >= C2D_ROWS * C2D_COLS, "dz2 plane");
 constexpr int C1W_HALF = 98;  // pooled conv1 pixels per half image (7 rows of 14)
 // fused conv1-wgrad tail: buffers carved from the (dead) weight region
@@ -1408,11 +1411,12 @@ __global__ __launch_bounds__(256) void conv2_wgrad_k(MnistStepArgs a, int kper) 
 constexpr int C2WL_IMG = 2;                 // images per block
 constexpr int C2WL_NTG = 4;                 // tap groups: [0,6) [6,12) [12,18) [18,25)
 constexpr int C2WL_MAXT = 7;
-constexpr int C2WL_CS = 40, C2WL_PW = 18;   // padded image: 18 x 18 positions x 40-ch stride
+constexpr int C2WL_CS = 48, C2WL_PW = 18;   // padded image: 18 x 18 positions x 48-ch stride
+                                            // (A tr-reads: 2296 LDS cycles per image vs 2968 at 40)
 constexpr int C2WL_DS = 72, C2WL_KP = 224;  // dz2 rows: pixels padded to 7 k-steps of 32
 constexpr int C2WL_IMG_ELEMS = C2WL_PW * C2WL_PW * C2WL_CS;
 constexpr int C2WL_BRED_OFF = (C2WL_IMG_ELEMS + C2WL_KP * C2WL_DS) * 2;
-constexpr int C2WL_SMEM = C2WL_BRED_OFF + 8 * 64 * 4;  // 60224 B: two blocks per CU
+constexpr int C2WL_SMEM = C2WL_BRED_OFF + 8 * 64 * 4;  // 65408 B: two blocks per CU
 static_assert(C2WL_BRED_OFF % 16 == 0 && (C2WL_IMG_ELEMS * 2) % 16 == 0, "LDS carve alignment");
 __global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -1444,18 +1448,23 @@ __global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) {
 #pragma unroll
   for (int j = 0; j < C2WL_MAXT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
+  // image ii + 1's global loads are issued before image ii's MFMAs, so its staging latency hides
+  // under them (one image at a time left the CU idle through each ~37 KB load)
+  uint4 v1[2], v2[4];
+  auto gload = [&](int b) {
+    const uint4* s1 = reinterpret_cast<const uint4*>(a.p1 + (size_t)b * 196 * 32);
+    const uint4* s2 = reinterpret_cast<const uint4*>(a.dz2 + (size_t)b * 196 * 64);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) { const int i = t + 512 * j; v1[j] = i < 784 ? s1[i] : zero4(); }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { const int i = t + 512 * j; v2[j] = i < 1568 ? s2[i] : zero4(); }
+  };
+  if (ip * C2WL_IMG < a.B) gload(ip * C2WL_IMG);
   for (int ii = 0; ii < C2WL_IMG; ++ii) {
     const int b = ip * C2WL_IMG + ii;
     if (b >= a.B) break;
     __syncthreads();  // the previous image's fragments are consumed
     {
-      const uint4* s1 = reinterpret_cast<const uint4*>(a.p1 + (size_t)b * 196 * 32);
-      const uint4* s2 = reinterpret_cast<const uint4*>(a.dz2 + (size_t)b * 196 * 64);
-      uint4 v1[2], v2[4];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) { const int i = t + 512 * j; v1[j] = i < 784 ? s1[i] : zero4(); }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { const int i = t + 512 * j; v2[j] = i < 1568 ? s2[i] : zero4(); }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int i = t + 512 * j;
@@ -1471,6 +1480,7 @@ __global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) {
       }
     }
     __syncthreads();
+    if (ii + 1 < C2WL_IMG && b + 1 < a.B) gload(b + 1);
     if (tg == 0) {  // bias row: column sums of dz2 (pixel slice t >> 6 of 8)
       for (int px = t >> 6; px < 196; px += 8) bsum += bf2f(dz[px * C2WL_DS + (t & 63)]);
     }

@@ -96,3 +96,75 @@ if __name__ == "__main__":
     for sw in (False, True):
         print("conv2 fwd B reads, swizzle=%s: %d, ideal %d" % ((sw,) + conv2_fwd_b(sw)))
         print("W2 staging stores, swizzle=%s: %d, ideal %d" % ((sw,) + w2_store(sw)))
+
+
+# ---- conv2 dgrad (conv2_dgrad_lds): image [8 chunks][224 px] x 16 B, weights [800][72]
+C2D_COLS, C2D_PLANE, C2D_WLD = 20, 224, 72
+
+
+def conv2_dgrad(wld=C2D_WLD):
+    ta = tb = ia = ib = 0
+    for w in range(8):
+        mt0, kq = w & 3, w >> 2
+        for tap in (range(13, 25) if kq else range(13)):
+            kh, kw = divmod(tap, 5)
+            for sk in range(2):
+                coff = -(kh * C2D_COLS + kw) * 8 + sk * 4 * C2D_PLANE * 8
+                for j in range(2):
+                    out = []
+                    for lane in range(64):
+                        g, iw = lane >> 4, lane & 15
+                        base = ((mt0 + 4 * j + 4) * C2D_COLS + iw + 4) * 8 + g * C2D_PLANE * 8
+                        out.append((base + coff) * 2)
+                    c, n = cycles(out, "r128")
+                    ta, ia = ta + c, ia + n
+                for half in range(2):
+                    out = []
+                    for lane in range(64):
+                        g = lane >> 4
+                        out.append(((lane & 15) * wld + 8 * g + tap * 32 * wld + sk * 32 + half * 16 * wld) * 2)
+                    c, n = cycles(out, "r128")
+                    tb, ib = tb + c, ib + n
+    return ta, ia, tb, ib
+
+
+if __name__ == "__main__":
+    print("conv2 dgrad A reads: %d, ideal %d; B reads: %d, ideal %d" % conv2_dgrad())
+    for wld in (64, 68, 72, 76, 80, 88):
+        print("  dgrad weight pitch", wld, "-> B %d (ideal %d)" % conv2_dgrad(wld)[2:])
+
+
+# ---- conv2 wgrad (conv2_wgrad_lds): image [18][18] x CS ch, dz2 rows [224][DS]; both via tr reads
+def conv2_wgrad(cs=40, ds=72):
+    PW = 18
+    ta = tb = ia = ib = 0
+    for w in range(8):
+        h, n = w >> 2, w & 3
+        for s in range(7):
+            for second in range(2):  # frag_tr16 = two ds_read_b64_tr_b16 (rows +0 / +4)
+                out = []
+                for lane in range(64):
+                    g, q, p4 = lane >> 4, (lane & 15) >> 2, lane & 3
+                    out.append((((32 * s + 8 * g + q + 4 * second) * ds) + 16 * n + 4 * p4) * 2)
+                c, m = cycles(out, "tr64")
+                tb, ib = tb + c, ib + m
+            for tap in range(7):
+                toff = (tap // 5) * PW + tap % 5
+                for u in range(2):
+                    out = []
+                    for lane in range(64):
+                        g, q, p4 = lane >> 4, (lane & 15) >> 2, lane & 3
+                        k = 32 * s + 8 * g + q + 4 * u
+                        pos = (k // 14) * PW + (k % 14) if k < 196 else 0
+                        out.append(((pos + toff) * cs + 16 * h + 4 * p4) * 2)
+                    c, m = cycles(out, "tr64")
+                    ta, ia = ta + c, ia + m
+    return ta, ia, tb, ib
+
+
+if __name__ == "__main__":
+    print("conv2 wgrad (per image, 7 taps): A %d (ideal %d), B %d (ideal %d)" % conv2_wgrad())
+    for cs in (32, 36, 40, 44, 48):
+        for ds in (64, 68, 72, 80):
+            r = conv2_wgrad(cs, ds)
+            print("  cs", cs, "ds", ds, "-> A %d B %d (ideal %d / %d)" % (r[0], r[2], r[1], r[3]))
