@@ -50,6 +50,9 @@ def main(argv=None):
                     "(fp32 accumulate/master/optimizer), or fp32 everything (the reference's precision)")
     ap.add_argument("--conv_fork", type=int, default=0, help="1: conv2 wgrad on a forked stream beside dgrad")
     ap.add_argument("--zero", type=int, default=0, help="1: ZeRO-1 sharding of the fc1 weight (N > 1)")
+    ap.add_argument("--fc_sfb", type=int, default=1, help="1 (N > 1 or --force_dp): fc-region gradients by "
+                    "sufficient-factor broadcasting -- all-gather the fc factors (1.33 MB/rank) and form the summed "
+                    "fc gradient locally instead of all-reducing it (6.4 MB); 0: bucketed all-reduce")
     ap.add_argument("--fused_tail", type=int, default=1, help="1: on one GPU the Adam kernel also reduces the "
                     "conv weight-gradient slabs and bumps the step (one kernel less)")
     ap.add_argument("--local_bf16_grads", type=int, default=1, help="1: on one GPU keep the fc-region gradients "
@@ -101,7 +104,8 @@ def main(argv=None):
     if mode == "auto":
         mode = "ipc" if ctx.shared_device else "rccl"
     tr = attach_engine(eng, rank, world, dev, mode=mode, comm=ctx.comm, bf16=not a.fp32_grads,
-                       small_ipc=bool(a.ipc_small), force_dp=bool(a.force_dp))
+                       small_ipc=bool(a.ipc_small), force_dp=bool(a.force_dp),
+                       sfb=bool(a.fc_sfb) and not a.zero and a.dtype == "bf16")
     if a.zero:
         eng.set_zero(True)
     s = torch.cuda.Stream(dev)
@@ -217,6 +221,7 @@ def main(argv=None):
                 "force_dp": bool(a.force_dp),
                 "zero1_fc1": bool(a.zero),
                 "fc_grads": ("fp32" if a.dtype == "fp32" else
+                             "summed from all-gathered factors (sfb), bf16" if "sfb" in tr.kind else
                              "fused into Adam (fp32, in registers)" if world == 1 and a.fc_adam and not a.force_dp
                              else "bf16" if (a.local_bf16_grads or world > 1) and not a.fp32_grads else "fp32"),
             },

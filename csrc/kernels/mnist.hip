@@ -23,6 +23,7 @@
 #include "../tfd_kernels.h"
 
 #include <algorithm>
+#include <stdexcept>
 
 #ifndef TFD_GEMM_RS
 #define TFD_GEMM_RS 2  // register stages of the LDS-staged GEMM core (csrc/gemm.h)
@@ -1103,6 +1104,95 @@ __global__ __launch_bounds__(256) void fc1_bwd_adam(MnistStepArgs a, MnistAdamAr
   fc1_dw_adam_block(a, o, id % FDW_GX, id / FDW_GX, (bf16*)smem_raw);
 }
 
+// ---------------- DP: fc gradients from all-gathered sufficient factors ----------------
+// The reference's PS sums the workers' gradients (/root/reference/mnist_python_m.py:216-222). For
+// the two fc layers the per-rank gradients are outer-product sums over the rank's batch, so the
+// SUM over ranks is the same GEMM with K = W*B over the ranks' factors concatenated along the
+// batch: gathering the factors (p2 [B][3136] + dh/hd [B][1024] bf16 + dlogits [B][10] fp32 =
+// 1.33 MB per rank at B = 128) replaces the all-reduce of the 6.4 MB bf16 fc gradient. On xGMI a
+// ring all-reduce moves 2(W-1)/W x 6.4 MB per rank, the gather (W-1) x 1.33 MB spread over W-1
+// peer links, so below W ~ 9 the gather moves fewer bytes per link (W = 2: 1.33 vs 6.4 MB over the
+// one link). Every rank then runs the identical GEMM on identical data: bit-identical gradients on
+// all ranks, fp32-accumulated over all W*B rows (no bf16 rounding of per-rank partial sums).
+// KC = false operand over per-rank slots: (mn, k) = X[row k % B of rank k / B][mn]
+struct RankRowsMC {
+  static constexpr bool KC = false;
+  const uint16_t* __restrict__ x;
+  int ld, mn_lim, k_lim, B;
+  int64_t rs;  // rank slot stride (elements)
+  __device__ __forceinline__ uint4 operator()(int mn, int k) const {
+    if (k >= k_lim || mn >= mn_lim) return zero4();
+    const int r = k / B;
+    const uint16_t* row = x + r * rs + (size_t)(k - r * B) * ld;
+    if (mn + 8 <= mn_lim) return *reinterpret_cast<const uint4*>(row + mn);
+    uint16_t t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = (mn + j < mn_lim) ? row[mn + j] : 0;
+    return *reinterpret_cast<uint4*>(t);
+  }
+};
+
+// Output layer [1025][10] = [Hd;1]^T dlogits over the W*B gathered rows: a block owns 16 rows m
+// (lane r = t & 15) x 16 row groups (q = t >> 4) of the K range, so even W = 8 leaves 64 rows per
+// thread; partials summed in fixed group order through LDS (deterministic, rank-independent).
+constexpr int OUTS_ROWS = 16, OUTS_GROUPS = 16, OUTS_LB = 8;
+constexpr int OUTS_BLOCKS = (HID + 1 + OUTS_ROWS - 1) / OUTS_ROWS;  // 65 (the last holds the bias row)
+__device__ __forceinline__ void out_grad_sfb_block(const MnistStepArgs& a, int blk, float* part) {
+  const int t = threadIdx.x, r = t & (OUTS_ROWS - 1), q = t / OUTS_ROWS;
+  const int m = blk * OUTS_ROWS + r;
+  const int B = a.B, WB = a.sfb_world * B;
+  const int per = (WB + OUTS_GROUPS - 1) / OUTS_GROUPS, k0 = min(WB, q * per), k1 = min(WB, k0 + per);
+  const int64_t hoff = (int64_t)B * HID, doff = 2 * (int64_t)B * HID;  // hd / dlogits inside a slot
+  float acc[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) acc[c] = 0.f;
+  if (m <= HID) {
+    for (int kb = k0; kb < k1; kb += OUTS_LB) {
+      float hv[OUTS_LB];
+      const float* dl[OUTS_LB];
+#pragma unroll
+      for (int u = 0; u < OUTS_LB; ++u) {  // every load of the batch in flight before the FMAs
+        const int k = min(kb + u, k1 - 1), rk = k / B, row = k - rk * B;
+        const uint16_t* slot = a.sfb_dr + rk * a.sfb_rs;
+        hv[u] = (kb + u < k1) ? (m < HID ? bf2f(slot[hoff + (int64_t)row * HID + m]) : 1.f) : 0.f;
+        dl[u] = reinterpret_cast<const float*>(slot + doff) + row * NCLS;
+      }
+#pragma unroll
+      for (int u = 0; u < OUTS_LB; ++u)
+#pragma unroll
+        for (int c = 0; c < NCLS; ++c) acc[c] = fmaf(hv[u], dl[u][c], acc[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) part[(q * OUTS_ROWS + r) * NCLS + c] = acc[c];
+  __syncthreads();
+  if (t < OUTS_ROWS * NCLS) {
+    const int rr = t / NCLS, c = t - rr * NCLS, mm = blk * OUTS_ROWS + rr;
+    float g = 0.f;
+#pragma unroll
+    for (int qq = 0; qq < OUTS_GROUPS; ++qq) g += part[(qq * OUTS_ROWS + rr) * NCLS + c];
+    if (mm <= HID) {
+      const size_t o = OFF_OUT + (size_t)mm * NCLS + c;
+      if (a.gbf_a) a.gbf_a[o] = f2bf_bits(g);
+      else a.grad[o] = g;
+    }
+  }
+}
+
+// [output-layer blocks | fc1 dW (+ bias row) tiles over K = W*B]
+__global__ __launch_bounds__(256) void fc_grad_sfb(MnistStepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  int id = blockIdx.x;
+  if (id < OUTS_BLOCKS) { out_grad_sfb_block(a, id, (float*)smem_raw); return; }
+  id -= OUTS_BLOCKS;
+  const int WB = a.sfb_world * a.B;
+  OnesRowMC la{a.sfb_p2, FEAT, FEAT, WB};
+  RankRowsMC lb{a.sfb_dr, HID, HID, WB, a.B, a.sfb_rs};
+  GradEpi epi{a.grad + OFF_WD1, a.gbf_a ? a.gbf_a + OFF_WD1 : nullptr, HID, FEAT + 1, HID};
+  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(
+      la, lb, epi, (id / FDW_GX) * FDW_BM, (id % FDW_GX) * FDW_BN, 0, WB, (bf16*)smem_raw);
+}
+
 // ---------------- K13 conv2 dgrad (+ conv1 relu/pool mask epilogue) ----------------
 struct Conv2DgradA {  // (m = (b,ih,iw), k = tap*64 + co)
   static constexpr bool KC = true;
@@ -1899,6 +1989,17 @@ void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_
 void mnist_adam_fc(const MnistStepArgs& a, MnistAdamArgs o, hipStream_t s, int blocks) {
   o.fc_only = 1;
   mnist_adam_kernel<<<blocks > 0 ? blocks : MAD_FC_BLOCKS, MAD_NT, 0, s>>>(a, o);
+}
+
+int64_t mnist_sfb_slot_elems(int B) { return ((int64_t)B * (2 * HID + 2 * NCLS) + 63) / 64 * 64; }
+
+void mnist_fc_grad_sfb(const MnistStepArgs& a, hipStream_t s) {
+  if (a.sfb_world < 1 || !a.sfb_p2 || !a.sfb_dr) throw std::runtime_error("mnist_fc_grad_sfb: no gathered factors");
+  constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, RankRowsMC>::BYTES;
+  constexpr int sm_og = OUTS_ROWS * OUTS_GROUPS * NCLS * 4;
+  constexpr int sm = sm_dw > sm_og ? sm_dw : sm_og;
+  set_smem<fc_grad_sfb>(sm);
+  fc_grad_sfb<<<OUTS_BLOCKS + FDW_GX * FDW_GY, 256, sm, s>>>(a);
 }
 
 void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s) {

@@ -79,6 +79,9 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipEventCreateWithFlags(&ev_ag_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_p2_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_dx_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_sfb_, hipEventDisableTiming));
     for (auto& e : pev_) HIP_OK(hipEventCreate(&e));  // timing events (phase timer)
   }
   ~MnistEngine() override {
@@ -94,6 +97,9 @@ class MnistEngine : public torch::CustomClassHolder {
     hipEventDestroy(ev_opt_a_);
     hipEventDestroy(ev_start_);
     hipEventDestroy(ev_ag_);
+    hipEventDestroy(ev_p2_);
+    hipEventDestroy(ev_dx_);
+    hipEventDestroy(ev_sfb_);
     for (auto& e : pev_) hipEventDestroy(e);
   }
 
@@ -108,8 +114,15 @@ class MnistEngine : public torch::CustomClassHolder {
   at::Tensor step_tensor() { return step_; }
   at::Tensor loss_rows() { return loss_row_; }
   at::Tensor correct_rows() { return correct_row_; }
-  at::Tensor hidden() { return fp32_ ? fhd_ : hd_; }
-  at::Tensor pool2() { return p2_; }
+  at::Tensor hidden() {
+    if (fp32_) return fhd_;
+    if (sfb_active()) return sfdr_.narrow(0, rank_in_comm() * sfb_rs_ + B_ * HID, B_ * HID).view({B_, HID});
+    return hd_;
+  }
+  at::Tensor pool2() {
+    if (sfb_active()) return sfp2_.narrow(0, rank_in_comm() * B_ * FEAT, B_ * FEAT).view({B_, FEAT});
+    return p2_;
+  }
   at::Tensor pool1() { return p1_; }
   at::Tensor feed_x() { return xbuf_; }
   at::Tensor feed_y() { return ybuf_; }
@@ -177,6 +190,7 @@ class MnistEngine : public torch::CustomClassHolder {
   // the reference's round-robin parameter sharding across PS tasks.
   void set_zero(bool on) {
     if (!on) { zero_ = false; return; }
+    sfb_ = false;  // ZeRO-1 shards the fc1 optimizer instead (reduce-scatter / all-gather)
     const int64_t W = world();
     TORCH_CHECK(W > 1, "set_zero: needs a communicator with world > 1");
     TORCH_CHECK((OFF_BD1 - OFF_WD1) % (W * 64) == 0, "set_zero: fc1 weight not divisible into ", W, " shards");
@@ -184,6 +198,25 @@ class MnistEngine : public torch::CustomClassHolder {
     zero_ = true;
   }
   bool zero() const { return zero_; }
+  // DP fc-region gradients by sufficient-factor broadcasting (mnist_fc_grad_sfb): all-gather the
+  // fc factors (p2 after the conv forward, dh / hd / dlogits after the head) and compute the summed
+  // fc gradients locally instead of all-reducing them. Needs the transport attached first.
+  void set_fc_sfb(bool on) {
+    if (!on) { sfb_ = false; return; }
+    TORCH_CHECK(comm_ || ipc_, "set_fc_sfb: attach a communicator first");
+    TORCH_CHECK(!zero_, "set_fc_sfb: ZeRO-1 is on");
+    const int64_t W = world();
+    sfb_rs_ = mnist_sfb_slot_elems((int)B_);
+    auto bf = at::TensorOptions().dtype(at::kBFloat16).device(at::kCUDA, device_);
+    if (!sfp2_.defined() || sfp2_.numel() != W * B_ * FEAT) {
+      sfp2_ = at::zeros({W * B_ * FEAT}, bf);
+      sfdr_ = at::zeros({W * sfb_rs_}, bf);
+    }
+    sfb_ = true;
+  }
+  bool fc_sfb() const { return sfb_active(); }
+  // bf16 elements of the larger of the two per-rank gather shards (IPC staging must hold it)
+  int64_t sfb_shard_elems() const { return std::max<int64_t>(B_ * FEAT, mnist_sfb_slot_elems((int)B_)); }
   // conv2 wgrad on a forked stream beside dgrad -> conv1 wgrad (1) or all on the main stream (0)
   void set_conv_fork(int64_t on) { conv_fork_ = on != 0; }
   void set_fused_tail(int64_t on) { fuse_tail_ = on != 0; }
@@ -332,7 +365,8 @@ class MnistEngine : public torch::CustomClassHolder {
       return;
     }
     if (dp) {
-      train_step_dp(join_end);
+      if (sfb_active()) train_step_sfb(join_end);
+      else train_step_dp(join_end);
       return;
     }
     mark(P_START, s);
@@ -499,6 +533,76 @@ class MnistEngine : public torch::CustomClassHolder {
     else pending_opt_a_ = true;
   }
 
+  // DP step with sufficient-factor fc gradients, three streams (main s, comm c, optimizer o):
+  //   s: [wait o: previous step's SFB GEMM done with the gathered factors] conv fwd (p2 -> own slot)
+  //      -> [wait o: previous fc optimizer] fc fwd + head (dh / hd / dlogits -> own slot) -> fc1 dX
+  //      -> conv bwd -> conv-slab reduce (bucket B bf16, step bump) -> [wait c] conv-region optimizer
+  //   c: [wait p2] all-gather p2 (overlaps fc fwd + head) -> [wait head] all-gather dh|hd|dlogits
+  //      -> [wait B] all-reduce B
+  //   o: [wait gathers] fc gradients over K = W*B (mnist_fc_grad_sfb) -> [wait dX: it reads the old
+  //      fc1 weights] fc-region optimizer
+  // Cross-step overlap as in train_step_dp: the fc optimizer runs beside the next conv forward.
+  void train_step_sfb(bool join_end) {
+    hipStream_t s = stream();
+    const double scale = 1.0 / (double)world();
+    const bool bf = bf16_comm_;
+    MnistStepArgs a = args();
+    a.t_out = (int64_t*)tnext_.data_ptr();
+    a.step_bump = (int64_t*)step_.data_ptr();
+    if (bf) {
+      a.gbf_a = (uint16_t*)gbf_.data_ptr();
+      a.gbf_b = (uint16_t*)gbf_.data_ptr();
+    }
+    mark(P_START, s);
+    if (pending_sfb_) {
+      HIP_OK(hipStreamWaitEvent(s, ev_sfb_, 0));
+      pending_sfb_ = false;
+    }
+    mnist_forward_conv(a, s);
+    HIP_OK(hipEventRecord(ev_p2_, s));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_p2_, 0));
+    mark(P_CA0, comm_stream_);
+    gather_sfb(true, comm_stream_);
+    if (pending_opt_a_) {
+      HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+      pending_opt_a_ = false;
+    }
+    mnist_forward_fc(a, true, s);
+    mark(P_FWD, s);
+    HIP_OK(hipEventRecord(ev_a_, s));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
+    gather_sfb(false, comm_stream_);
+    mark(P_CA1, comm_stream_);
+    HIP_OK(hipEventRecord(ev_ag_, comm_stream_));
+    HIP_OK(hipStreamWaitEvent(opt_stream_, ev_ag_, 0));
+    mnist_fc_grad_sfb(a, opt_stream_);
+    HIP_OK(hipEventRecord(ev_sfb_, opt_stream_));
+    mnist_backward_a(a, s, 2);  // fc1 dX from this rank's own rows
+    mark(P_BFC, s);
+    HIP_OK(hipEventRecord(ev_dx_, s));
+    HIP_OK(hipStreamWaitEvent(opt_stream_, ev_dx_, 0));
+    apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 0, opt_stream_, (const int64_t*)tnext_.data_ptr());
+    HIP_OK(hipEventRecord(ev_opt_a_, opt_stream_));
+    mnist_backward_b(a, s, conv_fork_ ? aux_stream_ : nullptr, ev_fork_, ev_join_);
+    mnist_conv_grad_reduce(a, s);
+    mark(P_BCONV, s);
+    HIP_OK(hipEventRecord(ev_b_, s));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
+    mark(P_CB0, comm_stream_);
+    reduce_bucket(0, BUCKET_SPLIT, bf);
+    mark(P_CB1, comm_stream_);
+    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+    apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s);
+    mark(P_OPT, s);
+    if (join_end) {
+      HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));  // after ev_sfb_ on the same stream: covers both
+    } else {
+      pending_opt_a_ = true;
+      pending_sfb_ = true;
+    }
+  }
+
   // fp32 step: forward, backward (fc grads + conv slabs), slab reduce + step bump, [fp32
   // all-reduce of the whole buffer], optimizer (t = bumped step).
   void train_step_f32(bool dp) {
@@ -545,7 +649,14 @@ class MnistEngine : public torch::CustomClassHolder {
     mnist_forward_conv(a, s);
     HIP_OK(hipStreamWaitEvent(s, ev_ag_, 0));
     mnist_forward_fc(a, true, s);
-    if (fused_bf16_a()) a.gbf_a = (uint16_t*)gbf_.data_ptr();
+    // bf16 wire format for both buckets, produced by the kernels themselves -- the same rounding
+    // points as train_step_dp (the conv bucket used to be summed from fp32 and rounded after the
+    // sum here, so ZeRO and replicated DP differed by bf16 rounding of the conv gradients)
+    const bool pre_b = fused_bf16_a();
+    if (pre_b) {
+      a.gbf_a = (uint16_t*)gbf_.data_ptr();
+      a.gbf_b = (uint16_t*)gbf_.data_ptr();
+    }
     mnist_backward_a(a, s);
     HIP_OK(hipEventRecord(ev_a_, s));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
@@ -560,7 +671,7 @@ class MnistEngine : public torch::CustomClassHolder {
     mnist_conv_grad_reduce(a, s);
     HIP_OK(hipEventRecord(ev_b_, s));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
-    reduce_bucket(0, BUCKET_SPLIT, false);
+    reduce_bucket(0, BUCKET_SPLIT, pre_b);
     HIP_OK(hipEventRecord(ev_done_, comm_stream_));
     HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
     apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s);
@@ -689,6 +800,21 @@ class MnistEngine : public torch::CustomClassHolder {
     else ipc_->all_gather_raw(pb, 2, S, st);
   }
 
+  bool sfb_active() const { return sfb_ && !zero_ && !fp32_ && dp() && sfp2_.defined(); }
+  // in-place all-gather of one SFB factor array ([W][S], this rank's shard at r*S): IPC when its
+  // staging holds the shard (one kernel reading every peer at once), else RCCL
+  void gather_sfb(bool p2part, hipStream_t st) {
+    const int64_t r = rank_in_comm();
+    uint16_t* base = (uint16_t*)(p2part ? sfp2_ : sfdr_).data_ptr();
+    const int64_t S = p2part ? B_ * FEAT : sfb_rs_;
+    if (ipc_ && ipc_->capacity() * 2 >= S) {
+      ipc_->all_gather_raw(base, 2, S, st);
+      return;
+    }
+    TORCH_CHECK(comm_, "SFB gather: no communicator holds a ", S, "-element shard");
+    comm_->all_gather_raw(base + r * S, base, (size_t)S, ncclBfloat16, st);
+  }
+
   // bucket A's gradients come out of the fc backward as bf16 in gbf_ (MnistStepArgs::gbf_a)
   bool fused_bf16_a() const { return bf16_comm_ && dp(); }
   bool in_gbf(int64_t beg) const { return fused_bf16_a() && beg >= BUCKET_SPLIT; }
@@ -791,6 +917,18 @@ class MnistEngine : public torch::CustomClassHolder {
     a.xpre = input_mode_ == 1 ? (float*)xpre_.data_ptr() : nullptr;
     a.ypre = input_mode_ == 1 ? (int*)ypre_.data_ptr() : nullptr;
     a.dbg = dbg_.defined() ? (int64_t*)dbg_.data_ptr() : nullptr;
+    if (sfb_active()) {
+      const int64_t r = rank_in_comm();
+      uint16_t* slot = (uint16_t*)sfdr_.data_ptr() + r * sfb_rs_;
+      a.p2 = (uint16_t*)sfp2_.data_ptr() + r * B_ * FEAT;
+      a.dh = slot;
+      a.hd = slot + B_ * HID;
+      a.dlogits = reinterpret_cast<float*>(slot + 2 * B_ * HID);
+      a.sfb_world = (int)world();
+      a.sfb_p2 = (const uint16_t*)sfp2_.data_ptr();
+      a.sfb_dr = (const uint16_t*)sfdr_.data_ptr();
+      a.sfb_rs = sfb_rs_;
+    }
     return a;
   }
 
@@ -820,6 +958,11 @@ class MnistEngine : public torch::CustomClassHolder {
   bool force_dp_ = false;
   int64_t zshard_ = 0;
   bool pending_opt_a_ = false;  // DP: the main stream still has to wait for the fc optimizer
+  // sufficient-factor fc gradients (set_fc_sfb): gathered factors, slot stride, events
+  bool sfb_ = false, pending_sfb_ = false;
+  at::Tensor sfp2_, sfdr_;
+  int64_t sfb_rs_ = 0;
+  hipEvent_t ev_p2_ = nullptr, ev_dx_ = nullptr, ev_sfb_ = nullptr;
   // measured on one MI355X: the forked conv2 wgrad only contends with dgrad for CUs (110 vs 100 us/step)
   bool conv_fork_ = false;
   // one GPU + Adam: the optimizer kernel also reduces the conv gradient slabs and bumps the step
@@ -874,6 +1017,9 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_comm", &MnistEngine::set_comm)
       .def("set_ipc", &MnistEngine::set_ipc)
       .def("set_zero", &MnistEngine::set_zero)
+      .def("set_fc_sfb", &MnistEngine::set_fc_sfb)
+      .def("fc_sfb", &MnistEngine::fc_sfb)
+      .def("sfb_shard_elems", &MnistEngine::sfb_shard_elems)
       .def("set_force_dp", &MnistEngine::set_force_dp)
       .def("dp", &MnistEngine::dp)
       .def("set_conv_fork", &MnistEngine::set_conv_fork)

@@ -54,6 +54,14 @@ struct MnistStepArgs {
   float* xpre;
   int* ypre;
   int64_t* dbg;                // timing-stamp builds only (TFD_STAMP): per-block phase clocks
+  // DP with sufficient-factor gradients (mnist_fc_grad_sfb): the fc-layer factors of ALL ranks,
+  // all-gathered. sfb_p2 = [W*B][3136] pooled conv2 activations (rank r's rows at r*B; rank r's p2
+  // IS its slot); sfb_dr = [W][sfb_rs] per-rank slots holding dh [B][1024] bf16, hd [B][1024] bf16
+  // and dlogits [B][10] fp32, in that order (this rank's dh / hd / dlogits point into its slot).
+  int sfb_world;
+  const uint16_t* sfb_p2;
+  const uint16_t* sfb_dr;
+  int64_t sfb_rs;
 };
 
 int mnist_fc1_splits(int B);
@@ -87,6 +95,13 @@ void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_
 // The fc region alone (`blocks` grid-stride blocks, default 1024), e.g. on a side stream beside the
 // conv backward; mnist_adam_fused(..., fc_region = false) then finishes the step.
 void mnist_adam_fc(const MnistStepArgs& a, MnistAdamArgs o, hipStream_t s, int blocks = 0);
+// DP, sufficient-factor broadcasting: every fc-layer weight gradient is a sum of per-example outer
+// products (dW_fc1 = [P2;1]^T dH, dW_out = [Hd;1]^T dlogits), so the all-reduced gradient is ONE
+// GEMM over the all-gathered factors (K = W*B). Writes the summed fc-region gradients (bucket A)
+// like mnist_backward_a part 1 (bf16 into gbf_a when set), identical on every rank.
+void mnist_fc_grad_sfb(const MnistStepArgs& a, hipStream_t s);
+// bf16 elements of one rank's sfb_dr slot for batch B (dh + hd + dlogits, padded to 64)
+int64_t mnist_sfb_slot_elems(int B);
 // One GPU: fc1 dW and the output-layer gradients with ApplyAdam fused into their epilogues (the fc
 // gradients never reach memory; t = global_step + 1). Launch after the dX GEMM (part 2).
 void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s);

@@ -97,12 +97,16 @@ class DPTransport:
 
 def attach_engine(eng, rank: int, world: int, device: torch.device, group=None, src: int = 0,
                   mode: str = "auto", comm=None, bf16: bool = True, small_ipc: bool = True,
-                  force_dp: bool = False, capacity: Optional[int] = None, log=None) -> DPTransport:
+                  force_dp: bool = False, capacity: Optional[int] = None, log=None,
+                  sfb: bool = False) -> DPTransport:
     """Give ``eng`` (``MnistEngine``) its gradient transport.
 
     mode: ``auto`` (IPC everywhere when ranks share a GPU, else RCCL + IPC small bucket),
     ``rccl``, ``ipc``. ``comm``: an existing RCCL communicator to reuse. ``force_dp`` with world 1
     runs the full DP schedule over a world-1 communicator (one-GPU coverage of the RCCL path).
+    ``sfb``: fc-region gradients by sufficient-factor broadcasting (``MnistEngine.set_fc_sfb``: the
+    fc factors are all-gathered -- over IPC when its staging holds them -- instead of all-reducing
+    the 6.4 MB fc gradient).
     """
     from ..models import mnist_cnn as M
     from .ipc import make_ipc_comm
@@ -114,12 +118,22 @@ def attach_engine(eng, rank: int, world: int, device: torch.device, group=None, 
     if mode == "auto":
         mode = "ipc" if shared else "rccl"
     cap = capacity or M.TOTAL
+    # IPC staging (fp32 units) that also holds one SFB gather shard (bf16 elements)
+    small_cap = max(M.BUCKET_SPLIT, (int(eng.sfb_shard_elems()) + 1) // 2) if sfb else M.BUCKET_SPLIT
+
+    def _sfb(tr: DPTransport) -> DPTransport:
+        if sfb and bf16:
+            eng.set_fc_sfb(True)
+            tr.kind += "+sfb"
+        return tr
+
     if mode == "ipc":
-        ipc = make_ipc_comm(rank, world, device.index or 0, cap, group=group, max_blocks=8 if shared else 64)
+        ipc = make_ipc_comm(rank, world, device.index or 0, max(cap, small_cap), group=group,
+                            max_blocks=8 if shared else 64)
         eng.set_ipc(ipc, cap, bf16)
         if force_dp:
             eng.set_force_dp(True)
-        return DPTransport("ipc", ipc=ipc)
+        return _sfb(DPTransport("ipc", ipc=ipc))
     if mode != "rccl":
         raise ValueError(f"unknown DP transport {mode!r}")
     if comm is None:
@@ -131,7 +145,7 @@ def attach_engine(eng, rank: int, world: int, device: torch.device, group=None, 
     if small_ipc and world > 1:
         ok, ipc = 0, None
         try:
-            ipc = make_ipc_comm(rank, world, device.index or 0, M.BUCKET_SPLIT, group=group)
+            ipc = make_ipc_comm(rank, world, device.index or 0, small_cap, group=group, max_blocks=64)
             ok = int(ipc_self_check(ipc, comm, M.BUCKET_SPLIT, device))
         except Exception as e:  # pragma: no cover - depends on the node's IPC support
             log(f"# ipc setup failed: {e!r}")
@@ -139,8 +153,8 @@ def attach_engine(eng, rank: int, world: int, device: torch.device, group=None, 
         dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)  # every rank must agree
         if int(flags.item()) == 0:
             eng.set_ipc(ipc, M.BUCKET_SPLIT, bf16)
-            return DPTransport("rccl+ipc", comm=comm, ipc=ipc)
+            return _sfb(DPTransport("rccl+ipc", comm=comm, ipc=ipc))
         log("# ipc self-check failed; the conv bucket stays on RCCL")
         if ipc is not None:
             ipc.close()
-    return DPTransport(kind, comm=comm)
+    return _sfb(DPTransport(kind, comm=comm))

@@ -70,6 +70,37 @@ def test_forced_dp_world1_gradients_are_the_fused_gradients(cuda, mode):
 
 
 @pytest.mark.parametrize("mode", ["rccl", "ipc"])
+def test_forced_dp_world1_sfb_gradients_are_the_fused_gradients(cuda, mode):
+    """Sufficient-factor fc gradients at world 1 (gather of the own factors, GEMM over K = B):
+    fc1 dW + bias are the one-GPU step's fp32 gradients rounded to bf16 bit for bit (same GEMM, same
+    K order); the output layer sums its rows in a different fixed order (<= 1 bf16 ulp)."""
+    from tensorflow_distributed_amd.parallel.transport import attach_engine
+
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        params, (ref, dp) = _engines_on_dataset(cuda, 2, keep=1.0, sgd=True)
+        tr = attach_engine(dp, 0, 1, cuda, mode=mode, force_dp=True, sfb=True)
+        assert tr.kind == mode + "+sfb" and dp.fc_sfb()
+        ref.train_step()
+        dp.train_step()
+    torch.cuda.synchronize()
+    tr.check()
+    g_ref = ref.grads().to(torch.bfloat16)
+    g_dp = dp.grads_bf16()
+    out = M.OFFSETS["out"]  # output layer [1024][10] + bias: summed in a different fixed order
+    assert torch.equal(g_dp[:out], g_ref[:out]), (g_dp[:out].float() - g_ref[:out].float()).abs().max().item()
+    torch.testing.assert_close(g_dp[out:].float(), g_ref[out:].float(), rtol=1.6e-2, atol=1e-6)
+    with torch.cuda.stream(s):  # more steps, eager and captured: the cross-step factor waits
+        dp.train_step()
+        dp.capture_train_steps("t", 3)
+        dp.replay("t", 2)
+    torch.cuda.synchronize()
+    tr.check()
+    assert int(dp.step_tensor().item()) == 8 and torch.isfinite(dp.params()).all()
+    tr.close()
+
+
+@pytest.mark.parametrize("mode", ["rccl", "ipc"])
 def test_forced_dp_world1_captured_steps_track_fused(cuda, mode):
     """Two eager + two graph-replayed steps (captured collectives) with dropout and Adam: same
     update direction as the fused one-GPU step (Adam's m/sqrt(v) amplifies the bf16 wire rounding
@@ -140,9 +171,12 @@ def _bench(args, nproc=1, timeout=300):
     return json.loads(lines[0])
 
 
-def test_bench_two_ranks_one_gpu_over_ipc(cuda):
-    r = _bench(["--gpus", "2", "--steps", "20", "--warmup", "5", "--min_warmup_ms", "50"], nproc=2)
-    assert r["n_gpus"] == 2 and r["config"]["dp_transport"] == "ipc" and r["config"]["parallelism"] == "dp2"
+@pytest.mark.parametrize("sfb", [1, 0])
+def test_bench_two_ranks_one_gpu_over_ipc(cuda, sfb):
+    r = _bench(["--gpus", "2", "--steps", "20", "--warmup", "5", "--min_warmup_ms", "50", "--fc_sfb", str(sfb)],
+               nproc=2)
+    kind = "ipc+sfb" if sfb else "ipc"
+    assert r["n_gpus"] == 2 and r["config"]["dp_transport"] == kind and r["config"]["parallelism"] == "dp2"
     assert r["value"] > 0 and r["config"]["global_batch"] == 256
     assert r["phases_ms"]["allreduce"] > 0, r["phases_ms"]
 
@@ -152,9 +186,11 @@ def test_bench_fp32_dtype(cuda):
     assert r["dtype"] == "fp32" and r["config"]["grad_allreduce"] == "fp32" and r["value"] > 0
 
 
-def test_bench_forced_dp_world1_rccl(cuda):
-    r = _bench(["--steps", "20", "--warmup", "5", "--force_dp", "1", "--min_warmup_ms", "50"])
-    assert r["config"]["dp_transport"] == "rccl" and r["config"]["force_dp"] and r["config"]["hipgraph"]
+@pytest.mark.parametrize("sfb", [1, 0])
+def test_bench_forced_dp_world1_rccl(cuda, sfb):
+    r = _bench(["--steps", "20", "--warmup", "5", "--force_dp", "1", "--min_warmup_ms", "50", "--fc_sfb", str(sfb)])
+    kind = "rccl+sfb" if sfb else "rccl"
+    assert r["config"]["dp_transport"] == kind and r["config"]["force_dp"] and r["config"]["hipgraph"]
 
 
 def test_dist_main_resnet18_two_workers_one_gpu(tmp_path):

@@ -168,7 +168,9 @@ def test_backup_workers_tolerate_a_straggler(tmp_path):
     assert r["ok"], r["outputs"]
     fast = [float(re.search(r"Training elapsed time: ([0-9.]+) s", _out(r, f"worker:{i}")).group(1)) for i in (0, 1)]
     slow = float(re.search(r"Training elapsed time: ([0-9.]+) s", _out(r, "worker:2")).group(1))
-    assert max(fast) < 6.0 < slow, (fast, slow)
+    # relative bound: the fast workers' time must not contain the straggler's 8 s stalls (an
+    # absolute bound flaked when the suite ran under pytest-xdist on a loaded host)
+    assert slow > 8.0 and max(fast) < 0.5 * slow, (fast, slow)
     assert "stale gradient dropped" in _out(r, "worker:2")
     m = re.search(r"(\d+) synchronous updates, (\d+) stale gradients dropped", _out(r, "ps:0"))
     assert m and int(m.group(1)) == 6 and int(m.group(2)) >= 1, _out(r, "ps:0")
