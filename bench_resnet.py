@@ -29,6 +29,10 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bucket_mb", type=float, default=8.0)
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--bn_stats", type=int, default=1, help="1: batch-norm statistics summed in the conv "
+                    "forward epilogue (no separate statistics pass over the conv output)")
+    ap.add_argument("--mask_from_y", type=int, default=1, help="1: residual-free BN backward recomputes its relu "
+                    "mask from the conv output instead of reading the BN output")
     ap.add_argument("--fuse_joins", type=int, default=0, help="1: residual-join gradient sums in the dgrad "
                     "epilogue (0: autograd adds; measured faster, see resnet.GradJoin)")
     ap.add_argument("--lr", type=float, default=0.1)
@@ -43,7 +47,9 @@ def main(argv=None):
     _native.require()
     ctx = D.init_from_env(use_gpu=True)
     dev = ctx.device
-    m = ResNet(a.depth, num_classes=1000, device=dev, seed=0, fuse_joins=bool(a.fuse_joins))
+    m = ResNet(a.depth, num_classes=1000, device=dev, seed=0, fuse_joins=bool(a.fuse_joins),
+               bn_stats=bool(a.bn_stats))
+    m.mask_from_y = bool(a.mask_from_y)
     if ctx.comm is not None:
         ctx.comm.broadcast(m.fp.master, 0)
         m.fp.shadow.copy_(m.fp.master)
@@ -95,7 +101,8 @@ def main(argv=None):
             "config": {"model": f"resnet{a.depth} v1.5 NHWC", "global_batch": ctx.world * a.batch_size,
                        "per_gpu_batch": a.batch_size, "seq_len": None, "parallelism": f"dp{ctx.world}",
                        "bucket_mb": a.bucket_mb, "optimizer": "sgd-momentum 0.9 wd 1e-4",
-                       "hipgraph": not a.eager, "fuse_joins": bool(a.fuse_joins)}}), flush=True)
+                       "hipgraph": not a.eager, "fuse_joins": bool(a.fuse_joins), "bn_stats": bool(a.bn_stats),
+                       "mask_from_y": bool(a.mask_from_y)}}), flush=True)
     ctx.shutdown()
     return 0
 

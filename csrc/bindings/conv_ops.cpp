@@ -33,7 +33,9 @@ ConvShape shape_of(const at::Tensor& x, const at::Tensor& w, int64_t stride, int
   TORCH_CHECK(w.size(2) == c.C, "conv: filter C ", w.size(2), " != input C ", c.C);
   TORCH_CHECK(c.C % 8 == 0 && c.K % 8 == 0, "conv: C and K must be multiples of 8 (pad the input channels)");
   TORCH_CHECK(c.Ho() > 0 && c.Wo() > 0 && stride >= 1 && pad >= 0, "conv: bad geometry");
-  TORCH_CHECK((int64_t)c.N * c.H * c.W * c.C < (1ll << 31), "conv: tensor too large for 32-bit indexing");
+  // the GEMM loaders address operands through 32-bit buffer descriptors (byte ranges < 2 GiB)
+  TORCH_CHECK((int64_t)c.N * c.H * c.W * c.C < (1ll << 30) && (int64_t)c.N * c.Ho() * c.Wo() * c.K < (1ll << 30),
+              "conv: tensor too large for 32-bit buffer addressing");
   return c;
 }
 
@@ -44,6 +46,17 @@ at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
   auto y = at::empty({c.N, c.Ho(), c.Wo(), c.K}, x.options());
   conv_fwd(c, bp(x), bp(w), bp(y), cur());
   return y;
+}
+
+std::tuple<at::Tensor, at::Tensor> conv2d_fwd_stats(const at::Tensor& x, const at::Tensor& w, int64_t stride,
+                                                    int64_t pad) {
+  check_bf16(x, "x", 4);
+  check_bf16(w, "w", 4);
+  const ConvShape c = shape_of(x, w, stride, pad);
+  auto y = at::empty({c.N, c.Ho(), c.Wo(), c.K}, x.options());
+  auto part = at::empty({conv_fwd_stats_rows(c), 2, c.K}, x.options().dtype(at::kFloat));
+  conv_fwd_stats(c, bp(x), bp(w), bp(y), fp(part), cur());
+  return {y, part};
 }
 
 at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, at::IntArrayRef xshape, int64_t stride, int64_t pad,
@@ -104,7 +117,8 @@ void linear_wgrad_op(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw) {
 std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& y, const at::Tensor& gamma,
                                                       const at::Tensor& beta, const c10::optional<at::Tensor>& res,
                                                       bool relu, at::Tensor running_mean, at::Tensor running_var,
-                                                      double momentum, double eps) {
+                                                      double momentum, double eps,
+                                                      const c10::optional<at::Tensor>& partials) {
   check_bf16(y, "y", -1);
   const int C = (int)y.size(-1);
   const int M = (int)(y.numel() / C);
@@ -118,17 +132,26 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& y, const
   auto out = at::empty_like(y);
   auto f = y.options().dtype(at::kFloat);
   auto mean = at::empty({C}, f), invstd = at::empty({C}, f);
+  float* rm = running_mean.defined() && running_mean.numel() ? fp(running_mean) : nullptr;
+  float* rv = running_var.defined() && running_var.numel() ? fp(running_var) : nullptr;
+  if (partials.has_value()) {  // statistics already summed by the producing conv (conv2d_fwd_stats)
+    check_f32(*partials, "partials");
+    TORCH_CHECK(partials->dim() == 3 && partials->size(1) == 2 && partials->size(2) == C, "bn: partials [nblk,2,C]");
+    bn_forward_partials(bp(y), fp(gamma), fp(beta), res ? bp(*res) : nullptr, relu ? 1 : 0, bp(out), fp(mean),
+                        fp(invstd), rm, rv, (float)momentum, (float)eps, M, C, fp(*partials),
+                        (int)partials->size(0), cur());
+    return {out, mean, invstd};
+  }
   auto part = at::empty({bn_partials_size(M, C)}, f);
-  bn_forward(bp(y), fp(gamma), fp(beta), res ? bp(*res) : nullptr, relu ? 1 : 0, bp(out), fp(mean), fp(invstd),
-             running_mean.defined() && running_mean.numel() ? fp(running_mean) : nullptr,
-             running_var.defined() && running_var.numel() ? fp(running_var) : nullptr, (float)momentum, (float)eps, M,
-             C, fp(part), cur());
+  bn_forward(bp(y), fp(gamma), fp(beta), res ? bp(*res) : nullptr, relu ? 1 : 0, bp(out), fp(mean), fp(invstd), rm, rv,
+             (float)momentum, (float)eps, M, C, fp(part), cur());
   return {out, mean, invstd};
 }
 
 std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tensor& out, const at::Tensor& y,
                                           const at::Tensor& gamma, const at::Tensor& mean, const at::Tensor& invstd,
-                                          bool relu, bool want_dres, at::Tensor dgamma, at::Tensor dbeta) {
+                                          bool relu, bool want_dres, at::Tensor dgamma, at::Tensor dbeta,
+                                          const c10::optional<at::Tensor>& beta) {
   check_bf16(dout, "dout", -1);
   check_bf16(out, "out", -1);
   check_bf16(y, "y", -1);
@@ -139,8 +162,9 @@ std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tens
   auto dy = at::empty_like(y);
   at::Tensor dres = want_dres ? at::empty_like(y) : at::Tensor();
   auto part = at::empty({bn_partials_size(M, C)}, y.options().dtype(at::kFloat));
-  bn_backward(bp(dout), bp(out), bp(y), fp(gamma), fp(mean), fp(invstd), relu ? 1 : 0, bp(dy),
-              want_dres ? bp(dres) : nullptr, fp(dgamma), fp(dbeta), M, C, fp(part), cur());
+  if (beta) check_f32(*beta, "beta");
+  bn_backward(bp(dout), bp(out), bp(y), fp(gamma), beta ? fp(*beta) : nullptr, fp(mean), fp(invstd), relu ? 1 : 0,
+              bp(dy), want_dres ? bp(dres) : nullptr, fp(dgamma), fp(dbeta), M, C, fp(part), cur());
   return {dy, dres};
 }
 
@@ -216,6 +240,8 @@ at::Tensor pad_channels_op(const at::Tensor& x, int64_t cout) {
 TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.def("conv2d_fwd(Tensor x, Tensor w, int stride, int pad) -> Tensor");
   m.impl("conv2d_fwd", c10::DispatchKey::CUDA, &conv2d_fwd);
+  m.def("conv2d_fwd_stats(Tensor x, Tensor w, int stride, int pad) -> (Tensor, Tensor)");
+  m.impl("conv2d_fwd_stats", c10::DispatchKey::CUDA, &conv2d_fwd_stats);
   m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc=None) -> Tensor");
   m.impl("conv2d_dgrad", c10::DispatchKey::CUDA, &conv2d_dgrad);
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad, bool zeroed=False) -> ()");
@@ -227,10 +253,10 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.def("linear_wgrad(Tensor x, Tensor dy, Tensor(a!) dw) -> ()");
   m.impl("linear_wgrad", c10::DispatchKey::CUDA, &linear_wgrad_op);
   m.def("bn_fwd(Tensor y, Tensor gamma, Tensor beta, Tensor? residual, bool relu, Tensor(a!) running_mean, "
-        "Tensor(b!) running_var, float momentum, float eps) -> (Tensor, Tensor, Tensor)");
+        "Tensor(b!) running_var, float momentum, float eps, Tensor? partials=None) -> (Tensor, Tensor, Tensor)");
   m.impl("bn_fwd", c10::DispatchKey::CUDA, &bn_fwd);
   m.def("bn_bwd(Tensor dout, Tensor out, Tensor y, Tensor gamma, Tensor mean, Tensor invstd, bool relu, "
-        "bool want_dres, Tensor(a!) dgamma, Tensor(b!) dbeta) -> (Tensor, Tensor)");
+        "bool want_dres, Tensor(a!) dgamma, Tensor(b!) dbeta, Tensor? beta=None) -> (Tensor, Tensor)");
   m.impl("bn_bwd", c10::DispatchKey::CUDA, &bn_bwd);
   m.def("bn_infer(Tensor y, Tensor gamma, Tensor beta, Tensor rm, Tensor rv, float eps, bool relu) -> Tensor");
   m.impl("bn_infer", c10::DispatchKey::CUDA, &bn_infer_op);

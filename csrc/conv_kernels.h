@@ -17,6 +17,12 @@ struct ConvShape {
 };
 
 void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, hipStream_t st);
+// conv forward that also emits the batch-norm statistics of its (bf16) output: part is fp32
+// [conv_fwd_stats_rows(c)][2][K] (per-row-block sums and sums of squares), consumed by
+// bn_forward_partials -- the forward BN then never re-reads the conv output for its statistics
+int conv_fwd_stats_rows(const ConvShape& c);
+void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
+                    hipStream_t st);
 // add (optional, must not alias dx): dx = add + dgrad in the epilogue -- the residual-join sum of
 // two gradient paths without a separate add kernel
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
@@ -40,11 +46,17 @@ int bn_partials_size(int M, int C);
 void bn_forward(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
                 uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var, float momentum,
                 float eps, int M, int C, float* partials, hipStream_t st);
+// same, with the statistics partials already produced by conv_fwd_stats ([nblk][2][C])
+void bn_forward_partials(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
+                         uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var,
+                         float momentum, float eps, int M, int C, const float* partials, int nblk, hipStream_t st);
 // dout -> dy (through relu/bn), writes dgamma/dbeta (fp32, overwritten) and, when dres != null, the
 // gradient of the residual input (== gradient after the relu mask).
-void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* mean,
-                 const float* invstd, int relu, uint16_t* dy, uint16_t* dres, float* dgamma, float* dbeta, int M,
-                 int C, float* partials, hipStream_t st);
+// beta != nullptr (only valid when the forward had no residual): the relu mask is recomputed from y
+// with the forward's constants instead of reading `out`.
+void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* beta,
+                 const float* mean, const float* invstd, int relu, uint16_t* dy, uint16_t* dres, float* dgamma,
+                 float* dbeta, int M, int C, float* partials, hipStream_t st);
 // inference-mode BN (running statistics), optional relu
 void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,
               float eps, int relu, uint16_t* out, int M, int C, hipStream_t st);

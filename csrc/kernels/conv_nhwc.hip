@@ -39,7 +39,37 @@ struct Geo {
   int N, H, W, C, K, R, S, st, pad, Ho, Wo;
   int M;       // rows of the GEMM
   int KD;      // reduction length
+  uint32_t xbytes, ybytes, wbytes;  // buffer-descriptor ranges of input, output(-gradient), filter
   FastDiv howo, wo, c, k, s, hw, w;
+};
+
+// Every loader below is BRANCH-FREE: one raw buffer load (a descriptor over the whole operand,
+// built from kernel arguments, so scalar) per 16-B chunk, and an out-of-range chunk gets an offset
+// past the descriptor's range, which the hardware range check returns as zeros. With a plain load
+// under `if (in range)` the compiler emits an exec-masked branch per load and cannot count the
+// loads in flight across the joins, so a deeper register pipeline (TFD_CONV_RS > 1) degenerated to
+// vmcnt(0) waits (measured: ResNet-50 b128 19.6 -> 24.5 ms/step at RS = 2).
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOOB = 0xFFFFFFF0u;  // offset past any descriptor range (operands < 4 GiB, host-checked)
+__device__ __forceinline__ uint4 buf_ld(const uint16_t* base, uint32_t nbytes, uint32_t elem_off, bool ok) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)nbytes, 0x00020000);
+  const i32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? elem_off * 2u : kOOB, 0, 0);
+  return make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
+}
+
+// Row-major X[rows][ld] bf16 with whole 16-B chunks (lims and ld multiples of 8; host-checked):
+//  KC=true : (mn, k) = X[mn][k];  KC=false: (mn, k) = X[k][mn]
+template <bool KC_>
+struct DenseX {
+  static constexpr bool KC = KC_;
+  const uint16_t* __restrict__ x;
+  int ld, mn_lim, k_lim;
+  __device__ __forceinline__ uint4 operator()(int mn, int k) const {
+    const bool ok = mn < mn_lim && k < k_lim;
+    const uint32_t nb = (uint32_t)(KC ? mn_lim : k_lim) * (uint32_t)ld * 2u;
+    if constexpr (KC) return buf_ld(x, nb, (uint32_t)mn * ld + k, ok);
+    else return buf_ld(x, nb, (uint32_t)k * ld + mn, ok);
+  }
 };
 
 // ---- forward: A = im2col(X) (KC), B = W [KD][K] (not KC) ----
@@ -48,12 +78,11 @@ struct FwdA {
   const uint16_t* __restrict__ x;
   Geo g;
   __device__ __forceinline__ uint4 operator()(int m, int k) const {
-    if (m >= g.M || k >= g.KD) return zero4();
     const int n = g.howo.div(m), r1 = m - n * g.Ho * g.Wo, ho = g.wo.div(r1), wo = r1 - ho * g.Wo;
     const int tap = g.c.div(k), c = k - tap * g.C, r = g.s.div(tap), s = tap - r * g.S;
     const int h = ho * g.st - g.pad + r, w = wo * g.st - g.pad + s;
-    if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return zero4();
-    return *reinterpret_cast<const uint4*>(x + ((size_t)(n * g.H + h) * g.W + w) * g.C + c);
+    const bool ok = m < g.M && k < g.KD && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+    return buf_ld(x, g.xbytes, (uint32_t)((n * g.H + h) * g.W + w) * g.C + c, ok);
   }
 };
 
@@ -63,19 +92,18 @@ struct DgradA {
   const uint16_t* __restrict__ dy;
   Geo g;  // M = N*H*W, KD = R*S*K
   __device__ __forceinline__ uint4 operator()(int m, int kk) const {
-    if (m >= g.M || kk >= g.KD) return zero4();
     const int n = g.hw.div(m), r1 = m - n * g.H * g.W, h = g.w.div(r1), w = r1 - h * g.W;
     const int tap = g.k.div(kk), k = kk - tap * g.K, r = g.s.div(tap), s = tap - r * g.S;
     const int hn = h + g.pad - r, wn = w + g.pad - s;
-    if (hn < 0 || wn < 0) return zero4();
+    bool ok = m < g.M && kk < g.KD && hn >= 0 && wn >= 0;
     int ho = hn, wo = wn;
-    if (g.st != 1) {
+    if (g.st != 1) {  // uniform branch, no load inside
       ho = hn / g.st;
       wo = wn / g.st;
-      if (ho * g.st != hn || wo * g.st != wn) return zero4();
+      ok = ok && ho * g.st == hn && wo * g.st == wn;
     }
-    if (ho >= g.Ho || wo >= g.Wo) return zero4();
-    return *reinterpret_cast<const uint4*>(dy + ((size_t)(n * g.Ho + ho) * g.Wo + wo) * g.K + k);
+    ok = ok && ho < g.Ho && wo < g.Wo;
+    return buf_ld(dy, g.ybytes, (uint32_t)((n * g.Ho + ho) * g.Wo + wo) * g.K + k, ok);
   }
 };
 struct DgradB {
@@ -83,9 +111,8 @@ struct DgradB {
   const uint16_t* __restrict__ w;
   Geo g;
   __device__ __forceinline__ uint4 operator()(int c, int kk) const {
-    if (c >= g.C || kk >= g.KD) return zero4();
     const int tap = g.k.div(kk), k = kk - tap * g.K;
-    return *reinterpret_cast<const uint4*>(w + ((size_t)tap * g.C + c) * g.K + k);
+    return buf_ld(w, g.wbytes, (uint32_t)(tap * g.C + c) * g.K + k, c < g.C && kk < g.KD);
   }
 };
 
@@ -95,12 +122,11 @@ struct WgradA {
   const uint16_t* __restrict__ x;
   Geo g;  // M = R*S*C rows (taps), KD = N*Ho*Wo pixels
   __device__ __forceinline__ uint4 operator()(int t, int m) const {
-    if (t >= g.M || m >= g.KD) return zero4();
     const int tap = g.c.div(t), c = t - tap * g.C, r = g.s.div(tap), s = tap - r * g.S;
     const int n = g.howo.div(m), r1 = m - n * g.Ho * g.Wo, ho = g.wo.div(r1), wo = r1 - ho * g.Wo;
     const int h = ho * g.st - g.pad + r, w = wo * g.st - g.pad + s;
-    if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return zero4();
-    return *reinterpret_cast<const uint4*>(x + ((size_t)(n * g.H + h) * g.W + w) * g.C + c);
+    const bool ok = t < g.M && m < g.KD && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+    return buf_ld(x, g.xbytes, (uint32_t)((n * g.H + h) * g.W + w) * g.C + c, ok);
   }
 };
 
@@ -156,22 +182,123 @@ struct AccF32 {  // dW[m][n] fp32: += (atomic, split-K) or = (single split)
   }
 };
 
+// Forward conv epilogue + batch-norm statistics: bf16 store, and per-column sums of the STORED
+// (bf16-rounded) values -- exactly what bn_partial_kernel would read back -- accumulated in the
+// calling lane's registers (WANTS_IJ: j is the compile-time column-tile index after unrolling).
+template <int TN>
+struct StoreBf16Stats {
+  static constexpr bool WANTS_IJ = true;
+  uint16_t* __restrict__ y;
+  int M, N;
+  float* s;  // [TN] per-lane column sums
+  float* q;  // [TN] per-lane column sums of squares
+  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v, int i, int j) const {
+    (void)i;
+    if (n >= N) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (m4 + r < M) {
+        const uint16_t b = f2bf_bits(v[r]);
+        y[(size_t)(m4 + r) * N + n] = b;
+        const float f = bf2f(b);
+        s[j] += f;
+        q[j] = fmaf(f, f, q[j]);
+      }
+  }
+};
+
 template <int BM, int BN>
 struct Tile {
   static constexpr int WM = 2, WN = 2, BK = 64;
 };
 
+#ifndef TFD_CONV_RS  // register stages of the conv/dense GEMM core (global-load prefetch depth)
+#define TFD_CONV_RS 1
+#endif
+#ifndef TFD_CONV_BK  // K-tile of the conv/dense GEMM core (LDS per block: 2 x (BM + BN) x (BK + pad) x 2 B)
+#define TFD_CONV_BK 64
+#endif
+#ifndef TFD_CONV_WPE  // > 0: amdgpu_waves_per_eu lower bound (register budget) of the GEMM kernels
+#define TFD_CONV_WPE 0
+#endif
+#if TFD_CONV_WPE > 0
+#define TFD_CONV_ATTR __attribute__((amdgpu_waves_per_eu(TFD_CONV_WPE)))
+#else
+#define TFD_CONV_ATTR
+#endif
+constexpr int CBK = TFD_CONV_BK;
 template <int BM, int BN, class LA, class LB, class EPI>
-__global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int kchunk, int KD) {
+__global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_kernel(LA la, LB lb, EPI epi, int kchunk, int KD) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int kb = blockIdx.z * kchunk, ke = min(KD, kb + kchunk);
-  gemm_block<BM, BN, 64, 2, 2, LA, LB, EPI, 1>(la, lb, epi, blockIdx.y * BM, blockIdx.x * BN, kb, ke,
-                                               (bf16*)smem_raw);
+  gemm_block<BM, BN, CBK, 2, 2, LA, LB, EPI, TFD_CONV_RS>(la, lb, epi, blockIdx.y * BM, blockIdx.x * BN, kb, ke,
+                                                         (bf16*)smem_raw);
 }
+
+// Forward conv + BN statistics: the block's column partials (sum, sum of squares over its BM rows)
+// go to part[blockIdx.y][2][N] -- the [nblk][2][C] layout bn_final_kernel reduces -- so the
+// forward BN needs no separate pass over the conv output. Fixed reduction order (deterministic).
+template <int BM, int BN, class LA, class LB>
+__global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB lb, uint16_t* y, int M, int N, int KD,
+                                                         float* part) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  constexpr int WM = 2, WN = 2, WTN = BN / WN, TN = WTN / 16;
+  float s[TN], q[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) { s[j] = 0.f; q[j] = 0.f; }
+  StoreBf16Stats<TN> epi{y, M, N, s, q};
+  gemm_block<BM, BN, CBK, WM, WN, LA, LB, StoreBf16Stats<TN>, TFD_CONV_RS>(la, lb, epi, blockIdx.y * BM,
+                                                                          blockIdx.x * BN, 0, KD, (bf16*)smem_raw);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {  // the 4 row groups of the MFMA C layout (lane >> 4)
+    s[j] += __shfl_xor(s[j], 16, 64);
+    s[j] += __shfl_xor(s[j], 32, 64);
+    q[j] += __shfl_xor(q[j], 16, 64);
+    q[j] += __shfl_xor(q[j], 32, 64);
+  }
+  __syncthreads();  // the GEMM's LDS tiles are dead: reuse them for the cross-wave sum
+  float* red = reinterpret_cast<float*>(smem_raw);  // [WM][BN][2]
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WTN + 16 * j + lane;
+      red[(wm * BN + col) * 2] = s[j];
+      red[(wm * BN + col) * 2 + 1] = q[j];
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < BN; c += 256) {
+    const int n = blockIdx.x * BN + c;
+    if (n >= N) continue;
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) { a += red[(w * BN + c) * 2]; b += red[(w * BN + c) * 2 + 1]; }
+    part[(size_t)blockIdx.y * 2 * N + n] = a;
+    part[(size_t)blockIdx.y * 2 * N + N + n] = b;
+  }
+}
+
+template <int BM, int BN, class LA, class LB>
+void launch_gemm_stats(const LA& la, const LB& lb, uint16_t* y, int M, int N, int KD, float* part, hipStream_t st) {
+  constexpr int sm = GemmSmem<BM, BN, CBK, LA, LB>::BYTES;
+  static_assert(sm >= 2 * 2 * BN * 4, "stats reduction fits in the GEMM's LDS");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_stats_kernel<BM, BN, LA, LB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+    attr = true;
+  }
+  dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, 1);
+  gemm_stats_kernel<BM, BN, LA, LB><<<grid, 256, sm, st>>>(la, lb, y, M, N, KD, part);
+}
+
+// same tile choice as dispatch(): 128x128 when that fills the chip
+bool use_big_tiles(int M, int N) { return (long)((M + 127) / 128) * ((N + 127) / 128) >= 256 && N >= 128; }
 
 template <int BM, int BN, class LA, class LB, class EPI>
 void launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N, int KD, int splits, hipStream_t st) {
-  constexpr int sm = GemmSmem<BM, BN, 64, LA, LB>::BYTES;
+  constexpr int sm = GemmSmem<BM, BN, CBK, LA, LB>::BYTES;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BM, BN, LA, LB, EPI>),
@@ -179,7 +306,7 @@ void launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K
     attr = true;
   }
   if (splits < 1) splits = 1;
-  int kchunk = ((KD + splits - 1) / splits + 63) / 64 * 64;
+  int kchunk = ((KD + splits - 1) / splits + CBK - 1) / CBK * CBK;
   splits = (KD + kchunk - 1) / kchunk;
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, splits);
   gemm_kernel<BM, BN, LA, LB, EPI><<<grid, 256, sm, st>>>(la, lb, epi, kchunk, KD);
@@ -200,6 +327,9 @@ Geo make_geo(const ConvShape& c, int M, int KD) {
   g.M = M; g.KD = KD;
   g.howo = FastDiv(g.Ho * g.Wo); g.wo = FastDiv(g.Wo); g.c = FastDiv(g.C); g.k = FastDiv(g.K); g.s = FastDiv(g.S);
   g.hw = FastDiv(g.H * g.W); g.w = FastDiv(g.W);
+  g.xbytes = (uint32_t)((int64_t)c.N * c.H * c.W * c.C * 2);
+  g.ybytes = (uint32_t)((int64_t)c.N * g.Ho * g.Wo * c.K * 2);
+  g.wbytes = (uint32_t)((int64_t)c.R * c.S * c.C * c.K * 2);
   return g;
 }
 
@@ -210,9 +340,9 @@ bool is_pointwise(const ConvShape& c) { return c.R == 1 && c.S == 1 && c.stride 
 void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, hipStream_t st) {
   const int M = c.N * c.Ho() * c.Wo(), KD = c.R * c.S * c.C;
   StoreBf16 epi{y, M, c.K};
-  DenseLoader<false> lb{w, c.K, c.K, KD};
+  DenseX<false> lb{w, c.K, c.K, KD};
   if (is_pointwise(c)) {
-    DenseLoader<true> la{x, c.C, M, c.C};
+    DenseX<true> la{x, c.C, M, c.C};
     dispatch(la, lb, epi, M, c.K, KD, 1, st);
   } else {
     FwdA la{x, make_geo(c, M, KD)};
@@ -220,12 +350,33 @@ void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t
   }
 }
 
+int conv_fwd_stats_rows(const ConvShape& c) {
+  const int M = c.N * c.Ho() * c.Wo();
+  return use_big_tiles(M, c.K) ? (M + 127) / 128 : (M + 63) / 64;
+}
+
+void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
+                    hipStream_t st) {
+  const int M = c.N * c.Ho() * c.Wo(), KD = c.R * c.S * c.C;
+  DenseX<false> lb{w, c.K, c.K, KD};
+  const bool big = use_big_tiles(M, c.K);
+  if (is_pointwise(c)) {
+    DenseX<true> la{x, c.C, M, c.C};
+    if (big) launch_gemm_stats<128, 128>(la, lb, y, M, c.K, KD, part, st);
+    else launch_gemm_stats<64, 64>(la, lb, y, M, c.K, KD, part, st);
+  } else {
+    FwdA la{x, make_geo(c, M, KD)};
+    if (big) launch_gemm_stats<128, 128>(la, lb, y, M, c.K, KD, part, st);
+    else launch_gemm_stats<64, 64>(la, lb, y, M, c.K, KD, part, st);
+  }
+}
+
 template <class Epi>
 static void conv_dgrad_impl(const ConvShape& c, const uint16_t* dy, const uint16_t* w, Epi epi, hipStream_t st) {
   const int M = c.N * c.H * c.W, KD = c.R * c.S * c.K;
   if (is_pointwise(c)) {  // dX = dY W^T: W [C][K] read k-contiguous
-    DenseLoader<true> la{dy, c.K, M, c.K};
-    DenseLoader<true> lb{w, c.K, c.C, c.K};
+    DenseX<true> la{dy, c.K, M, c.K};
+    DenseX<true> lb{w, c.K, c.C, c.K};
     dispatch(la, lb, epi, M, c.C, KD, 1, st);
   } else {
     Geo g = make_geo(c, M, KD);
@@ -247,9 +398,9 @@ void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float
   const int P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
   if (splits > 1 && !zeroed) (void)hipMemsetAsync(dw, 0, (size_t)MT * c.K * sizeof(float), st);
   AccF32 epi{dw, MT, c.K, splits > 1 ? 1 : 0};
-  DenseLoader<false> lb{dy, c.K, c.K, P};
+  DenseX<false> lb{dy, c.K, c.K, P};
   if (is_pointwise(c)) {  // dW = X^T dY
-    DenseLoader<false> la{x, c.C, c.C, P};
+    DenseX<false> la{x, c.C, c.C, P};
     dispatch(la, lb, epi, MT, c.K, P, splits, st);
   } else {
     WgradA la{x, make_geo(c, MT, P)};
@@ -268,24 +419,24 @@ int conv_wgrad_splits(const ConvShape& c) {
 
 void linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, float* y, int M, int Kin, int N,
                 hipStream_t st) {
-  DenseLoader<true> la{x, Kin, M, Kin};
-  DenseLoader<false> lb{w, N, N, Kin};
+  DenseX<true> la{x, Kin, M, Kin};
+  DenseX<false> lb{w, N, N, Kin};
   BiasStoreF32 epi{y, bias, M, N};
   dispatch(la, lb, epi, M, N, Kin, 1, st);
 }
 
 void linear_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int Kin, int N, hipStream_t st) {
   // dX[M][Kin] = dY[M][N] W^T ; W is [Kin][N] -> B operand (n = kin, k = n) is k-contiguous
-  DenseLoader<true> la{dy, N, M, N};
-  DenseLoader<true> lb{w, N, Kin, N};
+  DenseX<true> la{dy, N, M, N};
+  DenseX<true> lb{w, N, Kin, N};
   StoreBf16 epi{dx, M, Kin};
   dispatch(la, lb, epi, M, Kin, N, 1, st);
 }
 
 void linear_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int Kin, int N, hipStream_t st) {
   // dW[Kin][N] = X^T dY over the M rows
-  DenseLoader<false> la{x, Kin, Kin, M};
-  DenseLoader<false> lb{dy, N, N, M};
+  DenseX<false> la{x, Kin, Kin, M};
+  DenseX<false> lb{dy, N, N, M};
   AccF32 epi{dw, Kin, N, 0};
   dispatch(la, lb, epi, Kin, N, M, 1, st);
 }

@@ -39,22 +39,41 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
   return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
 }
 
+// The backward's relu mask is (out > 0). Without a residual, out = relu(y * sc + sh) with the
+// forward's per-channel sc = invstd * gamma, sh = beta - mean * sc (bn_apply_kernel), so the mask
+// is recomputed from y -- the same fmaf, bit for bit -- instead of reading `out` (one bf16 array
+// less per backward pass). out == nullptr selects that form (bn_backward: residual-free BNs).
+__device__ __forceinline__ void relu_mask_from_y(const float (&v)[8], const float (&sc)[8], const float (&sh)[8],
+                                                 float (&d)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] = fmaf(v[j], sc[j], sh[j]) > 0.f ? d[j] : 0.f;
+}
+
 // partial sums of (a, b) per channel over a row chunk; mode 0: a = y, b = y^2 ; mode 1 (backward):
 // a = dz, b = dz * xhat with dz = relu-masked dout
 __global__ __launch_bounds__(NT) void bn_partial_kernel(int mode, const uint16_t* __restrict__ y,
                                                         const uint16_t* __restrict__ dout,
                                                         const uint16_t* __restrict__ out, int relu,
                                                         const float* __restrict__ mean,
-                                                        const float* __restrict__ invstd, int M, int C, int tpr,
+                                                        const float* __restrict__ invstd,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, int M, int C, int tpr,
                                                         int rg, int rb, float* __restrict__ part) {
   __shared__ float red[2][NT][8];
   const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
-  float sa[8], sb[8], mu[8], is[8];
+  float sa[8], sb[8], mu[8], is[8], sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { sa[j] = 0.f; sb[j] = 0.f; }
   if (mode == 1 && g < rg) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j]; }
+    for (int j = 0; j < 8; ++j) {
+      mu[j] = mean[c0 + j];
+      is[j] = invstd[c0 + j];
+      if (relu && !out) {
+        sc[j] = is[j] * gamma[c0 + j];
+        sh[j] = beta[c0 + j] - mu[j] * sc[j];
+      }
+    }
   }
   const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
   if (g < rg) {
@@ -68,11 +87,13 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(int mode, const uint16_t
       } else {
         float d[8];
         unpack8(*reinterpret_cast<const uint4*>(dout + o), d);
-        if (relu) {
+        if (relu && out) {
           float ov[8];
           unpack8(*reinterpret_cast<const uint4*>(out + o), ov);
 #pragma unroll
           for (int j = 0; j < 8; ++j) d[j] = ov[j] > 0.f ? d[j] : 0.f;
+        } else if (relu) {
+          relu_mask_from_y(v, sc, sh, d);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) { sa[j] += d[j]; sb[j] = fmaf(d[j], (v[j] - mu[j]) * is[j], sb[j]); }
@@ -190,7 +211,8 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict
 
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout,
                                                           const uint16_t* __restrict__ out, const uint16_t* __restrict__ y,
-                                                          const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                          const float* __restrict__ mean,
                                                           const float* __restrict__ invstd, const float* __restrict__ dbeta,
                                                           const float* __restrict__ dgamma, int relu,
                                                           uint16_t* __restrict__ dy, uint16_t* __restrict__ dres,
@@ -199,7 +221,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __rest
   if (g >= rg) return;
   // dy = k1 * dz + k2 * y + k3 with k1 = gamma*invstd, k2 = -k1*invstd*dgamma/M,
   // k3 = -k1*(dbeta/M - mean*invstd^2*dgamma/M)
-  float k1[8], k2[8], k3[8];
+  float k1[8], k2[8], k3[8], sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = c0 + j;
@@ -207,6 +229,10 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __rest
     k1[j] = gamma[c] * is;
     k2[j] = -k1[j] * is * dgamma[c] * invM;
     k3[j] = -k1[j] * (dbeta[c] * invM - mean[c] * is * dgamma[c] * invM);
+    if (relu && !out) {
+      sc[j] = is * gamma[c];  // the forward's bn_apply constants (mask from y)
+      sh[j] = beta[c] - mean[c] * sc[j];
+    }
   }
   const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
   for (int r = r0 + g; r < r1; r += rg) {
@@ -214,11 +240,13 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __rest
     float d[8], v[8];
     unpack8(*reinterpret_cast<const uint4*>(dout + o), d);
     unpack8(*reinterpret_cast<const uint4*>(y + o), v);
-    if (relu) {
+    if (relu && out) {
       float ov[8];
       unpack8(*reinterpret_cast<const uint4*>(out + o), ov);
 #pragma unroll
       for (int j = 0; j < 8; ++j) d[j] = ov[j] > 0.f ? d[j] : 0.f;
+    } else if (relu) {
+      relu_mask_from_y(v, sc, sh, d);
     }
     if (dres) *reinterpret_cast<uint4*>(dres + o) = pack8(d);
     float w[8];
@@ -404,22 +432,34 @@ void bn_forward(const uint16_t* y, const float* gamma, const float* beta, const 
                 uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var, float momentum,
                 float eps, int M, int C, float* partials, hipStream_t st) {
   const RowSplit r = row_split(M, C);
-  bn_partial_kernel<<<r.nblk, NT, 0, st>>>(0, y, nullptr, nullptr, 0, nullptr, nullptr, M, C, r.tpr, r.rg, r.rb,
-                                           partials);
+  bn_partial_kernel<<<r.nblk, NT, 0, st>>>(0, y, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, M, C, r.tpr,
+                                           r.rg, r.rb, partials);
   bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, r.nblk, M, C, eps, momentum, mean, invstd,
                                                 running_mean, running_var);
   bn_apply_kernel<<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r.tpr, r.rg, r.rb);
 }
 
-void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* mean,
-                 const float* invstd, int relu, uint16_t* dy, uint16_t* dres, float* dgamma, float* dbeta, int M,
-                 int C, float* partials, hipStream_t st) {
+void bn_forward_partials(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
+                         uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var,
+                         float momentum, float eps, int M, int C, const float* partials, int nblk, hipStream_t st) {
   const RowSplit r = row_split(M, C);
-  bn_partial_kernel<<<r.nblk, NT, 0, st>>>(1, y, dout, out, relu, mean, invstd, M, C, r.tpr, r.rg, r.rb, partials);
+  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, nblk, M, C, eps, momentum, mean, invstd,
+                                                running_mean, running_var);
+  bn_apply_kernel<<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r.tpr, r.rg, r.rb);
+}
+
+void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* beta,
+                 const float* mean, const float* invstd, int relu, uint16_t* dy, uint16_t* dres, float* dgamma,
+                 float* dbeta, int M, int C, float* partials, hipStream_t st) {
+  const RowSplit r = row_split(M, C);
+  // beta given (no residual in the forward): the relu mask is recomputed from y, `out` is not read
+  const uint16_t* o = (relu && beta) ? nullptr : out;
+  bn_partial_kernel<<<r.nblk, NT, 0, st>>>(1, y, dout, o, relu, mean, invstd, gamma, beta, M, C, r.tpr, r.rg, r.rb,
+                                           partials);
   bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,
                                                 nullptr);
-  bn_bwd_apply_kernel<<<r.nblk, NT, 0, st>>>(dout, out, y, gamma, mean, invstd, dbeta, dgamma, relu, dy, dres, M, C,
-                                             r.tpr, r.rg, r.rb, 1.f / (float)M);
+  bn_bwd_apply_kernel<<<r.nblk, NT, 0, st>>>(dout, o, y, gamma, beta, mean, invstd, dbeta, dgamma, relu, dy, dres, M,
+                                             C, r.tpr, r.rg, r.rb, 1.f / (float)M);
 }
 
 void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,

@@ -763,6 +763,43 @@ class MnistEngine : public torch::CustomClassHolder {
     }
   }
 
+  // Cost probe of the sufficient-factor fc-gradient kernel at world W on THIS GPU (one GPU cannot
+  // run a W-rank job): factor buffers of W ranks (this rank's slot = its real factors, the others
+  // copies of it) and `iters` launches of mnist_fc_grad_sfb timed with HIP events; returns ms per
+  // launch. Writes the fc gradient region of grads_bf16() -- a diagnostic, not a training step.
+  double sfb_probe(int64_t W, int64_t iters) {
+    TORCH_CHECK(W >= 1 && W <= 64 && iters >= 1, "sfb_probe: 1 <= W <= 64");
+    hipStream_t s = stream();
+    const int64_t rs = mnist_sfb_slot_elems((int)B_);
+    auto bf = at::TensorOptions().dtype(at::kBFloat16).device(at::kCUDA, device_);
+    at::Tensor p2 = p2_.reshape({1, -1}).repeat({W, 1}).contiguous();
+    at::Tensor dr = at::zeros({W, rs}, bf);
+    auto slot0 = dr.select(0, 0);
+    slot0.narrow(0, 0, B_ * HID).copy_(dh_.reshape({-1}));
+    slot0.narrow(0, B_ * HID, B_ * HID).copy_(hd_.reshape({-1}));
+    slot0.narrow(0, 2 * B_ * HID, 2 * B_ * NCLS).copy_(dlogits_.reshape({-1}).view(at::kBFloat16));
+    dr.copy_(slot0.unsqueeze(0).expand({W, rs}));
+    MnistStepArgs a = args();
+    a.gbf_a = (uint16_t*)gbf_.data_ptr();
+    a.sfb_world = (int)W;
+    a.sfb_p2 = (const uint16_t*)p2.data_ptr();
+    a.sfb_dr = (const uint16_t*)dr.data_ptr();
+    a.sfb_rs = rs;
+    mnist_fc_grad_sfb(a, s);  // warm (kernel attributes)
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipEventRecord(e0, s));
+    for (int64_t i = 0; i < iters; ++i) mnist_fc_grad_sfb(a, s);
+    HIP_OK(hipEventRecord(e1, s));
+    HIP_OK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return (double)ms / (double)iters;
+  }
+
  private:
   hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
   enum { P_START, P_FWD, P_BFC, P_BCONV, P_OPT, P_CA0, P_CA1, P_CB0, P_CB1, P_N };
@@ -1020,6 +1057,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_fc_sfb", &MnistEngine::set_fc_sfb)
       .def("fc_sfb", &MnistEngine::fc_sfb)
       .def("sfb_shard_elems", &MnistEngine::sfb_shard_elems)
+      .def("sfb_probe", &MnistEngine::sfb_probe)
       .def("set_force_dp", &MnistEngine::set_force_dp)
       .def("dp", &MnistEngine::dp)
       .def("set_conv_fork", &MnistEngine::set_conv_fork)

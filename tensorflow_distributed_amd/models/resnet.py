@@ -194,14 +194,21 @@ class GradJoin:
 class _Conv(torch.autograd.Function):
     # `token` is a 0-d tensor that requires grad: weights are not autograd leaves (their gradients
     # go straight into the flat buffer), so the stem needs it to put the graph on the tape.
+    # With layer.model.bn_stats the conv also returns the batch-norm statistics partials of its
+    # output ([row blocks, 2, K], summed in the GEMM epilogue), which the following BN consumes.
     @staticmethod
     def forward(ctx, x, token, layer):
         ctx.layer = layer
         ctx.save_for_backward(x)
+        if layer.model.bn_stats:
+            y, part = _ops().conv2d_fwd_stats(x, layer.w(), layer.stride, layer.pad)
+            ctx.mark_non_differentiable(part)
+            ctx.set_materialize_grads(False)  # no zero-filled gradient for `part` in the backward
+            return y, part
         return _ops().conv2d_fwd(x, layer.w(), layer.stride, layer.pad)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, *_dpart):
         (x,) = ctx.saved_tensors
         L = ctx.layer
         dy = dy.contiguous()
@@ -218,9 +225,9 @@ class _Conv(torch.autograd.Function):
 
 class _BN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, res, layer, relu):
-        out, mean, invstd = _ops().bn_fwd(y, layer.gamma(), layer.beta(), res, relu, layer.rmean, layer.rvar,
-                                          layer.momentum, layer.eps)
+    def forward(ctx, y, res, layer, relu, part=None):
+        args = (y, layer.gamma(), layer.beta(), res, relu, layer.rmean, layer.rvar, layer.momentum, layer.eps)
+        out, mean, invstd = _ops().bn_fwd(*args, part) if part is not None else _ops().bn_fwd(*args)
         ctx.layer, ctx.relu, ctx.has_res = layer, relu, res is not None
         ctx.save_for_backward(y, out, mean, invstd)
         return out
@@ -229,13 +236,15 @@ class _BN(torch.autograd.Function):
     def backward(ctx, dout):
         y, out, mean, invstd = ctx.saved_tensors
         L = ctx.layer
-        dy, dres = _ops().bn_bwd(dout.contiguous(), out, y, L.gamma(), mean, invstd, ctx.relu, ctx.has_res,
-                                 L.g_gamma(), L.g_beta())
+        # residual-free BN: pass beta, the kernels recompute the relu mask from y (no read of out)
+        beta = L.beta() if (ctx.relu and not ctx.has_res and L.model.mask_from_y) else None
+        args = (dout.contiguous(), out, y, L.gamma(), mean, invstd, ctx.relu, ctx.has_res, L.g_gamma(), L.g_beta())
+        dy, dres = _ops().bn_bwd(*args, beta) if beta is not None else _ops().bn_bwd(*args)
         L.model.reducer.mark_ready(L.name + "/gamma")
         L.model.reducer.mark_ready(L.name + "/beta")
         if ctx.has_res and L.res_join is not None:
             dres = L.res_join.arrive(dres)
-        return dy, (dres if ctx.has_res else None), None, None
+        return dy, (dres if ctx.has_res else None), None, None, None
 
 
 class _MaxPool(torch.autograd.Function):
@@ -336,7 +345,10 @@ class BNLayer:
         return self.model.fp.g(self.name + "/beta")
 
     def __call__(self, y, relu=True, res=None):
-        return _BN.apply(y, res, self, relu)
+        part = None
+        if isinstance(y, tuple):  # (conv output, its statistics partials) from a stats conv
+            y, part = y
+        return _BN.apply(y, res, self, relu, part)
 
 
 class LinearLayer:
@@ -369,7 +381,7 @@ class ResNet:
            101: ("bottleneck", [3, 4, 23, 3])}
 
     def __init__(self, depth: int = 50, num_classes: int = 1000, device=None, seed: int = 0, width: int = 64,
-                 zero_init_residual: bool = True, fuse_joins: bool = False):
+                 zero_init_residual: bool = True, fuse_joins: bool = False, bn_stats: bool = True):
         kind, blocks = self.CFG[depth]
         if num_classes % 8 or width % 8:
             raise ValueError("num_classes and width must be multiples of 8 (16-byte MFMA operand chunks)")
@@ -383,6 +395,11 @@ class ResNet:
         self.joins: List[GradJoin] = []
         self.grads_zeroed = False  # set by train_step: the flat grad buffer was zeroed this step
         self.fuse_joins = fuse_joins
+        # BN statistics summed in the producing conv's epilogue (conv2d_fwd_stats) instead of a
+        # separate read pass over every conv output
+        self.bn_stats = bn_stats
+        # residual-free BN backward recomputes its relu mask from y instead of reading the output
+        self.mask_from_y = True
         cin = width
         exp = 4 if kind == "bottleneck" else 1
         for li, nb in enumerate(blocks):

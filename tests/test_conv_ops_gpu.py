@@ -62,6 +62,32 @@ def test_conv_fwd_dgrad_wgrad(cuda, N, H, W, C, K, R, st, pad):
     assert relerr(dw2.cpu(), wr.grad.permute(2, 3, 1, 0)) < 1e-3
 
 
+@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS + [(8, 28, 28, 64, 256, 1, 1, 0)])
+def test_conv_fwd_stats_feeds_bn(cuda, N, H, W, C, K, R, st, pad):
+    """conv2d_fwd_stats: same output as conv2d_fwd, and per-row-block sums of the stored bf16 output
+    that bn_fwd(partials=...) turns into the same normalisation as its own statistics pass. The
+    last shape takes the 128x128 tiles."""
+    torch.manual_seed(5)
+    x = rb(torch.randn(N, H, W, C)).to(cuda, torch.bfloat16)
+    w = rb(torch.randn(R, R, C, K) * 0.2).to(cuda, torch.bfloat16)
+    y0 = ops.conv2d_fwd(x, w, st, pad)
+    y, part = ops.conv2d_fwd_stats(x, w, st, pad)
+    assert torch.equal(y, y0)
+    yf = y.float().reshape(-1, K)
+    assert part.shape[1:] == (2, K)
+    torch.testing.assert_close(part[:, 0].sum(0), yf.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(part[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
+    g, b = torch.rand(K, device=cuda) + 0.5, torch.randn(K, device=cuda)
+    rm0, rv0 = torch.zeros(K, device=cuda), torch.ones(K, device=cuda)
+    rm1, rv1 = rm0.clone(), rv0.clone()
+    o0, m0, i0 = ops.bn_fwd(y, g, b, None, True, rm0, rv0, 0.9, 1e-5)
+    o1, m1, i1 = ops.bn_fwd(y, g, b, None, True, rm1, rv1, 0.9, 1e-5, part)
+    torch.testing.assert_close(m1, m0, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(i1, i0, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rv1, rv0, rtol=1e-4, atol=1e-5)
+    assert relerr(o1, o0) < 1e-2
+
+
 def test_linear(cuda):
     torch.manual_seed(1)
     M, Kin, N = 24, 64, 40
@@ -108,6 +134,11 @@ def test_batchnorm_train(cuda, relu, res):
     assert relerr(db.cpu(), dz.sum(0)) < 1e-3 and relerr(dg.cpu(), (dz * yh).sum(0)) < 1e-2
     if res:
         assert relerr(dres.cpu(), dz) < 1e-2
+    if relu and not res:  # mask recomputed from y (beta given): `out` is not read, same gradients
+        dg2, db2 = torch.empty_like(dg), torch.empty_like(db)
+        dy2, _ = ops.bn_bwd(dout.to(cuda, torch.bfloat16), torch.empty_like(out), y.to(cuda, torch.bfloat16),
+                            g.to(cuda), mean, invstd, relu, res, dg2, db2, b.to(cuda))
+        assert torch.equal(dy2, dy) and torch.equal(dg2, dg) and torch.equal(db2, db)
 
 
 def test_maxpool_avgpool(cuda):
