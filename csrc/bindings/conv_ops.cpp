@@ -123,6 +123,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& y, const
   const int C = (int)y.size(-1);
   const int M = (int)(y.numel() / C);
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn: C must be a multiple of 8 and <= 2048");
+  TORCH_CHECK(y.numel() < (1ll << 30), "bn: tensor too large for 32-bit buffer addressing");
   check_f32(gamma, "gamma");
   check_f32(beta, "beta");
   if (res) {
@@ -159,6 +160,7 @@ std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tens
   check_f32(dbeta, "dbeta");
   const int C = (int)y.size(-1);
   const int M = (int)(y.numel() / C);
+  TORCH_CHECK(y.numel() < (1ll << 30) && C % 8 == 0, "bn_bwd: C % 8 and < 2^30 elements (buffer addressing)");
   auto dy = at::empty_like(y);
   at::Tensor dres = want_dres ? at::empty_like(y) : at::Tensor();
   auto part = at::empty({bn_partials_size(M, C)}, y.options().dtype(at::kFloat));

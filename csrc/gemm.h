@@ -328,6 +328,18 @@ __device__ __forceinline__ void gemm_block_oneshot(const LA& la, const LB& lb, c
 // ---------------- common loaders ----------------
 __device__ __forceinline__ uint4 zero4() { return make_uint4(0u, 0u, 0u, 0u); }
 
+// Branch-free 16-B operand load: a raw buffer load through a descriptor over [base, base + nbytes)
+// (built from kernel arguments, so scalar); an out-of-range chunk (ok == false) gets an offset past
+// the range, which the hardware range check returns as zeros. No exec-masked branch around the
+// load, so the compiler can count loads in flight (register pipelines, RS > 1). nbytes < 2 GiB.
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+constexpr uint32_t kBufOOB = 0xFFFFFFF0u;
+__device__ __forceinline__ uint4 buf_ld(const uint16_t* base, uint32_t nbytes, uint32_t elem_off, bool ok) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)nbytes, 0x00020000);
+  const i32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? elem_off * 2u : kBufOOB, 0, 0);
+  return make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
+}
+
 // Row-major X[rows][ld] bf16; chunk runs along the contiguous (column) dimension.
 //  KC=true : operand index (mn, k) = X[mn][k]   (A as [M][K] or B as [N][K])
 //  KC=false: operand index (mn, k) = X[k][mn]   (A as [K][M] or B as [K][N])

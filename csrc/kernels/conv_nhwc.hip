@@ -49,13 +49,7 @@ struct Geo {
 // under `if (in range)` the compiler emits an exec-masked branch per load and cannot count the
 // loads in flight across the joins, so a deeper register pipeline (TFD_CONV_RS > 1) degenerated to
 // vmcnt(0) waits (measured: ResNet-50 b128 19.6 -> 24.5 ms/step at RS = 2).
-typedef int i32x4v __attribute__((ext_vector_type(4)));
-constexpr uint32_t kOOB = 0xFFFFFFF0u;  // offset past any descriptor range (operands < 4 GiB, host-checked)
-__device__ __forceinline__ uint4 buf_ld(const uint16_t* base, uint32_t nbytes, uint32_t elem_off, bool ok) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)nbytes, 0x00020000);
-  const i32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? elem_off * 2u : kOOB, 0, 0);
-  return make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
-}
+// (buf_ld: csrc/gemm.h)
 
 // Row-major X[rows][ld] bf16 with whole 16-B chunks (lims and ld multiples of 8; host-checked):
 //  KC=true : (mn, k) = X[mn][k];  KC=false: (mn, k) = X[k][mn]

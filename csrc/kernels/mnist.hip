@@ -1114,23 +1114,33 @@ __global__ __launch_bounds__(256) void fc1_bwd_adam(MnistStepArgs a, MnistAdamAr
 // peer links, so below W ~ 9 the gather moves fewer bytes per link (W = 2: 1.33 vs 6.4 MB over the
 // one link). Every rank then runs the identical GEMM on identical data: bit-identical gradients on
 // all ranks, fp32-accumulated over all W*B rows (no bf16 rounding of per-rank partial sums).
-// KC = false operand over per-rank slots: (mn, k) = X[row k % B of rank k / B][mn]
+// Branch-free (buffer-load) operands of the K = W*B GEMM, so its RS = 2 register pipeline keeps two
+// K-tiles of loads in flight (with branching loads the compiler waits for all of them each step).
+// KC = false over per-rank slots: (mn, k) = X[row k % B of rank k / B][mn]; mn_lim % 8 == 0.
 struct RankRowsMC {
   static constexpr bool KC = false;
   const uint16_t* __restrict__ x;
   int ld, mn_lim, k_lim, B;
-  int64_t rs;  // rank slot stride (elements)
+  int64_t rs;       // rank slot stride (elements)
+  uint32_t nbytes;  // whole gathered array
   __device__ __forceinline__ uint4 operator()(int mn, int k) const {
-    if (k >= k_lim || mn >= mn_lim) return zero4();
     const int r = k / B;
-    const uint16_t* row = x + r * rs + (size_t)(k - r * B) * ld;
-    if (mn + 8 <= mn_lim) return *reinterpret_cast<const uint4*>(row + mn);
-    uint16_t t[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t[j] = (mn + j < mn_lim) ? row[mn + j] : 0;
-    return *reinterpret_cast<uint4*>(t);
+    return buf_ld(x, nbytes, (uint32_t)(r * rs + (int64_t)(k - r * B) * ld + mn), k < k_lim && mn < mn_lim);
   }
 };
+// [P2_all; 1]^T as the KC = false A operand: (mn, k) = P2_all[k][mn] for mn < 3136, the bias
+// "ones row" at mn == 3136 (a chunk {1, 0, ..., 0}), zeros past K.
+struct OnesRowBuf {
+  static constexpr bool KC = false;
+  const uint16_t* __restrict__ x;
+  int k_lim;
+  uint32_t nbytes;
+  __device__ __forceinline__ uint4 operator()(int mn, int k) const {
+    const uint4 v = buf_ld(x, nbytes, (uint32_t)k * FEAT + mn, k < k_lim && mn < FEAT);
+    return (mn == FEAT && k < k_lim) ? make_uint4(0x3F80u, 0u, 0u, 0u) : v;
+  }
+};
+static_assert(FEAT % 8 == 0, "the ones row starts a fresh 8-element chunk");
 
 // Output layer [1025][10] = [Hd;1]^T dlogits over the W*B gathered rows: a block owns 16 rows m
 // (lane r = t & 15) x 16 row groups (q = t >> 4) of the K range, so even W = 8 leaves 64 rows per
@@ -1179,15 +1189,29 @@ __device__ __forceinline__ void out_grad_sfb_block(const MnistStepArgs& a, int b
   }
 }
 
+// XCD-grouped tile order: workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
+// one L2; MI355X_MICROARCH.md, workgroup dispatch), so a row-major tile order spreads the 16 tiles
+// that read the same A panel (64 dW rows x all K of p2) over all 8 L2s, each fetching it from MALL
+// / HBM. Mapping the tiles with b % 8 == x to the contiguous range [x * n/8, (x + 1) * n/8) keeps a
+// panel's readers on one XCD: A crosses into each L2 about once instead of 8 times. (The long-K
+// GEMM is bound by that traffic: 32 FLOP per byte of A + B for 64 x 64 tiles.)
+__device__ __forceinline__ int xcd_grouped_tile(int b, int first, int n) {
+  const int x = b & 7;
+  const int first_x = first + ((x - first) & 7);  // first block of [first, first + n) with b % 8 == x
+  return x * (n >> 3) + ((b - first_x) >> 3);
+}
+
 // [output-layer blocks | fc1 dW (+ bias row) tiles over K = W*B]
 __global__ __launch_bounds__(256) void fc_grad_sfb(MnistStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   int id = blockIdx.x;
   if (id < OUTS_BLOCKS) { out_grad_sfb_block(a, id, (float*)smem_raw); return; }
-  id -= OUTS_BLOCKS;
+  constexpr int NT_ = FDW_GX * FDW_GY;
+  static_assert(NT_ % 8 == 0, "XCD grouping deals whole residue classes");
+  id = xcd_grouped_tile(id, OUTS_BLOCKS, NT_);
   const int WB = a.sfb_world * a.B;
-  OnesRowMC la{a.sfb_p2, FEAT, FEAT, WB};
-  RankRowsMC lb{a.sfb_dr, HID, HID, WB, a.B, a.sfb_rs};
+  OnesRowBuf la{a.sfb_p2, WB, (uint32_t)((int64_t)WB * FEAT * 2)};
+  RankRowsMC lb{a.sfb_dr, HID, HID, WB, a.B, a.sfb_rs, (uint32_t)((int64_t)a.sfb_world * a.sfb_rs * 2)};
   GradEpi epi{a.grad + OFF_WD1, a.gbf_a ? a.gbf_a + OFF_WD1 : nullptr, HID, FEAT + 1, HID};
   gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(
       la, lb, epi, (id / FDW_GX) * FDW_BM, (id % FDW_GX) * FDW_BN, 0, WB, (bf16*)smem_raw);
@@ -1995,8 +2019,8 @@ int64_t mnist_sfb_slot_elems(int B) { return ((int64_t)B * (2 * HID + 2 * NCLS) 
 
 void mnist_fc_grad_sfb(const MnistStepArgs& a, hipStream_t s) {
   if (a.sfb_world < 1 || !a.sfb_p2 || !a.sfb_dr) throw std::runtime_error("mnist_fc_grad_sfb: no gathered factors");
-  constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, RankRowsMC>::BYTES;
   constexpr int sm_og = OUTS_ROWS * OUTS_GROUPS * NCLS * 4;
+  constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowBuf, RankRowsMC>::BYTES;
   constexpr int sm = sm_dw > sm_og ? sm_dw : sm_og;
   set_smem<fc_grad_sfb>(sm);
   fc_grad_sfb<<<OUTS_BLOCKS + FDW_GX * FDW_GY, 256, sm, s>>>(a);

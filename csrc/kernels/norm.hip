@@ -5,6 +5,7 @@
 // finalize kernel in a fixed order.
 #include "../common.h"
 #include "../conv_kernels.h"
+#include "../gemm.h"  // buf_ld
 
 namespace tfd {
 namespace {
@@ -49,11 +50,22 @@ __device__ __forceinline__ void relu_mask_from_y(const float (&v)[8], const floa
   for (int j = 0; j < 8; ++j) d[j] = fmaf(v[j], sc[j], sh[j]) > 0.f ? d[j] : 0.f;
 }
 
-// partial sums of (a, b) per channel over a row chunk; mode 0: a = y, b = y^2 ; mode 1 (backward):
-// a = dz, b = dz * xhat with dz = relu-masked dout
-__global__ __launch_bounds__(NT) void bn_partial_kernel(int mode, const uint16_t* __restrict__ y,
+// Rows are walked in batches of RU rows per thread: every 16-B load of a batch (y, dout, out) is
+// issued before the first use, through buffer descriptors whose hardware range check zero-fills the
+// rows past the block's chunk (no exec-masked branch around a load, so the loads of a batch are all
+// in flight together). With one row per iteration these kernels waited one memory latency per row.
+constexpr int RU = 4;
+__device__ __forceinline__ uint4 row_ld(const uint16_t* base, uint32_t nbytes, int r, int r1, int C, int c0) {
+  return buf_ld(base, nbytes, (uint32_t)r * (uint32_t)C + (uint32_t)c0, r < r1);
+}
+
+// partial sums of (a, b) per channel over a row chunk; MODE 0: a = y, b = y^2 ; MODE 1 (backward):
+// a = dz, b = dz * xhat with dz = relu-masked dout. MASK (MODE 1): 0 no relu, 1 mask = out > 0,
+// 2 mask recomputed from y (relu_mask_from_y).
+template <int MODE, int MASK>
+__global__ __launch_bounds__(NT) void bn_partial_kernel(const uint16_t* __restrict__ y,
                                                         const uint16_t* __restrict__ dout,
-                                                        const uint16_t* __restrict__ out, int relu,
+                                                        const uint16_t* __restrict__ out,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ invstd,
                                                         const float* __restrict__ gamma,
@@ -61,15 +73,16 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(int mode, const uint16_t
                                                         int rg, int rb, float* __restrict__ part) {
   __shared__ float red[2][NT][8];
   const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
+  const uint32_t nbytes = (uint32_t)M * (uint32_t)C * 2u;
   float sa[8], sb[8], mu[8], is[8], sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { sa[j] = 0.f; sb[j] = 0.f; }
-  if (mode == 1 && g < rg) {
+  if (MODE == 1 && g < rg) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       mu[j] = mean[c0 + j];
       is[j] = invstd[c0 + j];
-      if (relu && !out) {
+      if (MASK == 2) {
         sc[j] = is[j] * gamma[c0 + j];
         sh[j] = beta[c0 + j] - mu[j] * sc[j];
       }
@@ -77,26 +90,36 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(int mode, const uint16_t
   }
   const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
   if (g < rg) {
-    for (int r = r0 + g; r < r1; r += rg) {
-      const size_t o = (size_t)r * C + c0;
-      float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(y + o), v);
-      if (mode == 0) {
+    for (int rbase = r0 + g; rbase < r1; rbase += RU * rg) {
+      uint4 Y[RU], D[RU], O[RU];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { sa[j] += v[j]; sb[j] = fmaf(v[j], v[j], sb[j]); }
-      } else {
-        float d[8];
-        unpack8(*reinterpret_cast<const uint4*>(dout + o), d);
-        if (relu && out) {
-          float ov[8];
-          unpack8(*reinterpret_cast<const uint4*>(out + o), ov);
+      for (int u = 0; u < RU; ++u) {
+        const int r = rbase + u * rg;
+        Y[u] = row_ld(y, nbytes, r, r1, C, c0);
+        if (MODE == 1) D[u] = row_ld(dout, nbytes, r, r1, C, c0);
+        if (MODE == 1 && MASK == 1) O[u] = row_ld(out, nbytes, r, r1, C, c0);
+      }
 #pragma unroll
-          for (int j = 0; j < 8; ++j) d[j] = ov[j] > 0.f ? d[j] : 0.f;
-        } else if (relu) {
-          relu_mask_from_y(v, sc, sh, d);
+      for (int u = 0; u < RU; ++u) {  // rows past r1 loaded as zeros: they add nothing
+        float v[8];
+        unpack8(Y[u], v);
+        if (MODE == 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { sa[j] += v[j]; sb[j] = fmaf(v[j], v[j], sb[j]); }
+        } else {
+          float d[8];
+          unpack8(D[u], d);
+          if (MASK == 1) {
+            float ov[8];
+            unpack8(O[u], ov);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = ov[j] > 0.f ? d[j] : 0.f;
+          } else if (MASK == 2) {
+            relu_mask_from_y(v, sc, sh, d);
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { sa[j] += d[j]; sb[j] = fmaf(d[j], (v[j] - mu[j]) * is[j], sb[j]); }
         }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { sa[j] += d[j]; sb[j] = fmaf(d[j], (v[j] - mu[j]) * is[j], sb[j]); }
       }
     }
   }
@@ -178,14 +201,18 @@ __global__ __launch_bounds__(FIN_NT) void bn_final_kernel(int mode, const float*
 }
 
 // Elementwise passes walk the same row split as the partial kernel: thread = (8-channel chunk,
-// row group); its 8 channels' constants stay in registers for every row it touches.
+// row group); its 8 channels' constants stay in registers for every row it touches; RU rows' loads
+// per batch are issued before the first use (branch-free buffer loads, see bn_partial_kernel).
+// HAS_RES / RELU are compile-time so no load sits under a branch.
+template <bool HAS_RES, bool RELU>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, const float* __restrict__ mean,
                                                       const float* __restrict__ invstd,
-                                                      const uint16_t* __restrict__ res, int relu,
+                                                      const uint16_t* __restrict__ res,
                                                       uint16_t* __restrict__ out, int M, int C, int tpr, int rg, int rb) {
   const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
   if (g >= rg) return;
+  const uint32_t nbytes = (uint32_t)M * (uint32_t)C * 2u;
   float sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -193,32 +220,43 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict
     sh[j] = beta[c0 + j] - mean[c0 + j] * sc[j];
   }
   const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
-  for (int r = r0 + g; r < r1; r += rg) {
-    const size_t o = (size_t)r * C + c0;
-    float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(y + o), v);
-    float q[8];
-    if (res) unpack8(*reinterpret_cast<const uint4*>(res + o), q);
+  for (int rbase = r0 + g; rbase < r1; rbase += RU * rg) {
+    uint4 Y[RU], Q[RU];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float z = fmaf(v[j], sc[j], sh[j]);
-      if (res) z += q[j];
-      v[j] = relu ? fmaxf(z, 0.f) : z;
+    for (int u = 0; u < RU; ++u) {
+      Y[u] = row_ld(y, nbytes, rbase + u * rg, r1, C, c0);
+      if (HAS_RES) Q[u] = row_ld(res, nbytes, rbase + u * rg, r1, C, c0);
     }
-    *reinterpret_cast<uint4*>(out + o) = pack8(v);
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int r = rbase + u * rg;
+      float v[8], q[8];
+      unpack8(Y[u], v);
+      if (HAS_RES) unpack8(Q[u], q);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float z = fmaf(v[j], sc[j], sh[j]);
+        if (HAS_RES) z += q[j];
+        v[j] = RELU ? fmaxf(z, 0.f) : z;
+      }
+      if (r < r1) *reinterpret_cast<uint4*>(out + (size_t)r * C + c0) = pack8(v);
+    }
   }
 }
 
+// MASK: 0 no relu, 1 mask = out > 0, 2 mask recomputed from y
+template <int MASK>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout,
                                                           const uint16_t* __restrict__ out, const uint16_t* __restrict__ y,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd, const float* __restrict__ dbeta,
-                                                          const float* __restrict__ dgamma, int relu,
+                                                          const float* __restrict__ dgamma,
                                                           uint16_t* __restrict__ dy, uint16_t* __restrict__ dres,
                                                           int M, int C, int tpr, int rg, int rb, float invM) {
   const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
   if (g >= rg) return;
+  const uint32_t nbytes = (uint32_t)M * (uint32_t)C * 2u;
   // dy = k1 * dz + k2 * y + k3 with k1 = gamma*invstd, k2 = -k1*invstd*dgamma/M,
   // k3 = -k1*(dbeta/M - mean*invstd^2*dgamma/M)
   float k1[8], k2[8], k3[8], sc[8], sh[8];
@@ -229,30 +267,44 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __rest
     k1[j] = gamma[c] * is;
     k2[j] = -k1[j] * is * dgamma[c] * invM;
     k3[j] = -k1[j] * (dbeta[c] * invM - mean[c] * is * dgamma[c] * invM);
-    if (relu && !out) {
+    if (MASK == 2) {
       sc[j] = is * gamma[c];  // the forward's bn_apply constants (mask from y)
       sh[j] = beta[c] - mean[c] * sc[j];
     }
   }
   const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
-  for (int r = r0 + g; r < r1; r += rg) {
-    const size_t o = (size_t)r * C + c0;
-    float d[8], v[8];
-    unpack8(*reinterpret_cast<const uint4*>(dout + o), d);
-    unpack8(*reinterpret_cast<const uint4*>(y + o), v);
-    if (relu && out) {
-      float ov[8];
-      unpack8(*reinterpret_cast<const uint4*>(out + o), ov);
+  for (int rbase = r0 + g; rbase < r1; rbase += RU * rg) {
+    uint4 D[RU], Y[RU], O[RU];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = ov[j] > 0.f ? d[j] : 0.f;
-    } else if (relu) {
-      relu_mask_from_y(v, sc, sh, d);
+    for (int u = 0; u < RU; ++u) {
+      const int r = rbase + u * rg;
+      D[u] = row_ld(dout, nbytes, r, r1, C, c0);
+      Y[u] = row_ld(y, nbytes, r, r1, C, c0);
+      if (MASK == 1) O[u] = row_ld(out, nbytes, r, r1, C, c0);
     }
-    if (dres) *reinterpret_cast<uint4*>(dres + o) = pack8(d);
-    float w[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) w[j] = fmaf(k1[j], d[j], fmaf(k2[j], v[j], k3[j]));
-    *reinterpret_cast<uint4*>(dy + o) = pack8(w);
+    for (int u = 0; u < RU; ++u) {
+      const int r = rbase + u * rg;
+      float d[8], v[8];
+      unpack8(D[u], d);
+      unpack8(Y[u], v);
+      if (MASK == 1) {
+        float ov[8];
+        unpack8(O[u], ov);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = ov[j] > 0.f ? d[j] : 0.f;
+      } else if (MASK == 2) {
+        relu_mask_from_y(v, sc, sh, d);
+      }
+      float w[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = fmaf(k1[j], d[j], fmaf(k2[j], v[j], k3[j]));
+      if (r < r1) {
+        const size_t o = (size_t)r * C + c0;
+        if (dres) *reinterpret_cast<uint4*>(dres + o) = pack8(d);
+        *reinterpret_cast<uint4*>(dy + o) = pack8(w);
+      }
+    }
   }
 }
 
@@ -421,6 +473,14 @@ __global__ __launch_bounds__(NT) void pad_channels_kernel(const float* __restric
 
 inline int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + NT - 1) / NT)); }
 
+void launch_apply(const uint16_t* y, const float* gamma, const float* beta, const float* mean, const float* invstd,
+                  const uint16_t* res, int relu, uint16_t* out, int M, int C, const RowSplit& r, hipStream_t st) {
+  if (res && relu) bn_apply_kernel<true, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb);
+  else if (res) bn_apply_kernel<true, false><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb);
+  else if (relu) bn_apply_kernel<false, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb);
+  else bn_apply_kernel<false, false><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb);
+}
+
 }  // namespace
 
 int bn_partials_size(int M, int C) {
@@ -432,11 +492,11 @@ void bn_forward(const uint16_t* y, const float* gamma, const float* beta, const 
                 uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var, float momentum,
                 float eps, int M, int C, float* partials, hipStream_t st) {
   const RowSplit r = row_split(M, C);
-  bn_partial_kernel<<<r.nblk, NT, 0, st>>>(0, y, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, M, C, r.tpr,
-                                           r.rg, r.rb, partials);
+  bn_partial_kernel<0, 0><<<r.nblk, NT, 0, st>>>(y, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, C, r.tpr,
+                                                 r.rg, r.rb, partials);
   bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, r.nblk, M, C, eps, momentum, mean, invstd,
                                                 running_mean, running_var);
-  bn_apply_kernel<<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r.tpr, r.rg, r.rb);
+  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st);
 }
 
 void bn_forward_partials(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
@@ -445,7 +505,7 @@ void bn_forward_partials(const uint16_t* y, const float* gamma, const float* bet
   const RowSplit r = row_split(M, C);
   bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, nblk, M, C, eps, momentum, mean, invstd,
                                                 running_mean, running_var);
-  bn_apply_kernel<<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r.tpr, r.rg, r.rb);
+  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st);
 }
 
 void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* beta,
@@ -453,13 +513,18 @@ void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, c
                  float* dbeta, int M, int C, float* partials, hipStream_t st) {
   const RowSplit r = row_split(M, C);
   // beta given (no residual in the forward): the relu mask is recomputed from y, `out` is not read
-  const uint16_t* o = (relu && beta) ? nullptr : out;
-  bn_partial_kernel<<<r.nblk, NT, 0, st>>>(1, y, dout, o, relu, mean, invstd, gamma, beta, M, C, r.tpr, r.rg, r.rb,
-                                           partials);
-  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,
-                                                nullptr);
-  bn_bwd_apply_kernel<<<r.nblk, NT, 0, st>>>(dout, o, y, gamma, beta, mean, invstd, dbeta, dgamma, relu, dy, dres, M,
-                                             C, r.tpr, r.rg, r.rb, 1.f / (float)M);
+  const int mask = !relu ? 0 : (beta ? 2 : 1);
+#define TFD_BN_BWD(MK)                                                                                          \
+  bn_partial_kernel<1, MK><<<r.nblk, NT, 0, st>>>(y, dout, out, mean, invstd, gamma, beta, M, C, r.tpr, r.rg, r.rb, \
+                                                  partials);                                                   \
+  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,  \
+                                                nullptr);                                                       \
+  bn_bwd_apply_kernel<MK><<<r.nblk, NT, 0, st>>>(dout, out, y, gamma, beta, mean, invstd, dbeta, dgamma, dy, dres, M, \
+                                                 C, r.tpr, r.rg, r.rb, 1.f / (float)M);
+  if (mask == 0) { TFD_BN_BWD(0) }
+  else if (mask == 1) { TFD_BN_BWD(1) }
+  else { TFD_BN_BWD(2) }
+#undef TFD_BN_BWD
 }
 
 void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,

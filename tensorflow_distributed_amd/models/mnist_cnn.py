@@ -131,6 +131,37 @@ def conv_net(x: torch.Tensor, p: Dict[str, torch.Tensor], keep_prob: float = 1.0
     return h @ p["out"] + p["out_b"]
 
 
+def fc_sufficient_factors(x: torch.Tensor, labels: torch.Tensor, p: Dict[str, torch.Tensor],
+                          keep_prob: float = 1.0, dropout_mask: Optional[torch.Tensor] = None):
+    """The per-example factors of this rank's fc-layer gradients (what the native DP step
+    all-gathers instead of all-reducing the fc gradients, ``mnist_fc_grad_sfb``):
+    p2 [B,3136] (fc1 input), hd [B,1024] (fc1 output after relu + dropout), dh [B,1024] (gradient at
+    the fc1 pre-activation), dl [B,10] (gradient at the logits, 1/B of the mean folded in)."""
+    x = x.reshape(-1, IMG, IMG, 1)
+    h = torch.relu(conv2d_same_nhwc(x, p["wc1"], p["bc1"]))
+    h = maxpool_same_nhwc(h, 2)
+    h = torch.relu(conv2d_same_nhwc(h, p["wc2"], p["bc2"]))
+    p2 = maxpool_same_nhwc(h, 2).reshape(-1, FEAT).detach()
+    z = (p2 @ p["wd1"] + p["bd1"]).requires_grad_(True)
+    hd = torch.relu(z)
+    if dropout_mask is not None:
+        hd = hd * dropout_mask / keep_prob
+    hd_leaf = hd.detach().requires_grad_(True)
+    logits = (hd_leaf @ p["out"] + p["out_b"]).detach().requires_grad_(True)
+    loss = softmax_xent_mean(logits, labels)
+    (dl,) = torch.autograd.grad(loss, [logits])
+    dhd = dl @ p["out"].t()
+    (dh,) = torch.autograd.grad(hd, [z], dhd)
+    return p2, hd.detach(), dh.detach(), dl.detach()
+
+
+def fc_grads_from_factors(p2: torch.Tensor, hd: torch.Tensor, dh: torch.Tensor, dl: torch.Tensor):
+    """Summed fc-layer gradients over every row of the (gathered) factors -- equal to the sum of the
+    per-rank gradients because each is a sum of per-example outer products:
+    dW_fc1 = p2^T dh, d bd1 = 1^T dh, dW_out = hd^T dl, d out_b = 1^T dl."""
+    return {"wd1": p2.t() @ dh, "bd1": dh.sum(0), "out": hd.t() @ dl, "out_b": dl.sum(0)}
+
+
 def softmax_xent_mean(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     """reduce_mean(softmax_cross_entropy_with_logits(logits, onehot)) — labels: int class ids or one-hot."""
     if labels.dim() == 2:

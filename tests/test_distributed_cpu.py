@@ -228,3 +228,42 @@ def test_async_ps_state_pull_has_the_optimizer_slots():
     assert ps[1] == 2 and ps[2] == 2  # async: every push applied
     for _, w in outs[1:]:
         assert w["t"] == 2 and w["slots"]["m"].abs().sum() > 0 and w["slots"]["v"].abs().sum() > 0
+
+
+def _sfb_worker(rank, world, B):
+    import torch.distributed as dist
+
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+
+    torch.manual_seed(100 + rank)
+    p = {k: v * 0.05 for k, v in M.init_params(3).items()}
+    x = torch.rand(B, 784)
+    y = torch.randint(0, 10, (B,))
+    mask = (torch.rand(B, 1024) < 0.75).float()
+    # all-reduce path: this rank's autograd gradients, summed over ranks
+    q = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    loss = M.softmax_xent_mean(M.conv_net(x, q, keep_prob=0.75, dropout_mask=mask), y)
+    loss.backward()
+    ar = {k: q[k].grad.clone() for k in ("wd1", "bd1", "out", "out_b")}
+    for v in ar.values():
+        dist.all_reduce(v)
+    # sufficient-factor path: gather every rank's factors, one GEMM over all rows
+    facs = M.fc_sufficient_factors(x, y, p, keep_prob=0.75, dropout_mask=mask)
+    gathered = []
+    for f in facs:
+        parts = [torch.zeros_like(f) for _ in range(world)]
+        dist.all_gather(parts, f.contiguous())
+        gathered.append(torch.cat(parts))
+    sfb = M.fc_grads_from_factors(*gathered)
+    return {k: (ar[k], sfb[k]) for k in ar}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sufficient_factor_fc_gradients_equal_the_all_reduce(world):
+    """The DP fc-gradient algorithm of the native engine (mnist_fc_grad_sfb), on the fp32 oracle
+    over gloo: the GEMM over all ranks' gathered factors equals the all-reduced sum of the ranks'
+    own fc gradients (dropout included), for every fc tensor."""
+    res = run_ranks(_sfb_worker, world, 16, timeout=300)
+    for out in res:
+        for k, (ar, sfb) in out.items():
+            torch.testing.assert_close(sfb, ar, rtol=1e-4, atol=1e-5, msg=k)

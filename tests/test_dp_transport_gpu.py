@@ -69,16 +69,17 @@ def test_forced_dp_world1_gradients_are_the_fused_gradients(cuda, mode):
     tr.close()
 
 
-@pytest.mark.parametrize("mode", ["rccl", "ipc"])
-def test_forced_dp_world1_sfb_gradients_are_the_fused_gradients(cuda, mode):
+@pytest.mark.parametrize("mode,B", [("rccl", 128), ("ipc", 128), ("ipc", 512)])
+def test_forced_dp_world1_sfb_gradients_are_the_fused_gradients(cuda, mode, B):
     """Sufficient-factor fc gradients at world 1 (gather of the own factors, GEMM over K = B):
-    fc1 dW + bias are the one-GPU step's fp32 gradients rounded to bf16 bit for bit (same GEMM, same
-    K order); the output layer sums its rows in a different fixed order (<= 1 bf16 ulp)."""
+    fc1 dW + bias are the one-GPU step's fp32 gradients rounded to bf16 bit for bit (same K order;
+    B = 512 takes the 128 x 128 long-K tiles); the output layer sums its rows in a different fixed
+    order (<= 1 bf16 ulp)."""
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
-        params, (ref, dp) = _engines_on_dataset(cuda, 2, keep=1.0, sgd=True)
+        params, (ref, dp) = _engines_on_dataset(cuda, 2, B=B, keep=1.0, sgd=True)
         tr = attach_engine(dp, 0, 1, cuda, mode=mode, force_dp=True, sfb=True)
         assert tr.kind == mode + "+sfb" and dp.fc_sfb()
         ref.train_step()
