@@ -1206,9 +1206,16 @@ __global__ __launch_bounds__(256) void fc_grad_sfb(MnistStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   int id = blockIdx.x;
   if (id < OUTS_BLOCKS) { out_grad_sfb_block(a, id, (float*)smem_raw); return; }
-  constexpr int NT_ = FDW_GX * FDW_GY;
-  static_assert(NT_ % 8 == 0, "XCD grouping deals whole residue classes");
-  id = xcd_grouped_tile(id, OUTS_BLOCKS, NT_);
+  // tile rows: all FDW_GY, or (ZeRO shard) [by_lo, by_hi] plus the bias row's tile
+  const bool part = a.sfb_by_hi >= a.sfb_by_lo;
+  const int nby = part ? (a.sfb_by_hi - a.sfb_by_lo + 1) + (a.sfb_by_hi < FDW_GY - 1 ? 1 : 0) : FDW_GY;
+  static_assert(FDW_GX % 8 == 0, "XCD grouping deals whole residue classes");
+  id = xcd_grouped_tile(id, OUTS_BLOCKS, FDW_GX * nby);
+  if (part) {
+    int by = id / FDW_GX + a.sfb_by_lo;
+    if (by > a.sfb_by_hi) by = FDW_GY - 1;  // the bias row (3136) is updated by every rank
+    id = by * FDW_GX + id % FDW_GX;
+  }
   const int WB = a.sfb_world * a.B;
   OnesRowBuf la{a.sfb_p2, WB, (uint32_t)((int64_t)WB * FEAT * 2)};
   RankRowsMC lb{a.sfb_dr, HID, HID, WB, a.B, a.sfb_rs, (uint32_t)((int64_t)a.sfb_world * a.sfb_rs * 2)};
@@ -2023,7 +2030,15 @@ void mnist_fc_grad_sfb(const MnistStepArgs& a, hipStream_t s) {
   constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowBuf, RankRowsMC>::BYTES;
   constexpr int sm = sm_dw > sm_og ? sm_dw : sm_og;
   set_smem<fc_grad_sfb>(sm);
-  fc_grad_sfb<<<OUTS_BLOCKS + FDW_GX * FDW_GY, 256, sm, s>>>(a);
+  const bool part = a.sfb_by_hi >= a.sfb_by_lo;
+  if (part && (a.sfb_by_lo < 0 || a.sfb_by_hi >= FDW_GY)) throw std::runtime_error("mnist_fc_grad_sfb: tile rows");
+  const int nby = part ? (a.sfb_by_hi - a.sfb_by_lo + 1) + (a.sfb_by_hi < FDW_GY - 1 ? 1 : 0) : FDW_GY;
+  fc_grad_sfb<<<OUTS_BLOCKS + FDW_GX * nby, 256, sm, s>>>(a);
+}
+
+void mnist_sfb_tile_rows(int row0, int row1, int* by_lo, int* by_hi) {
+  *by_lo = row0 / FDW_BM;
+  *by_hi = (row1 - 1) / FDW_BM;
 }
 
 void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s) {

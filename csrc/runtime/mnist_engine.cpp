@@ -82,6 +82,7 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipEventCreateWithFlags(&ev_p2_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_dx_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_sfb_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_wag_, hipEventDisableTiming));
     for (auto& e : pev_) HIP_OK(hipEventCreate(&e));  // timing events (phase timer)
   }
   ~MnistEngine() override {
@@ -100,6 +101,7 @@ class MnistEngine : public torch::CustomClassHolder {
     hipEventDestroy(ev_p2_);
     hipEventDestroy(ev_dx_);
     hipEventDestroy(ev_sfb_);
+    hipEventDestroy(ev_wag_);
     for (auto& e : pev_) hipEventDestroy(e);
   }
 
@@ -190,7 +192,6 @@ class MnistEngine : public torch::CustomClassHolder {
   // the reference's round-robin parameter sharding across PS tasks.
   void set_zero(bool on) {
     if (!on) { zero_ = false; return; }
-    sfb_ = false;  // ZeRO-1 shards the fc1 optimizer instead (reduce-scatter / all-gather)
     const int64_t W = world();
     TORCH_CHECK(W > 1, "set_zero: needs a communicator with world > 1");
     TORCH_CHECK((OFF_BD1 - OFF_WD1) % (W * 64) == 0, "set_zero: fc1 weight not divisible into ", W, " shards");
@@ -204,7 +205,6 @@ class MnistEngine : public torch::CustomClassHolder {
   void set_fc_sfb(bool on) {
     if (!on) { sfb_ = false; return; }
     TORCH_CHECK(comm_ || ipc_, "set_fc_sfb: attach a communicator first");
-    TORCH_CHECK(!zero_, "set_fc_sfb: ZeRO-1 is on");
     const int64_t W = world();
     sfb_rs_ = mnist_sfb_slot_elems((int)B_);
     auto bf = at::TensorOptions().dtype(at::kBFloat16).device(at::kCUDA, device_);
@@ -352,7 +352,7 @@ class MnistEngine : public torch::CustomClassHolder {
   void train_step() { train_step_impl(true); }
 
   void train_step_impl(bool join_end) {
-    if (zero_) {
+    if (zero_ && !sfb_active()) {
       train_step_zero();
       return;
     }
@@ -542,11 +542,22 @@ class MnistEngine : public torch::CustomClassHolder {
   //   o: [wait gathers] fc gradients over K = W*B (mnist_fc_grad_sfb) -> [wait dX: it reads the old
   //      fc1 weights] fc-region optimizer
   // Cross-step overlap as in train_step_dp: the fc optimizer runs beside the next conv forward.
+  //   With ZeRO-1 on (set_zero), each rank computes only its fc1 shard's dW rows (plus the bias row
+  //   and the output layer), runs the fc optimizer on that shard, and the updated bf16 shards are
+  //   all-gathered at the start of the next step on c, beside the conv forward (the fc forward
+  //   waits for it): the K = W*B GEMM and the fc Adam shrink W-fold for one extra 6.4 MB / W
+  //   weight gather per rank.
   void train_step_sfb(bool join_end) {
     hipStream_t s = stream();
     const double scale = 1.0 / (double)world();
     const bool bf = bf16_comm_;
+    const bool shard = zero_;
+    const int64_t rk = rank_in_comm();
     MnistStepArgs a = args();
+    if (shard) {
+      const int64_t rows = zshard_ / HID;  // fc1 weight rows per rank
+      mnist_sfb_tile_rows((int)(rk * rows), (int)((rk + 1) * rows), &a.sfb_by_lo, &a.sfb_by_hi);
+    }
     a.t_out = (int64_t*)tnext_.data_ptr();
     a.step_bump = (int64_t*)step_.data_ptr();
     if (bf) {
@@ -558,6 +569,19 @@ class MnistEngine : public torch::CustomClassHolder {
       HIP_OK(hipStreamWaitEvent(s, ev_sfb_, 0));
       pending_sfb_ = false;
     }
+    if (shard) {  // last step's updated fc1 bf16 shards -> every rank, beside the conv forward
+      // the main stream takes the (sharded, W-fold smaller) fc optimizer's event first and the comm
+      // stream only the main stream's: a second stream waiting on the optimizer stream's event inside
+      // a multi-step capture crashed the HIP graph capture (host SIGSEGV, bench --zero 1 --fc_sfb 1)
+      if (pending_opt_a_) {
+        HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+        pending_opt_a_ = false;
+      }
+      HIP_OK(hipEventRecord(ev_start_, s));
+      HIP_OK(hipStreamWaitEvent(comm_stream_, ev_start_, 0));
+      ag_w(comm_stream_);
+      HIP_OK(hipEventRecord(ev_wag_, comm_stream_));
+    }
     mnist_forward_conv(a, s);
     HIP_OK(hipEventRecord(ev_p2_, s));
     HIP_OK(hipStreamWaitEvent(comm_stream_, ev_p2_, 0));
@@ -567,6 +591,7 @@ class MnistEngine : public torch::CustomClassHolder {
       HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
       pending_opt_a_ = false;
     }
+    if (shard) HIP_OK(hipStreamWaitEvent(s, ev_wag_, 0));
     mnist_forward_fc(a, true, s);
     mark(P_FWD, s);
     HIP_OK(hipEventRecord(ev_a_, s));
@@ -581,7 +606,13 @@ class MnistEngine : public torch::CustomClassHolder {
     mark(P_BFC, s);
     HIP_OK(hipEventRecord(ev_dx_, s));
     HIP_OK(hipStreamWaitEvent(opt_stream_, ev_dx_, 0));
-    apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 0, opt_stream_, (const int64_t*)tnext_.data_ptr());
+    if (shard) {
+      apply_optimizer_range(OFF_WD1 + rk * zshard_, OFF_WD1 + (rk + 1) * zshard_, scale, 0, opt_stream_,
+                            (const int64_t*)tnext_.data_ptr());
+      apply_optimizer_range(OFF_BD1, TOTAL, scale, 0, opt_stream_, (const int64_t*)tnext_.data_ptr());
+    } else {
+      apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 0, opt_stream_, (const int64_t*)tnext_.data_ptr());
+    }
     HIP_OK(hipEventRecord(ev_opt_a_, opt_stream_));
     mnist_backward_b(a, s, conv_fork_ ? aux_stream_ : nullptr, ev_fork_, ev_join_);
     mnist_conv_grad_reduce(a, s);
@@ -837,7 +868,7 @@ class MnistEngine : public torch::CustomClassHolder {
     else ipc_->all_gather_raw(pb, 2, S, st);
   }
 
-  bool sfb_active() const { return sfb_ && !zero_ && !fp32_ && dp() && sfp2_.defined(); }
+  bool sfb_active() const { return sfb_ && !fp32_ && dp() && sfp2_.defined(); }
   // in-place all-gather of one SFB factor array ([W][S], this rank's shard at r*S): IPC when its
   // staging holds the shard (one kernel reading every peer at once), else RCCL
   void gather_sfb(bool p2part, hipStream_t st) {
@@ -966,6 +997,8 @@ class MnistEngine : public torch::CustomClassHolder {
       a.sfb_dr = (const uint16_t*)sfdr_.data_ptr();
       a.sfb_rs = sfb_rs_;
     }
+    a.sfb_by_lo = 0;
+    a.sfb_by_hi = -1;  // all tile rows (train_step_sfb narrows it under ZeRO)
     return a;
   }
 
@@ -999,7 +1032,7 @@ class MnistEngine : public torch::CustomClassHolder {
   bool sfb_ = false, pending_sfb_ = false;
   at::Tensor sfp2_, sfdr_;
   int64_t sfb_rs_ = 0;
-  hipEvent_t ev_p2_ = nullptr, ev_dx_ = nullptr, ev_sfb_ = nullptr;
+  hipEvent_t ev_p2_ = nullptr, ev_dx_ = nullptr, ev_sfb_ = nullptr, ev_wag_ = nullptr;
   // measured on one MI355X: the forked conv2 wgrad only contends with dgrad for CUs (110 vs 100 us/step)
   bool conv_fork_ = false;
   // one GPU + Adam: the optimizer kernel also reduces the conv gradient slabs and bumps the step

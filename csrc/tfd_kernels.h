@@ -62,6 +62,9 @@ struct MnistStepArgs {
   const uint16_t* sfb_p2;
   const uint16_t* sfb_dr;
   int64_t sfb_rs;
+  // ZeRO-sharded SFB: only the 64-row fc1 dW tile rows [sfb_by_lo, sfb_by_hi] (this rank's shard)
+  // plus the bias tile row are computed; sfb_by_hi < sfb_by_lo (default 0, -1) means all rows
+  int sfb_by_lo, sfb_by_hi;
 };
 
 int mnist_fc1_splits(int B);
@@ -100,6 +103,8 @@ void mnist_adam_fc(const MnistStepArgs& a, MnistAdamArgs o, hipStream_t s, int b
 // GEMM over the all-gathered factors (K = W*B). Writes the summed fc-region gradients (bucket A)
 // like mnist_backward_a part 1 (bf16 into gbf_a when set), identical on every rank.
 void mnist_fc_grad_sfb(const MnistStepArgs& a, hipStream_t s);
+// fc1 dW tile-row range (64 rows per tile row) covering flat fc1 weight rows [row0, row1)
+void mnist_sfb_tile_rows(int row0, int row1, int* by_lo, int* by_hi);
 // bf16 elements of one rank's sfb_dr slot for batch B (dh + hd + dlogits, padded to 64)
 int64_t mnist_sfb_slot_elems(int B);
 // One GPU: fc1 dW and the output-layer gradients with ApplyAdam fused into their epilogues (the fc

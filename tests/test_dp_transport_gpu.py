@@ -172,10 +172,11 @@ def _bench(args, nproc=1, timeout=300):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("sfb", [1, 0])
-def test_bench_two_ranks_one_gpu_over_ipc(cuda, sfb):
-    r = _bench(["--gpus", "2", "--steps", "20", "--warmup", "5", "--min_warmup_ms", "50", "--fc_sfb", str(sfb)],
-               nproc=2)
+@pytest.mark.parametrize("sfb,zero", [(1, 0), (0, 0), (1, 1)])
+def test_bench_two_ranks_one_gpu_over_ipc(cuda, sfb, zero):
+    r = _bench(["--gpus", "2", "--steps", "20", "--warmup", "5", "--min_warmup_ms", "50", "--fc_sfb", str(sfb),
+                "--zero", str(zero)], nproc=2)
+    assert r["config"]["zero1_fc1"] == bool(zero)
     kind = "ipc+sfb" if sfb else "ipc"
     assert r["n_gpus"] == 2 and r["config"]["dp_transport"] == kind and r["config"]["parallelism"] == "dp2"
     assert r["value"] > 0 and r["config"]["global_batch"] == 256

@@ -60,7 +60,7 @@ def test_ipc_allreduce_multiprocess_one_gpu(cuda, world, n):
         assert torch.allclose(outs[2], torch.full((n,), float(tot * world ** 2)))
 
 
-def _engine_dp_worker(rank, world, B, steps, sfb=False):
+def _engine_dp_worker(rank, world, B, steps, sfb=False, zero=False):
     from tensorflow_distributed_amd.models import mnist_cnn as M
     from tensorflow_distributed_amd.parallel.ipc import make_ipc_comm
 
@@ -73,6 +73,8 @@ def _engine_dp_worker(rank, world, B, steps, sfb=False):
     if sfb:
         eng.set_fc_sfb(True)
         assert eng.fc_sfb()
+    if zero:
+        eng.set_zero(True)
     g = torch.Generator().manual_seed(7)
     x = torch.rand(steps, world * B, 784, generator=g)
     y = torch.randint(0, 10, (steps, world * B), generator=g, dtype=torch.int32)
@@ -89,6 +91,7 @@ def _engine_dp_worker(rank, world, B, steps, sfb=False):
             else:
                 eng.replay("t", 1)
             torch.cuda.current_stream().synchronize()
+        eng.sync_params()  # ZeRO: gather every rank's fc1 shard (master, slots, bf16 shadow)
     torch.cuda.synchronize()
     out = eng.params().cpu(), int(eng.step_tensor().item()), comm.error(), eng.world()
     comm.close()
@@ -263,3 +266,18 @@ def test_engine_zero1_matches_replicated_dp(cuda, world):
     d = (zr[0][0] - rp[0][0]).abs()
     assert torch.equal(zr[0][0], rp[0][0]), (d.max().item(), (d > 0).float().mean().item())
     assert torch.equal(zr[0][2], rp[0][2])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_engine_sfb_zero_shards_equal_sfb(cuda, world):
+    """SFB with ZeRO-1 (each rank forms and applies only its fc1 shard's gradient, bf16 shards
+    all-gathered beside the next conv forward) gives bit-identical parameters to plain SFB."""
+    B, steps = 32, 4
+    zr = run_ranks(_engine_dp_worker, world, B, steps, True, True, timeout=300)
+    rp = run_ranks(_engine_dp_worker, world, B, steps, True, False, timeout=300)
+    for p, st, e, w in zr + rp:
+        assert e == 0 and st == steps
+    for p, *_ in zr:
+        assert torch.equal(p, zr[0][0])
+    d = (zr[0][0] - rp[0][0]).abs()
+    assert torch.equal(zr[0][0], rp[0][0]), (d.max().item(), (d > 0).float().mean().item())
