@@ -178,12 +178,16 @@ def main(argv=None):
 
     ctx.barrier()
     torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     with torch.cuda.stream(s):
+        ev0.record(s)
         run(a.steps)
+        ev1.record(s)
     torch.cuda.synchronize(dev)
     ctx.barrier()
     dt = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)  # device time of the same K steps (diagnostic: host/sync overhead = dt - this)
     if a.zero:
         with torch.cuda.stream(s):
             eng.sync_params()
@@ -206,6 +210,7 @@ def main(argv=None):
             "warmup": a.warmup,
             "warmup_extra_steps": extra,
             "ms_per_step": round(ms, 5),
+            "gpu_event_ms_per_step": round(gpu_ms / a.steps, 5),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(img_s / BASELINE_IMG_PER_S, 1),
