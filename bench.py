@@ -44,6 +44,9 @@ def main(argv=None):
                     "untimed steps until this much warm-up time has passed (GPU clock ramp; reported in the JSON)")
     ap.add_argument("--graph_steps", type=int, default=20, help="training steps captured per hipGraph "
                     "(device-side step counter/data cursor/dropout key make step i+1 of a graph the next step)")
+    ap.add_argument("--lead_steps", type=int, default=0, help="timed region: launch this many one-step graphs "
+                    "first, then ONE graph of the remaining steps (the GPU starts on the small launch while the "
+                    "host enqueues the big one)")
     ap.add_argument("--phases", type=int, default=1, help="after the timed steps, replay a few steps of a graph "
                     "with HIP timing events at the phase boundaries and report the GPU phase breakdown (untimed)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="compute dtype: bf16 MFMA operands "
@@ -136,11 +139,14 @@ def main(argv=None):
         graph_mode = not a.eager
         eng.train_step()  # one eager step first: sets kernel attributes outside capture
         gsteps = max(1, a.graph_steps)
+        lead = max(0, min(a.lead_steps, a.steps - 1)) if graph_mode else 0
         if graph_mode:
             try:
                 eng.capture_train_step("train")
                 if gsteps > 1:
                     eng.capture_train_steps("trainN", gsteps)
+                if lead:
+                    eng.capture_train_steps("timed", a.steps - lead)
             except Exception as e:  # pragma: no cover - capture support depends on the RCCL build
                 print(f"# hipGraph capture failed ({e!r}); timing eager launches", file=sys.stderr)
                 graph_mode = False
@@ -182,11 +188,20 @@ def main(argv=None):
     t0 = time.perf_counter()
     with torch.cuda.stream(s):
         ev0.record(s)
-        run(a.steps)
+        if lead:
+            eng.replay("train", lead)
+            eng.replay("timed", 1)
+        else:
+            run(a.steps)
         ev1.record(s)
+    t_launched = time.perf_counter()
     torch.cuda.synchronize(dev)
+    t_synced = time.perf_counter()
     ctx.barrier()
     dt = time.perf_counter() - t0
+    if os.environ.get("TFD_BENCH_DIAG") and rank == 0:
+        print(f"# timed region: host launch {1e6 * (t_launched - t0):.1f} us, sync wait "
+              f"{1e6 * (t_synced - t_launched):.1f} us, barrier {1e6 * (t0 + dt - t_synced):.1f} us", file=sys.stderr)
     gpu_ms = ev0.elapsed_time(ev1)  # device time of the same K steps (diagnostic: host/sync overhead = dt - this)
     if a.zero:
         with torch.cuda.stream(s):

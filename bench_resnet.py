@@ -33,7 +33,7 @@ def main(argv=None):
                     "forward epilogue (no separate statistics pass over the conv output)")
     ap.add_argument("--mask_from_y", type=int, default=1, help="1: residual-free BN backward recomputes its relu "
                     "mask from the conv output instead of reading the BN output")
-    ap.add_argument("--fuse_joins", type=int, default=0, help="1: residual-join gradient sums in the dgrad "
+    ap.add_argument("--fuse_joins", type=int, default=1, help="1: residual-join gradient sums in the dgrad "
                     "epilogue (0: autograd adds; measured faster, see resnet.GradJoin)")
     ap.add_argument("--lr", type=float, default=0.1)
     a = ap.parse_args(argv)

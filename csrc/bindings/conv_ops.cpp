@@ -229,7 +229,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> softmax_xent_op(const at::Tensor&
 at::Tensor pad_channels_op(const at::Tensor& x, int64_t cout) {
   check_f32(x, "x");
   const int cin = (int)x.size(-1);
-  TORCH_CHECK(cout >= cin, "pad_channels: cout < cin");
+  TORCH_CHECK(cout >= cin && cout % 8 == 0, "pad_channels: need cout >= cin and cout % 8 == 0");
   std::vector<int64_t> sh(x.sizes().begin(), x.sizes().end());
   sh.back() = cout;
   auto y = at::empty(sh, x.options().dtype(at::kBFloat16));

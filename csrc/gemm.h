@@ -90,9 +90,13 @@ struct GemmSmem {
 // RS = register stages: with RS = 2 the global loads of tile t+2 are issued while tile t+1 still
 // sits in registers, so every load has ~2 K-iterations of latency cover (twice the bytes in flight
 // per CU -- these small GEMMs are bound by bytes-in-flight / memory latency, not by MFMA rate).
-template <int BM, int BN, int BK, int WM, int WN, class LA, class LB, class EPI, int RS = 1>
-__device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI& epi, int m0, int n0,
-                                           int kbeg, int kend, bf16* smem) {
+// gemm_mainloop: the K loop only, accumulating into the caller's acc[TM][TN] (TM = BM/WM/16,
+// TN = BN/WN/16); gemm_block = mainloop + per-fragment epilogue calls. Kernels with a block-wide
+// epilogue (LDS-staged stores, csrc/kernels/conv_nhwc.hip) call the mainloop directly. The loop
+// ends with a barrier, so the operand LDS images are dead when it returns.
+template <int BM, int BN, int BK, int WM, int WN, class LA, class LB, int RS = 1>
+__device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0, int n0, int kbeg, int kend,
+                                              bf16* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16]) {
   constexpr int NT = 64 * WM * WN;
   using TA = LdsTile<BM, BK, LA::KC>;
   using TB = LdsTile<BN, BK, LB::KC>;
@@ -109,7 +113,6 @@ __device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   uint4 ra[RS][CA], rb[RS][CB];
-  f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -226,6 +229,15 @@ __device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI
       }
     }
   }
+}
+
+template <int BM, int BN, int BK, int WM, int WN, class LA, class LB, class EPI, int RS = 1>
+__device__ __forceinline__ void gemm_block(const LA& la, const LB& lb, const EPI& epi, int m0, int n0,
+                                           int kbeg, int kend, bf16* smem) {
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+  f32x4 acc[TM][TN];
+  gemm_mainloop<BM, BN, BK, WM, WN, LA, LB, RS>(la, lb, m0, n0, kbeg, kend, smem, acc);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid / WN, wn = wid % WN;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll

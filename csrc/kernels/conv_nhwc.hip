@@ -201,6 +201,111 @@ struct StoreBf16Stats {
   }
 };
 
+// ---- LDS-staged epilogue (bf16 outputs) ----
+// The fragment-order epilogues above store 2 B per lane in 4 row-strided 32-B pieces per wave
+// instruction, and AddStoreBf16 serialises its scalar residual loads on memory latency (the
+// residual-join dgrad measured 3.6x slower with it). Here the block's fp32 accumulator tile goes to
+// LDS (row-major, pitch BN + 4 floats: the 4 row groups of a fragment store land 16 banks apart),
+// then every thread owns whole 8-column chunks: its residual chunks are loaded with 16-B buffer
+// loads issued BEFORE the accumulator is staged, and each output chunk leaves as ONE 16-B store, so
+// a wave writes whole 128-B lines. The sum v + add is formed in fp32 and rounded once (bit-identical
+// to AddStoreBf16). STATS: per-column sums / sums of squares of the stored (bf16-rounded) values,
+// fixed summation order (deterministic), written to part[blockIdx.y][2][N].
+template <int BM, int BN, int WM, int WN>
+struct LdsEpi {
+  static constexpr int NT = 64 * WM * WN;
+  static constexpr int PITCH = BN + 4;            // floats
+  static constexpr int CPR = BN / 8;              // 8-column chunks per row
+  static constexpr int CH = BM * CPR / NT;        // chunks per thread
+  static constexpr int RG = NT / CPR;             // row groups (threads sharing a chunk column)
+  static constexpr int BYTES = BM * PITCH * 4;
+  static_assert(BM * CPR % NT == 0 && NT % CPR == 0, "whole chunks per thread");
+};
+template <int BM, int BN, int WM, int WN, bool ADD, bool STATS>
+__device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], char* smem, uint16_t* __restrict__ y,
+                                             const uint16_t* __restrict__ add, int M, int N, int m0, int n0,
+                                             float* __restrict__ part) {
+  using E = LdsEpi<BM, BN, WM, WN>;
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+  const int cc = tid % E::CPR, g0 = tid / E::CPR;  // this thread's chunk column and first row
+  const int n = n0 + cc * 8;
+  const uint32_t ybytes = (uint32_t)M * (uint32_t)N * 2u;
+  uint4 q[E::CH];
+  if constexpr (ADD) {
+#pragma unroll
+    for (int c = 0; c < E::CH; ++c) {
+      const int m = m0 + g0 + c * E::RG;
+      q[c] = buf_ld(add, ybytes, (uint32_t)m * (uint32_t)N + (uint32_t)n, m < M && n < N);
+    }
+  }
+  float* cs = reinterpret_cast<float*>(smem);
+  __syncthreads();  // (the mainloop's last barrier already retired the operand images; cheap insurance)
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int r0 = wm * WTM + 16 * i + 4 * (lane >> 4), col = wn * WTN + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[(r0 + r) * E::PITCH + col] = acc[i][j][r];
+    }
+  __syncthreads();
+  float s[8], sq[8];
+  if constexpr (STATS) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s[k] = 0.f; sq[k] = 0.f; }
+  }
+#pragma unroll
+  for (int c = 0; c < E::CH; ++c) {
+    const int row = g0 + c * E::RG, m = m0 + row;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + row * E::PITCH + cc * 8);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * E::PITCH + cc * 8 + 4);
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if constexpr (ADD) {
+      const uint32_t w[4] = {q[c].x, q[c].y, q[c].z, q[c].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[2 * k] += __uint_as_float(w[k] << 16);
+        v[2 * k + 1] += __uint_as_float(w[k] & 0xFFFF0000u);
+      }
+    }
+    const uint4 o = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+    if (m < M && n < N) {
+      *reinterpret_cast<uint4*>(y + (size_t)m * N + n) = o;
+      if constexpr (STATS) {
+        const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float f0 = __uint_as_float(w[k] << 16), f1 = __uint_as_float(w[k] & 0xFFFF0000u);
+          s[2 * k] += f0;
+          sq[2 * k] = fmaf(f0, f0, sq[2 * k]);
+          s[2 * k + 1] += f1;
+          sq[2 * k + 1] = fmaf(f1, f1, sq[2 * k + 1]);
+        }
+      }
+    }
+  }
+  if constexpr (STATS) {
+    static_assert(2 * E::RG * BN * 4 <= E::BYTES, "stats reduction fits in the staged tile");
+    __syncthreads();  // every thread has read its chunks: reuse the tile for [2][RG][BN]
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      cs[g0 * BN + cc * 8 + k] = s[k];
+      cs[(E::RG + g0) * BN + cc * 8 + k] = sq[k];
+    }
+    __syncthreads();
+    for (int col = tid; col < BN; col += E::NT) {
+      const int nn = n0 + col;
+      if (nn >= N) continue;
+      float a = 0.f, b = 0.f;
+#pragma unroll 8
+      for (int g = 0; g < E::RG; ++g) { a += cs[g * BN + col]; b += cs[(E::RG + g) * BN + col]; }
+      part[(size_t)blockIdx.y * 2 * N + nn] = a;
+      part[(size_t)blockIdx.y * 2 * N + N + nn] = b;
+    }
+  }
+}
+
 template <int BM, int BN>
 struct Tile {
   static constexpr int WM = 2, WN = 2, BK = 64;
@@ -229,6 +334,21 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_kernel(LA la, LB lb, E
                                                          (bf16*)smem_raw);
 }
 
+#ifndef TFD_CONV_LDS_EPI  // 1: bf16-output conv GEMMs (fwd, fwd+stats, dgrad) use the LDS-staged epilogue
+#define TFD_CONV_LDS_EPI 1
+#endif
+
+// bf16-output GEMM with the LDS-staged epilogue: Y = A B (+ add), no split-K.
+template <int BM, int BN, class LA, class LB, bool ADD>
+__global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_kernel(LA la, LB lb, uint16_t* y, const uint16_t* add,
+                                                                      int M, int N, int KD) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  f32x4 acc[BM / 32][BN / 32];
+  gemm_mainloop<BM, BN, CBK, 2, 2, LA, LB, TFD_CONV_RS>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
+                                                       (bf16*)smem_raw, acc);
+  lds_epilogue<BM, BN, 2, 2, ADD, false>(acc, smem_raw, y, add, M, N, blockIdx.y * BM, blockIdx.x * BN, nullptr);
+}
+
 // Forward conv + BN statistics: the block's column partials (sum, sum of squares over its BM rows)
 // go to part[blockIdx.y][2][N] -- the [nblk][2][C] layout bn_final_kernel reduces -- so the
 // forward BN needs no separate pass over the conv output. Fixed reduction order (deterministic).
@@ -237,6 +357,13 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB
                                                          float* part) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   constexpr int WM = 2, WN = 2, WTN = BN / WN, TN = WTN / 16;
+#if TFD_CONV_LDS_EPI
+  (void)TN;
+  f32x4 acc[BM / 32][BN / 32];
+  gemm_mainloop<BM, BN, CBK, WM, WN, LA, LB, TFD_CONV_RS>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
+                                                         (bf16*)smem_raw, acc);
+  lds_epilogue<BM, BN, WM, WN, false, true>(acc, smem_raw, y, nullptr, M, N, blockIdx.y * BM, blockIdx.x * BN, part);
+#else
   float s[TN], q[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { s[j] = 0.f; q[j] = 0.f; }
@@ -271,11 +398,32 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB
     part[(size_t)blockIdx.y * 2 * N + n] = a;
     part[(size_t)blockIdx.y * 2 * N + N + n] = b;
   }
+#endif
+}
+
+template <int BM, int BN, class LA, class LB>
+constexpr int stats_smem() {
+  constexpr int g = GemmSmem<BM, BN, CBK, LA, LB>::BYTES;
+  return TFD_CONV_LDS_EPI && LdsEpi<BM, BN, 2, 2>::BYTES > g ? LdsEpi<BM, BN, 2, 2>::BYTES : g;
+}
+
+template <int BM, int BN, class LA, class LB, bool ADD>
+void launch_gemm_bf16(const LA& la, const LB& lb, uint16_t* y, const uint16_t* add, int M, int N, int KD,
+                      hipStream_t st) {
+  constexpr int sm = stats_smem<BM, BN, LA, LB>();
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_bf16_kernel<BM, BN, LA, LB, ADD>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+    attr = true;
+  }
+  dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, 1);
+  gemm_bf16_kernel<BM, BN, LA, LB, ADD><<<grid, 256, sm, st>>>(la, lb, y, add, M, N, KD);
 }
 
 template <int BM, int BN, class LA, class LB>
 void launch_gemm_stats(const LA& la, const LB& lb, uint16_t* y, int M, int N, int KD, float* part, hipStream_t st) {
-  constexpr int sm = GemmSmem<BM, BN, CBK, LA, LB>::BYTES;
+  constexpr int sm = stats_smem<BM, BN, LA, LB>();
   static_assert(sm >= 2 * 2 * BN * 4, "stats reduction fits in the GEMM's LDS");
   static bool attr = false;
   if (!attr) {
@@ -314,6 +462,19 @@ void dispatch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int KD, 
   else launch_gemm<64, 64>(la, lb, epi, M, N, KD, splits, st);
 }
 
+// bf16-output GEMM (optionally + add), same tile choice as dispatch()
+template <class LA, class LB>
+void dispatch_bf16(const LA& la, const LB& lb, uint16_t* y, const uint16_t* add, int M, int N, int KD, hipStream_t st) {
+  const bool big = use_big_tiles(M, N);
+  if (add) {
+    if (big) launch_gemm_bf16<128, 128, LA, LB, true>(la, lb, y, add, M, N, KD, st);
+    else launch_gemm_bf16<64, 64, LA, LB, true>(la, lb, y, add, M, N, KD, st);
+  } else {
+    if (big) launch_gemm_bf16<128, 128, LA, LB, false>(la, lb, y, add, M, N, KD, st);
+    else launch_gemm_bf16<64, 64, LA, LB, false>(la, lb, y, add, M, N, KD, st);
+  }
+}
+
 Geo make_geo(const ConvShape& c, int M, int KD) {
   Geo g;
   g.N = c.N; g.H = c.H; g.W = c.W; g.C = c.C; g.K = c.K; g.R = c.R; g.S = c.S; g.st = c.stride; g.pad = c.pad;
@@ -337,10 +498,12 @@ void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t
   DenseX<false> lb{w, c.K, c.K, KD};
   if (is_pointwise(c)) {
     DenseX<true> la{x, c.C, M, c.C};
-    dispatch(la, lb, epi, M, c.K, KD, 1, st);
+    if (TFD_CONV_LDS_EPI) dispatch_bf16(la, lb, y, nullptr, M, c.K, KD, st);
+    else dispatch(la, lb, epi, M, c.K, KD, 1, st);
   } else {
     FwdA la{x, make_geo(c, M, KD)};
-    dispatch(la, lb, epi, M, c.K, KD, 1, st);
+    if (TFD_CONV_LDS_EPI) dispatch_bf16(la, lb, y, nullptr, M, c.K, KD, st);
+    else dispatch(la, lb, epi, M, c.K, KD, 1, st);
   }
 }
 
@@ -383,8 +546,56 @@ static void conv_dgrad_impl(const ConvShape& c, const uint16_t* dy, const uint16
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                 const uint16_t* add) {
   const int M = c.N * c.H * c.W;
+  if (TFD_CONV_LDS_EPI) {
+    const int KD = c.R * c.S * c.K;
+    if (is_pointwise(c)) {
+      DenseX<true> la{dy, c.K, M, c.K};
+      DenseX<true> lb{w, c.K, c.C, c.K};
+      dispatch_bf16(la, lb, dx, add, M, c.C, KD, st);
+    } else {
+      Geo g = make_geo(c, M, KD);
+      dispatch_bf16(DgradA{dy, g}, DgradB{w, g}, dx, add, M, c.C, KD, st);
+    }
+    return;
+  }
   if (add) conv_dgrad_impl(c, dy, w, AddStoreBf16{dx, add, M, c.C}, st);
   else conv_dgrad_impl(c, dy, w, StoreBf16{dx, M, c.C}, st);
+}
+
+// Weight-gradient tile: dW is [R*S*C][K] with a very long reduction over pixels (split-K), so the
+// block's operand traffic per MFMA decides its speed. 64x64 tiles stream 32 FLOP per staged byte,
+// 128x64 43 and 128x128 64; the wide tiles are used whenever dW has the rows/columns for them
+// (TFD_WGRAD_TILES=0: always 64x64, the round-1 choice).
+#ifndef TFD_WGRAD_TILES
+#define TFD_WGRAD_TILES 1
+#endif
+enum WgTile { WG64x64, WG128x64, WG128x128 };
+WgTile wgrad_tile(const ConvShape& c) {
+  const int MT = c.R * c.S * c.C;
+  if (!TFD_WGRAD_TILES || MT < 128) return WG64x64;
+  if (c.K % 128 == 0) return WG128x128;
+  return WG128x64;
+}
+
+int conv_wgrad_splits(const ConvShape& c) {
+  // enough (tile x split) blocks to fill the chip; each split keeps >= 2048 pixels of K
+  const int P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
+  const WgTile t = wgrad_tile(c);
+  const int bm = t == WG64x64 ? 64 : 128, bn = t == WG128x128 ? 128 : 64;
+  const long tiles = (long)((MT + bm - 1) / bm) * ((c.K + bn - 1) / bn);
+  int s = (int)std::max<long>(1, 512 / std::max<long>(1, tiles));
+  s = std::min(s, std::max(1, P / 2048));
+  return s;
+}
+
+template <class LA>
+static void wgrad_launch(const ConvShape& c, const LA& la, const DenseX<false>& lb, const AccF32& epi, int MT, int P,
+                         int splits, hipStream_t st) {
+  switch (wgrad_tile(c)) {
+    case WG128x128: launch_gemm<128, 128>(la, lb, epi, MT, c.K, P, splits, st); break;
+    case WG128x64: launch_gemm<128, 64>(la, lb, epi, MT, c.K, P, splits, st); break;
+    default: launch_gemm<64, 64>(la, lb, epi, MT, c.K, P, splits, st);
+  }
 }
 
 void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float* dw, int splits, hipStream_t st,
@@ -395,20 +606,11 @@ void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float
   DenseX<false> lb{dy, c.K, c.K, P};
   if (is_pointwise(c)) {  // dW = X^T dY
     DenseX<false> la{x, c.C, c.C, P};
-    dispatch(la, lb, epi, MT, c.K, P, splits, st);
+    wgrad_launch(c, la, lb, epi, MT, P, splits, st);
   } else {
     WgradA la{x, make_geo(c, MT, P)};
-    dispatch(la, lb, epi, MT, c.K, P, splits, st);
+    wgrad_launch(c, la, lb, epi, MT, P, splits, st);
   }
-}
-
-int conv_wgrad_splits(const ConvShape& c) {
-  // enough (tile x split) blocks to fill the chip; each split keeps >= 2048 pixels of K
-  const int P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
-  const long tiles = (long)((MT + 63) / 64) * ((c.K + 63) / 64);
-  int s = (int)std::max<long>(1, 512 / std::max<long>(1, tiles));
-  s = std::min(s, std::max(1, P / 2048));
-  return s;
 }
 
 void linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, float* y, int M, int Kin, int N,

@@ -1762,7 +1762,10 @@ constexpr int MAD_C1F4 = (int)(OFF_WC2 / 4);   // 208
 constexpr int MAD_C2END = (int)(OFF_WD1 / 4);  // 13024
 constexpr int MAD_C1BLK = MAD_C1F4 / 16;       // 13
 constexpr int MAD_C2BLK = (MAD_C2END - MAD_C1F4 + 63) / 64;  // 201
-constexpr int MAD_FC_BLOCKS = 1024;
+#ifndef TFD_MAD_FC_BLOCKS  // grid-stride blocks of the fc-region Adam
+#define TFD_MAD_FC_BLOCKS 1024
+#endif
+constexpr int MAD_FC_BLOCKS = TFD_MAD_FC_BLOCKS;
 constexpr int MAD_CONV = MAD_C1BLK + MAD_C2BLK;
 constexpr int MAD_GRID = MAD_CONV + MAD_FC_BLOCKS;
 static_assert(MAD_C1F4 % 16 == 0, "conv1 region: whole blocks");

@@ -462,13 +462,18 @@ __global__ __launch_bounds__(NT) void softmax_xent_kernel(const float* __restric
     dl[(size_t)row * K + k] = f2bf_bits((__expf(z[k] - lse) - (k == lbl ? 1.f : 0.f)) * invN);
 }
 
+// one thread per 8-channel output chunk (16-B store; Cout % 8 == 0): the stem input [P][3] fp32 ->
+// [P][8] bf16 is one pixel per thread
 __global__ __launch_bounds__(NT) void pad_channels_kernel(const float* __restrict__ x, uint16_t* __restrict__ y,
                                                           int64_t P, int Cin, int Cout) {
-  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (i >= P * Cout) return;
-  const int c = (int)(i % Cout);
-  const int64_t p = i / Cout;
-  y[i] = c < Cin ? f2bf_bits(x[p * Cin + c]) : (uint16_t)0;
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x, nch = Cout / 8;
+  if (i >= P * nch) return;
+  const int c0 = (int)(i % nch) * 8;
+  const int64_t p = i / nch;
+  float f[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = c0 + j < Cin ? x[p * Cin + c0 + j] : 0.f;
+  reinterpret_cast<uint4*>(y)[i] = pack8(f);
 }
 
 inline int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + NT - 1) / NT)); }
@@ -560,7 +565,7 @@ void softmax_xent(const float* logits, const int* labels, float* loss_rows, floa
 }
 
 void pad_channels(const float* x, uint16_t* y, int P, int Cin, int Cout, hipStream_t s) {
-  const int64_t total = (int64_t)P * Cout;
+  const int64_t total = (int64_t)P * (Cout / 8);
   pad_channels_kernel<<<(int)((total + NT - 1) / NT), NT, 0, s>>>(x, y, P, Cin, Cout);
 }
 

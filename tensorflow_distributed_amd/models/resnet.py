@@ -159,10 +159,11 @@ class GradJoin:
     the parked tensor -- a conv adds it in its dgrad epilogue (``conv2d_dgrad(acc=...)``), so the sum
     costs no extra pass over the activation. Works for either execution order of the paths.
 
-    Off by default (``ResNet(fuse_joins=False)``): measured on MI355X (ResNet-50 b128) the add
-    epilogue's bf16 loads are issued after the K loop and serialise on memory latency, so the
-    pointwise dgrad got 3.6x slower (77 -> 277 us) -- more than the 40 us add kernels it removes.
-    Needs the add tile prefetched into registers before the K loop to pay off."""
+    On by default (``ResNet(fuse_joins=True)``). With the round-1 fragment-order epilogue the
+    add's scalar bf16 loads serialised on memory latency (pointwise dgrad 77 -> 277 us, so it was
+    off); the LDS-staged epilogue (csrc/kernels/conv_nhwc.hip ``lds_epilogue``) issues the add
+    tile as 16-B loads before staging the accumulator and stores whole lines: ResNet-50 b128
+    16.81 -> 16.28 ms/step on one MI355X (profiles/resnet50_epi_ab_r2.log)."""
 
     def __init__(self, n: int):
         self.n = n
@@ -381,7 +382,7 @@ class ResNet:
            101: ("bottleneck", [3, 4, 23, 3])}
 
     def __init__(self, depth: int = 50, num_classes: int = 1000, device=None, seed: int = 0, width: int = 64,
-                 zero_init_residual: bool = True, fuse_joins: bool = False, bn_stats: bool = True):
+                 zero_init_residual: bool = True, fuse_joins: bool = True, bn_stats: bool = True):
         kind, blocks = self.CFG[depth]
         if num_classes % 8 or width % 8:
             raise ValueError("num_classes and width must be multiples of 8 (16-byte MFMA operand chunks)")

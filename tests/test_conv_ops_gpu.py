@@ -32,7 +32,8 @@ CONVS = [  # N, H, W, C, K, R, stride, pad
 ]
 
 
-@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS)
+# the last shape's dgrad (M = 37632, C = 128) takes the 128x128 tiles of the LDS-staged epilogue
+@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS + [(48, 28, 28, 128, 32, 3, 1, 1)])
 def test_conv_fwd_dgrad_wgrad(cuda, N, H, W, C, K, R, st, pad):
     torch.manual_seed(0)
     x = rb(torch.randn(N, H, W, C))

@@ -138,6 +138,31 @@ def test_resnet_block_forward_backward(cuda, depth, bi, hw):
     assert all(v > 0.999 for v in checks.values()), checks
 
 
+@pytest.mark.parametrize("depth", [18, 50])
+def test_residual_join_fusion_matches_autograd_adds(cuda, depth):
+    """fuse_joins (the residual-join gradient sum formed in the dgrad epilogue, GradJoin) against
+    autograd's separate adds: same loss, and every parameter gradient equal up to the one extra
+    bf16 rounding the unfused sum takes."""
+    from tensorflow_distributed_amd.models.resnet import ResNet
+
+    torch.manual_seed(4)
+    x = torch.randn(4, 64, 64, 3, device=cuda)
+    lab = torch.randint(0, 16, (4,), dtype=torch.int32, device=cuda)
+    grads, losses = [], []
+    for fuse in (False, True):
+        m = ResNet(depth, num_classes=16, device=cuda, seed=1, width=16, zero_init_residual=False, fuse_joins=fuse)
+        m.fp.grad.zero_()
+        loss, _ = m.loss(x, lab)
+        loss.backward()
+        torch.cuda.synchronize()
+        losses.append(loss.item())
+        grads.append(m.fp.grad.cpu().clone())
+    assert losses[0] == losses[1]
+    cos = torch.nn.functional.cosine_similarity(grads[0], grads[1], dim=0).item()
+    rel = ((grads[0] - grads[1]).norm() / grads[0].norm()).item()
+    assert cos > 0.999 and rel < 3e-2, (cos, rel)
+
+
 def test_resnet_training_reduces_loss(cuda):
     from tensorflow_distributed_amd.models.resnet import ResNet
 
