@@ -110,6 +110,50 @@ struct DgradB {
   }
 };
 
+// ---- strided dgrad, one output phase (h % st, w % st) at a time ----
+// Input pixel (h, w) = (hh*st + ph, ww*st + pw) receives exactly the taps r = r0 + i*st
+// (r0 = (ph + pad) % st), s = s0 + j*st, each from dY[ho = hh + dh - i][wo = ww + dw - j] with
+// dh = (ph + pad - r0) / st: a dense implicit GEMM over the phase grid with KD = nr*ns*K and no
+// zero taps (the plain DgradA gathers st^2 x more MFMA work, 3/4 of it on zeros at st = 2).
+struct PhaseGeo {
+  int N, Hp, Wp, Ho, Wo, K, C, st, ph, pw, H, W;
+  int r0, s0, nr, ns, dh, dw;
+  int M, KD;
+  uint32_t ybytes, wbytes;
+  FastDiv hpwp, wp, k, nsd;
+};
+struct DgradPhaseA {
+  static constexpr bool KC = true;
+  const uint16_t* __restrict__ dy;
+  PhaseGeo g;
+  __device__ __forceinline__ uint4 operator()(int m, int kk) const {
+    const int n = g.hpwp.div(m), r1 = m - n * g.Hp * g.Wp, hh = g.wp.div(r1), ww = r1 - hh * g.Wp;
+    const int t = g.k.div(kk), k = kk - t * g.K, i = g.nsd.div(t), j = t - i * g.ns;
+    const int ho = hh + g.dh - i, wo = ww + g.dw - j;
+    const bool ok = m < g.M && kk < g.KD && (unsigned)ho < (unsigned)g.Ho && (unsigned)wo < (unsigned)g.Wo;
+    return buf_ld(dy, g.ybytes, (uint32_t)((n * g.Ho + ho) * g.Wo + wo) * g.K + k, ok);
+  }
+};
+struct DgradPhaseB {  // (c, kk) -> W[r][s][c][k], S = filter width
+  static constexpr bool KC = true;
+  const uint16_t* __restrict__ w;
+  PhaseGeo g;
+  int S;
+  __device__ __forceinline__ uint4 operator()(int c, int kk) const {
+    const int t = g.k.div(kk), k = kk - t * g.K, i = g.nsd.div(t), j = t - i * g.ns;
+    const int r = g.r0 + i * g.st, s = g.s0 + j * g.st;
+    return buf_ld(w, g.wbytes, (uint32_t)((r * S + s) * g.C + c) * g.K + k, c < g.C && kk < g.KD);
+  }
+};
+struct PhaseRows {  // phase GEMM row -> pixel row of dX
+  PhaseGeo g;
+  __device__ __forceinline__ uint32_t operator()(int m) const {
+    if (m >= g.M) return 0u;
+    const int n = g.hpwp.div(m), r1 = m - n * g.Hp * g.Wp, hh = g.wp.div(r1), ww = r1 - hh * g.Wp;
+    return (uint32_t)((n * g.H + hh * g.st + g.ph) * g.W + ww * g.st + g.pw);
+  }
+};
+
 // ---- wgrad: A = im2col(X)^T (not KC: chunk of 8 channels at one pixel), B = dY [pix][K] ----
 struct WgradA {
   static constexpr bool KC = false;
@@ -221,22 +265,29 @@ struct LdsEpi {
   static constexpr int BYTES = BM * PITCH * 4;
   static_assert(BM * CPR % NT == 0 && NT % CPR == 0, "whole chunks per thread");
 };
-template <int BM, int BN, int WM, int WN, bool ADD, bool STATS>
+// GEMM row m -> output row (identity; the strided-dgrad phase GEMMs scatter to every st-th pixel)
+struct RowId {
+  __device__ __forceinline__ uint32_t operator()(int m) const { return (uint32_t)m; }
+};
+template <int BM, int BN, int WM, int WN, bool ADD, bool STATS, class RM = RowId>
 __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], char* smem, uint16_t* __restrict__ y,
                                              const uint16_t* __restrict__ add, int M, int N, int m0, int n0,
-                                             float* __restrict__ part) {
+                                             float* __restrict__ part, RM rowmap = RM{}, uint32_t ybytes = 0) {
   using E = LdsEpi<BM, BN, WM, WN>;
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
   const int cc = tid % E::CPR, g0 = tid / E::CPR;  // this thread's chunk column and first row
   const int n = n0 + cc * 8;
-  const uint32_t ybytes = (uint32_t)M * (uint32_t)N * 2u;
+  if (ybytes == 0) ybytes = (uint32_t)M * (uint32_t)N * 2u;
   uint4 q[E::CH];
+  uint32_t orow[E::CH];
+#pragma unroll
+  for (int c = 0; c < E::CH; ++c) orow[c] = rowmap(m0 + g0 + c * E::RG);
   if constexpr (ADD) {
 #pragma unroll
     for (int c = 0; c < E::CH; ++c) {
       const int m = m0 + g0 + c * E::RG;
-      q[c] = buf_ld(add, ybytes, (uint32_t)m * (uint32_t)N + (uint32_t)n, m < M && n < N);
+      q[c] = buf_ld(add, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, m < M && n < N);
     }
   }
   float* cs = reinterpret_cast<float*>(smem);
@@ -271,7 +322,7 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
     }
     const uint4 o = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
     if (m < M && n < N) {
-      *reinterpret_cast<uint4*>(y + (size_t)m * N + n) = o;
+      *reinterpret_cast<uint4*>(y + (size_t)orow[c] * N + n) = o;
       if constexpr (STATS) {
         const uint32_t w[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
@@ -399,6 +450,33 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB
     part[(size_t)blockIdx.y * 2 * N + N + n] = b;
   }
 #endif
+}
+
+// one phase of a strided dgrad: Y rows scattered to the phase's pixels (+ add)
+template <int BM, int BN, bool ADD>
+__global__ __launch_bounds__(256) TFD_CONV_ATTR void dgrad_phase_kernel(DgradPhaseA la, DgradPhaseB lb, uint16_t* dx,
+                                                                        const uint16_t* add) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  f32x4 acc[BM / 32][BN / 32];
+  gemm_mainloop<BM, BN, CBK, 2, 2, DgradPhaseA, DgradPhaseB, TFD_CONV_RS>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0,
+                                                                         la.g.KD, (bf16*)smem_raw, acc);
+  const uint32_t xbytes = (uint32_t)la.g.N * la.g.H * la.g.W * la.g.C * 2u;
+  lds_epilogue<BM, BN, 2, 2, ADD, false, PhaseRows>(acc, smem_raw, dx, add, la.g.M, la.g.C, blockIdx.y * BM,
+                                                   blockIdx.x * BN, nullptr, PhaseRows{la.g}, xbytes);
+}
+
+// pixels of tap-less phases (a 1x1 stride-2 conv leaves 3 of 4 input pixels without a tap):
+// dX = add there, or 0. One thread per 8-channel chunk of a pixel of such a phase.
+__global__ __launch_bounds__(256) void dgrad_empty_phase_kernel(uint16_t* __restrict__ dx, const uint16_t* __restrict__ add,
+                                                                int N, int H, int W, int C, int st, int pad, int R,
+                                                                int S) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, cpp = C / 8;
+  if (i >= (int64_t)N * H * W * cpp) return;
+  const int64_t pix = i / cpp;
+  const int w = (int)(pix % W), h = (int)((pix / W) % H);
+  const int r0 = (h % st + pad) % st, s0 = (w % st + pad) % st;
+  if (r0 < R && s0 < S) return;  // a phase with taps: written by its GEMM
+  reinterpret_cast<uint4*>(dx)[i] = add ? reinterpret_cast<const uint4*>(add)[i] : make_uint4(0u, 0u, 0u, 0u);
 }
 
 template <int BM, int BN, class LA, class LB>
@@ -543,9 +621,67 @@ static void conv_dgrad_impl(const ConvShape& c, const uint16_t* dy, const uint16
   }
 }
 
+#ifndef TFD_DGRAD_PHASES  // 1: strided dgrads as one dense GEMM per output phase (dgrad_strided)
+#define TFD_DGRAD_PHASES 1
+#endif
+template <int BM, int BN, bool ADD>
+static void launch_phase(const DgradPhaseA& la, const DgradPhaseB& lb, uint16_t* dx, const uint16_t* add,
+                         hipStream_t st) {
+  constexpr int sm = GemmSmem<BM, BN, CBK, DgradPhaseA, DgradPhaseB>::BYTES > LdsEpi<BM, BN, 2, 2>::BYTES
+                         ? GemmSmem<BM, BN, CBK, DgradPhaseA, DgradPhaseB>::BYTES : LdsEpi<BM, BN, 2, 2>::BYTES;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dgrad_phase_kernel<BM, BN, ADD>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+    attr = true;
+  }
+  dim3 grid((la.g.C + BN - 1) / BN, (la.g.M + BM - 1) / BM, 1);
+  dgrad_phase_kernel<BM, BN, ADD><<<grid, 256, sm, st>>>(la, lb, dx, add);
+}
+static void dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, const uint16_t* add,
+                          hipStream_t st) {
+  const int s = c.stride;
+  bool empty = false;
+  for (int ph = 0; ph < s; ++ph)
+    for (int pw = 0; pw < s; ++pw) {
+      PhaseGeo g;
+      g.N = c.N; g.H = c.H; g.W = c.W; g.C = c.C; g.K = c.K; g.st = s; g.ph = ph; g.pw = pw;
+      g.Ho = c.Ho(); g.Wo = c.Wo();
+      g.Hp = (c.H - ph + s - 1) / s; g.Wp = (c.W - pw + s - 1) / s;
+      g.r0 = (ph + c.pad) % s; g.s0 = (pw + c.pad) % s;
+      g.nr = g.r0 < c.R ? (c.R - g.r0 + s - 1) / s : 0;
+      g.ns = g.s0 < c.S ? (c.S - g.s0 + s - 1) / s : 0;
+      if (g.nr == 0 || g.ns == 0 || g.Hp <= 0 || g.Wp <= 0) { empty = empty || (g.Hp > 0 && g.Wp > 0); continue; }
+      g.dh = (ph + c.pad - g.r0) / s; g.dw = (pw + c.pad - g.s0) / s;
+      g.M = c.N * g.Hp * g.Wp; g.KD = g.nr * g.ns * c.K;
+      g.ybytes = (uint32_t)((int64_t)c.N * g.Ho * g.Wo * c.K * 2);
+      g.wbytes = (uint32_t)((int64_t)c.R * c.S * c.C * c.K * 2);
+      g.hpwp = FastDiv(g.Hp * g.Wp); g.wp = FastDiv(g.Wp); g.k = FastDiv(c.K); g.nsd = FastDiv(g.ns);
+      DgradPhaseA la{dy, g};
+      DgradPhaseB lb{w, g, c.S};
+      const bool big = use_big_tiles(g.M, c.C);
+      if (add) {
+        if (big) launch_phase<128, 128, true>(la, lb, dx, add, st);
+        else launch_phase<64, 64, true>(la, lb, dx, add, st);
+      } else {
+        if (big) launch_phase<128, 128, false>(la, lb, dx, add, st);
+        else launch_phase<64, 64, false>(la, lb, dx, add, st);
+      }
+    }
+  if (empty) {
+    const int64_t total = (int64_t)c.N * c.H * c.W * (c.C / 8);
+    dgrad_empty_phase_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(dx, add, c.N, c.H, c.W, c.C, s, c.pad, c.R,
+                                                                         c.S);
+  }
+}
+
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                 const uint16_t* add) {
   const int M = c.N * c.H * c.W;
+  if (TFD_CONV_LDS_EPI && TFD_DGRAD_PHASES && c.stride > 1) {
+    dgrad_strided(c, dy, w, dx, add, st);
+    return;
+  }
   if (TFD_CONV_LDS_EPI) {
     const int KD = c.R * c.S * c.K;
     if (is_pointwise(c)) {

@@ -31,6 +31,13 @@ SHAPES = [
     ("l4.3x3.512", 7, 512, 512, 3, 1),
     ("l4.1x1.512-2048", 7, 512, 2048, 1, 1),
     ("l4.1x1.2048-512", 7, 2048, 512, 1, 1),
+    # stride-2 entries of each stage (v1.5: the 3x3 and the 1x1 downsample carry the stride)
+    ("l2.3x3.128.s2", 56, 128, 128, 3, 2),
+    ("l2.ds.256-512.s2", 56, 256, 512, 1, 2),
+    ("l3.3x3.256.s2", 28, 256, 256, 3, 2),
+    ("l3.ds.512-1024.s2", 28, 512, 1024, 1, 2),
+    ("l4.3x3.512.s2", 14, 512, 512, 3, 2),
+    ("l4.ds.1024-2048.s2", 14, 1024, 2048, 1, 2),
 ]
 
 
@@ -53,6 +60,7 @@ def main():
     ap.add_argument("--N", type=int, default=128)
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--torch", type=int, default=1)
+    ap.add_argument("--match", default="", help="only shapes whose name contains this")
     a = ap.parse_args()
     _native.require()
     dev = torch.device("cuda", 0)
@@ -65,7 +73,8 @@ def main():
     tt = timeit(lambda: x @ w, a.iters)
     print(f"dense4096^3 fwd: ours {t:8.1f} us {2 * 4096**3 / t / 1e6:7.1f} TF/s | torch {tt:8.1f} us "
           f"{2 * 4096**3 / tt / 1e6:7.1f} TF/s", flush=True)
-    for name, H, C, K, R, st in SHAPES:
+    shapes = SHAPES if not a.match else [x for x in SHAPES if a.match in x[0]]
+    for name, H, C, K, R, st in shapes:
         N, pad = a.N, R // 2
         x = torch.randn(N, H, H, C, device=dev).bfloat16()
         w = (torch.randn(R, R, C, K, device=dev) * 0.05).bfloat16()
