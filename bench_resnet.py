@@ -31,6 +31,8 @@ def main(argv=None):
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--bn_stats", type=int, default=1, help="1: batch-norm statistics summed in the conv "
                     "forward epilogue (no separate statistics pass over the conv output)")
+    ap.add_argument("--relu_bits", type=int, default=1, help="1: residual BNs keep their relu mask as bits for "
+                    "the backward instead of re-reading the block output")
     ap.add_argument("--mask_from_y", type=int, default=1, help="1: residual-free BN backward recomputes its relu "
                     "mask from the conv output instead of reading the BN output")
     ap.add_argument("--fuse_joins", type=int, default=1, help="1: residual-join gradient sums in the dgrad "
@@ -50,6 +52,7 @@ def main(argv=None):
     m = ResNet(a.depth, num_classes=1000, device=dev, seed=0, fuse_joins=bool(a.fuse_joins),
                bn_stats=bool(a.bn_stats))
     m.mask_from_y = bool(a.mask_from_y)
+    m.relu_bits = bool(a.relu_bits)
     if ctx.comm is not None:
         ctx.comm.broadcast(m.fp.master, 0)
         m.fp.shadow.copy_(m.fp.master)
@@ -102,7 +105,7 @@ def main(argv=None):
                        "per_gpu_batch": a.batch_size, "seq_len": None, "parallelism": f"dp{ctx.world}",
                        "bucket_mb": a.bucket_mb, "optimizer": "sgd-momentum 0.9 wd 1e-4",
                        "hipgraph": not a.eager, "fuse_joins": bool(a.fuse_joins), "bn_stats": bool(a.bn_stats),
-                       "mask_from_y": bool(a.mask_from_y)}}), flush=True)
+                       "mask_from_y": bool(a.mask_from_y), "relu_bits": bool(a.relu_bits)}}), flush=True)
     ctx.shutdown()
     return 0
 

@@ -118,7 +118,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& y, const
                                                       const at::Tensor& beta, const c10::optional<at::Tensor>& res,
                                                       bool relu, at::Tensor running_mean, at::Tensor running_var,
                                                       double momentum, double eps,
-                                                      const c10::optional<at::Tensor>& partials) {
+                                                      const c10::optional<at::Tensor>& partials,
+                                                      const c10::optional<at::Tensor>& mask) {
   check_bf16(y, "y", -1);
   const int C = (int)y.size(-1);
   const int M = (int)(y.numel() / C);
@@ -135,24 +136,30 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& y, const
   auto mean = at::empty({C}, f), invstd = at::empty({C}, f);
   float* rm = running_mean.defined() && running_mean.numel() ? fp(running_mean) : nullptr;
   float* rv = running_var.defined() && running_var.numel() ? fp(running_var) : nullptr;
+  uint8_t* mb = nullptr;
+  if (mask.has_value()) {  // relu bits for the backward ([M][C/8] uint8)
+    TORCH_CHECK(relu && mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                    mask->numel() == (int64_t)M * (C / 8), "bn: mask must be contiguous uint8 [M, C/8] (relu only)");
+    mb = mask->data_ptr<uint8_t>();
+  }
   if (partials.has_value()) {  // statistics already summed by the producing conv (conv2d_fwd_stats)
     check_f32(*partials, "partials");
     TORCH_CHECK(partials->dim() == 3 && partials->size(1) == 2 && partials->size(2) == C, "bn: partials [nblk,2,C]");
     bn_forward_partials(bp(y), fp(gamma), fp(beta), res ? bp(*res) : nullptr, relu ? 1 : 0, bp(out), fp(mean),
                         fp(invstd), rm, rv, (float)momentum, (float)eps, M, C, fp(*partials),
-                        (int)partials->size(0), cur());
+                        (int)partials->size(0), cur(), mb);
     return {out, mean, invstd};
   }
   auto part = at::empty({bn_partials_size(M, C)}, f);
   bn_forward(bp(y), fp(gamma), fp(beta), res ? bp(*res) : nullptr, relu ? 1 : 0, bp(out), fp(mean), fp(invstd), rm, rv,
-             (float)momentum, (float)eps, M, C, fp(part), cur());
+             (float)momentum, (float)eps, M, C, fp(part), cur(), mb);
   return {out, mean, invstd};
 }
 
 std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tensor& out, const at::Tensor& y,
                                           const at::Tensor& gamma, const at::Tensor& mean, const at::Tensor& invstd,
                                           bool relu, bool want_dres, at::Tensor dgamma, at::Tensor dbeta,
-                                          const c10::optional<at::Tensor>& beta) {
+                                          const c10::optional<at::Tensor>& beta, const c10::optional<at::Tensor>& mask) {
   check_bf16(dout, "dout", -1);
   check_bf16(out, "out", -1);
   check_bf16(y, "y", -1);
@@ -165,8 +172,14 @@ std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tens
   at::Tensor dres = want_dres ? at::empty_like(y) : at::Tensor();
   auto part = at::empty({bn_partials_size(M, C)}, y.options().dtype(at::kFloat));
   if (beta) check_f32(*beta, "beta");
+  const uint8_t* mb = nullptr;
+  if (mask.has_value()) {
+    TORCH_CHECK(relu && mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                    mask->numel() == (int64_t)M * (C / 8), "bn_bwd: mask must be the forward's uint8 [M, C/8] relu bits");
+    mb = mask->data_ptr<uint8_t>();
+  }
   bn_backward(bp(dout), bp(out), bp(y), fp(gamma), beta ? fp(*beta) : nullptr, fp(mean), fp(invstd), relu ? 1 : 0,
-              bp(dy), want_dres ? bp(dres) : nullptr, fp(dgamma), fp(dbeta), M, C, fp(part), cur());
+              bp(dy), want_dres ? bp(dres) : nullptr, fp(dgamma), fp(dbeta), M, C, fp(part), cur(), mb);
   return {dy, dres};
 }
 
@@ -255,10 +268,11 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.def("linear_wgrad(Tensor x, Tensor dy, Tensor(a!) dw) -> ()");
   m.impl("linear_wgrad", c10::DispatchKey::CUDA, &linear_wgrad_op);
   m.def("bn_fwd(Tensor y, Tensor gamma, Tensor beta, Tensor? residual, bool relu, Tensor(a!) running_mean, "
-        "Tensor(b!) running_var, float momentum, float eps, Tensor? partials=None) -> (Tensor, Tensor, Tensor)");
+        "Tensor(b!) running_var, float momentum, float eps, Tensor? partials=None, Tensor(c!)? mask=None) -> "
+        "(Tensor, Tensor, Tensor)");
   m.impl("bn_fwd", c10::DispatchKey::CUDA, &bn_fwd);
   m.def("bn_bwd(Tensor dout, Tensor out, Tensor y, Tensor gamma, Tensor mean, Tensor invstd, bool relu, "
-        "bool want_dres, Tensor(a!) dgamma, Tensor(b!) dbeta, Tensor? beta=None) -> (Tensor, Tensor)");
+        "bool want_dres, Tensor(a!) dgamma, Tensor(b!) dbeta, Tensor? beta=None, Tensor? mask=None) -> (Tensor, Tensor)");
   m.impl("bn_bwd", c10::DispatchKey::CUDA, &bn_bwd);
   m.def("bn_infer(Tensor y, Tensor gamma, Tensor beta, Tensor rm, Tensor rv, float eps, bool relu) -> Tensor");
   m.impl("bn_infer", c10::DispatchKey::CUDA, &bn_infer_op);

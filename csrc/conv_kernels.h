@@ -45,18 +45,21 @@ int bn_partials_size(int M, int C);
 // mean/invstd [C]; running stats updated with `momentum` (TF decay semantics: r = r*m + x*(1-m)).
 void bn_forward(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
                 uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var, float momentum,
-                float eps, int M, int C, float* partials, hipStream_t st);
+                float eps, int M, int C, float* partials, hipStream_t st, uint8_t* mask_bits = nullptr);
+// mask_bits (optional, relu only): [M][C/8] bytes, bit j of byte (m, c/8) = out[m][c/8*8 + j] > 0;
+// the backward takes them instead of `out` (bn_backward mask_bits)
 // same, with the statistics partials already produced by conv_fwd_stats ([nblk][2][C])
 void bn_forward_partials(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
                          uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var,
-                         float momentum, float eps, int M, int C, const float* partials, int nblk, hipStream_t st);
+                         float momentum, float eps, int M, int C, const float* partials, int nblk, hipStream_t st,
+                         uint8_t* mask_bits = nullptr);
 // dout -> dy (through relu/bn), writes dgamma/dbeta (fp32, overwritten) and, when dres != null, the
 // gradient of the residual input (== gradient after the relu mask).
 // beta != nullptr (only valid when the forward had no residual): the relu mask is recomputed from y
 // with the forward's constants instead of reading `out`.
 void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* beta,
                  const float* mean, const float* invstd, int relu, uint16_t* dy, uint16_t* dres, float* dgamma,
-                 float* dbeta, int M, int C, float* partials, hipStream_t st);
+                 float* dbeta, int M, int C, float* partials, hipStream_t st, const uint8_t* mask_bits = nullptr);
 // inference-mode BN (running statistics), optional relu
 void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,
               float eps, int relu, uint16_t* out, int M, int C, hipStream_t st);

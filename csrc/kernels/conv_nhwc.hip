@@ -12,9 +12,12 @@
 // All index math on the loaders' hot path uses multiply-shift division (FastDiv) by runtime
 // constants. C and K must be multiples of 8 (16-B chunks); the 3-channel stem input is padded to 8.
 // 1x1 / stride-1 / pad-0 convolutions are plain GEMMs and take the dense loaders.
+#include <stdexcept>
+
 #include "../common.h"
 #include "../conv_kernels.h"
 #include "../gemm.h"
+#include "../bn_totals.h"
 
 namespace tfd {
 namespace {
@@ -272,7 +275,8 @@ struct RowId {
 template <int BM, int BN, int WM, int WN, bool ADD, bool STATS, class RM = RowId>
 __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], char* smem, uint16_t* __restrict__ y,
                                              const uint16_t* __restrict__ add, int M, int N, int m0, int n0,
-                                             float* __restrict__ part, RM rowmap = RM{}, uint32_t ybytes = 0) {
+                                             float* __restrict__ part, RM rowmap = RM{}, uint32_t ybytes = 0,
+                                             int* tcnt = nullptr, int tG = 0, float* tot = nullptr) {
   using E = LdsEpi<BM, BN, WM, WN>;
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
@@ -351,9 +355,18 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
       float a = 0.f, b = 0.f;
 #pragma unroll 8
       for (int g = 0; g < E::RG; ++g) { a += cs[g * BN + col]; b += cs[(E::RG + g) * BN + col]; }
-      part[(size_t)blockIdx.y * 2 * N + nn] = a;
-      part[(size_t)blockIdx.y * 2 * N + N + nn] = b;
+      if (tcnt) {  // handed to the last arriver in this launch: write-through stores
+        tot_store(part + (size_t)blockIdx.y * 2 * N + nn, a);
+        tot_store(part + (size_t)blockIdx.y * 2 * N + N + nn, b);
+      } else {
+        part[(size_t)blockIdx.y * 2 * N + nn] = a;
+        part[(size_t)blockIdx.y * 2 * N + N + nn] = b;
+      }
     }
+    // column totals in this launch (bn_totals.h): no separate BN finalize pass
+    if (tcnt)
+      totals_last_arriver<E::NT>(part, gridDim.y, blockIdx.y, N, n0, min(BN, N - n0), tG,
+                                 tcnt + blockIdx.x * kTotCntPerTile, tot, tot + N, reinterpret_cast<int*>(smem));
   }
 }
 
@@ -405,7 +418,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_kernel(LA la, LB 
 // forward BN needs no separate pass over the conv output. Fixed reduction order (deterministic).
 template <int BM, int BN, class LA, class LB>
 __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB lb, uint16_t* y, int M, int N, int KD,
-                                                         float* part) {
+                                                         float* part, int* tcnt, int tG, float* tot) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   constexpr int WM = 2, WN = 2, WTN = BN / WN, TN = WTN / 16;
 #if TFD_CONV_LDS_EPI
@@ -413,8 +426,10 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB
   f32x4 acc[BM / 32][BN / 32];
   gemm_mainloop<BM, BN, CBK, WM, WN, LA, LB, TFD_CONV_RS>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
                                                          (bf16*)smem_raw, acc);
-  lds_epilogue<BM, BN, WM, WN, false, true>(acc, smem_raw, y, nullptr, M, N, blockIdx.y * BM, blockIdx.x * BN, part);
+  lds_epilogue<BM, BN, WM, WN, false, true>(acc, smem_raw, y, nullptr, M, N, blockIdx.y * BM, blockIdx.x * BN, part,
+                                            RowId{}, 0u, tcnt, tG, tot);
 #else
+  (void)tcnt; (void)tG; (void)tot;
   float s[TN], q[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { s[j] = 0.f; q[j] = 0.f; }
@@ -510,7 +525,12 @@ void launch_gemm_stats(const LA& la, const LB& lb, uint16_t* y, int M, int N, in
     attr = true;
   }
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, 1);
-  gemm_stats_kernel<BM, BN, LA, LB><<<grid, 256, sm, st>>>(la, lb, y, M, N, KD, part);
+  // column totals go to part row grid.y (conv_fwd_stats_rows counts it)
+  const bool tot = TFD_CONV_LDS_EPI && bn_totals_enabled();
+  if (tot && (int)grid.x > kTotMaxTiles) throw std::runtime_error("conv_fwd_stats: too many column tiles for the totals");
+  gemm_stats_kernel<BM, BN, LA, LB><<<grid, 256, sm, st>>>(la, lb, y, M, N, KD, part, tot ? bn_ticket_slot() : nullptr,
+                                                          tot ? bn_totals_group((int)grid.y) : 0,
+                                                          tot ? part + (size_t)grid.y * 2 * N : nullptr);
 }
 
 // same tile choice as dispatch(): 128x128 when that fills the chip
@@ -585,9 +605,10 @@ void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t
   }
 }
 
-int conv_fwd_stats_rows(const ConvShape& c) {
+int conv_fwd_stats_rows(const ConvShape& c) {  // row blocks (+ the totals row, see launch_gemm_stats)
   const int M = c.N * c.Ho() * c.Wo();
-  return use_big_tiles(M, c.K) ? (M + 127) / 128 : (M + 63) / 64;
+  const int rows = use_big_tiles(M, c.K) ? (M + 127) / 128 : (M + 63) / 64;
+  return rows + (TFD_CONV_LDS_EPI && bn_totals_enabled() ? 1 : 0);
 }
 
 void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,

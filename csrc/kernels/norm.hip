@@ -3,9 +3,22 @@
 // statistics and parameter gradients are fp32. Reductions are two-level and deterministic:
 // per-block partials over a row chunk (8 channels per thread, 16-B loads), then a per-channel
 // finalize kernel in a fixed order.
+#include <stdexcept>
+
 #include "../common.h"
 #include "../conv_kernels.h"
 #include "../gemm.h"  // buf_ld
+#include "../bn_totals.h"
+
+// 1: statistics / BN parameter gradients summed in the producing launch by last-arriver tickets
+// (csrc/bn_totals.h) instead of the bn_final launch. Correct (tests pass with it on) but measured
+// SLOWER (ResNet-50 b128 13.98 -> 17.60 ms/step, profiles/resnet50_bn_totals_ab_r2.log): the
+// hand-off words must be read with write-through/sc1 loads (~2 us round trips to the Infinity
+// Cache) and the last group's reduction is a serial tail after every other block has finished --
+// 60-70 us per BN, against a 5-7 us finalize launch. Kept as the documented negative result.
+#ifndef TFD_BN_TOTALS
+#define TFD_BN_TOTALS 0
+#endif
 
 namespace tfd {
 namespace {
@@ -50,6 +63,19 @@ __device__ __forceinline__ void relu_mask_from_y(const float (&v)[8], const floa
   for (int j = 0; j < 8; ++j) d[j] = fmaf(v[j], sc[j], sh[j]) > 0.f ? d[j] : 0.f;
 }
 
+// MASK 3: the forward's relu mask as bits ([M][C/8] bytes, bit j = channel c0 + j of the chunk was
+// > 0 after the relu), written by bn_apply_kernel for the residual BNs, where the mask cannot be
+// recomputed from y alone: the backward reads 1 bit instead of the 16-bit output per element
+// (two full-tensor reads of `out` per residual BN backward). Rows past the chunk read a clamped
+// in-range byte (branch-free); their dout is zero-filled, so the bits do not matter.
+__device__ __forceinline__ uint32_t mask_byte(const uint8_t* __restrict__ mask, int r, int r1, int cpr, int ch) {
+  return mask[(size_t)min(r, r1 - 1) * cpr + ch];
+}
+__device__ __forceinline__ void apply_mask_bits(uint32_t bits, float (&d)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] = (bits >> j) & 1u ? d[j] : 0.f;
+}
+
 // Rows are walked in batches of RU rows per thread: every 16-B load of a batch (y, dout, out) is
 // issued before the first use, through buffer descriptors whose hardware range check zero-fills the
 // rows past the block's chunk (no exec-masked branch around a load, so the loads of a batch are all
@@ -70,8 +96,11 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(const uint16_t* __restri
                                                         const float* __restrict__ invstd,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int M, int C, int tpr,
-                                                        int rg, int rb, float* __restrict__ part) {
+                                                        int rg, int rb, float* __restrict__ part, int* tcnt, int tG,
+                                                        float* __restrict__ tot_a, float* __restrict__ tot_b,
+                                                        const uint8_t* __restrict__ mbits) {
   __shared__ float red[2][NT][8];
+  __shared__ int tflag;
   const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
   const uint32_t nbytes = (uint32_t)M * (uint32_t)C * 2u;
   float sa[8], sb[8], mu[8], is[8], sc[8], sh[8];
@@ -92,12 +121,14 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(const uint16_t* __restri
   if (g < rg) {
     for (int rbase = r0 + g; rbase < r1; rbase += RU * rg) {
       uint4 Y[RU], D[RU], O[RU];
+      uint32_t MB[RU];
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         const int r = rbase + u * rg;
         Y[u] = row_ld(y, nbytes, r, r1, C, c0);
         if (MODE == 1) D[u] = row_ld(dout, nbytes, r, r1, C, c0);
         if (MODE == 1 && MASK == 1) O[u] = row_ld(out, nbytes, r, r1, C, c0);
+        if (MODE == 1 && MASK == 3) MB[u] = mask_byte(mbits, r, r1, tpr, ch);
       }
 #pragma unroll
       for (int u = 0; u < RU; ++u) {  // rows past r1 loaded as zeros: they add nothing
@@ -116,6 +147,8 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(const uint16_t* __restri
             for (int j = 0; j < 8; ++j) d[j] = ov[j] > 0.f ? d[j] : 0.f;
           } else if (MASK == 2) {
             relu_mask_from_y(v, sc, sh, d);
+          } else if (MASK == 3) {
+            apply_mask_bits(MB[u], d);
           }
 #pragma unroll
           for (int j = 0; j < 8; ++j) { sa[j] += d[j]; sb[j] = fmaf(d[j], (v[j] - mu[j]) * is[j], sb[j]); }
@@ -147,9 +180,15 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(const uint16_t* __restri
   }
   if (g == 0) {
     float* pa = part + (size_t)blockIdx.x * 2 * C;
+    if (tcnt) {  // handed to the last arriver in this launch: write-through stores
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { pa[c0 + j] = sa[j]; pa[C + c0 + j] = sb[j]; }
+      for (int j = 0; j < 8; ++j) { tot_store(pa + c0 + j, sa[j]); tot_store(pa + C + c0 + j, sb[j]); }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { pa[c0 + j] = sa[j]; pa[C + c0 + j] = sb[j]; }
+    }
   }
+  if (tcnt) totals_last_arriver<NT>(part, gridDim.x, blockIdx.x, C, 0, C, tG, tcnt, tot_a, tot_b, &tflag);
 }
 
 // per-channel finalize, block = 32 channels x 32 partial-row groups (1024 threads: coalesced 128-B
@@ -204,20 +243,57 @@ __global__ __launch_bounds__(FIN_NT) void bn_final_kernel(int mode, const float*
 // row group); its 8 channels' constants stay in registers for every row it touches; RU rows' loads
 // per batch are issued before the first use (branch-free buffer loads, see bn_partial_kernel).
 // HAS_RES / RELU are compile-time so no load sits under a branch.
+// Totals mode (tot != nullptr: [2][C] column sums and sums of squares from the producing launch):
+// every block derives mean / invstd itself -- the finalize math of bn_final_kernel mode 0 -- and
+// block 0 stores them (saved for the backward) and updates the running statistics.
+struct BnTot {
+  const float* tot;
+  float eps, momentum;
+  float *mean, *invstd, *rmean, *rvar;
+};
+__device__ __forceinline__ void bn_stats_from_totals(const BnTot& b, int M, int C, int c0, bool store, float (&mu)[8],
+                                                     float (&is)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    mu[j] = b.tot[c] / (float)M;
+    const float var = fmaxf(b.tot[C + c] / (float)M - mu[j] * mu[j], 0.f);
+    is[j] = rsqrtf(var + b.eps);
+    if (store) {
+      b.mean[c] = mu[j];
+      b.invstd[c] = is[j];
+      if (b.rmean) {
+        b.rmean[c] = b.rmean[c] * b.momentum + mu[j] * (1.f - b.momentum);
+        b.rvar[c] = b.rvar[c] * b.momentum + var * ((float)M / (float)max(M - 1, 1)) * (1.f - b.momentum);
+      }
+    }
+  }
+}
 template <bool HAS_RES, bool RELU>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, const float* __restrict__ mean,
                                                       const float* __restrict__ invstd,
                                                       const uint16_t* __restrict__ res,
-                                                      uint16_t* __restrict__ out, int M, int C, int tpr, int rg, int rb) {
+                                                      uint16_t* __restrict__ out, int M, int C, int tpr, int rg, int rb,
+                                                      BnTot bt, uint8_t* __restrict__ mbits) {
   const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
   if (g >= rg) return;
   const uint32_t nbytes = (uint32_t)M * (uint32_t)C * 2u;
   float sc[8], sh[8];
+  if (bt.tot) {
+    float mu[8], is[8];
+    bn_stats_from_totals(bt, M, C, c0, blockIdx.x == 0 && g == 0, mu, is);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sc[j] = invstd[c0 + j] * gamma[c0 + j];
-    sh[j] = beta[c0 + j] - mean[c0 + j] * sc[j];
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = is[j] * gamma[c0 + j];
+      sh[j] = beta[c0 + j] - mu[j] * sc[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = invstd[c0 + j] * gamma[c0 + j];
+      sh[j] = beta[c0 + j] - mean[c0 + j] * sc[j];
+    }
   }
   const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
   for (int rbase = r0 + g; rbase < r1; rbase += RU * rg) {
@@ -239,7 +315,17 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict
         if (HAS_RES) z += q[j];
         v[j] = RELU ? fmaxf(z, 0.f) : z;
       }
-      if (r < r1) *reinterpret_cast<uint4*>(out + (size_t)r * C + c0) = pack8(v);
+      if (r < r1) {
+        const uint4 o = pack8(v);
+        *reinterpret_cast<uint4*>(out + (size_t)r * C + c0) = o;
+        if (RELU && mbits) {  // bit j: the stored bf16 output of channel c0 + j is > 0
+          const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+          uint32_t b = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) b |= ((w[k] & 0xFFFFu) ? 1u : 0u) << (2 * k) | ((w[k] >> 16) ? 1u : 0u) << (2 * k + 1);
+          mbits[(size_t)r * tpr + ch] = (uint8_t)b;
+        }
+      }
     }
   }
 }
@@ -253,7 +339,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __rest
                                                           const float* __restrict__ invstd, const float* __restrict__ dbeta,
                                                           const float* __restrict__ dgamma,
                                                           uint16_t* __restrict__ dy, uint16_t* __restrict__ dres,
-                                                          int M, int C, int tpr, int rg, int rb, float invM) {
+                                                          int M, int C, int tpr, int rg, int rb, float invM,
+                                                          const uint8_t* __restrict__ mbits) {
   const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
   if (g >= rg) return;
   const uint32_t nbytes = (uint32_t)M * (uint32_t)C * 2u;
@@ -275,12 +362,14 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __rest
   const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
   for (int rbase = r0 + g; rbase < r1; rbase += RU * rg) {
     uint4 D[RU], Y[RU], O[RU];
+    uint32_t MB[RU];
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int r = rbase + u * rg;
       D[u] = row_ld(dout, nbytes, r, r1, C, c0);
       Y[u] = row_ld(y, nbytes, r, r1, C, c0);
       if (MASK == 1) O[u] = row_ld(out, nbytes, r, r1, C, c0);
+      if (MASK == 3) MB[u] = mask_byte(mbits, r, r1, tpr, ch);
     }
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
@@ -295,6 +384,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __rest
         for (int j = 0; j < 8; ++j) d[j] = ov[j] > 0.f ? d[j] : 0.f;
       } else if (MASK == 2) {
         relu_mask_from_y(v, sc, sh, d);
+      } else if (MASK == 3) {
+        apply_mask_bits(MB[u], d);
       }
       float w[8];
 #pragma unroll
@@ -479,56 +570,110 @@ __global__ __launch_bounds__(NT) void pad_channels_kernel(const float* __restric
 inline int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + NT - 1) / NT)); }
 
 void launch_apply(const uint16_t* y, const float* gamma, const float* beta, const float* mean, const float* invstd,
-                  const uint16_t* res, int relu, uint16_t* out, int M, int C, const RowSplit& r, hipStream_t st) {
-  if (res && relu) bn_apply_kernel<true, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb);
-  else if (res) bn_apply_kernel<true, false><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb);
-  else if (relu) bn_apply_kernel<false, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb);
-  else bn_apply_kernel<false, false><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb);
+                  const uint16_t* res, int relu, uint16_t* out, int M, int C, const RowSplit& r, hipStream_t st,
+                  BnTot bt = BnTot{nullptr, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr}, uint8_t* mb = nullptr) {
+  if (res && relu) bn_apply_kernel<true, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, bt, mb);
+  else if (res) bn_apply_kernel<true, false><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, bt, mb);
+  else if (relu) bn_apply_kernel<false, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, bt, mb);
+  else bn_apply_kernel<false, false><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, bt, mb);
+}
+
+// group size of the two-level ticket reduction: ~sqrt(rows) rows per group, <= kTotMaxGroups groups
+int tot_group(int nrows) {
+  int g = 8;
+  while (g * g < nrows) ++g;
+  while ((nrows + g - 1) / g > kTotMaxGroups) ++g;
+  return g;
 }
 
 }  // namespace
 
+int* bn_ticket_slot() {
+  static int* ws[64] = {nullptr};
+  static unsigned next[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) throw std::runtime_error("bn_ticket_slot: device index");
+  if (!ws[dev]) {
+    const size_t bytes = (size_t)kTotSlots * kTotMaxTiles * kTotCntPerTile * sizeof(int);
+    if (hipMalloc(&ws[dev], bytes) != hipSuccess || hipMemset(ws[dev], 0, bytes) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)
+      throw std::runtime_error("bn_ticket_slot: workspace allocation failed");
+  }
+  return ws[dev] + (size_t)(next[dev]++ % kTotSlots) * kTotMaxTiles * kTotCntPerTile;
+}
+
+bool bn_totals_enabled() { return TFD_BN_TOTALS != 0; }
+int bn_totals_group(int nrows) { return tot_group(nrows); }
+
 int bn_partials_size(int M, int C) {
   const RowSplit r = row_split(M, C);
-  return r.nblk * 2 * C;
+  return (r.nblk + 1) * 2 * C;  // + the totals row
 }
 
 void bn_forward(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
                 uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var, float momentum,
-                float eps, int M, int C, float* partials, hipStream_t st) {
+                float eps, int M, int C, float* partials, hipStream_t st, uint8_t* mask_bits) {
   const RowSplit r = row_split(M, C);
+  if (TFD_BN_TOTALS) {
+    float* tot = partials + (size_t)r.nblk * 2 * C;
+    bn_partial_kernel<0, 0><<<r.nblk, NT, 0, st>>>(y, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, C, r.tpr,
+                                                   r.rg, r.rb, partials, bn_ticket_slot(), tot_group(r.nblk), tot,
+                                                   tot + C, nullptr);
+    launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st,
+                 BnTot{tot, eps, momentum, mean, invstd, running_mean, running_var}, mask_bits);
+    return;
+  }
   bn_partial_kernel<0, 0><<<r.nblk, NT, 0, st>>>(y, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, C, r.tpr,
-                                                 r.rg, r.rb, partials);
+                                                 r.rg, r.rb, partials, nullptr, 0, nullptr, nullptr, nullptr);
   bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, r.nblk, M, C, eps, momentum, mean, invstd,
                                                 running_mean, running_var);
-  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st);
+  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st,
+               BnTot{nullptr, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr}, mask_bits);
 }
 
+// partials: [nrows][2][C] from conv_fwd_stats; with TFD_BN_TOTALS its last row holds the column totals
 void bn_forward_partials(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
                          uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var,
-                         float momentum, float eps, int M, int C, const float* partials, int nblk, hipStream_t st) {
+                         float momentum, float eps, int M, int C, const float* partials, int nrows, hipStream_t st,
+                         uint8_t* mask_bits) {
   const RowSplit r = row_split(M, C);
-  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, nblk, M, C, eps, momentum, mean, invstd,
+  if (TFD_BN_TOTALS) {
+    launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st,
+                 BnTot{partials + (size_t)(nrows - 1) * 2 * C, eps, momentum, mean, invstd, running_mean, running_var},
+                 mask_bits);
+    return;
+  }
+  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, nrows, M, C, eps, momentum, mean, invstd,
                                                 running_mean, running_var);
-  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st);
+  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st,
+               BnTot{nullptr, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr}, mask_bits);
 }
 
 void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* beta,
                  const float* mean, const float* invstd, int relu, uint16_t* dy, uint16_t* dres, float* dgamma,
-                 float* dbeta, int M, int C, float* partials, hipStream_t st) {
+                 float* dbeta, int M, int C, float* partials, hipStream_t st, const uint8_t* mask_bits) {
   const RowSplit r = row_split(M, C);
-  // beta given (no residual in the forward): the relu mask is recomputed from y, `out` is not read
-  const int mask = !relu ? 0 : (beta ? 2 : 1);
+  // beta given (no residual in the forward): the relu mask is recomputed from y, `out` is not read;
+  // mask_bits given: the forward's relu bits, `out` is not read
+  const int mask = !relu ? 0 : (mask_bits ? 3 : (beta ? 2 : 1));
 #define TFD_BN_BWD(MK)                                                                                          \
-  bn_partial_kernel<1, MK><<<r.nblk, NT, 0, st>>>(y, dout, out, mean, invstd, gamma, beta, M, C, r.tpr, r.rg, r.rb, \
-                                                  partials);                                                   \
-  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,  \
-                                                nullptr);                                                       \
+  if (TFD_BN_TOTALS) {  /* dbeta / dgamma summed by the partial kernel's last arrivers */                      \
+    bn_partial_kernel<1, MK><<<r.nblk, NT, 0, st>>>(y, dout, out, mean, invstd, gamma, beta, M, C, r.tpr, r.rg,   \
+                                                    r.rb, partials, bn_ticket_slot(), tot_group(r.nblk), dbeta,  \
+                                                    dgamma, mask_bits);                                          \
+  } else {                                                                                                      \
+    bn_partial_kernel<1, MK><<<r.nblk, NT, 0, st>>>(y, dout, out, mean, invstd, gamma, beta, M, C, r.tpr, r.rg,   \
+                                                    r.rb, partials, nullptr, 0, nullptr, nullptr, mask_bits);    \
+    bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,\
+                                                  nullptr);                                                     \
+  }                                                                                                             \
   bn_bwd_apply_kernel<MK><<<r.nblk, NT, 0, st>>>(dout, out, y, gamma, beta, mean, invstd, dbeta, dgamma, dy, dres, M, \
-                                                 C, r.tpr, r.rg, r.rb, 1.f / (float)M);
+                                                 C, r.tpr, r.rg, r.rb, 1.f / (float)M, mask_bits);
   if (mask == 0) { TFD_BN_BWD(0) }
   else if (mask == 1) { TFD_BN_BWD(1) }
-  else { TFD_BN_BWD(2) }
+  else if (mask == 2) { TFD_BN_BWD(2) }
+  else { TFD_BN_BWD(3) }
 #undef TFD_BN_BWD
 }
 

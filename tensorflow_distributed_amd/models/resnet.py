@@ -228,19 +228,28 @@ class _BN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, res, layer, relu, part=None):
         args = (y, layer.gamma(), layer.beta(), res, relu, layer.rmean, layer.rvar, layer.momentum, layer.eps)
-        out, mean, invstd = _ops().bn_fwd(*args, part) if part is not None else _ops().bn_fwd(*args)
+        # residual + relu: the relu mask cannot be recomputed from y; keep it as bits (1/16 of `out`)
+        # so the backward never re-reads the block output
+        mask = None
+        if relu and res is not None and layer.model.relu_bits:
+            mask = torch.empty(y.numel() // y.shape[-1], y.shape[-1] // 8, dtype=torch.uint8, device=y.device)
+        out, mean, invstd = _ops().bn_fwd(*args, part, mask)
         ctx.layer, ctx.relu, ctx.has_res = layer, relu, res is not None
-        ctx.save_for_backward(y, out, mean, invstd)
+        ctx.save_for_backward(y, out if mask is None else mask, mean, invstd)
+        ctx.bits = mask is not None
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        y, out, mean, invstd = ctx.saved_tensors
+        y, out_or_mask, mean, invstd = ctx.saved_tensors
         L = ctx.layer
-        # residual-free BN: pass beta, the kernels recompute the relu mask from y (no read of out)
+        # residual-free BN: pass beta, the kernels recompute the relu mask from y (no read of out);
+        # residual BN: the forward's relu bits (no read of out either)
         beta = L.beta() if (ctx.relu and not ctx.has_res and L.model.mask_from_y) else None
+        mask = out_or_mask if ctx.bits else None
+        out = y if ctx.bits else out_or_mask  # not read when a mask (bits or from y) is given
         args = (dout.contiguous(), out, y, L.gamma(), mean, invstd, ctx.relu, ctx.has_res, L.g_gamma(), L.g_beta())
-        dy, dres = _ops().bn_bwd(*args, beta) if beta is not None else _ops().bn_bwd(*args)
+        dy, dres = _ops().bn_bwd(*args, beta, mask)
         L.model.reducer.mark_ready(L.name + "/gamma")
         L.model.reducer.mark_ready(L.name + "/beta")
         if ctx.has_res and L.res_join is not None:
@@ -401,6 +410,8 @@ class ResNet:
         self.bn_stats = bn_stats
         # residual-free BN backward recomputes its relu mask from y instead of reading the output
         self.mask_from_y = True
+        # residual BN keeps its relu mask as bits for the backward instead of re-reading the output
+        self.relu_bits = True
         cin = width
         exp = 4 if kind == "bottleneck" else 1
         for li, nb in enumerate(blocks):

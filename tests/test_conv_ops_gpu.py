@@ -78,6 +78,8 @@ def test_conv_fwd_stats_feeds_bn(cuda, N, H, W, C, K, R, st, pad):
     assert part.shape[1:] == (2, K)
     torch.testing.assert_close(part[:, 0].sum(0), yf.sum(0), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(part[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
+    y2, part2 = ops.conv2d_fwd_stats(x, w, st, pad)  # deterministic: bit-identical partials on a rerun
+    assert torch.equal(part2, part) and torch.equal(y2, y)
     g, b = torch.rand(K, device=cuda) + 0.5, torch.randn(K, device=cuda)
     rm0, rv0 = torch.zeros(K, device=cuda), torch.ones(K, device=cuda)
     rm1, rv1 = rm0.clone(), rv0.clone()
@@ -135,11 +137,54 @@ def test_batchnorm_train(cuda, relu, res):
     assert relerr(db.cpu(), dz.sum(0)) < 1e-3 and relerr(dg.cpu(), (dz * yh).sum(0)) < 1e-2
     if res:
         assert relerr(dres.cpu(), dz) < 1e-2
+    if relu and res:  # relu bits from the forward instead of `out`: same output, same gradients
+        mask = torch.empty(M, C // 8, dtype=torch.uint8, device=cuda)
+        out3, _, _ = ops.bn_fwd(y.to(cuda, torch.bfloat16), g.to(cuda), b.to(cuda), r.to(cuda, torch.bfloat16), relu,
+                                torch.zeros(C, device=cuda), torch.ones(C, device=cuda), 0.9, 1e-5, None, mask)
+        assert torch.equal(out3, out)
+        bits = ((mask.cpu().long().unsqueeze(-1) >> torch.arange(8)) & 1).reshape(M, C).bool()
+        assert torch.equal(bits, out.cpu().float() > 0)
+        dg3, db3 = torch.empty_like(dg), torch.empty_like(db)
+        dy3, dres3 = ops.bn_bwd(dout.to(cuda, torch.bfloat16), torch.empty_like(out), y.to(cuda, torch.bfloat16),
+                                g.to(cuda), mean, invstd, relu, res, dg3, db3, None, mask)
+        assert torch.equal(dy3, dy) and torch.equal(dres3, dres) and torch.equal(dg3, dg) and torch.equal(db3, db)
     if relu and not res:  # mask recomputed from y (beta given): `out` is not read, same gradients
         dg2, db2 = torch.empty_like(dg), torch.empty_like(db)
         dy2, _ = ops.bn_bwd(dout.to(cuda, torch.bfloat16), torch.empty_like(out), y.to(cuda, torch.bfloat16),
                             g.to(cuda), mean, invstd, relu, res, dg2, db2, b.to(cuda))
         assert torch.equal(dy2, dy) and torch.equal(dg2, dg) and torch.equal(db2, db)
+
+
+@pytest.mark.parametrize("M,C", [(100000, 64), (20000, 520)])
+def test_batchnorm_totals_many_groups(cuda, M, C):
+    """Large M (1024 partial rows): statistics and dgamma/dbeta against fp64 sums, bit-identical when
+    repeated (fixed summation order) -- with TFD_BN_TOTALS=1 builds this covers the two-level
+    last-arriver reduction (32 groups, csrc/bn_totals.h)."""
+    torch.manual_seed(6)
+    y = rb(torch.randn(M, C) * 2 + 0.5)
+    g, b = torch.rand(C) + 0.5, torch.randn(C)
+    yd = y.to(cuda, torch.bfloat16)
+    outs = []
+    for _ in range(2):
+        rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+        out, mean, invstd = ops.bn_fwd(yd, g.to(cuda), b.to(cuda), None, True, rm, rv, 0.9, 1e-5)
+        dout = rb(torch.randn(M, C, generator=torch.Generator().manual_seed(1))).to(cuda, torch.bfloat16)
+        dg, db = torch.empty(C, device=cuda), torch.empty(C, device=cuda)
+        dy, _ = ops.bn_bwd(dout, out, yd, g.to(cuda), mean, invstd, True, False, dg, db)
+        outs.append([t.cpu() for t in (out, mean, invstd, rm, rv, dg, db, dy)])
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
+    out, mean, invstd, rm, rv, dg, db, dy = outs[0]
+    y64 = y.double()
+    mu, var = y64.mean(0), y64.var(0, unbiased=False)
+    torch.testing.assert_close(mean.double(), mu, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(invstd.double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rv.double(), 0.9 + 0.1 * y64.var(0, unbiased=True), rtol=1e-4, atol=1e-5)
+    dout64 = rb(torch.randn(M, C, generator=torch.Generator().manual_seed(1))).double()
+    mask = (out.double() > 0).double()
+    dz = dout64 * mask
+    yh = (y64 - mu) / torch.sqrt(var + 1e-5)
+    assert relerr(db, dz.sum(0)) < 1e-4 and relerr(dg, (dz * yh).sum(0)) < 2e-3
 
 
 def test_maxpool_avgpool(cuda):
