@@ -169,6 +169,8 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--num_ps", type=int, default=1)
     ap.add_argument("--num_workers", type=int, default=2)
+    ap.add_argument("--nproc", type=int, default=None, help="worker processes on this node (SURVEY 5.6 name; "
+                    "overrides --num_workers)")
     ap.add_argument("--script", default="mnist_python_m.py")
     ap.add_argument("--max_restarts", type=int, default=0)
     ap.add_argument("--log_dir", default=None)
@@ -176,6 +178,8 @@ def main(argv=None) -> int:
     ap.add_argument("--profile", default=None, metavar="DIR", help="run workers under rocprofv3 into DIR/worker<i>")
     ap.add_argument("--profile_pmc", default="", help="comma-separated PMC counters for one --profile pass")
     a = ap.parse_args(ours)
+    if a.nproc is not None:
+        a.num_workers = a.nproc
     r = launch(a.num_ps, a.num_workers, rest, a.script, a.max_restarts, a.log_dir, True, a.timeout,
                profile_dir=a.profile, profile_pmc=a.profile_pmc)
     print(f"[launch] {'ok' if r['ok'] else 'FAILED'} after {r['attempts']} attempt(s)", flush=True)

@@ -200,3 +200,16 @@ def test_async_checkpoint_holds_ps_adam_slots(tmp_path):
     ck2 = load_bundle(latest_checkpoint(str(tmp_path)))
     assert int(ck2["global_step"]) >= 6
     assert abs(float(ck2["beta1_power"]) - 0.9 ** int(ck2["global_step"])) < 1e-6
+
+
+def test_launcher_nproc_alias(monkeypatch):
+    """--nproc N (SURVEY 5.6 launcher flag) is the worker count; the rest after -- reaches the script."""
+    seen = {}
+
+    def fake(num_ps, num_workers, rest, *a, **k):
+        seen.update(num_ps=num_ps, num_workers=num_workers, rest=rest)
+        return {"ok": True, "attempts": 1}
+
+    monkeypatch.setattr(launch, "launch", fake)
+    assert launch.main(["--num_ps", "1", "--nproc", "3", "--", "--train_steps=2"]) == 0
+    assert seen == {"num_ps": 1, "num_workers": 3, "rest": ["--train_steps=2"]}
