@@ -47,6 +47,9 @@ def main(argv=None):
     ap.add_argument("--lead_steps", type=int, default=0, help="timed region: launch this many one-step graphs "
                     "first, then ONE graph of the remaining steps (the GPU starts on the small launch while the "
                     "host enqueues the big one)")
+    ap.add_argument("--spin_sync", type=int, default=0, help="1: after launching the timed steps, poll the end "
+                    "event (hipEventQuery) before the closing torch.cuda.synchronize(), so the host notices "
+                    "completion without the blocking wait's wake-up latency")
     ap.add_argument("--phases", type=int, default=1, help="after the timed steps, replay a few steps of a graph "
                     "with HIP timing events at the phase boundaries and report the GPU phase breakdown (untimed)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="compute dtype: bf16 MFMA operands "
@@ -195,6 +198,9 @@ def main(argv=None):
             run(a.steps)
         ev1.record(s)
     t_launched = time.perf_counter()
+    if a.spin_sync:
+        while not ev1.query():
+            pass
     torch.cuda.synchronize(dev)
     t_synced = time.perf_counter()
     ctx.barrier()
