@@ -50,6 +50,10 @@ def main(argv=None):
     ap.add_argument("--spin_sync", type=int, default=0, help="1: after launching the timed steps, poll the end "
                     "event (hipEventQuery) before the closing torch.cuda.synchronize(), so the host notices "
                     "completion without the blocking wait's wake-up latency")
+    ap.add_argument("--lean_gap", type=int, default=1, help="1: nothing but the barrier and synchronize between "
+                    "the last warm-up step and the timed region (events made and the warm-up loss read beforehand)")
+    ap.add_argument("--idle_us", type=float, default=0.0, help="diagnostic: host busy-wait before the timed region "
+                    "(GPU idle), to measure what an idle gap costs the first timed steps")
     ap.add_argument("--phases", type=int, default=1, help="after the timed steps, replay a few steps of a graph "
                     "with HIP timing events at the phase boundaries and report the GPU phase breakdown (untimed)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="compute dtype: bf16 MFMA operands "
@@ -170,6 +174,11 @@ def main(argv=None):
     # 5-step warm-up measures the ramp. Keep replaying untimed steps until --min_warmup_ms elapsed;
     # every rank runs the same count (decided by rank 0), so collectives stay matched.
     extra = 0
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if a.lean_gap:  # torch creates the HIP events at their first record: do that outside the timed region
+        with torch.cuda.stream(s):
+            ev0.record(s)
+            ev1.record(s)
     if a.min_warmup_ms > 0:
         t_w = time.perf_counter()
         chunk = 50
@@ -181,13 +190,21 @@ def main(argv=None):
                 break
             with torch.cuda.stream(s):
                 run(chunk)
+                if a.lean_gap:
+                    loss0_t = eng.loss_rows().mean()  # read after the timed region
             torch.cuda.synchronize(dev)
             extra += chunk
-    loss0 = float(eng.loss_rows().mean().item())
+    if a.lean_gap and extra:
+        loss0 = None
+    else:
+        loss0 = float(eng.loss_rows().mean().item())
 
     ctx.barrier()
     torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if a.idle_us > 0:
+        t_i = time.perf_counter()
+        while (time.perf_counter() - t_i) * 1e6 < a.idle_us:
+            pass
     t0 = time.perf_counter()
     with torch.cuda.stream(s):
         ev0.record(s)
@@ -215,6 +232,8 @@ def main(argv=None):
     dt = ctx.max_scalar(dt)
     tr.check("after the timed steps")
     phases = _phase_breakdown(eng, s, graph_mode, world, ctx) if a.phases else None
+    if loss0 is None:
+        loss0 = float(loss0_t.item())
     loss1 = float(eng.loss_rows().mean().item())
     gstep = int(eng.step_tensor().item())
     ms = dt * 1e3 / a.steps
