@@ -734,14 +734,20 @@ WgTile wgrad_tile(const ConvShape& c) {
   return WG128x64;
 }
 
+#ifndef TFD_WGRAD_MINPX  // fewest pixels (K of the weight-gradient GEMM) per split
+#define TFD_WGRAD_MINPX 2048
+#endif
+#ifndef TFD_WGRAD_BLOCKS  // (tile x split) blocks the split count aims for
+#define TFD_WGRAD_BLOCKS 512
+#endif
 int conv_wgrad_splits(const ConvShape& c) {
-  // enough (tile x split) blocks to fill the chip; each split keeps >= 2048 pixels of K
+  // enough (tile x split) blocks to fill the chip; each split keeps >= TFD_WGRAD_MINPX pixels of K
   const int P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
   const WgTile t = wgrad_tile(c);
   const int bm = t == WG64x64 ? 64 : 128, bn = t == WG128x128 ? 128 : 64;
   const long tiles = (long)((MT + bm - 1) / bm) * ((c.K + bn - 1) / bn);
-  int s = (int)std::max<long>(1, 512 / std::max<long>(1, tiles));
-  s = std::min(s, std::max(1, P / 2048));
+  int s = (int)std::max<long>(1, TFD_WGRAD_BLOCKS / std::max<long>(1, tiles));
+  s = std::min(s, std::max(1, P / TFD_WGRAD_MINPX));
   return s;
 }
 

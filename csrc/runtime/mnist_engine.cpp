@@ -193,7 +193,11 @@ class MnistEngine : public torch::CustomClassHolder {
   void set_zero(bool on) {
     if (!on) { zero_ = false; return; }
     const int64_t W = world();
-    TORCH_CHECK(W > 1, "set_zero: needs a communicator with world > 1");
+    // world 1 only as the forced-DP rehearsal (one shard = the whole fc1 weight): the sharded
+    // schedule -- reduce-scatter / sharded optimizer / weight all-gather over the real RCCL or IPC
+    // communicator -- runs on a one-GPU box exactly as an N-GPU node runs it
+    TORCH_CHECK(W > 1 || (force_dp_ && (comm_ || ipc_)), "set_zero: needs a communicator with world > 1 "
+                "(or set_force_dp at world 1)");
     TORCH_CHECK((OFF_BD1 - OFF_WD1) % (W * 64) == 0, "set_zero: fc1 weight not divisible into ", W, " shards");
     zshard_ = (OFF_BD1 - OFF_WD1) / W;
     zero_ = true;

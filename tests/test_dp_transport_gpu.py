@@ -101,6 +101,38 @@ def test_forced_dp_world1_sfb_gradients_are_the_fused_gradients(cuda, mode, B):
     tr.close()
 
 
+@pytest.mark.parametrize("mode,sfb", [("rccl", True), ("rccl", False), ("ipc", True)])
+def test_forced_dp_world1_zero1_tracks_plain_dp(cuda, mode, sfb):
+    """ZeRO-1 (the default from 8 GPUs) at world 1 over the real communicator: the sharded schedule
+    -- fc1 shard dW rows from the gathered factors (sfb) or reduce-scatter (no sfb), sharded Adam,
+    bf16 weight all-gather beside the next conv forward, eager and graph-captured -- against the
+    same DP schedule unsharded: bit-identical parameters, Adam state and bf16 shadow."""
+    from tensorflow_distributed_amd.parallel.transport import attach_engine
+
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        params, (ref, zr) = _engines_on_dataset(cuda, 2)
+        tr0 = attach_engine(ref, 0, 1, cuda, mode=mode, force_dp=True, sfb=sfb)
+        tr1 = attach_engine(zr, 0, 1, cuda, mode=mode, force_dp=True, sfb=sfb)
+        zr.set_zero(True)
+        assert zr.zero() and not ref.zero()
+        for e in (ref, zr):
+            e.train_step()
+            e.train_step()
+            e.capture_train_steps("t", 3)
+            e.replay("t", 2)
+        zr.sync_params()
+    torch.cuda.synchronize()
+    tr0.check()
+    tr1.check()
+    assert int(zr.step_tensor().item()) == int(ref.step_tensor().item()) == 8
+    assert torch.equal(zr.params(), ref.params())
+    assert torch.equal(zr.adam_v(), ref.adam_v())
+    assert torch.equal(zr.params_bf16(), ref.params_bf16())
+    tr0.close()
+    tr1.close()
+
+
 @pytest.mark.parametrize("mode", ["rccl", "ipc"])
 def test_forced_dp_world1_captured_steps_track_fused(cuda, mode):
     """Two eager + two graph-replayed steps (captured collectives) with dropout and Adam: same
@@ -188,11 +220,15 @@ def test_bench_fp32_dtype(cuda):
     assert r["dtype"] == "fp32" and r["config"]["grad_allreduce"] == "fp32" and r["value"] > 0
 
 
-@pytest.mark.parametrize("sfb", [1, 0])
-def test_bench_forced_dp_world1_rccl(cuda, sfb):
-    r = _bench(["--steps", "20", "--warmup", "5", "--force_dp", "1", "--min_warmup_ms", "50", "--fc_sfb", str(sfb)])
+@pytest.mark.parametrize("sfb,zero", [(1, 0), (0, 0), (1, 1)])
+def test_bench_forced_dp_world1_rccl(cuda, sfb, zero):
+    """bench.py's multi-GPU configuration rehearsed at world 1 over RCCL: (1, 1) is the 8-GPU
+    default (sufficient factors + ZeRO-1), multi-step graphs included."""
+    r = _bench(["--steps", "20", "--warmup", "5", "--force_dp", "1", "--min_warmup_ms", "50", "--fc_sfb", str(sfb),
+                "--zero", str(zero)])
     kind = "rccl+sfb" if sfb else "rccl"
     assert r["config"]["dp_transport"] == kind and r["config"]["force_dp"] and r["config"]["hipgraph"]
+    assert r["config"]["zero1_fc1"] == bool(zero) and r["value"] > 0
 
 
 def test_dist_main_resnet18_two_workers_one_gpu(tmp_path):
