@@ -66,6 +66,9 @@ def main(argv=None):
     ap.add_argument("--fc_sfb", type=int, default=1, help="1 (N > 1 or --force_dp): fc-region gradients by "
                     "sufficient-factor broadcasting -- all-gather the fc factors (1.33 MB/rank) and form the summed "
                     "fc gradient locally instead of all-reducing it (6.4 MB); 0: bucketed all-reduce")
+    ap.add_argument("--dp_serial", type=int, default=1, help="1: with --fc_sfb, every compute kernel on the main "
+                    "stream and only the collectives on the comm stream; 0: the overlapped three-stream schedule "
+                    "(SFB GEMM + fc optimizer beside the conv backward / next conv forward)")
     ap.add_argument("--fused_tail", type=int, default=1, help="1: on one GPU the Adam kernel also reduces the "
                     "conv weight-gradient slabs and bumps the step (one kernel less)")
     ap.add_argument("--local_bf16_grads", type=int, default=1, help="1: on one GPU keep the fc-region gradients "
@@ -111,6 +114,7 @@ def main(argv=None):
     eng.set_conv_unfused(a.conv_unfused)
     eng.set_fc_split(a.fc_split)
     eng.set_fc_defer(a.fc_defer)
+    eng.set_dp_serial(a.dp_serial)
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     mode = a.transport
@@ -270,6 +274,7 @@ def main(argv=None):
                 "dp_transport": tr.kind,
                 "force_dp": bool(a.force_dp),
                 "zero1_fc1": bool(a.zero),
+                "dp_schedule": "serial" if a.dp_serial else "overlapped",
                 "fc_grads": ("fp32" if a.dtype == "fp32" else
                              "summed from all-gathered factors (sfb), bf16" if "sfb" in tr.kind else
                              "fused into Adam (fp32, in registers)" if world == 1 and a.fc_adam and not a.force_dp

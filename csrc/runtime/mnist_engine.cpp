@@ -235,6 +235,9 @@ class MnistEngine : public torch::CustomClassHolder {
   void set_fc_defer(int64_t blocks) { fc_defer_ = blocks; }
   // 0 (default): conv1 fused into the conv2 forward kernel; 1: the two separate kernels (A/B)
   void set_conv_unfused(int64_t on) { conv_unfused_ = on != 0; }
+  // DP with sufficient factors: 1 (default) every compute kernel on the main stream, collectives on
+  // the comm stream (train_step_sfb_serial); 0 the overlapped three-stream schedule (train_step_sfb)
+  void set_dp_serial(int64_t on) { dp_serial_ = on != 0; }
   // Make every rank's state whole again after ZeRO-1 steps (before eval / checkpoint / broadcast):
   // each rank updated the fp32 master, m and v of its own fc1 shard only, so all four are
   // all-gathered -- the bf16 shadow (what the forward reads) and the fp32 master + Adam slots (what
@@ -369,8 +372,12 @@ class MnistEngine : public torch::CustomClassHolder {
       return;
     }
     if (dp) {
-      if (sfb_active()) train_step_sfb(join_end);
-      else train_step_dp(join_end);
+      if (sfb_active()) {
+        if (dp_serial_) train_step_sfb_serial(join_end);
+        else train_step_sfb(join_end);
+      } else {
+        train_step_dp(join_end);
+      }
       return;
     }
     mark(P_START, s);
@@ -636,6 +643,92 @@ class MnistEngine : public torch::CustomClassHolder {
       pending_opt_a_ = true;
       pending_sfb_ = true;
     }
+  }
+
+  // Serialized sufficient-factor step (set_dp_serial, the default): every compute kernel on the
+  // main stream in one order, only the collectives on the comm stream. The overlapped schedule above
+  // (SFB GEMM + fc optimizer on a second stream beside the conv backward and the next conv forward)
+  // measured 124 us/step in the world-1 rehearsal against 74 for the fused one-GPU step: these
+  // kernels each fill the GPU, so running two of them at once slowed both (conv2 wgrad 10 -> 19 us),
+  // as the one-GPU overlap A/Bs showed (profiles/ab_fc_adam_overlap_r2.log).
+  //   s: conv fwd -> fc fwd -> head -> fc1 dX -> conv wgrad / dgrad -> conv slab reduce (+ next
+  //      batch, step bump) -> [wait dh gather] SFB fc GEMM -> [wait conv bucket] ONE optimizer
+  //   c: [p2] gather p2 (beside fc fwd + head) -> [head] gather dh|hd|dlogits (beside dX + conv
+  //      backward) -> [slabs reduced] conv bucket all-reduce (beside the SFB GEMM)
+  //   ZeRO-1: the GEMM forms only this rank's fc1 shard rows, the optimizer runs on conv + shard +
+  //   tail, and the updated bf16 shards are all-gathered on c beside the next conv forward.
+  void train_step_sfb_serial(bool join_end) {
+    hipStream_t s = stream();
+    const double scale = 1.0 / (double)world();
+    const bool bf = bf16_comm_;
+    const bool shard = zero_;
+    const int64_t rk = rank_in_comm();
+    MnistStepArgs a = args();
+    if (shard) {
+      const int64_t rows = zshard_ / HID;
+      mnist_sfb_tile_rows((int)(rk * rows), (int)((rk + 1) * rows), &a.sfb_by_lo, &a.sfb_by_hi);
+    }
+    a.t_out = (int64_t*)tnext_.data_ptr();
+    a.step_bump = (int64_t*)step_.data_ptr();
+    if (bf) {
+      a.gbf_a = (uint16_t*)gbf_.data_ptr();
+      a.gbf_b = (uint16_t*)gbf_.data_ptr();
+    }
+    mark(P_START, s);
+    if (shard && pending_wag_) {  // last step's updated fc1 bf16 shards -> every rank, beside the conv forward
+      HIP_OK(hipEventRecord(ev_start_, s));
+      HIP_OK(hipStreamWaitEvent(comm_stream_, ev_start_, 0));
+      ag_w(comm_stream_);
+      HIP_OK(hipEventRecord(ev_wag_, comm_stream_));
+    }
+    mnist_forward_conv(a, s);
+    HIP_OK(hipEventRecord(ev_p2_, s));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_p2_, 0));
+    mark(P_CA0, comm_stream_);
+    gather_sfb(true, comm_stream_);
+    if (shard && pending_wag_) {
+      HIP_OK(hipStreamWaitEvent(s, ev_wag_, 0));
+      pending_wag_ = false;
+    }
+    mnist_forward_fc(a, true, s);
+    mark(P_FWD, s);
+    HIP_OK(hipEventRecord(ev_a_, s));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
+    gather_sfb(false, comm_stream_);
+    mark(P_CA1, comm_stream_);
+    HIP_OK(hipEventRecord(ev_ag_, comm_stream_));
+    mnist_backward_a(a, s, 2);  // fc1 dX from this rank's own rows
+    mark(P_BFC, s);
+    mnist_backward_b(a, s, conv_fork_ ? aux_stream_ : nullptr, ev_fork_, ev_join_);
+    mnist_conv_grad_reduce(a, s);
+    mark(P_BCONV, s);
+    HIP_OK(hipEventRecord(ev_b_, s));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
+    mark(P_CB0, comm_stream_);
+    reduce_bucket(0, BUCKET_SPLIT, bf);
+    mark(P_CB1, comm_stream_);
+    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    HIP_OK(hipStreamWaitEvent(s, ev_ag_, 0));
+    mnist_fc_grad_sfb(a, s);  // beside the conv bucket's all-reduce
+    HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+    const int64_t* t = (const int64_t*)tnext_.data_ptr();
+    if (shard) {
+      apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s, t);
+      apply_optimizer_range(OFF_WD1 + rk * zshard_, OFF_WD1 + (rk + 1) * zshard_, scale, 0, s, t);
+      apply_optimizer_range(OFF_BD1, TOTAL, scale, 0, s, t);
+      pending_wag_ = true;
+      if (join_end) {  // the caller reads whole weights after this step: gather the shards now
+        HIP_OK(hipEventRecord(ev_start_, s));
+        HIP_OK(hipStreamWaitEvent(comm_stream_, ev_start_, 0));
+        ag_w(comm_stream_);
+        HIP_OK(hipEventRecord(ev_wag_, comm_stream_));
+        HIP_OK(hipStreamWaitEvent(s, ev_wag_, 0));
+        pending_wag_ = false;
+      }
+    } else {
+      apply_optimizer_range(0, TOTAL, scale, 0, s, t);
+    }
+    mark(P_OPT, s);
   }
 
   // fp32 step: forward, backward (fc grads + conv slabs), slab reduce + step bump, [fp32
@@ -1029,6 +1122,8 @@ class MnistEngine : public torch::CustomClassHolder {
   hipStream_t aux_stream_ = nullptr, opt_stream_ = nullptr;
   hipEvent_t ev_opt_a_ = nullptr, ev_start_ = nullptr, ev_ag_ = nullptr;
   bool zero_ = false;
+  bool dp_serial_ = true;    // train_step_sfb_serial (default) vs the overlapped train_step_sfb
+  bool pending_wag_ = false;  // serialized ZeRO: this step's shards not yet all-gathered
   bool force_dp_ = false;
   int64_t zshard_ = 0;
   bool pending_opt_a_ = false;  // DP: the main stream still has to wait for the fc optimizer
@@ -1110,6 +1205,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("phase_times", &MnistEngine::phase_times)
       .def("zero", &MnistEngine::zero)
       .def("sync_params", &MnistEngine::sync_params)
+      .def("set_dp_serial", &MnistEngine::set_dp_serial)
       .def("world", &MnistEngine::world)
       .def("forward", &MnistEngine::forward)
       .def("backward_a", &MnistEngine::backward_a)

@@ -133,6 +133,37 @@ def test_forced_dp_world1_zero1_tracks_plain_dp(cuda, mode, sfb):
     tr1.close()
 
 
+@pytest.mark.parametrize("mode,zero", [("rccl", False), ("ipc", False), ("rccl", True)])
+def test_serialized_sfb_schedule_equals_overlapped(cuda, mode, zero):
+    """The serialized DP step (default: every compute kernel on the main stream, collectives on
+    the comm stream) against the overlapped three-stream schedule: identical kernels and data, so
+    the parameters, Adam state and bf16 shadow agree bit for bit after eager + captured steps."""
+    from tensorflow_distributed_amd.parallel.transport import attach_engine
+
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        params, (ov, se) = _engines_on_dataset(cuda, 2)
+        trs = []
+        for e, serial in ((ov, 0), (se, 1)):
+            trs.append(attach_engine(e, 0, 1, cuda, mode=mode, force_dp=True, sfb=True))
+            e.set_dp_serial(serial)
+            if zero:
+                e.set_zero(True)
+            e.train_step()
+            e.train_step()
+            e.capture_train_steps("t", 3)
+            e.replay("t", 2)
+            e.sync_params()
+    torch.cuda.synchronize()
+    for tr in trs:
+        tr.check()
+    assert int(se.step_tensor().item()) == int(ov.step_tensor().item()) == 8
+    assert torch.equal(se.params(), ov.params()) and torch.equal(se.adam_v(), ov.adam_v())
+    assert torch.equal(se.params_bf16(), ov.params_bf16())
+    for tr in trs:
+        tr.close()
+
+
 @pytest.mark.parametrize("mode", ["rccl", "ipc"])
 def test_forced_dp_world1_captured_steps_track_fused(cuda, mode):
     """Two eager + two graph-replayed steps (captured collectives) with dropout and Adam: same
