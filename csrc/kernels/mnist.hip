@@ -1733,9 +1733,16 @@ __device__ __forceinline__ void reduce_chunk(const float* __restrict__ slab, int
 constexpr int RED2_BLOCKS = (801 * 64 + 63) / 64;  // 801 blocks x 64 outputs (4 phases over the B/2 slabs)
 constexpr int RED1_BLOCKS = (832 + 15) / 16;       // 52 blocks x 16 outputs (16 phases over 2B slabs)
 __global__ __launch_bounds__(256) void gather_next_kernel(MnistStepArgs a) { gather_next(a, *a.step + 1, blockIdx.x); }
-__global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a) {
+// gb > 0: the first gb blocks gather the next step's batch (step number from MnistStepArgs::t_out,
+// written by this step's head kernel, so nothing here reads the step that block gb bumps) -- one
+// launch instead of gather_next_kernel + reduce_conv_grads on the DP path
+__global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a, int gb) {
   __shared__ float red[256];
-  const int id = blockIdx.x;
+  if ((int)blockIdx.x < gb) {
+    gather_next(a, *a.t_out, blockIdx.x);
+    return;
+  }
+  const int id = blockIdx.x - gb;
   if (id < RED2_BLOCKS)
     reduce_chunk<64>(a.wg2_slab, a.wg2_splits, 801 * 64, 801 * 64, id * 64, a.grad + OFF_WC2,
                      a.gbf_b ? a.gbf_b + OFF_WC2 : nullptr, red);
@@ -2010,9 +2017,14 @@ void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux, hi
 }
 
 void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s) {
+  const bool gather = a.step_bump && a.perm && a.xpre;
+  if (gather && a.t_out) {  // one launch: gather blocks read the next step from t_out
+    reduce_conv_grads<<<a.B + RED2_BLOCKS + RED1_BLOCKS, 256, 0, s>>>(a, a.B);
+    return;
+  }
   // the next step's batch first (this kernel bumps the step; the gather reads it unbumped)
-  if (a.step_bump && a.perm && a.xpre) gather_next_kernel<<<a.B, 256, 0, s>>>(a);
-  reduce_conv_grads<<<RED2_BLOCKS + RED1_BLOCKS, 256, 0, s>>>(a);
+  if (gather) gather_next_kernel<<<a.B, 256, 0, s>>>(a);
+  reduce_conv_grads<<<RED2_BLOCKS + RED1_BLOCKS, 256, 0, s>>>(a, 0);
 }
 
 void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region) {
