@@ -8,6 +8,8 @@
 // last conv-grad reduce kernel bumps it), so a captured step graph needs no host round trip and
 // the optimizer needs no cross-block arrival counter (a 2048-way fan-in on one word).
 #include <math.h>
+
+#include <stdexcept>
 #include "../common.h"
 #include "../tfd_kernels.h"
 
@@ -51,6 +53,56 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(AdamArgs a) {
     const float g = (a.gbf ? bf2f(a.gbf[i]) : a.g[i]) * a.grad_scale;
     float m = a.m[i] + (g - a.m[i]) * c1;
     float v = a.v[i] + (g * g - a.v[i]) * c2;
+    const float p = a.p[i] - lr_t * m / (sqrtf(v) + a.eps);
+    a.p[i] = p; a.m[i] = m; a.v[i] = v;
+    if (a.pbf) a.pbf[i] = f2bf_bits(p);
+  }
+}
+
+struct AdamRanges {
+  int nr;
+  int64_t beg4[3], pre4[4];  // range starts and prefix sums in float4 units
+  int64_t tail_beg, tail_n;  // the last range's n % 4 scalar elements
+};
+__device__ __forceinline__ void adam_elem4(const AdamArgs& a, int64_t i, float lr_t, float c1, float c2) {
+  f32x4 p = reinterpret_cast<f32x4*>(a.p)[i];
+  f32x4 m = reinterpret_cast<f32x4*>(a.m)[i];
+  f32x4 v = reinterpret_cast<f32x4*>(a.v)[i];
+  f32x4 g;
+  if (a.gbf) {
+    const uint2 gb = reinterpret_cast<const uint2*>(a.gbf)[i];
+    g = f32x4{bf2f((uint16_t)(gb.x & 0xFFFF)), bf2f((uint16_t)(gb.x >> 16)), bf2f((uint16_t)(gb.y & 0xFFFF)),
+              bf2f((uint16_t)(gb.y >> 16))};
+  } else {
+    g = reinterpret_cast<const f32x4*>(a.g)[i];
+  }
+  g *= a.grad_scale;
+  m = m + (g - m) * c1;
+  v = v + (g * g - v) * c2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) p[j] -= lr_t * m[j] / (sqrtf(v[j]) + a.eps);
+  reinterpret_cast<f32x4*>(a.p)[i] = p;
+  reinterpret_cast<f32x4*>(a.m)[i] = m;
+  reinterpret_cast<f32x4*>(a.v)[i] = v;
+  if (a.pbf) reinterpret_cast<uint2*>(a.pbf)[i] = make_uint2(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]));
+}
+// same per-element math as adam_kernel, over a table of ranges (the logical float4 index is mapped
+// to its range by the prefix sums)
+__global__ __launch_bounds__(kOptThreads) void adam_ranges_kernel(AdamArgs a, AdamRanges r) {
+  const int64_t t = (a.step ? *a.step : 0) + a.t_offset;
+  const float b1p = powf(a.beta1, (float)t), b2p = powf(a.beta2, (float)t);
+  const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  const float c1 = 1.f - a.beta1, c2 = 1.f - a.beta2;
+  const int64_t stride = (int64_t)gridDim.x * kOptThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kOptThreads + threadIdx.x; i < r.pre4[r.nr]; i += stride) {
+    const int k = i < r.pre4[1] ? 0 : (r.nr > 2 && i >= r.pre4[2] ? 2 : 1);
+    adam_elem4(a, r.beg4[k] + (i - r.pre4[k]), lr_t, c1, c2);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < r.tail_n) {
+    const int64_t i = r.tail_beg + threadIdx.x;
+    const float g = (a.gbf ? bf2f(a.gbf[i]) : a.g[i]) * a.grad_scale;
+    const float m = a.m[i] + (g - a.m[i]) * c1;
+    const float v = a.v[i] + (g * g - a.v[i]) * c2;
     const float p = a.p[i] - lr_t * m / (sqrtf(v) + a.eps);
     a.p[i] = p; a.m[i] = m; a.v[i] = v;
     if (a.pbf) a.pbf[i] = f2bf_bits(p);
@@ -102,6 +154,20 @@ inline int blocks_for(int64_t n, int per_thread) {
 
 void adam_apply(const AdamArgs& a, hipStream_t s) {
   adam_kernel<<<blocks_for(a.n, 4), kOptThreads, 0, s>>>(a);
+}
+void adam_apply_ranges(const AdamArgs& a, int nr, const int64_t* beg, const int64_t* n, hipStream_t s) {
+  if (nr < 1 || nr > 3) throw std::runtime_error("adam_apply_ranges: 1..3 ranges");
+  AdamRanges r{};
+  r.nr = nr;
+  r.pre4[0] = 0;
+  for (int k = 0; k < nr; ++k) {
+    if (beg[k] % 4 || (k < nr - 1 && n[k] % 4)) throw std::runtime_error("adam_apply_ranges: unaligned range");
+    r.beg4[k] = beg[k] / 4;
+    r.pre4[k + 1] = r.pre4[k] + n[k] / 4;
+  }
+  r.tail_beg = beg[nr - 1] + n[nr - 1] / 4 * 4;
+  r.tail_n = n[nr - 1] % 4;
+  adam_ranges_kernel<<<blocks_for(r.pre4[nr] * 4, 4), kOptThreads, 0, s>>>(a, r);
 }
 void sgd_apply(const SgdArgs& a, hipStream_t s) {
   sgd_kernel<<<blocks_for(a.n, 1), kOptThreads, 0, s>>>(a);

@@ -713,9 +713,18 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
     const int64_t* t = (const int64_t*)tnext_.data_ptr();
     if (shard) {
-      apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s, t);
-      apply_optimizer_range(OFF_WD1 + rk * zshard_, OFF_WD1 + (rk + 1) * zshard_, scale, 0, s, t);
-      apply_optimizer_range(OFF_BD1, TOTAL, scale, 0, s, t);
+      const int64_t beg[3] = {0, OFF_WD1 + rk * zshard_, OFF_BD1};
+      const int64_t end[3] = {BUCKET_SPLIT, OFF_WD1 + (rk + 1) * zshard_, TOTAL};
+      if (opt_ == 0 && BUCKET_SPLIT % 4 == 0 && zshard_ % 4 == 0) {  // one launch over the three ranges
+        const int64_t n[3] = {end[0] - beg[0], end[1] - beg[1], end[2] - beg[2]};
+        AdamArgs o{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(),
+                   (const float*)grad_.data_ptr(), (uint16_t*)pbf_.data_ptr(),
+                   bf16_comm_ ? (const uint16_t*)gbf_.data_ptr() : nullptr, 0, (float)lr_, (float)b1_, (float)b2_,
+                   (float)eps_, t, 0, (float)scale};
+        adam_apply_ranges(o, 3, beg, n, s);
+      } else {
+        for (int k = 0; k < 3; ++k) apply_optimizer_range(beg[k], end[k], scale, 0, s, t);
+      }
       pending_wag_ = true;
       if (join_end) {  // the caller reads whole weights after this step: gather the shards now
         HIP_OK(hipEventRecord(ev_start_, s));

@@ -151,6 +151,10 @@ struct AdamArgs {
   float grad_scale;            // multiply g (e.g. 1/N for sum-all-reduce)
 };
 void adam_apply(const AdamArgs& a, hipStream_t s);
+// ONE launch over up to 3 disjoint ranges [beg, beg + n) of the flat buffers (a's pointers are the
+// buffer bases, a.n is ignored): the ZeRO-1 optimizer (conv bucket + this rank's fc1 shard + tail)
+// without a launch per range. Every beg and every n but the last must be a multiple of 4.
+void adam_apply_ranges(const AdamArgs& a, int nr, const int64_t* beg, const int64_t* n, hipStream_t s);
 struct SgdArgs {
   float* p; float* mom; const float* g; uint16_t* pbf; const uint16_t* gbf; int64_t n;
   float lr, momentum, weight_decay, grad_scale; int nesterov;
