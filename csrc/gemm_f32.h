@@ -42,7 +42,12 @@ __device__ __forceinline__ float read_frag_f(const float* lds, int r0, int kk, i
 }
 
 // C tile (m0, n0) over k in [kbeg, kend); WM x WN waves; epilogue epi(m4, n, f32x4 rows m4..m4+3).
-template <int BM, int BN, int BK, int WM, int WN, class LA, class LB, class EPI>
+// RS = register stages: RS = 2 issues the global loads of K-tile t+2 while tile t+1 still waits in
+// registers (two K-iterations of latency cover instead of one).
+#ifndef TFD_F32_RS
+#define TFD_F32_RS 2
+#endif
+template <int BM, int BN, int BK, int WM, int WN, class LA, class LB, class EPI, int RS = TFD_F32_RS>
 __device__ __forceinline__ void gemm_block_f32(const LA& la, const LB& lb, const EPI& epi, int m0, int n0, int kbeg,
                                                int kend, float* smem) {
   constexpr int NT = 64 * WM * WN;
@@ -56,21 +61,22 @@ __device__ __forceinline__ void gemm_block_f32(const LA& la, const LB& lb, const
   float* Bs[2] = {smem + 2 * TA::ELEMS, smem + 2 * TA::ELEMS + TB::ELEMS};
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  f32x4 ra[CA], rb[CB];
+  static_assert(RS == 1 || RS == 2, "register stages");
+  f32x4 ra[RS][CA], rb[RS][CB];
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = zero_f4();
 
-  auto gload = [&](int k0) {
+  auto gload = [&](int k0, f32x4 (&xa)[CA], f32x4 (&xb)[CB]) {
 #pragma unroll
     for (int c = 0; c < CA; ++c) {
       const int idx = tid + c * NT;
       if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
         const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 4;
-        if constexpr (LA::KC) ra[c] = la(m0 + row, k0 + col);
-        else ra[c] = la(m0 + col, k0 + row);
+        if constexpr (LA::KC) xa[c] = la(m0 + row, k0 + col);
+        else xa[c] = la(m0 + col, k0 + row);
       }
     }
 #pragma unroll
@@ -78,18 +84,18 @@ __device__ __forceinline__ void gemm_block_f32(const LA& la, const LB& lb, const
       const int idx = tid + c * NT;
       if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
         const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 4;
-        if constexpr (LB::KC) rb[c] = lb(n0 + row, k0 + col);
-        else rb[c] = lb(n0 + col, k0 + row);
+        if constexpr (LB::KC) xb[c] = lb(n0 + row, k0 + col);
+        else xb[c] = lb(n0 + col, k0 + row);
       }
     }
   };
-  auto sstore = [&](float* A, float* Bt) {
+  auto sstore = [&](float* A, float* Bt, const f32x4 (&xa)[CA], const f32x4 (&xb)[CB]) {
 #pragma unroll
     for (int c = 0; c < CA; ++c) {
       const int idx = tid + c * NT;
       if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
         const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 4;
-        *reinterpret_cast<f32x4*>(A + row * TA::ROW + col) = ra[c];
+        *reinterpret_cast<f32x4*>(A + row * TA::ROW + col) = xa[c];
       }
     }
 #pragma unroll
@@ -97,7 +103,7 @@ __device__ __forceinline__ void gemm_block_f32(const LA& la, const LB& lb, const
       const int idx = tid + c * NT;
       if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
         const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 4;
-        *reinterpret_cast<f32x4*>(Bt + row * TB::ROW + col) = rb[c];
+        *reinterpret_cast<f32x4*>(Bt + row * TB::ROW + col) = xb[c];
       }
     }
   };
@@ -116,16 +122,37 @@ __device__ __forceinline__ void gemm_block_f32(const LA& la, const LB& lb, const
     }
   };
   const int nk = (kend - kbeg + BK - 1) / BK;
-  if (nk > 0) {
-    gload(kbeg);
-    sstore(As[0], Bs[0]);
-    __syncthreads();
-    for (int t = 0; t < nk; ++t) {
-      const int cur = t & 1;
-      if (t + 1 < nk) gload(kbeg + (t + 1) * BK);
-      compute(As[cur], Bs[cur]);
-      if (t + 1 < nk) sstore(As[cur ^ 1], Bs[cur ^ 1]);
+  if constexpr (RS == 1) {
+    if (nk > 0) {
+      gload(kbeg, ra[0], rb[0]);
+      sstore(As[0], Bs[0], ra[0], rb[0]);
       __syncthreads();
+      for (int t = 0; t < nk; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < nk) gload(kbeg + (t + 1) * BK, ra[0], rb[0]);
+        compute(As[cur], Bs[cur]);
+        if (t + 1 < nk) sstore(As[cur ^ 1], Bs[cur ^ 1], ra[0], rb[0]);
+        __syncthreads();
+      }
+    }
+  } else {
+    // LDS[t&1] holds tile t; register set (t+1)&1 holds tile t+1; tile t+2 loads into set t&1
+    if (nk > 0) {
+      gload(kbeg, ra[0], rb[0]);
+      if (nk > 1) gload(kbeg + BK, ra[1], rb[1]);
+      sstore(As[0], Bs[0], ra[0], rb[0]);
+      __syncthreads();
+      for (int t = 0; t < nk; t += 2) {
+        if (t + 2 < nk) gload(kbeg + (t + 2) * BK, ra[0], rb[0]);
+        compute(As[0], Bs[0]);
+        if (t + 1 < nk) sstore(As[1], Bs[1], ra[1], rb[1]);
+        __syncthreads();
+        if (t + 1 >= nk) break;
+        if (t + 3 < nk) gload(kbeg + (t + 3) * BK, ra[1], rb[1]);
+        compute(As[1], Bs[1]);
+        if (t + 2 < nk) sstore(As[0], Bs[0], ra[0], rb[0]);
+        __syncthreads();
+      }
     }
   }
 #pragma unroll

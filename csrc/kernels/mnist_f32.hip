@@ -12,6 +12,7 @@
 // f32_conv2_bwd K13 (+conv1 ReluGrad/pool-mask epilogue) + K14 (+K12 bias row) slabs;
 // f32_conv1_wgrad K15 (+K12). The slab reduce + optimizer are shared with the bf16 step.
 #include "../common.h"
+#include "../gemm.h"  // buf_ld
 #include "../gemm_f32.h"
 #include "../mnist_layout.h"
 #include "../tfd_kernels.h"
@@ -27,6 +28,14 @@ __device__ __forceinline__ int data_row_f(const int* perm, const int64_t* step, 
   if (!perm) return b;
   const int64_t s = *step;
   return perm[(int)((s * (int64_t)B + b) % (int64_t)n_data)];
+}
+
+// Branch-free float4 operand load (raw buffer load; an out-of-range chunk gets an offset past the
+// descriptor, which the hardware range check returns as zeros) -- csrc/gemm.h buf_ld for fp32: no
+// exec-masked branch per load, so the register pipeline can keep the next K-tile's loads in flight.
+__device__ __forceinline__ f32x4 buf_ld_f4(const float* base, uint32_t nbytes, uint32_t elem_off, bool ok) {
+  const uint4 u = buf_ld(reinterpret_cast<const uint16_t*>(base), nbytes, elem_off * 2u, ok);
+  return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
 }
 
 // ---------------- K1+K3: conv1 + bias + relu + maxpool + argmax (VALU, fp32 out) ----------------
@@ -93,13 +102,13 @@ struct Conv2FwdAF {
   const float* __restrict__ p1;
   int M;
   __device__ __forceinline__ f32x4 operator()(int m, int k) const {
-    if (m >= M || k >= 800) return zero_f4();
     const int b = m / 196, r = m - b * 196, pp = r >> 2, win = r & 3;
     const int ph = pp / 7, pw = pp - ph * 7;
     const int tap = k >> 5, ci0 = k & 31, kh = tap / 5, kw = tap - kh * 5;
     const int ih = 2 * ph + (win >> 1) + kh - 2, iw = 2 * pw + (win & 1) + kw - 2;
-    if ((unsigned)ih >= 14u || (unsigned)iw >= 14u) return zero_f4();
-    return *reinterpret_cast<const f32x4*>(p1 + ((size_t)(b * 14 + ih) * 14 + iw) * 32 + ci0);
+    const bool ok = m < M && k < 800 && (unsigned)ih < 14u && (unsigned)iw < 14u;
+    const uint32_t nb = (uint32_t)(M / 196) * 14u * 14u * 32u * 4u;
+    return buf_ld_f4(p1, nb, (uint32_t)((b * 14 + ih) * 14 + iw) * 32u + ci0, ok);
   }
 };
 struct PoolEpiF {
@@ -126,7 +135,10 @@ struct PoolEpiF {
     idx2[o] = (uint8_t)am;
   }
 };
-constexpr int F_BK = 32;
+#ifndef TFD_F_BK  // K-tile of the fp32 GEMM blocks
+#define TFD_F_BK 32
+#endif
+constexpr int F_BK = TFD_F_BK;
 __global__ __launch_bounds__(256) void f32_conv2_fwd(MnistF32Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int M = a.B * 196;
@@ -355,21 +367,20 @@ struct Conv2DgradAF {  // (m = (b,ih,iw), k = tap*64 + co) = dz2[b][ih-kh+2][iw-
   const float* __restrict__ dz2;
   int M;
   __device__ __forceinline__ f32x4 operator()(int m, int k) const {
-    if (m >= M || k >= 1600) return zero_f4();
     const int b = m / 196, r = m - b * 196, ih = r / 14, iw = r - ih * 14;
     const int tap = k >> 6, co0 = k & 63, kh = tap / 5, kw = tap - kh * 5;
     const int oh = ih - kh + 2, ow = iw - kw + 2;
-    if ((unsigned)oh >= 14u || (unsigned)ow >= 14u) return zero_f4();
-    return *reinterpret_cast<const f32x4*>(dz2 + ((size_t)(b * 14 + oh) * 14 + ow) * 64 + co0);
+    const bool ok = m < M && k < 1600 && (unsigned)oh < 14u && (unsigned)ow < 14u;
+    const uint32_t nb = (uint32_t)(M / 196) * 14u * 14u * 64u * 4u;
+    return buf_ld_f4(dz2, nb, (uint32_t)((b * 14 + oh) * 14 + ow) * 64u + co0, ok);
   }
 };
 struct Conv2DgradBF {  // (n = ci, k = tap*64 + co) -> W2[tap][ci][co]
   static constexpr bool KC = true;
   const float* __restrict__ w2;
   __device__ __forceinline__ f32x4 operator()(int n, int k) const {
-    if (n >= 32 || k >= 1600) return zero_f4();
     const int tap = k >> 6, co0 = k & 63;
-    return *reinterpret_cast<const f32x4*>(w2 + (size_t)(tap * 32 + n) * 64 + co0);
+    return buf_ld_f4(w2, 25u * 32u * 64u * 4u, (uint32_t)(tap * 32 + n) * 64u + co0, n < 32 && k < 1600);
   }
 };
 struct MaskEpiF {
@@ -391,13 +402,14 @@ struct Conv2WgradAF {  // (mn = tap*32+ci [800 = ones row], k = pixel): 4 consec
   const float* __restrict__ p1;
   int K;
   __device__ __forceinline__ f32x4 operator()(int mn, int k) const {
-    if (k >= K || mn > 800) return zero_f4();
-    if (mn == 800) return f32x4{1.f, 0.f, 0.f, 0.f};
     const int tap = mn >> 5, ci0 = mn & 31, kh = tap / 5, kw = tap - kh * 5;
     const int b = k / 196, r = k - b * 196, oh = r / 14, ow = r - oh * 14;
     const int ih = oh + kh - 2, iw = ow + kw - 2;
-    if ((unsigned)ih >= 14u || (unsigned)iw >= 14u) return zero_f4();
-    return *reinterpret_cast<const f32x4*>(p1 + ((size_t)(b * 14 + ih) * 14 + iw) * 32 + ci0);
+    const bool ok = k < K && mn < 800 && (unsigned)ih < 14u && (unsigned)iw < 14u;
+    const uint32_t nb = (uint32_t)(K / 196) * 14u * 14u * 32u * 4u;
+    const f32x4 v = buf_ld_f4(p1, nb, (uint32_t)((b * 14 + ih) * 14 + iw) * 32u + ci0, ok);
+    // the bias "ones row" (mn == 800): a select, not a branch around the load
+    return mn == 800 && k < K ? f32x4{1.f, 0.f, 0.f, 0.f} : v;
   }
 };
 constexpr int F_C2W_GX = (801 + 63) / 64;  // 13
