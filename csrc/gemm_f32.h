@@ -61,7 +61,7 @@ __device__ __forceinline__ void gemm_block_f32(const LA& la, const LB& lb, const
   float* Bs[2] = {smem + 2 * TA::ELEMS, smem + 2 * TA::ELEMS + TB::ELEMS};
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  static_assert(RS == 1 || RS == 2, "register stages");
+  static_assert(RS >= 1 && RS <= 6, "register stages");
   f32x4 ra[RS][CA], rb[RS][CB];
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -133,6 +133,28 @@ __device__ __forceinline__ void gemm_block_f32(const LA& la, const LB& lb, const
         compute(As[cur], Bs[cur]);
         if (t + 1 < nk) sstore(As[cur ^ 1], Bs[cur ^ 1], ra[0], rb[0]);
         __syncthreads();
+      }
+    }
+  } else if constexpr (RS > 2) {
+    // register ring: set u = t % RS holds tile t until it is written to LDS at step t-1, then is
+    // refilled with tile t+RS (RS tiles of loads in flight behind the MFMAs)
+    if (nk > 0) {
+#pragma unroll
+      for (int u = 0; u < RS; ++u)
+        if (u < nk) gload(kbeg + u * BK, ra[u], rb[u]);
+      sstore(As[0], Bs[0], ra[0], rb[0]);
+      __syncthreads();
+      for (int t0 = 0; t0 < nk; t0 += RS) {
+#pragma unroll
+        for (int u = 0; u < RS; ++u) {
+          const int t = t0 + u;
+          if (t < nk) {
+            if (t + RS < nk) gload(kbeg + (t + RS) * BK, ra[u], rb[u]);
+            compute(As[t & 1], Bs[t & 1]);
+            if (t + 1 < nk) sstore(As[(t + 1) & 1], Bs[(t + 1) & 1], ra[(u + 1) % RS], rb[(u + 1) % RS]);
+            __syncthreads();
+          }
+        }
       }
     }
   } else {
