@@ -378,6 +378,11 @@ struct Tile {
 #ifndef TFD_CONV_RS  // register stages of the conv/dense GEMM core (global-load prefetch depth)
 #define TFD_CONV_RS 1
 #endif
+#ifndef TFD_CONV_RS_SMALL  // register stages for tiles of at most 64x64 (fewer accumulator registers)
+#define TFD_CONV_RS_SMALL TFD_CONV_RS
+#endif
+template <int BM, int BN>
+constexpr int conv_rs() { return BM * BN <= 64 * 64 ? TFD_CONV_RS_SMALL : TFD_CONV_RS; }
 #ifndef TFD_CONV_BK  // K-tile of the conv/dense GEMM core (LDS per block: 2 x (BM + BN) x (BK + pad) x 2 B)
 #define TFD_CONV_BK 64
 #endif
@@ -394,7 +399,7 @@ template <int BM, int BN, class LA, class LB, class EPI>
 __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_kernel(LA la, LB lb, EPI epi, int kchunk, int KD) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int kb = blockIdx.z * kchunk, ke = min(KD, kb + kchunk);
-  gemm_block<BM, BN, CBK, 2, 2, LA, LB, EPI, TFD_CONV_RS>(la, lb, epi, blockIdx.y * BM, blockIdx.x * BN, kb, ke,
+  gemm_block<BM, BN, CBK, 2, 2, LA, LB, EPI, conv_rs<BM, BN>()>(la, lb, epi, blockIdx.y * BM, blockIdx.x * BN, kb, ke,
                                                          (bf16*)smem_raw);
 }
 
@@ -408,7 +413,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_kernel(LA la, LB 
                                                                       int M, int N, int KD) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   f32x4 acc[BM / 32][BN / 32];
-  gemm_mainloop<BM, BN, CBK, 2, 2, LA, LB, TFD_CONV_RS>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
+  gemm_mainloop<BM, BN, CBK, 2, 2, LA, LB, conv_rs<BM, BN>()>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
                                                        (bf16*)smem_raw, acc);
   lds_epilogue<BM, BN, 2, 2, ADD, false>(acc, smem_raw, y, add, M, N, blockIdx.y * BM, blockIdx.x * BN, nullptr);
 }
@@ -424,7 +429,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB
 #if TFD_CONV_LDS_EPI
   (void)TN;
   f32x4 acc[BM / 32][BN / 32];
-  gemm_mainloop<BM, BN, CBK, WM, WN, LA, LB, TFD_CONV_RS>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
+  gemm_mainloop<BM, BN, CBK, WM, WN, LA, LB, conv_rs<BM, BN>()>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
                                                          (bf16*)smem_raw, acc);
   lds_epilogue<BM, BN, WM, WN, false, true>(acc, smem_raw, y, nullptr, M, N, blockIdx.y * BM, blockIdx.x * BN, part,
                                             RowId{}, 0u, tcnt, tG, tot);
@@ -434,7 +439,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB
 #pragma unroll
   for (int j = 0; j < TN; ++j) { s[j] = 0.f; q[j] = 0.f; }
   StoreBf16Stats<TN> epi{y, M, N, s, q};
-  gemm_block<BM, BN, CBK, WM, WN, LA, LB, StoreBf16Stats<TN>, TFD_CONV_RS>(la, lb, epi, blockIdx.y * BM,
+  gemm_block<BM, BN, CBK, WM, WN, LA, LB, StoreBf16Stats<TN>, conv_rs<BM, BN>()>(la, lb, epi, blockIdx.y * BM,
                                                                           blockIdx.x * BN, 0, KD, (bf16*)smem_raw);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
 #pragma unroll
@@ -473,7 +478,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void dgrad_phase_kernel(DgradPha
                                                                         const uint16_t* add) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   f32x4 acc[BM / 32][BN / 32];
-  gemm_mainloop<BM, BN, CBK, 2, 2, DgradPhaseA, DgradPhaseB, TFD_CONV_RS>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0,
+  gemm_mainloop<BM, BN, CBK, 2, 2, DgradPhaseA, DgradPhaseB, conv_rs<BM, BN>()>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0,
                                                                          la.g.KD, (bf16*)smem_raw, acc);
   const uint32_t xbytes = (uint32_t)la.g.N * la.g.H * la.g.W * la.g.C * 2u;
   lds_epilogue<BM, BN, 2, 2, ADD, false, PhaseRows>(acc, smem_raw, dx, add, la.g.M, la.g.C, blockIdx.y * BM,
