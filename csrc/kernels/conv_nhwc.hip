@@ -13,6 +13,7 @@
 // constants. C and K must be multiples of 8 (16-B chunks); the 3-channel stem input is padded to 8.
 // 1x1 / stride-1 / pad-0 convolutions are plain GEMMs and take the dense loaders.
 #include <stdexcept>
+#include <type_traits>
 
 #include "../common.h"
 #include "../conv_kernels.h"
@@ -541,6 +542,20 @@ void launch_gemm_stats(const LA& la, const LB& lb, uint16_t* y, int M, int N, in
 // same tile choice as dispatch(): 128x128 when that fills the chip
 bool use_big_tiles(int M, int N) { return (long)((M + 127) / 128) * ((N + 127) / 128) >= 256 && N >= 128; }
 
+// bf16-output tile (fwd, fwd + stats, dgrad): 128x128 when that fills the chip; for a 64-column
+// output (the C = 64 stage of a ResNet) 128x64 when that does, else 64x64. TFD_TALL_TILES=0: no
+// 128x64 (the round-2 first pass).
+#ifndef TFD_TALL_TILES
+#define TFD_TALL_TILES 1
+#endif
+enum OutTile { OT64, OT128x64, OT128 };
+OutTile out_tile(int M, int N) {
+  if (use_big_tiles(M, N)) return OT128;
+  if (TFD_TALL_TILES && N == 64 && (long)((M + 127) / 128) >= 256) return OT128x64;
+  return OT64;
+}
+int out_tile_rows(int M, int N) { return out_tile(M, N) == OT64 ? (M + 63) / 64 : (M + 127) / 128; }
+
 template <int BM, int BN, class LA, class LB, class EPI>
 void launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N, int KD, int splits, hipStream_t st) {
   constexpr int sm = GemmSmem<BM, BN, CBK, LA, LB>::BYTES;
@@ -568,12 +583,14 @@ void dispatch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int KD, 
 // bf16-output GEMM (optionally + add), same tile choice as dispatch()
 template <class LA, class LB>
 void dispatch_bf16(const LA& la, const LB& lb, uint16_t* y, const uint16_t* add, int M, int N, int KD, hipStream_t st) {
-  const bool big = use_big_tiles(M, N);
+  const OutTile t = out_tile(M, N);
   if (add) {
-    if (big) launch_gemm_bf16<128, 128, LA, LB, true>(la, lb, y, add, M, N, KD, st);
+    if (t == OT128) launch_gemm_bf16<128, 128, LA, LB, true>(la, lb, y, add, M, N, KD, st);
+    else if (t == OT128x64) launch_gemm_bf16<128, 64, LA, LB, true>(la, lb, y, add, M, N, KD, st);
     else launch_gemm_bf16<64, 64, LA, LB, true>(la, lb, y, add, M, N, KD, st);
   } else {
-    if (big) launch_gemm_bf16<128, 128, LA, LB, false>(la, lb, y, add, M, N, KD, st);
+    if (t == OT128) launch_gemm_bf16<128, 128, LA, LB, false>(la, lb, y, add, M, N, KD, st);
+    else if (t == OT128x64) launch_gemm_bf16<128, 64, LA, LB, false>(la, lb, y, add, M, N, KD, st);
     else launch_gemm_bf16<64, 64, LA, LB, false>(la, lb, y, add, M, N, KD, st);
   }
 }
@@ -612,7 +629,7 @@ void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t
 
 int conv_fwd_stats_rows(const ConvShape& c) {  // row blocks (+ the totals row, see launch_gemm_stats)
   const int M = c.N * c.Ho() * c.Wo();
-  const int rows = use_big_tiles(M, c.K) ? (M + 127) / 128 : (M + 63) / 64;
+  const int rows = TFD_CONV_LDS_EPI ? out_tile_rows(M, c.K) : (use_big_tiles(M, c.K) ? (M + 127) / 128 : (M + 63) / 64);
   return rows + (TFD_CONV_LDS_EPI && bn_totals_enabled() ? 1 : 0);
 }
 
@@ -620,16 +637,15 @@ void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, ui
                     hipStream_t st) {
   const int M = c.N * c.Ho() * c.Wo(), KD = c.R * c.S * c.C;
   DenseX<false> lb{w, c.K, c.K, KD};
-  const bool big = use_big_tiles(M, c.K);
-  if (is_pointwise(c)) {
-    DenseX<true> la{x, c.C, M, c.C};
-    if (big) launch_gemm_stats<128, 128>(la, lb, y, M, c.K, KD, part, st);
-    else launch_gemm_stats<64, 64>(la, lb, y, M, c.K, KD, part, st);
-  } else {
-    FwdA la{x, make_geo(c, M, KD)};
-    if (big) launch_gemm_stats<128, 128>(la, lb, y, M, c.K, KD, part, st);
-    else launch_gemm_stats<64, 64>(la, lb, y, M, c.K, KD, part, st);
-  }
+  const OutTile t = TFD_CONV_LDS_EPI ? out_tile(M, c.K) : (use_big_tiles(M, c.K) ? OT128 : OT64);
+  auto go = [&](const auto& la) {
+    using LA = std::decay_t<decltype(la)>;
+    if (t == OT128) launch_gemm_stats<128, 128, LA, DenseX<false>>(la, lb, y, M, c.K, KD, part, st);
+    else if (t == OT128x64) launch_gemm_stats<128, 64, LA, DenseX<false>>(la, lb, y, M, c.K, KD, part, st);
+    else launch_gemm_stats<64, 64, LA, DenseX<false>>(la, lb, y, M, c.K, KD, part, st);
+  };
+  if (is_pointwise(c)) go(DenseX<true>{x, c.C, M, c.C});
+  else go(FwdA{x, make_geo(c, M, KD)});
 }
 
 template <class Epi>
@@ -685,12 +701,14 @@ static void dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t
       g.hpwp = FastDiv(g.Hp * g.Wp); g.wp = FastDiv(g.Wp); g.k = FastDiv(c.K); g.nsd = FastDiv(g.ns);
       DgradPhaseA la{dy, g};
       DgradPhaseB lb{w, g, c.S};
-      const bool big = use_big_tiles(g.M, c.C);
+      const OutTile ot = out_tile(g.M, c.C);
       if (add) {
-        if (big) launch_phase<128, 128, true>(la, lb, dx, add, st);
+        if (ot == OT128) launch_phase<128, 128, true>(la, lb, dx, add, st);
+        else if (ot == OT128x64) launch_phase<128, 64, true>(la, lb, dx, add, st);
         else launch_phase<64, 64, true>(la, lb, dx, add, st);
       } else {
-        if (big) launch_phase<128, 128, false>(la, lb, dx, add, st);
+        if (ot == OT128) launch_phase<128, 128, false>(la, lb, dx, add, st);
+        else if (ot == OT128x64) launch_phase<128, 64, false>(la, lb, dx, add, st);
         else launch_phase<64, 64, false>(la, lb, dx, add, st);
       }
     }

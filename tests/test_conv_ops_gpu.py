@@ -32,8 +32,11 @@ CONVS = [  # N, H, W, C, K, R, stride, pad
 ]
 
 
-# the last shape's dgrad (M = 37632, C = 128) takes the 128x128 tiles of the LDS-staged epilogue
-@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS + [(48, 28, 28, 128, 32, 3, 1, 1)])
+# (48, 28, 28, 128, ...): its dgrad (M = 37632, C = 128) takes the 128x128 tiles of the LDS-staged
+# epilogue; (48, 28, 28, 64, 64): 128x64 output tiles for fwd and dgrad; (48, 56, 56, 64, 64, s2): the
+# strided phase dgrad on 128x64 tiles
+@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS + [(48, 28, 28, 128, 32, 3, 1, 1), (48, 28, 28, 64, 64, 3, 1, 1),
+                                                   (48, 56, 56, 64, 64, 3, 2, 1)])
 def test_conv_fwd_dgrad_wgrad(cuda, N, H, W, C, K, R, st, pad):
     torch.manual_seed(0)
     x = rb(torch.randn(N, H, W, C))
@@ -63,7 +66,7 @@ def test_conv_fwd_dgrad_wgrad(cuda, N, H, W, C, K, R, st, pad):
     assert relerr(dw2.cpu(), wr.grad.permute(2, 3, 1, 0)) < 1e-3
 
 
-@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS + [(8, 28, 28, 64, 256, 1, 1, 0)])
+@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS + [(8, 28, 28, 64, 256, 1, 1, 0), (48, 28, 28, 32, 64, 3, 1, 1)])
 def test_conv_fwd_stats_feeds_bn(cuda, N, H, W, C, K, R, st, pad):
     """conv2d_fwd_stats: same output as conv2d_fwd, and per-row-block sums of the stored bf16 output
     that bn_fwd(partials=...) turns into the same normalisation as its own statistics pass. The
