@@ -746,6 +746,10 @@ class MnistEngine : public torch::CustomClassHolder {
     TORCH_CHECK(!zero_, "ZeRO-1 is a bf16-path option");
     hipStream_t s = stream();
     MnistF32Args f = args_f32();
+    // one GPU + Adam: ONE tail kernel reduces the conv slabs, runs Adam over every region and bumps
+    // the step (t from the head), as the bf16 step does
+    const bool fused = !dp && opt_ == 0 && fuse_tail_;
+    if (fused) f.t_out = (int64_t*)tnext_.data_ptr();
     mark(P_START, s);
     mnist_f32_forward(f, true, s);
     mark(P_FWD, s);
@@ -754,6 +758,16 @@ class MnistEngine : public torch::CustomClassHolder {
     MnistStepArgs r = args();
     r.wg2_slab = f.wg2_slab;
     r.wg2_splits = f.wg2_splits;
+    r.xpre = nullptr;  // the fp32 kernels read their batch rows through perm/step: no prefetch gather
+    if (fused) {
+      MnistAdamArgs o{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(),
+                      (uint16_t*)pbf_.data_ptr(), (float)lr_, (float)b1_, (float)b2_, (float)eps_,
+                      (const int64_t*)tnext_.data_ptr(), (int64_t*)step_.data_ptr(), nullptr};
+      mark(P_BCONV, s);
+      mnist_adam_fused(r, o, s, true);
+      mark(P_OPT, s);
+      return;
+    }
     r.step_bump = (int64_t*)step_.data_ptr();
     mnist_conv_grad_reduce(r, s);
     mark(P_BCONV, s);

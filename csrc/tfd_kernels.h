@@ -134,6 +134,7 @@ struct MnistF32Args {
   int fc1_splits, wg2_splits;
   float keep_prob;
   uint32_t seed, rank;
+  int64_t* t_out;              // if set: the head writes step + 1 here (the fused optimizer tail's t)
 };
 int mnist_f32_fc1_splits();
 int mnist_f32_wg2_splits(int B);

@@ -113,3 +113,31 @@ def test_fp32_adam_training_tracks_oracle_and_evaluates(cuda):
         ref_loss = torch.nn.functional.cross_entropy(logits, ys[0].long(), reduction="sum").item()
         ref_correct = int((logits.argmax(1) == ys[0].long()).sum())
     assert abs(float(ev[0]) - ref_loss) / ref_loss < 1e-4 and int(ev[1]) == ref_correct
+
+
+def test_fp32_fused_adam_tail_matches_unfused(cuda):
+    """One GPU + Adam: the fused tail (slab reduce + Adam over every region + step bump in one
+    kernel, t from the head) against slab reduce + the flat Adam kernel: same update up to the
+    slab summation order (fp32)."""
+    B = 128
+    g = torch.Generator().manual_seed(11)
+    xs = torch.rand(3, B, 784, generator=g)
+    ys = torch.randint(0, 10, (3, B), generator=g, dtype=torch.int32)
+    p0 = M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(5).items()})
+    out = []
+    for fused in (0, 1):
+        eng = _engine(B, cuda, 0.75)
+        eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+        eng.set_fused_tail(fused)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            eng.params().copy_(p0.to(cuda))
+            eng.sync_shadow()
+            for i in range(3):
+                eng.feed_x().copy_(xs[i].to(cuda))
+                eng.feed_y().copy_(ys[i].to(cuda))
+                eng.train_step()
+        torch.cuda.synchronize()
+        assert int(eng.step_tensor().item()) == 3
+        out.append(eng.params().cpu() - p0)
+    assert _relerr(out[1].double(), out[0].double()) < 1e-5
