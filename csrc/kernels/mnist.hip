@@ -1529,9 +1529,16 @@ __global__ __launch_bounds__(256) void conv2_wgrad_k(MnistStepArgs a, int kper) 
 // w >> 2, co-tile w & 3 and every tap of its group. One fp32 slab per image pair (rows of its tap
 // group; tap group 0 also the bias row 800), reduced by the optimizer tail / reduce_conv_grads.
 // Replaces the im2col GEMM that re-read p1 25x through L2 (83 MB -> 19 MB of staging).
-constexpr int C2WL_IMG = 2;                 // images per block
-constexpr int C2WL_NTG = 4;                 // tap groups: [0,6) [6,12) [12,18) [18,25)
-constexpr int C2WL_MAXT = 7;
+#ifndef TFD_C2WL_IMG
+#define TFD_C2WL_IMG 2
+#endif
+#ifndef TFD_C2WL_NTG
+#define TFD_C2WL_NTG 4
+#endif
+constexpr int C2WL_IMG = TFD_C2WL_IMG;      // images per block (= slab count B / C2WL_IMG)
+constexpr int C2WL_NTG = TFD_C2WL_NTG;      // tap groups (4: [0,6) [6,12) [12,18) [18,25))
+constexpr int C2WL_TPG = 25 / C2WL_NTG;     // taps per group (the last takes the remainder)
+constexpr int C2WL_MAXT = 25 - C2WL_TPG * (C2WL_NTG - 1);
 constexpr int C2WL_CS = 48, C2WL_PW = 18;   // padded image: 18 x 18 positions x 48-ch stride
                                             // (A tr-reads: 2296 LDS cycles per image vs 2968 at 40)
 constexpr int C2WL_DS = 72, C2WL_KP = 224;  // dz2 rows: pixels padded to 7 k-steps of 32
@@ -1545,7 +1552,7 @@ __global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) {
   bf16* dz = img + C2WL_IMG_ELEMS;
   float* bred = reinterpret_cast<float*>(smem_raw + C2WL_BRED_OFF);  // [8][64]
   const int tg = blockIdx.x % C2WL_NTG, ip = blockIdx.x / C2WL_NTG, t = threadIdx.x;
-  const int tap0 = tg * 6, ntaps = (tg == C2WL_NTG - 1) ? 25 - tap0 : 6;
+  const int tap0 = tg * C2WL_TPG, ntaps = (tg == C2WL_NTG - 1) ? 25 - tap0 : C2WL_TPG;
   const int lane = t & 63, w = t >> 6, h = w >> 2, n = w & 3, g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
   // the image border and the dz2 pad rows stay zero for every image of the block
   for (int i = t; i < C2WL_PW * C2WL_PW; i += 512) {
