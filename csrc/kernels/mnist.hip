@@ -992,23 +992,35 @@ struct UnpoolEpi {
 #ifndef TFD_FDX_RS  // register stages of the long-K (1024) fc1 dX blocks
 #define TFD_FDX_RS 1  // with BK 128: 8 K-steps, A/B vs RS 2 -1.3 us/step
 #endif
-constexpr int FDX_BM = 32, FDX_BN = 64, FDX_BK = TFD_FDX_BK;
+// fc1 dX tile width: 64 (196 blocks at B = 128) inside the fused fc backward, where the dX tiles
+// share the launch with ~800 dW tiles; 32 (392 blocks) when dX runs alone (DP step, part 2), where
+// 196 blocks left a quarter of the CUs idle (A/B: one GPU 64 better by 1.3 us, DP 32 better by 1.5)
+#ifndef TFD_FDX_BN
+#define TFD_FDX_BN 64
+#endif
+#ifndef TFD_FDX_BN_ALONE
+#define TFD_FDX_BN_ALONE 32
+#endif
+constexpr int FDX_BM = 32, FDX_BN = TFD_FDX_BN, FDX_BK = TFD_FDX_BK, FDX_BN2 = TFD_FDX_BN_ALONE;
+template <int BN = FDX_BN>
 __device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   DenseLoader<true> la{a.dh, HID, a.B, HID};
   DenseLoader<true> lb{a.pbf + OFF_WD1, HID, FEAT, HID};
   UnpoolEpi epi{a.p2, a.idx2, a.dz2, a.B};
-  gemm_block<FDX_BM, FDX_BN, FDX_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_FDX_RS>(la, lb, epi, by * FDX_BM, bx * FDX_BN, 0, HID, smem);
+  gemm_block<FDX_BM, BN, FDX_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_FDX_RS>(la, lb, epi, by * FDX_BM, bx * BN, 0, HID, smem);
 }
 
 // K8 + K10: every fc-layer gradient in ONE launch (horizontal fusion of three independent
 // products that all consume dH / dlogits): [fc1 dW tiles | fc1 dX tiles | out dW/db blocks].
 constexpr int FDW_GX = HID / FDW_BN, FDW_GY = (FEAT + 1 + FDW_BM - 1) / FDW_BM;  // 16 x 50
-constexpr int FDX_GX = FEAT / FDX_BN;                                             // 49
+constexpr int FDX_GX = FEAT / FDX_BN;                                             // 49 at BN 64
+constexpr int FDX_GX2 = FEAT / FDX_BN2;
+static_assert(FEAT % FDX_BN == 0 && FEAT % FDX_BN2 == 0, "fc1 dX tiles cover the 3136 features exactly");
 // part 0: all three products; part 1: dW + out-layer grads (bucket A complete); part 2: dX only.
 __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int part) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   int id = blockIdx.x;
-  if (part == 2) { fc1_dx_block(a, id % FDX_GX, id / FDX_GX, (bf16*)smem_raw); return; }
+  if (part == 2) { fc1_dx_block<FDX_BN2>(a, id % FDX_GX2, id / FDX_GX2, (bf16*)smem_raw); return; }
 #if TFD_OUTG_FIRST
   // the 17 output-layer blocks each walk the whole batch: dispatched first, their latency hides
   // under the GEMM tiles instead of forming the kernel's tail.
@@ -1992,7 +2004,7 @@ void mnist_backward_a(const MnistStepArgs& a, hipStream_t s, int part) {
   const int sm = std::max(std::max(sm_dw, sm_dx), sm_og);
   set_smem<fc1_bwd>(sm);
   const int n_dx = FDX_GX * ((B + FDX_BM - 1) / FDX_BM);
-  const int nb = part == 2 ? n_dx : FDW_GX * FDW_GY + (part == 0 ? n_dx : 0) + OUTG_BLOCKS;
+  const int nb = part == 2 ? FDX_GX2 * ((B + FDX_BM - 1) / FDX_BM) : FDW_GX * FDW_GY + (part == 0 ? n_dx : 0) + OUTG_BLOCKS;
   fc1_bwd<<<nb, 256, sm, s>>>(a, n_dx, part);
 }
 
