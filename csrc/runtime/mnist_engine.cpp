@@ -710,20 +710,33 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipEventRecord(ev_done_, comm_stream_));
     HIP_OK(hipStreamWaitEvent(s, ev_ag_, 0));
     mnist_fc_grad_sfb(a, s);  // beside the conv bucket's all-reduce
-    HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
     const int64_t* t = (const int64_t*)tnext_.data_ptr();
+    // With real peers the conv bucket's all-reduce can outlast the SFB GEMM (at 8 ranks the ZeRO
+    // GEMM is ~4 us): the fc-region optimizer (its gradients are local) then runs first and covers
+    // it, and only the small conv region waits for the collective. At world 1 (the rehearsal) the
+    // collective is instant and one launch is cheaper.
+    const bool split_opt = world() > 1;
+    if (!split_opt) HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
     if (shard) {
       const int64_t beg[3] = {0, OFF_WD1 + rk * zshard_, OFF_BD1};
       const int64_t end[3] = {BUCKET_SPLIT, OFF_WD1 + (rk + 1) * zshard_, TOTAL};
-      if (opt_ == 0 && BUCKET_SPLIT % 4 == 0 && zshard_ % 4 == 0) {  // one launch over the three ranges
+      if (opt_ == 0 && BUCKET_SPLIT % 4 == 0 && zshard_ % 4 == 0) {  // one launch over the ranges
         const int64_t n[3] = {end[0] - beg[0], end[1] - beg[1], end[2] - beg[2]};
         AdamArgs o{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(),
                    (const float*)grad_.data_ptr(), (uint16_t*)pbf_.data_ptr(),
                    bf16_comm_ ? (const uint16_t*)gbf_.data_ptr() : nullptr, 0, (float)lr_, (float)b1_, (float)b2_,
                    (float)eps_, t, 0, (float)scale};
-        adam_apply_ranges(o, 3, beg, n, s);
+        if (split_opt) {
+          adam_apply_ranges(o, 2, beg + 1, n + 1, s);
+          HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+          adam_apply_ranges(o, 1, beg, n, s);
+        } else {
+          adam_apply_ranges(o, 3, beg, n, s);
+        }
       } else {
-        for (int k = 0; k < 3; ++k) apply_optimizer_range(beg[k], end[k], scale, 0, s, t);
+        for (int k = 1; k < 3; ++k) apply_optimizer_range(beg[k], end[k], scale, 0, s, t);
+        if (split_opt) HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+        apply_optimizer_range(beg[0], end[0], scale, 0, s, t);
       }
       pending_wag_ = true;
       if (join_end) {  // the caller reads whole weights after this step: gather the shards now
@@ -734,6 +747,10 @@ class MnistEngine : public torch::CustomClassHolder {
         HIP_OK(hipStreamWaitEvent(s, ev_wag_, 0));
         pending_wag_ = false;
       }
+    } else if (split_opt) {
+      apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 0, s, t);
+      HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+      apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s, t);
     } else {
       apply_optimizer_range(0, TOTAL, scale, 0, s, t);
     }
