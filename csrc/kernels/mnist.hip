@@ -1001,13 +1001,16 @@ struct UnpoolEpi {
 #ifndef TFD_FDX_BN_ALONE
 #define TFD_FDX_BN_ALONE 32
 #endif
+#ifndef TFD_FDX_RS_ALONE
+#define TFD_FDX_RS_ALONE 2  // dX alone (DP): 2 register stages, A/B -0.3 us (profiles/ab_fc1_dx_tiles_r2.log)
+#endif
 constexpr int FDX_BM = 32, FDX_BN = TFD_FDX_BN, FDX_BK = TFD_FDX_BK, FDX_BN2 = TFD_FDX_BN_ALONE;
-template <int BN = FDX_BN>
+template <int BN = FDX_BN, int RS = TFD_FDX_RS>
 __device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   DenseLoader<true> la{a.dh, HID, a.B, HID};
   DenseLoader<true> lb{a.pbf + OFF_WD1, HID, FEAT, HID};
   UnpoolEpi epi{a.p2, a.idx2, a.dz2, a.B};
-  gemm_block<FDX_BM, BN, FDX_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_FDX_RS>(la, lb, epi, by * FDX_BM, bx * BN, 0, HID, smem);
+  gemm_block<FDX_BM, BN, FDX_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), RS>(la, lb, epi, by * FDX_BM, bx * BN, 0, HID, smem);
 }
 
 // K8 + K10: every fc-layer gradient in ONE launch (horizontal fusion of three independent
@@ -1020,7 +1023,7 @@ static_assert(FEAT % FDX_BN == 0 && FEAT % FDX_BN2 == 0, "fc1 dX tiles cover the
 __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int part) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   int id = blockIdx.x;
-  if (part == 2) { fc1_dx_block<FDX_BN2>(a, id % FDX_GX2, id / FDX_GX2, (bf16*)smem_raw); return; }
+  if (part == 2) { fc1_dx_block<FDX_BN2, TFD_FDX_RS_ALONE>(a, id % FDX_GX2, id / FDX_GX2, (bf16*)smem_raw); return; }
 #if TFD_OUTG_FIRST
   // the 17 output-layer blocks each walk the whole batch: dispatched first, their latency hides
   // under the GEMM tiles instead of forming the kernel's tail.
