@@ -997,12 +997,16 @@ class MnistEngine : public torch::CustomClassHolder {
       ipc_->reduce_scatter_raw(in, pre, out, bf16_comm_, S, 1.0, st);
     }
   }
+  // The updated bf16 fc1 shards -> every rank. Through the IPC one-shot all-gather (every rank reads
+  // all peers' shards at once over all xGMI links) when its staging holds a shard -- at 8 ranks the
+  // 0.8 MB shard exactly fills the staging sized for the SFB p2 gather -- else RCCL's all-gather.
   void ag_w(hipStream_t st) {
     const int64_t r = rank_in_comm();
     const int64_t S = zshard_;
     uint16_t* pb = (uint16_t*)pbf_.data_ptr() + OFF_WD1;
-    if (comm_) comm_->all_gather_raw(pb + r * S, pb, (size_t)S, ncclBfloat16, st);
-    else ipc_->all_gather_raw(pb, 2, S, st);
+    if (ipc_ && ipc_->capacity() * 2 >= S) ipc_->all_gather_raw(pb, 2, S, st);
+    else if (comm_) comm_->all_gather_raw(pb + r * S, pb, (size_t)S, ncclBfloat16, st);
+    else TORCH_CHECK(false, "ZeRO weight gather: no communicator holds a ", S, "-element shard");
   }
 
   bool sfb_active() const { return sfb_ && !fp32_ && dp() && sfp2_.defined(); }
