@@ -61,8 +61,9 @@ def main(argv=None):
     ap.add_argument("--conv_fork", type=int, default=0, help="1: conv2 wgrad on a forked stream beside dgrad")
     ap.add_argument("--zero", type=int, default=-1, help="1: ZeRO-1 sharding of the fc1 weight (N > 1): with "
                     "--fc_sfb each rank forms only its shard's fc1 gradient and updates only that shard, the bf16 "
-                    "shards are all-gathered beside the next conv forward; -1 (default): on from 8 ranks up, where "
-                    "the K = N*B fc GEMM would otherwise cost more than the 0.8 MB/link weight gather")
+                    "shards are all-gathered (IPC one-shot) beside the next conv forward; -1 (default): on from 4 "
+                    "ranks up, where the K = N*B fc GEMM and the full fc Adam (~28 us at N = 4) would otherwise "
+                    "cost more than the 1.6 MB/peer weight gather that hides behind the conv forward")
     ap.add_argument("--fc_sfb", type=int, default=1, help="1 (N > 1 or --force_dp): fc-region gradients by "
                     "sufficient-factor broadcasting -- all-gather the fc factors (1.33 MB/rank) and form the summed "
                     "fc gradient locally instead of all-reducing it (6.4 MB); 0: bucketed all-reduce")
@@ -121,10 +122,10 @@ def main(argv=None):
     if mode == "auto":
         mode = "ipc" if ctx.shared_device else "rccl"
     if a.zero < 0:
-        a.zero = 1 if (world >= 8 and a.dtype == "bf16") else 0
+        a.zero = 1 if (world >= 4 and a.dtype == "bf16") else 0
     tr = attach_engine(eng, rank, world, dev, mode=mode, comm=ctx.comm, bf16=not a.fp32_grads,
                        small_ipc=bool(a.ipc_small), force_dp=bool(a.force_dp),
-                       sfb=bool(a.fc_sfb) and a.dtype == "bf16")
+                       sfb=bool(a.fc_sfb) and a.dtype == "bf16", zero=bool(a.zero))
     if a.zero:
         eng.set_zero(True)
     s = torch.cuda.Stream(dev)

@@ -98,7 +98,7 @@ class DPTransport:
 def attach_engine(eng, rank: int, world: int, device: torch.device, group=None, src: int = 0,
                   mode: str = "auto", comm=None, bf16: bool = True, small_ipc: bool = True,
                   force_dp: bool = False, capacity: Optional[int] = None, log=None,
-                  sfb: bool = False) -> DPTransport:
+                  sfb: bool = False, zero: bool = False) -> DPTransport:
     """Give ``eng`` (``MnistEngine``) its gradient transport.
 
     mode: ``auto`` (IPC everywhere when ranks share a GPU, else RCCL + IPC small bucket),
@@ -106,7 +106,9 @@ def attach_engine(eng, rank: int, world: int, device: torch.device, group=None, 
     runs the full DP schedule over a world-1 communicator (one-GPU coverage of the RCCL path).
     ``sfb``: fc-region gradients by sufficient-factor broadcasting (``MnistEngine.set_fc_sfb``: the
     fc factors are all-gathered -- over IPC when its staging holds them -- instead of all-reducing
-    the 6.4 MB fc gradient).
+    the 6.4 MB fc gradient). ``zero``: the engine will shard fc1 (``set_zero``); the IPC staging is
+    sized to hold one bf16 fc1 shard too, so the per-step weight all-gather takes the IPC one-shot
+    path (every peer read at once) instead of RCCL's ring.
     """
     from ..models import mnist_cnn as M
     from .ipc import make_ipc_comm
@@ -120,6 +122,8 @@ def attach_engine(eng, rank: int, world: int, device: torch.device, group=None, 
     cap = capacity or M.TOTAL
     # IPC staging (fp32 units) that also holds one SFB gather shard (bf16 elements)
     small_cap = max(M.BUCKET_SPLIT, (int(eng.sfb_shard_elems()) + 1) // 2) if sfb else M.BUCKET_SPLIT
+    if zero and world > 1:  # one bf16 fc1 shard (MnistEngine.set_zero: zshard = |wd1| / world)
+        small_cap = max(small_cap, (M.FEAT * M.HID // world + 1) // 2)
 
     def _sfb(tr: DPTransport) -> DPTransport:
         if sfb and bf16:

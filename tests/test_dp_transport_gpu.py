@@ -246,6 +246,14 @@ def test_bench_two_ranks_one_gpu_over_ipc(cuda, sfb, zero):
     assert r["phases_ms"]["allreduce"] > 0, r["phases_ms"]
 
 
+def test_bench_four_ranks_default_zero(cuda):
+    """From 4 ranks bench.py's default adds ZeRO-1 on top of the sufficient factors (the fc1 shard
+    all-gather rides the IPC staging)."""
+    r = _bench(["--gpus", "4", "--steps", "10", "--warmup", "3", "--min_warmup_ms", "50"], nproc=4)
+    assert r["config"]["zero1_fc1"] and r["config"]["dp_transport"] == "ipc+sfb" and r["n_gpus"] == 4
+    assert r["value"] > 0 and r["config"]["global_batch"] == 512
+
+
 def test_bench_fp32_dtype(cuda):
     r = _bench(["--steps", "20", "--warmup", "5", "--dtype", "fp32", "--min_warmup_ms", "50"])
     assert r["dtype"] == "fp32" and r["config"]["grad_allreduce"] == "fp32" and r["value"] > 0
