@@ -675,7 +675,7 @@ class MnistEngine : public torch::CustomClassHolder {
       a.gbf_b = (uint16_t*)gbf_.data_ptr();
     }
     mark(P_START, s);
-    if (shard && pending_wag_) {  // last step's updated fc1 bf16 shards -> every rank, beside the conv forward
+    if (shard && pending_wag_ && !wag_issued_) {  // last step's fc1 bf16 shards -> every rank, beside the conv fwd
       HIP_OK(hipEventRecord(ev_start_, s));
       HIP_OK(hipStreamWaitEvent(comm_stream_, ev_start_, 0));
       ag_w(comm_stream_);
@@ -688,7 +688,7 @@ class MnistEngine : public torch::CustomClassHolder {
     gather_sfb(true, comm_stream_);
     if (shard && pending_wag_) {
       HIP_OK(hipStreamWaitEvent(s, ev_wag_, 0));
-      pending_wag_ = false;
+      pending_wag_ = wag_issued_ = false;
     }
     mnist_forward_fc(a, true, s);
     mark(P_FWD, s);
@@ -728,6 +728,13 @@ class MnistEngine : public torch::CustomClassHolder {
                    (float)eps_, t, 0, (float)scale};
         if (split_opt) {
           adam_apply_ranges(o, 2, beg + 1, n + 1, s);
+          // the updated shard can leave now: the gather queues behind the conv bucket's all-reduce on
+          // the comm stream and runs beside the conv-region Adam and the next conv forward
+          HIP_OK(hipEventRecord(ev_start_, s));
+          HIP_OK(hipStreamWaitEvent(comm_stream_, ev_start_, 0));
+          ag_w(comm_stream_);
+          HIP_OK(hipEventRecord(ev_wag_, comm_stream_));
+          wag_issued_ = true;
           HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
           adam_apply_ranges(o, 1, beg, n, s);
         } else {
@@ -740,12 +747,14 @@ class MnistEngine : public torch::CustomClassHolder {
       }
       pending_wag_ = true;
       if (join_end) {  // the caller reads whole weights after this step: gather the shards now
-        HIP_OK(hipEventRecord(ev_start_, s));
-        HIP_OK(hipStreamWaitEvent(comm_stream_, ev_start_, 0));
-        ag_w(comm_stream_);
-        HIP_OK(hipEventRecord(ev_wag_, comm_stream_));
+        if (!wag_issued_) {
+          HIP_OK(hipEventRecord(ev_start_, s));
+          HIP_OK(hipStreamWaitEvent(comm_stream_, ev_start_, 0));
+          ag_w(comm_stream_);
+          HIP_OK(hipEventRecord(ev_wag_, comm_stream_));
+        }
         HIP_OK(hipStreamWaitEvent(s, ev_wag_, 0));
-        pending_wag_ = false;
+        pending_wag_ = wag_issued_ = false;
       }
     } else if (split_opt) {
       apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 0, s, t);
@@ -1168,6 +1177,7 @@ class MnistEngine : public torch::CustomClassHolder {
   bool zero_ = false;
   bool dp_serial_ = true;    // train_step_sfb_serial (default) vs the overlapped train_step_sfb
   bool pending_wag_ = false;  // serialized ZeRO: this step's shards not yet all-gathered
+  bool wag_issued_ = false;   // ... their all-gather already queued on the comm stream (ev_wag_)
   bool force_dp_ = false;
   int64_t zshard_ = 0;
   bool pending_opt_a_ = false;  // DP: the main stream still has to wait for the fc optimizer
