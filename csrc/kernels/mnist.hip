@@ -712,10 +712,28 @@ __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   do {                                                                                                   \
     if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[4 * a.B * 8 + blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
   } while (0)
+#ifndef TFD_HEAD_PREF  // 1: the thread's 4 output-layer rows (40 floats) as 10 16-B loads issued first
+#define TFD_HEAD_PREF 0
+#endif
 __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   HEAD_STAMP(0);
   const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n0 = 4 * t;
+#if TFD_HEAD_PREF
+  float wreg[4 * NCLS];  // rows n0..n0+3 of the [1024][10] output weight are 40 contiguous floats
+  {
+    const f32x4* src = reinterpret_cast<const f32x4*>(a.p32 + OFF_OUT + (size_t)n0 * NCLS);
+#pragma unroll
+    for (int q = 0; q < NCLS; ++q) {
+      const f32x4 v = src[q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wreg[4 * q + e] = v[e];
+    }
+  }
+#define HEAD_W(j, c) wreg[(j) * NCLS + (c)]
+#else
+#define HEAD_W(j, c) (a.p32 + OFF_OUT)[(size_t)(n0 + (j)) * NCLS + (c)]
+#endif
   if (a.t_out && row == 0 && t == 0) *a.t_out = *a.step + 1;
   // the label's dependent chain (step -> perm -> label) starts first, hidden behind the fc1 math
   const int lbl = batch_label(a, row);
@@ -743,15 +761,13 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) hd[j] = fmaxf(h[j], 0.f) * scale[j];
   // logits partials
-  const float* wout = a.p32 + OFF_OUT;
   float lp[NCLS];
 #pragma unroll
   for (int c = 0; c < NCLS; ++c) lp[c] = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float* wr = wout + (size_t)(n0 + j) * NCLS;
 #pragma unroll
-    for (int c = 0; c < NCLS; ++c) lp[c] = fmaf(hd[j], wr[c], lp[c]);
+    for (int c = 0; c < NCLS; ++c) lp[c] = fmaf(hd[j], HEAD_W(j, c), lp[c]);
   }
   HEAD_STAMP(2);
   __shared__ float red[4][NCLS];
@@ -790,12 +806,12 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   float dhv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float* wr = wout + (size_t)(n0 + j) * NCLS;
     float d = 0.f;
 #pragma unroll
-    for (int c = 0; c < NCLS; ++c) d = fmaf(dl[c], wr[c], d);
+    for (int c = 0; c < NCLS; ++c) d = fmaf(dl[c], HEAD_W(j, c), d);
     dhv[j] = (h[j] > 0.f) ? d * scale[j] : 0.f;
   }
+#undef HEAD_W
   hdw[0] = pack_bf2(hd[0], hd[1]); hdw[1] = pack_bf2(hd[2], hd[3]);
   dhw[0] = pack_bf2(dhv[0], dhv[1]); dhw[1] = pack_bf2(dhv[2], dhv[3]);
   *reinterpret_cast<uint2*>(a.hd + (size_t)row * HID + n0) = make_uint2(hdw[0], hdw[1]);
