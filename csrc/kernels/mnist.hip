@@ -713,7 +713,7 @@ __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
     if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[4 * a.B * 8 + blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
   } while (0)
 #ifndef TFD_HEAD_DPP  // 1: the logits' wave sums by DPP instead of __shfl_xor (ds_bpermute) chains
-#define TFD_HEAD_DPP 0
+#define TFD_HEAD_DPP 1
 #endif
 #ifndef TFD_HEAD_PREF  // 1: the thread's 4 output-layer rows (40 floats) as 10 16-B loads issued first
 #define TFD_HEAD_PREF 0
