@@ -2,7 +2,10 @@
 N MI355X (BASELINE.json metric; reference config: per-worker batch 128, Adam lr 0.01,
 keep_prob 0.75 -- /root/reference/mnist_python_m.py:62-71,205-222).
 
-One process per GPU (torchrun env). Each step = fused HIP forward + backward + bucketed RCCL
+One process per GPU: under torchrun the env says which rank this is; without a launcher
+environment, ``--gpus N`` (N > 1) makes this process spawn the N ranks itself (parallel/spawn.py:
+the parent never touches the GPU, relays rank 0's JSON line and fails if any rank fails), and a
+job whose WORLD_SIZE differs from --gpus exits non-zero. Each step = fused HIP forward + backward + bucketed RCCL
 gradient all-reduce (sum, 1/N folded into Adam) + fused flat Adam, with every kernel and
 collective captured into ONE hipGraph that is replayed per step. Data is a device-resident
 synthetic MNIST-shaped split (55000 x 784 fp32 in [0,1], random labels) indexed by a per-rank
@@ -88,7 +91,13 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu", action="store_true", help="plumbing dry-run: fp32 PyTorch CPU runner + Gloo "
                     "(exercises the launcher/barrier/JSON contract without a GPU; not a performance number)")
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = ap.parse_args(argv)
+    from tensorflow_distributed_amd.parallel import spawn
+
+    if spawn.needs_self_launch(a.gpus):
+        # no launcher environment: this process only spawns the N ranks (it never touches the GPU)
+        return spawn.self_launch(os.path.abspath(__file__), argv, a.gpus)
     if a.cpu:
         return _cpu_dry_run(a)
 
@@ -101,8 +110,7 @@ def main(argv=None):
     _native.require()
     ctx = D.init_from_env(use_gpu=True)
     world, rank = ctx.world, ctx.rank
-    if world != a.gpus and rank == 0:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    spawn.check_world(a.gpus, world)
     dev = ctx.device
     B = a.batch_size
     eng = torch.classes.tfd.MnistEngine(B, dev.index, 0.75, a.seed, rank)
@@ -236,6 +244,7 @@ def main(argv=None):
             eng.sync_params()
     dt = ctx.max_scalar(dt)
     tr.check("after the timed steps")
+    topo = _job_topology(ctx, dev, tr, eng)
     phases = _phase_breakdown(eng, s, graph_mode, world, ctx) if a.phases else None
     if loss0 is None:
         loss0 = float(loss0_t.item())
@@ -262,6 +271,7 @@ def main(argv=None):
             "dtype": a.dtype,
             "data": "synthetic (device-resident MNIST-shaped 55000x784, random labels; random N(0,1) init)",
             "phases_ms": phases,
+            **topo,
             "config": {
                 "model": "MNIST 2-conv CNN (reference conv_net: conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout0.75-fc10), "
                          "Adam lr 0.01",
@@ -285,6 +295,36 @@ def main(argv=None):
     tr.close()
     ctx.shutdown()
     return 0
+
+
+def _job_topology(ctx, dev, tr, eng):
+    """What the job really ran on, for the JSON: the communicator's own world size, every rank's
+    device (index + PCI bus / uuid), and whether the replicas' parameters are bit-identical after
+    the timed steps (sha1 of each rank's flat fp32 master, compared on rank 0)."""
+    import hashlib
+
+    import torch
+
+    from tensorflow_distributed_amd.parallel.transport import device_label
+
+    comm_world = 1
+    if tr.comm is not None:
+        comm_world = int(tr.comm.world())
+    elif tr.ipc is not None:
+        comm_world = int(tr.ipc.world())
+    torch.cuda.synchronize(dev)
+    digest = hashlib.sha1(eng.params().detach().cpu().numpy().tobytes()).hexdigest()[:16]
+    mine = {"rank": ctx.rank, "device": device_label(dev), "params_sha1": digest}
+    if ctx.world > 1:
+        import torch.distributed as dist
+
+        rows = [None] * ctx.world
+        dist.all_gather_object(rows, mine)
+    else:
+        rows = [mine]
+    return {"comm_world": comm_world, "devices": [r["device"] for r in rows],
+            "replicas_identical": len({r["params_sha1"] for r in rows}) == 1,
+            "params_sha1": rows[0]["params_sha1"]}
 
 
 def _phase_breakdown(eng, stream, graph_mode, world, ctx):
@@ -326,8 +366,11 @@ def _cpu_dry_run(a):
     from tensorflow_distributed_amd.parallel.sync_replicas import SyncReplicasStepper, broadcast_state
     from tensorflow_distributed_amd.training.optimizers import AdamOptimizer
 
+    from tensorflow_distributed_amd.parallel import spawn
+
     ctx = D.init_from_env(use_gpu=False)
     world, rank = ctx.world, ctx.rank
+    spawn.check_world(a.gpus, world)
     r = TorchMnistRunner(a.batch_size, AdamOptimizer(a.lr), keep_prob=0.75, seed=a.seed, rank=rank)
     if rank == 0:
         r.load_flat(M.flat_from_dict(M.init_params(a.seed)), {}, 0)

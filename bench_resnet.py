@@ -1,7 +1,8 @@
 """Convnet-at-scale benchmark for BASELINE.json configs 4-5: synthetic 224x224x3 ResNet-18 /
 ResNet-50 (v1.5, bf16, NHWC) data-parallel training, images/sec (whole node).
 
-One process per GPU (torchrun env), native HIP conv/BN/pool kernels, bucketed RCCL gradient
+One process per GPU (torchrun env, or self-launched: ``--gpus N`` without a launcher environment
+spawns the N ranks from a GPU-clean parent, see parallel/spawn.py), native HIP conv/BN/pool kernels, bucketed RCCL gradient
 all-reduce overlapped with the backward, fused flat SGD-momentum, the whole step captured in a
 hipGraph and replayed. Synthetic data: one fixed device-resident random batch per rank.
 
@@ -38,7 +39,12 @@ def main(argv=None):
     ap.add_argument("--fuse_joins", type=int, default=1, help="1: residual-join gradient sums in the dgrad "
                     "epilogue (0: autograd adds; measured faster, see resnet.GradJoin)")
     ap.add_argument("--lr", type=float, default=0.1)
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = ap.parse_args(argv)
+    from tensorflow_distributed_amd.parallel import spawn
+
+    if spawn.needs_self_launch(a.gpus):
+        return spawn.self_launch(os.path.abspath(__file__), argv, a.gpus)
 
     import torch
 
@@ -48,15 +54,28 @@ def main(argv=None):
 
     _native.require()
     ctx = D.init_from_env(use_gpu=True)
+    spawn.check_world(a.gpus, ctx.world)
     dev = ctx.device
     m = ResNet(a.depth, num_classes=1000, device=dev, seed=0, fuse_joins=bool(a.fuse_joins),
                bn_stats=bool(a.bn_stats))
     m.mask_from_y = bool(a.mask_from_y)
     m.relu_bits = bool(a.relu_bits)
-    if ctx.comm is not None:
-        ctx.comm.broadcast(m.fp.master, 0)
+    comm, transport = None, "none"
+    if ctx.world > 1:
+        if ctx.comm is not None:  # one rank per GPU: RCCL over xGMI
+            comm, transport = ctx.comm, "rccl"
+            comm.broadcast(m.fp.master, 0)
+        elif ctx.shared_device:  # ranks share a GPU (RCCL refuses that): the IPC transport
+            from tensorflow_distributed_amd.parallel.ipc import IpcCollectives, make_ipc_comm
+
+            comm, transport = IpcCollectives(make_ipc_comm(ctx.rank, ctx.world, dev.index, m.fp.total)), "ipc"
+            host = m.fp.master.detach().cpu()
+            ctx.broadcast_tensor_cpu(host, 0)  # chief init -> every rank over Gloo
+            m.fp.master.copy_(host.to(dev))
+        else:
+            raise RuntimeError(f"world {ctx.world} but no gradient transport: refusing to report non-DP throughput")
         m.fp.shadow.copy_(m.fp.master)
-        m.set_comm(ctx.comm, a.bucket_mb)
+        m.set_comm(comm, a.bucket_mb)
     g = torch.Generator(device=dev).manual_seed(100 + ctx.rank)
     x = torch.randn(a.batch_size, a.image, a.image, 3, device=dev, generator=g)
     y = torch.randint(0, 1000, (a.batch_size,), device=dev, generator=g, dtype=torch.int32)
@@ -92,6 +111,7 @@ def main(argv=None):
     ctx.barrier()
     dt = ctx.max_scalar(time.perf_counter() - t0)
     img_s = ctx.world * a.batch_size * a.steps / dt
+    topo = _topology(ctx, dev, comm, m)
     if ctx.rank == 0:
         print(f"# resnet{a.depth} world={ctx.world} B/gpu={a.batch_size} loss={float(loss):.3f} "
               f"{dt * 1e3 / a.steps:.2f} ms/step", file=sys.stderr)
@@ -101,13 +121,44 @@ def main(argv=None):
             "warmup": a.warmup, "ms_per_step": round(dt * 1e3 / a.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": f"synthetic (random {a.image}x{a.image}x3 fp32 images, random labels; He init)",
+            **topo,
             "config": {"model": f"resnet{a.depth} v1.5 NHWC", "global_batch": ctx.world * a.batch_size,
                        "per_gpu_batch": a.batch_size, "seq_len": None, "parallelism": f"dp{ctx.world}",
+                       "dp_transport": transport,
                        "bucket_mb": a.bucket_mb, "optimizer": "sgd-momentum 0.9 wd 1e-4",
                        "hipgraph": not a.eager, "fuse_joins": bool(a.fuse_joins), "bn_stats": bool(a.bn_stats),
                        "mask_from_y": bool(a.mask_from_y), "relu_bits": bool(a.relu_bits)}}), flush=True)
+    if transport == "ipc":
+        if comm.ipc.error():
+            raise RuntimeError("IPC collective barrier timed out: replicas may have diverged")
+        comm.ipc.close()
     ctx.shutdown()
+    if not topo["replicas_identical"]:
+        print("error: DP replicas diverged (parameter digests differ across ranks)", file=sys.stderr)
+        return 3
     return 0
+
+
+def _topology(ctx, dev, comm, m):
+    """comm world as the transport reports it, every rank's device, and whether the replicas'
+    fp32 master weights are bit-identical after the timed steps."""
+    import hashlib
+
+    import torch
+
+    from tensorflow_distributed_amd.parallel.transport import device_label
+
+    torch.cuda.synchronize(dev)
+    mine = {"device": device_label(dev),
+            "sha1": hashlib.sha1(m.fp.master.detach().cpu().numpy().tobytes()).hexdigest()[:16]}
+    rows = [mine]
+    if ctx.world > 1:
+        import torch.distributed as dist
+
+        rows = [None] * ctx.world
+        dist.all_gather_object(rows, mine)
+    return {"comm_world": int(comm.world()) if comm is not None else 1, "devices": [r["device"] for r in rows],
+            "replicas_identical": len({r["sha1"] for r in rows}) == 1, "params_sha1": rows[0]["sha1"]}
 
 
 if __name__ == "__main__":

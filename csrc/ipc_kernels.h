@@ -5,6 +5,12 @@
 // 7 xGMI links in parallel), reduces in fp32 registers and writes the result locally. Cross-rank
 // ordering uses per-block START/END flag barriers in uncached (fine-grained) signal memory with
 // system-scope release/acquire; every spin is time-bounded (error flag instead of a hang).
+//
+// Single-stream requirement: the collectives of one communicator share its two staging halves,
+// its call counter and its arrival ticket, so two of them must never be in flight at once. The
+// host side (IpcComm::order/mark, csrc/runtime/ipc_comm.cpp) makes a launch on a new stream wait
+// for the previous launch; inside a captured graph the capture order on the engine's one comm
+// stream provides it.
 #pragma once
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>

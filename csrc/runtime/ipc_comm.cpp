@@ -37,6 +37,7 @@ IpcComm::IpcComm(int64_t world, int64_t rank, int64_t device, int64_t capacity_e
   HIP_OK2(hipMemset(sig_, 0, kIpcSigInts * sizeof(int)));
   HIP_OK2(hipMemset(stage_, 0, 2 * (size_t)cap_ * sizeof(float)));
   HIP_OK2(hipDeviceSynchronize());
+  HIP_OK2(hipEventCreateWithFlags(&last_ev_, hipEventDisableTiming));
   for (int i = 0; i < kIpcMaxRanks; ++i) {
     peer_stage_[i] = nullptr;
     peer_sig_[i] = nullptr;
@@ -92,6 +93,26 @@ void IpcComm::close() {
     hipFree(sig_);
     sig_ = nullptr;
   }
+  if (last_ev_) {
+    hipEventDestroy(last_ev_);
+    last_ev_ = nullptr;
+  }
+}
+
+static bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  HIP_OK2(hipStreamIsCapturing(s, &st));
+  return st != hipStreamCaptureStatusNone;
+}
+
+void IpcComm::order(hipStream_t s) {
+  if (last_recorded_ && s != last_stream_ && !capturing(s)) HIP_OK2(hipStreamWaitEvent(s, last_ev_, 0));
+}
+
+void IpcComm::mark(hipStream_t s) {
+  last_stream_ = s;
+  last_recorded_ = !capturing(s);
+  if (last_recorded_) HIP_OK2(hipEventRecord(last_ev_, s));
 }
 
 // Grid of a spinning collective: every block of it must become resident while the peers' blocks
@@ -127,7 +148,9 @@ void IpcComm::all_reduce_raw(const void* in, bool in_bf16, void* out, bool out_b
   a.scale = (float)scale;
   a.spin_limit_ticks = spin_ticks_;
   a.half_bytes = cap_ * (int64_t)sizeof(float);
+  order(s);
   ipc_allreduce(a, blocks(n), s);
+  mark(s);
 }
 
 void IpcComm::all_reduce(const at::Tensor& t, double scale) {
@@ -157,7 +180,9 @@ void IpcComm::reduce_scatter_raw(const void* in, bool in_bf16, void* out, bool o
   a.spin_limit_ticks = spin_ticks_;
   a.half_bytes = cap_ * (int64_t)sizeof(float);
   TORCH_CHECK(shard % 8 == 0, "IpcComm.reduce_scatter: shard must be a multiple of 8 elements");
+  order(s);
   ipc_reduce_scatter(a, blocks(shard), s);
+  mark(s);
 }
 
 void IpcComm::all_gather_raw(void* buf, int elem_bytes, int64_t shard, hipStream_t s) {
@@ -176,7 +201,9 @@ void IpcComm::all_gather_raw(void* buf, int elem_bytes, int64_t shard, hipStream
   a.spin_limit_ticks = spin_ticks_;
   a.half_bytes = cap_ * (int64_t)sizeof(float);
   TORCH_CHECK(shard % 8 == 0, "IpcComm.all_gather: shard must be a multiple of 8 elements");
+  order(s);
   ipc_all_gather(a, elem_bytes, blocks(shard), s);
+  mark(s);
 }
 
 void IpcComm::reduce_scatter(const at::Tensor& in, const at::Tensor& out, double scale) {

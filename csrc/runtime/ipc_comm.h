@@ -33,6 +33,16 @@ class IpcComm : public torch::CustomClassHolder {
   int64_t capacity() const { return cap_; }
 
  private:
+  // Every collective of one IpcComm shares the staging halves and the call counter, so they must
+  // execute one after another. order() makes a launch on a stream other than the previous
+  // launch's wait for that launch (an event recorded after it); mark() records that event. Under
+  // hipGraph capture the caller's capture order is the execution order (the engine captures all
+  // of its collectives on one comm stream), so nothing is recorded there.
+  void order(hipStream_t s);
+  void mark(hipStream_t s);
+  hipEvent_t last_ev_ = nullptr;
+  hipStream_t last_stream_ = nullptr;
+  bool last_recorded_ = false;
   int64_t world_, rank_, device_, cap_;
   void* stage_ = nullptr;
   void* sig_ = nullptr;

@@ -25,10 +25,25 @@ def make_ipc_comm(rank: int, world: int, device_index: int, capacity_elems: int,
         # generous: a peer may still be loading code objects on its first call (observed > 2 s when
         # ranks share a GPU); any finite limit keeps a missing peer from hanging the device
         spin_limit_ms = float(os.environ.get("TFD_IPC_SPIN_MS", "30000"))
-    comm = torch.classes.tfd.IpcComm(world, rank, device_index, capacity_elems)
-    comm.set_spin_limit_ms(spin_limit_ms)
-    comm.set_max_blocks(int(max_blocks or 8))
-    h = comm.handle()
+    # local step (allocation + export) first, then agree on its success before the collective
+    # handle exchange: a rank that failed locally must not leave its peers blocked in all_gather
+    comm, h, err = None, None, None
+    try:
+        comm = torch.classes.tfd.IpcComm(world, rank, device_index, capacity_elems)
+        comm.set_spin_limit_ms(spin_limit_ms)
+        comm.set_max_blocks(int(max_blocks or 8))
+        h = comm.handle()
+    except Exception as e:  # noqa: BLE001 - reported on every rank below
+        err = e
+    if world > 1:
+        bad = torch.tensor([1 if err is not None else 0], dtype=torch.int64)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=group)
+        if int(bad.item()):
+            if comm is not None:
+                comm.close()
+            raise IpcSetupError(f"IPC setup failed on at least one rank (here: {err!r})")
+    elif err is not None:
+        raise IpcSetupError(f"IPC setup failed: {err!r}") from err
     if world > 1:
         allh = [torch.zeros_like(h) for _ in range(world)]
         dist.all_gather(allh, h, group=group)
@@ -36,6 +51,10 @@ def make_ipc_comm(rank: int, world: int, device_index: int, capacity_elems: int,
     else:
         comm.open(h.reshape(1, -1))
     return comm
+
+
+class IpcSetupError(RuntimeError):
+    """Raised on EVERY rank when any rank's local IPC setup failed (collective decision)."""
 
 
 class IpcCollectives:

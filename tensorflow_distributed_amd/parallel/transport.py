@@ -37,6 +37,15 @@ def device_key(device: torch.device) -> str:
     return f"{socket.gethostname()}|{uid}" if uid else f"{socket.gethostname()}|{vis}|{idx}"
 
 
+def device_label(device: torch.device) -> str:
+    """Human-readable identity of a rank's GPU for benchmark records: index, PCI bus, uuid."""
+    idx = device.index or 0
+    p = torch.cuda.get_device_properties(idx)
+    bus = getattr(p, "pci_bus_id", None)
+    uid = str(getattr(p, "uuid", "") or "")
+    return f"cuda:{idx}" + (f" pci:{bus}" if bus is not None else "") + (f" uuid:{uid}" if uid else "")
+
+
 def devices_shared(device: torch.device, world: int, group=None) -> bool:
     """True when at least two ranks of ``group`` run on the same GPU (all-gather of device keys)."""
     if world <= 1:

@@ -283,7 +283,10 @@ def main(argv=None) -> int:
         comm = transport.comm
         runner.comm = comm
         runner.transport = transport
-    device_input = device.type == "cuda" and FLAGS.device_input
+    # PS modes overwrite the runner's step with the PS global step after every push, and the device
+    # permutation is indexed by that step: each worker would see ~1/N of its epoch. Those modes keep
+    # the reference's per-worker sequential next_batch (mnist_python_m.py:291) on the host instead.
+    device_input = device.type == "cuda" and FLAGS.device_input and not ps_mode
     if device_input:
         runner.set_device_dataset(mnist.train.images, mnist.train.labels,
                                   seed=FLAGS.seed * 1000 + FLAGS.task_index + 31)

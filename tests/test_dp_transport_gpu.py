@@ -219,15 +219,17 @@ def test_reference_quickstart_two_workers_share_one_gpu(cuda, tmp_path):
     assert all(rec["allreduce_ms"] > 0 and rec["fwd_ms"] > 0 and rec["loss"] > 0 for rec in steps[1:]), steps
 
 
-def _bench(args, nproc=1, timeout=300):
+def _bench(args, nproc=1, timeout=300, script="bench.py", self_launch=False):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    if nproc > 1:
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    if nproc > 1 and not self_launch:
         from dist_util import free_port
 
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py")]
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, script)]
     else:
-        cmd = [sys.executable, os.path.join(ROOT, "bench.py")]
+        cmd = [sys.executable, os.path.join(ROOT, script)]
     p = subprocess.run(cmd + args, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stdout + p.stderr
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -244,6 +246,28 @@ def test_bench_two_ranks_one_gpu_over_ipc(cuda, sfb, zero):
     assert r["n_gpus"] == 2 and r["config"]["dp_transport"] == kind and r["config"]["parallelism"] == "dp2"
     assert r["value"] > 0 and r["config"]["global_batch"] == 256
     assert r["phases_ms"]["allreduce"] > 0, r["phases_ms"]
+    assert r["comm_world"] == 2 and len(r["devices"]) == 2 and r["replicas_identical"], r
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_self_launches_n_ranks(cuda, n):
+    """``bench.py --gpus N`` with no torchrun: the parent spawns the N ranks itself (they share the
+    one GPU here, so DP goes over IPC with sufficient factors), one JSON line, identical replicas."""
+    r = _bench(["--gpus", str(n), "--steps", "20", "--warmup", "5", "--min_warmup_ms", "50"], nproc=n,
+               self_launch=True)
+    assert r["n_gpus"] == n and r["config"]["parallelism"] == f"dp{n}"
+    assert r["config"]["dp_transport"] == "ipc+sfb", r["config"]
+    assert r["comm_world"] == n and len(r["devices"]) == n and r["replicas_identical"], r
+    assert r["config"]["global_batch"] == 128 * n and r["value"] > 0
+
+
+def test_bench_resnet_self_launch_two_ranks_is_real_dp(cuda):
+    """bench_resnet.py --gpus 2 on one GPU: the IPC bucket reducer carries DP (not two independent
+    replicas): both ranks end with bit-identical weights."""
+    r = _bench(["--gpus", "2", "--depth", "18", "--batch_size", "8", "--image", "64", "--steps", "3", "--warmup", "1",
+                "--bucket_mb", "2"], nproc=2, script="bench_resnet.py", self_launch=True)
+    assert r["n_gpus"] == 2 and r["config"]["dp_transport"] == "ipc" and r["comm_world"] == 2
+    assert r["replicas_identical"], r
 
 
 def test_bench_four_ranks_default_zero(cuda):
@@ -252,6 +276,7 @@ def test_bench_four_ranks_default_zero(cuda):
     r = _bench(["--gpus", "4", "--steps", "10", "--warmup", "3", "--min_warmup_ms", "50"], nproc=4)
     assert r["config"]["zero1_fc1"] and r["config"]["dp_transport"] == "ipc+sfb" and r["n_gpus"] == 4
     assert r["value"] > 0 and r["config"]["global_batch"] == 512
+    assert r["comm_world"] == 4 and r["replicas_identical"], r
 
 
 def test_bench_fp32_dtype(cuda):
