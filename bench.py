@@ -26,6 +26,13 @@ sys.path.insert(0, ROOT)
 
 METRIC = "images/sec (whole node) MNIST CNN DP at 1/2/4/8 MI355X; step-time scaling"  # BASELINE.json
 BASELINE_IMG_PER_S = 52.1  # 120 global steps x 256 images / 590 s (performance:6)
+DATA_DESC = {
+    "strokes": "synthetic (device-resident learnable MNIST-shaped set: 55000 class-conditional stroke images "
+               "28x28 with their labels, utils/input_data.synthetic_mnist; random N(0,1) init; the timed steps "
+               "are a learning state, not a collapsed one)",
+    "random": "synthetic (device-resident MNIST-shaped 55000x784 uniform noise, random labels; random N(0,1) "
+              "init; the model collapses to the label prior)",
+}
 
 
 def main(argv=None):
@@ -87,6 +94,11 @@ def main(argv=None):
                     "stream with N workgroups, overlapping the conv backward and the next conv forward")
     ap.add_argument("--conv_unfused", type=int, default=0, help="1: conv1 and conv2 forward as two kernels "
                     "(A/B of the fused conv1->conv2 kernel)")
+    ap.add_argument("--state_steps", type=int, default=100, help="time the steps that follow this many training "
+                    "steps from init (snapshot before the clock-ramp warm-up, restored before the timed region); "
+                    "0: time whatever state the warm-up steps left")
+    ap.add_argument("--data", default="strokes", choices=["strokes", "random"], help="device-resident training "
+                    "set: learnable class-conditional strokes (default) or uniform noise with random labels")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu", action="store_true", help="plumbing dry-run: fp32 PyTorch CPU runner + Gloo "
@@ -138,10 +150,21 @@ def main(argv=None):
         eng.set_zero(True)
     s = torch.cuda.Stream(dev)
     n_data = 55000
+    if a.data == "strokes":  # the learnable synthetic MNIST set (same images on every rank, like the
+        # reference's workers that all read the full training split, mnist_python_m.py:291)
+        from tensorflow_distributed_amd.utils.input_data import synthetic_mnist
+
+        xi, yi = synthetic_mnist(n_data, 0)
+        host_x = torch.from_numpy(xi.reshape(n_data, 784))
+        host_y = torch.from_numpy(yi.astype("int32"))
     with torch.cuda.stream(s):
         g = torch.Generator(device=dev).manual_seed(1000 + rank)
-        data = torch.rand(n_data, 784, device=dev, generator=g)
-        labels = torch.randint(0, 10, (n_data,), device=dev, generator=g, dtype=torch.int32)
+        if a.data == "strokes":
+            data = host_x.to(dev).float().div_(255.0)
+            labels = host_y.to(dev)
+        else:
+            data = torch.rand(n_data, 784, device=dev, generator=g)
+            labels = torch.randint(0, 10, (n_data,), device=dev, generator=g, dtype=torch.int32)
         perm = torch.randperm(n_data, device=dev, generator=g).to(torch.int32)
         if rank == 0:
             eng.params().copy_(M.flat_from_dict(M.init_params(a.seed)).to(dev))
@@ -178,6 +201,14 @@ def main(argv=None):
                     eng.replay("train", k % gsteps if gsteps > 1 else k)
         else:
             run = lambda k: [eng.train_step() for _ in range(k)]  # noqa: E731
+        # The timed steps start from the training state after --state_steps steps (a model that is
+        # still learning), not from wherever the clock-ramp warm-up below leaves it: snapshot it now,
+        # warm up, restore it right before the timed region.
+        snap = None
+        if a.state_steps > 0:
+            run(a.state_steps - 1)
+            snap = [t.clone() for t in _state_tensors(eng)]
+            snap_loss = eng.loss_rows().mean()  # the loss of step state_steps (read after timing)
         run(a.warmup)
     torch.cuda.synchronize(dev)
     if os.environ.get("TFD_DEBUG_IPC"):
@@ -207,7 +238,15 @@ def main(argv=None):
                     loss0_t = eng.loss_rows().mean()  # read after the timed region
             torch.cuda.synchronize(dev)
             extra += chunk
-    if a.lean_gap and extra:
+    if snap is not None:  # back to the snapshotted learning state (every rank: same step)
+        with torch.cuda.stream(s):
+            for dst, src in zip(_state_tensors(eng), snap):
+                dst.copy_(src)
+            eng.invalidate_prefetch()
+            loss0_t = snap_loss
+        del snap
+        torch.cuda.synchronize(dev)
+    if a.lean_gap and (extra or a.state_steps > 0):
         loss0 = None
     else:
         loss0 = float(eng.loss_rows().mean().item())
@@ -249,11 +288,15 @@ def main(argv=None):
     if loss0 is None:
         loss0 = float(loss0_t.item())
     loss1 = float(eng.loss_rows().mean().item())
+    acc1 = float(eng.correct_rows().mean().item())  # last timed step's minibatch accuracy (train mode)
+    # the conv1 weight gradient skips zero pooled gradients (TFD_C1W_SKIP0); those are the pixels the
+    # pooled ReLU output is 0 at, so this is the share of that work the last timed step skipped
+    p1_zero = float((eng.pool1() == 0).float().mean().item())
     gstep = int(eng.step_tensor().item())
     ms = dt * 1e3 / a.steps
     img_s = world * B * a.steps / dt
     if rank == 0:
-        print(f"# world={world} B/gpu={B} steps={a.steps} global_step={gstep} loss {loss0:.3f}->{loss1:.3f} "
+        print(f"# world={world} B/gpu={B} steps={a.steps} global_step={gstep} loss {loss0:.3f}->{loss1:.3f} acc {acc1:.3f} "
               f"{ms:.4f} ms/step", file=sys.stderr)
         print(json.dumps({
             "metric": METRIC,
@@ -263,13 +306,16 @@ def main(argv=None):
             "steps": a.steps,
             "warmup": a.warmup,
             "warmup_extra_steps": extra,
+            "train_state": {"global_step": gstep, "loss_before_timed": round(loss0, 4),
+                            "loss_after_timed": round(loss1, 4), "minibatch_accuracy": round(acc1, 4),
+                            "state_steps": a.state_steps, "pool1_zero_fraction": round(p1_zero, 4)},
             "ms_per_step": round(ms, 5),
             "gpu_event_ms_per_step": round(gpu_ms / a.steps, 5),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(img_s / BASELINE_IMG_PER_S, 1),
             "dtype": a.dtype,
-            "data": "synthetic (device-resident MNIST-shaped 55000x784, random labels; random N(0,1) init)",
+            "data": DATA_DESC[a.data],
             "phases_ms": phases,
             **topo,
             "config": {
@@ -295,6 +341,12 @@ def main(argv=None):
     tr.close()
     ctx.shutdown()
     return 0
+
+
+def _state_tensors(eng):
+    """Everything a training step reads and updates across steps: fp32 master, bf16 shadow, Adam
+    slots, the device step counter (data cursor, dropout key, Adam's t)."""
+    return [eng.params(), eng.params_bf16(), eng.adam_m(), eng.adam_v(), eng.step_tensor()]
 
 
 def _job_topology(ctx, dev, tr, eng):

@@ -18,6 +18,10 @@
 //                    1-of-4 argmax positions carry gradient), deterministic per-image slabs. In the
 //                    LDS path it is the tail of conv2_dgrad_lds (same half-image rows, from LDS).
 #include "../common.h"
+
+#ifndef TFD_C1W_SKIP0  // 1 (A/B only): skip zero pooled gradients in the conv1 wgrad (value-dependent time)
+#define TFD_C1W_SKIP0 0
+#endif
 #include "../gemm.h"
 #include "../mnist_layout.h"
 #include "../tfd_kernels.h"
@@ -1524,7 +1528,7 @@ __global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) {
     for (int j = 0; j < 26; ++j) acc1[j] = 0.f;
     for (int lp = sub; lp < C1W_HALF; lp += 16) {
       const float gv = gsl[lp * 32 + c];
-      if (gv != 0.f) {
+      if (!TFD_C1W_SKIP0 || gv != 0.f) {  // no zero skip by default: time must not depend on values (fma(0, x, acc) == acc)
         const int pp = h * C1W_HALF + lp, w = isl[lp * 32 + c];
         const int oh = 2 * (pp / 14) + (w >> 1), ow = 2 * (pp % 14) + (w & 1);
 #pragma unroll
@@ -1744,7 +1748,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad(MnistStepArgs a) {
   for (int j = 0; j < 26; ++j) acc[j] = 0.f;
   for (int lp = sub; lp < C1W_HALF; lp += 8) {
     const float g = bf2f(gs[lp * 32 + c]);
-    if (g != 0.f) {
+    if (!TFD_C1W_SKIP0 || g != 0.f) {  // no zero skip by default: time must not depend on values (fma(0, x, acc) == acc)
       const int pp = half * C1W_HALF + lp, w = is[lp * 32 + c];
       const int oh = 2 * (pp / 14) + (w >> 1), ow = 2 * (pp % 14) + (w & 1);
 #pragma unroll

@@ -171,6 +171,11 @@ class MnistEngine : public torch::CustomClassHolder {
     ipc_small_ = small_max;
     if (!comm_) bf16_comm_ = bf16_grads && !fp32_;
   }
+  // Per-path fallback: false = the SFB factor and ZeRO shard all-gathers go through RCCL even when
+  // the IPC staging holds them (set when the startup self-check of the IPC gather disagreed with
+  // RCCL; parallel/transport.py)
+  void set_ipc_gather(bool on) { ipc_gather_ = on; }
+  bool ipc_gathers(int64_t shard) const { return ipc_ && ipc_gather_ && ipc_->capacity() * 2 >= shard; }
   int64_t world() const {
     if (comm_) return comm_->world();
     if (ipc_) return ipc_->world();
@@ -1013,7 +1018,7 @@ class MnistEngine : public torch::CustomClassHolder {
     const int64_t r = rank_in_comm();
     const int64_t S = zshard_;
     uint16_t* pb = (uint16_t*)pbf_.data_ptr() + OFF_WD1;
-    if (ipc_ && ipc_->capacity() * 2 >= S) ipc_->all_gather_raw(pb, 2, S, st);
+    if (ipc_gathers(S)) ipc_->all_gather_raw(pb, 2, S, st);
     else if (comm_) comm_->all_gather_raw(pb + r * S, pb, (size_t)S, ncclBfloat16, st);
     else TORCH_CHECK(false, "ZeRO weight gather: no communicator holds a ", S, "-element shard");
   }
@@ -1025,7 +1030,7 @@ class MnistEngine : public torch::CustomClassHolder {
     const int64_t r = rank_in_comm();
     uint16_t* base = (uint16_t*)(p2part ? sfp2_ : sfdr_).data_ptr();
     const int64_t S = p2part ? B_ * FEAT : sfb_rs_;
-    if (ipc_ && ipc_->capacity() * 2 >= S) {
+    if (ipc_gathers(S)) {
       ipc_->all_gather_raw(base, 2, S, st);
       return;
     }
@@ -1164,6 +1169,7 @@ class MnistEngine : public torch::CustomClassHolder {
   c10::intrusive_ptr<RcclComm> comm_;
   c10::intrusive_ptr<IpcComm> ipc_;
   int64_t ipc_small_ = 0;
+  bool ipc_gather_ = true;
   at::Tensor params_, pbf_, grad_, m_, v_, gbf_, step_, tnext_;
   at::Tensor p1_, idx1_, p2_, idx2_, fc1_slab_, hd_, dh_, dlogits_, loss_row_, correct_row_, dz2_, dp1m_, wg2_slab_,
       wg1_slab_, xbuf_, ybuf_;
@@ -1239,6 +1245,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_momentum", &MnistEngine::set_momentum)
       .def("set_comm", &MnistEngine::set_comm)
       .def("set_ipc", &MnistEngine::set_ipc)
+      .def("set_ipc_gather", &MnistEngine::set_ipc_gather)
       .def("set_zero", &MnistEngine::set_zero)
       .def("set_fc_sfb", &MnistEngine::set_fc_sfb)
       .def("fc_sfb", &MnistEngine::fc_sfb)

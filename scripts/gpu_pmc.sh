@@ -15,4 +15,5 @@ for set in "${SETS[@]}"; do
   # PMC_CMD overrides the profiled program (default: the MNIST bench), e.g. "bench_resnet.py --steps 2 --warmup 1"
   timeout -s KILL ${PMC_TIMEOUT:-120} rocprofv3 --pmc $set --kernel-trace -d gpurun_out/pmc$i -o run -- python3 ${PMC_CMD:-bench.py --steps 20 --warmup 5 --min_warmup_ms 0 --phases 0} > gpurun_out/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 gpurun_out/pmc$i.log; exit 1; }
   python scripts/pmc_summary.py $(find gpurun_out/pmc$i -name "*.db" | head -1) | tee gpurun_out/pmc$i.txt
+  rm -rf gpurun_out/pmc$i
 done

@@ -67,15 +67,65 @@ def make_rccl(rank: int, world: int, device_index: int, group=None, src: int = 0
     return torch.classes.tfd.RcclComm(uid, world, rank, device_index)
 
 
-def ipc_self_check(ipc, comm, n: int, device: torch.device) -> bool:
-    """One all-reduce through both transports on random data; the results must agree."""
+def _ref_all_reduce(comm, y, group):
+    """Reference sum: RCCL when there is a communicator, else Gloo on a host copy."""
+    if comm is not None:
+        comm.all_reduce(y, "sum")
+        return y
+    h = y.cpu()
+    dist.all_reduce(h, group=group)
+    return h.to(y.device)
+
+
+def _ref_all_gather(comm, mine, world, group):
+    if comm is not None:
+        out = torch.empty(world * mine.numel(), dtype=mine.dtype, device=mine.device)
+        comm.all_gather(mine, out)
+        return out
+    parts = [torch.empty(mine.numel(), dtype=torch.float32) for _ in range(world)]
+    dist.all_gather(parts, mine.float().cpu(), group=group)
+    return torch.cat(parts).to(mine.device, mine.dtype)
+
+
+def ipc_self_check(ipc, comm, n: int, device: torch.device, group=None) -> bool:
+    """One all-reduce through IPC and through the reference (RCCL, or Gloo when ranks share a GPU)
+    on random data; the results must agree."""
     g = torch.Generator(device=device).manual_seed(77 + ipc.rank())
     x = torch.randn(n, device=device, generator=g)
-    y = x.clone()
+    y = _ref_all_reduce(comm, x.clone(), group)
     ipc.all_reduce(x, 1.0)
-    comm.all_reduce(y, "sum")
     torch.cuda.synchronize(device)
     return bool(ipc.error() == 0 and torch.allclose(x, y, rtol=1e-4, atol=1e-4))
+
+
+def ipc_gather_self_check(ipc, comm, shards, device: torch.device, group=None) -> bool:
+    """The in-place bf16 all-gather (SFB factors, ZeRO weight shards) at every shard size the step
+    will run through IPC, against the reference gather: a gather is a copy, so bit-exact."""
+    W, r = int(ipc.world()), int(ipc.rank())
+    ok = True
+    for S in shards:
+        g = torch.Generator(device=device).manual_seed(91 + r + 1000 * S)
+        mine = torch.randn(S, device=device, generator=g).to(torch.bfloat16)
+        buf = torch.zeros(W * S, dtype=torch.bfloat16, device=device)
+        buf[r * S:(r + 1) * S] = mine
+        ipc.all_gather(buf)
+        ref = _ref_all_gather(comm, mine, W, group)
+        torch.cuda.synchronize(device)
+        ok = ok and bool(ipc.error() == 0 and torch.equal(buf, ref))
+    return ok
+
+
+def _gather_shards(eng, world: int, cap: int, sfb: bool, zero: bool):
+    """Shard sizes (bf16 elements) of the all-gathers that will run through an IPC staging of
+    ``cap`` fp32 elements (MnistEngine::ipc_gathers)."""
+    from ..models import mnist_cnn as M
+
+    shards = []
+    if sfb:
+        shards += [int(eng.batch()) * M.FEAT, int(eng.sfb_shard_elems())]
+    if zero and world > 1:
+        shards.append(M.FEAT * M.HID // world)
+    return sorted({S for S in shards if 2 * cap >= S and S % 8 == 0})
 
 
 class DPTransport:
@@ -143,6 +193,15 @@ def attach_engine(eng, rank: int, world: int, device: torch.device, group=None, 
     if mode == "ipc":
         ipc = make_ipc_comm(rank, world, device.index or 0, max(cap, small_cap), group=group,
                             max_blocks=8 if shared else 64)
+        if world > 1:  # every IPC collective of this configuration against Gloo; no fallback exists here
+            ok = int(ipc_self_check(ipc, None, M.BUCKET_SPLIT, device, group)
+                     and ipc_gather_self_check(ipc, None, _gather_shards(eng, world, max(cap, small_cap), sfb, zero),
+                                               device, group))
+            flags = torch.tensor([1 - ok], dtype=torch.int64)
+            dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)
+            if int(flags.item()):
+                ipc.close()
+                raise RuntimeError("IPC transport self-check failed (all-reduce or all-gather disagrees with Gloo)")
         eng.set_ipc(ipc, cap, bf16)
         if force_dp:
             eng.set_force_dp(True)
@@ -156,16 +215,23 @@ def attach_engine(eng, rank: int, world: int, device: torch.device, group=None, 
         eng.set_force_dp(True)
     kind = "rccl"
     if small_ipc and world > 1:
-        ok, ipc = 0, None
+        ok_ar, ok_ag, ipc = 0, 0, None
         try:
             ipc = make_ipc_comm(rank, world, device.index or 0, small_cap, group=group, max_blocks=64)
-            ok = int(ipc_self_check(ipc, comm, M.BUCKET_SPLIT, device))
-        except Exception as e:  # pragma: no cover - depends on the node's IPC support
+        except Exception as e:  # pragma: no cover - depends on the node's IPC support (all ranks raise)
             log(f"# ipc setup failed: {e!r}")
-        flags = torch.tensor([1 - ok], dtype=torch.int64)
+        if ipc is not None:  # every rank has one (make_ipc_comm agrees collectively) -> matched checks
+            ok_ar = int(ipc_self_check(ipc, comm, M.BUCKET_SPLIT, device, group))
+            ok_ag = int(ipc_gather_self_check(ipc, comm, _gather_shards(eng, world, small_cap, sfb, zero), device,
+                                              group))
+        flags = torch.tensor([1 - ok_ar, 1 - ok_ag], dtype=torch.int64)
         dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)  # every rank must agree
-        if int(flags.item()) == 0:
+        if int(flags[0].item()) == 0:
             eng.set_ipc(ipc, M.BUCKET_SPLIT, bf16)
+            if int(flags[1].item()):  # per-path fallback: the gathers go through RCCL
+                log("# ipc all-gather self-check failed; SFB / ZeRO gathers stay on RCCL")
+                eng.set_ipc_gather(False)
+                return _sfb(DPTransport("rccl+ipc(ar)", comm=comm, ipc=ipc))
             return _sfb(DPTransport("rccl+ipc", comm=comm, ipc=ipc))
         log("# ipc self-check failed; the conv bucket stays on RCCL")
         if ipc is not None:

@@ -131,6 +131,70 @@ def test_engine_dp_over_ipc_matches_single_rank_big_batch(cuda, world, sfb):
     assert cos > 0.99, cos  # bf16 gradient all-reduce vs one big-batch step: same update direction
 
 
+def _engine_dp_grads_worker(rank, world, B, sfb):
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+    from tensorflow_distributed_amd.parallel.ipc import make_ipc_comm
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    comm = make_ipc_comm(rank, world, 0, M.TOTAL)
+    eng = torch.classes.tfd.MnistEngine(B, 0, 1.0, 5, rank)
+    eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+    eng.set_ipc(comm, 1 << 30, True)
+    if sfb:
+        eng.set_fc_sfb(True)
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(world * B, 784, generator=g)
+    y = torch.randint(0, 10, (world * B,), generator=g, dtype=torch.int32)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        eng.params().copy_(M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()}).to(dev))
+        eng.sync_shadow()
+        eng.feed_x().copy_(x[rank * B:(rank + 1) * B].to(dev))
+        eng.feed_y().copy_(y[rank * B:(rank + 1) * B].to(dev))
+        eng.train_step()
+    torch.cuda.synchronize()
+    out = eng.grads_bf16().float().cpu(), comm.error()  # the summed gradients the optimizer read
+    comm.close()
+    return out
+
+
+@pytest.mark.parametrize("sfb", [False, True])
+def test_engine_dp_reduced_grads_elementwise(cuda, sfb):
+    """The gradient every rank's optimizer consumes after one DP=2 step (bf16 wire: per-rank mean
+    gradients cast to bf16, summed in fp32 in rank order, stored bf16; with sfb the fc gradients
+    are one GEMM over both ranks' gathered factors) equals 2x the DP=1 gradient of the 2B batch,
+    element by element within bf16 rounding."""
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+
+    world, B = 2, 32
+    res = run_ranks(_engine_dp_grads_worker, world, B, sfb, timeout=300)
+    assert all(e == 0 for _, e in res)
+    assert torch.equal(res[0][0], res[1][0]), "ranks consumed different gradients"
+    eng = torch.classes.tfd.MnistEngine(world * B, 0, 1.0, 5, 0)
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(world * B, 784, generator=g)
+    y = torch.randint(0, 10, (world * B,), generator=g, dtype=torch.int32)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        eng.params().copy_(M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()}).to(cuda))
+        eng.sync_shadow()
+        eng.feed_x().copy_(x.to(cuda))
+        eng.feed_y().copy_(y.to(cuda))
+        eng.forward(True)
+        eng.backward_a()
+        eng.backward_b()
+    torch.cuda.synchronize()
+    ref = M.dict_from_flat(eng.grads().cpu() * world)  # per-rank means summed = world x the 2B mean
+    got = M.dict_from_flat(res[0][0])
+    for k in ref:
+        r, d = ref[k].float(), got[k].float()
+        tol = 1.5e-2 * r.abs() + 4e-3 * r.abs().max()
+        bad = (d - r).abs() > tol
+        assert not bad.any(), (f"{k}: {int(bad.sum())}/{r.numel()} elements off; worst |d-r| "
+                               f"{(d - r).abs().max().item():.3e} vs max|r| {r.abs().max().item():.3e}")
+
+
 def _resnet_dp_worker(rank, world, steps):
     from tensorflow_distributed_amd.models.resnet import ResNet
     from tensorflow_distributed_amd.parallel.ipc import IpcCollectives, make_ipc_comm

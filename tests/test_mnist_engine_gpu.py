@@ -51,9 +51,8 @@ def test_step_grads_match_oracle(cuda, scale, B):
     loss = eng.loss_rows().cpu()
     assert _relerr(loss, loss_ref) < 2e-2, (loss[:4], loss_ref[:4])
     g = M.dict_from_flat(eng.grads().cpu())
-    for k in g_ref:
-        e = _relerr(g[k].float(), g_ref[k])
-        assert e < 5e-2, f"{k}: relerr {e}"
+    errs = {k: _relerr(g[k].float(), g_ref[k]) for k in g_ref}
+    assert max(errs.values()) < 2e-2, errs  # bf16 rounding points emulated by the oracle
     del pd
 
 
