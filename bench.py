@@ -68,7 +68,6 @@ def main(argv=None):
                     "with HIP timing events at the phase boundaries and report the GPU phase breakdown (untimed)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="compute dtype: bf16 MFMA operands "
                     "(fp32 accumulate/master/optimizer), or fp32 everything (the reference's precision)")
-    ap.add_argument("--conv_fork", type=int, default=0, help="1: conv2 wgrad on a forked stream beside dgrad")
     ap.add_argument("--zero", type=int, default=-1, help="1: ZeRO-1 sharding of the fc1 weight (N > 1): with "
                     "--fc_sfb each rank forms only its shard's fc1 gradient and updates only that shard, the bf16 "
                     "shards are all-gathered (IPC one-shot) beside the next conv forward; -1 (default): on from 4 "
@@ -77,21 +76,10 @@ def main(argv=None):
     ap.add_argument("--fc_sfb", type=int, default=1, help="1 (N > 1 or --force_dp): fc-region gradients by "
                     "sufficient-factor broadcasting -- all-gather the fc factors (1.33 MB/rank) and form the summed "
                     "fc gradient locally instead of all-reducing it (6.4 MB); 0: bucketed all-reduce")
-    ap.add_argument("--dp_serial", type=int, default=1, help="1: with --fc_sfb, every compute kernel on the main "
-                    "stream and only the collectives on the comm stream; 0: the overlapped three-stream schedule "
-                    "(SFB GEMM + fc optimizer beside the conv backward / next conv forward)")
     ap.add_argument("--fused_tail", type=int, default=1, help="1: on one GPU the Adam kernel also reduces the "
                     "conv weight-gradient slabs and bumps the step (one kernel less)")
     ap.add_argument("--local_bf16_grads", type=int, default=1, help="1: on one GPU keep the fc-region gradients "
                     "in bf16 (the DP all-reduce wire format): fc backward writes and Adam reads 2 B per gradient")
-    ap.add_argument("--fc_adam", type=int, default=0, help="1: on one GPU, ApplyAdam of the fc region runs in "
-                    "the fc backward epilogues (the fc gradients never reach memory)")
-    ap.add_argument("--fc_adam_fork", type=int, default=0, help="1: that fused fc backward+Adam kernel on a side "
-                    "stream beside the conv backward")
-    ap.add_argument("--fc_split", type=int, default=0, help="1: on one GPU, fc dW + the fc-region Adam on a "
-                    "second stream beside dX and the conv backward")
-    ap.add_argument("--fc_defer", type=int, default=0, help="N > 0: on one GPU, the fc-region Adam on a second "
-                    "stream with N workgroups, overlapping the conv backward and the next conv forward")
     ap.add_argument("--conv_unfused", type=int, default=0, help="1: conv1 and conv2 forward as two kernels "
                     "(A/B of the fused conv1->conv2 kernel)")
     ap.add_argument("--state_steps", type=int, default=100, help="time the steps that follow this many training "
@@ -128,14 +116,9 @@ def main(argv=None):
     eng = torch.classes.tfd.MnistEngine(B, dev.index, 0.75, a.seed, rank)
     eng.set_adam(a.lr, 0.9, 0.999, 1e-8)
     eng.set_dtype(a.dtype)
-    eng.set_conv_fork(a.conv_fork)
     eng.set_fused_tail(a.fused_tail)
     eng.set_local_bf16_grads(a.local_bf16_grads)
-    eng.set_fc_adam(a.fc_adam, a.fc_adam_fork)
     eng.set_conv_unfused(a.conv_unfused)
-    eng.set_fc_split(a.fc_split)
-    eng.set_fc_defer(a.fc_defer)
-    eng.set_dp_serial(a.dp_serial)
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     mode = a.transport
@@ -331,11 +314,9 @@ def main(argv=None):
                 "dp_transport": tr.kind,
                 "force_dp": bool(a.force_dp),
                 "zero1_fc1": bool(a.zero),
-                "dp_schedule": "serial" if a.dp_serial else "overlapped",
                 "fc_grads": ("fp32" if a.dtype == "fp32" else
                              "summed from all-gathered factors (sfb), bf16" if "sfb" in tr.kind else
-                             "fused into Adam (fp32, in registers)" if world == 1 and a.fc_adam and not a.force_dp
-                             else "bf16" if (a.local_bf16_grads or world > 1) and not a.fp32_grads else "fp32"),
+                             "bf16" if (a.local_bf16_grads or world > 1) and not a.fp32_grads else "fp32"),
             },
         }), flush=True)
     tr.close()

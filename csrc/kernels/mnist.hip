@@ -856,26 +856,7 @@ constexpr int OUTG_BLOCKS = (HID + 1 + OUTG_ROWS - 1) / OUTG_ROWS;  // 17 (last 
 #define TFD_OUTG_LB 16
 #endif
 constexpr int OUTG_LB = TFD_OUTG_LB;  // hd loads batched per thread (a one-at-a-time loop was a 32-deep latency chain)
-__device__ __forceinline__ void adam1(const MnistAdamArgs& o, int64_t i, float g, float lr_t, float c1, float c2) {
-  float p = o.p[i], m = o.m[i], v = o.v[i];
-  m = m + (g - m) * c1;
-  v = v + (g * g - v) * c2;
-  p -= lr_t * m / (sqrtf(v) + o.eps);
-  o.p[i] = p;
-  o.m[i] = m;
-  o.v[i] = v;
-  o.pbf[i] = f2bf_bits(p);
-}
-struct AdamCoef {
-  float lr_t, c1, c2;
-};
-// TF ApplyAdam coefficients for step t (lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t))
-__device__ __forceinline__ AdamCoef adam_coef(const MnistAdamArgs& o, int64_t t) {
-  const float b1p = powf(o.beta1, (float)t), b2p = powf(o.beta2, (float)t);
-  return AdamCoef{o.lr * sqrtf(1.f - b2p) / (1.f - b1p), 1.f - o.beta1, 1.f - o.beta2};
-}
-__device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, float* smem,
-                                               const MnistAdamArgs* adam = nullptr) {
+__device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, float* smem) {
   float* dl = smem;                      // [B][10]
   float* part = smem + a.B * NCLS;       // [4][64][10]
   const int t = threadIdx.x, r = t & 63, q = t >> 6;
@@ -916,10 +897,7 @@ __device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, 
       const size_t o = OFF_OUT + (size_t)mm * NCLS + (i - rr * NCLS);
       const float g =
           part[i] + part[OUTG_ROWS * NCLS + i] + part[2 * OUTG_ROWS * NCLS + i] + part[3 * OUTG_ROWS * NCLS + i];
-      if (adam) {  // one GPU: the gradient goes straight into Adam (t = global_step + 1)
-        const AdamCoef c = adam_coef(*adam, *a.step + 1);
-        adam1(*adam, (int64_t)o, g, c.lr_t, c.c1, c.c2);
-      } else if (a.gbf_a) {
+      if (a.gbf_a) {
         a.gbf_a[o] = f2bf_bits(g);
       } else {
         a.grad[o] = g;
@@ -962,33 +940,6 @@ struct GradEpi {
     }
   }
 };
-// Same output, one wide store per lane: a 4x4 transpose inside each 4-lane group (4 bpermute
-// rounds) turns "4 rows of one column" into "4 columns of one row", so each lane writes 8 B (bf16)
-// or 16 B (fp32) instead of four scattered 2/4-B stores. Needs every lane of the wave (no early
-// return before the shuffles) and N % 4 == 0.
-struct GradEpiT {
-  float* __restrict__ out;
-  uint16_t* __restrict__ outbf;
-  int ld, M, N;
-  __device__ __forceinline__ static float pick(f32x4 v, int i) {
-    return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
-  }
-  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
-    const int lane = threadIdx.x & 63, j = lane & 3;
-    f32x4 r;  // r[k] = column ((j + k) & 3) of row j, from lane (j + k) & 3 of the group
-#pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] = __shfl(pick(v, (j - k) & 3), (lane & ~3) | ((j + k) & 3), 64);
-    const f32x4 w = f32x4{pick(r, (0 - j) & 3), pick(r, (1 - j) & 3), pick(r, (2 - j) & 3), pick(r, (3 - j) & 3)};
-    const int m = m4 + j, nb = n - j;
-    if (m >= M || nb >= N) return;
-    const size_t o = (size_t)m * ld + nb;
-    if (outbf) *reinterpret_cast<uint2*>(outbf + o) = make_uint2(pack_bf2(w[0], w[1]), pack_bf2(w[2], w[3]));
-    else *reinterpret_cast<f32x4*>(out + o) = w;
-  }
-};
-#ifndef TFD_DW_EPIT  // 1: fc1 dW epilogue through the 4-lane transpose (GradEpiT)
-#define TFD_DW_EPIT 0
-#endif
 #ifndef TFD_FDW_BM
 #define TFD_FDW_BM 64
 #endif
@@ -996,12 +947,7 @@ constexpr int FDW_BM = TFD_FDW_BM, FDW_BN = 64, FDW_BK = TFD_FDW_BK;
 __device__ __forceinline__ void fc1_dw_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   OnesRowMC la{a.p2, FEAT, FEAT, a.B};
   DenseLoader<false> lb{a.dh, HID, HID, a.B};
-#if TFD_DW_EPIT
-  static_assert(OFF_WD1 % 4 == 0 && HID % 4 == 0, "wide dW stores");
-  GradEpiT epi{a.grad + OFF_WD1, a.gbf_a ? a.gbf_a + OFF_WD1 : nullptr, HID, FEAT + 1, HID};
-#else
   GradEpi epi{a.grad + OFF_WD1, a.gbf_a ? a.gbf_a + OFF_WD1 : nullptr, HID, FEAT + 1, HID};
-#endif
   gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, by * FDW_BM, bx * FDW_BN, 0, a.B, smem);
 }
 
@@ -1092,75 +1038,6 @@ __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int pa
   id -= FDW_GX * FDW_GY;
   out_grad_block(a, id, (float*)smem_raw);
 #endif
-}
-
-// ---------------- K10 + K16 (one GPU): fc1 dW with ApplyAdam in the epilogue ----------------
-// The dW tile never reaches memory: every lane prefetches the fp32 master, m and v of the 16
-// parameters its accumulators will cover (4 tiles x one row x 4 columns, 16-B loads) BEFORE the
-// K loop, so their latency hides behind the GEMM; the epilogue turns "4 rows of one column" into
-// "4 columns of one row" with a 4-lane transpose (GradEpiT) and applies TF ApplyAdam in registers
-// (t = global_step + 1), writing p, m, v and the bf16 shadow once. Row 3136 (the ones row) is the
-// bias bd1, contiguous after the weights (mnist_layout.h), so the same indexing covers it.
-struct AdamDwEpi {
-  static constexpr bool WANTS_IJ = true;
-  const MnistAdamArgs& o;
-  const f32x4 (&P)[2][2];
-  const f32x4 (&Mm)[2][2];
-  const f32x4 (&V)[2][2];
-  AdamCoef c;
-  __device__ __forceinline__ static float pick(f32x4 v, int i) {
-    return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
-  }
-  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v, int i, int j) const {
-    const int lane = threadIdx.x & 63, q = lane & 3;
-    f32x4 r;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] = __shfl(pick(v, (q - k) & 3), (lane & ~3) | ((q + k) & 3), 64);
-    const f32x4 g = f32x4{pick(r, (0 - q) & 3), pick(r, (1 - q) & 3), pick(r, (2 - q) & 3), pick(r, (3 - q) & 3)};
-    const int m = m4 + q, nb = n - q;
-    if (m > FEAT) return;  // rows 0..3135 weights, 3136 bias
-    const int64_t e = OFF_WD1 + (int64_t)m * HID + nb;
-    f32x4 p = P[i][j], mm = Mm[i][j], vv = V[i][j];
-    mm = mm + (g - mm) * c.c1;
-    vv = vv + (g * g - vv) * c.c2;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) p[k] -= c.lr_t * mm[k] / (sqrtf(vv[k]) + o.eps);
-    *reinterpret_cast<f32x4*>(o.p + e) = p;
-    *reinterpret_cast<f32x4*>(o.m + e) = mm;
-    *reinterpret_cast<f32x4*>(o.v + e) = vv;
-    *reinterpret_cast<uint2*>(o.pbf + e) = make_uint2(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]));
-  }
-};
-static_assert(FDW_BM == 64 && FDW_BN == 64, "AdamDwEpi assumes 2x2 waves of 32x32");
-__device__ __forceinline__ void fc1_dw_adam_block(const MnistStepArgs& a, const MnistAdamArgs& o, int bx, int by,
-                                                  bf16* smem) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wm = wid >> 1, wn = wid & 1;
-  const int m0 = by * FDW_BM, n0 = bx * FDW_BN;
-  f32x4 P[2][2], Mm[2][2], V[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int m = m0 + wm * 32 + 16 * i + 4 * (lane >> 4) + (lane & 3);
-      const int nb = n0 + wn * 32 + 16 * j + 4 * ((lane & 15) >> 2);
-      const int64_t e = OFF_WD1 + (int64_t)min(m, FEAT) * HID + nb;
-      P[i][j] = *reinterpret_cast<const f32x4*>(o.p + e);
-      Mm[i][j] = *reinterpret_cast<const f32x4*>(o.m + e);
-      V[i][j] = *reinterpret_cast<const f32x4*>(o.v + e);
-    }
-  OnesRowMC la{a.p2, FEAT, FEAT, a.B};
-  DenseLoader<false> lb{a.dh, HID, HID, a.B};
-  AdamDwEpi epi{o, P, Mm, V, adam_coef(o, *a.step + 1)};
-  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, m0, n0, 0, a.B, smem);
-}
-// [out-layer grad + Adam blocks | fc1 dW + Adam tiles]; the dX GEMM ran before (part 2), so the
-// fc1 weights it read are not yet updated.
-__global__ __launch_bounds__(256) void fc1_bwd_adam(MnistStepArgs a, MnistAdamArgs o) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  int id = blockIdx.x;
-  if (id < OUTG_BLOCKS) { out_grad_block(a, id, (float*)smem_raw, &o); return; }
-  id -= OUTG_BLOCKS;
-  fc1_dw_adam_block(a, o, id % FDW_GX, id / FDW_GX, (bf16*)smem_raw);
 }
 
 // ---------------- DP: fc gradients from all-gathered sufficient factors ----------------
@@ -1874,19 +1751,19 @@ __device__ __forceinline__ f32x4 slab_sum(const f32x4* __restrict__ s4, int64_t 
   return acc;
 }
 __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, MnistAdamArgs o) {
-  const int gb = o.fc_only ? 0 : gather_blocks(a);
+  const int gb = gather_blocks(a);
   if ((int)blockIdx.x < gb) {  // the next step's batch; t = the step started next
     gather_next(a, *o.t, blockIdx.x);
     return;
   }
   const int grid = (int)gridDim.x - gb;
   // grid == MAD_CONV: the fc region was updated by fc1_bwd_adam; the last conv2 block bumps the step
-  if (!o.fc_only && grid == MAD_CONV && (int)blockIdx.x - gb == grid - 1 && threadIdx.x == 0) *o.step += 1;
+  if (grid == MAD_CONV && (int)blockIdx.x - gb == grid - 1 && threadIdx.x == 0) *o.step += 1;
   const int64_t t = *o.t;
   const float b1p = powf(o.beta1, (float)t), b2p = powf(o.beta2, (float)t);
   const float lr_t = o.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float c1 = 1.f - o.beta1, c2 = 1.f - o.beta2;
-  const int bid = (int)blockIdx.x - gb + (o.fc_only ? MAD_CONV : 0), tid = threadIdx.x;
+  const int bid = (int)blockIdx.x - gb, tid = threadIdx.x;
   if (bid < MAD_CONV) {
     __shared__ f32x4 red[MAD_NT];
     const bool one = bid < MAD_C1BLK;
@@ -1908,7 +1785,7 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
     }
   } else {
     const int64_t i0 = MAD_C2END + (int64_t)(bid - MAD_CONV) * MAD_NT + tid;
-    const int64_t STRIDE = (int64_t)(o.fc_only ? (int)gridDim.x : MAD_FC_BLOCKS) * MAD_NT;
+    const int64_t STRIDE = (int64_t)MAD_FC_BLOCKS * MAD_NT;
 #if TFD_ADAM_U > 1
     // All U strides' loads issued before any math/store, so U x 56 B per lane are in flight
     // (the one-at-a-time loop leaves the compiler no room: p/m/v stores may alias the next loads).
@@ -1972,7 +1849,7 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
     } else {
       for (int64_t i = i0; i < TOTAL / 4; i += STRIDE) adam4(o, i, reinterpret_cast<const f32x4*>(a.grad)[i], lr_t, c1, c2);
     }
-    if (!o.fc_only && bid == MAD_GRID - 1 && tid == 0) *o.step += 1;  // see MnistAdamArgs
+    if (bid == MAD_GRID - 1 && tid == 0) *o.step += 1;  // see MnistAdamArgs
   }
 }
 
@@ -2055,21 +1932,18 @@ void mnist_backward_a(const MnistStepArgs& a, hipStream_t s, int part) {
   fc1_bwd<<<nb, 256, sm, s>>>(a, n_dx, part);
 }
 
-void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux, hipEvent_t fork, hipEvent_t join) {
+void mnist_backward_b(const MnistStepArgs& a, hipStream_t s) {
   const int B = a.B;
   const int K = B * 196;
   const int kper = ((K + a.wg2_splits - 1) / a.wg2_splits + C2W_BK - 1) / C2W_BK * C2W_BK;
 #if TFD_CONV2_LDS
-  // conv2 wgrad (one slab per image pair) optionally on the aux stream beside dgrad + conv1 wgrad
+  // conv2 wgrad (one slab per image pair), then dgrad + conv1 wgrad, one stream (a forked wgrad
+  // only contended with dgrad for the CUs: 110 vs 100 us/step, profiles/ab_conv_fork.log)
   (void)kper;
-  hipStream_t ws = aux ? aux : s;
-  if (aux) { (void)hipEventRecord(fork, s); (void)hipStreamWaitEvent(aux, fork, 0); }
-  conv2_wgrad_lds<<<C2WL_NTG * a.wg2_splits, 512, C2WL_SMEM, ws>>>(a);
+  conv2_wgrad_lds<<<C2WL_NTG * a.wg2_splits, 512, C2WL_SMEM, s>>>(a);
   set_smem<conv2_dgrad_lds>(C2D_SMEM);
   conv2_dgrad_lds<<<2 * B, 512, C2D_SMEM, s>>>(a);  // + conv1 wgrad (fused tail)
-  if (aux) { (void)hipEventRecord(join, aux); (void)hipStreamWaitEvent(s, join, 0); }
 #else
-  (void)aux; (void)fork; (void)join;
   {
     constexpr int sm_d = GemmSmem<C2D_BM, C2D_BN, C2D_BK, Conv2DgradA, Conv2DgradB>::BYTES;
     constexpr int sm_w = GemmSmem<C2W_BM, C2W_BN, C2W_BK, Conv2WgradA, DenseLoader<false>>::BYTES;
@@ -2098,11 +1972,6 @@ void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_
   mnist_adam_kernel<<<gb + (fc_region ? MAD_GRID : MAD_CONV), MAD_NT, 0, s>>>(a, o);
 }
 
-void mnist_adam_fc(const MnistStepArgs& a, MnistAdamArgs o, hipStream_t s, int blocks) {
-  o.fc_only = 1;
-  mnist_adam_kernel<<<blocks > 0 ? blocks : MAD_FC_BLOCKS, MAD_NT, 0, s>>>(a, o);
-}
-
 int64_t mnist_sfb_slot_elems(int B) { return ((int64_t)B * (2 * HID + 2 * NCLS) + 63) / 64 * 64; }
 
 void mnist_fc_grad_sfb(const MnistStepArgs& a, hipStream_t s) {
@@ -2120,14 +1989,6 @@ void mnist_fc_grad_sfb(const MnistStepArgs& a, hipStream_t s) {
 void mnist_sfb_tile_rows(int row0, int row1, int* by_lo, int* by_hi) {
   *by_lo = row0 / FDW_BM;
   *by_hi = (row1 - 1) / FDW_BM;
-}
-
-void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s) {
-  constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, DenseLoader<false>>::BYTES;
-  const int sm_og = (a.B * NCLS + 4 * OUTG_ROWS * NCLS) * 4;
-  const int sm = std::max(sm_dw, sm_og);
-  set_smem<fc1_bwd_adam>(sm);
-  fc1_bwd_adam<<<OUTG_BLOCKS + FDW_GX * FDW_GY, 256, sm, s>>>(a, o);
 }
 
 }  // namespace tfd

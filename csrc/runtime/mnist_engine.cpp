@@ -72,16 +72,11 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_b_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
-    HIP_OK(hipStreamCreateWithFlags(&aux_stream_, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&opt_stream_, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&ev_opt_a_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_start_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_ag_, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_p2_, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&ev_dx_, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&ev_sfb_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_wag_, hipEventDisableTiming));
     for (auto& e : pev_) HIP_OK(hipEventCreate(&e));  // timing events (phase timer)
   }
@@ -91,16 +86,11 @@ class MnistEngine : public torch::CustomClassHolder {
     hipEventDestroy(ev_b_);
     hipEventDestroy(ev_done_);
     hipStreamDestroy(comm_stream_);
-    hipEventDestroy(ev_fork_);
-    hipEventDestroy(ev_join_);
-    hipStreamDestroy(aux_stream_);
     hipStreamDestroy(opt_stream_);
     hipEventDestroy(ev_opt_a_);
     hipEventDestroy(ev_start_);
     hipEventDestroy(ev_ag_);
     hipEventDestroy(ev_p2_);
-    hipEventDestroy(ev_dx_);
-    hipEventDestroy(ev_sfb_);
     hipEventDestroy(ev_wag_);
     for (auto& e : pev_) hipEventDestroy(e);
   }
@@ -226,23 +216,11 @@ class MnistEngine : public torch::CustomClassHolder {
   bool fc_sfb() const { return sfb_active(); }
   // bf16 elements of the larger of the two per-rank gather shards (IPC staging must hold it)
   int64_t sfb_shard_elems() const { return std::max<int64_t>(B_ * FEAT, mnist_sfb_slot_elems((int)B_)); }
-  // conv2 wgrad on a forked stream beside dgrad -> conv1 wgrad (1) or all on the main stream (0)
-  void set_conv_fork(int64_t on) { conv_fork_ = on != 0; }
   void set_fused_tail(int64_t on) { fuse_tail_ = on != 0; }
   // one GPU, fused tail: keep the fc-region gradients in bf16 (as DP all-reduces them)
   void set_local_bf16_grads(int64_t on) { local_bf16_grads_ = on != 0; }
-  // one GPU + Adam: fc-region ApplyAdam fused into the fc backward (gradients never reach memory);
-  // fork = that kernel on a side stream beside the conv backward
-  void set_fc_adam(int64_t on, int64_t fork) { fc_adam_ = on != 0; fc_adam_fork_ = fork != 0; }
-  // one GPU: fc dW + fc Adam on the optimizer stream beside dX + the conv backward
-  void set_fc_split(int64_t on) { fc_split_ = on != 0; }
-  // one GPU: the fc-region Adam deferred onto the optimizer stream with `blocks` workgroups (0: off)
-  void set_fc_defer(int64_t blocks) { fc_defer_ = blocks; }
   // 0 (default): conv1 fused into the conv2 forward kernel; 1: the two separate kernels (A/B)
   void set_conv_unfused(int64_t on) { conv_unfused_ = on != 0; }
-  // DP with sufficient factors: 1 (default) every compute kernel on the main stream, collectives on
-  // the comm stream (train_step_sfb_serial); 0 the overlapped three-stream schedule (train_step_sfb)
-  void set_dp_serial(int64_t on) { dp_serial_ = on != 0; }
   // Make every rank's state whole again after ZeRO-1 steps (before eval / checkpoint / broadcast):
   // each rank updated the fp32 master, m and v of its own fc1 shard only, so all four are
   // all-gathered -- the bf16 shadow (what the forward reads) and the fp32 master + Adam slots (what
@@ -332,7 +310,7 @@ class MnistEngine : public torch::CustomClassHolder {
       mnist_conv_grad_reduce(a, stream());
       return;
     }
-    mnist_backward_b(a, stream(), conv_fork_ ? aux_stream_ : nullptr, ev_fork_, ev_join_);
+    mnist_backward_b(a, stream());
     mnist_conv_grad_reduce(a, stream());
   }
   void apply_optimizer(double grad_scale) {
@@ -378,15 +356,13 @@ class MnistEngine : public torch::CustomClassHolder {
     }
     if (dp) {
       if (sfb_active()) {
-        if (dp_serial_) train_step_sfb_serial(join_end);
-        else train_step_sfb(join_end);
+        train_step_sfb_serial(join_end);
       } else {
         train_step_dp(join_end);
       }
       return;
     }
     mark(P_START, s);
-    hipStream_t ws = conv_fork_ ? aux_stream_ : nullptr;
     MnistStepArgs a = args();
     // one GPU: nothing to overlap with. With Adam ONE kernel ends the step: it reduces the conv
     // weight-gradient slabs itself and bumps the step (its t was written by the head kernel).
@@ -395,81 +371,6 @@ class MnistEngine : public torch::CustomClassHolder {
     MnistAdamArgs o{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(),
                     (uint16_t*)pbf_.data_ptr(), (float)lr_, (float)b1_, (float)b2_, (float)eps_,
                     (const int64_t*)tnext_.data_ptr(), (int64_t*)step_.data_ptr(), nullptr};
-    if (fused && fc_adam_) {
-      // fc-region Adam inside the fc backward epilogues (dX first: it reads the old fc1 weights);
-      // optionally on a side stream beside the conv backward, which only needs dX
-      mnist_forward(a, true, s);
-      mark(P_FWD, s);
-      mnist_backward_a(a, s, 2);
-      mark(P_BFC, s);
-      hipStream_t fs = fc_adam_fork_ ? opt_stream_ : s;
-      if (fc_adam_fork_) {
-        HIP_OK(hipEventRecord(ev_a_, s));
-        HIP_OK(hipStreamWaitEvent(fs, ev_a_, 0));
-      }
-      mnist_backward_a_adam(a, o, fs);
-      mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
-      if (fc_adam_fork_) {
-        HIP_OK(hipEventRecord(ev_opt_a_, fs));
-        HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
-      }
-      mark(P_BCONV, s);
-      mnist_adam_fused(a, o, s, false);
-      mark(P_OPT, s);
-      return;
-    }
-    if (fused && fc_defer_ > 0) {
-      // fc-region Adam on the optimizer stream with a small grid (fc_defer_ blocks: it leaves the
-      // CUs' wave slots to the conv kernels), overlapping the conv backward, the conv Adam and the
-      // NEXT step's conv forward; the main stream waits for it just before the next fc forward
-      // (the same cross-step schedule as train_step_dp, without the collectives)
-      a.gbf_a = (uint16_t*)gbf_.data_ptr();
-      o.gbf = (const uint16_t*)gbf_.data_ptr();
-      mnist_forward_conv(a, s);
-      if (pending_opt_a_) {
-        HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
-        pending_opt_a_ = false;
-      }
-      mnist_forward_fc(a, true, s);
-      mark(P_FWD, s);
-      mnist_backward_a(a, s, 0);
-      mark(P_BFC, s);
-      HIP_OK(hipEventRecord(ev_a_, s));
-      HIP_OK(hipStreamWaitEvent(opt_stream_, ev_a_, 0));
-      mnist_adam_fc(a, o, opt_stream_, (int)fc_defer_);
-      HIP_OK(hipEventRecord(ev_opt_a_, opt_stream_));
-      mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
-      mark(P_BCONV, s);
-      mnist_adam_fused(a, o, s, false);
-      mark(P_OPT, s);
-      if (join_end) HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
-      else pending_opt_a_ = true;
-      return;
-    }
-    if (fused && fc_split_) {
-      // fc dW + output-layer grads and then the fc-region Adam on the optimizer stream, beside the
-      // dX GEMM and the conv backward on the main stream (the fc Adam waits for dX, which reads the
-      // old fc1 weights); the conv-region Adam + slab reduce + step bump end the step after the join
-      a.gbf_a = (uint16_t*)gbf_.data_ptr();
-      o.gbf = (const uint16_t*)gbf_.data_ptr();
-      mnist_forward(a, true, s);
-      mark(P_FWD, s);
-      HIP_OK(hipEventRecord(ev_a_, s));
-      HIP_OK(hipStreamWaitEvent(opt_stream_, ev_a_, 0));
-      mnist_backward_a(a, opt_stream_, 1);
-      mnist_backward_a(a, s, 2);
-      mark(P_BFC, s);
-      HIP_OK(hipEventRecord(ev_b_, s));
-      HIP_OK(hipStreamWaitEvent(opt_stream_, ev_b_, 0));
-      mnist_adam_fc(a, o, opt_stream_);
-      mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
-      mark(P_BCONV, s);
-      HIP_OK(hipEventRecord(ev_opt_a_, opt_stream_));
-      HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
-      mnist_adam_fused(a, o, s, false);
-      mark(P_OPT, s);
-      return;
-    }
     // bf16 fc-region gradients (the DP wire format): the fc backward writes 2 B and Adam reads
     // 2 B per gradient instead of 4 + 4 (13 MB less HBM traffic per step)
     const bool gbf_local = fused && local_bf16_grads_;
@@ -479,7 +380,7 @@ class MnistEngine : public torch::CustomClassHolder {
     mnist_backward_a(a, s);
     mark(P_BFC, s);
     a.step_bump = (int64_t*)step_.data_ptr();
-    mnist_backward_b(a, s, ws, ev_fork_, ev_join_);
+    mnist_backward_b(a, s);
     if (fused) {
       mark(P_BCONV, s);
       o.gbf = gbf_local ? (const uint16_t*)gbf_.data_ptr() : nullptr;
@@ -533,7 +434,7 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipStreamWaitEvent(opt_stream_, ev_ag_, 0));
     apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 0, opt_stream_, (const int64_t*)tnext_.data_ptr());
     HIP_OK(hipEventRecord(ev_opt_a_, opt_stream_));
-    mnist_backward_b(a, s, conv_fork_ ? aux_stream_ : nullptr, ev_fork_, ev_join_);
+    mnist_backward_b(a, s);
     mnist_conv_grad_reduce(a, s);
     mark(P_BCONV, s);
     HIP_OK(hipEventRecord(ev_b_, s));
@@ -549,111 +450,10 @@ class MnistEngine : public torch::CustomClassHolder {
     else pending_opt_a_ = true;
   }
 
-  // DP step with sufficient-factor fc gradients, three streams (main s, comm c, optimizer o):
-  //   s: [wait o: previous step's SFB GEMM done with the gathered factors] conv fwd (p2 -> own slot)
-  //      -> [wait o: previous fc optimizer] fc fwd + head (dh / hd / dlogits -> own slot) -> fc1 dX
-  //      -> conv bwd -> conv-slab reduce (bucket B bf16, step bump) -> [wait c] conv-region optimizer
-  //   c: [wait p2] all-gather p2 (overlaps fc fwd + head) -> [wait head] all-gather dh|hd|dlogits
-  //      -> [wait B] all-reduce B
-  //   o: [wait gathers] fc gradients over K = W*B (mnist_fc_grad_sfb) -> [wait dX: it reads the old
-  //      fc1 weights] fc-region optimizer
-  // Cross-step overlap as in train_step_dp: the fc optimizer runs beside the next conv forward.
-  //   With ZeRO-1 on (set_zero), each rank computes only its fc1 shard's dW rows (plus the bias row
-  //   and the output layer), runs the fc optimizer on that shard, and the updated bf16 shards are
-  //   all-gathered at the start of the next step on c, beside the conv forward (the fc forward
-  //   waits for it): the K = W*B GEMM and the fc Adam shrink W-fold for one extra 6.4 MB / W
-  //   weight gather per rank.
-  void train_step_sfb(bool join_end) {
-    hipStream_t s = stream();
-    const double scale = 1.0 / (double)world();
-    const bool bf = bf16_comm_;
-    const bool shard = zero_;
-    const int64_t rk = rank_in_comm();
-    MnistStepArgs a = args();
-    if (shard) {
-      const int64_t rows = zshard_ / HID;  // fc1 weight rows per rank
-      mnist_sfb_tile_rows((int)(rk * rows), (int)((rk + 1) * rows), &a.sfb_by_lo, &a.sfb_by_hi);
-    }
-    a.t_out = (int64_t*)tnext_.data_ptr();
-    a.step_bump = (int64_t*)step_.data_ptr();
-    if (bf) {
-      a.gbf_a = (uint16_t*)gbf_.data_ptr();
-      a.gbf_b = (uint16_t*)gbf_.data_ptr();
-    }
-    mark(P_START, s);
-    if (pending_sfb_) {
-      HIP_OK(hipStreamWaitEvent(s, ev_sfb_, 0));
-      pending_sfb_ = false;
-    }
-    if (shard) {  // last step's updated fc1 bf16 shards -> every rank, beside the conv forward
-      // the main stream takes the (sharded, W-fold smaller) fc optimizer's event first and the comm
-      // stream only the main stream's: a second stream waiting on the optimizer stream's event inside
-      // a multi-step capture crashed the HIP graph capture (host SIGSEGV, bench --zero 1 --fc_sfb 1)
-      if (pending_opt_a_) {
-        HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
-        pending_opt_a_ = false;
-      }
-      HIP_OK(hipEventRecord(ev_start_, s));
-      HIP_OK(hipStreamWaitEvent(comm_stream_, ev_start_, 0));
-      ag_w(comm_stream_);
-      HIP_OK(hipEventRecord(ev_wag_, comm_stream_));
-    }
-    mnist_forward_conv(a, s);
-    HIP_OK(hipEventRecord(ev_p2_, s));
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_p2_, 0));
-    mark(P_CA0, comm_stream_);
-    gather_sfb(true, comm_stream_);
-    if (pending_opt_a_) {
-      HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
-      pending_opt_a_ = false;
-    }
-    if (shard) HIP_OK(hipStreamWaitEvent(s, ev_wag_, 0));
-    mnist_forward_fc(a, true, s);
-    mark(P_FWD, s);
-    HIP_OK(hipEventRecord(ev_a_, s));
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
-    gather_sfb(false, comm_stream_);
-    mark(P_CA1, comm_stream_);
-    HIP_OK(hipEventRecord(ev_ag_, comm_stream_));
-    HIP_OK(hipStreamWaitEvent(opt_stream_, ev_ag_, 0));
-    mnist_fc_grad_sfb(a, opt_stream_);
-    HIP_OK(hipEventRecord(ev_sfb_, opt_stream_));
-    mnist_backward_a(a, s, 2);  // fc1 dX from this rank's own rows
-    mark(P_BFC, s);
-    HIP_OK(hipEventRecord(ev_dx_, s));
-    HIP_OK(hipStreamWaitEvent(opt_stream_, ev_dx_, 0));
-    if (shard) {
-      apply_optimizer_range(OFF_WD1 + rk * zshard_, OFF_WD1 + (rk + 1) * zshard_, scale, 0, opt_stream_,
-                            (const int64_t*)tnext_.data_ptr());
-      apply_optimizer_range(OFF_BD1, TOTAL, scale, 0, opt_stream_, (const int64_t*)tnext_.data_ptr());
-    } else {
-      apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 0, opt_stream_, (const int64_t*)tnext_.data_ptr());
-    }
-    HIP_OK(hipEventRecord(ev_opt_a_, opt_stream_));
-    mnist_backward_b(a, s, conv_fork_ ? aux_stream_ : nullptr, ev_fork_, ev_join_);
-    mnist_conv_grad_reduce(a, s);
-    mark(P_BCONV, s);
-    HIP_OK(hipEventRecord(ev_b_, s));
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
-    mark(P_CB0, comm_stream_);
-    reduce_bucket(0, BUCKET_SPLIT, bf);
-    mark(P_CB1, comm_stream_);
-    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
-    HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
-    apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s);
-    mark(P_OPT, s);
-    if (join_end) {
-      HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));  // after ev_sfb_ on the same stream: covers both
-    } else {
-      pending_opt_a_ = true;
-      pending_sfb_ = true;
-    }
-  }
-
-  // Serialized sufficient-factor step (set_dp_serial, the default): every compute kernel on the
-  // main stream in one order, only the collectives on the comm stream. The overlapped schedule above
-  // (SFB GEMM + fc optimizer on a second stream beside the conv backward and the next conv forward)
-  // measured 124 us/step in the world-1 rehearsal against 74 for the fused one-GPU step: these
+  // DP step with sufficient-factor fc gradients (set_fc_sfb): every compute kernel on the main
+  // stream in one order, only the collectives on the comm stream. The round-2 overlapped schedule
+  // (SFB GEMM + fc optimizer on a second stream beside the conv backward and the next conv forward;
+  // removed in round 3, A/B in profiles/mnist_dp_schedule_ab_r2.log) measured 124 us/step in the world-1 rehearsal against 74 for the fused one-GPU step: these
   // kernels each fill the GPU, so running two of them at once slowed both (conv2 wgrad 10 -> 19 us),
   // as the one-GPU overlap A/Bs showed (profiles/ab_fc_adam_overlap_r2.log).
   //   s: conv fwd -> fc fwd -> head -> fc1 dX -> conv wgrad / dgrad -> conv slab reduce (+ next
@@ -704,7 +504,7 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipEventRecord(ev_ag_, comm_stream_));
     mnist_backward_a(a, s, 2);  // fc1 dX from this rank's own rows
     mark(P_BFC, s);
-    mnist_backward_b(a, s, conv_fork_ ? aux_stream_ : nullptr, ev_fork_, ev_join_);
+    mnist_backward_b(a, s);
     mnist_conv_grad_reduce(a, s);
     mark(P_BCONV, s);
     HIP_OK(hipEventRecord(ev_b_, s));
@@ -848,7 +648,7 @@ class MnistEngine : public torch::CustomClassHolder {
     apply_optimizer_range(OFF_BD1, TOTAL, scale, 1, comm_stream_);
     HIP_OK(hipEventRecord(ev_opt_a_, comm_stream_));
     a.step_bump = (int64_t*)step_.data_ptr();
-    mnist_backward_b(a, s, conv_fork_ ? aux_stream_ : nullptr, ev_fork_, ev_join_);
+    mnist_backward_b(a, s);
     HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
     mnist_conv_grad_reduce(a, s);
     HIP_OK(hipEventRecord(ev_b_, s));
@@ -1177,28 +977,23 @@ class MnistEngine : public torch::CustomClassHolder {
   at::Tensor f1_, f2_, fhd_, fdh_, fdz2_, fdp1m_, fslab_, fwg2_;  // fp32-mode activations / slabs
   bool fp32_ = false;
   hipStream_t comm_stream_ = nullptr;
-  hipEvent_t ev_a_ = nullptr, ev_b_ = nullptr, ev_done_ = nullptr, ev_fork_ = nullptr, ev_join_ = nullptr;
-  hipStream_t aux_stream_ = nullptr, opt_stream_ = nullptr;
+  hipEvent_t ev_a_ = nullptr, ev_b_ = nullptr, ev_done_ = nullptr;
+  hipStream_t opt_stream_ = nullptr;  // train_step_dp: the fc-region optimizer
   hipEvent_t ev_opt_a_ = nullptr, ev_start_ = nullptr, ev_ag_ = nullptr;
   bool zero_ = false;
-  bool dp_serial_ = true;    // train_step_sfb_serial (default) vs the overlapped train_step_sfb
   bool pending_wag_ = false;  // serialized ZeRO: this step's shards not yet all-gathered
   bool wag_issued_ = false;   // ... their all-gather already queued on the comm stream (ev_wag_)
   bool force_dp_ = false;
   int64_t zshard_ = 0;
   bool pending_opt_a_ = false;  // DP: the main stream still has to wait for the fc optimizer
   // sufficient-factor fc gradients (set_fc_sfb): gathered factors, slot stride, events
-  bool sfb_ = false, pending_sfb_ = false;
+  bool sfb_ = false;
   at::Tensor sfp2_, sfdr_;
   int64_t sfb_rs_ = 0;
-  hipEvent_t ev_p2_ = nullptr, ev_dx_ = nullptr, ev_sfb_ = nullptr, ev_wag_ = nullptr;
-  // measured on one MI355X: the forked conv2 wgrad only contends with dgrad for CUs (110 vs 100 us/step)
-  bool conv_fork_ = false;
+  hipEvent_t ev_p2_ = nullptr, ev_wag_ = nullptr;
   // one GPU + Adam: the optimizer kernel also reduces the conv gradient slabs and bumps the step
   bool fuse_tail_ = true;
   bool local_bf16_grads_ = false;
-  bool fc_adam_ = false, fc_adam_fork_ = false, fc_split_ = false;
-  int64_t fc_defer_ = 0;
   bool conv_unfused_ = false;  // measured slower (docs/DESIGN.md)
   std::map<std::string, hipGraphExec_t> graphs_;
   hipEvent_t pev_[P_N] = {};
@@ -1253,12 +1048,8 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("sfb_probe", &MnistEngine::sfb_probe)
       .def("set_force_dp", &MnistEngine::set_force_dp)
       .def("dp", &MnistEngine::dp)
-      .def("set_conv_fork", &MnistEngine::set_conv_fork)
-      .def("set_fc_split", &MnistEngine::set_fc_split)
-      .def("set_fc_defer", &MnistEngine::set_fc_defer)
       .def("set_fused_tail", &MnistEngine::set_fused_tail)
       .def("set_local_bf16_grads", &MnistEngine::set_local_bf16_grads)
-      .def("set_fc_adam", &MnistEngine::set_fc_adam)
       .def("set_conv_unfused", &MnistEngine::set_conv_unfused)
       .def("set_dtype", &MnistEngine::set_dtype)
       .def("dtype", &MnistEngine::dtype)
@@ -1266,7 +1057,6 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("phase_times", &MnistEngine::phase_times)
       .def("zero", &MnistEngine::zero)
       .def("sync_params", &MnistEngine::sync_params)
-      .def("set_dp_serial", &MnistEngine::set_dp_serial)
       .def("world", &MnistEngine::world)
       .def("forward", &MnistEngine::forward)
       .def("backward_a", &MnistEngine::backward_a)

@@ -77,8 +77,7 @@ void mnist_forward_fc(const MnistStepArgs& a, bool train, hipStream_t s);     //
 void mnist_backward_a(const MnistStepArgs& a, hipStream_t s, int part = 0);
 // conv2/conv1 grads -> bucket B done. With `aux` set, independent kernels fork onto it (fork/join
 // events recorded on s/aux; both are captured into the step graph as parallel branches).
-void mnist_backward_b(const MnistStepArgs& a, hipStream_t s, hipStream_t aux = nullptr, hipEvent_t fork = nullptr,
-                      hipEvent_t join = nullptr);
+void mnist_backward_b(const MnistStepArgs& a, hipStream_t s);
 // deterministic conv weight-gradient slab reduction (+ the global_step bump, MnistStepArgs::step_bump)
 void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s);
 
@@ -91,13 +90,9 @@ struct MnistAdamArgs {
   const int64_t* t;
   int64_t* step;
   const uint16_t* gbf;  // if non-null: the fc-region (bucket A) gradients are bf16 here (gbf_a)
-  int fc_only;          // 1: the fc region only (no gather, no step bump; see mnist_adam_fc)
 };
-// fc_region = false: the conv region only (the fc region was updated by mnist_backward_a_adam)
+// fc_region = false: the conv region only
 void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region = true);
-// The fc region alone (`blocks` grid-stride blocks, default 1024), e.g. on a side stream beside the
-// conv backward; mnist_adam_fused(..., fc_region = false) then finishes the step.
-void mnist_adam_fc(const MnistStepArgs& a, MnistAdamArgs o, hipStream_t s, int blocks = 0);
 // DP, sufficient-factor broadcasting: every fc-layer weight gradient is a sum of per-example outer
 // products (dW_fc1 = [P2;1]^T dH, dW_out = [Hd;1]^T dlogits), so the all-reduced gradient is ONE
 // GEMM over the all-gathered factors (K = W*B). Writes the summed fc-region gradients (bucket A)
@@ -107,9 +102,6 @@ void mnist_fc_grad_sfb(const MnistStepArgs& a, hipStream_t s);
 void mnist_sfb_tile_rows(int row0, int row1, int* by_lo, int* by_hi);
 // bf16 elements of one rank's sfb_dr slot for batch B (dh + hd + dlogits, padded to 64)
 int64_t mnist_sfb_slot_elems(int B);
-// One GPU: fc1 dW and the output-layer gradients with ApplyAdam fused into their epilogues (the fc
-// gradients never reach memory; t = global_step + 1). Launch after the dX GEMM (part 2).
-void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s);
 
 // ---------------- reference-precision (fp32) MNIST step: csrc/kernels/mnist_f32.hip ----------------
 // Same dataflow and flat parameter layout as the bf16 step, every operand and activation fp32,

@@ -133,33 +133,37 @@ def test_forced_dp_world1_zero1_tracks_plain_dp(cuda, mode, sfb):
     tr1.close()
 
 
-@pytest.mark.parametrize("mode,zero", [("rccl", False), ("ipc", False), ("rccl", True)])
-def test_serialized_sfb_schedule_equals_overlapped(cuda, mode, zero):
-    """The serialized DP step (default: every compute kernel on the main stream, collectives on
-    the comm stream) against the overlapped three-stream schedule: identical kernels and data, so
-    the parameters, Adam state and bf16 shadow agree bit for bit after eager + captured steps."""
+@pytest.mark.parametrize("mode,sfb,zero", [("rccl", True, False), ("ipc", True, False), ("rccl", True, True),
+                                           ("rccl", False, False), ("rccl", False, True)])
+def test_dp_schedules_captured_equal_eager(cuda, mode, sfb, zero):
+    """Every DP schedule that remains (SFB serialized step, with and without ZeRO-1; bucketed
+    all-reduce step, with and without reduce-scatter ZeRO-1), forced at world 1 over the real
+    communicator: multi-step hipGraphs with captured collectives replay exactly the eager steps --
+    parameters, Adam state and bf16 shadow bit for bit."""
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
-        params, (ov, se) = _engines_on_dataset(cuda, 2)
+        params, (gr, ea) = _engines_on_dataset(cuda, 2)
         trs = []
-        for e, serial in ((ov, 0), (se, 1)):
-            trs.append(attach_engine(e, 0, 1, cuda, mode=mode, force_dp=True, sfb=True))
-            e.set_dp_serial(serial)
+        for e in (gr, ea):
+            trs.append(attach_engine(e, 0, 1, cuda, mode=mode, force_dp=True, sfb=sfb))
             if zero:
                 e.set_zero(True)
             e.train_step()
             e.train_step()
-            e.capture_train_steps("t", 3)
-            e.replay("t", 2)
+        gr.capture_train_steps("t", 3)
+        gr.replay("t", 2)
+        for _ in range(6):
+            ea.train_step()
+        for e in (gr, ea):
             e.sync_params()
     torch.cuda.synchronize()
     for tr in trs:
         tr.check()
-    assert int(se.step_tensor().item()) == int(ov.step_tensor().item()) == 8
-    assert torch.equal(se.params(), ov.params()) and torch.equal(se.adam_v(), ov.adam_v())
-    assert torch.equal(se.params_bf16(), ov.params_bf16())
+    assert int(gr.step_tensor().item()) == int(ea.step_tensor().item()) == 8
+    assert torch.equal(gr.params(), ea.params()) and torch.equal(gr.adam_v(), ea.adam_v())
+    assert torch.equal(gr.params_bf16(), ea.params_bf16())
     for tr in trs:
         tr.close()
 
