@@ -145,6 +145,17 @@ __global__ void axpy_kernel(float* __restrict__ d, const float* __restrict__ s, 
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) d[i] += alpha * s[i];
 }
 
+// plain fp32 copy, float4 per lane when both ends are 16-B aligned (IPC peer buffers of the GPU
+// parameter server, csrc/runtime/gpu_ps.cpp)
+__global__ void copy_f32_kernel(float* __restrict__ d, const float* __restrict__ s, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool v4 = ((reinterpret_cast<uintptr_t>(d) | reinterpret_cast<uintptr_t>(s)) & 15) == 0;
+  const int64_t n4 = v4 ? n >> 2 : 0;
+  for (int64_t i = i0; i < n4; i += stride) reinterpret_cast<f32x4*>(d)[i] = reinterpret_cast<const f32x4*>(s)[i];
+  for (int64_t i = (n4 << 2) + i0; i < n; i += stride) d[i] = s[i];
+}
+
 inline int blocks_for(int64_t n, int per_thread) {
   const int64_t b = (n / per_thread + kOptThreads - 1) / kOptThreads;
   return (int)(b < 1 ? 1 : (b > kOptMaxBlocks ? kOptMaxBlocks : b));
@@ -177,6 +188,9 @@ void cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s) {
 }
 void cast_bf16_f32(const uint16_t* x, float* y, int64_t n, float scale, hipStream_t s) {
   cast_bf16_f32_kernel<<<blocks_for(n, 1), kOptThreads, 0, s>>>(x, y, n, scale);
+}
+void copy_f32(float* dst, const float* src, int64_t n, hipStream_t s) {
+  if (n > 0) copy_f32_kernel<<<blocks_for(n, 4), kOptThreads, 0, s>>>(dst, src, n);
 }
 void scale_f32(float* x, int64_t n, float scale, hipStream_t s) {
   scale_kernel<<<blocks_for(n, 1), kOptThreads, 0, s>>>(x, n, scale);

@@ -222,6 +222,7 @@ class NativeMnistRunner(MnistRunnerBase):
         self.stream = torch.cuda.Stream(self.device)
         self.use_graph = use_graph
         self._graph_ready = False
+        self._grads_graph = False
         self._x_stage = torch.empty(batch_size, 784, dtype=torch.float32).pin_memory()
         self._y_stage = torch.empty(batch_size, dtype=torch.int32).pin_memory()
         self.transport = None  # parallel.transport.DPTransport when DP runs over RCCL/IPC
@@ -380,16 +381,34 @@ class NativeMnistRunner(MnistRunnerBase):
             # the pinned staging buffers are reused next step: wait for the H2D copies to land
             self.stream.synchronize()
 
-    def compute_grads(self, x, y) -> Tuple[torch.Tensor, float]:
-        """Forward + backward only (no reduction / optimizer). Bumps the engine's local step."""
+    def compute_grads(self, x, y, with_loss: bool = True) -> Tuple[torch.Tensor, Optional[float]]:
+        """Forward + backward only (no reduction / optimizer). Bumps the engine's local step. With
+        ``use_graph`` the three launches replay as one captured graph (``MnistEngine.capture_grads``).
+        ``with_loss=False`` skips the loss read-back (no device-to-host transfer)."""
         self._feed(x, y)
         with torch.cuda.stream(self.stream):
-            self.eng.forward(True)
-            self.eng.backward_a()
-            self.eng.backward_b()
+            if self.use_graph:
+                if not self._grads_graph:
+                    self.eng.forward(True)
+                    self.eng.backward_a()
+                    self.eng.backward_b()
+                    self.eng.capture_grads("grads")
+                    self._grads_graph = True
+                else:
+                    self.eng.replay("grads", 1)
+            else:
+                self.eng.forward(True)
+                self.eng.backward_a()
+                self.eng.backward_b()
         self.stream.synchronize()
         self._hstep += 1
-        return self.eng.grads(), float(self.eng.loss_rows().mean().item())
+        return self.eng.grads(), (float(self.eng.loss_rows().mean().item()) if with_loss else None)
+
+    def sync_shadow(self) -> None:
+        """Re-derive the bf16 operand shadow from the fp32 master (after a parameter server wrote the
+        fresh values into ``params()``)."""
+        with torch.cuda.stream(self.stream):
+            self.eng.sync_shadow()
 
     def reduce_grads(self, weight: float = 1.0) -> None:
         """Sum-all-reduce of (weight * local grads) over the worker communicator."""

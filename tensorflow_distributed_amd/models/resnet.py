@@ -95,14 +95,20 @@ class BucketReducer:
     """Contiguous gradient buckets of ~``bucket_bytes``; a bucket's all-reduce is launched on the
     comm stream the moment its last parameter gradient has been written (backward overlap)."""
 
-    def __init__(self, fp: FlatParams, comm=None, bucket_bytes: int = 8 << 20, bf16: bool = False):
+    def __init__(self, fp: FlatParams, comm=None, bucket_bytes: int = 8 << 20, bf16: bool = False,
+                 force_dp: bool = False):
+        """``force_dp``: run the DP schedule (comm stream, per-bucket bf16 casts and collectives,
+        1/N in the optimizer) even when the communicator has ONE rank -- the exact multi-GPU code
+        path, rehearsed on a one-GPU box over a real world-1 RcclComm (MnistEngine.set_force_dp's
+        analogue)."""
         self.fp = fp
         self.comm = comm
         self.world = comm.world() if comm is not None else 1
+        dp = comm is not None and (self.world > 1 or force_dp)
         self.buckets: List[Tuple[int, int]] = []
         self.bucket_of: Dict[str, int] = {}
         cur_lo, cur_n = 0, 0
-        elt = 2 if (bf16 and comm is not None and self.world > 1) else 4  # wire bytes per gradient
+        elt = 2 if (bf16 and dp) else 4  # wire bytes per gradient
         order = list(reversed(fp.specs))  # flat-buffer order
         for s in order:
             if cur_n and (s.offset + s.numel - cur_lo) * elt > bucket_bytes:
@@ -115,7 +121,7 @@ class BucketReducer:
         for s in fp.specs:
             self.need[self.bucket_of[s.name]] += 1
         self.count = [0] * len(self.buckets)
-        self.stream = torch.cuda.Stream(fp.device) if (comm is not None and self.world > 1) else None
+        self.stream = torch.cuda.Stream(fp.device) if dp else None
         self.events = []
         self.launched = 0
         # bf16 wire format halves the all-reduce bytes; the optimizer reads the bf16 sums directly
@@ -458,8 +464,8 @@ class ResNet:
     def num_params(self) -> int:
         return sum(s.numel for s in self.specs)
 
-    def set_comm(self, comm, bucket_mb: float = 8.0, bf16_grads: bool = True):
-        self.reducer = BucketReducer(self.fp, comm, int(bucket_mb * (1 << 20)), bf16=bf16_grads)
+    def set_comm(self, comm, bucket_mb: float = 8.0, bf16_grads: bool = True, force_dp: bool = False):
+        self.reducer = BucketReducer(self.fp, comm, int(bucket_mb * (1 << 20)), bf16=bf16_grads, force_dp=force_dp)
 
     def forward(self, x_nhwc_f32: torch.Tensor) -> torch.Tensor:
         for j in self.joins:

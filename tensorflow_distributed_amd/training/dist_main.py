@@ -110,6 +110,11 @@ def define_flags(task_index_default: int = 0, job_name_default: str = "ps") -> N
                    "generic bucket reducer (--model resnet*)")
     f.DEFINE_enum("model", "mnist_cnn", ["mnist_cnn", "resnet18", "resnet50"], "Model: the reference CNN, or the "
                   "synthetic-ImageNet ResNet family (BASELINE configs 4-5; trained by bench_resnet.py)")
+    f.DEFINE_boolean("ps_on_gpu", True, "Parameter-server modes (async, backup workers) with --num_gpus > 0: each "
+                     "ps task keeps its variables, optimizer slots and accumulator on GPU task_index % num_gpus; "
+                     "workers push gradients into its GPU mailbox and the ps writes fresh values straight into "
+                     "the workers' engine parameters (IPC peer memory, no host copies). False = the reference's "
+                     "CPU ps (ps_device=/job:ps/cpu:0)")
     f.DEFINE_boolean("device_input", True, "GPU: upload the training split once and index it on the device "
                      "by a per-epoch shuffle (no per-step host feed); False = host next_batch + H2D per step")
 
@@ -244,7 +249,15 @@ def main(argv=None) -> int:
         # (reference quirk Q9: ps + existing_servers fell through to the worker code; a PS here
         #  always serves and then exits once every worker has finished)
         service = None
-        if ps_mode:
+        if ps_mode and FLAGS.ps_on_gpu and FLAGS.num_gpus > 0 and FLAGS.model == "mnist_cnn":
+            from ..parallel.gpu_ps import GpuParameterServerService
+
+            ps_gpu = FLAGS.task_index % FLAGS.num_gpus
+            torch.cuda.set_device(ps_gpu)
+            service = GpuParameterServerService(FLAGS.task_index, cluster.num_ps, num_workers, layout, opt,
+                                                torch.device("cuda", ps_gpu), sync=backup_ps,
+                                                replicas_to_aggregate=r2a)
+        elif ps_mode:
             service = async_ps.ParameterServerService(FLAGS.task_index, cluster.num_ps, num_workers, layout, opt,
                                                       sync=backup_ps, replicas_to_aggregate=r2a)
         server.join(service)
@@ -270,7 +283,7 @@ def main(argv=None) -> int:
 
     runner = make_runner(FLAGS.batch_size, opt, device, keep_prob=FLAGS.keep_prob, seed=FLAGS.seed,
                          rank=FLAGS.task_index, comm=None, bf16_grads=FLAGS.bf16_grads,
-                         use_graph=FLAGS.use_graph and (sopt is None or not sopt.has_backup_workers),
+                         use_graph=FLAGS.use_graph and (sopt is None or not sopt.has_backup_workers or backup_ps),
                          dtype=FLAGS.dtype)
     comm = None
     transport = None
@@ -296,10 +309,27 @@ def main(argv=None) -> int:
         runner.load_flat(flat, {}, 0)
 
     client = None
+    gpu_ps = ps_mode and FLAGS.ps_on_gpu and device.type == "cuda"
     if not ps_mode:
         def broadcast_fn():
             if num_workers > 1:
                 sync_replicas.broadcast_state(runner, 0, group=server.worker_group, group_src_rank=cluster.num_ps)
+    elif gpu_ps:
+        from ..parallel.gpu_ps import GpuPSClient
+        from .optimizers import FlatApplier
+
+        client = GpuPSClient(FLAGS.task_index, layout, runner.params(), runner.sync_shadow,
+                             slot_names=list(FlatApplier(opt, 0).slots()))
+        runner.ps_client = client  # the chief's checkpoints read the PS-resident state (params + slots)
+
+        def broadcast_fn():
+            if is_chief:
+                # the ps tasks read the initial / restored values from the chief's engine (peer memory);
+                # restored moments follow as host tensors, fresh ones start at zero
+                slots = {("m" if k == "accum" else k): v.detach().float().cpu()
+                         for k, v in runner.slot_tensors().items()} if sv.restored_from else None
+                client.init(step=runner.global_step(), t=runner.global_step(), slots=slots)
+            runner.set_global_step(client.pull())
     else:
         from .optimizers import FlatApplier
 
@@ -340,10 +370,15 @@ def main(argv=None) -> int:
         wdev = "/job:worker/task:%d/%s:%d" % (FLAGS.task_index, "gpu" if device.type == "cuda" else "cpu",
                                               device.index or 0)
         placed = replica_device_setter(cluster, names, wdev) if ps_mode else {n: wdev + " (replicated)" for n in names}
+        if gpu_ps:  # each ps task's shard lives on its GPU (task % num_gpus), not on the reference's ps cpu
+            from ..parallel.cluster import ps_task_of
+
+            placed = {n: "/job:ps/task:%d/gpu:%d" % (ps_task_of(placed, n), ps_task_of(placed, n) % FLAGS.num_gpus)
+                      for n in names}
         for n in names:
             print("%s: %s" % (n, placed[n]))
         print("compute (conv_net, loss, gradients): %s; gradient sync: %s" % (
-            wdev, ("async PS push/pull" if not sync else
+            wdev, (("GPU ps mailbox push / peer-memory pull" if gpu_ps else "async PS push/pull") if not sync else
                    "PS accumulator (%d of %d replicas)" % (r2a, num_workers) if backup_ps else
                    (transport.kind.replace("+sfb", "") + " all-reduce"
                     + (" (fc layers: all-gathered sufficient factors)" if "+sfb" in transport.kind else ""))
@@ -390,6 +425,14 @@ def main(argv=None) -> int:
             if not ps_mode:
                 stepper.step(batch_xs, batch_ys)
                 step = runner.global_step()
+            elif gpu_ps:
+                g, _ = runner.compute_grads(batch_xs, batch_ys, with_loss=False)
+                if FLAGS.task_index in delays:
+                    time.sleep(delays[FLAGS.task_index])  # test hook: a straggling worker
+                # the gradient goes GPU -> the ps tasks' GPU mailboxes, the fresh values come back into
+                # the engine's parameters; only the 32-byte control messages touch the host
+                step = client.push_pull(g, local_step=step)
+                runner.set_global_step(step)
             else:
                 g, _ = runner.compute_grads(batch_xs, batch_ys)
                 if grad_cpu is None:

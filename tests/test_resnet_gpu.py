@@ -194,3 +194,50 @@ def test_resnet_graph_capture(cuda):
         g.replay()
         vals.append(out.item())
     assert all(v == v for v in vals) and vals[-1] < vals[0] + 1.0
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_resnet_rccl_bucketed_world1_equals_no_comm(cuda, bf16):
+    """The ResNet DP path (BucketReducer: comm stream, per-bucket collectives launched from inside
+    the backward, 1/N in the fused SGD) forced at world 1 over a REAL RcclComm, eager and captured
+    in a CUDA graph: the world-1 sum is the identity, so the parameters equal the no-communicator
+    step bit for bit -- with the bf16 wire, the one whose optimizer reads bf16-rounded gradients (a
+    bucket cast before its last gradient landed would show up here)."""
+    from tensorflow_distributed_amd import _native
+    from tensorflow_distributed_amd.models.resnet import ResNet
+
+    _native.require()
+    uid = torch.classes.tfd.RcclComm.unique_id()
+    comm = torch.classes.tfd.RcclComm(uid, 1, 0, cuda.index)
+    x = torch.randn(8, 32, 32, 3, device=cuda)
+    lab = torch.randint(0, 16, (8,), dtype=torch.int32, device=cuda)
+    ms = []
+    for dp in (False, True):
+        m = ResNet(18, num_classes=16, device=cuda, seed=5, width=16)
+        if dp:
+            m.set_comm(comm, bucket_mb=0.05, bf16_grads=bf16, force_dp=True)
+            assert m.reducer.stream is not None and len(m.reducer.buckets) > 3
+        elif bf16:  # the reference step reads its gradients rounded to bf16, as the wire delivers them
+            fp = m.fp
+            m.reducer.reduced_grads = lambda fp=fp: fp.grad.to(torch.bfloat16)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                m.train_step(x, lab, lr=0.01)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            m.train_step(x, lab, lr=0.01)
+        for _ in range(2):
+            g.replay()
+        torch.cuda.synchronize()
+        if dp:
+            assert m.reducer.launched == len(m.reducer.buckets)
+        ms.append(m)
+    p0, p1 = ms[0].fp.master, ms[1].fp.master
+    assert torch.isfinite(p1).all()
+    if not torch.equal(p0, p1):
+        bad = (p0 != p1).nonzero().flatten()
+        names = sorted({s.name for s in ms[0].fp.specs for i in bad[:64].tolist() if s.offset <= i < s.offset + s.numel})
+        raise AssertionError(f"{bad.numel()} parameters differ (first in {names[:8]})")
