@@ -80,11 +80,6 @@ def main(argv=None):
                     "conv weight-gradient slabs and bumps the step (one kernel less)")
     ap.add_argument("--local_bf16_grads", type=int, default=1, help="1: on one GPU keep the fc-region gradients "
                     "in bf16 (the DP all-reduce wire format): fc backward writes and Adam reads 2 B per gradient")
-    ap.add_argument("--wg2_bf16", type=int, default=0, help="1: conv2 weight-gradient split-K slabs in bf16 (the "
-                    "gradient wire precision; partials still summed in fp32): half the slab bytes")
-    ap.add_argument("--defer_fc1_adam", type=int, default=0, help="1: one GPU, the fc1-weight ApplyAdam of step t "
-                    "runs inside step t+1's fc1 forward (the kernel that reads W1 next), flushed at the end of each "
-                    "captured step sequence")
     ap.add_argument("--conv_unfused", type=int, default=0, help="1: conv1 and conv2 forward as two kernels "
                     "(A/B of the fused conv1->conv2 kernel)")
     ap.add_argument("--state_steps", type=int, default=100, help="time the steps that follow this many training "
@@ -124,10 +119,6 @@ def main(argv=None):
     eng.set_fused_tail(a.fused_tail)
     eng.set_local_bf16_grads(a.local_bf16_grads)
     eng.set_conv_unfused(a.conv_unfused)
-    if a.wg2_bf16:  # (only when asked: older A/B variant libraries lack the setters)
-        eng.set_wg2_bf16(1)
-    if a.defer_fc1_adam:
-        eng.set_defer_fc1_adam(1)
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     mode = a.transport

@@ -25,6 +25,7 @@
 #include "../gemm.h"
 #include "../mnist_layout.h"
 #include "../tfd_kernels.h"
+#include "../c2wl_perm.h"
 
 #include <algorithm>
 #include <stdexcept>
@@ -409,7 +410,10 @@ __global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
 // half's loads are issued FIRST and stay in flight behind the conv1 arithmetic; they are written
 // to LDS after it. One launch and one activation round trip less than conv1_pool_fwd +
 // conv2_fwd_lds. LDS: p1 image 27 KiB + W2 half 75 KiB + x / W1 staging 7.5 KiB.
-constexpr int C12_XS = 36;                                   // x image row stride (floats): fewer bank conflicts than 32
+#ifndef TFD_C12_XS
+#define TFD_C12_XS 36
+#endif
+constexpr int C12_XS = TFD_C12_XS;                           // x image row stride (floats): fewer bank conflicts than 32
 constexpr int C12_XR = 60;                                   // rows: 32 (zero-bordered 28 x 28) + 28 zero rows
 constexpr int C12_XZ = 32 * C12_XS;                          // a padded tap (k >= 25): lands in the zero rows for any pixel
 constexpr int C12_XOFF = C2L_FWD_SMEM;                       // fp32 [C12_XR][C12_XS] x image
@@ -708,130 +712,6 @@ __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   gemm_block<FC1_BM, FC1_BN, FC1_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, blockIdx.y * FC1_BM, blockIdx.x * FC1_BN, kb, ke,
                                            (bf16*)smem_raw);
 #endif
-}
-
-// ---------------- K4 + K16 (one GPU): fc1 forward with the previous step's fc1-weight Adam ----------------
-// The fc1 weight W1 [3136][1024] is 98 % of the parameters, so its ApplyAdam is most of the
-// optimizer's HBM traffic. Its update for step t is deferred into step t + 1's fc1 forward, the
-// first kernel that reads W1 again: block (split z, 32-column tile nt) owns the W1 tile
-// [448 z, +448) x [32 nt, +32) -- each weight belongs to exactly one block (BM = 128 covers the
-// whole batch) -- loads its fp32 master / m / v and bf16 gradient, applies TF ApplyAdam
-// (t = *a.step: the previous step's t, the step bump already happened), writes master / m / v /
-// bf16 shadow back and puts the updated bf16 tile straight into LDS as the MFMA B operand. This
-// removes the separate pass's re-read of the shadow and one kernel boundary; the numbers are the
-// fused-tail Adam's bit for bit (same expression order) and the slabs fc1_fwd's (same K order).
-// apply = 0: the B tile comes from the bf16 shadow (no pending update).
-// LDS: A = p2 rows [128][464] bf16 (pitch 464: conflict-free ds_read_b128 fragments), B = the W
-// tile [448][32] bf16 with odd 8-row groups' 16-column halves swapped (conflict-free
-// ds_read_b64_tr_b16 fragments; scripts/debug/lds_banks.py model).
-constexpr int FA_BM = 128, FA_BN = 32, FA_SPLITS = 7, FA_KPER = FEAT / FA_SPLITS;  // 448
-constexpr int FA_NT = HID / FA_BN;                                                   // 32
-constexpr int FA_AROW = FA_KPER + 16;                                                // 464
-constexpr int FA_SMEM = (FA_BM * FA_AROW + FA_KPER * FA_BN) * 2;                     // 147456 B
-constexpr int FA_F4 = FA_KPER * FA_BN / 4 / 256;                                     // 14 float4 per thread
-constexpr int FA_AC = FA_BM * FA_KPER / 8 / 256;                                     // 28 A chunks per thread
-static_assert(FA_KPER * FA_SPLITS == FEAT && FA_KPER % 32 == 0 && FA_F4 * 256 * 4 == FA_KPER * FA_BN, "fc1+adam tiling");
-static_assert(OFF_WD1 % 4 == 0 && FA_SMEM <= 160 * 1024, "fc1+adam layout");
-__device__ __forceinline__ int fa_bidx(int row, int col) { return row * FA_BN + (col ^ (((row >> 3) & 1) << 4)); }
-__global__ __launch_bounds__(256) void fc1_fwd_adam(MnistStepArgs a, MnistAdamArgs o, int apply) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  bf16* As = (bf16*)smem_raw;
-  bf16* Bs = As + FA_BM * FA_AROW;
-  // XCD-grouped order: workgroup b runs on XCD b % 8; the 28 workgroups of one XCD take a
-  // contiguous range of (split, tile) pairs, so each XCD's L2 pulls at most two A panels
-  const int L = (blockIdx.x & 7) * (FA_NT * FA_SPLITS / 8) + (blockIdx.x >> 3);
-  const int z = L / FA_NT, nt = L - z * FA_NT, kb = z * FA_KPER, n0 = nt * FA_BN;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  // A panel: rows 0..B-1 of p2, k in [kb, kb + 448): loads issued first, stored after the W tile
-  uint4 va[FA_AC];
-#pragma unroll
-  for (int c = 0; c < FA_AC; ++c) {
-    const int idx = t + 256 * c, row = idx / (FA_KPER / 8), kc = idx - row * (FA_KPER / 8);
-    va[c] = row < a.B ? *reinterpret_cast<const uint4*>(a.p2 + (size_t)row * FEAT + kb + kc * 8) : zero4();
-  }
-  const int64_t e40 = (OFF_WD1 + (int64_t)kb * HID + n0) / 4;  // float4 index of the tile's (0, 0)
-  if (apply) {
-    const int64_t tt = *a.step;
-    const float b1p = powf(o.beta1, (float)tt), b2p = powf(o.beta2, (float)tt);
-    const float lr_t = o.lr * sqrtf(1.f - b2p) / (1.f - b1p);
-    const float c1 = 1.f - o.beta1, c2 = 1.f - o.beta2;
-    constexpr int U = 7;
-#pragma unroll
-    for (int i0 = 0; i0 < FA_F4; i0 += U) {
-      f32x4 p[U], m[U], v[U];
-      uint2 h[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int f = t + 256 * (i0 + u), row = f >> 3, c4 = f & 7;
-        const int64_t e4 = e40 + (int64_t)row * (HID / 4) + c4;
-        p[u] = reinterpret_cast<const f32x4*>(o.p)[e4];
-        m[u] = reinterpret_cast<const f32x4*>(o.m)[e4];
-        v[u] = reinterpret_cast<const f32x4*>(o.v)[e4];
-        h[u] = reinterpret_cast<const uint2*>(o.gbf)[e4];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int f = t + 256 * (i0 + u), row = f >> 3, c4 = f & 7;
-        const int64_t e4 = e40 + (int64_t)row * (HID / 4) + c4;
-        const f32x4 g = f32x4{__uint_as_float(h[u].x << 16), __uint_as_float(h[u].x & 0xFFFF0000u),
-                              __uint_as_float(h[u].y << 16), __uint_as_float(h[u].y & 0xFFFF0000u)};
-        m[u] = m[u] + (g - m[u]) * c1;
-        v[u] = v[u] + (g * g - v[u]) * c2;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) p[u][j] -= lr_t * m[u][j] / (sqrtf(v[u][j]) + o.eps);
-        reinterpret_cast<f32x4*>(o.p)[e4] = p[u];
-        reinterpret_cast<f32x4*>(o.m)[e4] = m[u];
-        reinterpret_cast<f32x4*>(o.v)[e4] = v[u];
-        const uint2 pb = make_uint2(pack_bf2(p[u][0], p[u][1]), pack_bf2(p[u][2], p[u][3]));
-        reinterpret_cast<uint2*>(o.pbf)[e4] = pb;
-        *reinterpret_cast<uint2*>(Bs + fa_bidx(row, 4 * c4)) = pb;
-      }
-    }
-  } else {
-    uint2 pb[FA_F4];
-#pragma unroll
-    for (int i = 0; i < FA_F4; ++i) {
-      const int f = t + 256 * i, row = f >> 3, c4 = f & 7;
-      pb[i] = reinterpret_cast<const uint2*>(a.pbf)[e40 + (int64_t)row * (HID / 4) + c4];
-    }
-#pragma unroll
-    for (int i = 0; i < FA_F4; ++i) {
-      const int f = t + 256 * i, row = f >> 3, c4 = f & 7;
-      *reinterpret_cast<uint2*>(Bs + fa_bidx(row, 4 * c4)) = pb[i];
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < FA_AC; ++c) {
-    const int idx = t + 256 * c, row = idx / (FA_KPER / 8), kc = idx - row * (FA_KPER / 8);
-    *reinterpret_cast<uint4*>(As + row * FA_AROW + kc * 8) = va[c];
-  }
-  __syncthreads();
-  // wave w: rows [32 w, 32 w + 32) x all 32 columns; the 14 K-steps of 32 in order (as fc1_fwd)
-  const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kk = 0; kk < FA_KPER; kk += 32) {
-    bf16x8 af[2], bfr[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      af[i] = *reinterpret_cast<const bf16x8*>(As + (32 * w + 16 * i + (lane & 15)) * FA_AROW + kk + 8 * g);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r0 = kk + 8 * g + q;
-      bfr[j] = frag_tr16(Bs + fa_bidx(r0, 16 * j + 4 * p4), Bs + fa_bidx(r0 + 4, 16 * j + 4 * p4));
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
-  }
-  SlabEpi epi{a.fc1_slab + (size_t)z * a.B * HID, HID, a.B, HID};
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) epi(32 * w + 16 * i + 4 * g, n0 + 16 * j + (lane & 15), acc[i][j]);
 }
 
 // ---------------- K4-K9 head: reduce slabs, bias, relu, dropout, FC10, softmax-xent, bwd ----------
@@ -1648,6 +1528,9 @@ __global__ __launch_bounds__(256) void conv2_wgrad_k(MnistStepArgs a, int kper) 
 #ifndef TFD_C2WL_NTG
 #define TFD_C2WL_NTG 4
 #endif
+#ifndef TFD_C2WL_PERM  // 1: K (pixel) order grouped by LDS bank class (csrc/c2wl_perm.h): conflict-free
+#define TFD_C2WL_PERM 1  //    A-fragment tr-reads (MI355X LDS model 1968 -> 1344 cycles per image)
+#endif
 constexpr int C2WL_IMG = TFD_C2WL_IMG;      // images per block (= slab count B / C2WL_IMG)
 constexpr int C2WL_NTG = TFD_C2WL_NTG;      // tap groups (4: [0,6) [6,12) [12,18) [18,25))
 constexpr int C2WL_TPG = 25 / C2WL_NTG;     // taps per group (the last takes the remainder)
@@ -1675,16 +1558,30 @@ __global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) {
       d[0] = zero4(); d[1] = zero4(); d[2] = zero4(); d[3] = zero4();
     }
   }
+#if TFD_C2WL_PERM
+  for (int i = t; i < (C2WL_KP - 196) * (C2WL_DS / 8); i += 512)
+    reinterpret_cast<uint4*>(dz + c2wl_pad[i / (C2WL_DS / 8)] * C2WL_DS)[i % (C2WL_DS / 8)] = zero4();
+#else
   for (int i = t; i < (C2WL_KP - 196) * (C2WL_DS / 8); i += 512) reinterpret_cast<uint4*>(dz + 196 * C2WL_DS)[i] = zero4();
-  // padded-image positions of this lane's two tr-read rows (pixels 32s + 8g + q and +4) per k-step
+#endif
+  // padded-image positions of this lane's two tr-read rows (k-slots 32s + 8g + q and +4) per k-step
   int pos[7][2];
 #pragma unroll
   for (int s = 0; s < 7; ++s)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int k = 32 * s + 8 * g + q + 4 * u;
+#if TFD_C2WL_PERM
+      pos[s][u] = c2wl_kpos[k];  // pad slots: a border position of the missing bank class (dz2 row zero)
+#else
       pos[s][u] = k < 196 ? (k / 14) * C2WL_PW + (k % 14) : 0;  // pad pixels: dz2 rows are zero
+#endif
     }
+#if TFD_C2WL_PERM
+  int dzrow[4];  // the LDS (k-slot) row of each dz2 chunk this thread stages
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dzrow[j] = c2wl_row[min((t + 512 * j) >> 3, 195)];
+#endif
   f32x4 acc[C2WL_MAXT];
 #pragma unroll
   for (int j = 0; j < C2WL_MAXT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1717,13 +1614,17 @@ __global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int i = t + 512 * j;
+#if TFD_C2WL_PERM
+        if (i < 1568) *reinterpret_cast<uint4*>(dz + dzrow[j] * C2WL_DS + (i & 7) * 8) = v2[j];
+#else
         if (i < 1568) *reinterpret_cast<uint4*>(dz + (i >> 3) * C2WL_DS + (i & 7) * 8) = v2[j];
+#endif
       }
     }
     __syncthreads();
     if (ii + 1 < C2WL_IMG && b + 1 < a.B) gload(b + 1);
     if (tg == 0) {  // bias row: column sums of dz2 (pixel slice t >> 6 of 8)
-      for (int px = t >> 6; px < 196; px += 8) bsum += bf2f(dz[px * C2WL_DS + (t & 63)]);
+      for (int px = t >> 6; px < (TFD_C2WL_PERM ? C2WL_KP : 196); px += 8) bsum += bf2f(dz[px * C2WL_DS + (t & 63)]);
     }
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
@@ -1741,33 +1642,12 @@ __global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) {
     }
   }
   float* slab = a.wg2_slab + (size_t)ip * 801 * 64;
-  uint16_t* slabh = reinterpret_cast<uint16_t*>(a.wg2_slab) + (size_t)ip * 801 * 64;
-  if (a.wg2_bf16) {
-    // bf16 slab: lanes l and l ^ 1 hold columns c, c + 1 of the same 4 rows; each sends the other the
-    // two rows it does not store, so the even lane writes rows 0-1 and the odd lane rows 2-3 as
-    // bf16 pairs (4-B stores of adjacent columns)
-    const bool odd = lane & 1;
-    const int c0 = 16 * n + (lane & 14);
 #pragma unroll
-    for (int j = 0; j < C2WL_MAXT; ++j) {
-      const float s0 = __shfl_xor(odd ? acc[j][0] : acc[j][2], 1, 64);
-      const float s1 = __shfl_xor(odd ? acc[j][1] : acc[j][3], 1, 64);
-      if (j < ntaps) {
-        const int row = (tap0 + j) * 32 + 16 * h + 4 * g + (odd ? 2 : 0);
-        const uint32_t w0 = odd ? pack_bf2(s0, acc[j][2]) : pack_bf2(acc[j][0], s0);
-        const uint32_t w1 = odd ? pack_bf2(s1, acc[j][3]) : pack_bf2(acc[j][1], s1);
-        *reinterpret_cast<uint32_t*>(slabh + (size_t)row * 64 + c0) = w0;
-        *reinterpret_cast<uint32_t*>(slabh + (size_t)(row + 1) * 64 + c0) = w1;
-      }
-    }
-  } else {
+  for (int j = 0; j < C2WL_MAXT; ++j) {
+    if (j < ntaps) {
+      const int tap = tap0 + j;
 #pragma unroll
-    for (int j = 0; j < C2WL_MAXT; ++j) {
-      if (j < ntaps) {
-        const int tap = tap0 + j;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) slab[(size_t)(tap * 32 + 16 * h + 4 * g + r) * 64 + 16 * n + (lane & 15)] = acc[j][r];
-      }
+      for (int r = 0; r < 4; ++r) slab[(size_t)(tap * 32 + 16 * h + 4 * g + r) * 64 + 16 * n + (lane & 15)] = acc[j][r];
     }
   }
   if (tg == 0) {
@@ -1777,8 +1657,7 @@ __global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) {
       float sm = 0.f;
 #pragma unroll
       for (int sl = 0; sl < 8; ++sl) sm += bred[sl * 64 + t];
-      if (a.wg2_bf16) slabh[800 * 64 + t] = f2bf_bits(sm);
-      else slab[800 * 64 + t] = sm;
+      slab[800 * 64 + t] = sm;
     }
   }
 }
@@ -1847,16 +1726,8 @@ __global__ __launch_bounds__(256) void conv1_wgrad(MnistStepArgs a) {
 
 // Deterministic slab reductions of both conv weight-gradient slab sets in ONE launch:
 // thread (x = output column of a 64-wide chunk, y = slab phase 0..3); fixed summation order.
-struct SlabF32 {
-  const float* p;
-  __device__ __forceinline__ float operator()(size_t i) const { return p[i]; }
-};
-struct SlabBf16 {
-  const uint16_t* p;
-  __device__ __forceinline__ float operator()(size_t i) const { return bf2f(p[i]); }
-};
-template <int XW, class SL>  // XW outputs per block row, 256/XW slab phases
-__device__ __forceinline__ void reduce_chunk(const SL slab, int nslab, int64_t stride, int n, int i0,
+template <int XW>  // XW outputs per block row, 256/XW slab phases
+__device__ __forceinline__ void reduce_chunk(const float* __restrict__ slab, int nslab, int64_t stride, int n, int i0,
                                              float* __restrict__ out, uint16_t* __restrict__ outbf, float* red) {
   constexpr int NY = 256 / XW;
   const int x = threadIdx.x % XW, y = threadIdx.x / XW, i = i0 + x;
@@ -1864,11 +1735,11 @@ __device__ __forceinline__ void reduce_chunk(const SL slab, int nslab, int64_t s
   if (i < n) {
     int k = y;
     for (; k + 3 * NY < nslab; k += 4 * NY) {  // 4 independent loads in flight per thread
-      const float v0 = slab((size_t)k * stride + i), v1 = slab((size_t)(k + NY) * stride + i);
-      const float v2 = slab((size_t)(k + 2 * NY) * stride + i), v3 = slab((size_t)(k + 3 * NY) * stride + i);
+      const float v0 = slab[(size_t)k * stride + i], v1 = slab[(size_t)(k + NY) * stride + i];
+      const float v2 = slab[(size_t)(k + 2 * NY) * stride + i], v3 = slab[(size_t)(k + 3 * NY) * stride + i];
       s += (v0 + v1) + (v2 + v3);
     }
-    for (; k < nslab; k += NY) s += slab((size_t)k * stride + i);
+    for (; k < nslab; k += NY) s += slab[(size_t)k * stride + i];
   }
   red[threadIdx.x] = s;
   __syncthreads();
@@ -1893,14 +1764,11 @@ __global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a, int gb
     return;
   }
   const int id = blockIdx.x - gb;
-  if (id < RED2_BLOCKS && a.wg2_bf16)
-    reduce_chunk<64>(SlabBf16{reinterpret_cast<const uint16_t*>(a.wg2_slab)}, a.wg2_splits, 801 * 64, 801 * 64,
-                     id * 64, a.grad + OFF_WC2, a.gbf_b ? a.gbf_b + OFF_WC2 : nullptr, red);
-  else if (id < RED2_BLOCKS)
-    reduce_chunk<64>(SlabF32{a.wg2_slab}, a.wg2_splits, 801 * 64, 801 * 64, id * 64, a.grad + OFF_WC2,
+  if (id < RED2_BLOCKS)
+    reduce_chunk<64>(a.wg2_slab, a.wg2_splits, 801 * 64, 801 * 64, id * 64, a.grad + OFF_WC2,
                      a.gbf_b ? a.gbf_b + OFF_WC2 : nullptr, red);
   else
-    reduce_chunk<16>(SlabF32{a.wg1_slab}, 2 * a.B, 832, 832, (id - RED2_BLOCKS) * 16, a.grad + OFF_WC1,
+    reduce_chunk<16>(a.wg1_slab, 2 * a.B, 832, 832, (id - RED2_BLOCKS) * 16, a.grad + OFF_WC1,
                      a.gbf_b ? a.gbf_b + OFF_WC1 : nullptr, red);
   if (id == 0 && threadIdx.x == 0 && a.step_bump) *a.step_bump += 1;  // see MnistStepArgs::step_bump
 }
@@ -1960,24 +1828,6 @@ __device__ __forceinline__ f32x4 slab_sum(const f32x4* __restrict__ s4, int64_t 
   }
   return acc;
 }
-// the same over a bf16 slab array (4 bf16 = 8 B per float4 column)
-template <int QS>
-__device__ __forceinline__ f32x4 slab_sum_bf16(const uint2* __restrict__ s4, int64_t stride4, int ns, int q) {
-  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = q; k0 < ns; k0 += QS * MAD_SL) {
-    uint2 v[MAD_SL];
-#pragma unroll
-    for (int u = 0; u < MAD_SL; ++u) {
-      const int k = k0 + u * QS;
-      v[u] = k < ns ? s4[(size_t)k * stride4] : make_uint2(0u, 0u);
-    }
-#pragma unroll
-    for (int u = 0; u < MAD_SL; ++u)
-      acc += f32x4{__uint_as_float(v[u].x << 16), __uint_as_float(v[u].x & 0xFFFF0000u), __uint_as_float(v[u].y << 16),
-                   __uint_as_float(v[u].y & 0xFFFF0000u)};
-  }
-  return acc;
-}
 __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, MnistAdamArgs o) {
   const int gb = gather_blocks(a);
   if ((int)blockIdx.x < gb) {  // the next step's batch; t = the step started next
@@ -2001,10 +1851,7 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
     if (one) {
       g = slab_sum<16>(reinterpret_cast<const f32x4*>(a.wg1_slab) + i, 832 / 4, 2 * a.B, q, 0);
     } else if (i < MAD_C2END) {
-      if (a.wg2_bf16)
-        g = slab_sum_bf16<4>(reinterpret_cast<const uint2*>(a.wg2_slab) + (i - MAD_C1F4), 801 * 64 / 4, a.wg2_splits, q);
-      else
-        g = slab_sum<4>(reinterpret_cast<const f32x4*>(a.wg2_slab) + (i - MAD_C1F4), 801 * 64 / 4, a.wg2_splits, q, 0);
+      g = slab_sum<4>(reinterpret_cast<const f32x4*>(a.wg2_slab) + (i - MAD_C1F4), 801 * 64 / 4, a.wg2_splits, q, 0);
     }
     red[tid] = g;
     __syncthreads();
@@ -2015,8 +1862,7 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
       adam4(o, i, s, lr_t, c1, c2);
     }
   } else {
-    // skip_w1: the fc1 weight's update is deferred into the next fc1 forward (fc1_fwd_adam)
-    const int64_t i0 = (o.skip_w1 ? OFF_BD1 / 4 : MAD_C2END) + (int64_t)(bid - MAD_CONV) * MAD_NT + tid;
+    const int64_t i0 = MAD_C2END + (int64_t)(bid - MAD_CONV) * MAD_NT + tid;
     const int64_t STRIDE = (int64_t)(grid - MAD_CONV) * MAD_NT;
 #if TFD_ADAM_U > 1
     // All U strides' loads issued before any math/store, so U x 56 B per lane are in flight
@@ -2201,26 +2047,7 @@ void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s) {
 
 void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region) {
   const int gb = (a.perm && a.xpre) ? a.B : 0;
-  // skip_w1: bias + output layer (11,274 parameters) need a handful of blocks, not 1024
-  const int fc = fc_region ? (o.skip_w1 ? 12 : MAD_FC_BLOCKS) : 0;
-  mnist_adam_kernel<<<gb + MAD_CONV + fc, MAD_NT, 0, s>>>(a, o);
-}
-
-void mnist_forward_fc_adam(const MnistStepArgs& a, const MnistAdamArgs& o, int apply, bool train, hipStream_t s) {
-  if (a.B > FA_BM) throw std::runtime_error("mnist_forward_fc_adam: batch > 128");
-  if (apply && !o.gbf) throw std::runtime_error("mnist_forward_fc_adam: needs bf16 fc gradients");
-  if (a.fc1_splits != FA_SPLITS) throw std::runtime_error("mnist_forward_fc_adam: fc1 split count");
-  set_smem<fc1_fwd_adam>(FA_SMEM);
-  fc1_fwd_adam<<<FA_NT * FA_SPLITS, 256, FA_SMEM, s>>>(a, o, apply);
-  head_kernel<<<a.B, 256, 0, s>>>(a, train ? 1 : 0);
-}
-
-void mnist_adam_w1_flush(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s) {
-  (void)a;
-  AdamArgs r{o.p, o.m, o.v, nullptr, o.pbf, o.gbf, (int64_t)(OFF_BD1 - OFF_WD1), o.lr, o.beta1, o.beta2, o.eps,
-             o.step, 0, 1.f};
-  r.p += OFF_WD1; r.m += OFF_WD1; r.v += OFF_WD1; r.pbf += OFF_WD1; r.gbf += OFF_WD1;
-  adam_apply(r, s);
+  mnist_adam_kernel<<<gb + MAD_CONV + (fc_region ? MAD_FC_BLOCKS : 0), MAD_NT, 0, s>>>(a, o);
 }
 
 int64_t mnist_sfb_slot_elems(int B) { return ((int64_t)B * (2 * HID + 2 * NCLS) + 63) / 64 * 64; }

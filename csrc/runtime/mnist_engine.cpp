@@ -221,14 +221,6 @@ class MnistEngine : public torch::CustomClassHolder {
   void set_local_bf16_grads(int64_t on) { local_bf16_grads_ = on != 0; }
   // 0 (default): conv1 fused into the conv2 forward kernel; 1: the two separate kernels (A/B)
   void set_conv_unfused(int64_t on) { conv_unfused_ = on != 0; }
-  // 1: the conv2 weight-gradient split-K slabs (one per image pair) are stored in bf16 -- the
-  // gradient wire precision -- halving the bytes the wgrad kernel writes and the reduce re-reads;
-  // the partials are still summed in fp32 (bf16 engine only)
-  void set_wg2_bf16(int64_t on) { wg2_bf16_ = on != 0; }
-  // one GPU + Adam + bf16 fc gradients: the fc1-weight update of step t runs inside step t + 1's
-  // fc1 forward (mnist_forward_fc_adam) instead of the optimizer tail (flushed at the end of every
-  // host call, so parameters read between calls are always current)
-  void set_defer_fc1_adam(int64_t on) { defer_fc1_ = on != 0; }
   // Make every rank's state whole again after ZeRO-1 steps (before eval / checkpoint / broadcast):
   // each rank updated the fp32 master, m and v of its own fc1 shard only, so all four are
   // all-gathered -- the bf16 shadow (what the forward reads) and the fp32 master + Adam slots (what
@@ -315,7 +307,6 @@ class MnistEngine : public torch::CustomClassHolder {
     if (fp32_) {
       a.wg2_slab = (float*)fwg2_.data_ptr();
       a.wg2_splits = mnist_f32_wg2_splits((int)B_);
-      a.wg2_bf16 = 0;
       mnist_conv_grad_reduce(a, stream());
       return;
     }
@@ -385,13 +376,7 @@ class MnistEngine : public torch::CustomClassHolder {
     const bool gbf_local = fused && local_bf16_grads_;
     if (gbf_local) a.gbf_a = (uint16_t*)gbf_.data_ptr();
     o.gbf = gbf_local ? (const uint16_t*)gbf_.data_ptr() : nullptr;
-    // deferred fc1-weight Adam (set_defer_fc1_adam): this step's fc1 forward applies the previous
-    // step's pending update; the tail skips the fc1 weight, and the step that ends a host call
-    // (eager step, last step of a captured sequence) flushes it so params() is always current
-    const bool defer = gbf_local && defer_fc1_ && B_ <= 128;
-    mnist_forward_conv(a, s);
-    if (defer) mnist_forward_fc_adam(a, o, pending_fc1_ ? 1 : 0, true, s);
-    else mnist_forward_fc(a, true, s);
+    mnist_forward(a, true, s);
     mark(P_FWD, s);
     mnist_backward_a(a, s);
     mark(P_BFC, s);
@@ -399,12 +384,7 @@ class MnistEngine : public torch::CustomClassHolder {
     mnist_backward_b(a, s);
     if (fused) {
       mark(P_BCONV, s);
-      o.skip_w1 = defer ? 1 : 0;
       mnist_adam_fused(a, o, s);
-      if (defer) {
-        if (join_end) mnist_adam_w1_flush(a, o, s);  // t = the bumped step = this step's t
-        pending_fc1_ = !join_end;
-      }
     } else {
       mnist_conv_grad_reduce(a, s);
       mark(P_BCONV, s);
@@ -609,7 +589,6 @@ class MnistEngine : public torch::CustomClassHolder {
     MnistStepArgs r = args();
     r.wg2_slab = f.wg2_slab;
     r.wg2_splits = f.wg2_splits;
-    r.wg2_bf16 = 0;
     r.xpre = nullptr;  // the fp32 kernels read their batch rows through perm/step: no prefetch gather
     if (fused) {
       MnistAdamArgs o{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(),
@@ -979,7 +958,6 @@ class MnistEngine : public torch::CustomClassHolder {
     a.wg1_slab = (float*)wg1_slab_.data_ptr();
     a.fc1_splits = fc1_splits_;
     a.wg2_splits = wg2_splits_;
-    a.wg2_bf16 = wg2_bf16_ ? 1 : 0;
     a.keep_prob = (float)keep_prob_;
     a.seed = seed_;
     a.rank = rank_;
@@ -1043,8 +1021,6 @@ class MnistEngine : public torch::CustomClassHolder {
   bool fuse_tail_ = true;
   bool local_bf16_grads_ = false;
   bool conv_unfused_ = false;  // measured slower (docs/DESIGN.md)
-  bool wg2_bf16_ = false;
-  bool defer_fc1_ = false, pending_fc1_ = false;
   std::map<std::string, hipGraphExec_t> graphs_;
   hipEvent_t pev_[P_N] = {};
   bool timing_ = false, timed_ = false, timed_dp_ = false;
@@ -1101,8 +1077,6 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_fused_tail", &MnistEngine::set_fused_tail)
       .def("set_local_bf16_grads", &MnistEngine::set_local_bf16_grads)
       .def("set_conv_unfused", &MnistEngine::set_conv_unfused)
-      .def("set_wg2_bf16", &MnistEngine::set_wg2_bf16)
-      .def("set_defer_fc1_adam", &MnistEngine::set_defer_fc1_adam)
       .def("set_dtype", &MnistEngine::set_dtype)
       .def("dtype", &MnistEngine::dtype)
       .def("set_phase_timing", &MnistEngine::set_phase_timing)

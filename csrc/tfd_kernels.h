@@ -41,8 +41,6 @@ struct MnistStepArgs {
   float* wg2_slab;                // [wg2_splits][801][64]
   float* wg1_slab;                // [2B][832] (one slab per half image)
   int fc1_splits, wg2_splits;
-  int wg2_bf16;                   // 1: the conv2 wgrad slabs hold bf16 ([wg2_splits][801][64] uint16 in
-                                  // the same buffer): half the slab bytes written and re-read; 0: fp32
   float keep_prob;
   uint32_t seed, rank;
   int conv_unfused;            // 1: conv1 and conv2 forward as two kernels (A/B; default: one fused kernel)
@@ -92,19 +90,9 @@ struct MnistAdamArgs {
   const int64_t* t;
   int64_t* step;
   const uint16_t* gbf;  // if non-null: the fc-region (bucket A) gradients are bf16 here (gbf_a)
-  int skip_w1;          // 1: leave the fc1 weight [OFF_WD1, OFF_BD1) alone (its update is deferred
-                        // into the next step's fc1 forward, mnist_forward_fc_adam); bias + output
-                        // layer only in the fc region
 };
 // fc_region = false: the conv region only
 void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region = true);
-// One GPU, deferred fc1-weight optimizer: fc1 forward whose blocks first apply the PREVIOUS step's
-// TF ApplyAdam to the fc1-weight tile they read (fp32 master / m / v + bf16 shadow written back,
-// t = *a.step, gradients bf16 in o.gbf) and feed the updated tile straight from registers to the
-// MFMAs (apply = 0: plain forward from the shadow); then the head. B <= 128.
-void mnist_forward_fc_adam(const MnistStepArgs& a, const MnistAdamArgs& o, int apply, bool train, hipStream_t s);
-// The deferred fc1-weight update on its own (end of a captured step sequence / eager step), t = *step.
-void mnist_adam_w1_flush(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s);
 // DP, sufficient-factor broadcasting: every fc-layer weight gradient is a sum of per-example outer
 // products (dW_fc1 = [P2;1]^T dH, dW_out = [Hd;1]^T dlogits), so the all-reduced gradient is ONE
 // GEMM over the all-gathered factors (K = W*B). Writes the summed fc-region gradients (bucket A)

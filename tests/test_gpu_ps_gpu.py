@@ -16,6 +16,12 @@ from tensorflow_distributed_amd.models import mnist_cnn as M
 pytestmark = pytest.mark.gpu
 
 
+def _padded_zero(flat):
+    n = M.OFFSETS["out_b"] + 10  # end of the last variable; [n, TOTAL) is alignment padding
+    flat[n:] = 0
+    return flat
+
+
 def _shard_worker(rank, world, kind):
     """rank 0 = ps (one shard = every variable), ranks 1..2 = workers with fixed gradients."""
     from tensorflow_distributed_amd import _native
@@ -38,7 +44,7 @@ def _shard_worker(rank, world, kind):
     refreshed = []
     client = GpuPSClient(w, layout, params, lambda: refreshed.append(1), slot_names=["m", "v"] if kind == "adam" else ["m"])
     g0 = torch.Generator().manual_seed(11)
-    init = torch.randn(M.TOTAL, generator=g0) * 0.05
+    init = _padded_zero(torch.randn(M.TOTAL, generator=g0) * 0.05)  # the flat buffer's tail padding is no variable
     if w == 0:
         params.copy_(init.to(dev))
         client.init(step=0, t=0)
@@ -47,7 +53,7 @@ def _shard_worker(rank, world, kind):
     steps = []
     for s in range(3):
         g = torch.Generator().manual_seed(100 + 10 * s + w)
-        grad = (torch.randn(M.TOTAL, generator=g) * 1e-2).to(dev)
+        grad = _padded_zero(torch.randn(M.TOTAL, generator=g) * 1e-2).to(dev)
         steps.append(client.push_pull(grad, local_step=s))
     torch.cuda.synchronize()
     out = params.cpu().clone()
@@ -70,10 +76,11 @@ def test_gpu_ps_sync_accumulator_matches_host_optimizer(cuda, kind):
 
     res = run_ranks(_shard_worker, 3, kind, timeout=300)
     opt = AdamOptimizer(0.01) if kind == "adam" else MomentumOptimizer(0.01, 0.9)
-    ref = torch.randn(M.TOTAL, generator=torch.Generator().manual_seed(11)) * 0.05
+    ref = _padded_zero(torch.randn(M.TOTAL, generator=torch.Generator().manual_seed(11)) * 0.05)
     ap = FlatApplier(opt, M.TOTAL)
     for s in range(3):
-        gs = [torch.randn(M.TOTAL, generator=torch.Generator().manual_seed(100 + 10 * s + w)) * 1e-2 for w in range(2)]
+        gs = [_padded_zero(torch.randn(M.TOTAL, generator=torch.Generator().manual_seed(100 + 10 * s + w)) * 1e-2)
+              for w in range(2)]
         ap.apply(ref, gs[0] + gs[1], 0.5)
     assert res[0]["updates"] == 3 and res[0]["t"] == 3 and res[0]["dropped"] == 0
     for w in (1, 2):
