@@ -75,6 +75,50 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, at::IntArrayR
   return x;
 }
 
+// dgrad + the BN-backward statistics partials of its output (conv_dgrad_bn): the conv's input was
+// the output of a batch norm (y, mean, invstd, gamma; beta for a residual-free relu BN, whose mask
+// is recomputed from y; mask = the forward's relu bits for a residual BN; neither: no relu)
+std::tuple<at::Tensor, at::Tensor> conv2d_dgrad_bn(const at::Tensor& dy, const at::Tensor& w, at::IntArrayRef xshape,
+                                                   int64_t stride, int64_t pad, const c10::optional<at::Tensor>& acc,
+                                                   const at::Tensor& y, const at::Tensor& mean, const at::Tensor& invstd,
+                                                   const at::Tensor& gamma, const c10::optional<at::Tensor>& beta,
+                                                   const c10::optional<at::Tensor>& mask, bool relu) {
+  check_bf16(dy, "dy", 4);
+  check_bf16(w, "w", 4);
+  check_bf16(y, "y", 4);
+  TORCH_CHECK(xshape.size() == 4 && y.sizes() == xshape, "dgrad_bn: y must have the conv input's shape");
+  auto x = at::empty(xshape, dy.options());
+  if (acc.has_value()) {
+    check_bf16(*acc, "acc", 4);
+    TORCH_CHECK(acc->sizes() == xshape, "dgrad_bn: acc shape must equal xshape");
+  }
+  const ConvShape c = shape_of(x, w, stride, pad);
+  TORCH_CHECK(dy.size(1) == c.Ho() && dy.size(2) == c.Wo() && dy.size(3) == c.K, "dgrad_bn: dy shape mismatch");
+  TORCH_CHECK(conv_dgrad_bn_supported(c), "dgrad_bn: stride-1 dgrads with C % 8 == 0 only");
+  TORCH_CHECK(y.numel() < (1ll << 30), "dgrad_bn: < 2^30 elements (buffer addressing)");
+  check_f32(mean, "mean");
+  check_f32(invstd, "invstd");
+  check_f32(gamma, "gamma");
+  const int C = (int)c.C, M = (int)(y.numel() / C);
+  BnBwdStats b{bp(y), fp(mean), fp(invstd), fp(gamma), nullptr, nullptr, 0};
+  if (relu) {
+    if (mask.has_value()) {
+      TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                      mask->numel() == (int64_t)M * (C / 8), "dgrad_bn: mask must be the forward's uint8 [M, C/8] relu bits");
+      b.bits = mask->data_ptr<uint8_t>();
+      b.mode = 3;
+    } else {
+      TORCH_CHECK(beta.has_value(), "dgrad_bn: a relu BN needs beta (mask from y) or its relu bits");
+      check_f32(*beta, "beta");
+      b.beta = fp(*beta);
+      b.mode = 2;
+    }
+  }
+  auto part = at::empty({conv_dgrad_bn_rows(c), 2, C}, dy.options().dtype(at::kFloat));
+  conv_dgrad_bn(c, bp(dy), bp(w), bp(x), cur(), acc.has_value() ? bp(*acc) : nullptr, b, fp(part));
+  return {x, part};
+}
+
 void conv2d_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, int64_t stride, int64_t pad, bool zeroed) {
   check_bf16(x, "x", 4);
   check_bf16(dy, "dy", 4);
@@ -159,7 +203,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& y, const
 std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tensor& out, const at::Tensor& y,
                                           const at::Tensor& gamma, const at::Tensor& mean, const at::Tensor& invstd,
                                           bool relu, bool want_dres, at::Tensor dgamma, at::Tensor dbeta,
-                                          const c10::optional<at::Tensor>& beta, const c10::optional<at::Tensor>& mask) {
+                                          const c10::optional<at::Tensor>& beta, const c10::optional<at::Tensor>& mask,
+                                          const c10::optional<at::Tensor>& partials) {
   check_bf16(dout, "dout", -1);
   check_bf16(out, "out", -1);
   check_bf16(y, "y", -1);
@@ -170,7 +215,6 @@ std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tens
   TORCH_CHECK(y.numel() < (1ll << 30) && C % 8 == 0, "bn_bwd: C % 8 and < 2^30 elements (buffer addressing)");
   auto dy = at::empty_like(y);
   at::Tensor dres = want_dres ? at::empty_like(y) : at::Tensor();
-  auto part = at::empty({bn_partials_size(M, C)}, y.options().dtype(at::kFloat));
   if (beta) check_f32(*beta, "beta");
   const uint8_t* mb = nullptr;
   if (mask.has_value()) {
@@ -178,6 +222,15 @@ std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tens
                     mask->numel() == (int64_t)M * (C / 8), "bn_bwd: mask must be the forward's uint8 [M, C/8] relu bits");
     mb = mask->data_ptr<uint8_t>();
   }
+  if (partials.has_value()) {  // statistics partials from the producing dgrad (conv2d_dgrad_bn)
+    check_f32(*partials, "partials");
+    TORCH_CHECK(partials->dim() == 3 && partials->size(1) == 2 && partials->size(2) == C, "bn_bwd: partials [nblk,2,C]");
+    bn_backward_partials(bp(dout), bp(out), bp(y), fp(gamma), beta ? fp(*beta) : nullptr, fp(mean), fp(invstd),
+                         relu ? 1 : 0, bp(dy), want_dres ? bp(dres) : nullptr, fp(dgamma), fp(dbeta), M, C,
+                         fp(*partials), (int)partials->size(0), cur(), mb);
+    return {dy, dres};
+  }
+  auto part = at::empty({bn_partials_size(M, C)}, y.options().dtype(at::kFloat));
   bn_backward(bp(dout), bp(out), bp(y), fp(gamma), beta ? fp(*beta) : nullptr, fp(mean), fp(invstd), relu ? 1 : 0,
               bp(dy), want_dres ? bp(dres) : nullptr, fp(dgamma), fp(dbeta), M, C, fp(part), cur(), mb);
   return {dy, dres};
@@ -259,6 +312,9 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.impl("conv2d_fwd_stats", c10::DispatchKey::CUDA, &conv2d_fwd_stats);
   m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc=None) -> Tensor");
   m.impl("conv2d_dgrad", c10::DispatchKey::CUDA, &conv2d_dgrad);
+  m.def("conv2d_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc, Tensor y, Tensor mean, "
+        "Tensor invstd, Tensor gamma, Tensor? beta, Tensor? mask, bool relu) -> (Tensor, Tensor)");
+  m.impl("conv2d_dgrad_bn", c10::DispatchKey::CUDA, &conv2d_dgrad_bn);
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad, bool zeroed=False) -> ()");
   m.impl("conv2d_wgrad", c10::DispatchKey::CUDA, &conv2d_wgrad);
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias) -> Tensor");
@@ -272,7 +328,8 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
         "(Tensor, Tensor, Tensor)");
   m.impl("bn_fwd", c10::DispatchKey::CUDA, &bn_fwd);
   m.def("bn_bwd(Tensor dout, Tensor out, Tensor y, Tensor gamma, Tensor mean, Tensor invstd, bool relu, "
-        "bool want_dres, Tensor(a!) dgamma, Tensor(b!) dbeta, Tensor? beta=None, Tensor? mask=None) -> (Tensor, Tensor)");
+        "bool want_dres, Tensor(a!) dgamma, Tensor(b!) dbeta, Tensor? beta=None, Tensor? mask=None, "
+        "Tensor? partials=None) -> (Tensor, Tensor)");
   m.impl("bn_bwd", c10::DispatchKey::CUDA, &bn_bwd);
   m.def("bn_infer(Tensor y, Tensor gamma, Tensor beta, Tensor rm, Tensor rv, float eps, bool relu) -> Tensor");
   m.impl("bn_infer", c10::DispatchKey::CUDA, &bn_infer_op);

@@ -27,6 +27,21 @@ void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, ui
 // two gradient paths without a separate add kernel
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                 const uint16_t* add = nullptr);
+// dgrad whose epilogue also emits the backward statistics partials of the batch norm whose output
+// was this conv's input (its dout is the dgrad output): part fp32 [conv_dgrad_bn_rows(c)][2][C] of
+// per-row-block sums of d and d * (y - mean) * invstd, d = dout through the BN's relu mask -- what
+// bn_backward's partial pass would read back; bn_backward_partials consumes them. mode: 0 no relu,
+// 2 mask recomputed from y (gamma, beta: the forward's constants), 3 relu bits. Stride 1 only.
+struct BnBwdStats {
+  const uint16_t* y;
+  const float *mean, *invstd, *gamma, *beta;
+  const uint8_t* bits;
+  int mode;
+};
+bool conv_dgrad_bn_supported(const ConvShape& c);
+int conv_dgrad_bn_rows(const ConvShape& c);
+void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
+                   const uint16_t* add, const BnBwdStats& b, float* part);
 // dw: fp32 [R*S*C][K]; overwritten (zeroed first when split)
 // zeroed: dw is known to be zero already (the model zeroes its flat gradient buffer once per
 // step), so split-K needs no per-layer memset
@@ -60,6 +75,11 @@ void bn_forward_partials(const uint16_t* y, const float* gamma, const float* bet
 void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* beta,
                  const float* mean, const float* invstd, int relu, uint16_t* dy, uint16_t* dres, float* dgamma,
                  float* dbeta, int M, int C, float* partials, hipStream_t st, const uint8_t* mask_bits = nullptr);
+// same, with the partials already summed by the producing dgrad's epilogue (conv_dgrad_bn, [nblk][2][C])
+void bn_backward_partials(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma,
+                          const float* beta, const float* mean, const float* invstd, int relu, uint16_t* dy,
+                          uint16_t* dres, float* dgamma, float* dbeta, int M, int C, const float* partials, int nblk,
+                          hipStream_t st, const uint8_t* mask_bits = nullptr);
 // inference-mode BN (running statistics), optional relu
 void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,
               float eps, int relu, uint16_t* out, int M, int C, hipStream_t st);

@@ -273,12 +273,30 @@ struct LdsEpi {
 struct RowId {
   __device__ __forceinline__ uint32_t operator()(int m) const { return (uint32_t)m; }
 };
-template <int BM, int BN, int WM, int WN, bool ADD, bool STATS, class RM = RowId>
+// BN-backward statistics in a dgrad epilogue (BS::MODE >= 0): the dgrad output is the dout of the
+// batch norm whose output was this conv's input, so the epilogue also sums, per column, d and
+// d * xhat with d = the STORED bf16 gradient through that BN's relu mask and xhat = (y - mean) *
+// invstd -- exactly what bn_partial_kernel<1, MODE> reads back from memory, without the second pass
+// over dout and y. MODE 0: no relu; 2: mask recomputed from y with the forward's constants; 3: the
+// forward's relu bits ([M][N/8] bytes). Partials go to part[blockIdx.y][2][N] (bn_final's layout).
+struct NoBnB {
+  static constexpr int MODE = -1;
+};
+template <int MK>
+struct BnB {
+  static constexpr int MODE = MK;
+  const uint16_t* __restrict__ y;
+  const float *mean, *invstd, *gamma, *beta;
+  const uint8_t* __restrict__ bits;
+};
+template <int BM, int BN, int WM, int WN, bool ADD, bool STATS, class RM = RowId, class BS = NoBnB>
 __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], char* smem, uint16_t* __restrict__ y,
                                              const uint16_t* __restrict__ add, int M, int N, int m0, int n0,
                                              float* __restrict__ part, RM rowmap = RM{}, uint32_t ybytes = 0,
-                                             int* tcnt = nullptr, int tG = 0, float* tot = nullptr) {
+                                             int* tcnt = nullptr, int tG = 0, float* tot = nullptr, BS bs = BS{}) {
   using E = LdsEpi<BM, BN, WM, WN>;
+  constexpr bool BSTAT = BS::MODE >= 0;
+  static_assert(!(STATS && BSTAT), "one statistics kind per epilogue");
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
   const int cc = tid % E::CPR, g0 = tid / E::CPR;  // this thread's chunk column and first row
@@ -305,9 +323,33 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
 #pragma unroll
       for (int r = 0; r < 4; ++r) cs[(r0 + r) * E::PITCH + col] = acc[i][j][r];
     }
+  // BN-backward operands: y chunks (and relu bytes) issued once the accumulator is staged (its
+  // registers are free), in flight across the barrier
+  [[maybe_unused]] uint4 yq[E::CH];
+  [[maybe_unused]] uint32_t mbits[E::CH];
+  [[maybe_unused]] float bmu[8], bis[8], bsc[8], bsh[8];
+  if constexpr (BSTAT) {
+#pragma unroll
+    for (int c = 0; c < E::CH; ++c) {
+      const int m = m0 + g0 + c * E::RG;
+      const bool ok = m < M && n < N;
+      yq[c] = buf_ld(bs.y, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, ok);
+      if constexpr (BS::MODE == 3) mbits[c] = ok ? bs.bits[(size_t)orow[c] * (N / 8) + n / 8] : 0u;
+    }
+    const int nc = n < N ? n : 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bmu[k] = bs.mean[nc + k];
+      bis[k] = bs.invstd[nc + k];
+      if constexpr (BS::MODE == 2) {
+        bsc[k] = bis[k] * bs.gamma[nc + k];
+        bsh[k] = bs.beta[nc + k] - bmu[k] * bsc[k];
+      }
+    }
+  }
   __syncthreads();
   float s[8], sq[8];
-  if constexpr (STATS) {
+  if constexpr (STATS || BSTAT) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) { s[k] = 0.f; sq[k] = 0.f; }
   }
@@ -339,9 +381,28 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
           sq[2 * k + 1] = fmaf(f1, f1, sq[2 * k + 1]);
         }
       }
+      if constexpr (BSTAT) {  // bn_partial_kernel<1, MODE>'s per-element math, same operands
+        const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+        const uint32_t yw[4] = {yq[c].x, yq[c].y, yq[c].z, yq[c].w};
+        float d[8], yv[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          d[2 * k] = __uint_as_float(w[k] << 16);
+          d[2 * k + 1] = __uint_as_float(w[k] & 0xFFFF0000u);
+          yv[2 * k] = __uint_as_float(yw[k] << 16);
+          yv[2 * k + 1] = __uint_as_float(yw[k] & 0xFFFF0000u);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if constexpr (BS::MODE == 2) d[k] = fmaf(yv[k], bsc[k], bsh[k]) > 0.f ? d[k] : 0.f;
+          if constexpr (BS::MODE == 3) d[k] = (mbits[c] >> k) & 1u ? d[k] : 0.f;
+          s[k] += d[k];
+          sq[k] = fmaf(d[k], (yv[k] - bmu[k]) * bis[k], sq[k]);
+        }
+      }
     }
   }
-  if constexpr (STATS) {
+  if constexpr (STATS || BSTAT) {
     static_assert(2 * E::RG * BN * 4 <= E::BYTES, "stats reduction fits in the staged tile");
     __syncthreads();  // every thread has read its chunks: reuse the tile for [2][RG][BN]
 #pragma unroll
@@ -417,6 +478,18 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_kernel(LA la, LB 
   gemm_mainloop<BM, BN, CBK, 2, 2, LA, LB, conv_rs<BM, BN>()>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
                                                        (bf16*)smem_raw, acc);
   lds_epilogue<BM, BN, 2, 2, ADD, false>(acc, smem_raw, y, add, M, N, blockIdx.y * BM, blockIdx.x * BN, nullptr);
+}
+
+// dgrad (+ add) whose epilogue also emits the BN-backward partials of its output (BnB above)
+template <int BM, int BN, class LA, class LB, bool ADD, class BS>
+__global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_bnb_kernel(LA la, LB lb, uint16_t* y, const uint16_t* add,
+                                                                          int M, int N, int KD, float* part, BS bs) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  f32x4 acc[BM / 32][BN / 32];
+  gemm_mainloop<BM, BN, CBK, 2, 2, LA, LB, conv_rs<BM, BN>()>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
+                                                       (bf16*)smem_raw, acc);
+  lds_epilogue<BM, BN, 2, 2, ADD, false, RowId, BS>(acc, smem_raw, y, add, M, N, blockIdx.y * BM, blockIdx.x * BN, part,
+                                                    RowId{}, 0u, nullptr, 0, nullptr, bs);
 }
 
 // Forward conv + BN statistics: the block's column partials (sum, sum of squares over its BM rows)
@@ -520,6 +593,20 @@ void launch_gemm_bf16(const LA& la, const LB& lb, uint16_t* y, const uint16_t* a
   gemm_bf16_kernel<BM, BN, LA, LB, ADD><<<grid, 256, sm, st>>>(la, lb, y, add, M, N, KD);
 }
 
+template <int BM, int BN, class LA, class LB, bool ADD, class BS>
+void launch_gemm_bf16_bnb(const LA& la, const LB& lb, uint16_t* y, const uint16_t* add, int M, int N, int KD, float* part,
+                          const BS& bs, hipStream_t st) {
+  constexpr int sm = stats_smem<BM, BN, LA, LB>();
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_bf16_bnb_kernel<BM, BN, LA, LB, ADD, BS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+    attr = true;
+  }
+  dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, 1);
+  gemm_bf16_bnb_kernel<BM, BN, LA, LB, ADD, BS><<<grid, 256, sm, st>>>(la, lb, y, add, M, N, KD, part, bs);
+}
+
 template <int BM, int BN, class LA, class LB>
 void launch_gemm_stats(const LA& la, const LB& lb, uint16_t* y, int M, int N, int KD, float* part, hipStream_t st) {
   constexpr int sm = stats_smem<BM, BN, LA, LB>();
@@ -592,6 +679,21 @@ void dispatch_bf16(const LA& la, const LB& lb, uint16_t* y, const uint16_t* add,
     if (t == OT128) launch_gemm_bf16<128, 128, LA, LB, false>(la, lb, y, add, M, N, KD, st);
     else if (t == OT128x64) launch_gemm_bf16<128, 64, LA, LB, false>(la, lb, y, add, M, N, KD, st);
     else launch_gemm_bf16<64, 64, LA, LB, false>(la, lb, y, add, M, N, KD, st);
+  }
+}
+
+template <class LA, class LB, class BS>
+void dispatch_bf16_bnb(const LA& la, const LB& lb, uint16_t* y, const uint16_t* add, int M, int N, int KD, float* part,
+                       const BS& bs, hipStream_t st) {
+  const OutTile t = out_tile(M, N);
+  if (add) {
+    if (t == OT128) launch_gemm_bf16_bnb<128, 128, LA, LB, true>(la, lb, y, add, M, N, KD, part, bs, st);
+    else if (t == OT128x64) launch_gemm_bf16_bnb<128, 64, LA, LB, true>(la, lb, y, add, M, N, KD, part, bs, st);
+    else launch_gemm_bf16_bnb<64, 64, LA, LB, true>(la, lb, y, add, M, N, KD, part, bs, st);
+  } else {
+    if (t == OT128) launch_gemm_bf16_bnb<128, 128, LA, LB, false>(la, lb, y, add, M, N, KD, part, bs, st);
+    else if (t == OT128x64) launch_gemm_bf16_bnb<128, 64, LA, LB, false>(la, lb, y, add, M, N, KD, part, bs, st);
+    else launch_gemm_bf16_bnb<64, 64, LA, LB, false>(la, lb, y, add, M, N, KD, part, bs, st);
   }
 }
 
@@ -740,6 +842,27 @@ void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint1
   }
   if (add) conv_dgrad_impl(c, dy, w, AddStoreBf16{dx, add, M, c.C}, st);
   else conv_dgrad_impl(c, dy, w, StoreBf16{dx, M, c.C}, st);
+}
+
+bool conv_dgrad_bn_supported(const ConvShape& c) { return TFD_CONV_LDS_EPI && c.stride == 1 && c.C % 8 == 0; }
+int conv_dgrad_bn_rows(const ConvShape& c) { return out_tile_rows(c.N * c.H * c.W, c.C); }
+
+void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
+                   const uint16_t* add, const BnBwdStats& b, float* part) {
+  if (!conv_dgrad_bn_supported(c)) throw std::runtime_error("conv_dgrad_bn: stride-1 dgrads with C % 8 == 0 only");
+  const int M = c.N * c.H * c.W, KD = c.R * c.S * c.K;
+  auto go = [&](const auto& bs) {
+    if (is_pointwise(c)) {
+      dispatch_bf16_bnb(DenseX<true>{dy, c.K, M, c.K}, DenseX<true>{w, c.K, c.C, c.K}, dx, add, M, c.C, KD, part, bs, st);
+    } else {
+      Geo g = make_geo(c, M, KD);
+      dispatch_bf16_bnb(DgradA{dy, g}, DgradB{w, g}, dx, add, M, c.C, KD, part, bs, st);
+    }
+  };
+  if (b.mode == 0) go(BnB<0>{b.y, b.mean, b.invstd, b.gamma, b.beta, b.bits});
+  else if (b.mode == 2) go(BnB<2>{b.y, b.mean, b.invstd, b.gamma, b.beta, b.bits});
+  else if (b.mode == 3) go(BnB<3>{b.y, b.mean, b.invstd, b.gamma, b.beta, b.bits});
+  else throw std::runtime_error("conv_dgrad_bn: mask mode must be 0 (no relu), 2 (from y) or 3 (relu bits)");
 }
 
 // Weight-gradient tile: dW is [R*S*C][K] with a very long reduction over pixels (split-K), so the

@@ -419,7 +419,14 @@ constexpr int C12_XZ = 32 * C12_XS;                          // a padded tap (k 
 constexpr int C12_XOFF = C2L_FWD_SMEM;                       // fp32 [C12_XR][C12_XS] x image
 constexpr int C12_WOFF = C12_XOFF + C12_XR * C12_XS * 4;     // fp32 [25][32] W1 + [32] bias
 constexpr int C12_IOFF = C12_WOFF + (KTAPS * C1 + C1) * 4;   // uint8 [196][32] conv1 argmax
-constexpr int C12_SMEM = C12_IOFF + 196 * 32;                // 122,944 B
+#ifndef TFD_C1_X8  // 1: conv1's A fragments are 16-B reads of a bf16 "5-wide row" image (see conv12_fwd_lds)
+#define TFD_C1_X8 1
+#endif
+constexpr int C12_X8P = 40;                                  // X8 row pitch (16-B entries): rows oh, oh + 1 of a
+                                                             // 16-lane read group land 8 slots apart mod 16 (no overlap)
+constexpr int C12_X8OFF = C12_IOFF + 196 * 32;               // bf16x8 [32][C12_X8P] = x[r][c..c+4], 0, 0, 0
+constexpr int C12_SMEM = C12_X8OFF + (TFD_C1_X8 ? 32 * C12_X8P * 16 : 0);  // 122,944 B (+20,480 with X8)
+static_assert(C12_X8OFF % 16 == 0 && C12_SMEM <= 160 * 1024, "conv12 LDS carve");
 static_assert(C12_IOFF % 16 == 0, "LDS carve alignment");
 #ifndef TFD_STAMP
 #define TFD_STAMP 0  // 1: thread 0 of every conv12 block records s_memtime at its phase boundaries
@@ -514,6 +521,22 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
   }
   C12_STAMPW(5);
   __syncthreads();
+#if TFD_C1_X8
+  // the "5-wide row" image: X8[r][c] = bf16(x[r][c .. c+4]) and three zeros (zero-bordered 32 x 32
+  // coordinates, c <= 27), so the 8 taps (kh, kw = 0..7) of one kernel row are one 16-B LDS read
+  {
+    bf16* x8 = reinterpret_cast<bf16*>(smem_raw + C12_X8OFF);
+    for (int i = t; i < 32 * 28; i += 512) {
+      const int r = i / 28, c = i - r * 28;
+      const float* src = xs + r * C12_XS + c;
+      bf16x8 e;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[j] = (bf16)(j < 5 ? src[j] : 0.f);
+      *reinterpret_cast<bf16x8*>(x8 + (r * C12_X8P + c) * 8) = e;
+    }
+    __syncthreads();
+  }
+#endif
   C12_STAMP(2);
   C12_STAMPW(6);
 #ifndef TFD_EXP_C12
@@ -537,6 +560,37 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
   {
     const int lane = t & 63, w = t >> 6, g = lane >> 4, col = lane & 15;
     uint8_t* idx_l = reinterpret_cast<uint8_t*>(smem_raw + C12_IOFF);  // [196][32]
+    const float bias0 = w1[KTAPS * C1 + col], bias1 = w1[KTAPS * C1 + 16 + col];
+    constexpr int MT = 7;  // ceil(49 / 8)
+#if TFD_C1_X8
+    // K = kernel row kh * 8 + kw (kw < 5 real): MFMA 1 covers kh = 0..3 (lane group g reads kernel
+    // row g: one 16-B read of X8), MFMA 2 kh = 4 (every group reads row 4; only group 0's weights
+    // are non-zero). 2 MFMAs + 2 ds_read_b128 per M-tile instead of 8 scalar reads + 8 converts.
+    bf16x8 bw1[2], bw2[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        bw1[nt][jj] = (bf16)(jj < 5 ? w1[(g * 5 + jj) * C1 + nt * 16 + col] : 0.f);
+        bw2[nt][jj] = (bf16)(jj < 5 && g == 0 ? w1[(20 + jj) * C1 + nt * 16 + col] : 0.f);
+      }
+    const bf16* x8 = reinterpret_cast<const bf16*>(smem_raw + C12_X8OFF);
+    bf16x8 af[MT], af2[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int mt = w + 8 * i;
+      const int m = min(mt, 48) * 16 + col, pp = m >> 2, win = m & 3;
+      const int orow = 2 * (pp / 14) + (win >> 1), ocol = 2 * (pp % 14) + (win & 1);
+      af[i] = *reinterpret_cast<const bf16x8*>(x8 + ((orow + g) * C12_X8P + ocol) * 8);
+      af2[i] = *reinterpret_cast<const bf16x8*>(x8 + ((orow + 4) * C12_X8P + ocol) * 8);
+    }
+    f32x4 z[MT][2];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        z[i][nt] = mfma16x16x32(af2[i], bw2[nt], mfma16x16x32(af[i], bw1[nt], f32x4{0.f, 0.f, 0.f, 0.f}));
+#else
     bf16x8 bw[2];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
@@ -545,8 +599,6 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
         const int k = 8 * g + jj;
         bw[nt][jj] = (bf16)(k < KTAPS ? w1[k * C1 + nt * 16 + col] : 0.f);
       }
-    const float bias0 = w1[KTAPS * C1 + col], bias1 = w1[KTAPS * C1 + 16 + col];
-    constexpr int MT = 7;  // ceil(49 / 8)
     // The A gather is VALU-bound (wave64 VALU = 4 cycles, 2 waves per SIMD): per-lane tap offsets
     // are computed once, a padded tap (k >= 25) points into the zero rows (no select, no exec-masked
     // read: a masked read per element made the compiler wait lgkmcnt(0) 56 times, 7.6 K cycles),
@@ -571,6 +623,7 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) z[i][nt] = mfma16x16x32(af[i], bw[nt], f32x4{0.f, 0.f, 0.f, 0.f});
+#endif
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       const int mt = w + 8 * i;
@@ -1248,14 +1301,14 @@ constexpr int C2D_P_OFF = C2D_I_OFF + C1W_HALF * 32;
 static_assert(C2D_I_OFF % 16 == 0 && C2D_P_OFF % 16 == 0, "LDS carve alignment");
 static_assert(C2D_P_OFF + 16 * 833 * 4 <= C2D_SMEM, "fused conv1-wgrad tail exceeds the dgrad LDS");
 static_assert(4 * 4 * 64 * 16 <= C2D_X_OFF, "park region overlaps the fused tail");
-__global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) {
+__device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const int bid) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* img = (bf16*)smem_raw;                           // [8][224][8]
   bf16* wt = img + 8 * C2D_PLANE * 8;                    // [800][72]
-  const int b = blockIdx.x >> 1, h = blockIdx.x & 1, t = threadIdx.x;
+  const int b = bid >> 1, h = bid & 1, t = threadIdx.x;
   const uint16_t* src = a.dz2 + (size_t)b * 196 * 64;
   const uint16_t* wsrc = a.pbf + OFF_WC2;
-  const int rot = TFD_WROT ? (int)((blockIdx.x * 1031u) % 6400u) : 0;  // per-block start: spread L2 channels
+  const int rot = TFD_WROT ? (int)((bid * 1031u) % 6400u) : 0;  // per-block start: spread L2 channels
 #if TFD_C1_EARLY_X
   // the conv1-wgrad tail's step -> perm chain resolved now, behind the staging loads
   const int xrow_idx = data_row(a, b);
@@ -1480,7 +1533,7 @@ __global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) {
     float sm = 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) sm += part[q * 833 + i];
-    a.wg1_slab[(size_t)blockIdx.x * 832 + i] = sm;
+    a.wg1_slab[(size_t)bid * 832 + i] = sm;
   }
 }
 
@@ -1529,7 +1582,7 @@ __global__ __launch_bounds__(256) void conv2_wgrad_k(MnistStepArgs a, int kper) 
 #define TFD_C2WL_NTG 4
 #endif
 #ifndef TFD_C2WL_PERM  // 1: K (pixel) order grouped by LDS bank class (csrc/c2wl_perm.h): conflict-free
-#define TFD_C2WL_PERM 1  //    A-fragment tr-reads (MI355X LDS model 1968 -> 1344 cycles per image)
+#define TFD_C2WL_PERM 0  //    A-fragment tr-reads (LDS model 1968 -> 1344 cycles per image, but measured +1.1 us/step: profiles/ab_c2wl_perm_r3.log)
 #endif
 constexpr int C2WL_IMG = TFD_C2WL_IMG;      // images per block (= slab count B / C2WL_IMG)
 constexpr int C2WL_NTG = TFD_C2WL_NTG;      // tap groups (4: [0,6) [6,12) [12,18) [18,25))
@@ -1542,12 +1595,12 @@ constexpr int C2WL_IMG_ELEMS = C2WL_PW * C2WL_PW * C2WL_CS;
 constexpr int C2WL_BRED_OFF = (C2WL_IMG_ELEMS + C2WL_KP * C2WL_DS) * 2;
 constexpr int C2WL_SMEM = C2WL_BRED_OFF + 8 * 64 * 4;  // 65408 B: two blocks per CU
 static_assert(C2WL_BRED_OFF % 16 == 0 && (C2WL_IMG_ELEMS * 2) % 16 == 0, "LDS carve alignment");
-__global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) {
+__device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const int bid) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* img = (bf16*)smem_raw;
   bf16* dz = img + C2WL_IMG_ELEMS;
   float* bred = reinterpret_cast<float*>(smem_raw + C2WL_BRED_OFF);  // [8][64]
-  const int tg = blockIdx.x % C2WL_NTG, ip = blockIdx.x / C2WL_NTG, t = threadIdx.x;
+  const int tg = bid % C2WL_NTG, ip = bid / C2WL_NTG, t = threadIdx.x;
   const int tap0 = tg * C2WL_TPG, ntaps = (tg == C2WL_NTG - 1) ? 25 - tap0 : C2WL_TPG;
   const int lane = t & 63, w = t >> 6, h = w >> 2, n = w & 3, g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
   // the image border and the dz2 pad rows stay zero for every image of the block
@@ -1660,6 +1713,19 @@ __global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) {
       slab[800 * 64 + t] = sm;
     }
   }
+}
+
+__global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) { conv2_wgrad_body(a, blockIdx.x); }
+__global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) { conv2_dgrad_body(a, blockIdx.x); }
+// conv2 wgrad and dgrad (+ the conv1 wgrad tail) in ONE launch: both consume only dz2, so the
+// dgrad blocks start on each CU as its wgrad block finishes instead of after a kernel boundary
+// (the dgrad's LDS size is the launch's: one block per CU either way). Blocks [0, nw) wgrad.
+#ifndef TFD_C2_BWD_ONE
+#define TFD_C2_BWD_ONE 1
+#endif
+__global__ __launch_bounds__(512) void conv2_bwd_lds(MnistStepArgs a, int nw) {
+  if ((int)blockIdx.x < nw) conv2_wgrad_body(a, blockIdx.x);
+  else conv2_dgrad_body(a, blockIdx.x - nw);
 }
 
 // K13 + K14 in one launch: conv2 dgrad and wgrad both consume dz2 only (independent).
@@ -2018,6 +2084,13 @@ void mnist_backward_b(const MnistStepArgs& a, hipStream_t s) {
   // conv2 wgrad (one slab per image pair), then dgrad + conv1 wgrad, one stream (a forked wgrad
   // only contended with dgrad for the CUs: 110 vs 100 us/step, profiles/ab_conv_fork.log)
   (void)kper;
+  static_assert(C2WL_SMEM <= C2D_SMEM, "conv2_bwd_lds: the dgrad LDS size covers the wgrad blocks");
+  if (TFD_C2_BWD_ONE) {
+    set_smem<conv2_bwd_lds>(C2D_SMEM);
+    const int nw = C2WL_NTG * a.wg2_splits;
+    conv2_bwd_lds<<<nw + 2 * B, 512, C2D_SMEM, s>>>(a, nw);
+    return;
+  }
   conv2_wgrad_lds<<<C2WL_NTG * a.wg2_splits, 512, C2WL_SMEM, s>>>(a);
   set_smem<conv2_dgrad_lds>(C2D_SMEM);
   conv2_dgrad_lds<<<2 * B, 512, C2D_SMEM, s>>>(a);  // + conv1 wgrad (fused tail)

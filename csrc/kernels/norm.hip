@@ -677,6 +677,23 @@ void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, c
 #undef TFD_BN_BWD
 }
 
+void bn_backward_partials(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma,
+                          const float* beta, const float* mean, const float* invstd, int relu, uint16_t* dy,
+                          uint16_t* dres, float* dgamma, float* dbeta, int M, int C, const float* partials, int nblk,
+                          hipStream_t st, const uint8_t* mask_bits) {
+  const RowSplit r = row_split(M, C);
+  const int mask = !relu ? 0 : (mask_bits ? 3 : (beta ? 2 : 1));
+  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr, nullptr);
+#define TFD_BN_BWDP(MK)                                                                                          \
+  bn_bwd_apply_kernel<MK><<<r.nblk, NT, 0, st>>>(dout, out, y, gamma, beta, mean, invstd, dbeta, dgamma, dy, dres, M, \
+                                                 C, r.tpr, r.rg, r.rb, 1.f / (float)M, mask_bits);
+  if (mask == 0) { TFD_BN_BWDP(0) }
+  else if (mask == 1) { TFD_BN_BWDP(1) }
+  else if (mask == 2) { TFD_BN_BWDP(2) }
+  else { TFD_BN_BWDP(3) }
+#undef TFD_BN_BWDP
+}
+
 void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,
               float eps, int relu, uint16_t* out, int M, int C, hipStream_t st) {
   const int64_t nch = (int64_t)M * C / 8;

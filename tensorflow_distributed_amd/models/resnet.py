@@ -173,6 +173,7 @@ class GradJoin:
 
     def __init__(self, n: int):
         self.n = n
+        self.bn = None  # the batch norm whose output is the joined activation (its dout is the sum)
         self.reset()
 
     def reset(self):
@@ -185,7 +186,9 @@ class GradJoin:
         last = self.seen == self.n
         if conv is not None:
             dy, L, xs = conv
-            if self.acc is not None:
+            if last and _bn_stats_fusable(L, self.bn):  # the sum is the BN's whole dout
+                g = _dgrad_bn(dy, L, xs, self.acc, self.bn)
+            elif self.acc is not None:
                 g = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad, self.acc)
             else:
                 g = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad)
@@ -196,6 +199,28 @@ class GradJoin:
             self.acc = None
             return g
         return None
+
+
+def _bn_stats_fusable(L, bn) -> bool:
+    """Can conv ``L``'s dgrad (the whole dout of batch norm ``bn``) emit that BN's backward
+    statistics partials (``conv2d_dgrad_bn``)? Stride-1 dgrads, and a BN whose relu mask the epilogue
+    can form the way the BN backward will: none, relu bits (residual BN), or recomputed from y
+    (residual-free BN with ``mask_from_y``)."""
+    if bn is None or not L.model.bn_bwd_stats or L.stride != 1 or bn.fwd_state is None:
+        return False
+    _, _, _, mask, relu, has_res = bn.fwd_state
+    return (not relu) or mask is not None or (not has_res and L.model.mask_from_y)
+
+
+def _dgrad_bn(dy, L, xs, acc, bn):
+    """dX of conv ``L`` (+ ``acc``) with BN ``bn``'s backward partials summed in the same epilogue;
+    the partials wait on the BN layer for its backward (which then skips its own partial pass)."""
+    y, mean, invstd, mask, relu, has_res = bn.fwd_state
+    beta = bn.beta() if (relu and mask is None) else None
+    g, part = _ops().conv2d_dgrad_bn(dy, L.w(), xs, L.stride, L.pad, acc, y, mean, invstd, bn.gamma(), beta, mask,
+                                     relu)
+    bn.bwd_part = part
+    return g
 
 
 class _Conv(torch.autograd.Function):
@@ -225,6 +250,8 @@ class _Conv(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if L.in_join is not None:
                 dx = L.in_join.arrive(conv=(dy, L, list(x.shape)))
+            elif _bn_stats_fusable(L, L.in_bn):  # this conv is the BN output's only consumer
+                dx = _dgrad_bn(dy, L, list(x.shape), None, L.in_bn)
             else:
                 dx = _ops().conv2d_dgrad(dy, L.w(), list(x.shape), L.stride, L.pad)
         return dx, None, None
@@ -241,6 +268,8 @@ class _BN(torch.autograd.Function):
             mask = torch.empty(y.numel() // y.shape[-1], y.shape[-1] // 8, dtype=torch.uint8, device=y.device)
         out, mean, invstd = _ops().bn_fwd(*args, part, mask)
         ctx.layer, ctx.relu, ctx.has_res = layer, relu, res is not None
+        # for the consuming conv's dgrad epilogue (conv2d_dgrad_bn): this step's forward state
+        layer.fwd_state = (y, mean, invstd, mask, relu, res is not None)
         ctx.save_for_backward(y, out if mask is None else mask, mean, invstd)
         ctx.bits = mask is not None
         return out
@@ -255,7 +284,9 @@ class _BN(torch.autograd.Function):
         mask = out_or_mask if ctx.bits else None
         out = y if ctx.bits else out_or_mask  # not read when a mask (bits or from y) is given
         args = (dout.contiguous(), out, y, L.gamma(), mean, invstd, ctx.relu, ctx.has_res, L.g_gamma(), L.g_beta())
-        dy, dres = _ops().bn_bwd(*args, beta, mask)
+        part, L.bwd_part = L.bwd_part, None  # partials from the dgrad that produced dout, if it made them
+        L.fwd_state = None  # its consumers' dgrads have run
+        dy, dres = _ops().bn_bwd(*args, beta, mask, part)
         L.model.reducer.mark_ready(L.name + "/gamma")
         L.model.reducer.mark_ready(L.name + "/beta")
         if ctx.has_res and L.res_join is not None:
@@ -327,6 +358,7 @@ class ConvLayer:
     def __init__(self, model, name, cin, cout, k, stride, pad):
         self.model, self.name, self.stride, self.pad = model, name, stride, pad
         self.in_join = None  # GradJoin of this conv's input (residual block inputs)
+        self.in_bn = None  # the BN whose output is this conv's only input consumer (BN-backward stats)
         model.specs.append(PSpec(name, (k, k, cin, cout), "he", fan_in=k * k * cin))
 
     def w(self):
@@ -344,6 +376,8 @@ class BNLayer:
         self.model, self.name, self.c = model, name, c
         self.momentum, self.eps = 0.9, 1e-5
         self.res_join = None  # GradJoin of the residual input (identity shortcut)
+        self.fwd_state = None  # (y, mean, invstd, relu bits, relu, has_res) of this step's forward
+        self.bwd_part = None  # backward statistics partials left by the dgrad that produced dout
         model.specs.append(PSpec(name + "/gamma", (c,), "zeros" if zero_init else "ones"))
         model.specs.append(PSpec(name + "/beta", (c,), "zeros"))
         model.bns.append(self)
@@ -397,7 +431,8 @@ class ResNet:
            101: ("bottleneck", [3, 4, 23, 3])}
 
     def __init__(self, depth: int = 50, num_classes: int = 1000, device=None, seed: int = 0, width: int = 64,
-                 zero_init_residual: bool = True, fuse_joins: bool = True, bn_stats: bool = True):
+                 zero_init_residual: bool = True, fuse_joins: bool = True, bn_stats: bool = True,
+                 bn_bwd_stats: bool = True):
         kind, blocks = self.CFG[depth]
         if num_classes % 8 or width % 8:
             raise ValueError("num_classes and width must be multiples of 8 (16-byte MFMA operand chunks)")
@@ -414,12 +449,16 @@ class ResNet:
         # BN statistics summed in the producing conv's epilogue (conv2d_fwd_stats) instead of a
         # separate read pass over every conv output
         self.bn_stats = bn_stats
+        # BN-backward statistics summed in the epilogue of the dgrad that produces the BN's dout
+        # (conv2d_dgrad_bn) instead of bn_bwd's separate read pass over dout and y
+        self.bn_bwd_stats = bn_bwd_stats
         # residual-free BN backward recomputes its relu mask from y instead of reading the output
         self.mask_from_y = True
         # residual BN keeps its relu mask as bits for the backward instead of re-reading the output
         self.relu_bits = True
         cin = width
         exp = 4 if kind == "bottleneck" else 1
+        prev_out_bn = None  # the BN that produced the current block input (None: the stem's maxpool)
         for li, nb in enumerate(blocks):
             w = width * (2 ** li)
             for bi in range(nb):
@@ -439,8 +478,12 @@ class ResNet:
                 if st != 1 or cin != cout:
                     blk["cd"] = ConvLayer(self, nm + ".downsample", cin, cout, 1, st, 0)
                     blk["bd"] = BNLayer(self, nm + ".downsample_bn", cout)
+                blk["c2"].in_bn = blk["b1"]
+                if kind != "basic":
+                    blk["c3"].in_bn = blk["b2"]
                 # the block input feeds conv1 and the shortcut: join their gradients in place
                 j = GradJoin(2)
+                j.bn = prev_out_bn
                 if not fuse_joins:
                     j = None
                 blk["c1"].in_join = j
@@ -451,6 +494,7 @@ class ResNet:
                 if j is not None:
                     self.joins.append(j)
                 self.blocks.append(blk)
+                prev_out_bn = blk["b2" if kind == "basic" else "b3"]
                 cin = cout
         self.fc = LinearLayer(self, "fc", cin, num_classes)
         self.fp = FlatParams(self.specs, self.device, seed)
@@ -470,6 +514,8 @@ class ResNet:
     def forward(self, x_nhwc_f32: torch.Tensor) -> torch.Tensor:
         for j in self.joins:
             j.reset()
+        for bn in self.bns:
+            bn.fwd_state, bn.bwd_part = None, None
         x = _ops().pad_channels(x_nhwc_f32, 8)
         x = self.stem_bn(self.stem(x))
         x = _MaxPool.apply(x, 3, 2, 1)
