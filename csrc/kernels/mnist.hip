@@ -118,6 +118,10 @@ __device__ __forceinline__ void gather_next(const MnistStepArgs& a, int64_t next
   }
 }
 __device__ __forceinline__ int gather_blocks(const MnistStepArgs& a) { return (a.perm && a.xpre) ? a.B : 0; }
+// the bf16 fc1 weights this step reads (MnistStepArgs::pbf_alt: double-buffered by step parity)
+__device__ __forceinline__ const uint16_t* fc1_wbf(const MnistStepArgs& a) {
+  return (a.pbf_alt && (*a.step & 1)) ? a.pbf_alt + OFF_WD1 : a.pbf + OFF_WD1;
+}
 // the prefetched label of batch row b (speculative load beside the tag and the step)
 __device__ __forceinline__ int batch_label(const MnistStepArgs& a, int b) {
   if (a.perm && a.xpre) {
@@ -754,7 +758,7 @@ static_assert(FC1_NKT * FC1_BK * FC1_SPLITS == FEAT, "fc1 split-K must tile K ex
 __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DenseLoader<true> la{a.p2, FEAT, a.B, FEAT};
-  DenseLoader<false> lb{a.pbf + OFF_WD1, HID, HID, FEAT};
+  DenseLoader<false> lb{fc1_wbf(a), HID, HID, FEAT};
   const int z = blockIdx.z;
   SlabEpi epi{a.fc1_slab + (size_t)z * a.B * HID, HID, a.B, HID};
   const int kb = z * kper, ke = min(FEAT, kb + kper);
@@ -1055,7 +1059,7 @@ constexpr int FDX_BM = 32, FDX_BN = TFD_FDX_BN, FDX_BK = TFD_FDX_BK, FDX_BN2 = T
 template <int BN = FDX_BN, int RS = TFD_FDX_RS>
 __device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   DenseLoader<true> la{a.dh, HID, a.B, HID};
-  DenseLoader<true> lb{a.pbf + OFF_WD1, HID, FEAT, HID};
+  DenseLoader<true> lb{fc1_wbf(a), HID, FEAT, HID};
   UnpoolEpi epi{a.p2, a.idx2, a.dz2, a.B};
   gemm_block<FDX_BM, BN, FDX_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), RS>(la, lb, epi, by * FDX_BM, bx * BN, 0, HID, smem);
 }
@@ -1095,6 +1099,95 @@ __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int pa
   id -= FDW_GX * FDW_GY;
   out_grad_block(a, id, (float*)smem_raw);
 #endif
+}
+
+// ---------------- one-GPU: fc1 dW (+ bias row) with ApplyAdam in the epilogue ----------------
+// The fp32 dW tile is staged in LDS (pitch BN + 4), then each thread owns two 8-column chunks:
+// their p / m / v (fp32) are loaded before the barrier, updated with the TF ApplyAdam equations of
+// adam4 (same expressions, the un-rounded fp32 gradient), and stored with the bf16 shadow going to
+// the NEXT step's half of the double-buffered fc1 shadow (MnistStepArgs::pbf_alt) -- the dX blocks
+// of this launch still read this step's half. ~1000 blocks at 3 per CU: one block's Adam stream
+// overlaps another's GEMM phase, so the 90 MB of fc1 optimizer traffic rides beside the fc
+// backward instead of forming a separate ~15 us pass (and the 6.4 MB bf16 gradient is never written
+// or read back).
+constexpr int FDWA_PITCH = FDW_BN + 4;
+constexpr int FDWA_CPR = FDW_BN / 8, FDWA_NCH = FDW_BM * FDWA_CPR / 256;
+static_assert(FDW_BM * FDWA_CPR % 256 == 0, "whole chunks per thread");
+__device__ __forceinline__ void fc1_dw_adam_block(const MnistStepArgs& a, const MnistAdamArgs& o, int bx, int by,
+                                                  bf16* smem) {
+  OnesRowMC la{a.p2, FEAT, FEAT, a.B};
+  DenseLoader<false> lb{a.dh, HID, HID, a.B};
+  constexpr int WM = 2, WN = 2, WTM = FDW_BM / WM, WTN = FDW_BN / WN, TM = WTM / 16, TN = WTN / 16;
+  static_assert(FDW_BM * FDWA_PITCH * 4 <= GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, DenseLoader<false>>::BYTES,
+                "staged dW tile fits in the GEMM's LDS");
+  f32x4 acc[TM][TN];
+  const int m0 = by * FDW_BM, n0 = bx * FDW_BN;
+  gemm_mainloop<FDW_BM, FDW_BN, FDW_BK, WM, WN, OnesRowMC, DenseLoader<false>, TFD_GEMM_RS>(la, lb, m0, n0, 0, a.B,
+                                                                                            smem, acc);
+  float* cs = reinterpret_cast<float*>(smem);  // the mainloop ended with a barrier: operands are dead
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int r0 = wm * WTM + 16 * i + 4 * (lane >> 4), col = wn * WTN + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[(r0 + r) * FDWA_PITCH + col] = acc[i][j][r];
+    }
+  f32x4 P[FDWA_NCH][2], Mm[FDWA_NCH][2], Vv[FDWA_NCH][2];
+  int64_t q4[FDWA_NCH];
+  bool ok[FDWA_NCH];
+#pragma unroll
+  for (int c = 0; c < FDWA_NCH; ++c) {
+    const int q = tid + 256 * c, row = m0 + q / FDWA_CPR, col = n0 + (q % FDWA_CPR) * 8;
+    ok[c] = row <= FEAT;  // rows 0..3135 weights, row 3136 the bias (OFF_BD1 follows the weight)
+    q4[c] = (OFF_WD1 + (int64_t)row * HID + col) / 4;
+    if (ok[c]) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        P[c][h] = reinterpret_cast<const f32x4*>(o.p)[q4[c] + h];
+        Mm[c][h] = reinterpret_cast<const f32x4*>(o.m)[q4[c] + h];
+        Vv[c][h] = reinterpret_cast<const f32x4*>(o.v)[q4[c] + h];
+      }
+    }
+  }
+  const int64_t t = *o.t;
+  const float b1p = powf(o.beta1, (float)t), b2p = powf(o.beta2, (float)t);
+  const float lr_t = o.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  const float c1 = 1.f - o.beta1, c2 = 1.f - o.beta2;
+  uint16_t* nxt = ((*a.step + 1) & 1) ? a.pbf_alt : o.pbf;
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < FDWA_NCH; ++c) {
+    if (!ok[c]) continue;
+    const int q = tid + 256 * c, rl = q / FDWA_CPR, cl = (q % FDWA_CPR) * 8;
+    uint32_t sh[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 g = *reinterpret_cast<const f32x4*>(cs + rl * FDWA_PITCH + cl + 4 * h);
+      f32x4 p = P[c][h], m = Mm[c][h], v = Vv[c][h];
+      m = m + (g - m) * c1;
+      v = v + (g * g - v) * c2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[j] -= lr_t * m[j] / (sqrtf(v[j]) + o.eps);
+      reinterpret_cast<f32x4*>(o.p)[q4[c] + h] = p;
+      reinterpret_cast<f32x4*>(o.m)[q4[c] + h] = m;
+      reinterpret_cast<f32x4*>(o.v)[q4[c] + h] = v;
+      sh[2 * h] = pack_bf2(p[0], p[1]);
+      sh[2 * h + 1] = pack_bf2(p[2], p[3]);
+    }
+    *reinterpret_cast<uint4*>(nxt + 4 * q4[c]) = make_uint4(sh[0], sh[1], sh[2], sh[3]);
+  }
+}
+// the one-GPU fc backward with fused fc1 Adam: [out-layer grads | fc1 dX tiles | fc1 dW+Adam tiles]
+__global__ __launch_bounds__(256) void fc1_bwd_adam(MnistStepArgs a, MnistAdamArgs o, int n_dx) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  int id = blockIdx.x;
+  if (id < OUTG_BLOCKS) { out_grad_block(a, id, (float*)smem_raw); return; }
+  id -= OUTG_BLOCKS;
+  if (id < n_dx) { fc1_dx_block(a, id % FDX_GX, id / FDX_GX, (bf16*)smem_raw); return; }
+  id -= n_dx;
+  fc1_dw_adam_block(a, o, id % FDW_GX, id / FDW_GX, (bf16*)smem_raw);
 }
 
 // ---------------- DP: fc gradients from all-gathered sufficient factors ----------------
@@ -1894,7 +1987,7 @@ __device__ __forceinline__ f32x4 slab_sum(const f32x4* __restrict__ s4, int64_t 
   }
   return acc;
 }
-__global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, MnistAdamArgs o) {
+__global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, MnistAdamArgs o, int fcb4) {
   const int gb = gather_blocks(a);
   if ((int)blockIdx.x < gb) {  // the next step's batch; t = the step started next
     gather_next(a, *o.t, blockIdx.x);
@@ -1928,7 +2021,7 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
       adam4(o, i, s, lr_t, c1, c2);
     }
   } else {
-    const int64_t i0 = MAD_C2END + (int64_t)(bid - MAD_CONV) * MAD_NT + tid;
+    const int64_t i0 = fcb4 + (int64_t)(bid - MAD_CONV) * MAD_NT + tid;  // fcb4: MAD_C2END, or the out layer
     const int64_t STRIDE = (int64_t)(grid - MAD_CONV) * MAD_NT;
 #if TFD_ADAM_U > 1
     // All U strides' loads issued before any math/store, so U x 56 B per lane are in flight
@@ -2118,10 +2211,35 @@ void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s) {
   reduce_conv_grads<<<RED2_BLOCKS + RED1_BLOCKS, 256, 0, s>>>(a, 0);
 }
 
-void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region) {
+void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region, int64_t fc_beg) {
   const int gb = (a.perm && a.xpre) ? a.B : 0;
-  mnist_adam_kernel<<<gb + MAD_CONV + (fc_region ? MAD_FC_BLOCKS : 0), MAD_NT, 0, s>>>(a, o);
+  if (fc_beg < 0) fc_beg = OFF_WD1;
+  if (fc_beg != OFF_WD1 && fc_beg != OFF_OUT) throw std::runtime_error("mnist_adam_fused: fc_beg must be OFF_WD1 or OFF_OUT");
+  // after mnist_backward_a_adam only the out layer is left: 2,576 float4 -> 16 grid-stride blocks
+  const int nfc = !fc_region ? 0 : (fc_beg == OFF_OUT ? 16 : MAD_FC_BLOCKS);
+  mnist_adam_kernel<<<gb + MAD_CONV + nfc, MAD_NT, 0, s>>>(a, o, (int)(fc_beg / 4));
 }
+
+void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s) {
+  if (!a.pbf_alt) throw std::runtime_error("mnist_backward_a_adam: needs the double-buffered fc1 shadow (pbf_alt)");
+  const int B = a.B;
+  constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, DenseLoader<false>>::BYTES;
+  constexpr int sm_dx = GemmSmem<FDX_BM, FDX_BN, FDX_BK, DenseLoader<true>, DenseLoader<true>>::BYTES;
+  const int sm_og = (B * NCLS + 4 * OUTG_ROWS * NCLS) * 4;
+  const int sm = std::max(std::max(sm_dw, sm_dx), sm_og);
+  set_smem<fc1_bwd_adam>(sm);
+  const int n_dx = FDX_GX * ((B + FDX_BM - 1) / FDX_BM);
+  fc1_bwd_adam<<<OUTG_BLOCKS + n_dx + FDW_GX * FDW_GY, 256, sm, s>>>(a, o, n_dx);
+}
+
+__global__ __launch_bounds__(256) void settle_shadow_kernel(MnistStepArgs a) {
+  if (!a.pbf_alt || !(*a.step & 1)) return;  // even step: pbf already holds the live fc1 shadow
+  const int64_t n = (int64_t)(FEAT + 1) * HID / 8;
+  const uint4* src = reinterpret_cast<const uint4*>(a.pbf_alt + OFF_WD1);
+  uint4* dst = reinterpret_cast<uint4*>(const_cast<uint16_t*>(a.pbf) + OFF_WD1);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+void mnist_settle_shadow(const MnistStepArgs& a, hipStream_t s) { settle_shadow_kernel<<<512, 256, 0, s>>>(a); }
 
 int64_t mnist_sfb_slot_elems(int B) { return ((int64_t)B * (2 * HID + 2 * NCLS) + 63) / 64 * 64; }
 

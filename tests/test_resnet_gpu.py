@@ -255,3 +255,39 @@ def test_resnet_rccl_bucketed_world1_equals_no_comm(cuda, bf16):
     (n_bad, names, finite), = run_ranks(_rccl_bucketed_worker, 1, bf16, timeout=240)
     assert finite
     assert n_bad == 0, f"{n_bad} parameters differ (first in {names})"
+
+
+@pytest.mark.parametrize("depth", [18, 50])
+def test_bn_bwd_stats_in_dgrad_epilogue(cuda, depth, monkeypatch):
+    """BN-backward statistics summed in the epilogue of the dgrad that produces the BN's dout
+    (conv2d_dgrad_bn: relu mask from y for residual-free BNs, relu bits for the residual BN behind a
+    residual-join conv) give the same gradients as bn_bwd's separate partial pass: only the fp32
+    summation order of the per-channel sums differs. Both mask kinds must actually take the fused
+    path."""
+    from tensorflow_distributed_amd.models import resnet as R
+
+    kinds = []
+    orig = R._dgrad_bn
+
+    def spy(dy, L, xs, acc, bn):
+        kinds.append(("bits" if bn.fwd_state[3] is not None else "from_y", acc is not None))
+        return orig(dy, L, xs, acc, bn)
+
+    monkeypatch.setattr(R, "_dgrad_bn", spy)
+    torch.manual_seed(depth)
+    x = torch.randn(4, 32, 32, 3, device=cuda)
+    lab = torch.randint(0, 16, (4,), dtype=torch.int32, device=cuda)
+    out = []
+    for on in (False, True):
+        m = R.ResNet(depth, num_classes=16, device=cuda, seed=3, width=16, zero_init_residual=False, bn_bwd_stats=on)
+        m.fp.grad.zero_()
+        loss, _ = m.loss(x, lab)
+        loss.backward()
+        torch.cuda.synchronize()
+        out.append((loss.item(), m.fp.grad.clone()))
+    assert out[0][0] == out[1][0]  # same forward
+    g0, g1 = out[0][1], out[1][1]
+    assert torch.isfinite(g1).all()
+    rel = ((g1 - g0).norm() / g0.norm()).item()
+    assert rel < 1e-2, rel
+    assert ("from_y", False) in kinds and ("bits", True) in kinds, kinds
