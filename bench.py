@@ -80,6 +80,9 @@ def main(argv=None):
                     "conv weight-gradient slabs and bumps the step (one kernel less)")
     ap.add_argument("--local_bf16_grads", type=int, default=1, help="1: on one GPU keep the fc-region gradients "
                     "in bf16 (the DP all-reduce wire format): fc backward writes and Adam reads 2 B per gradient")
+    ap.add_argument("--fc_adam", type=int, default=0, help="1: on one GPU the fc1 Adam update runs in the fc1 "
+                    "weight-gradient epilogue (fp32 gradient straight from the GEMM, fc1 bf16 shadow double-buffered; A/B neutral: "
+                    "profiles/ab_fc1_adam_dw_epi_r3.log)")
     ap.add_argument("--conv_unfused", type=int, default=0, help="1: conv1 and conv2 forward as two kernels "
                     "(A/B of the fused conv1->conv2 kernel)")
     ap.add_argument("--state_steps", type=int, default=100, help="time the steps that follow this many training "
@@ -118,6 +121,7 @@ def main(argv=None):
     eng.set_dtype(a.dtype)
     eng.set_fused_tail(a.fused_tail)
     eng.set_local_bf16_grads(a.local_bf16_grads)
+    eng.set_fc_adam(bool(a.fc_adam))
     eng.set_conv_unfused(a.conv_unfused)
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
@@ -316,6 +320,7 @@ def main(argv=None):
                 "zero1_fc1": bool(a.zero),
                 "fc_grads": ("fp32" if a.dtype == "fp32" else
                              "summed from all-gathered factors (sfb), bf16" if "sfb" in tr.kind else
+                             "fc1: fp32 into Adam in the dW epilogue; out: bf16" if eng.fc_adam_active() else
                              "bf16" if (a.local_bf16_grads or world > 1) and not a.fp32_grads else "fp32"),
             },
         }), flush=True)

@@ -97,7 +97,10 @@ class MnistEngine : public torch::CustomClassHolder {
 
   // ---- state accessors (views share storage with the engine) ----
   at::Tensor params() { return params_; }
-  at::Tensor params_bf16() { return pbf_; }
+  at::Tensor params_bf16() {  // the live fc1 shadow settled into pbf_ first (fc_adam double buffer)
+    if (alt_live_) mnist_settle_shadow(args(), stream());
+    return pbf_;
+  }
   at::Tensor grads() { return grad_; }
   // bf16 gradient buffer: the DP wire format (reduced in place by the bucket all-reduces)
   at::Tensor grads_bf16() { return gbf_; }
@@ -142,7 +145,18 @@ class MnistEngine : public torch::CustomClassHolder {
     input_mode_ = mode;
   }
   void set_keep_prob(double kp) { keep_prob_ = kp; }
-  void sync_shadow() { cast_f32_bf16((const float*)params_.data_ptr(), (uint16_t*)pbf_.data_ptr(), TOTAL, stream()); }
+  void sync_shadow() {
+    cast_f32_bf16((const float*)params_.data_ptr(), (uint16_t*)pbf_.data_ptr(), TOTAL, stream());
+    if (alt_live_) copy_shadow_to_alt();
+  }
+  // One-GPU fc1 Adam fused into the fc1 dW epilogue (mnist_backward_a_adam, default on): used by
+  // the one-GPU bf16 Adam step with the fused optimizer tail; any other step kind first settles the
+  // double-buffered fc1 shadow back into pbf (leave_alt) and runs as before.
+  void set_fc_adam(bool on) {
+    if (!on) leave_alt();
+    fc_adam_ = on;
+  }
+  bool fc_adam_active() const { return fc_adam_ && !dp() && !fp32_ && opt_ == 0 && fuse_tail_ && !zero_; }
 
   void set_adam(double lr, double b1, double b2, double eps) {
     opt_ = 0; lr_ = lr; b1_ = b1; b2_ = b2; eps_ = eps;
@@ -342,6 +356,7 @@ class MnistEngine : public torch::CustomClassHolder {
   void train_step() { train_step_impl(true); }
 
   void train_step_impl(bool join_end) {
+    if (!fc_adam_active()) leave_alt();  // every other step kind writes the single shadow pbf_
     if (zero_ && !sfb_active()) {
       train_step_zero();
       return;
@@ -362,6 +377,8 @@ class MnistEngine : public torch::CustomClassHolder {
       }
       return;
     }
+    const bool fca = fc_adam_active();
+    if (fca) enter_alt();
     mark(P_START, s);
     MnistStepArgs a = args();
     // one GPU: nothing to overlap with. With Adam ONE kernel ends the step: it reduces the conv
@@ -378,13 +395,14 @@ class MnistEngine : public torch::CustomClassHolder {
     o.gbf = gbf_local ? (const uint16_t*)gbf_.data_ptr() : nullptr;
     mnist_forward(a, true, s);
     mark(P_FWD, s);
-    mnist_backward_a(a, s);
+    if (fca) mnist_backward_a_adam(a, o, s);  // fc1 Adam in the dW epilogue
+    else mnist_backward_a(a, s);
     mark(P_BFC, s);
     a.step_bump = (int64_t*)step_.data_ptr();
     mnist_backward_b(a, s);
     if (fused) {
       mark(P_BCONV, s);
-      mnist_adam_fused(a, o, s);
+      mnist_adam_fused(a, o, s, true, fca ? OFF_OUT : OFF_WD1);
     } else {
       mnist_conv_grad_reduce(a, s);
       mark(P_BCONV, s);
@@ -715,6 +733,10 @@ class MnistEngine : public torch::CustomClassHolder {
     hipStream_t s = stream();
     TORCH_CHECK(s != nullptr, "capture needs a non-default stream (use torch.cuda.stream(...))");
     drop_graph(name);
+    // the fc1 shadow mode switch copies weights: done eagerly, never recorded into the graph (a
+    // captured copy would re-run on every replay and overwrite the live half)
+    if (fc_adam_active()) enter_alt();
+    else leave_alt();
     HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
     try {
       for (int64_t i = 0; i < n; ++i) train_step_impl(i == n - 1);
@@ -730,6 +752,7 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
     HIP_OK(hipGraphDestroy(g));
     graphs_[name] = ex;
+    graph_alt_[name] = alt_live_;
   }
   // forward + backward (fc gradients, conv slab reduce, step bump) as one graph, no optimizer: the
   // compute part of a parameter-server worker step (the update runs on the PS task's GPU,
@@ -739,6 +762,7 @@ class MnistEngine : public torch::CustomClassHolder {
     TORCH_CHECK(s != nullptr, "capture needs a non-default stream (use torch.cuda.stream(...))");
     drop_graph(name);
     timed_ = false;
+    leave_alt();  // (eager, see capture_train_steps)
     HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
     try {
       forward(true);
@@ -756,10 +780,15 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
     HIP_OK(hipGraphDestroy(g));
     graphs_[name] = ex;
+    graph_alt_[name] = alt_live_;
   }
   void replay(const std::string& name, int64_t times) {
     auto it = graphs_.find(name);
     TORCH_CHECK(it != graphs_.end(), "no graph named ", name);
+    // the graph's kernels were recorded with or without the double-buffered fc1 shadow: restore
+    // that mode eagerly first (both switches keep the weights; see enter_alt / leave_alt)
+    if (graph_alt_[name]) enter_alt();
+    else leave_alt();
     hipStream_t s = stream();
     for (int64_t i = 0; i < times; ++i) HIP_OK(hipGraphLaunch(it->second, s));
   }
@@ -980,7 +1009,26 @@ class MnistEngine : public torch::CustomClassHolder {
     }
     a.sfb_by_lo = 0;
     a.sfb_by_hi = -1;  // all tile rows (train_step_sfb narrows it under ZeRO)
+    a.pbf_alt = alt_live_ ? (uint16_t*)pbf_alt_.data_ptr() : nullptr;
     return a;
+  }
+
+  // fc1 region [OFF_WD1, OFF_OUT) of the bf16 shadow, pbf_ -> pbf_alt_ (both halves equal)
+  void copy_shadow_to_alt() {
+    const size_t bytes = (size_t)(OFF_OUT - OFF_WD1) * 2;
+    TORCH_CHECK(hipMemcpyAsync((uint16_t*)pbf_alt_.data_ptr() + OFF_WD1, (const uint16_t*)pbf_.data_ptr() + OFF_WD1,
+                               bytes, hipMemcpyDeviceToDevice, stream()) == hipSuccess, "fc1 shadow copy failed");
+  }
+  void enter_alt() {
+    if (alt_live_) return;
+    if (!pbf_alt_.defined()) pbf_alt_ = at::empty_like(pbf_);
+    copy_shadow_to_alt();  // either parity reads the current weights
+    alt_live_ = true;
+  }
+  void leave_alt() {
+    if (!alt_live_) return;
+    mnist_settle_shadow(args(), stream());  // the live half -> pbf_ (device step parity)
+    alt_live_ = false;
   }
 
   int64_t B_, device_;
@@ -1019,9 +1067,13 @@ class MnistEngine : public torch::CustomClassHolder {
   hipEvent_t ev_p2_ = nullptr, ev_wag_ = nullptr;
   // one GPU + Adam: the optimizer kernel also reduces the conv gradient slabs and bumps the step
   bool fuse_tail_ = true;
+  bool fc_adam_ = false;    // one-GPU fc1 Adam in the dW epilogue (set_fc_adam; A/B neutral, off)
+  bool alt_live_ = false;   // the fc1 shadow is double-buffered (pbf_ / pbf_alt_ by step parity)
+  at::Tensor pbf_alt_;
   bool local_bf16_grads_ = false;
   bool conv_unfused_ = false;  // measured slower (docs/DESIGN.md)
   std::map<std::string, hipGraphExec_t> graphs_;
+  std::map<std::string, bool> graph_alt_;  // captured with the double-buffered fc1 shadow live
   hipEvent_t pev_[P_N] = {};
   bool timing_ = false, timed_ = false, timed_dp_ = false;
 };
@@ -1076,6 +1128,8 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("dp", &MnistEngine::dp)
       .def("set_fused_tail", &MnistEngine::set_fused_tail)
       .def("set_local_bf16_grads", &MnistEngine::set_local_bf16_grads)
+      .def("set_fc_adam", &MnistEngine::set_fc_adam)
+      .def("fc_adam_active", &MnistEngine::fc_adam_active)
       .def("set_conv_unfused", &MnistEngine::set_conv_unfused)
       .def("set_dtype", &MnistEngine::set_dtype)
       .def("dtype", &MnistEngine::dtype)

@@ -203,6 +203,51 @@ def test_local_bf16_fc_grads_match_fp32(cuda):
     assert torch.equal(engs[0].params_bf16(), engs[0].params().to(torch.bfloat16))
 
 
+def test_fc1_adam_in_dw_epilogue_matches_separate_pass(cuda):
+    """One GPU: the fc1 Adam update inside the fc1 dW epilogue (set_fc_adam, opt-in: fp32
+    gradient straight from the GEMM, bf16 fc1 shadow double-buffered by step parity) == the separate
+    Adam pass over an fp32 gradient buffer, to fp32 rounding; the shadow stays the bf16 of the
+    master across odd/even steps and after leaving the mode (set_fc_adam(False))."""
+    B = 128
+    params = M.flat_from_dict(M.init_params(19)).to(cuda) * 0.05
+    n = 1024
+    data = torch.rand(n, 784, device=cuda)
+    labels = torch.randint(0, 10, (n,), dtype=torch.int32, device=cuda)
+    perm = torch.randperm(n, device=cuda).to(torch.int32)
+    engs = []
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for on in (True, False):
+            e = _engine(B, cuda, keep=0.75)
+            e.set_adam(0.01, 0.9, 0.999, 1e-8)
+            e.set_local_bf16_grads(0)
+            e.set_fc_adam(on)
+            e.params().copy_(params)
+            e.sync_shadow()
+            e.set_dataset(data, labels, perm)
+            e.set_input_mode(1)
+            engs.append(e)
+        for e in engs:
+            for _ in range(3):
+                e.train_step()
+    torch.cuda.synchronize()
+    assert engs[0].fc_adam_active() and not engs[1].fc_adam_active()
+    d0, d1 = engs[0].params() - params, engs[1].params() - params
+    assert _relerr(d0, d1) < 1e-4, _relerr(d0, d1)
+    for e in engs:
+        assert torch.equal(e.params_bf16(), e.params().to(torch.bfloat16))  # odd step: pbf_alt was live
+    with torch.cuda.stream(s):
+        r = [e.evaluate(data[:512], labels[:512]) for e in engs]
+        engs[0].set_fc_adam(False)
+        for e in engs:
+            e.train_step()
+    torch.cuda.synchronize()
+    assert torch.allclose(r[0], r[1], rtol=1e-3, atol=1e-3), r
+    d0, d1 = engs[0].params() - params, engs[1].params() - params
+    assert _relerr(d0, d1) < 1e-4, _relerr(d0, d1)
+    assert torch.equal(engs[0].params_bf16(), engs[0].params().to(torch.bfloat16))
+
+
 def _assert_same_regions(p0, p1, what):
     bad = {}
     for name, sl in (("conv1", slice(0, 832)), ("conv2", slice(832, M.BUCKET_SPLIT)),
