@@ -37,13 +37,37 @@ __device__ __forceinline__ void epi_call(const EPI& epi, int m4, int n, const f3
   else epi(m4, n, v);
 }
 
+// LDS images (MI355X LDS: 64 banks x 4 B; ds_read_b128 in 4 groups of 16 lanes, ds_read_b64_tr_b16
+// in 2 groups of 32, scripts/debug/lds_banks.py):
+//  KC = true : [MN][BK + 16] -- the 16 rows of a b128 fragment read land 8 banks apart per row
+//              (pad 8 put rows r and r + 8 on the same banks: 2-way on every read);
+//  KC = false: [BK][MN] with the 16-B chunk index of row k XORed by swz_chunk(k) (no pad): the 8
+//              rows k = kk + 8g + q (g < 2, q < 4) of one tr-read lane group cover 8 disjoint 8-bank
+//              windows (pad 16 mapped rows k and k + 8 to the same banks: 2-way on every read).
+// TFD_LDS_SWZ=0 restores the padded round-2 images.
+#ifndef TFD_LDS_SWZ
+#define TFD_LDS_SWZ 1
+#endif
+template <int CPR>
+__device__ __forceinline__ int swz_chunk(int k) {
+  if constexpr (!TFD_LDS_SWZ || (CPR & (CPR - 1)) != 0 || CPR < 4) return 0;
+  else if constexpr (CPR >= 16) return (2 * (k & 1) + 4 * ((k >> 1) & 1) + 8 * ((k >> 3) & 1)) & (CPR - 1);
+  else if constexpr (CPR == 8) return 2 * ((k >> 1) & 1) + 4 * ((k >> 3) & 1);
+  else return 2 * ((k >> 3) & 1);
+}
 template <int MN, int BK, bool KC>
 struct LdsTile {
-  static constexpr int PAD = KC ? 8 : 16;                 // elements (16 B / 32 B: bank spread)
+  static constexpr int CH_PER_ROW = KC ? BK / 8 : MN / 8; // 16-byte chunks per LDS row
+  static constexpr bool SWZ = !KC && TFD_LDS_SWZ && (CH_PER_ROW & (CH_PER_ROW - 1)) == 0 && CH_PER_ROW >= 4;
+  static constexpr int PAD = KC ? (TFD_LDS_SWZ ? 16 : 8) : (SWZ ? 0 : 16);  // elements
   static constexpr int ROW = KC ? (BK + PAD) : (MN + PAD);
   static constexpr int ELEMS = KC ? MN * ROW : BK * ROW;
-  static constexpr int CH_PER_ROW = KC ? BK / 8 : MN / 8; // 16-byte chunks per LDS row
   static constexpr int CHUNKS = MN * BK / 8;
+  // element offset of (LDS row, column col) -- col a multiple of 4 inside one 16-B chunk
+  static __device__ __forceinline__ int at(int row, int col) {
+    if constexpr (SWZ) return row * ROW + (((col >> 3) ^ swz_chunk<CH_PER_ROW>(row)) << 3) + (col & 7);
+    else return row * ROW + col;
+  }
 };
 
 typedef __attribute__((ext_vector_type(8))) short s16x8;
@@ -56,8 +80,8 @@ __device__ __forceinline__ bf16x8 read_frag(const bf16* lds, int r0, int kk, int
     return *reinterpret_cast<const bf16x8*>(p);
   } else {
     const int g = lane >> 4, i = lane & 15, q = i >> 2, p4 = i & 3;
-    const bf16* p0 = lds + (kk + 8 * g + q) * L::ROW + r0 + 4 * p4;
-    const bf16* p1 = p0 + 4 * L::ROW;
+    const bf16* p0 = lds + L::at(kk + 8 * g + q, r0 + 4 * p4);
+    const bf16* p1 = lds + L::at(kk + 8 * g + q + 4, r0 + 4 * p4);
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0));
     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p1));
     s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -144,7 +168,7 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
       const int idx = tid + c * NT;
       if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
         const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 8;
-        *reinterpret_cast<uint4*>(As + row * TA::ROW + col) = xa[c];
+        *reinterpret_cast<uint4*>(As + TA::at(row, col)) = xa[c];
       }
     }
 #pragma unroll
@@ -152,7 +176,7 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
       const int idx = tid + c * NT;
       if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
         const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 8;
-        *reinterpret_cast<uint4*>(Bs + row * TB::ROW + col) = xb[c];
+        *reinterpret_cast<uint4*>(Bs + TB::at(row, col)) = xb[c];
       }
     }
   };
@@ -298,7 +322,7 @@ __device__ __forceinline__ void gemm_block_oneshot(const LA& la, const LB& lb, c
       const int idx = tid + c * NT;
       if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
         const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 8;
-        *reinterpret_cast<uint4*>(As + t * TA::ELEMS + row * TA::ROW + col) = ra[t][c];
+        *reinterpret_cast<uint4*>(As + t * TA::ELEMS + TA::at(row, col)) = ra[t][c];
       }
     }
 #pragma unroll
@@ -306,7 +330,7 @@ __device__ __forceinline__ void gemm_block_oneshot(const LA& la, const LB& lb, c
       const int idx = tid + c * NT;
       if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
         const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 8;
-        *reinterpret_cast<uint4*>(Bs + t * TB::ELEMS + row * TB::ROW + col) = rb[t][c];
+        *reinterpret_cast<uint4*>(Bs + t * TB::ELEMS + TB::at(row, col)) = rb[t][c];
       }
     }
   }
