@@ -40,8 +40,6 @@ def main(argv=None):
                     "epilogue (0: autograd adds; measured faster, see resnet.GradJoin)")
     ap.add_argument("--bn_bwd_stats", type=int, default=1, help="1: batch-norm backward statistics summed in the "
                     "epilogue of the dgrad that produces the BN's gradient (no separate partial pass)")
-    ap.add_argument("--bn_final_side", type=int, default=1, help="1: the BN-backward finalize (dgamma / dbeta) "
-                    "runs on a side stream beside the conv weight gradient")
     ap.add_argument("--lr", type=float, default=0.1)
     argv = list(sys.argv[1:] if argv is None else argv)
     a = ap.parse_args(argv)
@@ -61,7 +59,7 @@ def main(argv=None):
     spawn.check_world(a.gpus, ctx.world)
     dev = ctx.device
     m = ResNet(a.depth, num_classes=1000, device=dev, seed=0, fuse_joins=bool(a.fuse_joins),
-               bn_stats=bool(a.bn_stats), bn_bwd_stats=bool(a.bn_bwd_stats), bn_final_side=bool(a.bn_final_side))
+               bn_stats=bool(a.bn_stats), bn_bwd_stats=bool(a.bn_bwd_stats))
     m.mask_from_y = bool(a.mask_from_y)
     m.relu_bits = bool(a.relu_bits)
     comm, transport = None, "none"
@@ -132,7 +130,7 @@ def main(argv=None):
                        "bucket_mb": a.bucket_mb, "optimizer": "sgd-momentum 0.9 wd 1e-4",
                        "hipgraph": not a.eager, "fuse_joins": bool(a.fuse_joins), "bn_stats": bool(a.bn_stats),
                        "mask_from_y": bool(a.mask_from_y), "relu_bits": bool(a.relu_bits),
-                       "bn_bwd_stats": bool(a.bn_bwd_stats), "bn_final_side": bool(a.bn_final_side)}}), flush=True)
+                       "bn_bwd_stats": bool(a.bn_bwd_stats)}}), flush=True)
     if transport == "ipc":
         if comm.ipc.error():
             raise RuntimeError("IPC collective barrier timed out: replicas may have diverged")

@@ -204,7 +204,7 @@ std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tens
                                           const at::Tensor& gamma, const at::Tensor& mean, const at::Tensor& invstd,
                                           bool relu, bool want_dres, at::Tensor dgamma, at::Tensor dbeta,
                                           const c10::optional<at::Tensor>& beta, const c10::optional<at::Tensor>& mask,
-                                          const c10::optional<at::Tensor>& partials, bool totals_ready) {
+                                          const c10::optional<at::Tensor>& partials) {
   check_bf16(dout, "dout", -1);
   check_bf16(out, "out", -1);
   check_bf16(y, "y", -1);
@@ -222,12 +222,6 @@ std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tens
                     mask->numel() == (int64_t)M * (C / 8), "bn_bwd: mask must be the forward's uint8 [M, C/8] relu bits");
     mb = mask->data_ptr<uint8_t>();
   }
-  if (totals_ready) {  // dgamma / dbeta already finalized (bn_bwd_final, side stream)
-    bn_backward_partials(bp(dout), bp(out), bp(y), fp(gamma), beta ? fp(*beta) : nullptr, fp(mean), fp(invstd),
-                         relu ? 1 : 0, bp(dy), want_dres ? bp(dres) : nullptr, fp(dgamma), fp(dbeta), M, C, nullptr, 0,
-                         cur(), mb);
-    return {dy, dres};
-  }
   if (partials.has_value()) {  // statistics partials from the producing dgrad (conv2d_dgrad_bn)
     check_f32(*partials, "partials");
     TORCH_CHECK(partials->dim() == 3 && partials->size(1) == 2 && partials->size(2) == C, "bn_bwd: partials [nblk,2,C]");
@@ -240,15 +234,6 @@ std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tens
   bn_backward(bp(dout), bp(out), bp(y), fp(gamma), beta ? fp(*beta) : nullptr, fp(mean), fp(invstd), relu ? 1 : 0,
               bp(dy), want_dres ? bp(dres) : nullptr, fp(dgamma), fp(dbeta), M, C, fp(part), cur(), mb);
   return {dy, dres};
-}
-
-void bn_bwd_final(const at::Tensor& part, int64_t M, at::Tensor dgamma, at::Tensor dbeta) {
-  check_f32(part, "partials");
-  check_f32(dgamma, "dgamma");
-  check_f32(dbeta, "dbeta");
-  TORCH_CHECK(part.dim() == 3 && part.size(1) == 2 && part.size(2) == dgamma.numel() && dbeta.numel() == dgamma.numel(),
-              "bn_bwd_final: partials [nblk,2,C]");
-  bn_backward_final(fp(part), (int)part.size(0), (int)M, (int)part.size(2), fp(dgamma), fp(dbeta), cur());
 }
 
 at::Tensor bn_infer_op(const at::Tensor& y, const at::Tensor& gamma, const at::Tensor& beta, const at::Tensor& rm,
@@ -344,9 +329,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.impl("bn_fwd", c10::DispatchKey::CUDA, &bn_fwd);
   m.def("bn_bwd(Tensor dout, Tensor out, Tensor y, Tensor gamma, Tensor mean, Tensor invstd, bool relu, "
         "bool want_dres, Tensor(a!) dgamma, Tensor(b!) dbeta, Tensor? beta=None, Tensor? mask=None, "
-        "Tensor? partials=None, bool totals_ready=False) -> (Tensor, Tensor)");
-  m.def("bn_bwd_final(Tensor part, int M, Tensor(a!) dgamma, Tensor(b!) dbeta) -> ()");
-  m.impl("bn_bwd_final", c10::DispatchKey::CUDA, &bn_bwd_final);
+        "Tensor? partials=None) -> (Tensor, Tensor)");
   m.impl("bn_bwd", c10::DispatchKey::CUDA, &bn_bwd);
   m.def("bn_infer(Tensor y, Tensor gamma, Tensor beta, Tensor rm, Tensor rv, float eps, bool relu) -> Tensor");
   m.impl("bn_infer", c10::DispatchKey::CUDA, &bn_infer_op);

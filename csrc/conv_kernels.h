@@ -80,10 +80,6 @@ void bn_backward_partials(const uint16_t* dout, const uint16_t* out, const uint1
                           const float* beta, const float* mean, const float* invstd, int relu, uint16_t* dy,
                           uint16_t* dres, float* dgamma, float* dbeta, int M, int C, const float* partials, int nblk,
                           hipStream_t st, const uint8_t* mask_bits = nullptr);
-// dbeta / dgamma from the backward partials alone (bn_final's backward mode): lets the finalize run
-// on a side stream beside the conv's weight gradient; bn_backward_partials(partials = nullptr) then
-// applies with them
-void bn_backward_final(const float* partials, int nblk, int M, int C, float* dgamma, float* dbeta, hipStream_t st);
 // inference-mode BN (running statistics), optional relu
 void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,
               float eps, int relu, uint16_t* out, int M, int C, hipStream_t st);

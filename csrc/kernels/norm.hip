@@ -683,9 +683,7 @@ void bn_backward_partials(const uint16_t* dout, const uint16_t* out, const uint1
                           hipStream_t st, const uint8_t* mask_bits) {
   const RowSplit r = row_split(M, C);
   const int mask = !relu ? 0 : (mask_bits ? 3 : (beta ? 2 : 1));
-  // partials == nullptr: dbeta / dgamma were already finalized (bn_backward_final on a side stream)
-  if (partials)
-    bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr, nullptr);
+  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr, nullptr);
 #define TFD_BN_BWDP(MK)                                                                                          \
   bn_bwd_apply_kernel<MK><<<r.nblk, NT, 0, st>>>(dout, out, y, gamma, beta, mean, invstd, dbeta, dgamma, dy, dres, M, \
                                                  C, r.tpr, r.rg, r.rb, 1.f / (float)M, mask_bits);
@@ -694,10 +692,6 @@ void bn_backward_partials(const uint16_t* dout, const uint16_t* out, const uint1
   else if (mask == 2) { TFD_BN_BWDP(2) }
   else { TFD_BN_BWDP(3) }
 #undef TFD_BN_BWDP
-}
-
-void bn_backward_final(const float* partials, int nblk, int M, int C, float* dgamma, float* dbeta, hipStream_t st) {
-  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr, nullptr);
 }
 
 void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,

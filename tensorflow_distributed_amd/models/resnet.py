@@ -219,21 +219,7 @@ def _dgrad_bn(dy, L, xs, acc, bn):
     beta = bn.beta() if (relu and mask is None) else None
     g, part = _ops().conv2d_dgrad_bn(dy, L.w(), xs, L.stride, L.pad, acc, y, mean, invstd, bn.gamma(), beta, mask,
                                      relu)
-    model = L.model
-    if model.side_finalize():
-        # dbeta / dgamma finalized on a side stream while this conv's weight gradient runs (the
-        # finalize is a few-us latency island otherwise); the BN backward waits for its event
-        main = torch.cuda.current_stream(g.device)
-        side = model.side_stream()
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            _ops().bn_bwd_final(part, y.numel() // y.shape[-1], bn.g_gamma(), bn.g_beta())
-        part.record_stream(side)
-        ev = torch.cuda.Event()
-        ev.record(side)
-        bn.bwd_totals = ev
-    else:
-        bn.bwd_part = part
+    bn.bwd_part = part
     return g
 
 
@@ -258,11 +244,8 @@ class _Conv(torch.autograd.Function):
         (x,) = ctx.saved_tensors
         L = ctx.layer
         dy = dy.contiguous()
-        # with bn_final_side the dgrad goes first: a BN finalize it forks then runs beside the wgrad
-        wgrad_first = not L.model.side_finalize()
-        if wgrad_first:
-            _ops().conv2d_wgrad(x, dy, L.g(), L.stride, L.pad, L.model.grads_zeroed)
-            L.model.reducer.mark_ready(L.name)
+        _ops().conv2d_wgrad(x, dy, L.g(), L.stride, L.pad, L.model.grads_zeroed)
+        L.model.reducer.mark_ready(L.name)
         dx = None
         if ctx.needs_input_grad[0]:
             if L.in_join is not None:
@@ -271,9 +254,6 @@ class _Conv(torch.autograd.Function):
                 dx = _dgrad_bn(dy, L, list(x.shape), None, L.in_bn)
             else:
                 dx = _ops().conv2d_dgrad(dy, L.w(), list(x.shape), L.stride, L.pad)
-        if not wgrad_first:
-            _ops().conv2d_wgrad(x, dy, L.g(), L.stride, L.pad, L.model.grads_zeroed)
-            L.model.reducer.mark_ready(L.name)
         return dx, None, None
 
 
@@ -305,11 +285,8 @@ class _BN(torch.autograd.Function):
         out = y if ctx.bits else out_or_mask  # not read when a mask (bits or from y) is given
         args = (dout.contiguous(), out, y, L.gamma(), mean, invstd, ctx.relu, ctx.has_res, L.g_gamma(), L.g_beta())
         part, L.bwd_part = L.bwd_part, None  # partials from the dgrad that produced dout, if it made them
-        ev, L.bwd_totals = L.bwd_totals, None  # or dbeta / dgamma already finalized on the side stream
         L.fwd_state = None  # its consumers' dgrads have run
-        if ev is not None:
-            torch.cuda.current_stream(dout.device).wait_event(ev)
-        dy, dres = _ops().bn_bwd(*args, beta, mask, part, ev is not None)
+        dy, dres = _ops().bn_bwd(*args, beta, mask, part)
         L.model.reducer.mark_ready(L.name + "/gamma")
         L.model.reducer.mark_ready(L.name + "/beta")
         if ctx.has_res and L.res_join is not None:
@@ -401,7 +378,6 @@ class BNLayer:
         self.res_join = None  # GradJoin of the residual input (identity shortcut)
         self.fwd_state = None  # (y, mean, invstd, relu bits, relu, has_res) of this step's forward
         self.bwd_part = None  # backward statistics partials left by the dgrad that produced dout
-        self.bwd_totals = None  # or: event of the side-stream finalize of dgamma / dbeta
         model.specs.append(PSpec(name + "/gamma", (c,), "zeros" if zero_init else "ones"))
         model.specs.append(PSpec(name + "/beta", (c,), "zeros"))
         model.bns.append(self)
@@ -456,7 +432,7 @@ class ResNet:
 
     def __init__(self, depth: int = 50, num_classes: int = 1000, device=None, seed: int = 0, width: int = 64,
                  zero_init_residual: bool = True, fuse_joins: bool = True, bn_stats: bool = True,
-                 bn_bwd_stats: bool = True, bn_final_side: bool = True):
+                 bn_bwd_stats: bool = True):
         kind, blocks = self.CFG[depth]
         if num_classes % 8 or width % 8:
             raise ValueError("num_classes and width must be multiples of 8 (16-byte MFMA operand chunks)")
@@ -476,9 +452,6 @@ class ResNet:
         # BN-backward statistics summed in the epilogue of the dgrad that produces the BN's dout
         # (conv2d_dgrad_bn) instead of bn_bwd's separate read pass over dout and y
         self.bn_bwd_stats = bn_bwd_stats
-        # ... and their finalize (dgamma / dbeta) on a side stream beside the conv's weight gradient
-        self.bn_final_side = bn_final_side and bn_bwd_stats
-        self._side = None
         # residual-free BN backward recomputes its relu mask from y instead of reading the output
         self.mask_from_y = True
         # residual BN keeps its relu mask as bits for the backward instead of re-reading the output
@@ -531,17 +504,6 @@ class ResNet:
         self.reducer = BucketReducer(self.fp)
         self.token = torch.zeros((), device=self.device, requires_grad=True)
 
-    def side_finalize(self) -> bool:
-        """BN-backward finalize on the side stream: one GPU only. Beside the DP reducer's comm stream
-        a captured step with RCCL collectives hung at replay (forced-DP world-1 test), so the DP step
-        keeps the in-order finalize."""
-        return self.bn_final_side and self.reducer.stream is None
-
-    def side_stream(self):
-        if self._side is None:
-            self._side = torch.cuda.Stream(self.device)
-        return self._side
-
     @property
     def num_params(self) -> int:
         return sum(s.numel for s in self.specs)
@@ -553,7 +515,7 @@ class ResNet:
         for j in self.joins:
             j.reset()
         for bn in self.bns:
-            bn.fwd_state, bn.bwd_part, bn.bwd_totals = None, None, None
+            bn.fwd_state, bn.bwd_part = None, None
         x = _ops().pad_channels(x_nhwc_f32, 8)
         x = self.stem_bn(self.stem(x))
         x = _MaxPool.apply(x, 3, 2, 1)

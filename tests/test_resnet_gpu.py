@@ -278,17 +278,14 @@ def test_bn_bwd_stats_in_dgrad_epilogue(cuda, depth, monkeypatch):
     x = torch.randn(4, 32, 32, 3, device=cuda)
     lab = torch.randint(0, 16, (4,), dtype=torch.int32, device=cuda)
     out = []
-    for on, side in ((False, False), (True, False), (True, True)):
-        m = R.ResNet(depth, num_classes=16, device=cuda, seed=3, width=16, zero_init_residual=False, bn_bwd_stats=on,
-                     bn_final_side=side)
+    for on in (False, True):
+        m = R.ResNet(depth, num_classes=16, device=cuda, seed=3, width=16, zero_init_residual=False, bn_bwd_stats=on)
         m.fp.grad.zero_()
         loss, _ = m.loss(x, lab)
         loss.backward()
         torch.cuda.synchronize()
         out.append((loss.item(), m.fp.grad.clone()))
-    assert out[0][0] == out[1][0] == out[2][0]  # same forward
-    # the side-stream finalize (and dgrad-before-wgrad order) changes no bit
-    assert torch.equal(out[1][1], out[2][1])
+    assert out[0][0] == out[1][0]  # same forward
     g0, g1 = out[0][1], out[1][1]
     assert torch.isfinite(g1).all()
     rel = ((g1 - g0).norm() / g0.norm()).item()
