@@ -1816,9 +1816,15 @@ __global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) { conv2_
 #ifndef TFD_C2_BWD_ONE
 #define TFD_C2_BWD_ONE 1
 #endif
+#ifndef TFD_DIAG_C2BWD  // timing diagnosis only (wrong gradients): 1 drops the wgrad blocks, 2 the dgrad blocks
+#define TFD_DIAG_C2BWD 0
+#endif
 __global__ __launch_bounds__(512) void conv2_bwd_lds(MnistStepArgs a, int nw) {
-  if ((int)blockIdx.x < nw) conv2_wgrad_body(a, blockIdx.x);
-  else conv2_dgrad_body(a, blockIdx.x - nw);
+  if ((int)blockIdx.x < nw) {
+    if (TFD_DIAG_C2BWD != 1) conv2_wgrad_body(a, blockIdx.x);
+  } else if (TFD_DIAG_C2BWD != 2) {
+    conv2_dgrad_body(a, blockIdx.x - nw);
+  }
 }
 
 // K13 + K14 in one launch: conv2 dgrad and wgrad both consume dz2 only (independent).
