@@ -1370,10 +1370,20 @@ __device__ __forceinline__ void conv2_dgrad_block(const MnistStepArgs& a, int bx
 #define TFD_C2D_PIPE 1
 #endif
 constexpr int C2D_ROWS = 11, C2D_COLS = 20, C2D_PLANE = 224;
-// weight row pitch 80 (not 72): the B-fragment ds_read_b128 of rows co = lane & 15 is conflict-free
-// (72: 2-way, 3.2 K vs 1.6 K LDS cycles per block; scripts/debug/lds_banks.py)
-constexpr int C2D_WLD = 80;
-constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 800 * C2D_WLD) * 2;  // 156672 B
+// weight rows (tap, ci) x 64 co. TFD_C2D_GLDS=1: staged by LDS-DMA (global_load_lds_dwordx4: no
+// VGPR round trip, no ds_write pass; one wave instruction fills 1 KiB = 8 rows) into an unpadded
+// image whose 16-B chunk c of row r holds global chunk c ^ (r & 7) -- the swizzle is applied to
+// the per-lane SOURCE address, and the 16 rows of a B-fragment ds_read_b128 group then hit 16
+// distinct bank quads. 0: register staging into rows of pitch 80 (not 72: the B-fragment reads of
+// rows co = lane & 15 are conflict-free; 72: 2-way, 3.2 K vs 1.6 K LDS cycles per block).
+#ifndef TFD_C2D_GLDS
+#define TFD_C2D_GLDS 1
+#endif
+constexpr int C2D_WLD = TFD_C2D_GLDS ? 64 : 80;
+__device__ __forceinline__ const bf16* c2d_w(const bf16* wt, int rr, int ch) {
+  return TFD_C2D_GLDS ? wt + rr * 64 + ((ch ^ (rr & 7)) << 3) : wt + rr * C2D_WLD + ch * 8;
+}
+constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 800 * C2D_WLD) * 2;  // 131072 B (156672 at pitch 80)
 static_assert(C2D_PLANE * 16 % 256 == 0 && C2D_PLANE >= C2D_ROWS * C2D_COLS, "dz2 plane");
 constexpr int C1W_HALF = 98;  // pooled conv1 pixels per half image (7 rows of 14)
 #ifndef TFD_C1W_XS  // row pitch (floats) of the tail's zero-bordered x image
@@ -1394,7 +1404,14 @@ constexpr int C2D_P_OFF = C2D_I_OFF + C1W_HALF * 32;
 static_assert(C2D_I_OFF % 16 == 0 && C2D_P_OFF % 16 == 0, "LDS carve alignment");
 static_assert(C2D_P_OFF + 16 * 833 * 4 <= C2D_SMEM, "fused conv1-wgrad tail exceeds the dgrad LDS");
 static_assert(4 * 4 * 64 * 16 <= C2D_X_OFF, "park region overlaps the fused tail");
+// timing-stamp builds (TFD_STAMP): thread 0 of dgrad block bid records s_memtime at 8 phase
+// boundaries into dbg[5 * B * 8 + bid * 8 + k] (scripts/debug/stamps.py dgrad)
+#define C2D_STAMP(k)                                                                                     \
+  do {                                                                                                   \
+    if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[5 * a.B * 8 + bid * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
+  } while (0)
 __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const int bid) {
+  C2D_STAMP(0);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* img = (bf16*)smem_raw;                           // [8][224][8]
   bf16* wt = img + 8 * C2D_PLANE * 8;                    // [800][72]
@@ -1408,6 +1425,17 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
 #endif
   {
     constexpr int CI = 8 * C2D_PLANE, NI = (CI + 511) / 512;  // 1792 chunks -> 4 per thread
+#if TFD_C2D_GLDS
+    {  // 6400 weight chunks = 100 LDS-DMA wave instructions, 12-13 per wave, all in flight at once
+      (void)rot;
+      const int wv = t >> 6, ln = t & 63;
+      for (int ii = wv; ii < 100; ii += 8) {
+        const int p = ii * 64 + ln, rr = p >> 3, sl = p & 7;
+        __builtin_amdgcn_global_load_lds((const void*)(wsrc + rr * 64 + ((sl ^ (rr & 7)) << 3)),
+                                         (__attribute__((address_space(3))) void*)(wt + ii * 64 * 8), 16, 0, 0);
+      }
+    }
+#endif
     uint4 vi[NI];
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -1417,7 +1445,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
                   ? *reinterpret_cast<const uint4*>(src + (r * 14 + c) * 64 + ch * 8) : zero4();
     }
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
+    for (int half = 0; half < (TFD_C2D_GLDS ? 0 : 2); ++half) {
       constexpr int NH = (3200 + 511) / 512;
       uint4 vw[NH];
 #pragma unroll
@@ -1437,6 +1465,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
       if (i < CI) *reinterpret_cast<uint4*>(img + i * 8) = vi[j];
     }
   }
+  C2D_STAMP(1);
   const int lane = t & 63, w = t >> 6, g = lane >> 4, mt0 = w & 3, kq = w >> 2;
   const int two = (mt0 + 4 < 7);
 #if TFD_C1W_PRE
@@ -1469,6 +1498,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
   }
 #endif
   __syncthreads();
+  C2D_STAMP(2);
   const int iw = lane & 15;
   int base[2];
 #pragma unroll
@@ -1476,7 +1506,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
   f32x4 acc[2][2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bf16* wrow = wt + (lane & 15) * C2D_WLD + 8 * g;
+  const int nl = lane & 15;
 #if TFD_C2D_PIPE
   // Fully unrolled, software-pipelined K loop: step st = (tap, co half sk), step st + 1's four
   // fragments are read while step st's MFMAs run; both M-tiles on every wave (the second tile of
@@ -1490,9 +1520,8 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
     auto ld = [&](int st, int slot) {
       const int tap = tapb + (st >> 1), sk = st & 1;
       const int kh = tap / 5, kw = tap - kh * 5, coff = -(kh * C2D_COLS + kw) * 8 + sk * 4 * C2D_PLANE * 8;
-      const bf16* wr = wrow + tap * 32 * C2D_WLD + sk * 32;
-      fb[slot][0] = *reinterpret_cast<const bf16x8*>(wr);
-      fb[slot][1] = *reinterpret_cast<const bf16x8*>(wr + 16 * C2D_WLD);
+      fb[slot][0] = *reinterpret_cast<const bf16x8*>(c2d_w(wt, tap * 32 + nl, g + 4 * sk));
+      fb[slot][1] = *reinterpret_cast<const bf16x8*>(c2d_w(wt, tap * 32 + 16 + nl, g + 4 * sk));
       fa[slot][0] = *reinterpret_cast<const bf16x8*>(img + base[0] + coff);
       fa[slot][1] = *reinterpret_cast<const bf16x8*>(img + base[1] + coff);
     };
@@ -1521,9 +1550,8 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
     const int kh = tap / 5, kw = tap - kh * 5, toff = -(kh * C2D_COLS + kw) * 8;
 #pragma unroll
     for (int sk = 0; sk < 2; ++sk) {
-      const bf16* wr = wrow + tap * 32 * C2D_WLD + sk * 32;
-      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(wr);
-      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(wr + 16 * C2D_WLD);
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(c2d_w(wt, tap * 32 + nl, g + 4 * sk));
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(c2d_w(wt, tap * 32 + 16 + nl, g + 4 * sk));
       const int coff = toff + sk * 4 * C2D_PLANE * 8;  // co chunk 4sk + g
       const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(img + base[0] + coff);
       acc[0][0] = mfma16x16x32(a0, b0, acc[0][0]);
@@ -1536,6 +1564,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
     }
   }
   // sum the two K halves: waves 4..7 park their accumulators in LDS (image region is dead now)
+  C2D_STAMP(3);
   __syncthreads();
   f32x4* park = reinterpret_cast<f32x4*>(smem_raw);  // [4 waves][4 tiles][64 lanes]
   if (kq) {
@@ -1545,6 +1574,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
       for (int nt = 0; nt < 2; ++nt) park[(mt0 * 4 + j * 2 + nt) * 64 + lane] = acc[j][nt];
   }
   __syncthreads();
+  C2D_STAMP(4);
   // K15 + K12 fused: this block's dX rows ARE conv1's pooled-gradient rows [7h, 7h + 7) of image b,
   // so conv1's weight/bias gradient partial for them is computed here from LDS (no dp1m round trip,
   // no separate launch). The weight region of LDS is dead now: x image, masked gradient, argmax.
@@ -1600,6 +1630,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
 #endif
   }
   __syncthreads();
+  C2D_STAMP(5);
   {
     // only the argmax position of each 2x2 window carries gradient: dW1[tap][c] += g * x[argmax + tap]
     const int c = t & 31, sub = t >> 5;
@@ -1621,6 +1652,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
 #pragma unroll
     for (int j = 0; j < 26; ++j) part[sub * 833 + j * 32 + c] = acc1[j];
   }
+  C2D_STAMP(6);
   __syncthreads();
   for (int i = t; i < 26 * 32; i += 512) {
     float sm = 0.f;
@@ -1628,6 +1660,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
     for (int q = 0; q < 16; ++q) sm += part[q * 833 + i];
     a.wg1_slab[(size_t)bid * 832 + i] = sm;
   }
+  C2D_STAMP(7);
 }
 
 // ---------------- K14 conv2 wgrad (+bias row), split-K slabs ----------------

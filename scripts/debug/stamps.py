@@ -1,4 +1,4 @@
-"""Per-phase clocks of the conv12 kernel from a TFD_STAMP build (TFD_NATIVE_LIB=..._C_stamp.so):
+"""Per-phase clocks of the conv12, head and conv2-dgrad kernels from a TFD_STAMP build (TFD_NATIVE_LIB=..._C_stamp.so):
 median over blocks of the s_memtime deltas between consecutive stamps, after warm replays."""
 import os
 import sys
@@ -15,7 +15,7 @@ dev = torch.device("cuda", 0)
 B = 128
 eng = torch.classes.tfd.MnistEngine(B, 0, 0.75, 1, 0)
 eng.set_adam(0.01, 0.9, 0.999, 1e-8)
-dbg = torch.zeros(5 * B * 8, dtype=torch.int64, device=dev)
+dbg = torch.zeros(8 * B * 8, dtype=torch.int64, device=dev)
 eng.set_debug_buffer(dbg)
 s = torch.cuda.Stream()
 with torch.cuda.stream(s):
@@ -68,3 +68,12 @@ print("head block span: median", (h[:, 4] - h[:, 0]).median().item())
 for k in range(4):
     dd = h[:, k + 1] - h[:, k]
     print(f"head {hn[k]:23s} median {dd.median().item():8d}  p90 {dd.float().quantile(0.9).item():8.0f}")
+
+dg = dbg.view(-1, 8).cpu()[5 * B:5 * B + 2 * B]
+if (dg[:, 7] > 0).all():
+    dn = ["issue staging loads", "image LDS stores + barrier", "K loop (MFMA)", "park barrier",
+          "gsl / x / argmax + barrier", "conv1-wgrad accumulate", "partial reduce + slab store"]
+    print("dgrad block span: median", (dg[:, 7] - dg[:, 0]).median().item())
+    for k in range(7):
+        dd = dg[:, k + 1] - dg[:, k]
+        print(f"dgrad {dn[k]:28s} median {dd.median().item():8d}  p90 {dd.float().quantile(0.9).item():8.0f}")
