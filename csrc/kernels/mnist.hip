@@ -1404,6 +1404,24 @@ constexpr int C2D_P_OFF = C2D_I_OFF + C1W_HALF * 32;
 static_assert(C2D_I_OFF % 16 == 0 && C2D_P_OFF % 16 == 0, "LDS carve alignment");
 static_assert(C2D_P_OFF + 16 * 833 * 4 <= C2D_SMEM, "fused conv1-wgrad tail exceeds the dgrad LDS");
 static_assert(4 * 4 * 64 * 16 <= C2D_X_OFF, "park region overlaps the fused tail");
+// TFD_C1W_MFMA=1: the conv1 weight gradient of the tail on the matrix core. dW1[tap][c] =
+// sum_px X[tap][px] dz1[px][c] over the half image's 14 x 28 conv1 output pixels (rows padded to
+// 32, K = 448 = 14 k-steps) with dz1 the unpooled pre-activation gradient (the bf16-rounded pooled
+// gradient at its window's argmax position, zero elsewhere) and X the im2col of the zero-bordered x
+// image, read from 5 column-shifted bf16 copies of its 18 rows so every A fragment is one 16-B read;
+// row 25 of A is ones (the bias). 8 waves = 2 tap tiles x 2 channel tiles x 2 K halves. Replaces the
+// per-thread loop of 25 scalar LDS reads + FMAs per pooled pixel (phase clocks: 7.0 k of the dgrad
+// block's 18.4 k cycles, profiles/stamps_dgrad_r3.log).
+#ifndef TFD_C1W_MFMA
+#define TFD_C1W_MFMA 1
+#endif
+constexpr int C2D_Z_OFF = C2D_X_OFF;                        // dz1 [448][32] bf16, chunk-swizzled
+constexpr int C2D_XS_OFF = C2D_Z_OFF + 448 * 32 * 2;        // x copies [5][18][40] bf16
+constexpr int C2D_T_END = C2D_XS_OFF + 5 * 18 * 40 * 2;
+static_assert(C2D_T_END <= C2D_SMEM && C2D_XS_OFF % 16 == 0 && (C2D_T_END - C2D_Z_OFF) % 16 == 0, "MFMA tail LDS");
+__device__ __forceinline__ int c1w_dz(int px, int c) {  // element offset of dz1[px][c]
+  return px * 32 + (((c >> 3) ^ (2 * ((px >> 3) & 1))) << 3) + (c & 7);
+}
 // timing-stamp builds (TFD_STAMP): thread 0 of dgrad block bid records s_memtime at 8 phase
 // boundaries into dbg[5 * B * 8 + bid * 8 + k] (scripts/debug/stamps.py dgrad)
 #define C2D_STAMP(k)                                                                                     \
@@ -1475,6 +1493,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
   float xpre[4];
   uint4 ipre = zero4();
   uint16_t p1pre[2][2][4];
+  [[maybe_unused]] uint8_t ipb[2][2][4];  // MFMA tail: the argmax window position of each dX value
   if (kq) {
     const int u = t - 256;
     const float* xrow = a.data + (size_t)data_row(a, b) * 784;
@@ -1494,6 +1513,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
         for (int r = 0; r < 4; ++r) {
           const int x = min(4 * g + r, 13), n = nt * 16 + (lane & 15), ih = 7 * h + min(mt0 + 4 * j, 6);
           p1pre[j][nt][r] = a.p1[((size_t)b * 196 + ih * 14 + x) * 32 + n];
+          if (TFD_C1W_MFMA) ipb[j][nt][r] = a.idx1[((size_t)b * 196 + ih * 14 + x) * 32 + n];
         }
   }
 #endif
@@ -1573,8 +1593,81 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) park[(mt0 * 4 + j * 2 + nt) * 64 + lane] = acc[j][nt];
   }
+#if TFD_C1W_PRE && TFD_C1W_MFMA
+  for (int i = t; i < (C2D_T_END - C2D_Z_OFF) / 16; i += 512)  // dz1 and the x copies start zero
+    reinterpret_cast<uint4*>(smem_raw + C2D_Z_OFF)[i] = zero4();
+#endif
   __syncthreads();
   C2D_STAMP(4);
+#if TFD_C1W_PRE && TFD_C1W_MFMA
+  {
+    bf16* dz1 = reinterpret_cast<bf16*>(smem_raw + C2D_Z_OFF);
+    bf16* xsh = reinterpret_cast<bf16*>(smem_raw + C2D_XS_OFF);
+    if (!kq) {  // dX (+ the parked K half) through conv1's relu mask, scattered to the argmax pixel
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (j == 1 && !two) break;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const f32x4 v = acc[j][nt] + park[(mt0 * 4 + j * 2 + nt) * 64 + lane];
+          const int n = nt * 16 + (lane & 15), lr = mt0 + 4 * j;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int x = 4 * g + r;
+            if (x >= 14) break;
+            const int wi = ipb[j][nt][r], px = (2 * lr + (wi >> 1)) * 32 + 2 * x + (wi & 1);
+            reinterpret_cast<uint16_t*>(dz1)[c1w_dz(px, n)] = p1pre[j][nt][r] != 0 ? f2bf_bits(v[r]) : (uint16_t)0;
+          }
+        }
+      }
+    } else {  // x rows 14h .. 14h + 17 of the zero-bordered image, 5 column shifts, bf16
+      const int u = t - 256;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 4 * u + q, r = i >> 5, c = i & 31, rr = r - 14 * h;
+        if ((unsigned)rr < 18u) {
+          const uint16_t xv = f2bf_bits(xpre[q]);
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw)
+            if (c >= kw) reinterpret_cast<uint16_t*>(xsh)[(kw * 18 + rr) * 40 + c - kw] = xv;
+        }
+      }
+    }
+    __syncthreads();
+    C2D_STAMP(5);
+    const int mi = w & 1, ni = (w >> 1) & 1, kh2 = w >> 2;
+    const int tap = 16 * mi + (lane & 15), tc = min(tap, 24), tkh = tc / 5, tkw = tc - 5 * tkh;
+    const int q = (lane & 15) >> 2, p4 = lane & 3;
+    bf16x8 ones, zer;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { ones[e] = (bf16)1.0f; zer[e] = (bf16)0.0f; }
+    f32x4 c2 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k7 = 0; k7 < 7; ++k7) {
+      const int ks = 7 * kh2 + k7, px0 = ks * 32 + 8 * g, rl = px0 >> 5, col0 = px0 & 31;
+      bf16x8 af = *reinterpret_cast<const bf16x8*>(xsh + (tkw * 18 + rl + tkh) * 40 + col0);
+      if (tap >= 25) af = (tap == 25) ? ones : zer;
+      const int row0 = ks * 32 + 8 * g + q, col = 16 * ni + 4 * p4;
+      const bf16x8 bfr = frag_tr16(dz1 + c1w_dz(row0, col), dz1 + c1w_dz(row0 + 4, col));
+      c2 = mfma16x16x32(af, bfr, c2);
+    }
+    f32x4* park2 = reinterpret_cast<f32x4*>(smem_raw);  // the first park is dead (read above)
+    if (kh2) park2[(w & 3) * 64 + lane] = c2;
+    C2D_STAMP(6);
+    __syncthreads();
+    if (!kh2) {
+      c2 += park2[(w & 3) * 64 + lane];
+      const int c = 16 * ni + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int to = 16 * mi + 4 * g + r;  // taps 0..24, 25 = bias
+        if (to < 26) a.wg1_slab[(size_t)bid * 832 + to * 32 + c] = c2[r];
+      }
+    }
+    C2D_STAMP(7);
+    return;
+  }
+#endif
   // K15 + K12 fused: this block's dX rows ARE conv1's pooled-gradient rows [7h, 7h + 7) of image b,
   // so conv1's weight/bias gradient partial for them is computed here from LDS (no dp1m round trip,
   // no separate launch). The weight region of LDS is dead now: x image, masked gradient, argmax.
