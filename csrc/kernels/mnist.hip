@@ -25,7 +25,6 @@
 #include "../gemm.h"
 #include "../mnist_layout.h"
 #include "../tfd_kernels.h"
-#include "../c2wl_perm.h"
 
 #include <algorithm>
 #include <stdexcept>
@@ -1800,9 +1799,6 @@ __global__ __launch_bounds__(256) void conv2_wgrad_k(MnistStepArgs a, int kper) 
 #ifndef TFD_C2WL_NTG
 #define TFD_C2WL_NTG 4
 #endif
-#ifndef TFD_C2WL_PERM  // 1: K (pixel) order grouped by LDS bank class (csrc/c2wl_perm.h): conflict-free
-#define TFD_C2WL_PERM 0  //    A-fragment tr-reads (LDS model 1968 -> 1344 cycles per image, but measured +1.1 us/step: profiles/ab_c2wl_perm_r3.log)
-#endif
 constexpr int C2WL_IMG = TFD_C2WL_IMG;      // images per block (= slab count B / C2WL_IMG)
 constexpr int C2WL_NTG = TFD_C2WL_NTG;      // tap groups (4: [0,6) [6,12) [12,18) [18,25))
 constexpr int C2WL_TPG = 25 / C2WL_NTG;     // taps per group (the last takes the remainder)
@@ -1814,7 +1810,12 @@ constexpr int C2WL_IMG_ELEMS = C2WL_PW * C2WL_PW * C2WL_CS;
 constexpr int C2WL_BRED_OFF = (C2WL_IMG_ELEMS + C2WL_KP * C2WL_DS) * 2;
 constexpr int C2WL_SMEM = C2WL_BRED_OFF + 8 * 64 * 4;  // 65408 B: two blocks per CU
 static_assert(C2WL_BRED_OFF % 16 == 0 && (C2WL_IMG_ELEMS * 2) % 16 == 0, "LDS carve alignment");
+#define C2W_STAMP(k)                                                                                     \
+  do {                                                                                                   \
+    if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[7 * a.B * 8 + bid * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
+  } while (0)
 __device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const int bid) {
+  C2W_STAMP(0);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* img = (bf16*)smem_raw;
   bf16* dz = img + C2WL_IMG_ELEMS;
@@ -1822,44 +1823,6 @@ __device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const i
   const int tg = bid % C2WL_NTG, ip = bid / C2WL_NTG, t = threadIdx.x;
   const int tap0 = tg * C2WL_TPG, ntaps = (tg == C2WL_NTG - 1) ? 25 - tap0 : C2WL_TPG;
   const int lane = t & 63, w = t >> 6, h = w >> 2, n = w & 3, g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
-  // the image border and the dz2 pad rows stay zero for every image of the block
-  for (int i = t; i < C2WL_PW * C2WL_PW; i += 512) {
-    const int r = i / C2WL_PW, c = i - r * C2WL_PW;
-    if (r < 2 || r >= 16 || c < 2 || c >= 16) {
-      uint4* d = reinterpret_cast<uint4*>(img + i * C2WL_CS);
-      d[0] = zero4(); d[1] = zero4(); d[2] = zero4(); d[3] = zero4();
-    }
-  }
-#if TFD_C2WL_PERM
-  for (int i = t; i < (C2WL_KP - 196) * (C2WL_DS / 8); i += 512)
-    reinterpret_cast<uint4*>(dz + c2wl_pad[i / (C2WL_DS / 8)] * C2WL_DS)[i % (C2WL_DS / 8)] = zero4();
-#else
-  for (int i = t; i < (C2WL_KP - 196) * (C2WL_DS / 8); i += 512) reinterpret_cast<uint4*>(dz + 196 * C2WL_DS)[i] = zero4();
-#endif
-  // padded-image positions of this lane's two tr-read rows (k-slots 32s + 8g + q and +4) per k-step
-  int pos[7][2];
-#pragma unroll
-  for (int s = 0; s < 7; ++s)
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int k = 32 * s + 8 * g + q + 4 * u;
-#if TFD_C2WL_PERM
-      pos[s][u] = c2wl_kpos[k];  // pad slots: a border position of the missing bank class (dz2 row zero)
-#else
-      pos[s][u] = k < 196 ? (k / 14) * C2WL_PW + (k % 14) : 0;  // pad pixels: dz2 rows are zero
-#endif
-    }
-#if TFD_C2WL_PERM
-  int dzrow[4];  // the LDS (k-slot) row of each dz2 chunk this thread stages
-#pragma unroll
-  for (int j = 0; j < 4; ++j) dzrow[j] = c2wl_row[min((t + 512 * j) >> 3, 195)];
-#endif
-  f32x4 acc[C2WL_MAXT];
-#pragma unroll
-  for (int j = 0; j < C2WL_MAXT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;
-  // image ii + 1's global loads are issued before image ii's MFMAs, so its staging latency hides
-  // under them (one image at a time left the CU idle through each ~37 KB load)
   uint4 v1[2], v2[4];
   auto gload = [&](int b) {
     const uint4* s1 = reinterpret_cast<const uint4*>(a.p1 + (size_t)b * 196 * 32);
@@ -1869,7 +1832,31 @@ __device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const i
 #pragma unroll
     for (int j = 0; j < 4; ++j) { const int i = t + 512 * j; v2[j] = i < 1568 ? s2[i] : zero4(); }
   };
-  if (ip * C2WL_IMG < a.B) gload(ip * C2WL_IMG);
+  if (ip * C2WL_IMG < a.B) gload(ip * C2WL_IMG);  // first image's loads before the LDS zeroing
+  // the image border and the dz2 pad rows stay zero for every image of the block
+  for (int i = t; i < C2WL_PW * C2WL_PW; i += 512) {
+    const int r = i / C2WL_PW, c = i - r * C2WL_PW;
+    if (r < 2 || r >= 16 || c < 2 || c >= 16) {
+      uint4* d = reinterpret_cast<uint4*>(img + i * C2WL_CS);
+      d[0] = zero4(); d[1] = zero4(); d[2] = zero4(); d[3] = zero4();
+    }
+  }
+  for (int i = t; i < (C2WL_KP - 196) * (C2WL_DS / 8); i += 512) reinterpret_cast<uint4*>(dz + 196 * C2WL_DS)[i] = zero4();
+  // padded-image positions of this lane's two tr-read rows (k-slots 32s + 8g + q and +4) per k-step
+  int pos[7][2];
+#pragma unroll
+  for (int s = 0; s < 7; ++s)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = 32 * s + 8 * g + q + 4 * u;
+      pos[s][u] = k < 196 ? (k / 14) * C2WL_PW + (k % 14) : 0;  // pad pixels: dz2 rows are zero
+    }
+  f32x4 acc[C2WL_MAXT];
+#pragma unroll
+  for (int j = 0; j < C2WL_MAXT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  // image ii + 1's global loads are issued before image ii's MFMAs, so its staging latency hides
+  // under them (one image at a time left the CU idle through each ~37 KB load)
   for (int ii = 0; ii < C2WL_IMG; ++ii) {
     const int b = ip * C2WL_IMG + ii;
     if (b >= a.B) break;
@@ -1886,17 +1873,14 @@ __device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const i
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int i = t + 512 * j;
-#if TFD_C2WL_PERM
-        if (i < 1568) *reinterpret_cast<uint4*>(dz + dzrow[j] * C2WL_DS + (i & 7) * 8) = v2[j];
-#else
         if (i < 1568) *reinterpret_cast<uint4*>(dz + (i >> 3) * C2WL_DS + (i & 7) * 8) = v2[j];
-#endif
       }
     }
     __syncthreads();
+    C2W_STAMP(1 + 2 * ii);
     if (ii + 1 < C2WL_IMG && b + 1 < a.B) gload(b + 1);
     if (tg == 0) {  // bias row: column sums of dz2 (pixel slice t >> 6 of 8)
-      for (int px = t >> 6; px < (TFD_C2WL_PERM ? C2WL_KP : 196); px += 8) bsum += bf2f(dz[px * C2WL_DS + (t & 63)]);
+      for (int px = t >> 6; px < 196; px += 8) bsum += bf2f(dz[px * C2WL_DS + (t & 63)]);
     }
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
@@ -1912,6 +1896,7 @@ __device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const i
         }
       }
     }
+    C2W_STAMP(2 + 2 * ii);
   }
   float* slab = a.wg2_slab + (size_t)ip * 801 * 64;
 #pragma unroll
@@ -1932,6 +1917,7 @@ __device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const i
       slab[800 * 64 + t] = sm;
     }
   }
+  C2W_STAMP(7);
 }
 
 __global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) { conv2_wgrad_body(a, blockIdx.x); }

@@ -15,7 +15,7 @@ dev = torch.device("cuda", 0)
 B = 128
 eng = torch.classes.tfd.MnistEngine(B, 0, 0.75, 1, 0)
 eng.set_adam(0.01, 0.9, 0.999, 1e-8)
-dbg = torch.zeros(8 * B * 8, dtype=torch.int64, device=dev)
+dbg = torch.zeros(10 * B * 8, dtype=torch.int64, device=dev)
 eng.set_debug_buffer(dbg)
 s = torch.cuda.Stream()
 with torch.cuda.stream(s):
@@ -77,3 +77,14 @@ if (dg[:, 7] > 0).all():
     for k in range(7):
         dd = dg[:, k + 1] - dg[:, k]
         print(f"dgrad {dn[k]:28s} median {dd.median().item():8d}  p90 {dd.float().quantile(0.9).item():8.0f}")
+
+wg = dbg.view(-1, 8).cpu()[7 * B:9 * B]
+if (wg[:, 7] > 0).all():
+    wn2 = ["zero + image 0 loads + LDS stores + barrier", "image 0 MFMAs", "image 1 LDS stores + barrier",
+           "image 1 MFMAs"]
+    print("wgrad block span: median", (wg[:, 7] - wg[:, 0]).median().item())
+    for k in range(4):
+        dd = wg[:, k + 1] - wg[:, k]
+        print(f"wgrad {wn2[k]:44s} median {dd.median().item():8d}  p90 {dd.float().quantile(0.9).item():8.0f}")
+    dd = wg[:, 7] - wg[:, 4]
+    print(f"wgrad {'slab epilogue (+ bias sum)':44s} median {dd.median().item():8d}")
