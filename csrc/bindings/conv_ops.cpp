@@ -94,7 +94,7 @@ std::tuple<at::Tensor, at::Tensor> conv2d_dgrad_bn(const at::Tensor& dy, const a
   }
   const ConvShape c = shape_of(x, w, stride, pad);
   TORCH_CHECK(dy.size(1) == c.Ho() && dy.size(2) == c.Wo() && dy.size(3) == c.K, "dgrad_bn: dy shape mismatch");
-  TORCH_CHECK(conv_dgrad_bn_supported(c), "dgrad_bn: stride-1 dgrads with C % 8 == 0 only");
+  TORCH_CHECK(conv_dgrad_bn_supported(c), "dgrad_bn: unsupported conv (C % 8, or a strided dgrad with tap-less phases)");
   TORCH_CHECK(y.numel() < (1ll << 30), "dgrad_bn: < 2^30 elements (buffer addressing)");
   check_f32(mean, "mean");
   check_f32(invstd, "invstd");

@@ -547,16 +547,20 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB
 }
 
 // one phase of a strided dgrad: Y rows scattered to the phase's pixels (+ add)
-template <int BM, int BN, bool ADD>
+// BS (BnB<MODE>): the phase's rows of the BN-backward partials go to part[blockIdx.y] (part is
+// offset per phase by the caller, so the phases' row blocks stack)
+template <int BM, int BN, bool ADD, class BS = NoBnB>
 __global__ __launch_bounds__(256) TFD_CONV_ATTR void dgrad_phase_kernel(DgradPhaseA la, DgradPhaseB lb, uint16_t* dx,
-                                                                        const uint16_t* add) {
+                                                                        const uint16_t* add, float* part = nullptr,
+                                                                        BS bs = BS{}) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   f32x4 acc[BM / 32][BN / 32];
   gemm_mainloop<BM, BN, CBK, 2, 2, DgradPhaseA, DgradPhaseB, conv_rs<BM, BN>()>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0,
                                                                          la.g.KD, (bf16*)smem_raw, acc);
   const uint32_t xbytes = (uint32_t)la.g.N * la.g.H * la.g.W * la.g.C * 2u;
-  lds_epilogue<BM, BN, 2, 2, ADD, false, PhaseRows>(acc, smem_raw, dx, add, la.g.M, la.g.C, blockIdx.y * BM,
-                                                   blockIdx.x * BN, nullptr, PhaseRows{la.g}, xbytes);
+  lds_epilogue<BM, BN, 2, 2, ADD, false, PhaseRows, BS>(acc, smem_raw, dx, add, la.g.M, la.g.C, blockIdx.y * BM,
+                                                       blockIdx.x * BN, part, PhaseRows{la.g}, xbytes, nullptr, 0,
+                                                       nullptr, bs);
 }
 
 // pixels of tap-less phases (a 1x1 stride-2 conv leaves 3 of 4 input pixels without a tap):
@@ -768,24 +772,28 @@ static void conv_dgrad_impl(const ConvShape& c, const uint16_t* dy, const uint16
 #ifndef TFD_DGRAD_PHASES  // 1: strided dgrads as one dense GEMM per output phase (dgrad_strided)
 #define TFD_DGRAD_PHASES 1
 #endif
-template <int BM, int BN, bool ADD>
+template <int BM, int BN, bool ADD, class BS = NoBnB>
 static void launch_phase(const DgradPhaseA& la, const DgradPhaseB& lb, uint16_t* dx, const uint16_t* add,
-                         hipStream_t st) {
+                         hipStream_t st, float* part = nullptr, const BS& bs = BS{}) {
   constexpr int sm = GemmSmem<BM, BN, CBK, DgradPhaseA, DgradPhaseB>::BYTES > LdsEpi<BM, BN, 2, 2>::BYTES
                          ? GemmSmem<BM, BN, CBK, DgradPhaseA, DgradPhaseB>::BYTES : LdsEpi<BM, BN, 2, 2>::BYTES;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dgrad_phase_kernel<BM, BN, ADD>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dgrad_phase_kernel<BM, BN, ADD, BS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, sm);
     attr = true;
   }
   dim3 grid((la.g.C + BN - 1) / BN, (la.g.M + BM - 1) / BM, 1);
-  dgrad_phase_kernel<BM, BN, ADD><<<grid, 256, sm, st>>>(la, lb, dx, add);
+  dgrad_phase_kernel<BM, BN, ADD, BS><<<grid, 256, sm, st>>>(la, lb, dx, add, part, bs);
 }
-static void dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, const uint16_t* add,
-                          hipStream_t st) {
+// BS != NoBnB: every phase also emits its BN-backward partial rows at part + (rows so far) * 2 * C
+// (callers ensure no phase is tap-less: those pixels would carry no partials). Returns the rows.
+template <class BS = NoBnB>
+static int dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, const uint16_t* add,
+                         hipStream_t st, float* part = nullptr, const BS& bs = BS{}) {
   const int s = c.stride;
   bool empty = false;
+  int rows = 0;
   for (int ph = 0; ph < s; ++ph)
     for (int pw = 0; pw < s; ++pw) {
       PhaseGeo g;
@@ -804,14 +812,16 @@ static void dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t
       DgradPhaseA la{dy, g};
       DgradPhaseB lb{w, g, c.S};
       const OutTile ot = out_tile(g.M, c.C);
+      float* pp = part ? part + (size_t)rows * 2 * c.C : nullptr;
+      rows += ot == OT64 ? (g.M + 63) / 64 : (g.M + 127) / 128;
       if (add) {
-        if (ot == OT128) launch_phase<128, 128, true>(la, lb, dx, add, st);
-        else if (ot == OT128x64) launch_phase<128, 64, true>(la, lb, dx, add, st);
-        else launch_phase<64, 64, true>(la, lb, dx, add, st);
+        if (ot == OT128) launch_phase<128, 128, true>(la, lb, dx, add, st, pp, bs);
+        else if (ot == OT128x64) launch_phase<128, 64, true>(la, lb, dx, add, st, pp, bs);
+        else launch_phase<64, 64, true>(la, lb, dx, add, st, pp, bs);
       } else {
-        if (ot == OT128) launch_phase<128, 128, false>(la, lb, dx, add, st);
-        else if (ot == OT128x64) launch_phase<128, 64, false>(la, lb, dx, add, st);
-        else launch_phase<64, 64, false>(la, lb, dx, add, st);
+        if (ot == OT128) launch_phase<128, 128, false>(la, lb, dx, add, st, pp, bs);
+        else if (ot == OT128x64) launch_phase<128, 64, false>(la, lb, dx, add, st, pp, bs);
+        else launch_phase<64, 64, false>(la, lb, dx, add, st, pp, bs);
       }
     }
   if (empty) {
@@ -819,6 +829,7 @@ static void dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t
     dgrad_empty_phase_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(dx, add, c.N, c.H, c.W, c.C, s, c.pad, c.R,
                                                                          c.S);
   }
+  return rows;
 }
 
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
@@ -844,15 +855,31 @@ void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint1
   else conv_dgrad_impl(c, dy, w, StoreBf16{dx, M, c.C}, st);
 }
 
-bool conv_dgrad_bn_supported(const ConvShape& c) { return TFD_CONV_LDS_EPI && c.stride == 1 && c.C % 8 == 0; }
-int conv_dgrad_bn_rows(const ConvShape& c) { return out_tile_rows(c.N * c.H * c.W, c.C); }
+// stride 1, or a strided dgrad by output phases none of which is tap-less (every input pixel is in
+// some phase GEMM, e.g. ResNet v1.5's 3x3 stride-2 convs)
+bool conv_dgrad_bn_supported(const ConvShape& c) {
+  if (!TFD_CONV_LDS_EPI || c.C % 8 != 0) return false;
+  return c.stride == 1 || (TFD_DGRAD_PHASES && c.R >= c.stride && c.S >= c.stride);
+}
+int conv_dgrad_bn_rows(const ConvShape& c) {
+  if (c.stride == 1) return out_tile_rows(c.N * c.H * c.W, c.C);
+  int rows = 0;
+  for (int ph = 0; ph < c.stride; ++ph)
+    for (int pw = 0; pw < c.stride; ++pw) {
+      const int Hp = (c.H - ph + c.stride - 1) / c.stride, Wp = (c.W - pw + c.stride - 1) / c.stride;
+      if (Hp > 0 && Wp > 0) rows += out_tile_rows(c.N * Hp * Wp, c.C);
+    }
+  return rows;
+}
 
 void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                    const uint16_t* add, const BnBwdStats& b, float* part) {
-  if (!conv_dgrad_bn_supported(c)) throw std::runtime_error("conv_dgrad_bn: stride-1 dgrads with C % 8 == 0 only");
+  if (!conv_dgrad_bn_supported(c)) throw std::runtime_error("conv_dgrad_bn: unsupported conv (C % 8, tap-less phases)");
   const int M = c.N * c.H * c.W, KD = c.R * c.S * c.K;
   auto go = [&](const auto& bs) {
-    if (is_pointwise(c)) {
+    if (c.stride > 1) {
+      dgrad_strided(c, dy, w, dx, add, st, part, bs);
+    } else if (is_pointwise(c)) {
       dispatch_bf16_bnb(DenseX<true>{dy, c.K, M, c.K}, DenseX<true>{w, c.K, c.C, c.K}, dx, add, M, c.C, KD, part, bs, st);
     } else {
       Geo g = make_geo(c, M, KD);

@@ -18,6 +18,8 @@ Execution model (MI355X-first, not a framework-module port):
 """
 from __future__ import annotations
 
+import os
+
 import math
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
@@ -201,12 +203,19 @@ class GradJoin:
         return None
 
 
+# A/B switch: TFD_BN_STATS_STRIDED=0 keeps the strided (phase) dgrads out of the BN-statistics fusion
+_BN_STATS_STRIDED = os.environ.get("TFD_BN_STATS_STRIDED", "1") != "0"
+
+
 def _bn_stats_fusable(L, bn) -> bool:
     """Can conv ``L``'s dgrad (the whole dout of batch norm ``bn``) emit that BN's backward
-    statistics partials (``conv2d_dgrad_bn``)? Stride-1 dgrads, and a BN whose relu mask the epilogue
+    statistics partials (``conv2d_dgrad_bn``)? Stride-1 dgrads and strided ones whose output phases all
+    have taps (3x3 stride 2, by phase GEMMs), and a BN whose relu mask the epilogue
     can form the way the BN backward will: none, relu bits (residual BN), or recomputed from y
     (residual-free BN with ``mask_from_y``)."""
-    if bn is None or not L.model.bn_bwd_stats or L.stride != 1 or bn.fwd_state is None:
+    if bn is None or not L.model.bn_bwd_stats or bn.fwd_state is None:
+        return False
+    if L.stride != 1 and (L.k < L.stride or not _BN_STATS_STRIDED):  # tap-less phases (1x1 stride 2)
         return False
     _, _, _, mask, relu, has_res = bn.fwd_state
     return (not relu) or mask is not None or (not has_res and L.model.mask_from_y)
@@ -356,7 +365,7 @@ class _SoftmaxXent(torch.autograd.Function):
 # ----------------------------------------------------------------------------- layers
 class ConvLayer:
     def __init__(self, model, name, cin, cout, k, stride, pad):
-        self.model, self.name, self.stride, self.pad = model, name, stride, pad
+        self.model, self.name, self.stride, self.pad, self.k = model, name, stride, pad, k
         self.in_join = None  # GradJoin of this conv's input (residual block inputs)
         self.in_bn = None  # the BN whose output is this conv's only input consumer (BN-backward stats)
         model.specs.append(PSpec(name, (k, k, cin, cout), "he", fan_in=k * k * cin))
