@@ -195,6 +195,7 @@ def main(argv=None):
         if a.state_steps > 0:
             run(a.state_steps - 1)
             snap = [t.clone() for t in _state_tensors(eng)]
+            _diag_digest("snapshot", eng, rank)
             snap_loss = eng.loss_rows().mean()  # the loss of step state_steps (read after timing)
         run(a.warmup)
     torch.cuda.synchronize(dev)
@@ -233,6 +234,7 @@ def main(argv=None):
             loss0_t = snap_loss
         del snap
         torch.cuda.synchronize(dev)
+        _diag_digest("restored", eng, rank)
     if a.lean_gap and (extra or a.state_steps > 0):
         loss0 = None
     else:
@@ -264,6 +266,7 @@ def main(argv=None):
     if os.environ.get("TFD_BENCH_DIAG") and rank == 0:
         print(f"# timed region: host launch {1e6 * (t_launched - t0):.1f} us, sync wait "
               f"{1e6 * (t_synced - t_launched):.1f} us, barrier {1e6 * (t0 + dt - t_synced):.1f} us", file=sys.stderr)
+    _diag_digest("timed", eng, rank)
     gpu_ms = ev0.elapsed_time(ev1)  # device time of the same K steps (diagnostic: host/sync overhead = dt - this)
     if a.zero:
         with torch.cuda.stream(s):
@@ -272,6 +275,10 @@ def main(argv=None):
     tr.check("after the timed steps")
     topo = _job_topology(ctx, dev, tr, eng)
     phases = _phase_breakdown(eng, s, graph_mode, world, ctx) if a.phases else None
+    # the phase steps ran on stream s: wait for them before reading the state on the default stream
+    # (without this the last step's loss rows could be read mid-write: two runs of the same binary
+    # printed the loss of step N or N - 1)
+    torch.cuda.synchronize(dev)
     if loss0 is None:
         loss0 = float(loss0_t.item())
     loss1 = float(eng.loss_rows().mean().item())
@@ -327,6 +334,20 @@ def main(argv=None):
     tr.close()
     ctx.shutdown()
     return 0
+
+
+def _diag_digest(where, eng, rank):
+    """TFD_BENCH_DIAG: sha1 of the training state at a point of the run (reproducibility checks)."""
+    if not os.environ.get("TFD_BENCH_DIAG") or rank != 0:
+        return
+    import hashlib
+
+    import torch
+
+    torch.cuda.synchronize()
+    h = [hashlib.sha1(t.detach().contiguous().cpu().view(torch.uint8).numpy().tobytes()).hexdigest()[:10] for t in _state_tensors(eng)]
+    print(f"# digest {where}: params {h[0]} bf16 {h[1]} m {h[2]} v {h[3]} step {int(eng.step_tensor().item())} "
+          f"loss {float(eng.loss_rows().float().mean().item()):.4f}", file=sys.stderr)
 
 
 def _state_tensors(eng):

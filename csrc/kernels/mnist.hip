@@ -1070,10 +1070,29 @@ constexpr int FDX_GX = FEAT / FDX_BN;                                           
 constexpr int FDX_GX2 = FEAT / FDX_BN2;
 static_assert(FEAT % FDX_BN == 0 && FEAT % FDX_BN2 == 0, "fc1 dX tiles cover the 3136 features exactly");
 // part 0: all three products; part 1: dW + out-layer grads (bucket A complete); part 2: dX only.
+#ifndef TFD_FDX_XCD  // 1: the dX blocks that share a W1 column tile run on one XCD (one L2 fill of it)
+#define TFD_FDX_XCD 1
+#endif
+// dX block j of gx * gy tiles -> (bx, by). Workgroups are dealt to the 8 XCDs round-robin by id, so
+// blocks j, j + 8, j + 16, ... share an XCD and its L2. Without the remap the gy row tiles reading
+// one W1 column tile (bx) sit on gy different XCDs (gx odd), and W1 (6.4 MB) is pulled into L2 gy
+// times; with it, tile T = (j % 8) * per + j / 8 (bx = T / gy) keeps each column tile on one XCD.
+__device__ __forceinline__ void fdx_tile(int j, int gx, int gy, int& bx, int& by) {
+  const int full = TFD_FDX_XCD ? (gx * gy) / (8 * gy) * (8 * gy) : 0;
+  const int T = j < full ? (j & 7) * (full >> 3) + (j >> 3) : j;
+  bx = T / gy;
+  by = T - bx * gy;
+}
 __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int part) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   int id = blockIdx.x;
-  if (part == 2) { fc1_dx_block<FDX_BN2, TFD_FDX_RS_ALONE>(a, id % FDX_GX2, id / FDX_GX2, (bf16*)smem_raw); return; }
+  const int gy = (a.B + FDX_BM - 1) / FDX_BM;
+  if (part == 2) {
+    int bx, by;
+    fdx_tile(id, FDX_GX2, gy, bx, by);
+    fc1_dx_block<FDX_BN2, TFD_FDX_RS_ALONE>(a, bx, by, (bf16*)smem_raw);
+    return;
+  }
 #if TFD_OUTG_FIRST
   // the 17 output-layer blocks each walk the whole batch: dispatched first, their latency hides
   // under the GEMM tiles instead of forming the kernel's tail.
@@ -1087,7 +1106,12 @@ __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int pa
 #if TFD_DIAG_FC1BWD == 1  // timing diagnosis only (wrong gradients): drop the dX blocks
     if (id < n_dx) return;
 #endif
-    if (id < n_dx) { fc1_dx_block(a, id % FDX_GX, id / FDX_GX, (bf16*)smem_raw); return; }
+    if (id < n_dx) {
+      int bx, by;
+      fdx_tile(id, FDX_GX, gy, bx, by);
+      fc1_dx_block(a, bx, by, (bf16*)smem_raw);
+      return;
+    }
     id -= n_dx;
   }
 #if TFD_DIAG_FC1BWD == 2  // timing diagnosis only (wrong gradients): drop the dW blocks
