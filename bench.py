@@ -5,13 +5,21 @@ keep_prob 0.75 -- /root/reference/mnist_python_m.py:62-71,205-222).
 One process per GPU: under torchrun the env says which rank this is; without a launcher
 environment, ``--gpus N`` (N > 1) makes this process spawn the N ranks itself (parallel/spawn.py:
 the parent never touches the GPU, relays rank 0's JSON line and fails if any rank fails), and a
-job whose WORLD_SIZE differs from --gpus exits non-zero. Each step = fused HIP forward + backward + bucketed RCCL
-gradient all-reduce (sum, 1/N folded into Adam) + fused flat Adam, with every kernel and
-collective captured into ONE hipGraph that is replayed per step. Data is a device-resident
-synthetic MNIST-shaped split (55000 x 784 fp32 in [0,1], random labels) indexed by a per-rank
-permutation and the device global_step, so there is no host work inside the timed region.
+job whose WORLD_SIZE differs from --gpus exits non-zero. Each step = fused HIP forward + backward
++ the DP gradient exchange (RCCL / peer-to-peer IPC collectives on a comm stream) + fused flat
+Adam, with every kernel and collective captured into ONE hipGraph that is replayed per step.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch_size 128]
+Data: a device-resident synthetic MNIST-shaped split (55000 x 784 fp32 in [0,1]): by default the
+learnable class-conditional stroke images of utils/input_data.synthetic_mnist with their labels
+(``--data random``: uniform noise, random labels), indexed by a per-rank permutation and the
+device global_step, so there is no host work inside the timed region.
+
+Schedule: with N > 1 the ranks first probe every candidate DP schedule at this N (sufficient
+factors + ZeRO-1, sufficient factors, bucketed all-reduce; parallel/schedule.py), untimed, and
+time the fastest; the JSON reports every candidate's ms/step and the choice. ``--schedule NAME``
+skips the probes. The job exits non-zero if the replicas' parameters differ after the timed steps.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch_size 128] [--schedule auto]
 """
 from __future__ import annotations
 
@@ -33,9 +41,18 @@ DATA_DESC = {
     "random": "synthetic (device-resident MNIST-shaped 55000x784 uniform noise, random labels; random N(0,1) "
               "init; the model collapses to the label prior)",
 }
+# DP schedules of the bf16 step (N > 1 or --force_dp). "sfb": fc-region gradients by sufficient-
+# factor broadcasting (all-gather the fc factors, 1.33 MB/rank, and form the summed gradient
+# locally); "+zero": ZeRO-1 sharding of the fc1 weight on top; "allreduce": the bucketed bf16
+# gradient all-reduce (6.4 MB fc bucket + IPC one-shot conv bucket).
+SCHEDULES = {
+    "sfb+zero": {"fc_sfb": 1, "zero": 1},
+    "sfb": {"fc_sfb": 1, "zero": 0},
+    "allreduce": {"fc_sfb": 0, "zero": 0},
+}
 
 
-def main(argv=None):
+def _args(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
@@ -50,6 +67,18 @@ def main(argv=None):
                     "(+ IPC for the small bucket)")
     ap.add_argument("--force_dp", type=int, default=0, help="1: run the full DP schedule (comm stream, captured "
                     "collectives) even at world 1 -- one-GPU rehearsal of the multi-GPU path")
+    ap.add_argument("--schedule", default="auto", choices=["auto"] + list(SCHEDULES),
+                    help="DP schedule (N > 1 or --force_dp): auto = probe every candidate at this N and time the "
+                    "fastest; a name = that schedule, no probes")
+    ap.add_argument("--candidates", default=",".join(SCHEDULES), help="comma list of the schedules --schedule auto "
+                    "probes")
+    ap.add_argument("--probe_steps", type=int, default=200, help="timed steps per schedule probe (untimed for the "
+                    "record)")
+    ap.add_argument("--probe_warmup", type=int, default=60, help="untimed steps before each probe's timing")
+    ap.add_argument("--zero", type=int, default=-1, help="override: 1/0 = ZeRO-1 fc1 sharding on/off (fixes the "
+                    "schedule together with --fc_sfb; -1 = from --schedule)")
+    ap.add_argument("--fc_sfb", type=int, default=-1, help="override: 1/0 = sufficient-factor fc gradients on/off "
+                    "(-1 = from --schedule)")
     ap.add_argument("--min_warmup_ms", type=float, default=300.0, help="after --warmup steps, keep replaying "
                     "untimed steps until this much warm-up time has passed (GPU clock ramp; reported in the JSON)")
     ap.add_argument("--graph_steps", type=int, default=20, help="training steps captured per hipGraph "
@@ -68,23 +97,10 @@ def main(argv=None):
                     "with HIP timing events at the phase boundaries and report the GPU phase breakdown (untimed)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="compute dtype: bf16 MFMA operands "
                     "(fp32 accumulate/master/optimizer), or fp32 everything (the reference's precision)")
-    ap.add_argument("--zero", type=int, default=-1, help="1: ZeRO-1 sharding of the fc1 weight (N > 1): with "
-                    "--fc_sfb each rank forms only its shard's fc1 gradient and updates only that shard, the bf16 "
-                    "shards are all-gathered (IPC one-shot) beside the next conv forward; -1 (default): on from 4 "
-                    "ranks up, where the K = N*B fc GEMM and the full fc Adam (~28 us at N = 4) would otherwise "
-                    "cost more than the 1.6 MB/peer weight gather that hides behind the conv forward")
-    ap.add_argument("--fc_sfb", type=int, default=1, help="1 (N > 1 or --force_dp): fc-region gradients by "
-                    "sufficient-factor broadcasting -- all-gather the fc factors (1.33 MB/rank) and form the summed "
-                    "fc gradient locally instead of all-reducing it (6.4 MB); 0: bucketed all-reduce")
     ap.add_argument("--fused_tail", type=int, default=1, help="1: on one GPU the Adam kernel also reduces the "
                     "conv weight-gradient slabs and bumps the step (one kernel less)")
     ap.add_argument("--local_bf16_grads", type=int, default=1, help="1: on one GPU keep the fc-region gradients "
                     "in bf16 (the DP all-reduce wire format): fc backward writes and Adam reads 2 B per gradient")
-    ap.add_argument("--fc_adam", type=int, default=0, help="1: on one GPU the fc1 Adam update runs in the fc1 "
-                    "weight-gradient epilogue (fp32 gradient straight from the GEMM, fc1 bf16 shadow double-buffered; A/B neutral: "
-                    "profiles/ab_fc1_adam_dw_epi_r3.log)")
-    ap.add_argument("--conv_unfused", type=int, default=0, help="1: conv1 and conv2 forward as two kernels "
-                    "(A/B of the fused conv1->conv2 kernel)")
     ap.add_argument("--state_steps", type=int, default=100, help="time the steps that follow this many training "
                     "steps from init (snapshot before the clock-ramp warm-up, restored before the timed region); "
                     "0: time whatever state the warm-up steps left")
@@ -94,8 +110,149 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu", action="store_true", help="plumbing dry-run: fp32 PyTorch CPU runner + Gloo "
                     "(exercises the launcher/barrier/JSON contract without a GPU; not a performance number)")
+    return ap.parse_args(argv)
+
+
+def _candidates(a, dp: bool):
+    """(names to run, how the schedule was chosen). No DP: the one-GPU step, no schedule."""
+    if not dp:
+        return [None], "single"
+    if a.dtype == "fp32":  # fp32 DP all-reduces the whole fp32 buffer (no SFB / ZeRO variants)
+        return ["allreduce"], "fp32"
+    if a.fc_sfb >= 0 or a.zero >= 0:  # explicit switches fix the schedule
+        sfb = a.fc_sfb != 0
+        zero = a.zero == 1
+        name = ("sfb+zero" if zero else "sfb") if sfb else ("allreduce" if not zero else None)
+        if name is None:
+            raise SystemExit("error: --zero 1 needs --fc_sfb 1 (the ZeRO-1 path of this bench rides the SFB step)")
+        return [name], "flag"
+    if a.schedule != "auto":
+        return [a.schedule], "flag"
+    names = [c.strip() for c in a.candidates.split(",") if c.strip()]
+    bad = [c for c in names if c not in SCHEDULES]
+    if bad or not names:
+        raise SystemExit(f"error: unknown schedule candidates {bad} (known: {list(SCHEDULES)})")
+    return names, "probe"
+
+
+class _Job:
+    """One configured engine: params initialised on rank 0 and broadcast (reference M6), the
+    device-resident dataset attached, the DP transport wired for ``sched``, graphs captured."""
+
+    def __init__(self, a, ctx, data, labels, sched, graph_steps, extra_graph=0):
+        import torch
+
+        from tensorflow_distributed_amd.models import mnist_cnn as M
+        from tensorflow_distributed_amd.parallel.transport import attach_engine
+
+        self.a, self.ctx = a, ctx
+        dev, rank, world = ctx.device, ctx.rank, ctx.world
+        self.sched = sched
+        cfg = SCHEDULES[sched] if sched else {"fc_sfb": 0, "zero": 0}
+        self.zero = bool(cfg["zero"]) and a.dtype == "bf16"
+        eng = torch.classes.tfd.MnistEngine(a.batch_size, dev.index, 0.75, a.seed, rank)
+        eng.set_adam(a.lr, 0.9, 0.999, 1e-8)
+        eng.set_dtype(a.dtype)
+        eng.set_fused_tail(a.fused_tail)
+        eng.set_local_bf16_grads(a.local_bf16_grads)
+        mode = a.transport
+        if mode == "auto":
+            mode = "ipc" if ctx.shared_device else "rccl"
+        self.tr = attach_engine(eng, rank, world, dev, mode=mode, comm=ctx.comm, bf16=not a.fp32_grads,
+                                small_ipc=bool(a.ipc_small), force_dp=bool(a.force_dp),
+                                sfb=bool(cfg["fc_sfb"]) and a.dtype == "bf16", zero=self.zero)
+        if self.zero:
+            eng.set_zero(True)
+        self.eng = eng
+        self.stream = s = torch.cuda.Stream(dev)
+        with torch.cuda.stream(s):
+            g = torch.Generator(device=dev).manual_seed(1000 + rank)
+            perm = torch.randperm(data.shape[0], device=dev, generator=g).to(torch.int32)
+            if rank == 0:
+                eng.params().copy_(M.flat_from_dict(M.init_params(a.seed)).to(dev))
+            if world > 1:  # chief init -> everyone (reference M6): RCCL, or Gloo when ranks share a GPU
+                if ctx.comm is not None:
+                    ctx.comm.broadcast(eng.params(), 0)
+                else:
+                    torch.cuda.synchronize(dev)
+                    host = eng.params().cpu()
+                    ctx.broadcast_tensor_cpu(host, 0)
+                    eng.params().copy_(host.to(dev))
+            eng.sync_shadow()
+            eng.set_dataset(data, labels, perm)
+            eng.set_input_mode(1)
+            self.graph_mode = not a.eager
+            eng.train_step()  # one eager step first: sets kernel attributes outside capture
+            self.gsteps = max(1, graph_steps)
+            if self.graph_mode:
+                try:
+                    eng.capture_train_step("train")
+                    if self.gsteps > 1:
+                        eng.capture_train_steps("trainN", self.gsteps)
+                    if extra_graph:
+                        eng.capture_train_steps("timed", extra_graph)
+                except Exception as e:  # pragma: no cover - capture support depends on the RCCL build
+                    print(f"# hipGraph capture failed ({e!r}); timing eager launches", file=sys.stderr)
+                    self.graph_mode = False
+
+    def run(self, k):
+        eng, gs = self.eng, self.gsteps
+        if not self.graph_mode:
+            for _ in range(k):
+                eng.train_step()
+            return
+        if gs > 1 and k >= gs:
+            eng.replay("trainN", k // gs)
+        if k % gs or gs == 1:
+            eng.replay("train", k % gs if gs > 1 else k)
+
+    def close(self):
+        """Tear down after every rank's kernels finished (a peer may still read our IPC staging)."""
+        import torch
+
+        torch.cuda.synchronize(self.ctx.device)
+        self.ctx.barrier()
+        for name in ("train", "trainN", "timed", "phases"):
+            self.eng.drop_graph(name)
+        self.tr.close()
+        self.ctx.barrier()
+        self.eng = None
+
+
+def _probe_once(a, ctx, data, labels, sched) -> float:
+    """Local ms/step of ``sched``: fresh engine + transport, ``--probe_warmup`` untimed steps, then
+    ``--probe_steps`` graph-replayed steps between barriers. Setup failures are agreed on first, so
+    no rank enters the timing collectives alone."""
+    import torch
+
+    job, err = None, None
+    try:
+        job = _Job(a, ctx, data, labels, sched, a.graph_steps)
+    except Exception as e:  # noqa: BLE001 - agreed below
+        err = e
+    if ctx.max_scalar(1.0 if err is not None else 0.0) > 0:
+        if job is not None:
+            job.close()
+        raise RuntimeError(f"setup failed on at least one rank (here: {err!r})")
+    try:
+        with torch.cuda.stream(job.stream):
+            job.run(a.probe_warmup)
+        torch.cuda.synchronize(ctx.device)
+        ctx.barrier()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(job.stream):
+            job.run(a.probe_steps)
+        torch.cuda.synchronize(ctx.device)
+        dt = time.perf_counter() - t0
+        job.tr.check(f"schedule probe {sched}")
+    finally:
+        job.close()
+    return dt * 1e3 / max(1, a.probe_steps)
+
+
+def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
-    a = ap.parse_args(argv)
+    a = _args(argv)
     from tensorflow_distributed_amd.parallel import spawn
 
     if spawn.needs_self_launch(a.gpus):
@@ -107,8 +264,8 @@ def main(argv=None):
     import torch
 
     from tensorflow_distributed_amd import _native
-    from tensorflow_distributed_amd.models import mnist_cnn as M
     from tensorflow_distributed_amd.parallel import dist as D
+    from tensorflow_distributed_amd.parallel import schedule as SCH
 
     _native.require()
     ctx = D.init_from_env(use_gpu=True)
@@ -116,78 +273,37 @@ def main(argv=None):
     spawn.check_world(a.gpus, world)
     dev = ctx.device
     B = a.batch_size
-    eng = torch.classes.tfd.MnistEngine(B, dev.index, 0.75, a.seed, rank)
-    eng.set_adam(a.lr, 0.9, 0.999, 1e-8)
-    eng.set_dtype(a.dtype)
-    eng.set_fused_tail(a.fused_tail)
-    eng.set_local_bf16_grads(a.local_bf16_grads)
-    eng.set_fc_adam(bool(a.fc_adam))
-    eng.set_conv_unfused(a.conv_unfused)
-    from tensorflow_distributed_amd.parallel.transport import attach_engine
-
-    mode = a.transport
-    if mode == "auto":
-        mode = "ipc" if ctx.shared_device else "rccl"
-    if a.zero < 0:
-        a.zero = 1 if (world >= 4 and a.dtype == "bf16") else 0
-    tr = attach_engine(eng, rank, world, dev, mode=mode, comm=ctx.comm, bf16=not a.fp32_grads,
-                       small_ipc=bool(a.ipc_small), force_dp=bool(a.force_dp),
-                       sfb=bool(a.fc_sfb) and a.dtype == "bf16", zero=bool(a.zero))
-    if a.zero:
-        eng.set_zero(True)
-    s = torch.cuda.Stream(dev)
     n_data = 55000
     if a.data == "strokes":  # the learnable synthetic MNIST set (same images on every rank, like the
         # reference's workers that all read the full training split, mnist_python_m.py:291)
         from tensorflow_distributed_amd.utils.input_data import synthetic_mnist
 
         xi, yi = synthetic_mnist(n_data, 0)
-        host_x = torch.from_numpy(xi.reshape(n_data, 784))
-        host_y = torch.from_numpy(yi.astype("int32"))
-    with torch.cuda.stream(s):
+        data = torch.from_numpy(xi.reshape(n_data, 784)).to(dev).float().div_(255.0)
+        labels = torch.from_numpy(yi.astype("int32")).to(dev)
+    else:
         g = torch.Generator(device=dev).manual_seed(1000 + rank)
-        if a.data == "strokes":
-            data = host_x.to(dev).float().div_(255.0)
-            labels = host_y.to(dev)
-        else:
-            data = torch.rand(n_data, 784, device=dev, generator=g)
-            labels = torch.randint(0, 10, (n_data,), device=dev, generator=g, dtype=torch.int32)
-        perm = torch.randperm(n_data, device=dev, generator=g).to(torch.int32)
-        if rank == 0:
-            eng.params().copy_(M.flat_from_dict(M.init_params(a.seed)).to(dev))
-        if world > 1:  # chief init -> everyone (reference M6): RCCL, or Gloo when ranks share a GPU
-            if ctx.comm is not None:
-                ctx.comm.broadcast(eng.params(), 0)
-            else:
-                torch.cuda.synchronize(dev)
-                host = eng.params().cpu()
-                ctx.broadcast_tensor_cpu(host, 0)
-                eng.params().copy_(host.to(dev))
-        eng.sync_shadow()
-        eng.set_dataset(data, labels, perm)
-        eng.set_input_mode(1)
-        graph_mode = not a.eager
-        eng.train_step()  # one eager step first: sets kernel attributes outside capture
-        gsteps = max(1, a.graph_steps)
-        lead = max(0, min(a.lead_steps, a.steps - 1)) if graph_mode else 0
-        if graph_mode:
-            try:
-                eng.capture_train_step("train")
-                if gsteps > 1:
-                    eng.capture_train_steps("trainN", gsteps)
-                if lead:
-                    eng.capture_train_steps("timed", a.steps - lead)
-            except Exception as e:  # pragma: no cover - capture support depends on the RCCL build
-                print(f"# hipGraph capture failed ({e!r}); timing eager launches", file=sys.stderr)
-                graph_mode = False
-        if graph_mode:
-            def run(k):
-                if gsteps > 1 and k >= gsteps:
-                    eng.replay("trainN", k // gsteps)
-                if k % gsteps or gsteps == 1:
-                    eng.replay("train", k % gsteps if gsteps > 1 else k)
-        else:
-            run = lambda k: [eng.train_step() for _ in range(k)]  # noqa: E731
+        data = torch.rand(n_data, 784, device=dev, generator=g)
+        labels = torch.randint(0, 10, (n_data,), device=dev, generator=g, dtype=torch.int32)
+    torch.cuda.synchronize(dev)
+
+    dp = world > 1 or bool(a.force_dp)
+    cands, source = _candidates(a, dp)
+    probe_ms = None
+    if source == "probe" and len(cands) > 1:
+        log = (lambda m: print(m, file=sys.stderr, flush=True)) if rank == 0 else None
+        probe_ms = SCH.probe(cands, lambda name: _probe_once(a, ctx, data, labels, name), ctx.max_scalar, log)
+        sched = SCH.pick(probe_ms)
+    else:
+        sched = cands[0]
+
+    lead = max(0, min(a.lead_steps, a.steps - 1)) if not a.eager else 0
+    job = _Job(a, ctx, data, labels, sched, a.graph_steps, extra_graph=(a.steps - lead) if lead else 0)
+    eng, tr, s, run = job.eng, job.tr, job.stream, job.run
+    graph_mode, gsteps = job.graph_mode, job.gsteps
+    if not graph_mode:
+        lead = 0
+    with torch.cuda.stream(s):
         # The timed steps start from the training state after --state_steps steps (a model that is
         # still learning), not from wherever the clock-ramp warm-up below leaves it: snapshot it now,
         # warm up, restore it right before the timed region.
@@ -268,7 +384,7 @@ def main(argv=None):
               f"{1e6 * (t_synced - t_launched):.1f} us, barrier {1e6 * (t0 + dt - t_synced):.1f} us", file=sys.stderr)
     _diag_digest("timed", eng, rank)
     gpu_ms = ev0.elapsed_time(ev1)  # device time of the same K steps (diagnostic: host/sync overhead = dt - this)
-    if a.zero:
+    if job.zero:
         with torch.cuda.stream(s):
             eng.sync_params()
     dt = ctx.max_scalar(dt)
@@ -283,15 +399,12 @@ def main(argv=None):
         loss0 = float(loss0_t.item())
     loss1 = float(eng.loss_rows().mean().item())
     acc1 = float(eng.correct_rows().mean().item())  # last timed step's minibatch accuracy (train mode)
-    # the conv1 weight gradient skips zero pooled gradients (TFD_C1W_SKIP0); those are the pixels the
-    # pooled ReLU output is 0 at, so this is the share of that work the last timed step skipped
-    p1_zero = float((eng.pool1() == 0).float().mean().item())
     gstep = int(eng.step_tensor().item())
     ms = dt * 1e3 / a.steps
     img_s = world * B * a.steps / dt
     if rank == 0:
-        print(f"# world={world} B/gpu={B} steps={a.steps} global_step={gstep} loss {loss0:.3f}->{loss1:.3f} acc {acc1:.3f} "
-              f"{ms:.4f} ms/step", file=sys.stderr)
+        print(f"# world={world} B/gpu={B} schedule={sched} steps={a.steps} global_step={gstep} "
+              f"loss {loss0:.3f}->{loss1:.3f} acc {acc1:.3f} {ms:.4f} ms/step", file=sys.stderr)
         print(json.dumps({
             "metric": METRIC,
             "value": round(img_s, 1),
@@ -302,7 +415,7 @@ def main(argv=None):
             "warmup_extra_steps": extra,
             "train_state": {"global_step": gstep, "loss_before_timed": round(loss0, 4),
                             "loss_after_timed": round(loss1, 4), "minibatch_accuracy": round(acc1, 4),
-                            "state_steps": a.state_steps, "pool1_zero_fraction": round(p1_zero, 4)},
+                            "state_steps": a.state_steps},
             "ms_per_step": round(ms, 5),
             "gpu_event_ms_per_step": round(gpu_ms / a.steps, 5),
             "higher_is_better": True,
@@ -311,6 +424,10 @@ def main(argv=None):
             "dtype": a.dtype,
             "data": DATA_DESC[a.data],
             "phases_ms": phases,
+            "schedule": {"chosen": sched, "source": source,
+                         "candidates_ms_per_step": ({k: round(v, 5) for k, v in probe_ms.items()}
+                                                    if probe_ms else None),
+                         "probe_steps": a.probe_steps if probe_ms else 0},
             **topo,
             "config": {
                 "model": "MNIST 2-conv CNN (reference conv_net: conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout0.75-fc10), "
@@ -324,15 +441,17 @@ def main(argv=None):
                 "steps_per_graph": gsteps if graph_mode else 0,
                 "dp_transport": tr.kind,
                 "force_dp": bool(a.force_dp),
-                "zero1_fc1": bool(a.zero),
+                "zero1_fc1": job.zero,
                 "fc_grads": ("fp32" if a.dtype == "fp32" else
                              "summed from all-gathered factors (sfb), bf16" if "sfb" in tr.kind else
-                             "fc1: fp32 into Adam in the dW epilogue; out: bf16" if eng.fc_adam_active() else
                              "bf16" if (a.local_bf16_grads or world > 1) and not a.fp32_grads else "fp32"),
             },
         }), flush=True)
     tr.close()
     ctx.shutdown()
+    if not topo["replicas_identical"]:
+        print("error: DP replicas diverged (parameter digests differ across ranks)", file=sys.stderr)
+        return 3
     return 0
 
 
@@ -422,23 +541,53 @@ def _cpu_dry_run(a):
     from tensorflow_distributed_amd.models import mnist_cnn as M
     from tensorflow_distributed_amd.models.mnist_runner import TorchMnistRunner
     from tensorflow_distributed_amd.parallel import dist as D
+    from tensorflow_distributed_amd.parallel import schedule as SCH
+    from tensorflow_distributed_amd.parallel import spawn
     from tensorflow_distributed_amd.parallel.sync_replicas import SyncReplicasStepper, broadcast_state
     from tensorflow_distributed_amd.training.optimizers import AdamOptimizer
-
-    from tensorflow_distributed_amd.parallel import spawn
 
     ctx = D.init_from_env(use_gpu=False)
     world, rank = ctx.world, ctx.rank
     spawn.check_world(a.gpus, world)
-    r = TorchMnistRunner(a.batch_size, AdamOptimizer(a.lr), keep_prob=0.75, seed=a.seed, rank=rank)
-    if rank == 0:
-        r.load_flat(M.flat_from_dict(M.init_params(a.seed)), {}, 0)
-    if world > 1:
-        broadcast_state(r, 0)
-    st = SyncReplicasStepper(r, rank, world, world)
     g = torch.Generator().manual_seed(1000 + rank)
     x = torch.rand(a.batch_size, 784, generator=g)
     y = torch.randint(0, 10, (a.batch_size,), generator=g)
+
+    def make():
+        r = TorchMnistRunner(a.batch_size, AdamOptimizer(a.lr), keep_prob=0.75, seed=a.seed, rank=rank)
+        if rank == 0:
+            r.load_flat(M.flat_from_dict(M.init_params(a.seed)), {}, 0)
+        if world > 1:
+            broadcast_state(r, 0)
+        return SyncReplicasStepper(r, rank, world, world)
+
+    # the same probe/choose protocol as the GPU path, over CPU "schedules" (the Gloo all-reduce of
+    # the whole flat gradient, or of the conv and fc buckets separately), so its collective
+    # discipline is covered by the CPU suite
+    from tensorflow_distributed_amd.parallel.sync_replicas import GlooGradAverager
+
+    def configure(st, name):
+        if world > 1:
+            st.runner.comm = GlooGradAverager(None, world, [M.BUCKET_SPLIT] if name == "buckets" else None)
+
+    probe_ms = None
+    if world > 1 and a.schedule == "auto":
+        def one(name):
+            st = make()
+            configure(st, name)
+            st.step(x, y)
+            ctx.barrier()
+            t0 = time.perf_counter()
+            for _ in range(max(1, min(a.probe_steps, 5))):
+                st.step(x, y)
+            return (time.perf_counter() - t0) * 1e3 / max(1, min(a.probe_steps, 5))
+
+        probe_ms = SCH.probe(["flat", "buckets"], one, ctx.max_scalar)
+        chosen = SCH.pick(probe_ms)
+    else:
+        chosen = "flat"
+    st = make()
+    configure(st, chosen)
     for _ in range(a.warmup):
         st.step(x, y)
     ctx.barrier()
@@ -447,15 +596,19 @@ def _cpu_dry_run(a):
         st.step(x, y)
     ctx.barrier()
     dt = ctx.max_scalar(time.perf_counter() - t0)
+    digest = float(st.runner.params().double().sum())
+    hi, lo = ctx.max_scalar(digest), -ctx.max_scalar(-digest)
     if rank == 0:
         print(json.dumps({"metric": "images/sec (whole node) MNIST CNN DP [CPU dry-run]", "value": world * a.batch_size * a.steps / dt,
                           "unit": "images/s", "n_gpus": 0, "n_ranks": world, "steps": a.steps, "warmup": a.warmup,
                           "ms_per_step": dt * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak",
                           "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+                          "schedule": {"chosen": chosen, "candidates_ms_per_step": probe_ms},
+                          "replicas_identical": hi == lo,
                           "config": {"model": "mnist_cnn", "global_batch": world * a.batch_size, "seq_len": None,
                                      "parallelism": f"dp{world}", "device": "cpu"}}), flush=True)
     ctx.shutdown()
-    return 0
+    return 0 if hi == lo else 3
 
 
 if __name__ == "__main__":

@@ -6,7 +6,12 @@ spawns the N ranks from a GPU-clean parent, see parallel/spawn.py), native HIP c
 all-reduce overlapped with the backward, fused flat SGD-momentum, the whole step captured in a
 hipGraph and replayed. Synthetic data: one fixed device-resident random batch per rank.
 
-    python bench_resnet.py [--depth 50] [--batch_size 128] [--steps 20] [--warmup 5] [--bucket_mb 8]
+With N > 1 the ranks first probe every gradient bucket size of ``--bucket_candidates`` (SURVEY.md
+§5.8 item 5: 2/4/8/16/25 MB), untimed, each with its own captured graph, and time the fastest
+(parallel/schedule.py); ``--bucket_mb X`` skips the probes. The job exits non-zero if the
+replicas' weights differ after the timed steps.
+
+    python bench_resnet.py [--depth 50] [--batch_size 128] [--steps 20] [--warmup 5] [--bucket_mb auto]
 """
 from __future__ import annotations
 
@@ -28,7 +33,11 @@ def main(argv=None):
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--bucket_mb", type=float, default=8.0)
+    ap.add_argument("--bucket_mb", default="auto", help="gradient bucket size in MB (N > 1), or auto = probe "
+                    "--bucket_candidates at this N and time the fastest")
+    ap.add_argument("--bucket_candidates", default="2,4,8,16,25")
+    ap.add_argument("--probe_steps", type=int, default=10, help="timed steps per bucket-size probe")
+    ap.add_argument("--probe_warmup", type=int, default=3)
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--bn_stats", type=int, default=1, help="1: batch-norm statistics summed in the conv "
                     "forward epilogue (no separate statistics pass over the conv output)")
@@ -77,24 +86,27 @@ def main(argv=None):
         else:
             raise RuntimeError(f"world {ctx.world} but no gradient transport: refusing to report non-DP throughput")
         m.fp.shadow.copy_(m.fp.master)
-        m.set_comm(comm, a.bucket_mb)
     g = torch.Generator(device=dev).manual_seed(100 + ctx.rank)
     x = torch.randn(a.batch_size, a.image, a.image, 3, device=dev, generator=g)
     y = torch.randint(0, 1000, (a.batch_size,), device=dev, generator=g, dtype=torch.int32)
-
     s = torch.cuda.Stream(dev)
-    s.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(s):
-        for _ in range(2):
-            m.train_step(x, y, lr=a.lr)
-    torch.cuda.current_stream(dev).wait_stream(s)
-    torch.cuda.synchronize(dev)
-    if a.eager:
-        def run(k):
-            for _ in range(k):
-                out = m.train_step(x, y, lr=a.lr)
-            return out
-    else:
+
+    def configure(mb):
+        """Reducer with ``mb``-MB buckets, two eager steps, the step captured; returns run(k)."""
+        if comm is not None:
+            m.set_comm(comm, mb)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                m.train_step(x, y, lr=a.lr)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        if a.eager:
+            def run(k):
+                for _ in range(k):
+                    out = m.train_step(x, y, lr=a.lr)
+                return out
+            return run, None
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             out_static = m.train_step(x, y, lr=a.lr)
@@ -103,6 +115,40 @@ def main(argv=None):
             for _ in range(k):
                 graph.replay()
             return out_static
+        return run, graph
+
+    probe_ms, source = None, "single"
+    if comm is None:
+        bucket_mb = None
+    elif a.bucket_mb != "auto":
+        bucket_mb, source = float(a.bucket_mb), "flag"
+    else:
+        from tensorflow_distributed_amd.parallel import schedule as SCH
+
+        cands = [float(c) for c in a.bucket_candidates.split(",") if c.strip()]
+        # every probe trains: start the timed job from the same weights afterwards (every rank alike)
+        snap = [t.clone() for t in (m.fp.master, m.fp.momentum, m.fp.shadow)]
+
+        def one(name):
+            run_p, graph_p = configure(float(name))
+            run_p(a.probe_warmup)
+            torch.cuda.synchronize(dev)
+            ctx.barrier()
+            t0 = time.perf_counter()
+            run_p(a.probe_steps)
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+            del run_p, graph_p
+            return dt * 1e3 / max(1, a.probe_steps)
+
+        log = (lambda msg: print(msg, file=sys.stderr, flush=True)) if ctx.rank == 0 else None
+        probe_ms = SCH.probe([f"{c:g}" for c in cands], one, ctx.max_scalar, log)
+        bucket_mb, source = float(SCH.pick(probe_ms)), "probe"
+        for dst, src in zip((m.fp.master, m.fp.momentum, m.fp.shadow), snap):
+            dst.copy_(src)
+        del snap
+        torch.cuda.synchronize(dev)
+    run, graph = configure(bucket_mb)
     run(a.warmup)
     torch.cuda.synchronize(dev)
     ctx.barrier()
@@ -127,7 +173,10 @@ def main(argv=None):
             "config": {"model": f"resnet{a.depth} v1.5 NHWC", "global_batch": ctx.world * a.batch_size,
                        "per_gpu_batch": a.batch_size, "seq_len": None, "parallelism": f"dp{ctx.world}",
                        "dp_transport": transport,
-                       "bucket_mb": a.bucket_mb, "optimizer": "sgd-momentum 0.9 wd 1e-4",
+                       "bucket_mb": bucket_mb,
+                       "bucket_schedule": {"source": source, "candidates_ms_per_step": (
+                           {k: round(v, 4) for k, v in probe_ms.items()} if probe_ms else None)},
+                       "optimizer": "sgd-momentum 0.9 wd 1e-4",
                        "hipgraph": not a.eager, "fuse_joins": bool(a.fuse_joins), "bn_stats": bool(a.bn_stats),
                        "mask_from_y": bool(a.mask_from_y), "relu_bits": bool(a.relu_bits),
                        "bn_bwd_stats": bool(a.bn_bwd_stats)}}), flush=True)

@@ -3,25 +3,24 @@
 //  softmax-xent mean loss; /root/reference/mnist_python_m.py:93-128, :205).
 //
 // Kernel map:
-//   conv1_pool_fwd   K1+K3 (+K18 batch gather): VALU direct conv (K=25, Cin=1 is MFMA-hostile),
-//                    bias+relu+2x2 pool+argmax fused; reads the device-resident dataset row
-//                    perm[(step*B+b) % n] so the whole step can be replayed from one hipGraph.
-//   conv2_pool_fwd   K2+K3: implicit GEMM on MFMA (M = B*196 in pool-window-major order, N=64,
-//                    K=800); each lane's 4 accumulator rows ARE one 2x2 pool window, so
-//                    bias+relu+maxpool+argmax happen in registers.
-//   fc1_fwd          K4 (split-K MFMA GEMM, fp32 slabs; the reducer is the head kernel).
-//   head             K4 finish + K5 dropout (Philox) + K6 + K7 + K8(dX) + K9 fused per batch row.
-//   fc1_dw / fc1_dx  K10: dW (+ bias row) and dX (with MaxPoolGrad+ReluGrad unpool epilogue, K11).
-//   conv2_dgrad      K13 with conv1 ReluGrad/pool-mask epilogue; conv2_wgrad K14 (+K12 bias row),
-//                    split-K slabs; out_grad K8 dW/db.
-//   conv1_wgrad      K15 (+K12): sparse wgrad straight from the pooled gradient and argmax (only the
-//                    1-of-4 argmax positions carry gradient), deterministic per-image slabs. In the
-//                    LDS path it is the tail of conv2_dgrad_lds (same half-image rows, from LDS).
+//   conv12_fwd_lds   K1+K3+K2+K3 (+K18 batch gather): per (image, conv2 channel half) block, conv1
+//                    on the matrix core from a bf16 "5-wide row" x image, bias+relu+2x2 pool+argmax
+//                    in registers into a zero-bordered LDS image, then conv2 as a whole-image
+//                    implicit GEMM from LDS with the same pooled epilogue.
+//   fc1_fwd          K4 (split-K MFMA GEMM, each split's K range in one memory round trip; fp32
+//                    slabs, reduced by the head kernel).
+//   head_kernel      K4 finish + K5 dropout (Philox) + K6 + K7 + K8(dX) + K9 fused per batch row.
+//   fc1_bwd          K8 dW/db + K10 dW (+ bias row) and dX with the MaxPoolGrad + ReluGrad unpool
+//                    epilogue (K11), one launch.
+//   conv2_bwd_lds    K14 (+K12 bias row) wgrad slabs and K13 dgrad with conv1's relu/pool-mask
+//                    epilogue, one launch; the dgrad blocks' tail is K15 (+K12) conv1 wgrad on MFMA.
+//   reduce_conv_grads / mnist_adam_kernel  deterministic slab reduction (+ the next batch's gather,
+//                    the step bump) / K16 ApplyAdam (one-GPU: with the slab reduction fused).
+//   fc_grad_sfb      DP: the fc gradients from all-gathered sufficient factors.
+// Each kernel's configuration constants won their A/B on one MI355X (logs: profiles/ab_*.log,
+// docs/DESIGN.md); losing arms and timing-only experiments are not kept in the source.
 #include "../common.h"
 
-#ifndef TFD_C1W_SKIP0  // 1 (A/B only): skip zero pooled gradients in the conv1 wgrad (value-dependent time)
-#define TFD_C1W_SKIP0 0
-#endif
 #include "../gemm.h"
 #include "../mnist_layout.h"
 #include "../tfd_kernels.h"
@@ -29,57 +28,13 @@
 #include <algorithm>
 #include <stdexcept>
 
-#ifndef TFD_GEMM_RS
-#define TFD_GEMM_RS 2  // register stages of the LDS-staged GEMM core (csrc/gemm.h)
-#endif
-
-#ifndef TFD_WROT
-#define TFD_WROT 1
-#endif
-
-#ifndef TFD_EXP_SKIP_MAIN
-#define TFD_EXP_SKIP_MAIN 0  // experiment: skip the MFMA main loops of the LDS conv kernels
-#endif
-
-#ifndef TFD_CONV2_LDS
-#define TFD_CONV2_LDS 1  // LDS-staged whole-image conv2 kernels (0 = im2col-through-L2 GEMM path)
-#endif
-
-#ifndef TFD_C2W_KPER
-#define TFD_C2W_KPER 1024  // conv2 wgrad split-K chunk (pixels per slab)
-#endif
-
-#ifndef TFD_C2W_BK
-#define TFD_C2W_BK 64
-#endif
-
-#ifndef TFD_C2D_BK
-#define TFD_C2D_BK 64
-#endif
-
-#ifndef TFD_FDX_BK
-#define TFD_FDX_BK 128
-#endif
-
-#ifndef TFD_FDW_BK
-#define TFD_FDW_BK 64
-#endif
-
-#ifndef TFD_C1_EARLY_X  // 1: conv1 forward issues its image load before the filter-staging barrier
-#define TFD_C1_EARLY_X 0
-#endif
-
-#ifndef TFD_ADAM_U  // fc-region Adam: strides per lane with all loads issued up front (1 = plain loop)
-#define TFD_ADAM_U 2
-#endif
-
-#ifndef TFD_FC1_BK
-#define TFD_FC1_BK 32  // one-shot fc1: 14 K-tiles of 32 (140 KiB LDS) measured 0.6 us/step faster than 7 of 64
-#endif
-
-#ifndef TFD_C2F_BK
-#define TFD_C2F_BK 64
-#endif
+// Compile-time configuration of the kernels below (each value won its A/B on one MI355X; the losing
+// arms and the timing-only experiment switches were removed, logs in profiles/ab_*.log):
+constexpr int GEMM_RS = 2;       // register stages of the LDS-staged GEMM core (csrc/gemm.h)
+constexpr int FDX_BK_ = 128;     // fc1 dX K-tile
+constexpr int FDW_BK_ = 64;      // fc1 dW K-tile
+constexpr int ADAM_U = 2;        // fc-region Adam: strides per lane with all loads issued up front
+constexpr int FC1_BK_ = 32;      // one-shot fc1: 14 K-tiles of 32 (140 KiB LDS), 0.6 us/step faster than 7 of 64
 
 namespace tfd {
 using namespace mnist;
@@ -117,10 +72,6 @@ __device__ __forceinline__ void gather_next(const MnistStepArgs& a, int64_t next
   }
 }
 __device__ __forceinline__ int gather_blocks(const MnistStepArgs& a) { return (a.perm && a.xpre) ? a.B : 0; }
-// the bf16 fc1 weights this step reads (MnistStepArgs::pbf_alt: double-buffered by step parity)
-__device__ __forceinline__ const uint16_t* fc1_wbf(const MnistStepArgs& a) {
-  return (a.pbf_alt && (*a.step & 1)) ? a.pbf_alt + OFF_WD1 : a.pbf + OFF_WD1;
-}
 // the prefetched label of batch row b (speculative load beside the tag and the step)
 __device__ __forceinline__ int batch_label(const MnistStepArgs& a, int b) {
   if (a.perm && a.xpre) {
@@ -131,129 +82,10 @@ __device__ __forceinline__ int batch_label(const MnistStepArgs& a, int b) {
   return a.labels[data_row(a, b)];
 }
 
-// ---------------- K1: conv1 + bias + relu + maxpool + argmax ----------------
-// Block = (image b, output-channel group cg of 8): the 28x28 fp32 image is staged once into a
-// zero-bordered 32x32 LDS tile (coalesced 16 B loads), thread pp < 196 computes the 4 window
-// pre-activations of pooled pixel pp for 8 channels from a 6x6 LDS patch (fp32 VALU: K = 25 with
-// Cin = 1 is MFMA-hostile). Grid = 4B blocks (512 at B = 128: every CU busy).
-__global__ __launch_bounds__(256) void conv1_pool_fwd(MnistStepArgs a) {
-  __shared__ float img[32 * 32];
-  __shared__ float w[KTAPS * 8 + 8];
-  const int b = blockIdx.x >> 2, cg = blockIdx.x & 3, t = threadIdx.x;
-  const float* x = a.data + (size_t)data_row(a, b) * 784;
-#if TFD_C1_EARLY_X
-  // the image load is issued before the first barrier, so its step -> perm -> row chain overlaps
-  // the filter loads instead of starting after them
-  f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (t < 196) v = reinterpret_cast<const f32x4*>(x)[t];
-#endif
-  for (int i = t; i < 32 * 32; i += 256) img[i] = 0.f;
-  if (t < KTAPS * 8) w[t] = a.p32[OFF_WC1 + (t >> 3) * C1 + cg * 8 + (t & 7)];
-  else if (t < KTAPS * 8 + 8) w[t] = a.p32[OFF_BC1 + cg * 8 + (t - KTAPS * 8)];
-  __syncthreads();
-  if (t < 196) {  // 196 float4 = one image
-#if !TFD_C1_EARLY_X
-    const f32x4 v = reinterpret_cast<const f32x4*>(x)[t];
-#endif
-    const int r = (4 * t) / 28, c = (4 * t) % 28;
-    float* d = img + (r + 2) * 32 + c + 2;
-    d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
-  }
-  __syncthreads();
-  if (t >= 196) return;
-  const int ph = t / 14, pw = t - ph * 14;
-  float patch[6][6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) patch[i][j] = img[(2 * ph + i) * 32 + 2 * pw + j];
-  // channel pairs in a rolled loop: keeps the live set at patch (36) + 2x4 accumulators, so the
-  // kernel runs at high occupancy instead of one wave per SIMD with AGPR spills.
-  const size_t gp = (size_t)b * 196 + t;
-  uint32_t* outp = reinterpret_cast<uint32_t*>(a.p1 + gp * 32 + cg * 8);
-  uint64_t idxw = 0;
-#pragma unroll 1
-  for (int cp = 0; cp < 4; ++cp) {
-    uint32_t word = 0;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int cc = 2 * cp + h;
-      const float bias = w[KTAPS * 8 + cc];
-      float z[4] = {bias, bias, bias, bias};
-#pragma unroll
-      for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-        for (int kw = 0; kw < 5; ++kw) {
-          const float wt = w[(kh * 5 + kw) * 8 + cc];
-          z[0] = fmaf(patch[kh][kw], wt, z[0]);
-          z[1] = fmaf(patch[kh][kw + 1], wt, z[1]);
-          z[2] = fmaf(patch[kh + 1][kw], wt, z[2]);
-          z[3] = fmaf(patch[kh + 1][kw + 1], wt, z[3]);
-        }
-      float mx = z[0];
-      int am = 0;
-#pragma unroll
-      for (int win = 1; win < 4; ++win)
-        if (z[win] > mx) { mx = z[win]; am = win; }
-      word |= f2bf_bits(fmaxf(mx, 0.f)) << (16 * h);
-      idxw |= (uint64_t)am << (8 * cc);
-    }
-    outp[cp] = word;
-  }
-  *reinterpret_cast<uint2*>(a.idx1 + gp * 32 + cg * 8) = make_uint2((uint32_t)idxw, (uint32_t)(idxw >> 32));
-}
 
-// ---------------- K2: conv2 implicit GEMM, pooled epilogue ----------------
-// m = ((b*49 + pp)*4 + win); k = tap*32 + ci.
-struct Conv2FwdA {
-  static constexpr bool KC = true;
-  const uint16_t* __restrict__ p1;
-  int M;
-  __device__ __forceinline__ uint4 operator()(int m, int k) const {
-    if (m >= M || k >= 800) return zero4();
-    const int b = m / 196, r = m - b * 196, pp = r >> 2, win = r & 3;
-    const int ph = pp / 7, pw = pp - ph * 7;
-    const int tap = k >> 5, ci0 = k & 31, kh = tap / 5, kw = tap - kh * 5;
-    const int ih = 2 * ph + (win >> 1) + kh - 2, iw = 2 * pw + (win & 1) + kw - 2;
-    if ((unsigned)ih >= 14u || (unsigned)iw >= 14u) return zero4();
-    return *reinterpret_cast<const uint4*>(p1 + ((size_t)(b * 14 + ih) * 14 + iw) * 32 + ci0);
-  }
-};
-struct PoolEpi {
-  const float* __restrict__ bias;
-  uint16_t* __restrict__ p2;
-  uint8_t* __restrict__ idx2;
-  int M;
-  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
-    if (m4 >= M) return;
-    const int b = m4 / 196, pp = (m4 - b * 196) >> 2;
-    const float bb = bias[n];
-    float mx = v[0] + bb;
-    int am = 0;
-#pragma unroll
-    for (int r = 1; r < 4; ++r) {
-      const float z = v[r] + bb;
-      if (z > mx) { mx = z; am = r; }
-    }
-    const size_t o = (size_t)b * FEAT + pp * 64 + n;
-    p2[o] = f2bf_bits(fmaxf(mx, 0.f));
-    idx2[o] = (uint8_t)am;
-  }
-};
-constexpr int C2F_BM = 64, C2F_BN = 64, C2F_BK = TFD_C2F_BK;
-using C2F_B = DenseLoader<false>;
-__global__ __launch_bounds__(256) void conv2_pool_fwd(MnistStepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  const int M = a.B * 196;
-  Conv2FwdA la{a.p1, M};
-  C2F_B lb{a.pbf + OFF_WC2, 64, 64, 800};
-  PoolEpi epi{a.p32 + OFF_BC2, a.p2, a.idx2, M};
-  gemm_block<C2F_BM, C2F_BN, C2F_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, blockIdx.x * C2F_BM, 0, 0, 800, (bf16*)smem_raw);
-}
-
-// ---------------- K2 (LDS-staged): whole-image implicit GEMM ----------------
-// Block = (image b, output-channel half nh), 512 threads (8 waves), 102 KiB LDS: 2B blocks (256 at
-// B = 128, every CU busy). The image's 14x14x32 bf16 activations are staged into a zero-bordered,
+// ---------------- K2 layout: conv2 as a whole-image implicit GEMM from LDS ----------------
+// Per (image b, output-channel half nh) block, 512 threads (8 waves): 2B blocks (256 at B = 128,
+// every CU busy). The image's 14x14x32 bf16 activations sit in a zero-bordered,
 // channel-chunk-major LDS image [4 chunks][18 rows][24 cols] x 16 B and the block's half of W2
 // as [800 k][32 n + 16] rows; every im2col A fragment is then one ds_read_b128 at
 // (pixel(m) + tap offset) -- no global re-reads of the 25x-expanded im2col matrix. Row stride
@@ -276,9 +108,6 @@ constexpr int C2F_WTAP = 4 * 384;  // one tap = 32 rows = 4 groups
 constexpr int C2F_WR4 = 4 * 32;    // + 4 rows inside a group
 static_assert(C2F_WTAP == 32 * C2F_WLD, "the layout keeps the [800][48] footprint");
 constexpr int C2L_FWD_SMEM = (4 * C2F_PLANE * 8 + 800 * C2F_WLD) * 2;  // 104448 B
-#ifndef TFD_C2_PIPE  // 1: conv2 forward tap loop software-pipelined, both M-tiles on every wave
-#define TFD_C2_PIPE 1
-#endif
 // conv2 forward main loop over the 25 taps: two M-tiles (rows base[0], base[1] of the LDS image) x
 // two 16-channel N-tiles. Every wave runs both M-tiles (a second tile past row 196 reads row 0's
 // valid LDS address; the epilogue drops it) so there is no exec-masked branch in the loop, and
@@ -308,127 +137,24 @@ __device__ __forceinline__ void conv2_taps(const bf16* img, const bf16* wcol, co
   }
 }
 static_assert(C2F_PLANE * 16 % 256 == 0, "chunk planes must be bank-row aligned");
-__global__ __launch_bounds__(512) void conv2_fwd_lds(MnistStepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  bf16* img = (bf16*)smem_raw;                        // [4][18*24][8]
-  bf16* wt = img + 4 * C2F_PLANE * 8;                 // [800][48] (32 used)
-  const int b = blockIdx.x >> 1, nh = blockIdx.x & 1, t = threadIdx.x;
-  // Staging: every thread issues ALL of its 16-B loads before its first LDS store (a load->store
-  // loop serialises one global latency per iteration).
-  const uint16_t* src = a.p1 + (size_t)b * 196 * 32;
-  const uint16_t* wsrc = a.pbf + OFF_WC2 + nh * 32;
-  const int rot = TFD_WROT ? (int)((blockIdx.x * 1031u) % 3200u) : 0;  // per-block start: spread L2 channels
-  {
-    constexpr int CI = 4 * C2F_PLANE, NI = (CI + 511) / 512;  // 1728 chunks -> 4 per thread
-    constexpr int NW = (3200 + 511) / 512;                    // 800 rows x 4 chunks -> 7 per thread
-    uint4 vi[NI], vw[NW];
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int i = t + 512 * j, ch = i / C2F_PLANE, px = i - ch * C2F_PLANE;
-      const int r = px / C2F_W - 2, c = px % C2F_W - 2;
-      vi[j] = (i < CI && (unsigned)r < 14u && (unsigned)c < 14u)
-                  ? *reinterpret_cast<const uint4*>(src + (r * 14 + c) * 32 + ch * 8) : zero4();
-    }
-#pragma unroll
-    for (int j = 0; j < NW; ++j) {
-      const int i = (t + 512 * j + rot) % 3200;
-      vw[j] = (t + 512 * j < 3200) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 2) * 64 + (i & 3) * 8) : zero4();
-    }
-#pragma unroll
-    for (int j = 0; j < NW; ++j) {
-      const int i = (t + 512 * j + rot) % 3200;
-      if (t + 512 * j < 3200) *reinterpret_cast<uint4*>(wt + c2f_wrow(i >> 2) + (i & 3) * 8) = vw[j];
-    }
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int i = t + 512 * j;
-      if (i < CI) *reinterpret_cast<uint4*>(img + i * 8) = vi[j];
-    }
-  }
-  __syncthreads();
-  const int lane = t & 63, w = t >> 6, g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
-  const int nmt = (w + 8 < 13) ? 2 : 1;
-  int base[2];
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int m = (w + 8 * j) * 16 + (lane & 15);
-    int px = 0;
-    if (m < 196) {
-      const int pp = m >> 2, win = m & 3;
-      px = (2 * (pp / 7) + (win >> 1)) * C2F_W + 2 * (pp % 7) + (win & 1);  // + (kh*24 + kw) per tap
-    }
-    base[j] = (g * C2F_PLANE + px) * 8;
-  }
-  const bf16* wcol = wt + c2f_wrow(8 * g + q) + 4 * p4;  // rows tap*32 + 8g + q (+4)
-  if (TFD_C2_PIPE && !TFD_EXP_SKIP_MAIN) {
-    conv2_taps(img, wcol, base, acc);
-  } else {
-#pragma unroll
-  for (int kh = 0; kh < (TFD_EXP_SKIP_MAIN ? 0 : 5); ++kh) {
-#pragma unroll
-    for (int kw = 0; kw < 5; ++kw) {
-      const int tap = kh * 5 + kw, toff = (kh * C2F_W + kw) * 8;
-      const bf16* wr = wcol + tap * C2F_WTAP;
-      const bf16x8 b0 = frag_tr16(wr, wr + C2F_WR4);
-      const bf16x8 b1 = frag_tr16(wr + 16, wr + 16 + C2F_WR4);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        if (j < nmt) {
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + base[j] + toff);
-          acc[j][0] = mfma16x16x32(af, b0, acc[j][0]);
-          acc[j][1] = mfma16x16x32(af, b1, acc[j][1]);
-        }
-    }
-  }
-  }
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int n = nh * 32 + nt * 16 + (lane & 15);
-    const float bb = a.p32[OFF_BC2 + n];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int m4 = (w + 8 * j) * 16 + 4 * g;
-      if (j >= nmt || m4 >= 196) continue;
-      float mx = acc[j][nt][0] + bb;
-      int am = 0;
-#pragma unroll
-      for (int r = 1; r < 4; ++r) {
-        const float z = acc[j][nt][r] + bb;
-        if (z > mx) { mx = z; am = r; }
-      }
-      const size_t o = (size_t)b * FEAT + (m4 >> 2) * 64 + n;
-      a.p2[o] = f2bf_bits(fmaxf(mx, 0.f));
-      a.idx2[o] = (uint8_t)am;
-    }
-  }
-}
 
 // ---------------- K1+K3+K2+K3 fused: conv1 -> pool -> conv2 -> pool per image, p1 in LDS ----------------
 // Block = (image b, conv2 output-channel half nh), 512 threads. conv2 needs all 32 conv1 channels
-// of the image, so each half recomputes conv1 (fp32 VALU, exactly the K1 kernel's math) straight
-// into the zero-bordered, channel-chunk-major LDS image that conv2_fwd_lds used to stage from
-// global memory; p1 / idx1 still go to global (half 0 only) for the backward. The conv2 weight
-// half's loads are issued FIRST and stay in flight behind the conv1 arithmetic; they are written
-// to LDS after it. One launch and one activation round trip less than conv1_pool_fwd +
-// conv2_fwd_lds. LDS: p1 image 27 KiB + W2 half 75 KiB + x / W1 staging 7.5 KiB.
-#ifndef TFD_C12_XS
-#define TFD_C12_XS 36
-#endif
-constexpr int C12_XS = TFD_C12_XS;                           // x image row stride (floats): fewer bank conflicts than 32
+// of the image, so each half recomputes conv1 (on the matrix core, step 3 below) straight into the
+// zero-bordered, channel-chunk-major LDS image conv2 reads; p1 / idx1 still go to global (half 0
+// only) for the backward. The conv2 weight half's loads are issued FIRST and stay in flight behind
+// the conv1 arithmetic; they are written to LDS after it. One launch and no activation round trip
+// between the two convolutions (a separate conv1 kernel + conv2 kernel measured slower).
+// LDS: p1 image 27 KiB + W2 half 75 KiB + x / W1 staging + the bf16 "5-wide row" x image.
+constexpr int C12_XS = 36;                                  // x image row stride (floats): fewer bank conflicts than 32
 constexpr int C12_XR = 60;                                   // rows: 32 (zero-bordered 28 x 28) + 28 zero rows
-constexpr int C12_XZ = 32 * C12_XS;                          // a padded tap (k >= 25): lands in the zero rows for any pixel
 constexpr int C12_XOFF = C2L_FWD_SMEM;                       // fp32 [C12_XR][C12_XS] x image
 constexpr int C12_WOFF = C12_XOFF + C12_XR * C12_XS * 4;     // fp32 [25][32] W1 + [32] bias
 constexpr int C12_IOFF = C12_WOFF + (KTAPS * C1 + C1) * 4;   // uint8 [196][32] conv1 argmax
-#ifndef TFD_C1_X8  // 1: conv1's A fragments are 16-B reads of a bf16 "5-wide row" image (see conv12_fwd_lds)
-#define TFD_C1_X8 1
-#endif
 constexpr int C12_X8P = 40;                                  // X8 row pitch (16-B entries): rows oh, oh + 1 of a
                                                              // 16-lane read group land 8 slots apart mod 16 (no overlap)
 constexpr int C12_X8OFF = C12_IOFF + 196 * 32;               // bf16x8 [32][C12_X8P] = x[r][c..c+4], 0, 0, 0
-constexpr int C12_SMEM = C12_X8OFF + (TFD_C1_X8 ? 32 * C12_X8P * 16 : 0);  // 122,944 B (+20,480 with X8)
+constexpr int C12_SMEM = C12_X8OFF + 32 * C12_X8P * 16;     // 143,424 B
 static_assert(C12_X8OFF % 16 == 0 && C12_SMEM <= 160 * 1024, "conv12 LDS carve");
 static_assert(C12_IOFF % 16 == 0, "LDS carve alignment");
 #ifndef TFD_STAMP
@@ -457,29 +183,20 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
   //    16 B per lane, written to LDS only after conv1); waves 4-7 the W1 / bias and the x image
   //    (prefetched row -> x) that conv1 needs first. Both overlap the LDS zeroing.
   const uint16_t* wsrc = a.pbf + OFF_WC2 + nh * 32;
-  const int rot = TFD_WROT ? (int)((blockIdx.x * 1031u) % 3200u) : 0;
+  const int rot = (int)((blockIdx.x * 1031u) % 3200u);  // per-block start: spread L2 channels
   constexpr int NW = (3200 + 255) / 256;
   uint4 vw[NW];
   f32x4 xv = f32x4{0.f, 0.f, 0.f, 0.f}, w1v = f32x4{0.f, 0.f, 0.f, 0.f};
   const int u = t - 256;
-#ifndef TFD_EXP_C12L
-#define TFD_EXP_C12L 0  // timing experiments only (wrong results): 1 no W2 loads, 2 x from a fixed row
-#endif
-#ifndef TFD_C12_XFIRST  // 1: the x / W1 loads are issued before the W2 loads (a barrier orders them)
-#define TFD_C12_XFIRST 0  // measured: no gain (75.6 vs 75.4 us/step), kept as a switch
-#endif
   auto load_w2 = [&]() {
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
       const int i = (t + 256 * j + rot) % 3200;
-      vw[j] = (t + 256 * j < 3200 && !(TFD_EXP_C12L & 1)) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 2) * 64 + (i & 3) * 8) : zero4();
+      vw[j] = (t + 256 * j < 3200) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 2) * 64 + (i & 3) * 8) : zero4();
     }
   };
   if (t < 256) {
-    if (!TFD_C12_XFIRST) load_w2();
-  } else if (TFD_EXP_C12L & 2) {
-    if (u < (KTAPS * C1 + C1) / 4) w1v = reinterpret_cast<const f32x4*>(a.p32 + OFF_WC1)[u];
-    if (u < 196) xv = reinterpret_cast<const f32x4*>(a.data)[u];
+    load_w2();
   } else {
     if (u < (KTAPS * C1 + C1) / 4) w1v = reinterpret_cast<const f32x4*>(a.p32 + OFF_WC1)[u];
     // the prefetched image, loaded speculatively beside its tag and the step
@@ -493,13 +210,6 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
       if (u < 196) xv = reinterpret_cast<const f32x4*>(x)[u];
     }
   }
-#if TFD_C12_XFIRST
-  // conv1 needs x / W1 first; the 51 KB W2 half is only needed after conv1. The CU's memory
-  // pipeline serves a block's loads at ~11 B/cycle, so W2 issued beside x delayed x by ~3.5 K
-  // cycles: waves 0-3 issue W2 only after waves 4-7 have issued x / W1 (plain s_barrier, no fence)
-  __builtin_amdgcn_s_barrier();
-  if (t < 256) load_w2();
-#endif
   C12_STAMP(1);
   C12_STAMPW(1);
 #if TFD_STAMP
@@ -524,7 +234,6 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
   }
   C12_STAMPW(5);
   __syncthreads();
-#if TFD_C1_X8
   // the "5-wide row" image: X8[r][c] = bf16(x[r][c .. c+4]) and three zeros (zero-bordered 32 x 32
   // coordinates, c <= 27), so the 8 taps (kh, kw = 0..7) of one kernel row are one 16-B LDS read
   {
@@ -539,19 +248,8 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
     }
     __syncthreads();
   }
-#endif
   C12_STAMP(2);
   C12_STAMPW(6);
-#ifndef TFD_EXP_C12
-#define TFD_EXP_C12 0  // timing experiments only (wrong results): 1 skip conv1, 2 skip conv2's MFMA loop
-#endif
-#ifndef TFD_EXP_C12REP
-#define TFD_EXP_C12REP 1  // timing experiment only: >1 runs the conv1 section that many times (warm I-cache)
-#endif
-#pragma nounroll
-  for (int rep = 0; rep < TFD_EXP_C12REP; ++rep) {
-  if (rep == 1) C12_STAMP(7);
-  if (!(TFD_EXP_C12 & 1))
   // 3. conv1 on the matrix core: implicit GEMM M = 784 pixels (pool-window-major, m = pp*4 + win),
   //    N = 32 channels, K = 25 taps padded to 32 -> one v_mfma_f32_16x16x32_bf16 per (M-tile, N-tile);
   //    each lane's 4 accumulator rows are one 2x2 window, so bias + relu + max + argmax happen in
@@ -565,7 +263,6 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
     uint8_t* idx_l = reinterpret_cast<uint8_t*>(smem_raw + C12_IOFF);  // [196][32]
     const float bias0 = w1[KTAPS * C1 + col], bias1 = w1[KTAPS * C1 + 16 + col];
     constexpr int MT = 7;  // ceil(49 / 8)
-#if TFD_C1_X8
     // K = kernel row kh * 8 + kw (kw < 5 real): MFMA 1 covers kh = 0..3 (lane group g reads kernel
     // row g: one 16-B read of X8), MFMA 2 kh = 4 (every group reads row 4; only group 0's weights
     // are non-zero). 2 MFMAs + 2 ds_read_b128 per M-tile instead of 8 scalar reads + 8 converts.
@@ -593,40 +290,6 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
         z[i][nt] = mfma16x16x32(af2[i], bw2[nt], mfma16x16x32(af[i], bw1[nt], f32x4{0.f, 0.f, 0.f, 0.f}));
-#else
-    bf16x8 bw[2];
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int k = 8 * g + jj;
-        bw[nt][jj] = (bf16)(k < KTAPS ? w1[k * C1 + nt * 16 + col] : 0.f);
-      }
-    // The A gather is VALU-bound (wave64 VALU = 4 cycles, 2 waves per SIMD): per-lane tap offsets
-    // are computed once, a padded tap (k >= 25) points into the zero rows (no select, no exec-masked
-    // read: a masked read per element made the compiler wait lgkmcnt(0) 56 times, 7.6 K cycles),
-    // so each element costs one add + the read.
-    int toff[8];
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const int k = 8 * g + jj;
-      toff[jj] = k < KTAPS ? (k / 5) * C12_XS + (k % 5) : C12_XZ;
-    }
-    bf16x8 af[MT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const int mt = w + 8 * i;
-      const int m = min(mt, 48) * 16 + col, pp = m >> 2, win = m & 3;
-      const int pb = (2 * (pp / 14) + (win >> 1)) * C12_XS + 2 * (pp % 14) + (win & 1);
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) af[i][jj] = (bf16)xs[pb + toff[jj]];
-    }
-    f32x4 z[MT][2];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) z[i][nt] = mfma16x16x32(af[i], bw[nt], f32x4{0.f, 0.f, 0.f, 0.f});
-#endif
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       const int mt = w + 8 * i;
@@ -649,7 +312,6 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
       }
     }
   }
-  }  // rep
   C12_STAMP(3);
   // 4. the W2 half (landed during conv1) into LDS
   if (t < 256) {
@@ -688,27 +350,7 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
     base[j] = (g * C2F_PLANE + px) * 8;
   }
   const bf16* wcol = wt + c2f_wrow(8 * g + q) + 4 * p4;  // rows tap*32 + 8g + q (+4)
-  if (TFD_C2_PIPE && !(TFD_EXP_C12 & 2)) {
-    conv2_taps(img, wcol, base, acc);
-  } else {
-#pragma unroll
-  for (int kh = 0; kh < ((TFD_EXP_C12 & 2) ? 0 : 5); ++kh) {
-#pragma unroll
-    for (int kw = 0; kw < 5; ++kw) {
-      const int tap = kh * 5 + kw, toff = (kh * C2F_W + kw) * 8;
-      const bf16* wr = wcol + tap * C2F_WTAP;
-      const bf16x8 b0 = frag_tr16(wr, wr + C2F_WR4);
-      const bf16x8 b1 = frag_tr16(wr + 16, wr + 16 + C2F_WR4);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        if (j < nmt) {
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + base[j] + toff);
-          acc[j][0] = mfma16x16x32(af, b0, acc[j][0]);
-          acc[j][1] = mfma16x16x32(af, b1, acc[j][1]);
-        }
-    }
-  }
-  }
+  conv2_taps(img, wcol, base, acc);
   C12_STAMP(5);
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
@@ -744,30 +386,18 @@ struct SlabEpi {
       if (m4 + r < M) out[(size_t)(m4 + r) * ld + n] = v[r];
   }
 };
-constexpr int FC1_BM = 64, FC1_BN = 64, FC1_BK = TFD_FC1_BK;
-#ifndef TFD_FC1_SPLITS
-#define TFD_FC1_SPLITS 7
-#endif
-constexpr int FC1_SPLITS = TFD_FC1_SPLITS;  // 3136 = 7 * 448 = 7 * 7 * 64 (14 splits need FC1_BK 32)
-#ifndef TFD_FC1_ONESHOT  // 1: every split's whole K range staged in one memory round trip (gemm_block_oneshot)
-#define TFD_FC1_ONESHOT 1
-#endif
+constexpr int FC1_BM = 64, FC1_BN = 64, FC1_BK = FC1_BK_;
+constexpr int FC1_SPLITS = 7;  // 3136 = 7 * 448; each split's whole K range staged in one memory round trip
 constexpr int FC1_NKT = FEAT / FC1_SPLITS / FC1_BK;  // K-tiles per split
 static_assert(FC1_NKT * FC1_BK * FC1_SPLITS == FEAT, "fc1 split-K must tile K exactly");
 __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DenseLoader<true> la{a.p2, FEAT, a.B, FEAT};
-  DenseLoader<false> lb{fc1_wbf(a), HID, HID, FEAT};
+  DenseLoader<false> lb{a.pbf + OFF_WD1, HID, HID, FEAT};
   const int z = blockIdx.z;
   SlabEpi epi{a.fc1_slab + (size_t)z * a.B * HID, HID, a.B, HID};
-  const int kb = z * kper, ke = min(FEAT, kb + kper);
-#if TFD_FC1_ONESHOT
-  (void)ke;
+  const int kb = z * kper;
   gemm_block_oneshot<FC1_BM, FC1_BN, FC1_BK, FC1_NKT, 2, 2>(la, lb, epi, blockIdx.y * FC1_BM, blockIdx.x * FC1_BN, kb, (bf16*)smem_raw);
-#else
-  gemm_block<FC1_BM, FC1_BN, FC1_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, blockIdx.y * FC1_BM, blockIdx.x * FC1_BN, kb, ke,
-                                           (bf16*)smem_raw);
-#endif
 }
 
 // ---------------- K4-K9 head: reduce slabs, bias, relu, dropout, FC10, softmax-xent, bwd ----------
@@ -776,12 +406,6 @@ __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   do {                                                                                                   \
     if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[4 * a.B * 8 + blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
   } while (0)
-#ifndef TFD_HEAD_DPP  // 1: the logits' wave sums by DPP instead of __shfl_xor (ds_bpermute) chains
-#define TFD_HEAD_DPP 1
-#endif
-#ifndef TFD_HEAD_PREF  // 1: the thread's 4 output-layer rows (40 floats) as 10 16-B loads issued first
-#define TFD_HEAD_PREF 0
-#endif
 template <int CTRL, int RMASK, int BMASK, int N>
 __device__ __forceinline__ void dpp_add(float (&x)[N]) {  // x += x[DPP source lane]; masked-off lanes add 0
 #pragma unroll
@@ -792,21 +416,7 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   HEAD_STAMP(0);
   const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n0 = 4 * t;
-#if TFD_HEAD_PREF
-  float wreg[4 * NCLS];  // rows n0..n0+3 of the [1024][10] output weight are 40 contiguous floats
-  {
-    const f32x4* src = reinterpret_cast<const f32x4*>(a.p32 + OFF_OUT + (size_t)n0 * NCLS);
-#pragma unroll
-    for (int q = 0; q < NCLS; ++q) {
-      const f32x4 v = src[q];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) wreg[4 * q + e] = v[e];
-    }
-  }
-#define HEAD_W(j, c) wreg[(j) * NCLS + (c)]
-#else
 #define HEAD_W(j, c) (a.p32 + OFF_OUT)[(size_t)(n0 + (j)) * NCLS + (c)]
-#endif
   if (a.t_out && row == 0 && t == 0) *a.t_out = *a.step + 1;
   // the label's dependent chain (step -> perm -> label) starts first, hidden behind the fc1 math
   const int lbl = batch_label(a, row);
@@ -844,7 +454,6 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   }
   HEAD_STAMP(2);
   __shared__ float red[4][NCLS];
-#if TFD_HEAD_DPP
   // DPP wave sums (quad swaps, row shifts, row broadcasts: no LDS round trips) of the 10 partials,
   // interleaved; the wave total lands in lane 63
   dpp_add<0xB1, 0xF, 0xF>(lp);   // quad_perm [1,0,3,2]
@@ -857,13 +466,6 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
 #pragma unroll
     for (int c = 0; c < NCLS; ++c) red[wv][c] = lp[c];
   }
-#else
-#pragma unroll
-  for (int c = 0; c < NCLS; ++c) {
-    const float v = wave_sum(lp[c]);
-    if (lane == 0) red[wv][c] = v;
-  }
-#endif
   __syncthreads();
   float logit[NCLS];
 #pragma unroll
@@ -912,10 +514,7 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
 // [B][10] staged in LDS; the 4 batch quarters are summed through LDS (deterministic).
 constexpr int OUTG_ROWS = 64;
 constexpr int OUTG_BLOCKS = (HID + 1 + OUTG_ROWS - 1) / OUTG_ROWS;  // 17 (last block: bias row)
-#ifndef TFD_OUTG_LB
-#define TFD_OUTG_LB 16
-#endif
-constexpr int OUTG_LB = TFD_OUTG_LB;  // hd loads batched per thread (a one-at-a-time loop was a 32-deep latency chain)
+constexpr int OUTG_LB = 16; // hd loads batched per thread (a one-at-a-time loop was a 32-deep latency chain)
 __device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, float* smem) {
   float* dl = smem;                      // [B][10]
   float* part = smem + a.B * NCLS;       // [4][64][10]
@@ -1000,15 +599,12 @@ struct GradEpi {
     }
   }
 };
-#ifndef TFD_FDW_BM
-#define TFD_FDW_BM 64
-#endif
-constexpr int FDW_BM = TFD_FDW_BM, FDW_BN = 64, FDW_BK = TFD_FDW_BK;
+constexpr int FDW_BM = 64, FDW_BN = 64, FDW_BK = FDW_BK_;
 __device__ __forceinline__ void fc1_dw_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   OnesRowMC la{a.p2, FEAT, FEAT, a.B};
   DenseLoader<false> lb{a.dh, HID, HID, a.B};
   GradEpi epi{a.grad + OFF_WD1, a.gbf_a ? a.gbf_a + OFF_WD1 : nullptr, HID, FEAT + 1, HID};
-  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, by * FDW_BM, bx * FDW_BN, 0, a.B, smem);
+  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), GEMM_RS>(la, lb, epi, by * FDW_BM, bx * FDW_BN, 0, a.B, smem);
 }
 
 // ---------------- K10 fc1 dX + K11 MaxPoolGrad + ReluGrad -> dz2 (dense, conv2 pre-act grad) --------
@@ -1036,29 +632,17 @@ struct UnpoolEpi {
     }
   }
 };
-#ifndef TFD_OUTG_FIRST  // 1: output-layer gradient blocks get the lowest block ids of fc1_bwd
-#define TFD_OUTG_FIRST 1
-#endif
-#ifndef TFD_FDX_RS  // register stages of the long-K (1024) fc1 dX blocks
-#define TFD_FDX_RS 1  // with BK 128: 8 K-steps, A/B vs RS 2 -1.3 us/step
-#endif
 // fc1 dX tile width: 64 (196 blocks at B = 128) inside the fused fc backward, where the dX tiles
 // share the launch with ~800 dW tiles; 32 (392 blocks) when dX runs alone (DP step, part 2), where
 // 196 blocks left a quarter of the CUs idle (A/B: one GPU 64 better by 1.3 us, DP 32 better by 1.5)
-#ifndef TFD_FDX_BN
-#define TFD_FDX_BN 64
-#endif
-#ifndef TFD_FDX_BN_ALONE
-#define TFD_FDX_BN_ALONE 32
-#endif
-#ifndef TFD_FDX_RS_ALONE
-#define TFD_FDX_RS_ALONE 2  // dX alone (DP): 2 register stages, A/B -0.3 us (profiles/ab_fc1_dx_tiles_r2.log)
-#endif
-constexpr int FDX_BM = 32, FDX_BN = TFD_FDX_BN, FDX_BK = TFD_FDX_BK, FDX_BN2 = TFD_FDX_BN_ALONE;
-template <int BN = FDX_BN, int RS = TFD_FDX_RS>
+constexpr int FDX_BM = 32, FDX_BN = 64, FDX_BK = FDX_BK_, FDX_BN2 = 32;
+// register stages of the long-K (1024) fc1 dX blocks: 1 with BK 128 (8 K-steps; RS 2 +1.3 us/step);
+// dX alone (DP): 2 (-0.3 us, profiles/ab_fc1_dx_tiles_r2.log)
+constexpr int FDX_RS = 1, FDX_RS_ALONE = 2;
+template <int BN = FDX_BN, int RS = FDX_RS>
 __device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   DenseLoader<true> la{a.dh, HID, a.B, HID};
-  DenseLoader<true> lb{fc1_wbf(a), HID, FEAT, HID};
+  DenseLoader<true> lb{a.pbf + OFF_WD1, HID, FEAT, HID};
   UnpoolEpi epi{a.p2, a.idx2, a.dz2, a.B};
   gemm_block<FDX_BM, BN, FDX_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), RS>(la, lb, epi, by * FDX_BM, bx * BN, 0, HID, smem);
 }
@@ -1070,15 +654,12 @@ constexpr int FDX_GX = FEAT / FDX_BN;                                           
 constexpr int FDX_GX2 = FEAT / FDX_BN2;
 static_assert(FEAT % FDX_BN == 0 && FEAT % FDX_BN2 == 0, "fc1 dX tiles cover the 3136 features exactly");
 // part 0: all three products; part 1: dW + out-layer grads (bucket A complete); part 2: dX only.
-#ifndef TFD_FDX_XCD  // 1: the dX blocks that share a W1 column tile run on one XCD (one L2 fill of it)
-#define TFD_FDX_XCD 1
-#endif
 // dX block j of gx * gy tiles -> (bx, by). Workgroups are dealt to the 8 XCDs round-robin by id, so
 // blocks j, j + 8, j + 16, ... share an XCD and its L2. Without the remap the gy row tiles reading
 // one W1 column tile (bx) sit on gy different XCDs (gx odd), and W1 (6.4 MB) is pulled into L2 gy
 // times; with it, tile T = (j % 8) * per + j / 8 (bx = T / gy) keeps each column tile on one XCD.
 __device__ __forceinline__ void fdx_tile(int j, int gx, int gy, int& bx, int& by) {
-  const int full = TFD_FDX_XCD ? (gx * gy) / (8 * gy) * (8 * gy) : 0;
+  const int full = (gx * gy) / (8 * gy) * (8 * gy);
   const int T = j < full ? (j & 7) * (full >> 3) + (j >> 3) : j;
   bx = T / gy;
   by = T - bx * gy;
@@ -1090,22 +671,17 @@ __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int pa
   if (part == 2) {
     int bx, by;
     fdx_tile(id, FDX_GX2, gy, bx, by);
-    fc1_dx_block<FDX_BN2, TFD_FDX_RS_ALONE>(a, bx, by, (bf16*)smem_raw);
+    fc1_dx_block<FDX_BN2, FDX_RS_ALONE>(a, bx, by, (bf16*)smem_raw);
     return;
   }
-#if TFD_OUTG_FIRST
   // the 17 output-layer blocks each walk the whole batch: dispatched first, their latency hides
   // under the GEMM tiles instead of forming the kernel's tail.
   if (id < OUTG_BLOCKS) { out_grad_block(a, id, (float*)smem_raw); return; }
   id -= OUTG_BLOCKS;
-#endif
   // part 0: the dX blocks (K = 1024: 16 k-steps each) get the lowest block ids so they are
   // dispatched first and the short dW blocks (K = B) fill in around them, instead of the long
   // blocks starting last and forming the kernel's tail.
   if (part == 0) {
-#if TFD_DIAG_FC1BWD == 1  // timing diagnosis only (wrong gradients): drop the dX blocks
-    if (id < n_dx) return;
-#endif
     if (id < n_dx) {
       int bx, by;
       fdx_tile(id, FDX_GX, gy, bx, by);
@@ -1114,103 +690,7 @@ __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int pa
     }
     id -= n_dx;
   }
-#if TFD_DIAG_FC1BWD == 2  // timing diagnosis only (wrong gradients): drop the dW blocks
-  if (id < FDW_GX * FDW_GY) return;
-#endif
-  if (id < FDW_GX * FDW_GY) { fc1_dw_block(a, id % FDW_GX, id / FDW_GX, (bf16*)smem_raw); return; }
-#if !TFD_OUTG_FIRST
-  id -= FDW_GX * FDW_GY;
-  out_grad_block(a, id, (float*)smem_raw);
-#endif
-}
-
-// ---------------- one-GPU: fc1 dW (+ bias row) with ApplyAdam in the epilogue ----------------
-// The fp32 dW tile is staged in LDS (pitch BN + 4), then each thread owns two 8-column chunks:
-// their p / m / v (fp32) are loaded before the barrier, updated with the TF ApplyAdam equations of
-// adam4 (same expressions, the un-rounded fp32 gradient), and stored with the bf16 shadow going to
-// the NEXT step's half of the double-buffered fc1 shadow (MnistStepArgs::pbf_alt) -- the dX blocks
-// of this launch still read this step's half. ~1000 blocks at 3 per CU: one block's Adam stream
-// overlaps another's GEMM phase, so the 90 MB of fc1 optimizer traffic rides beside the fc
-// backward instead of forming a separate ~15 us pass (and the 6.4 MB bf16 gradient is never written
-// or read back).
-constexpr int FDWA_PITCH = FDW_BN + 4;
-constexpr int FDWA_CPR = FDW_BN / 8, FDWA_NCH = FDW_BM * FDWA_CPR / 256;
-static_assert(FDW_BM * FDWA_CPR % 256 == 0, "whole chunks per thread");
-__device__ __forceinline__ void fc1_dw_adam_block(const MnistStepArgs& a, const MnistAdamArgs& o, int bx, int by,
-                                                  bf16* smem) {
-  OnesRowMC la{a.p2, FEAT, FEAT, a.B};
-  DenseLoader<false> lb{a.dh, HID, HID, a.B};
-  constexpr int WM = 2, WN = 2, WTM = FDW_BM / WM, WTN = FDW_BN / WN, TM = WTM / 16, TN = WTN / 16;
-  static_assert(FDW_BM * FDWA_PITCH * 4 <= GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, DenseLoader<false>>::BYTES,
-                "staged dW tile fits in the GEMM's LDS");
-  f32x4 acc[TM][TN];
-  const int m0 = by * FDW_BM, n0 = bx * FDW_BN;
-  gemm_mainloop<FDW_BM, FDW_BN, FDW_BK, WM, WN, OnesRowMC, DenseLoader<false>, TFD_GEMM_RS>(la, lb, m0, n0, 0, a.B,
-                                                                                            smem, acc);
-  float* cs = reinterpret_cast<float*>(smem);  // the mainloop ended with a barrier: operands are dead
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int r0 = wm * WTM + 16 * i + 4 * (lane >> 4), col = wn * WTN + 16 * j + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cs[(r0 + r) * FDWA_PITCH + col] = acc[i][j][r];
-    }
-  f32x4 P[FDWA_NCH][2], Mm[FDWA_NCH][2], Vv[FDWA_NCH][2];
-  int64_t q4[FDWA_NCH];
-  bool ok[FDWA_NCH];
-#pragma unroll
-  for (int c = 0; c < FDWA_NCH; ++c) {
-    const int q = tid + 256 * c, row = m0 + q / FDWA_CPR, col = n0 + (q % FDWA_CPR) * 8;
-    ok[c] = row <= FEAT;  // rows 0..3135 weights, row 3136 the bias (OFF_BD1 follows the weight)
-    q4[c] = (OFF_WD1 + (int64_t)row * HID + col) / 4;
-    if (ok[c]) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        P[c][h] = reinterpret_cast<const f32x4*>(o.p)[q4[c] + h];
-        Mm[c][h] = reinterpret_cast<const f32x4*>(o.m)[q4[c] + h];
-        Vv[c][h] = reinterpret_cast<const f32x4*>(o.v)[q4[c] + h];
-      }
-    }
-  }
-  const int64_t t = *o.t;
-  const float b1p = powf(o.beta1, (float)t), b2p = powf(o.beta2, (float)t);
-  const float lr_t = o.lr * sqrtf(1.f - b2p) / (1.f - b1p);
-  const float c1 = 1.f - o.beta1, c2 = 1.f - o.beta2;
-  uint16_t* nxt = ((*a.step + 1) & 1) ? a.pbf_alt : o.pbf;
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < FDWA_NCH; ++c) {
-    if (!ok[c]) continue;
-    const int q = tid + 256 * c, rl = q / FDWA_CPR, cl = (q % FDWA_CPR) * 8;
-    uint32_t sh[4];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x4 g = *reinterpret_cast<const f32x4*>(cs + rl * FDWA_PITCH + cl + 4 * h);
-      f32x4 p = P[c][h], m = Mm[c][h], v = Vv[c][h];
-      m = m + (g - m) * c1;
-      v = v + (g * g - v) * c2;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) p[j] -= lr_t * m[j] / (sqrtf(v[j]) + o.eps);
-      reinterpret_cast<f32x4*>(o.p)[q4[c] + h] = p;
-      reinterpret_cast<f32x4*>(o.m)[q4[c] + h] = m;
-      reinterpret_cast<f32x4*>(o.v)[q4[c] + h] = v;
-      sh[2 * h] = pack_bf2(p[0], p[1]);
-      sh[2 * h + 1] = pack_bf2(p[2], p[3]);
-    }
-    *reinterpret_cast<uint4*>(nxt + 4 * q4[c]) = make_uint4(sh[0], sh[1], sh[2], sh[3]);
-  }
-}
-// the one-GPU fc backward with fused fc1 Adam: [out-layer grads | fc1 dX tiles | fc1 dW+Adam tiles]
-__global__ __launch_bounds__(256) void fc1_bwd_adam(MnistStepArgs a, MnistAdamArgs o, int n_dx) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  int id = blockIdx.x;
-  if (id < OUTG_BLOCKS) { out_grad_block(a, id, (float*)smem_raw); return; }
-  id -= OUTG_BLOCKS;
-  if (id < n_dx) { fc1_dx_block(a, id % FDX_GX, id / FDX_GX, (bf16*)smem_raw); return; }
-  id -= n_dx;
-  fc1_dw_adam_block(a, o, id % FDW_GX, id / FDW_GX, (bf16*)smem_raw);
+  if (id < FDW_GX * FDW_GY) fc1_dw_block(a, id % FDW_GX, id / FDW_GX, (bf16*)smem_raw);
 }
 
 // ---------------- DP: fc gradients from all-gathered sufficient factors ----------------
@@ -1329,55 +809,8 @@ __global__ __launch_bounds__(256) void fc_grad_sfb(MnistStepArgs a) {
   OnesRowBuf la{a.sfb_p2, WB, (uint32_t)((int64_t)WB * FEAT * 2)};
   RankRowsMC lb{a.sfb_dr, HID, HID, WB, a.B, a.sfb_rs, (uint32_t)((int64_t)a.sfb_world * a.sfb_rs * 2)};
   GradEpi epi{a.grad + OFF_WD1, a.gbf_a ? a.gbf_a + OFF_WD1 : nullptr, HID, FEAT + 1, HID};
-  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(
+  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), GEMM_RS>(
       la, lb, epi, (id / FDW_GX) * FDW_BM, (id % FDW_GX) * FDW_BN, 0, WB, (bf16*)smem_raw);
-}
-
-// ---------------- K13 conv2 dgrad (+ conv1 relu/pool mask epilogue) ----------------
-struct Conv2DgradA {  // (m = (b,ih,iw), k = tap*64 + co)
-  static constexpr bool KC = true;
-  const uint16_t* __restrict__ dz2;
-  int M;
-  __device__ __forceinline__ uint4 operator()(int m, int k) const {
-    if (m >= M || k >= 1600) return zero4();
-    const int b = m / 196, r = m - b * 196, ih = r / 14, iw = r - ih * 14;
-    const int tap = k >> 6, co0 = k & 63, kh = tap / 5, kw = tap - kh * 5;
-    const int oh = ih - kh + 2, ow = iw - kw + 2;
-    if ((unsigned)oh >= 14u || (unsigned)ow >= 14u) return zero4();
-    return *reinterpret_cast<const uint4*>(dz2 + ((size_t)(b * 14 + oh) * 14 + ow) * 64 + co0);
-  }
-};
-struct Conv2DgradB {  // (n = ci, k = tap*64 + co) -> W2[tap][ci][co]
-  static constexpr bool KC = true;
-  const uint16_t* __restrict__ w2;
-  __device__ __forceinline__ uint4 operator()(int n, int k) const {
-    if (n >= 32 || k >= 1600) return zero4();
-    const int tap = k >> 6, co0 = k & 63;
-    return *reinterpret_cast<const uint4*>(w2 + (size_t)(tap * 32 + n) * 64 + co0);
-  }
-};
-struct MaskEpi {
-  const uint16_t* __restrict__ p1;
-  uint16_t* __restrict__ dp1m;
-  int M;
-  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m4 + r;
-      if (m >= M) return;
-      const size_t o = (size_t)m * 32 + n;
-      const uint16_t pv = p1[o];
-      dp1m[o] = pv != 0 ? f2bf_bits(v[r]) : (uint16_t)0;  // relu output > 0
-    }
-  }
-};
-constexpr int C2D_BM = 64, C2D_BN = 32, C2D_BK = TFD_C2D_BK;
-__device__ __forceinline__ void conv2_dgrad_block(const MnistStepArgs& a, int bx, bf16* smem) {
-  const int M = a.B * 196;
-  Conv2DgradA la{a.dz2, M};
-  Conv2DgradB lb{a.pbf + OFF_WC2};
-  MaskEpi epi{a.p1, a.dp1m, M};
-  gemm_block<C2D_BM, C2D_BN, C2D_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, bx * C2D_BM, 0, 0, 1600, smem);
 }
 
 // ---------------- K13 (LDS-staged): conv2 dgrad + conv1 relu/pool-mask epilogue ----------------
@@ -1389,45 +822,20 @@ __device__ __forceinline__ void conv2_dgrad_block(const MnistStepArgs& a, int bx
 // A-fragment lanes read 16 consecutive 16-B slots (conflict-free); N = 32 (2 tiles); K = 1600.
 // Wave w owns M-tiles {w & 3, (w & 3) + 4}, both N-tiles, and taps [0,13) (w < 4) or [13,25):
 // 2 A + 2 B fragment reads per 4 MFMAs; the two K halves are summed through LDS at the end.
-#ifndef TFD_C2D_PIPE  // 1: conv2 dgrad K loop unrolled + software-pipelined (see conv2_dgrad_lds)
-#define TFD_C2D_PIPE 1
-#endif
 constexpr int C2D_ROWS = 11, C2D_COLS = 20, C2D_PLANE = 224;
-// weight rows (tap, ci) x 64 co. TFD_C2D_GLDS=1: staged by LDS-DMA (global_load_lds_dwordx4: no
-// VGPR round trip, no ds_write pass; one wave instruction fills 1 KiB = 8 rows) into an unpadded
-// image whose 16-B chunk c of row r holds global chunk c ^ (r & 7) -- the swizzle is applied to
-// the per-lane SOURCE address, and the 16 rows of a B-fragment ds_read_b128 group then hit 16
-// distinct bank quads. 0: register staging into rows of pitch 80 (not 72: the B-fragment reads of
-// rows co = lane & 15 are conflict-free; 72: 2-way, 3.2 K vs 1.6 K LDS cycles per block).
-#ifndef TFD_C2D_GLDS
-#define TFD_C2D_GLDS 1
-#endif
-constexpr int C2D_WLD = TFD_C2D_GLDS ? 64 : 80;
+// weight rows (tap, ci) x 64 co, staged by LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no
+// ds_write pass; one wave instruction fills 1 KiB = 8 rows) into an unpadded image whose 16-B chunk
+// c of row r holds global chunk c ^ (r & 7) -- the swizzle is applied to the per-lane SOURCE
+// address, and the 16 rows of a B-fragment ds_read_b128 group then hit 16 distinct bank quads
+// (time-neutral against register staging into pitch-80 rows, 25 KB less LDS).
 __device__ __forceinline__ const bf16* c2d_w(const bf16* wt, int rr, int ch) {
-  return TFD_C2D_GLDS ? wt + rr * 64 + ((ch ^ (rr & 7)) << 3) : wt + rr * C2D_WLD + ch * 8;
+  return wt + rr * 64 + ((ch ^ (rr & 7)) << 3);
 }
-constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 800 * C2D_WLD) * 2;  // 131072 B (156672 at pitch 80)
+constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 800 * 64) * 2;  // 131072 B
 static_assert(C2D_PLANE * 16 % 256 == 0 && C2D_PLANE >= C2D_ROWS * C2D_COLS, "dz2 plane");
-constexpr int C1W_HALF = 98;  // pooled conv1 pixels per half image (7 rows of 14)
-#ifndef TFD_C1W_XS  // row pitch (floats) of the tail's zero-bordered x image
-#define TFD_C1W_XS 34
-#endif
-// 34, not 32: the 32 lanes of one ds_read_b32 group (same pooled pixel, channels c) read the 2x2
-// window position that channel's argmax picked, {0, 1, XS, XS + 1} + tap; with XS = 32 the two
-// window rows share banks (2-way), with XS = 34 the four positions are four banks.
-constexpr int C1W_XS = TFD_C1W_XS;
-#ifndef TFD_C1W_PRE  // 1: the tail's global operands (x image, argmax bytes, relu mask) loaded before
-#define TFD_C1W_PRE 1  //    the K loop (in flight behind it) instead of after it
-#endif
-// fused conv1-wgrad tail: buffers carved from the (dead) weight region
-constexpr int C2D_X_OFF = 8 * C2D_PLANE * 8 * 2;          // 28672
-constexpr int C2D_G_OFF = C2D_X_OFF + 32 * C1W_XS * 4;
-constexpr int C2D_I_OFF = C2D_G_OFF + C1W_HALF * 32 * 4;
-constexpr int C2D_P_OFF = C2D_I_OFF + C1W_HALF * 32;
-static_assert(C2D_I_OFF % 16 == 0 && C2D_P_OFF % 16 == 0, "LDS carve alignment");
-static_assert(C2D_P_OFF + 16 * 833 * 4 <= C2D_SMEM, "fused conv1-wgrad tail exceeds the dgrad LDS");
+constexpr int C2D_X_OFF = 8 * C2D_PLANE * 8 * 2;          // 28672: the fused tail's buffers (dead weight region)
 static_assert(4 * 4 * 64 * 16 <= C2D_X_OFF, "park region overlaps the fused tail");
-// TFD_C1W_MFMA=1: the conv1 weight gradient of the tail on the matrix core. dW1[tap][c] =
+// The conv1 weight gradient of the tail on the matrix core. dW1[tap][c] =
 // sum_px X[tap][px] dz1[px][c] over the half image's 14 x 28 conv1 output pixels (rows padded to
 // 32, K = 448 = 14 k-steps) with dz1 the unpooled pre-activation gradient (the bf16-rounded pooled
 // gradient at its window's argmax position, zero elsewhere) and X the im2col of the zero-bordered x
@@ -1435,9 +843,6 @@ static_assert(4 * 4 * 64 * 16 <= C2D_X_OFF, "park region overlaps the fused tail
 // row 25 of A is ones (the bias). 8 waves = 2 tap tiles x 2 channel tiles x 2 K halves. Replaces the
 // per-thread loop of 25 scalar LDS reads + FMAs per pooled pixel (phase clocks: 7.0 k of the dgrad
 // block's 18.4 k cycles, profiles/stamps_dgrad_r3.log).
-#ifndef TFD_C1W_MFMA
-#define TFD_C1W_MFMA 1
-#endif
 constexpr int C2D_Z_OFF = C2D_X_OFF;                        // dz1 [448][32] bf16, chunk-swizzled
 constexpr int C2D_XS_OFF = C2D_Z_OFF + 448 * 32 * 2;        // x copies [5][18][40] bf16
 constexpr int C2D_T_END = C2D_XS_OFF + 5 * 18 * 40 * 2;
@@ -1459,16 +864,9 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
   const int b = bid >> 1, h = bid & 1, t = threadIdx.x;
   const uint16_t* src = a.dz2 + (size_t)b * 196 * 64;
   const uint16_t* wsrc = a.pbf + OFF_WC2;
-  const int rot = TFD_WROT ? (int)((bid * 1031u) % 6400u) : 0;  // per-block start: spread L2 channels
-#if TFD_C1_EARLY_X
-  // the conv1-wgrad tail's step -> perm chain resolved now, behind the staging loads
-  const int xrow_idx = data_row(a, b);
-#endif
   {
     constexpr int CI = 8 * C2D_PLANE, NI = (CI + 511) / 512;  // 1792 chunks -> 4 per thread
-#if TFD_C2D_GLDS
     {  // 6400 weight chunks = 100 LDS-DMA wave instructions, 12-13 per wave, all in flight at once
-      (void)rot;
       const int wv = t >> 6, ln = t & 63;
       for (int ii = wv; ii < 100; ii += 8) {
         const int p = ii * 64 + ln, rr = p >> 3, sl = p & 7;
@@ -1476,7 +874,6 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
                                          (__attribute__((address_space(3))) void*)(wt + ii * 64 * 8), 16, 0, 0);
       }
     }
-#endif
     uint4 vi[NI];
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -1484,21 +881,6 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
       const int r = px / C2D_COLS + 7 * h - 2, c = px % C2D_COLS - 2;
       vi[j] = (i < CI && px < C2D_ROWS * C2D_COLS && (unsigned)r < 14u && (unsigned)c < 14u)
                   ? *reinterpret_cast<const uint4*>(src + (r * 14 + c) * 64 + ch * 8) : zero4();
-    }
-#pragma unroll
-    for (int half = 0; half < (TFD_C2D_GLDS ? 0 : 2); ++half) {
-      constexpr int NH = (3200 + 511) / 512;
-      uint4 vw[NH];
-#pragma unroll
-      for (int j = 0; j < NH; ++j) {
-        const int i = (half * 3200 + t + 512 * j + rot) % 6400;
-        vw[j] = (t + 512 * j < 3200) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 3) * 64 + (i & 7) * 8) : zero4();
-      }
-#pragma unroll
-      for (int j = 0; j < NH; ++j) {
-        const int i = (half * 3200 + t + 512 * j + rot) % 6400;
-        if (t + 512 * j < 3200) *reinterpret_cast<uint4*>(wt + (i >> 3) * C2D_WLD + (i & 7) * 8) = vw[j];
-      }
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -1509,14 +891,12 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
   C2D_STAMP(1);
   const int lane = t & 63, w = t >> 6, g = lane >> 4, mt0 = w & 3, kq = w >> 2;
   const int two = (mt0 + 4 < 7);
-#if TFD_C1W_PRE
   // the conv1-wgrad tail's global operands, issued now and consumed after the K loop (which reads
   // only LDS), so their latency hides behind it: waves 4-7 the x image and the argmax bytes, waves
   // 0-3 the conv1 relu outputs that mask their dX rows
   float xpre[4];
-  uint4 ipre = zero4();
   uint16_t p1pre[2][2][4];
-  [[maybe_unused]] uint8_t ipb[2][2][4];  // MFMA tail: the argmax window position of each dX value
+  uint8_t ipb[2][2][4];  // the argmax window position of each dX value
   if (kq) {
     const int u = t - 256;
     const float* xrow = a.data + (size_t)data_row(a, b) * 784;
@@ -1525,8 +905,6 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
       const int i = 4 * u + q, r = i >> 5, c = i & 31;
       xpre[q] = (r >= 2 && r < 30 && c >= 2 && c < 30) ? xrow[(r - 2) * 28 + c - 2] : 0.f;
     }
-    if (u < C1W_HALF * 32 / 16)
-      ipre = reinterpret_cast<const uint4*>(a.idx1 + ((size_t)b * 196 + h * C1W_HALF) * 32)[u];
   } else {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -1536,10 +914,9 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
         for (int r = 0; r < 4; ++r) {
           const int x = min(4 * g + r, 13), n = nt * 16 + (lane & 15), ih = 7 * h + min(mt0 + 4 * j, 6);
           p1pre[j][nt][r] = a.p1[((size_t)b * 196 + ih * 14 + x) * 32 + n];
-          if (TFD_C1W_MFMA) ipb[j][nt][r] = a.idx1[((size_t)b * 196 + ih * 14 + x) * 32 + n];
+          ipb[j][nt][r] = a.idx1[((size_t)b * 196 + ih * 14 + x) * 32 + n];
         }
   }
-#endif
   __syncthreads();
   C2D_STAMP(2);
   const int iw = lane & 15;
@@ -1550,7 +927,6 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
 #pragma unroll
   for (int j = 0; j < 2; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nl = lane & 15;
-#if TFD_C2D_PIPE
   // Fully unrolled, software-pipelined K loop: step st = (tap, co half sk), step st + 1's four
   // fragments are read while step st's MFMAs run; both M-tiles on every wave (the second tile of
   // wave 3 reads rows past the image, dropped by the epilogue), and the per-half step count is a
@@ -1558,7 +934,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
   // lgkmcnt(0) twice per step.
   {
     const int kqu = __builtin_amdgcn_readfirstlane(kq);
-    const int tapb = kqu ? 13 : 0, ns = TFD_EXP_SKIP_MAIN ? 0 : (kqu ? 24 : 26);
+    const int tapb = kqu ? 13 : 0, ns = kqu ? 24 : 26;
     bf16x8 fb[2][2], fa[2][2];
     auto ld = [&](int st, int slot) {
       const int tap = tapb + (st >> 1), sk = st & 1;
@@ -1587,25 +963,6 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
       }
     }
   }
-  if (false)
-#endif
-  for (int tap = (kq ? 13 : 0); tap < (TFD_EXP_SKIP_MAIN ? (kq ? 13 : 0) : (kq ? 25 : 13)); ++tap) {
-    const int kh = tap / 5, kw = tap - kh * 5, toff = -(kh * C2D_COLS + kw) * 8;
-#pragma unroll
-    for (int sk = 0; sk < 2; ++sk) {
-      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(c2d_w(wt, tap * 32 + nl, g + 4 * sk));
-      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(c2d_w(wt, tap * 32 + 16 + nl, g + 4 * sk));
-      const int coff = toff + sk * 4 * C2D_PLANE * 8;  // co chunk 4sk + g
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(img + base[0] + coff);
-      acc[0][0] = mfma16x16x32(a0, b0, acc[0][0]);
-      acc[0][1] = mfma16x16x32(a0, b1, acc[0][1]);
-      if (two) {
-        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(img + base[1] + coff);
-        acc[1][0] = mfma16x16x32(a1, b0, acc[1][0]);
-        acc[1][1] = mfma16x16x32(a1, b1, acc[1][1]);
-      }
-    }
-  }
   // sum the two K halves: waves 4..7 park their accumulators in LDS (image region is dead now)
   C2D_STAMP(3);
   __syncthreads();
@@ -1616,13 +973,10 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) park[(mt0 * 4 + j * 2 + nt) * 64 + lane] = acc[j][nt];
   }
-#if TFD_C1W_PRE && TFD_C1W_MFMA
   for (int i = t; i < (C2D_T_END - C2D_Z_OFF) / 16; i += 512)  // dz1 and the x copies start zero
     reinterpret_cast<uint4*>(smem_raw + C2D_Z_OFF)[i] = zero4();
-#endif
   __syncthreads();
   C2D_STAMP(4);
-#if TFD_C1W_PRE && TFD_C1W_MFMA
   {
     bf16* dz1 = reinterpret_cast<bf16*>(smem_raw + C2D_Z_OFF);
     bf16* xsh = reinterpret_cast<bf16*>(smem_raw + C2D_XS_OFF);
@@ -1688,126 +1042,9 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
       }
     }
     C2D_STAMP(7);
-    return;
   }
-#endif
-  // K15 + K12 fused: this block's dX rows ARE conv1's pooled-gradient rows [7h, 7h + 7) of image b,
-  // so conv1's weight/bias gradient partial for them is computed here from LDS (no dp1m round trip,
-  // no separate launch). The weight region of LDS is dead now: x image, masked gradient, argmax.
-  float* xs = reinterpret_cast<float*>(smem_raw + C2D_X_OFF);     // [32][C1W_XS] zero-bordered input
-  float* gsl = reinterpret_cast<float*>(smem_raw + C2D_G_OFF);    // [98][32] conv1 pre-act grad
-  uint8_t* isl = reinterpret_cast<uint8_t*>(smem_raw + C2D_I_OFF);  // [98][32] pool argmax
-  float* part = reinterpret_cast<float*>(smem_raw + C2D_P_OFF);   // [16][833] partials
-  if (!kq) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (j == 1 && !two) break;
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const f32x4 v = acc[j][nt] + park[(mt0 * 4 + j * 2 + nt) * 64 + lane];
-        const int n = nt * 16 + (lane & 15), lr = mt0 + 4 * j, ih = 7 * h + lr;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int x = 4 * g + r;  // C row = input column iw
-          if (x >= 14) break;
-          const size_t o = ((size_t)b * 196 + ih * 14 + x) * 32 + n;
-          // conv1 relu output > 0; rounded to bf16 like the stored activation gradients
-#if TFD_C1W_PRE
-          (void)o;
-          gsl[(lr * 14 + x) * 32 + n] = p1pre[j][nt][r] != 0 ? bf2f(f2bf_bits(v[r])) : 0.f;
-#else
-          gsl[(lr * 14 + x) * 32 + n] = a.p1[o] != 0 ? bf2f(f2bf_bits(v[r])) : 0.f;
-#endif
-        }
-      }
-    }
-  } else {
-    const int u = t - 256;
-#if TFD_C1W_PRE
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = 4 * u + q, r = i >> 5, c = i & 31;
-      xs[r * C1W_XS + c] = xpre[q];
-    }
-    if (u < C1W_HALF * 32 / 16) reinterpret_cast<uint4*>(isl)[u] = ipre;
-#else
-#if TFD_C1_EARLY_X
-    const float* xrow = a.data + (size_t)xrow_idx * 784;
-#else
-    const float* xrow = a.data + (size_t)data_row(a, b) * 784;
-#endif
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = 4 * u + q, r = i >> 5, c = i & 31;
-      xs[r * C1W_XS + c] = (r >= 2 && r < 30 && c >= 2 && c < 30) ? xrow[(r - 2) * 28 + c - 2] : 0.f;
-    }
-    if (u < C1W_HALF * 32 / 16)
-      reinterpret_cast<uint4*>(isl)[u] = reinterpret_cast<const uint4*>(a.idx1 + ((size_t)b * 196 + h * C1W_HALF) * 32)[u];
-#endif
-  }
-  __syncthreads();
-  C2D_STAMP(5);
-  {
-    // only the argmax position of each 2x2 window carries gradient: dW1[tap][c] += g * x[argmax + tap]
-    const int c = t & 31, sub = t >> 5;
-    float acc1[26];
-#pragma unroll
-    for (int j = 0; j < 26; ++j) acc1[j] = 0.f;
-    for (int lp = sub; lp < C1W_HALF; lp += 16) {
-      const float gv = gsl[lp * 32 + c];
-      if (!TFD_C1W_SKIP0 || gv != 0.f) {  // no zero skip by default: time must not depend on values (fma(0, x, acc) == acc)
-        const int pp = h * C1W_HALF + lp, w = isl[lp * 32 + c];
-        const int oh = 2 * (pp / 14) + (w >> 1), ow = 2 * (pp % 14) + (w & 1);
-#pragma unroll
-        for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-          for (int kw = 0; kw < 5; ++kw) acc1[kh * 5 + kw] = fmaf(gv, xs[(oh + kh) * C1W_XS + ow + kw], acc1[kh * 5 + kw]);
-        acc1[25] += gv;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 26; ++j) part[sub * 833 + j * 32 + c] = acc1[j];
-  }
-  C2D_STAMP(6);
-  __syncthreads();
-  for (int i = t; i < 26 * 32; i += 512) {
-    float sm = 0.f;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) sm += part[q * 833 + i];
-    a.wg1_slab[(size_t)bid * 832 + i] = sm;
-  }
-  C2D_STAMP(7);
 }
 
-// ---------------- K14 conv2 wgrad (+bias row), split-K slabs ----------------
-struct Conv2WgradA {  // (mn = tap*32+ci [800 = ones row], k = pixel (b,oh,ow))
-  static constexpr bool KC = false;
-  const uint16_t* __restrict__ p1;
-  int K;
-  __device__ __forceinline__ uint4 operator()(int mn, int k) const {
-    if (k >= K || mn > 800) return zero4();
-    if (mn == 800) return make_uint4(0x3F80u, 0u, 0u, 0u);
-    const int tap = mn >> 5, ci0 = mn & 31, kh = tap / 5, kw = tap - kh * 5;
-    const int b = k / 196, r = k - b * 196, oh = r / 14, ow = r - oh * 14;
-    const int ih = oh + kh - 2, iw = ow + kw - 2;
-    if ((unsigned)ih >= 14u || (unsigned)iw >= 14u) return zero4();
-    return *reinterpret_cast<const uint4*>(p1 + ((size_t)(b * 14 + ih) * 14 + iw) * 32 + ci0);
-  }
-};
-constexpr int C2W_BM = 64, C2W_BN = 64, C2W_BK = TFD_C2W_BK;
-constexpr int C2W_GX = (801 + C2W_BM - 1) / C2W_BM;  // 13
-__device__ __forceinline__ void conv2_wgrad_block(const MnistStepArgs& a, int bx, int z, int kper, bf16* smem) {
-  const int K = a.B * 196;
-  Conv2WgradA la{a.p1, K};
-  DenseLoader<false> lb{a.dz2, 64, 64, K};
-  SlabEpi epi{a.wg2_slab + (size_t)z * 801 * 64, 64, 801, 64};
-  const int kb = z * kper, ke = min(K, kb + kper);
-  gemm_block<C2W_BM, C2W_BN, C2W_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), TFD_GEMM_RS>(la, lb, epi, bx * C2W_BM, 0, kb, ke, smem);
-}
-__global__ __launch_bounds__(256) void conv2_wgrad_k(MnistStepArgs a, int kper) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  conv2_wgrad_block(a, blockIdx.x % C2W_GX, blockIdx.x / C2W_GX, kper, (bf16*)smem_raw);
-}
 // ---------------- K14 (LDS-staged): conv2 wgrad (+ K12 bias row) ----------------
 // Block = (tap group tg, image pair ip), 512 threads; 4 x 64 = 256 blocks at B = 128 (one per CU).
 // Per image: p1 (14x14x32) goes into a zero-bordered LDS image [18][18] x 40 ch and dz2 (196 x 64)
@@ -1817,14 +1054,8 @@ __global__ __launch_bounds__(256) void conv2_wgrad_k(MnistStepArgs a, int kper) 
 // w >> 2, co-tile w & 3 and every tap of its group. One fp32 slab per image pair (rows of its tap
 // group; tap group 0 also the bias row 800), reduced by the optimizer tail / reduce_conv_grads.
 // Replaces the im2col GEMM that re-read p1 25x through L2 (83 MB -> 19 MB of staging).
-#ifndef TFD_C2WL_IMG
-#define TFD_C2WL_IMG 2
-#endif
-#ifndef TFD_C2WL_NTG
-#define TFD_C2WL_NTG 4
-#endif
-constexpr int C2WL_IMG = TFD_C2WL_IMG;      // images per block (= slab count B / C2WL_IMG)
-constexpr int C2WL_NTG = TFD_C2WL_NTG;      // tap groups (4: [0,6) [6,12) [12,18) [18,25))
+constexpr int C2WL_IMG = 2;      // images per block (= slab count B / C2WL_IMG; 4 x 8 tap groups: +1.7 us)
+constexpr int C2WL_NTG = 4;      // tap groups (4: [0,6) [6,12) [12,18) [18,25))
 constexpr int C2WL_TPG = 25 / C2WL_NTG;     // taps per group (the last takes the remainder)
 constexpr int C2WL_MAXT = 25 - C2WL_TPG * (C2WL_NTG - 1);
 constexpr int C2WL_CS = 48, C2WL_PW = 18;   // padded image: 18 x 18 positions x 48-ch stride
@@ -1944,84 +1175,14 @@ __device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const i
   C2W_STAMP(7);
 }
 
-__global__ __launch_bounds__(512) void conv2_wgrad_lds(MnistStepArgs a) { conv2_wgrad_body(a, blockIdx.x); }
-__global__ __launch_bounds__(512) void conv2_dgrad_lds(MnistStepArgs a) { conv2_dgrad_body(a, blockIdx.x); }
 // conv2 wgrad and dgrad (+ the conv1 wgrad tail) in ONE launch: both consume only dz2, so the
 // dgrad blocks start on each CU as its wgrad block finishes instead of after a kernel boundary
 // (the dgrad's LDS size is the launch's: one block per CU either way). Blocks [0, nw) wgrad.
-#ifndef TFD_C2_BWD_ONE
-#define TFD_C2_BWD_ONE 1
-#endif
-#ifndef TFD_DIAG_C2BWD  // timing diagnosis only (wrong gradients): 1 drops the wgrad blocks, 2 the dgrad blocks
-#define TFD_DIAG_C2BWD 0
-#endif
 __global__ __launch_bounds__(512) void conv2_bwd_lds(MnistStepArgs a, int nw) {
   if ((int)blockIdx.x < nw) {
-    if (TFD_DIAG_C2BWD != 1) conv2_wgrad_body(a, blockIdx.x);
-  } else if (TFD_DIAG_C2BWD != 2) {
+    conv2_wgrad_body(a, blockIdx.x);
+  } else {
     conv2_dgrad_body(a, blockIdx.x - nw);
-  }
-}
-
-// K13 + K14 in one launch: conv2 dgrad and wgrad both consume dz2 only (independent).
-__global__ __launch_bounds__(256) void conv2_bwd(MnistStepArgs a, int n_dgrad, int kper) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  const int id = blockIdx.x;
-  if (id < n_dgrad) { conv2_dgrad_block(a, id, (bf16*)smem_raw); return; }
-  const int w = id - n_dgrad;
-  conv2_wgrad_block(a, w % C2W_GX, w / C2W_GX, kper, (bf16*)smem_raw);
-}
-
-// ---------------- K15 conv1 wgrad + bias grad (sparse, from pooled grad + argmax) ----------------
-// Only the argmax position of each 2x2 window carries gradient, so dW1[tap][c] =
-// sum_{b,pp} g[b,pp,c] * x[b, argmax-pixel(pp,c) + tap]. Block = (image, half of the 196 pooled
-// pixels): the padded image and the block's dp1m / argmax rows are staged in LDS with 16-B loads
-// (no dependent global loads in the loop), thread (c = t & 31, sub = t >> 5) accumulates 26
-// partials (25 taps + bias), then the 8 subs are summed in LDS into one deterministic slab per block.
-__global__ __launch_bounds__(256) void conv1_wgrad(MnistStepArgs a) {
-  __shared__ float img[32 * 32];
-  __shared__ __attribute__((aligned(16))) uint16_t gs[C1W_HALF * 32];
-  __shared__ __attribute__((aligned(16))) uint8_t is[C1W_HALF * 32];
-  __shared__ float part[8][26 * 32 + 1];
-  const int b = blockIdx.x >> 1, half = blockIdx.x & 1, t = threadIdx.x, c = t & 31, sub = t >> 5;
-  const float* x = a.data + (size_t)data_row(a, b) * 784;
-  for (int i = t; i < 32 * 32; i += 256) img[i] = 0.f;
-  const size_t base = ((size_t)b * 196 + half * C1W_HALF) * 32;
-  for (int i = t; i < C1W_HALF * 32 / 8; i += 256)   // 392 x 16 B of bf16 grads
-    reinterpret_cast<uint4*>(gs)[i] = reinterpret_cast<const uint4*>(a.dp1m + base)[i];
-  for (int i = t; i < C1W_HALF * 32 / 16; i += 256)  // 196 x 16 B of argmax bytes
-    reinterpret_cast<uint4*>(is)[i] = reinterpret_cast<const uint4*>(a.idx1 + base)[i];
-  __syncthreads();
-  if (t < 196) {
-    const f32x4 v = reinterpret_cast<const f32x4*>(x)[t];
-    const int r = (4 * t) / 28, q = (4 * t) % 28;
-    float* d = img + (r + 2) * 32 + q + 2;
-    d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
-  }
-  __syncthreads();
-  float acc[26];
-#pragma unroll
-  for (int j = 0; j < 26; ++j) acc[j] = 0.f;
-  for (int lp = sub; lp < C1W_HALF; lp += 8) {
-    const float g = bf2f(gs[lp * 32 + c]);
-    if (!TFD_C1W_SKIP0 || g != 0.f) {  // no zero skip by default: time must not depend on values (fma(0, x, acc) == acc)
-      const int pp = half * C1W_HALF + lp, w = is[lp * 32 + c];
-      const int oh = 2 * (pp / 14) + (w >> 1), ow = 2 * (pp % 14) + (w & 1);
-#pragma unroll
-      for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-        for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] = fmaf(g, img[(oh + kh) * 32 + ow + kw], acc[kh * 5 + kw]);
-      acc[25] += g;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 26; ++j) part[sub][j * 32 + c] = acc[j];
-  __syncthreads();
-  for (int i = t; i < 26 * 32; i += 256) {
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) s += part[q][i];
-    a.wg1_slab[(size_t)blockIdx.x * 832 + i] = s;
   }
 }
 
@@ -2091,12 +1252,8 @@ constexpr int MAD_C1F4 = (int)(OFF_WC2 / 4);   // 208
 constexpr int MAD_C2END = (int)(OFF_WD1 / 4);  // 13024
 constexpr int MAD_C1BLK = MAD_C1F4 / 16;       // 13
 constexpr int MAD_C2BLK = (MAD_C2END - MAD_C1F4 + 63) / 64;  // 201
-#ifndef TFD_MAD_FC_BLOCKS  // grid-stride blocks of the fc-region Adam
-#define TFD_MAD_FC_BLOCKS 1024
-#endif
-constexpr int MAD_FC_BLOCKS = TFD_MAD_FC_BLOCKS;
+constexpr int MAD_FC_BLOCKS = 1024;  // grid-stride blocks of the fc-region Adam
 constexpr int MAD_CONV = MAD_C1BLK + MAD_C2BLK;
-constexpr int MAD_GRID = MAD_CONV + MAD_FC_BLOCKS;
 static_assert(MAD_C1F4 % 16 == 0, "conv1 region: whole blocks");
 constexpr int MAD_SL = 16;  // slab loads in flight per thread
 __device__ __forceinline__ void adam4(const MnistAdamArgs& o, int64_t i, f32x4 g, float lr_t, float c1, float c2) {
@@ -2165,11 +1322,11 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
   } else {
     const int64_t i0 = fcb4 + (int64_t)(bid - MAD_CONV) * MAD_NT + tid;  // fcb4: MAD_C2END, or the out layer
     const int64_t STRIDE = (int64_t)(grid - MAD_CONV) * MAD_NT;
-#if TFD_ADAM_U > 1
-    // All U strides' loads issued before any math/store, so U x 56 B per lane are in flight
-    // (the one-at-a-time loop leaves the compiler no room: p/m/v stores may alias the next loads).
+    // ADAM_U strides' loads issued before any math/store, so U x 56 B per lane are in flight
+    // (the one-at-a-time loop leaves the compiler no room: p/m/v stores may alias the next loads;
+    // streaming non-temporal loads/stores were +0.9 us: the next step re-reads p/m/v from MALL)
     if (o.gbf) {
-      constexpr int U = TFD_ADAM_U;
+      constexpr int U = ADAM_U;
       for (int64_t base = i0; base < TOTAL / 4; base += STRIDE * U) {
         uint2 h[U];
         f32x4 p[U], m[U], v[U];
@@ -2178,19 +1335,9 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
           const int64_t i = base + (int64_t)u * STRIDE;
           if (i < TOTAL / 4) {
             p[u] = reinterpret_cast<const f32x4*>(o.p)[i];
-#if TFD_ADAM_NT
-            {
-              typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-              const u32x2 hv = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(o.gbf) + i);
-              h[u] = make_uint2(hv[0], hv[1]);
-            }
-            m[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.m) + i);
-            v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(o.v) + i);
-#else
             h[u] = reinterpret_cast<const uint2*>(o.gbf)[i];
             m[u] = reinterpret_cast<const f32x4*>(o.m)[i];
             v[u] = reinterpret_cast<const f32x4*>(o.v)[i];
-#endif
           }
         }
 #pragma unroll
@@ -2203,27 +1350,12 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
             v[u] = v[u] + (g * g - v[u]) * c2;
 #pragma unroll
             for (int j = 0; j < 4; ++j) p[u][j] -= lr_t * m[u][j] / (sqrtf(v[u][j]) + o.eps);
-#if TFD_ADAM_NT  // streaming stores for the optimizer state (m, v are not read again this step)
-            reinterpret_cast<f32x4*>(o.p)[i] = p[u];
-            __builtin_nontemporal_store(m[u], reinterpret_cast<f32x4*>(o.m) + i);
-            __builtin_nontemporal_store(v[u], reinterpret_cast<f32x4*>(o.v) + i);
-#else
             reinterpret_cast<f32x4*>(o.p)[i] = p[u];
             reinterpret_cast<f32x4*>(o.m)[i] = m[u];
             reinterpret_cast<f32x4*>(o.v)[i] = v[u];
-#endif
             reinterpret_cast<uint2*>(o.pbf)[i] = make_uint2(pack_bf2(p[u][0], p[u][1]), pack_bf2(p[u][2], p[u][3]));
           }
         }
-      }
-    } else
-#endif
-    if (o.gbf) {  // bf16 gradients: 8 B instead of 16 B per float4 of parameters
-      for (int64_t i = i0; i < TOTAL / 4; i += STRIDE) {
-        const uint2 h = reinterpret_cast<const uint2*>(o.gbf)[i];
-        const f32x4 g = f32x4{__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xFFFF0000u),
-                              __uint_as_float(h.y << 16), __uint_as_float(h.y & 0xFFFF0000u)};
-        adam4(o, i, g, lr_t, c1, c2);
       }
     } else {
       for (int64_t i = i0; i < TOTAL / 4; i += STRIDE) adam4(o, i, reinterpret_cast<const f32x4*>(a.grad)[i], lr_t, c1, c2);
@@ -2243,54 +1375,23 @@ inline void set_smem(int bytes) {
 }  // namespace
 
 int mnist_fc1_splits(int B) { (void)B; return FC1_SPLITS; }
-int mnist_wg2_splits(int B) {
-#if TFD_CONV2_LDS
-  return (B + C2WL_IMG - 1) / C2WL_IMG;  // one slab per image pair (conv2_wgrad_lds)
-#endif
-  const int K = B * 196;
-  const int kper = TFD_C2W_KPER;
-  return (K + kper - 1) / kper;
-}
+int mnist_wg2_splits(int B) { return (B + C2WL_IMG - 1) / C2WL_IMG; }  // one slab per image pair
 
 void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s) {
   mnist_forward_conv(a, s);
   mnist_forward_fc(a, train, s);
 }
 
-#ifndef TFD_CONV12_FUSED  // 1: conv1 fused into the conv2 kernel (p1 stays in LDS)
-#define TFD_CONV12_FUSED 1
-#endif
 void mnist_forward_conv(const MnistStepArgs& a, hipStream_t s) {
-  const int B = a.B;
-#if TFD_CONV12_FUSED && TFD_CONV2_LDS
-  if (!a.conv_unfused) {
-    set_smem<conv12_fwd_lds>(C12_SMEM);
-    conv12_fwd_lds<<<2 * B, 512, C12_SMEM, s>>>(a);
-    return;
-  }
-#endif
-  conv1_pool_fwd<<<4 * B, 256, 0, s>>>(a);
-#if TFD_CONV2_LDS
-  set_smem<conv2_fwd_lds>(C2L_FWD_SMEM);
-  conv2_fwd_lds<<<2 * B, 512, C2L_FWD_SMEM, s>>>(a);
-#else
-  {
-    constexpr int sm = GemmSmem<C2F_BM, C2F_BN, C2F_BK, Conv2FwdA, C2F_B>::BYTES;
-    set_smem<conv2_pool_fwd>(sm);
-    conv2_pool_fwd<<<(B * 196 + C2F_BM - 1) / C2F_BM, 256, sm, s>>>(a);
-  }
-#endif
+  set_smem<conv12_fwd_lds>(C12_SMEM);
+  conv12_fwd_lds<<<2 * a.B, 512, C12_SMEM, s>>>(a);
 }
 
 void mnist_forward_fc(const MnistStepArgs& a, bool train, hipStream_t s) {
   const int B = a.B;
   {
-#if TFD_FC1_ONESHOT
     constexpr int sm = GemmSmemOneshot<FC1_BM, FC1_BN, FC1_BK, FC1_NKT, DenseLoader<true>, DenseLoader<false>>::BYTES;
     static_assert(sm <= 160 * 1024, "fc1 one-shot LDS");
-#else
-    constexpr int sm = GemmSmem<FC1_BM, FC1_BN, FC1_BK, DenseLoader<true>, DenseLoader<false>>::BYTES;
-#endif
     set_smem<fc1_fwd>(sm);
     const int kper = (FEAT + a.fc1_splits - 1) / a.fc1_splits;
     dim3 g(HID / FC1_BN, (B + FC1_BM - 1) / FC1_BM, a.fc1_splits);
@@ -2312,34 +1413,12 @@ void mnist_backward_a(const MnistStepArgs& a, hipStream_t s, int part) {
 }
 
 void mnist_backward_b(const MnistStepArgs& a, hipStream_t s) {
-  const int B = a.B;
-  const int K = B * 196;
-  const int kper = ((K + a.wg2_splits - 1) / a.wg2_splits + C2W_BK - 1) / C2W_BK * C2W_BK;
-#if TFD_CONV2_LDS
-  // conv2 wgrad (one slab per image pair), then dgrad + conv1 wgrad, one stream (a forked wgrad
-  // only contended with dgrad for the CUs: 110 vs 100 us/step, profiles/ab_conv_fork.log)
-  (void)kper;
+  // conv2 wgrad (one slab per image pair), then dgrad + conv1 wgrad, in one launch (a forked wgrad
+  // stream only contended with dgrad for the CUs: 110 vs 100 us/step, profiles/ab_conv_fork.log)
   static_assert(C2WL_SMEM <= C2D_SMEM, "conv2_bwd_lds: the dgrad LDS size covers the wgrad blocks");
-  if (TFD_C2_BWD_ONE) {
-    set_smem<conv2_bwd_lds>(C2D_SMEM);
-    const int nw = C2WL_NTG * a.wg2_splits;
-    conv2_bwd_lds<<<nw + 2 * B, 512, C2D_SMEM, s>>>(a, nw);
-    return;
-  }
-  conv2_wgrad_lds<<<C2WL_NTG * a.wg2_splits, 512, C2WL_SMEM, s>>>(a);
-  set_smem<conv2_dgrad_lds>(C2D_SMEM);
-  conv2_dgrad_lds<<<2 * B, 512, C2D_SMEM, s>>>(a);  // + conv1 wgrad (fused tail)
-#else
-  {
-    constexpr int sm_d = GemmSmem<C2D_BM, C2D_BN, C2D_BK, Conv2DgradA, Conv2DgradB>::BYTES;
-    constexpr int sm_w = GemmSmem<C2W_BM, C2W_BN, C2W_BK, Conv2WgradA, DenseLoader<false>>::BYTES;
-    constexpr int sm = sm_d > sm_w ? sm_d : sm_w;
-    set_smem<conv2_bwd>(sm);
-    const int n_dgrad = (B * 196 + C2D_BM - 1) / C2D_BM;
-    conv2_bwd<<<n_dgrad + C2W_GX * a.wg2_splits, 256, sm, s>>>(a, n_dgrad, kper);
-  }
-  conv1_wgrad<<<2 * B, 256, 0, s>>>(a);
-#endif
+  set_smem<conv2_bwd_lds>(C2D_SMEM);
+  const int nw = C2WL_NTG * a.wg2_splits;
+  conv2_bwd_lds<<<nw + 2 * a.B, 512, C2D_SMEM, s>>>(a, nw);
 }
 
 void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s) {
@@ -2353,35 +1432,10 @@ void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s) {
   reduce_conv_grads<<<RED2_BLOCKS + RED1_BLOCKS, 256, 0, s>>>(a, 0);
 }
 
-void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region, int64_t fc_beg) {
+void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region) {
   const int gb = (a.perm && a.xpre) ? a.B : 0;
-  if (fc_beg < 0) fc_beg = OFF_WD1;
-  if (fc_beg != OFF_WD1 && fc_beg != OFF_OUT) throw std::runtime_error("mnist_adam_fused: fc_beg must be OFF_WD1 or OFF_OUT");
-  // after mnist_backward_a_adam only the out layer is left: 2,576 float4 -> 16 grid-stride blocks
-  const int nfc = !fc_region ? 0 : (fc_beg == OFF_OUT ? 16 : MAD_FC_BLOCKS);
-  mnist_adam_kernel<<<gb + MAD_CONV + nfc, MAD_NT, 0, s>>>(a, o, (int)(fc_beg / 4));
+  mnist_adam_kernel<<<gb + MAD_CONV + (fc_region ? MAD_FC_BLOCKS : 0), MAD_NT, 0, s>>>(a, o, (int)(OFF_WD1 / 4));
 }
-
-void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s) {
-  if (!a.pbf_alt) throw std::runtime_error("mnist_backward_a_adam: needs the double-buffered fc1 shadow (pbf_alt)");
-  const int B = a.B;
-  constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, DenseLoader<false>>::BYTES;
-  constexpr int sm_dx = GemmSmem<FDX_BM, FDX_BN, FDX_BK, DenseLoader<true>, DenseLoader<true>>::BYTES;
-  const int sm_og = (B * NCLS + 4 * OUTG_ROWS * NCLS) * 4;
-  const int sm = std::max(std::max(sm_dw, sm_dx), sm_og);
-  set_smem<fc1_bwd_adam>(sm);
-  const int n_dx = FDX_GX * ((B + FDX_BM - 1) / FDX_BM);
-  fc1_bwd_adam<<<OUTG_BLOCKS + n_dx + FDW_GX * FDW_GY, 256, sm, s>>>(a, o, n_dx);
-}
-
-__global__ __launch_bounds__(256) void settle_shadow_kernel(MnistStepArgs a) {
-  if (!a.pbf_alt || !(*a.step & 1)) return;  // even step: pbf already holds the live fc1 shadow
-  const int64_t n = (int64_t)(FEAT + 1) * HID / 8;
-  const uint4* src = reinterpret_cast<const uint4*>(a.pbf_alt + OFF_WD1);
-  uint4* dst = reinterpret_cast<uint4*>(const_cast<uint16_t*>(a.pbf) + OFF_WD1);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
-}
-void mnist_settle_shadow(const MnistStepArgs& a, hipStream_t s) { settle_shadow_kernel<<<512, 256, 0, s>>>(a); }
 
 int64_t mnist_sfb_slot_elems(int B) { return ((int64_t)B * (2 * HID + 2 * NCLS) + 63) / 64 * 64; }
 

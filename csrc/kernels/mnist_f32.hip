@@ -13,9 +13,6 @@
 // f32_conv1_wgrad K15 (+K12). The slab reduce + optimizer are shared with the bf16 step.
 #include "../common.h"
 
-#ifndef TFD_C1W_SKIP0  // 1 (A/B only): skip zero pooled gradients in the conv1 wgrad (value-dependent time)
-#define TFD_C1W_SKIP0 0
-#endif
 #include "../gemm.h"  // buf_ld
 #include "../gemm_f32.h"
 #include "../mnist_layout.h"
@@ -466,7 +463,7 @@ __global__ __launch_bounds__(256) void f32_conv1_wgrad(MnistF32Args a) {
   for (int j = 0; j < 26; ++j) acc[j] = 0.f;
   for (int lp = sub; lp < F_C1W_HALF; lp += 8) {
     const float g = gs[lp * 32 + c];
-    if (!TFD_C1W_SKIP0 || g != 0.f) {  // no zero skip by default: time must not depend on values (fma(0, x, acc) == acc)
+    {  // no zero skip: time must not depend on values (fma(0, x, acc) == acc)
       const int pp = half * F_C1W_HALF + lp, w = is[lp * 32 + c];
       const int oh = 2 * (pp / 14) + (w >> 1), ow = 2 * (pp % 14) + (w & 1);
 #pragma unroll

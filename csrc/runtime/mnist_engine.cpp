@@ -11,8 +11,12 @@
 #include <torch/custom_class.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <map>
+#include <set>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "../mnist_layout.h"
 #include "../tfd_kernels.h"
@@ -97,10 +101,7 @@ class MnistEngine : public torch::CustomClassHolder {
 
   // ---- state accessors (views share storage with the engine) ----
   at::Tensor params() { return params_; }
-  at::Tensor params_bf16() {  // the live fc1 shadow settled into pbf_ first (fc_adam double buffer)
-    if (alt_live_) mnist_settle_shadow(args(), stream());
-    return pbf_;
-  }
+  at::Tensor params_bf16() { return pbf_; }
   at::Tensor grads() { return grad_; }
   // bf16 gradient buffer: the DP wire format (reduced in place by the bucket all-reduces)
   at::Tensor grads_bf16() { return gbf_; }
@@ -147,16 +148,7 @@ class MnistEngine : public torch::CustomClassHolder {
   void set_keep_prob(double kp) { keep_prob_ = kp; }
   void sync_shadow() {
     cast_f32_bf16((const float*)params_.data_ptr(), (uint16_t*)pbf_.data_ptr(), TOTAL, stream());
-    if (alt_live_) copy_shadow_to_alt();
   }
-  // One-GPU fc1 Adam fused into the fc1 dW epilogue (mnist_backward_a_adam, default on): used by
-  // the one-GPU bf16 Adam step with the fused optimizer tail; any other step kind first settles the
-  // double-buffered fc1 shadow back into pbf (leave_alt) and runs as before.
-  void set_fc_adam(bool on) {
-    if (!on) leave_alt();
-    fc_adam_ = on;
-  }
-  bool fc_adam_active() const { return fc_adam_ && !dp() && !fp32_ && opt_ == 0 && fuse_tail_ && !zero_; }
 
   void set_adam(double lr, double b1, double b2, double eps) {
     opt_ = 0; lr_ = lr; b1_ = b1; b2_ = b2; eps_ = eps;
@@ -233,8 +225,6 @@ class MnistEngine : public torch::CustomClassHolder {
   void set_fused_tail(int64_t on) { fuse_tail_ = on != 0; }
   // one GPU, fused tail: keep the fc-region gradients in bf16 (as DP all-reduces them)
   void set_local_bf16_grads(int64_t on) { local_bf16_grads_ = on != 0; }
-  // 0 (default): conv1 fused into the conv2 forward kernel; 1: the two separate kernels (A/B)
-  void set_conv_unfused(int64_t on) { conv_unfused_ = on != 0; }
   // Make every rank's state whole again after ZeRO-1 steps (before eval / checkpoint / broadcast):
   // each rank updated the fp32 master, m and v of its own fc1 shard only, so all four are
   // all-gathered -- the bf16 shadow (what the forward reads) and the fp32 master + Adam slots (what
@@ -356,7 +346,6 @@ class MnistEngine : public torch::CustomClassHolder {
   void train_step() { train_step_impl(true); }
 
   void train_step_impl(bool join_end) {
-    if (!fc_adam_active()) leave_alt();  // every other step kind writes the single shadow pbf_
     if (zero_ && !sfb_active()) {
       train_step_zero();
       return;
@@ -377,8 +366,6 @@ class MnistEngine : public torch::CustomClassHolder {
       }
       return;
     }
-    const bool fca = fc_adam_active();
-    if (fca) enter_alt();
     mark(P_START, s);
     MnistStepArgs a = args();
     // one GPU: nothing to overlap with. With Adam ONE kernel ends the step: it reduces the conv
@@ -393,20 +380,27 @@ class MnistEngine : public torch::CustomClassHolder {
     const bool gbf_local = fused && local_bf16_grads_;
     if (gbf_local) a.gbf_a = (uint16_t*)gbf_.data_ptr();
     o.gbf = gbf_local ? (const uint16_t*)gbf_.data_ptr() : nullptr;
-    mnist_forward(a, true, s);
+    mnist_forward_conv(a, s);
+    tag("conv_fwd", s);
+    mnist_forward_fc(a, true, s);
+    tag("fc_fwd", s);
     mark(P_FWD, s);
-    if (fca) mnist_backward_a_adam(a, o, s);  // fc1 Adam in the dW epilogue
-    else mnist_backward_a(a, s);
+    mnist_backward_a(a, s);
+    tag("fc_bwd", s);
     mark(P_BFC, s);
     a.step_bump = (int64_t*)step_.data_ptr();
     mnist_backward_b(a, s);
+    tag("conv_bwd", s);
     if (fused) {
       mark(P_BCONV, s);
-      mnist_adam_fused(a, o, s, true, fca ? OFF_OUT : OFF_WD1);
+      mnist_adam_fused(a, o, s, true);
+      tag("opt", s);
     } else {
       mnist_conv_grad_reduce(a, s);
+      tag("slab_reduce", s);
       mark(P_BCONV, s);
       apply_optimizer_range(0, TOTAL, 1.0, 0, s);
+      tag("opt", s);
     }
     mark(P_OPT, s);
   }
@@ -435,36 +429,45 @@ class MnistEngine : public torch::CustomClassHolder {
     }
     mark(P_START, s);
     mnist_forward_conv(a, s);
+    tag("conv_fwd", s);
     if (pending_opt_a_) {
-      HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+      wait(s, ev_opt_a_, "fc_fwd<-opt_fc");
       pending_opt_a_ = false;
     }
     mnist_forward_fc(a, true, s);
+    tag("fc_fwd", s);
     mark(P_FWD, s);
     mnist_backward_a(a, s, 0);
+    tag("fc_bwd", s);
     mark(P_BFC, s);
     HIP_OK(hipEventRecord(ev_a_, s));
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
+    wait(comm_stream_, ev_a_, "ar_fc<-fc_bwd");
     mark(P_CA0, comm_stream_);
     reduce_bucket(BUCKET_SPLIT, TOTAL, bf);
+    tag("ar_fc", comm_stream_);
     mark(P_CA1, comm_stream_);
     HIP_OK(hipEventRecord(ev_ag_, comm_stream_));
-    HIP_OK(hipStreamWaitEvent(opt_stream_, ev_ag_, 0));
+    wait(opt_stream_, ev_ag_, "opt_fc<-ar_fc");
     apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 0, opt_stream_, (const int64_t*)tnext_.data_ptr());
+    tag("opt_fc", opt_stream_);
     HIP_OK(hipEventRecord(ev_opt_a_, opt_stream_));
     mnist_backward_b(a, s);
+    tag("conv_bwd", s);
     mnist_conv_grad_reduce(a, s);
+    tag("slab_reduce", s);
     mark(P_BCONV, s);
     HIP_OK(hipEventRecord(ev_b_, s));
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
+    wait(comm_stream_, ev_b_, "ar_conv<-slab_reduce");
     mark(P_CB0, comm_stream_);
     reduce_bucket(0, BUCKET_SPLIT, bf);
+    tag("ar_conv", comm_stream_);
     mark(P_CB1, comm_stream_);
     HIP_OK(hipEventRecord(ev_done_, comm_stream_));
-    HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+    wait(s, ev_done_, "opt_conv<-ar_conv");
     apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s);
+    tag("opt_conv", s);
     mark(P_OPT, s);
-    if (join_end) HIP_OK(hipStreamWaitEvent(s, ev_opt_a_, 0));
+    if (join_end) wait(s, ev_opt_a_, "end<-opt_fc");
     else pending_opt_a_ = true;
   }
 
@@ -500,46 +503,56 @@ class MnistEngine : public torch::CustomClassHolder {
     mark(P_START, s);
     if (shard && pending_wag_ && !wag_issued_) {  // last step's fc1 bf16 shards -> every rank, beside the conv fwd
       HIP_OK(hipEventRecord(ev_start_, s));
-      HIP_OK(hipStreamWaitEvent(comm_stream_, ev_start_, 0));
+      wait(comm_stream_, ev_start_, "wag<-opt");
       ag_w(comm_stream_);
+      tag("wag", comm_stream_);
       HIP_OK(hipEventRecord(ev_wag_, comm_stream_));
     }
     mnist_forward_conv(a, s);
+    tag("conv_fwd", s);
     HIP_OK(hipEventRecord(ev_p2_, s));
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_p2_, 0));
+    wait(comm_stream_, ev_p2_, "gather_p2<-conv_fwd");
     mark(P_CA0, comm_stream_);
     gather_sfb(true, comm_stream_);
+    tag("gather_p2", comm_stream_);
     if (shard && pending_wag_) {
-      HIP_OK(hipStreamWaitEvent(s, ev_wag_, 0));
+      wait(s, ev_wag_, "fc_fwd<-wag");
       pending_wag_ = wag_issued_ = false;
     }
     mnist_forward_fc(a, true, s);
+    tag("fc_fwd", s);
     mark(P_FWD, s);
     HIP_OK(hipEventRecord(ev_a_, s));
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_a_, 0));
+    wait(comm_stream_, ev_a_, "gather_dr<-fc_fwd");
     gather_sfb(false, comm_stream_);
+    tag("gather_dr", comm_stream_);
     mark(P_CA1, comm_stream_);
     HIP_OK(hipEventRecord(ev_ag_, comm_stream_));
     mnist_backward_a(a, s, 2);  // fc1 dX from this rank's own rows
+    tag("fc1_dx", s);
     mark(P_BFC, s);
     mnist_backward_b(a, s);
+    tag("conv_bwd", s);
     mnist_conv_grad_reduce(a, s);
+    tag("slab_reduce", s);
     mark(P_BCONV, s);
     HIP_OK(hipEventRecord(ev_b_, s));
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ev_b_, 0));
+    wait(comm_stream_, ev_b_, "ar_conv<-slab_reduce");
     mark(P_CB0, comm_stream_);
     reduce_bucket(0, BUCKET_SPLIT, bf);
+    tag("ar_conv", comm_stream_);
     mark(P_CB1, comm_stream_);
     HIP_OK(hipEventRecord(ev_done_, comm_stream_));
-    HIP_OK(hipStreamWaitEvent(s, ev_ag_, 0));
+    wait(s, ev_ag_, "sfb_gemm<-gather_dr");
     mnist_fc_grad_sfb(a, s);  // beside the conv bucket's all-reduce
+    tag("sfb_gemm", s);
     const int64_t* t = (const int64_t*)tnext_.data_ptr();
     // With real peers the conv bucket's all-reduce can outlast the SFB GEMM (at 8 ranks the ZeRO
     // GEMM is ~4 us): the fc-region optimizer (its gradients are local) then runs first and covers
     // it, and only the small conv region waits for the collective. At world 1 (the rehearsal) the
     // collective is instant and one launch is cheaper.
     const bool split_opt = world() > 1;
-    if (!split_opt) HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+    if (!split_opt) wait(s, ev_done_, "opt<-ar_conv");
     if (shard) {
       const int64_t beg[3] = {0, OFF_WD1 + rk * zshard_, OFF_BD1};
       const int64_t end[3] = {BUCKET_SPLIT, OFF_WD1 + (rk + 1) * zshard_, TOTAL};
@@ -551,40 +564,50 @@ class MnistEngine : public torch::CustomClassHolder {
                    (float)eps_, t, 0, (float)scale};
         if (split_opt) {
           adam_apply_ranges(o, 2, beg + 1, n + 1, s);
+          tag("opt_fc", s);
           // the updated shard can leave now: the gather queues behind the conv bucket's all-reduce on
           // the comm stream and runs beside the conv-region Adam and the next conv forward
           HIP_OK(hipEventRecord(ev_start_, s));
-          HIP_OK(hipStreamWaitEvent(comm_stream_, ev_start_, 0));
+          wait(comm_stream_, ev_start_, "wag<-opt_fc");
           ag_w(comm_stream_);
+          tag("wag", comm_stream_);
           HIP_OK(hipEventRecord(ev_wag_, comm_stream_));
           wag_issued_ = true;
-          HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+          wait(s, ev_done_, "opt_conv<-ar_conv");
           adam_apply_ranges(o, 1, beg, n, s);
+          tag("opt_conv", s);
         } else {
           adam_apply_ranges(o, 3, beg, n, s);
+          tag("opt", s);
         }
       } else {
         for (int k = 1; k < 3; ++k) apply_optimizer_range(beg[k], end[k], scale, 0, s, t);
-        if (split_opt) HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+        tag("opt_fc", s);
+        if (split_opt) wait(s, ev_done_, "opt_conv<-ar_conv");
         apply_optimizer_range(beg[0], end[0], scale, 0, s, t);
+        tag("opt_conv", s);
       }
       pending_wag_ = true;
       if (join_end) {  // the caller reads whole weights after this step: gather the shards now
         if (!wag_issued_) {
           HIP_OK(hipEventRecord(ev_start_, s));
-          HIP_OK(hipStreamWaitEvent(comm_stream_, ev_start_, 0));
+          wait(comm_stream_, ev_start_, "wag<-opt");
           ag_w(comm_stream_);
+          tag("wag", comm_stream_);
           HIP_OK(hipEventRecord(ev_wag_, comm_stream_));
         }
-        HIP_OK(hipStreamWaitEvent(s, ev_wag_, 0));
+        wait(s, ev_wag_, "end<-wag");
         pending_wag_ = wag_issued_ = false;
       }
     } else if (split_opt) {
       apply_optimizer_range(BUCKET_SPLIT, TOTAL, scale, 0, s, t);
-      HIP_OK(hipStreamWaitEvent(s, ev_done_, 0));
+      tag("opt_fc", s);
+      wait(s, ev_done_, "opt_conv<-ar_conv");
       apply_optimizer_range(0, BUCKET_SPLIT, scale, 0, s, t);
+      tag("opt_conv", s);
     } else {
       apply_optimizer_range(0, TOTAL, scale, 0, s, t);
+      tag("opt", s);
     }
     mark(P_OPT, s);
   }
@@ -733,10 +756,6 @@ class MnistEngine : public torch::CustomClassHolder {
     hipStream_t s = stream();
     TORCH_CHECK(s != nullptr, "capture needs a non-default stream (use torch.cuda.stream(...))");
     drop_graph(name);
-    // the fc1 shadow mode switch copies weights: done eagerly, never recorded into the graph (a
-    // captured copy would re-run on every replay and overwrite the live half)
-    if (fc_adam_active()) enter_alt();
-    else leave_alt();
     HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
     try {
       for (int64_t i = 0; i < n; ++i) train_step_impl(i == n - 1);
@@ -752,7 +771,6 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
     HIP_OK(hipGraphDestroy(g));
     graphs_[name] = ex;
-    graph_alt_[name] = alt_live_;
   }
   // forward + backward (fc gradients, conv slab reduce, step bump) as one graph, no optimizer: the
   // compute part of a parameter-server worker step (the update runs on the PS task's GPU,
@@ -762,7 +780,6 @@ class MnistEngine : public torch::CustomClassHolder {
     TORCH_CHECK(s != nullptr, "capture needs a non-default stream (use torch.cuda.stream(...))");
     drop_graph(name);
     timed_ = false;
-    leave_alt();  // (eager, see capture_train_steps)
     HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
     try {
       forward(true);
@@ -780,15 +797,10 @@ class MnistEngine : public torch::CustomClassHolder {
     HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
     HIP_OK(hipGraphDestroy(g));
     graphs_[name] = ex;
-    graph_alt_[name] = alt_live_;
   }
   void replay(const std::string& name, int64_t times) {
     auto it = graphs_.find(name);
     TORCH_CHECK(it != graphs_.end(), "no graph named ", name);
-    // the graph's kernels were recorded with or without the double-buffered fc1 shadow: restore
-    // that mode eagerly first (both switches keep the weights; see enter_alt / leave_alt)
-    if (graph_alt_[name]) enter_alt();
-    else leave_alt();
     hipStream_t s = stream();
     for (int64_t i = 0; i < times; ++i) HIP_OK(hipGraphLaunch(it->second, s));
   }
@@ -799,6 +811,75 @@ class MnistEngine : public torch::CustomClassHolder {
       graphs_.erase(it);
     }
   }
+
+  // Dependency structure of the captured step graph (tests/test_graph_topology_gpu.py): captures n
+  // consecutive training steps exactly as capture_train_steps does -- every stream, collective and
+  // cross-stream event edge -- but instead of instantiating the graph returns its topology as text:
+  //   "node <i> <hipGraphNodeType>", "edge <from> <to>", "tag <label>@<step> <node> <node> ..."
+  // where a tag lists the nodes one operation of the schedule added (tag() calls in the train-step
+  // functions). The test checks that every collective depends on the kernel that produced its
+  // operand and that its consumers depend on it (read-after-write and write-after-read across steps).
+  std::vector<std::string> capture_topology(int64_t n) {
+    TORCH_CHECK(n >= 1 && n <= 8, "capture_topology: 1 <= n <= 8");
+    hipStream_t s = stream();
+    TORCH_CHECK(s != nullptr, "capture needs a non-default stream (use torch.cuda.stream(...))");
+    topo_seen_.clear();
+    topo_tags_.clear();
+    topo_ = true;
+    HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+    try {
+      for (int64_t i = 0; i < n; ++i) {
+        topo_step_ = i;
+        train_step_impl(i == n - 1);
+      }
+    } catch (...) {
+      topo_ = false;
+      hipGraph_t g = nullptr;
+      hipStreamEndCapture(s, &g);
+      if (g) hipGraphDestroy(g);
+      throw;
+    }
+    topo_ = false;
+    hipGraph_t g = nullptr;
+    HIP_OK(hipStreamEndCapture(s, &g));
+    std::vector<std::string> out;
+    try {
+      size_t nn = 0, ne = 0;
+      HIP_OK(hipGraphGetNodes(g, nullptr, &nn));
+      std::vector<hipGraphNode_t> nodes(nn);
+      HIP_OK(hipGraphGetNodes(g, nodes.data(), &nn));
+      std::map<hipGraphNode_t, size_t> idx;
+      for (size_t i = 0; i < nn; ++i) {
+        idx[nodes[i]] = i;
+        hipGraphNodeType ty = hipGraphNodeTypeEmpty;
+        HIP_OK(hipGraphNodeGetType(nodes[i], &ty));
+        out.push_back("node " + std::to_string(i) + " " + std::to_string((int)ty));
+      }
+      HIP_OK(hipGraphGetEdges(g, nullptr, nullptr, &ne));
+      std::vector<hipGraphNode_t> from(ne), to(ne);
+      if (ne) HIP_OK(hipGraphGetEdges(g, from.data(), to.data(), &ne));
+      for (size_t e = 0; e < ne; ++e)
+        out.push_back("edge " + std::to_string(idx.at(from[e])) + " " + std::to_string(idx.at(to[e])));
+      for (auto& kv : topo_tags_) {
+        std::string line = "tag " + kv.first;
+        for (auto nd : kv.second) {
+          auto it = idx.find(nd);
+          if (it != idx.end()) line += " " + std::to_string(it->second);
+        }
+        out.push_back(line);
+      }
+    } catch (...) {
+      hipGraphDestroy(g);
+      throw;
+    }
+    HIP_OK(hipGraphDestroy(g));
+    topo_tags_.clear();
+    topo_seen_.clear();
+    return out;
+  }
+  // Fault injection for the topology test: skip the cross-stream wait named `name` in later
+  // captures ("" restores every wait). A graph captured this way is wrong by construction.
+  void set_debug_drop_wait(const std::string& name) { drop_wait_ = name; }
 
   // Cost probe of the sufficient-factor fc-gradient kernel at world W on THIS GPU (one GPU cannot
   // run a W-rank job): factor buffers of W ranks (this rank's slot = its real factors, the others
@@ -842,6 +923,32 @@ class MnistEngine : public torch::CustomClassHolder {
   enum { P_START, P_FWD, P_BFC, P_BCONV, P_OPT, P_CA0, P_CA1, P_CB0, P_CB1, P_N };
   void mark(int k, hipStream_t st) {
     if (timing_) HIP_OK(hipEventRecord(pev_[k], st));
+  }
+  // A cross-stream dependency of the schedule: `st` waits for `ev`. `name` ("consumer<-producer")
+  // identifies the edge for the topology test's fault injection (set_debug_drop_wait).
+  void wait(hipStream_t st, hipEvent_t ev, const char* name) {
+    if (!drop_wait_.empty() && drop_wait_ == name) return;
+    HIP_OK(hipStreamWaitEvent(st, ev, 0));
+  }
+  // capture_topology: the graph nodes this operation added (everything new since the last tag; the
+  // host issues operations one after another, so the difference is exactly this operation's nodes)
+  void tag(const char* label, hipStream_t st) {
+    if (!topo_) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    HIP_OK(hipStreamGetCaptureInfo_v2(st, &cs, &id, &g, &deps, &nd));
+    TORCH_CHECK(cs == hipStreamCaptureStatusActive && g, "tag: stream not capturing");
+    size_t n = 0;
+    HIP_OK(hipGraphGetNodes(g, nullptr, &n));
+    std::vector<hipGraphNode_t> nodes(n);
+    HIP_OK(hipGraphGetNodes(g, nodes.data(), &n));
+    std::vector<hipGraphNode_t> fresh;
+    for (auto nd_ : nodes)
+      if (topo_seen_.insert(nd_).second) fresh.push_back(nd_);
+    topo_tags_.emplace_back(std::string(label) + "@" + std::to_string(topo_step_), std::move(fresh));
   }
 
   // ZeRO helpers (fc1 weight region W = [OFF_WD1, OFF_BD1))
@@ -990,7 +1097,6 @@ class MnistEngine : public torch::CustomClassHolder {
     a.keep_prob = (float)keep_prob_;
     a.seed = seed_;
     a.rank = rank_;
-    a.conv_unfused = conv_unfused_ ? 1 : 0;
     a.rows = input_mode_ == 1 ? (int*)rows_.data_ptr() : nullptr;
     a.xpre = input_mode_ == 1 ? (float*)xpre_.data_ptr() : nullptr;
     a.ypre = input_mode_ == 1 ? (int*)ypre_.data_ptr() : nullptr;
@@ -1009,26 +1115,7 @@ class MnistEngine : public torch::CustomClassHolder {
     }
     a.sfb_by_lo = 0;
     a.sfb_by_hi = -1;  // all tile rows (train_step_sfb narrows it under ZeRO)
-    a.pbf_alt = alt_live_ ? (uint16_t*)pbf_alt_.data_ptr() : nullptr;
     return a;
-  }
-
-  // fc1 region [OFF_WD1, OFF_OUT) of the bf16 shadow, pbf_ -> pbf_alt_ (both halves equal)
-  void copy_shadow_to_alt() {
-    const size_t bytes = (size_t)(OFF_OUT - OFF_WD1) * 2;
-    TORCH_CHECK(hipMemcpyAsync((uint16_t*)pbf_alt_.data_ptr() + OFF_WD1, (const uint16_t*)pbf_.data_ptr() + OFF_WD1,
-                               bytes, hipMemcpyDeviceToDevice, stream()) == hipSuccess, "fc1 shadow copy failed");
-  }
-  void enter_alt() {
-    if (alt_live_) return;
-    if (!pbf_alt_.defined()) pbf_alt_ = at::empty_like(pbf_);
-    copy_shadow_to_alt();  // either parity reads the current weights
-    alt_live_ = true;
-  }
-  void leave_alt() {
-    if (!alt_live_) return;
-    mnist_settle_shadow(args(), stream());  // the live half -> pbf_ (device step parity)
-    alt_live_ = false;
   }
 
   int64_t B_, device_;
@@ -1067,13 +1154,14 @@ class MnistEngine : public torch::CustomClassHolder {
   hipEvent_t ev_p2_ = nullptr, ev_wag_ = nullptr;
   // one GPU + Adam: the optimizer kernel also reduces the conv gradient slabs and bumps the step
   bool fuse_tail_ = true;
-  bool fc_adam_ = false;    // one-GPU fc1 Adam in the dW epilogue (set_fc_adam; A/B neutral, off)
-  bool alt_live_ = false;   // the fc1 shadow is double-buffered (pbf_ / pbf_alt_ by step parity)
-  at::Tensor pbf_alt_;
   bool local_bf16_grads_ = false;
-  bool conv_unfused_ = false;  // measured slower (docs/DESIGN.md)
   std::map<std::string, hipGraphExec_t> graphs_;
-  std::map<std::string, bool> graph_alt_;  // captured with the double-buffered fc1 shadow live
+  // capture_topology: nodes added by each tagged operation (label@step -> node handles)
+  bool topo_ = false;
+  int64_t topo_step_ = 0;
+  std::set<hipGraphNode_t> topo_seen_;
+  std::vector<std::pair<std::string, std::vector<hipGraphNode_t>>> topo_tags_;
+  std::string drop_wait_;  // fault injection for the topology test: this named wait is skipped
   hipEvent_t pev_[P_N] = {};
   bool timing_ = false, timed_ = false, timed_dp_ = false;
 };
@@ -1128,9 +1216,8 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("dp", &MnistEngine::dp)
       .def("set_fused_tail", &MnistEngine::set_fused_tail)
       .def("set_local_bf16_grads", &MnistEngine::set_local_bf16_grads)
-      .def("set_fc_adam", &MnistEngine::set_fc_adam)
-      .def("fc_adam_active", &MnistEngine::fc_adam_active)
-      .def("set_conv_unfused", &MnistEngine::set_conv_unfused)
+      .def("capture_topology", &MnistEngine::capture_topology)
+      .def("set_debug_drop_wait", &MnistEngine::set_debug_drop_wait)
       .def("set_dtype", &MnistEngine::set_dtype)
       .def("dtype", &MnistEngine::dtype)
       .def("set_phase_timing", &MnistEngine::set_phase_timing)

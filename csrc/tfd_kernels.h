@@ -43,7 +43,6 @@ struct MnistStepArgs {
   int fc1_splits, wg2_splits;
   float keep_prob;
   uint32_t seed, rank;
-  int conv_unfused;            // 1: conv1 and conv2 forward as two kernels (A/B; default: one fused kernel)
   // Next-batch prefetch (device dataset mode): the kernel that bumps the step also gathers the NEXT
   // step's batch -- rows[b] = perm[...], xpre[b] = data[rows[b]] ([B][784] fp32), ypre[b] = its label
   // -- and tags it with that step in rows[B]. Consumers load the prefetched value speculatively
@@ -65,12 +64,6 @@ struct MnistStepArgs {
   // ZeRO-sharded SFB: only the 64-row fc1 dW tile rows [sfb_by_lo, sfb_by_hi] (this rank's shard)
   // plus the bias tile row are computed; sfb_by_hi < sfb_by_lo (default 0, -1) means all rows
   int sfb_by_lo, sfb_by_hi;
-  // One-GPU fc1 Adam in the dW epilogue (mnist_backward_a with Adam args): the fc1 dW blocks update
-  // the fc1 weights while the fc1 dX blocks of the SAME launch still read the old bf16 ones, so the
-  // bf16 shadow of the fc1 region is double-buffered: step s reads pbf if s is even, pbf_alt if odd
-  // (the device step counter decides, so captured multi-step graphs stay valid), and its dW-Adam
-  // epilogue writes the other one. nullptr: a single shadow (pbf).
-  uint16_t* pbf_alt;
 };
 
 int mnist_fc1_splits(int B);
@@ -81,14 +74,7 @@ void mnist_forward_fc(const MnistStepArgs& a, bool train, hipStream_t s);     //
 // fc1 dW/dX + out-layer grads. part 0: one launch; part 1: dW + out grads (bucket A complete);
 // part 2: dX (DP launches 1 then 2 so bucket A's all-reduce starts before the dX GEMM)
 void mnist_backward_a(const MnistStepArgs& a, hipStream_t s, int part = 0);
-struct MnistAdamArgs;
-// one-GPU step: the fc backward with ApplyAdam fused into the fc1 dW (+ bias row) epilogue (the fc1
-// region's gradient never leaves the GEMM: no gradient write / read, and the Adam traffic streams
-// beside the GEMM tiles of the same launch). Needs a.pbf_alt (double-buffered fc1 shadow) and is
-// followed by mnist_adam_fused(..., fc_beg = OFF_OUT) for the rest of the parameters.
-void mnist_backward_a_adam(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s);
-// conv2/conv1 grads -> bucket B done. With `aux` set, independent kernels fork onto it (fork/join
-// events recorded on s/aux; both are captured into the step graph as parallel branches).
+// conv2 wgrad slabs + conv2 dgrad + conv1 wgrad slabs (one launch) -> bucket B's slabs done
 void mnist_backward_b(const MnistStepArgs& a, hipStream_t s);
 // deterministic conv weight-gradient slab reduction (+ the global_step bump, MnistStepArgs::step_bump)
 void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s);
@@ -103,12 +89,8 @@ struct MnistAdamArgs {
   int64_t* step;
   const uint16_t* gbf;  // if non-null: the fc-region (bucket A) gradients are bf16 here (gbf_a)
 };
-// fc_region = false: the conv region only; fc_beg: first flat index of the fc region it updates
-// (OFF_WD1; OFF_OUT after mnist_backward_a_adam has updated fc1)
-void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region = true,
-                      int64_t fc_beg = -1);
-// copy the live (step-parity) half of the double-buffered fc1 shadow into pbf (leaving fc_adam mode)
-void mnist_settle_shadow(const MnistStepArgs& a, hipStream_t s);
+// fc_region = false: the conv region only
+void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_t s, bool fc_region = true);
 // DP, sufficient-factor broadcasting: every fc-layer weight gradient is a sum of per-example outer
 // products (dW_fc1 = [P2;1]^T dH, dW_out = [Hd;1]^T dlogits), so the all-reduced gradient is ONE
 // GEMM over the all-gathered factors (K = W*B). Writes the summed fc-region gradients (bucket A)

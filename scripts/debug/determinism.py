@@ -16,7 +16,7 @@ def _worker(rank, world, B, R, unfused):
     dev = torch.device("cuda", 0)
     eng = torch.classes.tfd.MnistEngine(B, 0, 1.0, 5, 0)
     eng.set_adam(0.01, 0.9, 0.999, 1e-8)
-    eng.set_conv_unfused(unfused)
+    assert not unfused, 'the two-kernel conv forward was removed (fused conv12 only)'
     g = torch.Generator().manual_seed(7)
     x = torch.rand(B, 784, generator=g)
     y = torch.randint(0, 10, (B,), generator=g, dtype=torch.int32)

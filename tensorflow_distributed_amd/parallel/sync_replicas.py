@@ -27,15 +27,18 @@ import torch.distributed as dist
 class GlooGradAverager:
     """CPU gradient averaging over a (worker) process group; in-place on the flat buffer."""
 
-    def __init__(self, group=None, world: int = 1):
+    def __init__(self, group=None, world: int = 1, splits=None):
         self.group = group
         self.world = world
+        self.splits = sorted(splits or [])  # bucket boundaries (flat offsets); none = one bucket
         self.last_ms = 0.0  # host time of the last all-reduce (metrics JSONL: allreduce_ms)
 
     def __call__(self, flat_grad: torch.Tensor) -> None:
         if self.world > 1:
             t0 = time.perf_counter()
-            dist.all_reduce(flat_grad, group=self.group)
+            edges = [0] + [e for e in self.splits if 0 < e < flat_grad.numel()] + [flat_grad.numel()]
+            for lo, hi in zip(edges[:-1], edges[1:]):
+                dist.all_reduce(flat_grad[lo:hi], group=self.group)
             flat_grad.div_(self.world)
             self.last_ms = (time.perf_counter() - t0) * 1e3
 

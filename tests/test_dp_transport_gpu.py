@@ -257,27 +257,40 @@ def test_bench_two_ranks_one_gpu_over_ipc(cuda, sfb, zero):
 def test_bench_self_launches_n_ranks(cuda, n):
     """``bench.py --gpus N`` with no torchrun: the parent spawns the N ranks itself (they share the
     one GPU here, so DP goes over IPC with sufficient factors), one JSON line, identical replicas."""
-    r = _bench(["--gpus", str(n), "--steps", "20", "--warmup", "5", "--min_warmup_ms", "50"], nproc=n,
-               self_launch=True)
+    r = _bench(["--gpus", str(n), "--steps", "20", "--warmup", "5", "--min_warmup_ms", "50", "--probe_steps", "40",
+                "--probe_warmup", "10"], nproc=n, self_launch=True)
     assert r["n_gpus"] == n and r["config"]["parallelism"] == f"dp{n}"
-    assert r["config"]["dp_transport"] == "ipc+sfb", r["config"]
     assert r["comm_world"] == n and len(r["devices"]) == n and r["replicas_identical"], r
     assert r["config"]["global_batch"] == 128 * n and r["value"] > 0
+    # the ranks probed all three DP schedules at this N and timed the fastest
+    sch = r["schedule"]
+    c = sch["candidates_ms_per_step"]
+    assert sch["source"] == "probe" and set(c) == {"sfb+zero", "sfb", "allreduce"}, sch
+    assert all(v > 0 for v in c.values()) and sch["chosen"] == min(c, key=c.get), sch
+    assert r["config"]["zero1_fc1"] == (sch["chosen"] == "sfb+zero")
+    assert r["config"]["dp_transport"] == ("ipc+sfb" if "sfb" in sch["chosen"] else "ipc"), r["config"]
 
 
 def test_bench_resnet_self_launch_two_ranks_is_real_dp(cuda):
     """bench_resnet.py --gpus 2 on one GPU: the IPC bucket reducer carries DP (not two independent
     replicas): both ranks end with bit-identical weights."""
     r = _bench(["--gpus", "2", "--depth", "18", "--batch_size", "8", "--image", "64", "--steps", "3", "--warmup", "1",
-                "--bucket_mb", "2"], nproc=2, script="bench_resnet.py", self_launch=True)
+                "--bucket_candidates", "0.5,2", "--probe_steps", "3", "--probe_warmup", "1"], nproc=2,
+               script="bench_resnet.py", self_launch=True)
     assert r["n_gpus"] == 2 and r["config"]["dp_transport"] == "ipc" and r["comm_world"] == 2
     assert r["replicas_identical"], r
+    bs = r["config"]["bucket_schedule"]
+    c = bs["candidates_ms_per_step"]
+    assert bs["source"] == "probe" and set(c) == {"0.5", "2"}, bs
+    assert r["config"]["bucket_mb"] == float(min(c, key=c.get))
 
 
-def test_bench_four_ranks_default_zero(cuda):
-    """From 4 ranks bench.py's default adds ZeRO-1 on top of the sufficient factors (the fc1 shard
-    all-gather rides the IPC staging)."""
-    r = _bench(["--gpus", "4", "--steps", "10", "--warmup", "3", "--min_warmup_ms", "50"], nproc=4)
+def test_bench_four_ranks_zero(cuda):
+    """4 ranks with ZeRO-1 on top of the sufficient factors (the fc1 shard all-gather rides the IPC
+    staging), under torchrun, schedule fixed by flag."""
+    r = _bench(["--gpus", "4", "--steps", "10", "--warmup", "3", "--min_warmup_ms", "50", "--schedule", "sfb+zero"],
+               nproc=4)
+    assert r["schedule"]["source"] == "flag" and r["schedule"]["chosen"] == "sfb+zero"
     assert r["config"]["zero1_fc1"] and r["config"]["dp_transport"] == "ipc+sfb" and r["n_gpus"] == 4
     assert r["value"] > 0 and r["config"]["global_batch"] == 512
     assert r["comm_world"] == 4 and r["replicas_identical"], r

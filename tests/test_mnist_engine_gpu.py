@@ -203,51 +203,6 @@ def test_local_bf16_fc_grads_match_fp32(cuda):
     assert torch.equal(engs[0].params_bf16(), engs[0].params().to(torch.bfloat16))
 
 
-def test_fc1_adam_in_dw_epilogue_matches_separate_pass(cuda):
-    """One GPU: the fc1 Adam update inside the fc1 dW epilogue (set_fc_adam, opt-in: fp32
-    gradient straight from the GEMM, bf16 fc1 shadow double-buffered by step parity) == the separate
-    Adam pass over an fp32 gradient buffer, to fp32 rounding; the shadow stays the bf16 of the
-    master across odd/even steps and after leaving the mode (set_fc_adam(False))."""
-    B = 128
-    params = M.flat_from_dict(M.init_params(19)).to(cuda) * 0.05
-    n = 1024
-    data = torch.rand(n, 784, device=cuda)
-    labels = torch.randint(0, 10, (n,), dtype=torch.int32, device=cuda)
-    perm = torch.randperm(n, device=cuda).to(torch.int32)
-    engs = []
-    s = torch.cuda.Stream()
-    with torch.cuda.stream(s):
-        for on in (True, False):
-            e = _engine(B, cuda, keep=0.75)
-            e.set_adam(0.01, 0.9, 0.999, 1e-8)
-            e.set_local_bf16_grads(0)
-            e.set_fc_adam(on)
-            e.params().copy_(params)
-            e.sync_shadow()
-            e.set_dataset(data, labels, perm)
-            e.set_input_mode(1)
-            engs.append(e)
-        for e in engs:
-            for _ in range(3):
-                e.train_step()
-    torch.cuda.synchronize()
-    assert engs[0].fc_adam_active() and not engs[1].fc_adam_active()
-    d0, d1 = engs[0].params() - params, engs[1].params() - params
-    assert _relerr(d0, d1) < 1e-4, _relerr(d0, d1)
-    for e in engs:
-        assert torch.equal(e.params_bf16(), e.params().to(torch.bfloat16))  # odd step: pbf_alt was live
-    with torch.cuda.stream(s):
-        r = [e.evaluate(data[:512], labels[:512]) for e in engs]
-        engs[0].set_fc_adam(False)
-        for e in engs:
-            e.train_step()
-    torch.cuda.synchronize()
-    assert torch.allclose(r[0], r[1], rtol=1e-3, atol=1e-3), r
-    d0, d1 = engs[0].params() - params, engs[1].params() - params
-    assert _relerr(d0, d1) < 1e-4, _relerr(d0, d1)
-    assert torch.equal(engs[0].params_bf16(), engs[0].params().to(torch.bfloat16))
-
-
 def _assert_same_regions(p0, p1, what):
     bad = {}
     for name, sl in (("conv1", slice(0, 832)), ("conv2", slice(832, M.BUCKET_SPLIT)),
@@ -322,38 +277,35 @@ def test_phase_timing_events_inside_graph(cuda):
         assert step < 5.0, ph  # ms
 
 
-def test_fused_conv12_forward_matches_oracle_and_two_kernel_path(cuda):
-    """conv1 fused into the conv2 kernel (bf16 MFMA, p1 computed into LDS) and the two-kernel path
-    (fp32 VALU conv1) each match the oracle that rounds their conv1 operands the same way."""
+def test_fused_conv12_forward_matches_oracle(cuda):
+    """conv1 fused into the conv2 kernel (bf16 MFMA, p1 computed into LDS) matches the fp32 oracle
+    that rounds its conv1 operands (x, W1) to bf16 the same way; so do the gradients."""
     B = 128
     params = {k: v * 0.05 for k, v in M.init_params(21).items()}
     x = torch.rand(B, 784)
     y = torch.randint(0, 10, (B,), dtype=torch.int32)
     s = torch.cuda.Stream()
-    for unfused in (0, 1):
-        with torch.cuda.stream(s):
-            e = _engine(B, cuda, keep=1.0)
-            e.set_conv_unfused(unfused)
-            e.params().copy_(M.flat_from_dict(params).to(cuda))
-            e.sync_shadow()
-            e.feed_x().copy_(x.to(cuda))
-            e.feed_y().copy_(y.to(cuda))
-            e.forward(True)
-            e.backward_a()
-            e.backward_b()
-        torch.cuda.synchronize()
-        r = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
-        x4 = x.reshape(-1, 28, 28, 1)
-        xin, w1 = (x4, params["wc1"]) if unfused else (r(x4), r(params["wc1"]))
-        p1 = r(M.maxpool_same_nhwc(torch.relu(M.conv2d_same_nhwc(xin, w1, params["bc1"])), 2))
-        got = e.pool1().float().cpu()
-        assert _relerr(got, p1) < 4e-3, (unfused, _relerr(got, p1))
-        p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
-        logits = M.conv_net(x, p, 1.0, emulate_bf16=True, bf16_conv1=not unfused)
-        torch.nn.functional.cross_entropy(logits, y.long()).backward()
-        g = M.dict_from_flat(e.grads().cpu())
-        for k in p:
-            assert _relerr(g[k], p[k].grad) < 3e-2, (unfused, k, _relerr(g[k], p[k].grad))
+    with torch.cuda.stream(s):
+        e = _engine(B, cuda, keep=1.0)
+        e.params().copy_(M.flat_from_dict(params).to(cuda))
+        e.sync_shadow()
+        e.feed_x().copy_(x.to(cuda))
+        e.feed_y().copy_(y.to(cuda))
+        e.forward(True)
+        e.backward_a()
+        e.backward_b()
+    torch.cuda.synchronize()
+    r = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
+    x4 = x.reshape(-1, 28, 28, 1)
+    p1 = r(M.maxpool_same_nhwc(torch.relu(M.conv2d_same_nhwc(r(x4), r(params["wc1"]), params["bc1"])), 2))
+    got = e.pool1().float().cpu()
+    assert _relerr(got, p1) < 4e-3, _relerr(got, p1)
+    p = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    logits = M.conv_net(x, p, 1.0, emulate_bf16=True, bf16_conv1=True)
+    torch.nn.functional.cross_entropy(logits, y.long()).backward()
+    g = M.dict_from_flat(e.grads().cpu())
+    for k in p:
+        assert _relerr(g[k], p[k].grad) < 3e-2, (k, _relerr(g[k], p[k].grad))
 
 
 def test_device_dataset_rows_equal_host_gathered_batches(cuda):

@@ -9,7 +9,7 @@ The kernel-side explanation that fits that signature is a packed instruction rea
 half that nothing in the kernel wrote: its value would be whatever the previous wave on that SIMD
 left, stable when every wave is this kernel, different when other processes' waves run between.
 This test rules it out in the code object: it compiles the kernels with packed fp32 ops, builds
-the control-flow graph of ``conv1_pool_fwd`` (and of the SLP-vectorised ``head_kernel``) and runs
+the control-flow graph of the SLP-vectorised ``head_kernel`` (the VALU ``conv1_pool_fwd`` is gone) and runs
 a must-be-written dataflow over the VGPRs (a packed operand counts only the halves its
 ``op_sel``/``op_sel_hi`` select). No path reads a VGPR before writing it, and the kernel's LDS
 use is barrier-separated (stage -> __syncthreads -> read, no LDS reuse), so the divergence is
@@ -150,14 +150,19 @@ def packed_asm(tmp_path_factory):
                           capture_output=True, text=True).stdout
 
 
-@pytest.mark.parametrize("kernel", ["conv1_pool_fwd", "head_kernel"])
-def test_packed_build_reads_no_unwritten_vgpr(packed_asm, kernel):
-    func = next(m for m in re.findall(r"^[0-9a-f]+ <(.+)>:$", packed_asm, re.M) if kernel in m)
+def test_packed_build_reads_no_unwritten_vgpr(packed_asm):
+    """The SLP-vectorised head kernel in the packed build (the VALU conv1 kernel that showed the
+    divergence was replaced in round 4 by conv1 on the matrix core inside conv12_fwd_lds, whose
+    packed build has no packed FMAs). The dataflow model covers VALU / LDS / flat-global
+    instructions, which is what these two kernels are made of -- not the buffer-load GEMM cores."""
+    func = next(m for m in re.findall(r"^[0-9a-f]+ <(.+)>:$", packed_asm, re.M) if "head_kernel" in m)
     ins = _parse(packed_asm, func)
     assert len(ins) > 200
     assert any(c.startswith("v_pk_fma_f32") for _, c, _ in ins), "expected packed fp32 FMAs in this build"
     bad = maybe_uninitialised_reads(ins)
     assert not bad, [f"{a:x} v{r}: {c}" for a, r, c in bad[:10]]
+    conv12 = next(m for m in re.findall(r"^[0-9a-f]+ <(.+)>:$", packed_asm, re.M) if "conv12_fwd_lds" in m)
+    assert not any(c.startswith("v_pk_fma_f32") for _, c, _ in _parse(packed_asm, conv12))
 
 
 def test_analysis_flags_an_unwritten_packed_half():

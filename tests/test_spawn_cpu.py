@@ -36,6 +36,11 @@ def test_bench_self_launch_parent_stays_gpu_clean():
     assert len(lines) == 1, p.stdout
     r = json.loads(lines[0])
     assert r["n_ranks"] == 2 and r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 256
+    # the ranks probed both CPU schedules (the parent above still never imported torch) and kept the
+    # faster one; the replicas agree after the timed steps
+    c = r["schedule"]["candidates_ms_per_step"]
+    assert set(c) == {"flat", "buckets"} and r["schedule"]["chosen"] == min(c, key=c.get)
+    assert r["replicas_identical"]
 
 
 def test_bench_refuses_wrong_world():
@@ -77,3 +82,45 @@ def test_spawn_relays_rank0_stdout_only(tmp_path):
     assert p.returncode == 0, p.stderr
     assert p.stdout.strip() == "LINE 0 0"
     assert "LINE 1 1" in p.stderr
+
+
+def test_schedule_pick_takes_max_over_ranks_and_fastest():
+    """probe() reports each candidate's MAX over ranks (a step is as slow as its slowest rank) and
+    pick() the fastest of those; a failing candidate is +inf, never chosen; all failing raises."""
+    import math
+
+    import pytest
+
+    sys.path.insert(0, ROOT)
+    from tensorflow_distributed_amd.parallel import schedule as S
+
+    local = {"a": 1.0, "b": 2.0, "c": 0.5}
+    other_rank = {"a": 3.0, "b": 2.5, "c": 9.0}  # rank 1 is slow on c
+    order = ["a", "b", "c"]
+    got = S.probe(order, lambda n: local[n], lambda x, it=iter(order): max(x, other_rank[next(it)]))
+    assert got == {"a": 3.0, "b": 2.5, "c": 9.0} and S.pick(got) == "b"
+
+    def flaky(n):
+        if n == "x":
+            raise RuntimeError("capture failed")
+        return 4.0
+    got = S.probe(["x", "y"], flaky, lambda v: v)
+    assert math.isinf(got["x"]) and S.pick(got) == "y"
+    assert S.pick({"p": 1.0, "q": 1.0}) == "p"  # ties: probe order
+    with pytest.raises(RuntimeError):
+        S.pick({"x": math.inf})
+
+
+def test_bench_schedule_flags_resolve():
+    """--schedule NAME and the --fc_sfb/--zero overrides fix the schedule without probes; a one-GPU
+    job without --force_dp has no DP schedule at all."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    a = bench._args(["--gpus", "4"])
+    assert bench._candidates(a, True) == (list(bench.SCHEDULES), "probe")
+    assert bench._candidates(a, False) == ([None], "single")
+    assert bench._candidates(bench._args(["--schedule", "sfb"]), True) == (["sfb"], "flag")
+    assert bench._candidates(bench._args(["--fc_sfb", "0", "--zero", "0"]), True) == (["allreduce"], "flag")
+    assert bench._candidates(bench._args(["--fc_sfb", "1", "--zero", "1"]), True) == (["sfb+zero"], "flag")
+    assert bench._candidates(bench._args(["--candidates", "sfb,allreduce"]), True) == (["sfb", "allreduce"], "probe")
