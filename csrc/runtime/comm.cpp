@@ -3,6 +3,8 @@
 #include <c10/hip/HIPStream.h>
 #include <c10/util/Exception.h>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 namespace tfd {
 
@@ -51,11 +53,42 @@ RcclComm::RcclComm(const at::Tensor& uid, int64_t world, int64_t rank, int64_t d
   rccl_check(ncclCommInitRank(&comm_, (int)world, id, (int)rank), "CommInitRank");
 }
 
+// A collective captured into a hipGraph stays tied to its communicator's resources until that
+// graph is destroyed, and Python frees a job's objects in no fixed order: a communicator dropped
+// before a graph that captured it (a test's locals, a model rebuilt between bucket-size probes)
+// left the later graph teardown / replay working on a destroyed communicator -- the in-suite
+// segfault inside CUDAGraph.replay of round 3 (profiles/pytest_gpu_r3_segv.log). The destructor
+// therefore only retires the handle; retired communicators are destroyed by reap(), which a caller
+// runs once no graph that captured them exists (or never: the process exit releases them).
+namespace {
+std::mutex g_retired_mu;
+std::vector<ncclComm_t>& retired() {
+  static auto* v = new std::vector<ncclComm_t>();  // intentionally never destroyed (exit order)
+  return *v;
+}
+}  // namespace
+
 RcclComm::~RcclComm() {
   if (comm_) {
-    ncclCommDestroy(comm_);
+    std::lock_guard<std::mutex> g(g_retired_mu);
+    retired().push_back(comm_);
     comm_ = nullptr;
   }
+}
+
+int64_t RcclComm::reap() {
+  std::vector<ncclComm_t> v;
+  {
+    std::lock_guard<std::mutex> g(g_retired_mu);
+    v.swap(retired());
+  }
+  for (auto c : v) ncclCommDestroy(c);
+  return (int64_t)v.size();
+}
+
+int64_t RcclComm::retired_count() {
+  std::lock_guard<std::mutex> g(g_retired_mu);
+  return (int64_t)retired().size();
 }
 
 void RcclComm::abort() {

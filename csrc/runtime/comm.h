@@ -19,8 +19,11 @@ class RcclComm : public torch::CustomClassHolder {
  public:
   // uid: 128-byte ncclUniqueId produced by unique_id() on rank 0 and distributed via the store.
   RcclComm(const at::Tensor& uid, int64_t world, int64_t rank, int64_t device);
-  ~RcclComm() override;
+  ~RcclComm() override;  // retires the handle (see comm.cpp): ncclCommDestroy happens in reap()
   static at::Tensor unique_id();
+  // destroy every retired communicator; only when no captured graph that used one is still alive
+  static int64_t reap();
+  static int64_t retired_count();
 
   int64_t world() const { return world_; }
   int64_t rank() const { return rank_; }

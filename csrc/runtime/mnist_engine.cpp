@@ -1170,6 +1170,8 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.class_<RcclComm>("RcclComm")
       .def(torch::init<at::Tensor, int64_t, int64_t, int64_t>())
       .def_static("unique_id", &RcclComm::unique_id)
+      .def_static("reap", &RcclComm::reap)
+      .def_static("retired_count", &RcclComm::retired_count)
       .def("world", &RcclComm::world)
       .def("rank", &RcclComm::rank)
       .def("all_reduce", &RcclComm::all_reduce)

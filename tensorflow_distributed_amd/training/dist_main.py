@@ -129,6 +129,49 @@ def _make_optimizer():
     return AdamOptimizer(FLAGS.learning_rate)
 
 
+def host_identity() -> str:
+    """This machine as far as IPC peer memory is concerned: hostname + kernel boot id."""
+    import socket
+
+    boot = ""
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        pass
+    return f"{socket.gethostname()}|{boot}"
+
+
+def gpu_ps_capable() -> bool:
+    """This task could run its side of the GPU-resident PS (flags + a visible GPU)."""
+    return bool(FLAGS.ps_on_gpu and FLAGS.num_gpus > 0 and FLAGS.model == "mnist_cnn" and torch.cuda.is_available())
+
+
+def agree_gpu_ps(capable: bool, host: str, group=None):
+    """All-gather (host identity, capable) over every ps and worker task of ``group``. Returns
+    (use the GPU-resident PS, reason if not): yes only if every task is capable and all share one
+    host; otherwise every task falls back to the host parameter server -- the same answer on all."""
+    import torch.distributed as dist
+
+    rows = [(host, bool(capable))]
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        rows = [None] * dist.get_world_size(group)
+        dist.all_gather_object(rows, (host, bool(capable)), group=group)
+    if len({h for h, _ in rows}) > 1:
+        return False, "tasks on different hosts"
+    if not all(c for _, c in rows):
+        return False, "a task without a GPU or with --ps_on_gpu=False"
+    return True, ""
+
+
+def _agree_gpu_ps() -> bool:
+    ok, why = agree_gpu_ps(gpu_ps_capable(), host_identity())
+    if FLAGS.ps_on_gpu and not ok:
+        print("%s %d: --ps_on_gpu needs every task on one host with a GPU (%s); using the host parameter server"
+              % (FLAGS.job_name, FLAGS.task_index, why))
+    return ok
+
+
 def _resnet_worker(server, cluster, num_workers: int, is_chief: bool) -> int:
     """``--model resnet18|resnet50``: the same cluster roles and stdout, training the synthetic-
     ImageNet ResNet family (BASELINE configs 4-5) with synchronous DP -- bucketed bf16 gradient
@@ -245,11 +288,16 @@ def main(argv=None) -> int:
     backup_ps = sync and r2a < num_workers and layout is not None
     ps_mode = (not sync) or backup_ps
 
+    # GPU-resident PS only when EVERY task (ps and worker) can take part: same host (the data path is
+    # IPC peer memory) and a GPU on each. Decided collectively so the PS and the workers never pick
+    # different protocols (the reference's default cluster spans three hosts, mnist_python_m.py:81-84).
+    use_gpu_ps = ps_mode and _agree_gpu_ps()
+
     if FLAGS.job_name == "ps":
         # (reference quirk Q9: ps + existing_servers fell through to the worker code; a PS here
         #  always serves and then exits once every worker has finished)
         service = None
-        if ps_mode and FLAGS.ps_on_gpu and FLAGS.num_gpus > 0 and FLAGS.model == "mnist_cnn":
+        if use_gpu_ps:
             from ..parallel.gpu_ps import GpuParameterServerService
 
             ps_gpu = FLAGS.task_index % FLAGS.num_gpus
@@ -309,7 +357,7 @@ def main(argv=None) -> int:
         runner.load_flat(flat, {}, 0)
 
     client = None
-    gpu_ps = ps_mode and FLAGS.ps_on_gpu and device.type == "cuda"
+    gpu_ps = use_gpu_ps
     if not ps_mode:
         def broadcast_fn():
             if num_workers > 1:

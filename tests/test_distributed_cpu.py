@@ -267,3 +267,22 @@ def test_sufficient_factor_fc_gradients_equal_the_all_reduce(world):
     for out in res:
         for k, (ar, sfb) in out.items():
             torch.testing.assert_close(sfb, ar, rtol=1e-4, atol=1e-5, msg=k)
+
+
+def _gpu_ps_vote(rank, world, hosts, capable):
+    from tensorflow_distributed_amd.training.dist_main import agree_gpu_ps
+
+    return agree_gpu_ps(capable[rank], hosts[rank])
+
+
+def test_gpu_ps_use_is_decided_collectively():
+    """the GPU-resident PS (IPC peer memory) is used only when every ps and worker task
+    is on one host and has a GPU; every task gets the same answer (no PS serving one protocol while
+    a worker speaks the other)."""
+    same, split = ["h|1"] * 3, ["h|1", "h|1", "other|2"]
+    for hosts, capable, want in ((same, [True] * 3, True), (split, [True] * 3, False),
+                                 (same, [True, False, True], False)):
+        res = run_ranks(_gpu_ps_vote, 3, hosts, capable)
+        assert [ok for ok, _ in res] == [want] * 3, (hosts, capable, res)
+        if not want:
+            assert len({why for _, why in res}) == 1 and res[0][1]

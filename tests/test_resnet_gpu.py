@@ -247,14 +247,44 @@ def test_resnet_rccl_bucketed_world1_equals_no_comm(cuda, bf16):
     step bit for bit -- with the bf16 wire, the one whose optimizer reads bf16-rounded gradients (a
     bucket cast before its last gradient landed would show up here).
 
-    Runs in a fresh process: in the full suite's single process, after the earlier tests' RCCL
-    communicators and captured graphs, RCCL's graph replay here segfaulted (the test alone and its
-    file pass, profiles/pytest_gpu_r3_segv.log); a fresh process is the state a training job has."""
-    from dist_util import run_ranks
-
-    (n_bad, names, finite), = run_ranks(_rccl_bucketed_worker, 1, bf16, timeout=240)
+    Runs in the suite's process again (round 3 moved it to a fresh one after an in-suite segfault in
+    CUDAGraph.replay): RcclComm's destructor no longer destroys a communicator that an earlier
+    test's still-alive captured graph used (see test_rccl_comm_outlives_its_python_object)."""
+    n_bad, names, finite = _rccl_bucketed_worker(0, 1, bf16)
     assert finite
     assert n_bad == 0, f"{n_bad} parameters differ (first in {names})"
+
+
+def test_rccl_comm_outlives_its_python_object(cuda):
+    """A graph that captured collectives stays replayable after the Python RcclComm (and the model
+    holding it) is gone: the destructor only retires the handle; reap() destroys it once the graph
+    is gone too."""
+    from tensorflow_distributed_amd.models.resnet import ResNet
+
+    comm = torch.classes.tfd.RcclComm(torch.classes.tfd.RcclComm.unique_id(), 1, 0, cuda.index)
+    before = torch.classes.tfd.RcclComm.retired_count()
+    m = ResNet(18, num_classes=16, device=cuda, seed=5, width=16)
+    m.set_comm(comm, bucket_mb=0.05, bf16_grads=True, force_dp=True)
+    x = torch.randn(4, 32, 32, 3, device=cuda)
+    lab = torch.randint(0, 16, (4,), dtype=torch.int32, device=cuda)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        m.train_step(x, lab, lr=0.01)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = m.train_step(x, lab, lr=0.01)
+    master = m.fp.master
+    del m, comm
+    assert torch.classes.tfd.RcclComm.retired_count() == before + 1
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all() and torch.isfinite(master).all()
+    del g, out
+    torch.cuda.synchronize()
+    assert torch.classes.tfd.RcclComm.reap() >= 1 and torch.classes.tfd.RcclComm.retired_count() == 0
 
 
 @pytest.mark.parametrize("depth", [18, 50])
