@@ -131,6 +131,15 @@ void conv2d_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, int6
   conv_wgrad(c, bp(x), bp(dy), fp(dw), conv_wgrad_splits(c), cur(), zeroed);
 }
 
+at::Tensor gemm_nt_op(const at::Tensor& a, const at::Tensor& bt) {
+  check_bf16(a, "a", 2);
+  check_bf16(bt, "bt", 2);
+  TORCH_CHECK(a.size(1) == bt.size(1) && a.size(1) % 8 == 0 && bt.size(0) % 8 == 0, "gemm_nt: shapes / multiples of 8");
+  auto c = at::empty({a.size(0), bt.size(0)}, a.options());
+  gemm_nt_bf16(bp(a), bp(bt), bp(c), (int)a.size(0), (int)bt.size(0), (int)a.size(1), cur());
+  return c;
+}
+
 at::Tensor linear_fwd_op(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias) {
   check_bf16(x, "x", 2);
   check_bf16(w, "w", 2);
@@ -317,6 +326,8 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.impl("conv2d_dgrad_bn", c10::DispatchKey::CUDA, &conv2d_dgrad_bn);
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad, bool zeroed=False) -> ()");
   m.impl("conv2d_wgrad", c10::DispatchKey::CUDA, &conv2d_wgrad);
+  m.def("gemm_nt(Tensor a, Tensor bt) -> Tensor");
+  m.impl("gemm_nt", c10::DispatchKey::CUDA, &gemm_nt_op);
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias) -> Tensor");
   m.impl("linear_fwd", c10::DispatchKey::CUDA, &linear_fwd_op);
   m.def("linear_dgrad(Tensor dy, Tensor w) -> Tensor");

@@ -53,6 +53,8 @@ void linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, float* 
                 hipStream_t st);
 void linear_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int Kin, int N, hipStream_t st);
 void linear_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int Kin, int N, hipStream_t st);
+// C[M][N] bf16 = A[M][K] . Bt[N][K]^T on the 256 x 256 core (csrc/kernels/gemm256.hip)
+void gemm_nt_bf16(const uint16_t* a, const uint16_t* bt, uint16_t* c, int M, int N, int K, hipStream_t st);
 
 // ---- batch norm (training mode, per-channel over the M = N*H*W rows of a [M][C] bf16 tensor) ----
 // partials: fp32 workspace of bn_partials_size(M, C) floats.

@@ -221,3 +221,15 @@ def test_softmax_xent_and_pad(cuda):
     x = torch.randn(2, 4, 4, 3)
     p = ops.pad_channels(x.to(cuda), 8)
     assert p.shape == (2, 4, 4, 8) and torch.equal(p.cpu()[..., :3].float(), rb(x)) and p[..., 3:].abs().sum() == 0
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 264, 72), (1000, 520, 1032), (513, 2048, 576)])
+def test_gemm256_nt_matches_fp32(cuda, M, N, K):
+    """The 256 x 256 core (buffer-load-to-LDS staging, 32x32x16 MFMA, XCD-grouped tiles): C = A Bt^T
+    against an fp32 reference of the same bf16 operands, ragged M / N / K tails included."""
+    g = torch.Generator(device=cuda).manual_seed(M + N + K)
+    A = (torch.rand(M, K, device=cuda, generator=g) * 2 - 1).bfloat16()
+    Bt = (torch.rand(N, K, device=cuda, generator=g) * 2 - 1).bfloat16()
+    C = torch.ops.tfd.gemm_nt(A, Bt).float()
+    ref = A.float() @ Bt.float().t()
+    torch.testing.assert_close(C, ref.bfloat16().float(), rtol=1e-2, atol=1e-2 * ref.abs().max().item())
