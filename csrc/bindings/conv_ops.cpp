@@ -326,6 +326,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.impl("conv2d_dgrad_bn", c10::DispatchKey::CUDA, &conv2d_dgrad_bn);
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad, bool zeroed=False) -> ()");
   m.impl("conv2d_wgrad", c10::DispatchKey::CUDA, &conv2d_wgrad);
+  m.def("conv_gemm_core(int mode) -> int", [](int64_t mode) -> int64_t { return conv_gemm_core((int)mode); });
   m.def("gemm_nt(Tensor a, Tensor bt) -> Tensor");
   m.impl("gemm_nt", c10::DispatchKey::CUDA, &gemm_nt_op);
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias) -> Tensor");

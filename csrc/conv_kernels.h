@@ -53,6 +53,10 @@ void linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, float* 
                 hipStream_t st);
 void linear_dgrad(const uint16_t* dy, const uint16_t* w, uint16_t* dx, int M, int Kin, int N, hipStream_t st);
 void linear_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int Kin, int N, hipStream_t st);
+// GEMM core of the conv ops: 0 = the 128-row core, 1 = the 256-row core where its tiles fill the
+// chip (default; env TFD_G256 at the first call), 2 = the 256-row core wherever it applies. Returns the
+// previous mode; -1 only queries. (A/B switch for tests and the per-layer probe.)
+int conv_gemm_core(int mode);
 // C[M][N] bf16 = A[M][K] . Bt[N][K]^T on the 256 x 256 core (csrc/kernels/gemm256.hip)
 void gemm_nt_bf16(const uint16_t* a, const uint16_t* bt, uint16_t* c, int M, int N, int K, hipStream_t st);
 

@@ -12,12 +12,14 @@
 // All index math on the loaders' hot path uses multiply-shift division (FastDiv) by runtime
 // constants. C and K must be multiples of 8 (16-B chunks); the 3-channel stem input is padded to 8.
 // 1x1 / stride-1 / pad-0 convolutions are plain GEMMs and take the dense loaders.
+#include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
 
 #include "../common.h"
 #include "../conv_kernels.h"
 #include "../gemm.h"
+#include "../gemm256.h"
 #include "../bn_totals.h"
 
 namespace tfd {
@@ -57,17 +59,29 @@ struct Geo {
 
 // Row-major X[rows][ld] bf16 with whole 16-B chunks (lims and ld multiples of 8; host-checked):
 //  KC=true : (mn, k) = X[mn][k];  KC=false: (mn, k) = X[k][mn]
+// Every loader also exposes rsrc() + off(mn, k) (byte offset of the chunk, or past the range): the
+// 256-row core (csrc/gemm256.h) DMAs the same chunks straight into LDS.
+__device__ __forceinline__ uint4 rsrc_ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const i32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
+}
+__device__ __forceinline__ uint32_t boff(uint32_t elem, bool ok) { return ok ? elem * 2u : kBufOOB; }
+#define TFD_LOADER_CALL                                                                        \
+  __device__ __forceinline__ uint4 operator()(int mn, int k) const { return rsrc_ld(rsrc(), off(mn, k)); }
+
 template <bool KC_>
 struct DenseX {
   static constexpr bool KC = KC_;
   const uint16_t* __restrict__ x;
   int ld, mn_lim, k_lim;
-  __device__ __forceinline__ uint4 operator()(int mn, int k) const {
-    const bool ok = mn < mn_lim && k < k_lim;
-    const uint32_t nb = (uint32_t)(KC ? mn_lim : k_lim) * (uint32_t)ld * 2u;
-    if constexpr (KC) return buf_ld(x, nb, (uint32_t)mn * ld + k, ok);
-    else return buf_ld(x, nb, (uint32_t)k * ld + mn, ok);
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
+    return make_rsrc(x, (uint32_t)(KC ? mn_lim : k_lim) * (uint32_t)ld * 2u);
   }
+  __device__ __forceinline__ uint32_t off(int mn, int k) const {
+    const bool ok = mn < mn_lim && k < k_lim;
+    return boff(KC ? (uint32_t)mn * ld + k : (uint32_t)k * ld + mn, ok);
+  }
+  TFD_LOADER_CALL
 };
 
 // ---- forward: A = im2col(X) (KC), B = W [KD][K] (not KC) ----
@@ -75,13 +89,15 @@ struct FwdA {
   static constexpr bool KC = true;
   const uint16_t* __restrict__ x;
   Geo g;
-  __device__ __forceinline__ uint4 operator()(int m, int k) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return make_rsrc(x, g.xbytes); }
+  __device__ __forceinline__ uint32_t off(int m, int k) const {
     const int n = g.howo.div(m), r1 = m - n * g.Ho * g.Wo, ho = g.wo.div(r1), wo = r1 - ho * g.Wo;
     const int tap = g.c.div(k), c = k - tap * g.C, r = g.s.div(tap), s = tap - r * g.S;
     const int h = ho * g.st - g.pad + r, w = wo * g.st - g.pad + s;
     const bool ok = m < g.M && k < g.KD && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-    return buf_ld(x, g.xbytes, (uint32_t)((n * g.H + h) * g.W + w) * g.C + c, ok);
+    return boff((uint32_t)((n * g.H + h) * g.W + w) * g.C + c, ok);
   }
+  TFD_LOADER_CALL
 };
 
 // ---- dgrad: A = "col2im" gather of dY (KC), B = W as [C][(r,s,k)] (KC) ----
@@ -89,7 +105,9 @@ struct DgradA {
   static constexpr bool KC = true;
   const uint16_t* __restrict__ dy;
   Geo g;  // M = N*H*W, KD = R*S*K
-  __device__ __forceinline__ uint4 operator()(int m, int kk) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return make_rsrc(dy, g.ybytes); }
+  TFD_LOADER_CALL
+  __device__ __forceinline__ uint32_t off(int m, int kk) const {
     const int n = g.hw.div(m), r1 = m - n * g.H * g.W, h = g.w.div(r1), w = r1 - h * g.W;
     const int tap = g.k.div(kk), k = kk - tap * g.K, r = g.s.div(tap), s = tap - r * g.S;
     const int hn = h + g.pad - r, wn = w + g.pad - s;
@@ -101,17 +119,19 @@ struct DgradA {
       ok = ok && ho * g.st == hn && wo * g.st == wn;
     }
     ok = ok && ho < g.Ho && wo < g.Wo;
-    return buf_ld(dy, g.ybytes, (uint32_t)((n * g.Ho + ho) * g.Wo + wo) * g.K + k, ok);
+    return boff((uint32_t)((n * g.Ho + ho) * g.Wo + wo) * g.K + k, ok);
   }
 };
 struct DgradB {
   static constexpr bool KC = true;
   const uint16_t* __restrict__ w;
   Geo g;
-  __device__ __forceinline__ uint4 operator()(int c, int kk) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return make_rsrc(w, g.wbytes); }
+  __device__ __forceinline__ uint32_t off(int c, int kk) const {
     const int tap = g.k.div(kk), k = kk - tap * g.K;
-    return buf_ld(w, g.wbytes, (uint32_t)(tap * g.C + c) * g.K + k, c < g.C && kk < g.KD);
+    return boff((uint32_t)(tap * g.C + c) * g.K + k, c < g.C && kk < g.KD);
   }
+  TFD_LOADER_CALL
 };
 
 // ---- strided dgrad, one output phase (h % st, w % st) at a time ----
@@ -130,24 +150,28 @@ struct DgradPhaseA {
   static constexpr bool KC = true;
   const uint16_t* __restrict__ dy;
   PhaseGeo g;
-  __device__ __forceinline__ uint4 operator()(int m, int kk) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return make_rsrc(dy, g.ybytes); }
+  __device__ __forceinline__ uint32_t off(int m, int kk) const {
     const int n = g.hpwp.div(m), r1 = m - n * g.Hp * g.Wp, hh = g.wp.div(r1), ww = r1 - hh * g.Wp;
     const int t = g.k.div(kk), k = kk - t * g.K, i = g.nsd.div(t), j = t - i * g.ns;
     const int ho = hh + g.dh - i, wo = ww + g.dw - j;
     const bool ok = m < g.M && kk < g.KD && (unsigned)ho < (unsigned)g.Ho && (unsigned)wo < (unsigned)g.Wo;
-    return buf_ld(dy, g.ybytes, (uint32_t)((n * g.Ho + ho) * g.Wo + wo) * g.K + k, ok);
+    return boff((uint32_t)((n * g.Ho + ho) * g.Wo + wo) * g.K + k, ok);
   }
+  TFD_LOADER_CALL
 };
 struct DgradPhaseB {  // (c, kk) -> W[r][s][c][k], S = filter width
   static constexpr bool KC = true;
   const uint16_t* __restrict__ w;
   PhaseGeo g;
   int S;
-  __device__ __forceinline__ uint4 operator()(int c, int kk) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return make_rsrc(w, g.wbytes); }
+  __device__ __forceinline__ uint32_t off(int c, int kk) const {
     const int t = g.k.div(kk), k = kk - t * g.K, i = g.nsd.div(t), j = t - i * g.ns;
     const int r = g.r0 + i * g.st, s = g.s0 + j * g.st;
-    return buf_ld(w, g.wbytes, (uint32_t)((r * S + s) * g.C + c) * g.K + k, c < g.C && kk < g.KD);
+    return boff((uint32_t)((r * S + s) * g.C + c) * g.K + k, c < g.C && kk < g.KD);
   }
+  TFD_LOADER_CALL
 };
 struct PhaseRows {  // phase GEMM row -> pixel row of dX
   PhaseGeo g;
@@ -163,13 +187,15 @@ struct WgradA {
   static constexpr bool KC = false;
   const uint16_t* __restrict__ x;
   Geo g;  // M = R*S*C rows (taps), KD = N*Ho*Wo pixels
-  __device__ __forceinline__ uint4 operator()(int t, int m) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return make_rsrc(x, g.xbytes); }
+  __device__ __forceinline__ uint32_t off(int t, int m) const {
     const int tap = g.c.div(t), c = t - tap * g.C, r = g.s.div(tap), s = tap - r * g.S;
     const int n = g.howo.div(m), r1 = m - n * g.Ho * g.Wo, ho = g.wo.div(r1), wo = r1 - ho * g.Wo;
     const int h = ho * g.st - g.pad + r, w = wo * g.st - g.pad + s;
     const bool ok = t < g.M && m < g.KD && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-    return buf_ld(x, g.xbytes, (uint32_t)((n * g.H + h) * g.W + w) * g.C + c, ok);
+    return boff((uint32_t)((n * g.H + h) * g.W + w) * g.C + c, ok);
   }
+  TFD_LOADER_CALL
 };
 
 // ---- epilogues ----
@@ -716,12 +742,286 @@ Geo make_geo(const ConvShape& c, int M, int KD) {
 
 bool is_pointwise(const ConvShape& c) { return c.R == 1 && c.S == 1 && c.stride == 1 && c.pad == 0; }
 
+// ---------------- the conv GEMMs on the 256-row core (csrc/gemm256.h) ----------------
+// Block tile 256 x BN (BN = 256 / 128 / 64 by the output width), 8 waves, 32x32x16 MFMA, operands
+// DMA'd into LDS through the same loaders (their off() / rsrc()). Forward: A = im2col(X) (KC), B = the
+// HWIO weight (MNC, transposed fragment reads); dgrad: A = dY gather, B = W as [C][(r,s,k)] (both KC);
+// weight gradient: A = im2col(X)^T, B = dY (both MNC). TFD_G256 (read at the first launch): 0 = the
+// 128-row core everywhere, 1 (default) = this core where its tiles fill the chip, 2 = wherever it
+// applies -- the switch the per-layer A/B (scripts/debug/gemm_probe.py) runs on.
+int g256_mode_v = -1;
+int g256_mode() {
+  if (g256_mode_v < 0) {
+    const char* e = std::getenv("TFD_G256");
+    g256_mode_v = e ? std::atoi(e) : 1;
+  }
+  return g256_mode_v;
+}
+int g256_bn(int N) { return N >= 256 ? 256 : (N >= 128 ? 128 : 64); }
+long g256_tiles(int M, int N) { return (long)((M + 255) / 256) * ((N + g256_bn(N) - 1) / g256_bn(N)); }
+// Mode 1 takes the 256-row core only where the per-layer A/B measured it faster
+// (profiles/gemm256_conv_layers_r4.txt): bf16-output GEMMs (forward, dgrad) with >= 1024 output
+// channels -- e.g. ResNet-50 l3 1x1 256->1024 forward 30.8 vs 33.8 us, l4 1x1 2048->512 dgrad 22.7 vs
+// 26.9. Narrower outputs (fewer, 256-row tiles for the chip; one 8-wave block per CU instead of 3-4
+// 4-wave blocks hiding each other's latency on these short-K, often memory-bound layers) and every
+// weight gradient measured slower there; ResNet-50 b128 13.65 ms/step with the 128-row core
+// everywhere, 14.37 with the 256-row core wherever it had >= 256 tiles, 19.6 with it everywhere.
+bool use_g256(int M, int N) {
+  const int mode = g256_mode();
+  if (mode == 0 || N % 8 || bn_totals_enabled()) return false;
+  return mode == 2 || (N >= 1024 && g256_tiles(M, N) >= 32);
+}
+
+template <int BN> struct G256WM { static constexpr int v = BN == 256 ? 2 : 4; };
+
+// bf16 epilogue of a 256 x BN tile, in two 128-row halves through an fp32 LDS image (pitch BN + 8:
+// the two row groups of an accumulator register write land 32 banks apart): each thread then owns
+// whole 8-column chunks -- residual chunks loaded as 16-B buffer loads before the half is staged, one
+// 16-B store per output chunk, the sum v + add formed in fp32 and rounded once. STATS: per-column sums
+// / sums of squares of the stored bf16 values; BnB (BS::MODE >= 0): the BN-backward sums of the stored
+// gradient (see lds_epilogue). Both halves accumulate in registers; one partial row per tile at part.
+template <int BN>
+struct G256Epi {
+  static constexpr int PITCH = BN + 8, CPR = BN / 8, RG = 512 / CPR, CH = 128 / RG;
+  static constexpr int BYTES = 128 * PITCH * 4;
+  static_assert(2 * RG * BN * 4 <= BYTES, "stats reduction fits");
+};
+template <class C, bool ADD, bool STATS, class RM, class BS>
+__device__ __forceinline__ void g256_epilogue(f32x16 (&acc)[C::TM][C::TN], char* smem, uint16_t* __restrict__ y,
+                                              const uint16_t* __restrict__ add, int M, int N, int m0, int n0,
+                                              float* __restrict__ part, RM rowmap, uint32_t ybytes, BS bs) {
+  using E = G256Epi<C::BN>;
+  constexpr bool BSTAT = BS::MODE >= 0;
+  static_assert(!(STATS && BSTAT), "one statistics kind per epilogue");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w / C::WN, wn = w % C::WN;
+  const int cc = tid % E::CPR, g0 = tid / E::CPR, n = n0 + cc * 8;
+  const int my_half = (wm * C::WTM) >> 7;
+  if (ybytes == 0) ybytes = (uint32_t)M * (uint32_t)N * 2u;
+  float s[8], sq[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s[k] = 0.f; sq[k] = 0.f; }
+  [[maybe_unused]] float bmu[8], bis[8], bsc[8], bsh[8];
+  if constexpr (BSTAT) {
+    const int nc = n < N ? n : 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bmu[k] = bs.mean[nc + k];
+      bis[k] = bs.invstd[nc + k];
+      if constexpr (BS::MODE == 2) {
+        bsc[k] = bis[k] * bs.gamma[nc + k];
+        bsh[k] = bs.beta[nc + k] - bmu[k] * bsc[k];
+      }
+    }
+  }
+  float* cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int mb = m0 + 128 * h;
+    uint32_t orow[E::CH];
+    [[maybe_unused]] uint4 q[E::CH], yq[E::CH];
+    [[maybe_unused]] uint32_t mbits[E::CH];
+#pragma unroll
+    for (int c = 0; c < E::CH; ++c) {
+      const int m = mb + g0 + c * E::RG;
+      orow[c] = rowmap(m);
+      const bool ok = m < M && n < N;
+      if constexpr (ADD) q[c] = buf_ld(add, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, ok);
+      if constexpr (BSTAT) {
+        yq[c] = buf_ld(bs.y, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, ok);
+        if constexpr (BS::MODE == 3) mbits[c] = ok ? bs.bits[(size_t)orow[c] * (N / 8) + n / 8] : 0u;
+      }
+    }
+    __syncthreads();  // the previous half's chunks (or the mainloop's operands) are consumed
+    if (my_half == h) {
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            cs[(g256_row<C>(wm, i, r, lane) - 128 * h) * E::PITCH + g256_col<C>(wn, j, lane)] = acc[i][j][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < E::CH; ++c) {
+      const int row = g0 + c * E::RG, m = mb + row;
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + row * E::PITCH + cc * 8);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * E::PITCH + cc * 8 + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if constexpr (ADD) {
+        const uint32_t wq[4] = {q[c].x, q[c].y, q[c].z, q[c].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] += __uint_as_float(wq[k] << 16);
+          v[2 * k + 1] += __uint_as_float(wq[k] & 0xFFFF0000u);
+        }
+      }
+      const uint4 o = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+      if (m < M && n < N) {
+        *reinterpret_cast<uint4*>(y + (size_t)orow[c] * N + n) = o;
+        const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+        float d[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          d[2 * k] = __uint_as_float(ow[k] << 16);
+          d[2 * k + 1] = __uint_as_float(ow[k] & 0xFFFF0000u);
+        }
+        if constexpr (STATS) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            s[k] += d[k];
+            sq[k] = fmaf(d[k], d[k], sq[k]);
+          }
+        }
+        if constexpr (BSTAT) {
+          const uint32_t yw[4] = {yq[c].x, yq[c].y, yq[c].z, yq[c].w};
+          float yv[8];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            yv[2 * k] = __uint_as_float(yw[k] << 16);
+            yv[2 * k + 1] = __uint_as_float(yw[k] & 0xFFFF0000u);
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            if constexpr (BS::MODE == 2) d[k] = fmaf(yv[k], bsc[k], bsh[k]) > 0.f ? d[k] : 0.f;
+            if constexpr (BS::MODE == 3) d[k] = (mbits[c] >> k) & 1u ? d[k] : 0.f;
+            s[k] += d[k];
+            sq[k] = fmaf(d[k], (yv[k] - bmu[k]) * bis[k], sq[k]);
+          }
+        }
+      }
+    }
+  }
+  if constexpr (STATS || BSTAT) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      cs[g0 * C::BN + cc * 8 + k] = s[k];
+      cs[(E::RG + g0) * C::BN + cc * 8 + k] = sq[k];
+    }
+    __syncthreads();
+    for (int col = tid; col < C::BN; col += 512) {
+      const int nn = n0 + col;
+      if (nn >= N) continue;
+      float a = 0.f, b = 0.f;
+#pragma unroll 8
+      for (int g = 0; g < E::RG; ++g) { a += cs[g * C::BN + col]; b += cs[(E::RG + g) * C::BN + col]; }
+      part[nn] = a;
+      part[N + nn] = b;
+    }
+  }
+}
+
+template <int BN>
+constexpr int g256_smem() {
+  using C = G256<BN, G256WM<BN>::v>;
+  return C::SMEM > G256Epi<BN>::BYTES ? C::SMEM : G256Epi<BN>::BYTES;
+}
+
+// bf16-output conv GEMM: part (STATS / BnB) gets one row per 256-row tile at part + tile_m * 2N
+template <int BN, bool AKC, bool BKC, class SA, class SB, bool ADD, bool STATS, class RM, class BS>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void g256_conv_kernel(
+    SA sa, SB sb, uint16_t* y, const uint16_t* add, int M, int N, int KD, float* part, RM rm, uint32_t ybytes, BS bs,
+    int tiles_m, int tiles_n) {
+  using C = G256<BN, G256WM<BN>::v, AKC, BKC>;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  int tm, tn;
+  g256_tile(blockIdx.x, gridDim.x, tiles_m, tiles_n, tm, tn);
+  f32x16 acc[C::TM][C::TN];
+  g256_mainloop<C>(sa, sb, tm * 256, tn * BN, 0, KD, smem_raw, acc);
+  g256_epilogue<C, ADD, STATS, RM, BS>(acc, smem_raw, y, add, M, N, tm * 256, tn * BN,
+                                       part ? part + (size_t)tm * 2 * N : nullptr, rm, ybytes, bs);
+}
+
+// (plain template launchers, no generic lambdas: instantiating the kernel template from a host
+// lambda made hipcc's host pass reject the device-only DMA builtin inside it)
+template <int BN, bool AKC, bool BKC, bool ADD, bool STATS, class SA, class SB, class RM, class BS>
+void g256_launch_bf16_bn(const SA& sa, const SB& sb, uint16_t* y, const uint16_t* add, int M, int N, int KD, float* part,
+                         hipStream_t st, RM rm, uint32_t ybytes, BS bs) {
+  auto* k = &g256_conv_kernel<BN, AKC, BKC, SA, SB, ADD, STATS, RM, BS>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              g256_smem<BN>());
+    attr = true;
+  }
+  const int tm = (M + 255) / 256, tn = (N + BN - 1) / BN;
+  k<<<tm * tn, 512, g256_smem<BN>(), st>>>(sa, sb, y, add, M, N, KD, part, rm, ybytes, bs, tm, tn);
+}
+template <bool AKC, bool BKC, bool ADD, bool STATS, class SA, class SB, class RM = RowId, class BS = NoBnB>
+void g256_launch_bf16(const SA& sa, const SB& sb, uint16_t* y, const uint16_t* add, int M, int N, int KD, float* part,
+                      hipStream_t st, RM rm = RM{}, uint32_t ybytes = 0, BS bs = BS{}) {
+  const int bn = g256_bn(N);
+  if (bn == 256) g256_launch_bf16_bn<256, AKC, BKC, ADD, STATS>(sa, sb, y, add, M, N, KD, part, st, rm, ybytes, bs);
+  else if (bn == 128) g256_launch_bf16_bn<128, AKC, BKC, ADD, STATS>(sa, sb, y, add, M, N, KD, part, st, rm, ybytes, bs);
+  else g256_launch_bf16_bn<64, AKC, BKC, ADD, STATS>(sa, sb, y, add, M, N, KD, part, st, rm, ybytes, bs);
+}
+
+// weight gradient: dW [M = R*S*C][N = K] fp32, split-K over pixels (KD); the accumulator registers go
+// straight out (a 32 x 32 register holds two 128-B row segments: full-rate stores and atomics)
+template <int BN, class SA, class SB>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void g256_wgrad_kernel(
+    SA sa, SB sb, float* dw, int M, int N, int KD, int kchunk, int tiles_m, int tiles_n, int atomic) {
+  using C = G256<BN, G256WM<BN>::v, false, false>;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int tiles = tiles_m * tiles_n, split = blockIdx.x / tiles;
+  int tm, tn;
+  g256_tile(blockIdx.x - split * tiles, tiles, tiles_m, tiles_n, tm, tn);
+  const int kb = split * kchunk, ke = min(KD, kb + kchunk);
+  f32x16 acc[C::TM][C::TN];
+  g256_mainloop<C>(sa, sb, tm * 256, tn * BN, kb, ke, smem_raw, acc);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w / C::WN, wn = w % C::WN;
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) {
+      const int col = tn * BN + g256_col<C>(wn, j, lane);
+      if (col >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = tm * 256 + g256_row<C>(wm, i, r, lane);
+        if (row >= M) continue;
+        float* p = dw + (size_t)row * N + col;
+        if (atomic) atomicAdd(p, acc[i][j][r]);
+        else *p = acc[i][j][r];
+      }
+    }
+}
+
+template <int BN, class SA>
+void g256_launch_wgrad_bn(const SA& sa, const DenseX<false>& sb, float* dw, int M, int N, int KD, int splits,
+                          hipStream_t st) {
+  using C = G256<BN, G256WM<BN>::v, false, false>;
+  auto* k = &g256_wgrad_kernel<BN, SA, DenseX<false>>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
+    attr = true;
+  }
+  const int tm = (M + 255) / 256, tn = (N + BN - 1) / BN;
+  const int kchunk = ((KD + splits - 1) / splits + 63) / 64 * 64;
+  const int sp = (KD + kchunk - 1) / kchunk;
+  k<<<tm * tn * sp, 512, C::SMEM, st>>>(sa, sb, dw, M, N, KD, kchunk, tm, tn, sp > 1 ? 1 : 0);
+}
+template <class SA>
+void g256_launch_wgrad(const SA& sa, const DenseX<false>& sb, float* dw, int M, int N, int KD, int splits, hipStream_t st) {
+  const int bn = g256_bn(N);
+  if (bn == 256) g256_launch_wgrad_bn<256>(sa, sb, dw, M, N, KD, splits, st);
+  else if (bn == 128) g256_launch_wgrad_bn<128>(sa, sb, dw, M, N, KD, splits, st);
+  else g256_launch_wgrad_bn<64>(sa, sb, dw, M, N, KD, splits, st);
+}
+
 }  // namespace
 
 void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, hipStream_t st) {
   const int M = c.N * c.Ho() * c.Wo(), KD = c.R * c.S * c.C;
   StoreBf16 epi{y, M, c.K};
   DenseX<false> lb{w, c.K, c.K, KD};
+  if (use_g256(M, c.K)) {  // A = im2col(X) (KC), B = HWIO weight (MNC)
+    if (is_pointwise(c)) g256_launch_bf16<true, false, false, false>(DenseX<true>{x, c.C, M, c.C}, lb, y, nullptr, M, c.K, KD, nullptr, st);
+    else g256_launch_bf16<true, false, false, false>(FwdA{x, make_geo(c, M, KD)}, lb, y, nullptr, M, c.K, KD, nullptr, st);
+    return;
+  }
   if (is_pointwise(c)) {
     DenseX<true> la{x, c.C, M, c.C};
     if (TFD_CONV_LDS_EPI) dispatch_bf16(la, lb, y, nullptr, M, c.K, KD, st);
@@ -735,6 +1035,7 @@ void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t
 
 int conv_fwd_stats_rows(const ConvShape& c) {  // row blocks (+ the totals row, see launch_gemm_stats)
   const int M = c.N * c.Ho() * c.Wo();
+  if (use_g256(M, c.K)) return (M + 255) / 256;
   const int rows = TFD_CONV_LDS_EPI ? out_tile_rows(M, c.K) : (use_big_tiles(M, c.K) ? (M + 127) / 128 : (M + 63) / 64);
   return rows + (TFD_CONV_LDS_EPI && bn_totals_enabled() ? 1 : 0);
 }
@@ -743,6 +1044,11 @@ void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, ui
                     hipStream_t st) {
   const int M = c.N * c.Ho() * c.Wo(), KD = c.R * c.S * c.C;
   DenseX<false> lb{w, c.K, c.K, KD};
+  if (use_g256(M, c.K)) {
+    if (is_pointwise(c)) g256_launch_bf16<true, false, false, true>(DenseX<true>{x, c.C, M, c.C}, lb, y, nullptr, M, c.K, KD, part, st);
+    else g256_launch_bf16<true, false, false, true>(FwdA{x, make_geo(c, M, KD)}, lb, y, nullptr, M, c.K, KD, part, st);
+    return;
+  }
   const OutTile t = TFD_CONV_LDS_EPI ? out_tile(M, c.K) : (use_big_tiles(M, c.K) ? OT128 : OT64);
   auto go = [&](const auto& la) {
     using LA = std::decay_t<decltype(la)>;
@@ -811,8 +1117,15 @@ static int dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t*
       g.hpwp = FastDiv(g.Hp * g.Wp); g.wp = FastDiv(g.Wp); g.k = FastDiv(c.K); g.nsd = FastDiv(g.ns);
       DgradPhaseA la{dy, g};
       DgradPhaseB lb{w, g, c.S};
-      const OutTile ot = out_tile(g.M, c.C);
       float* pp = part ? part + (size_t)rows * 2 * c.C : nullptr;
+      if (use_g256(g.M, c.C)) {
+        rows += (g.M + 255) / 256;
+        const uint32_t xbytes = (uint32_t)((int64_t)c.N * c.H * c.W * c.C * 2);
+        if (add) g256_launch_bf16<true, true, true, false>(la, lb, dx, add, g.M, c.C, g.KD, pp, st, PhaseRows{g}, xbytes, bs);
+        else g256_launch_bf16<true, true, false, false>(la, lb, dx, add, g.M, c.C, g.KD, pp, st, PhaseRows{g}, xbytes, bs);
+        continue;
+      }
+      const OutTile ot = out_tile(g.M, c.C);
       rows += ot == OT64 ? (g.M + 63) / 64 : (g.M + 127) / 128;
       if (add) {
         if (ot == OT128) launch_phase<128, 128, true>(la, lb, dx, add, st, pp, bs);
@@ -839,6 +1152,20 @@ void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint1
     dgrad_strided(c, dy, w, dx, add, st);
     return;
   }
+  if (use_g256(M, c.C)) {  // A = dY gather, B = W as [C][(r,s,k)]: both KC
+    const int KD = c.R * c.S * c.K;
+    auto go = [&](const auto& la, const auto& lb) {
+      if (add) g256_launch_bf16<true, true, true, false>(la, lb, dx, add, M, c.C, KD, nullptr, st);
+      else g256_launch_bf16<true, true, false, false>(la, lb, dx, add, M, c.C, KD, nullptr, st);
+    };
+    if (is_pointwise(c)) {
+      go(DenseX<true>{dy, c.K, M, c.K}, DenseX<true>{w, c.K, c.C, c.K});
+    } else {
+      Geo g = make_geo(c, M, KD);
+      go(DgradA{dy, g}, DgradB{w, g});
+    }
+    return;
+  }
   if (TFD_CONV_LDS_EPI) {
     const int KD = c.R * c.S * c.K;
     if (is_pointwise(c)) {
@@ -861,13 +1188,14 @@ bool conv_dgrad_bn_supported(const ConvShape& c) {
   if (!TFD_CONV_LDS_EPI || c.C % 8 != 0) return false;
   return c.stride == 1 || (TFD_DGRAD_PHASES && c.R >= c.stride && c.S >= c.stride);
 }
+static int bf16_out_rows(int M, int N) { return use_g256(M, N) ? (M + 255) / 256 : out_tile_rows(M, N); }
 int conv_dgrad_bn_rows(const ConvShape& c) {
-  if (c.stride == 1) return out_tile_rows(c.N * c.H * c.W, c.C);
+  if (c.stride == 1) return bf16_out_rows(c.N * c.H * c.W, c.C);
   int rows = 0;
   for (int ph = 0; ph < c.stride; ++ph)
     for (int pw = 0; pw < c.stride; ++pw) {
       const int Hp = (c.H - ph + c.stride - 1) / c.stride, Wp = (c.W - pw + c.stride - 1) / c.stride;
-      if (Hp > 0 && Wp > 0) rows += out_tile_rows(c.N * Hp * Wp, c.C);
+      if (Hp > 0 && Wp > 0) rows += bf16_out_rows(c.N * Hp * Wp, c.C);
     }
   return rows;
 }
@@ -879,6 +1207,16 @@ void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, ui
   auto go = [&](const auto& bs) {
     if (c.stride > 1) {
       dgrad_strided(c, dy, w, dx, add, st, part, bs);
+    } else if (use_g256(M, c.C)) {
+      auto g2 = [&](const auto& la, const auto& lb) {
+        if (add) g256_launch_bf16<true, true, true, false>(la, lb, dx, add, M, c.C, KD, part, st, RowId{}, 0u, bs);
+        else g256_launch_bf16<true, true, false, false>(la, lb, dx, add, M, c.C, KD, part, st, RowId{}, 0u, bs);
+      };
+      if (is_pointwise(c)) g2(DenseX<true>{dy, c.K, M, c.K}, DenseX<true>{w, c.K, c.C, c.K});
+      else {
+        Geo g = make_geo(c, M, KD);
+        g2(DgradA{dy, g}, DgradB{w, g});
+      }
     } else if (is_pointwise(c)) {
       dispatch_bf16_bnb(DenseX<true>{dy, c.K, M, c.K}, DenseX<true>{w, c.K, c.C, c.K}, dx, add, M, c.C, KD, part, bs, st);
     } else {
@@ -913,7 +1251,21 @@ WgTile wgrad_tile(const ConvShape& c) {
 #ifndef TFD_WGRAD_BLOCKS  // (tile x split) blocks the split count aims for
 #define TFD_WGRAD_BLOCKS 512
 #endif
+// weight gradients on the 256-row core: mode 2 only (the A/B switch)
+static bool use_g256_wgrad(const ConvShape& c) {
+  const int mode = g256_mode(), P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
+  if (mode == 0 || c.K % 8 || c.C % 8) return false;
+  (void)P; (void)MT;
+  return mode == 2;  // measured slower than the 128-row core on every ResNet-50 weight gradient
+}
+static int g256_wgrad_splits(const ConvShape& c) {
+  const int P = c.N * c.Ho() * c.Wo();
+  const long tiles = g256_tiles(c.R * c.S * c.C, c.K);
+  int s = (int)std::max<long>(1, 256 / std::max<long>(1, tiles));
+  return std::min(s, std::max(1, P / 4096));
+}
 int conv_wgrad_splits(const ConvShape& c) {
+  if (use_g256_wgrad(c)) return g256_wgrad_splits(c);
   // enough (tile x split) blocks to fill the chip; each split keeps >= TFD_WGRAD_MINPX pixels of K
   const int P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
   const WgTile t = wgrad_tile(c);
@@ -940,6 +1292,11 @@ void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float
   if (splits > 1 && !zeroed) (void)hipMemsetAsync(dw, 0, (size_t)MT * c.K * sizeof(float), st);
   AccF32 epi{dw, MT, c.K, splits > 1 ? 1 : 0};
   DenseX<false> lb{dy, c.K, c.K, P};
+  if (use_g256_wgrad(c)) {  // A = im2col(X)^T, B = dY: both MNC
+    if (is_pointwise(c)) g256_launch_wgrad(DenseX<false>{x, c.C, c.C, P}, lb, dw, MT, c.K, P, splits, st);
+    else g256_launch_wgrad(WgradA{x, make_geo(c, MT, P)}, lb, dw, MT, c.K, P, splits, st);
+    return;
+  }
   if (is_pointwise(c)) {  // dW = X^T dY
     DenseX<false> la{x, c.C, c.C, P};
     wgrad_launch(c, la, lb, epi, MT, P, splits, st);
@@ -947,6 +1304,12 @@ void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float
     WgradA la{x, make_geo(c, MT, P)};
     wgrad_launch(c, la, lb, epi, MT, P, splits, st);
   }
+}
+
+int conv_gemm_core(int mode) {  // -1: query
+  const int old = g256_mode();
+  if (mode >= 0) g256_mode_v = mode;
+  return old;
 }
 
 void linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, float* y, int M, int Kin, int N,

@@ -17,7 +17,8 @@ namespace {
 // pieces of 2-B scalars.
 constexpr int G256_CPITCH = 256 + 8;  // bf16 elements
 constexpr int G256_CBYTES = 256 * G256_CPITCH * 2;
-constexpr int G256_DENSE_SMEM = G256::SMEM > G256_CBYTES ? G256::SMEM : G256_CBYTES;
+using GD = G256<256, 2, true, true>;
+constexpr int G256_DENSE_SMEM = GD::SMEM > G256_CBYTES ? GD::SMEM : G256_CBYTES;
 static_assert(G256_DENSE_SMEM <= 160 * 1024, "LDS budget");
 
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm256_nt_kernel(DenseKC sa, DenseKC sb, uint16_t* __restrict__ c, int M, int N,
@@ -25,17 +26,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int tm, tn;
   g256_tile(blockIdx.x, gridDim.x, tiles_m, tiles_n, tm, tn);
-  const int m0 = tm * G256::BM, n0 = tn * G256::BN;
-  f32x16 acc[G256::TM][G256::TN];
-  g256_mainloop(sa, sb, m0, n0, 0, K, smem, acc);
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, wm = w / G256::WN, wn = w % G256::WN;
+  const int m0 = tm * GD::BM, n0 = tn * GD::BN;
+  f32x16 acc[GD::TM][GD::TN];
+  g256_mainloop<GD>(sa, sb, m0, n0, 0, K, smem, acc);
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, wm = w / GD::WN, wn = w % GD::WN;
   uint16_t* cs = reinterpret_cast<uint16_t*>(smem);  // the mainloop ended with a barrier
 #pragma unroll
-  for (int i = 0; i < G256::TM; ++i)
+  for (int i = 0; i < GD::TM; ++i)
 #pragma unroll
-    for (int j = 0; j < G256::TN; ++j)
+    for (int j = 0; j < GD::TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) cs[g256_row(wm, i, r, l) * G256_CPITCH + g256_col(wn, j, l)] = f2bf_bits(acc[i][j][r]);
+      for (int r = 0; r < 16; ++r)
+        cs[g256_row<GD>(wm, i, r, l) * G256_CPITCH + g256_col<GD>(wn, j, l)] = f2bf_bits(acc[i][j][r]);
   __syncthreads();
 #pragma unroll 4
   for (int q = tid; q < 256 * 32; q += 512) {

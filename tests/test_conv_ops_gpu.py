@@ -8,10 +8,15 @@ pytestmark = pytest.mark.gpu
 ops = None
 
 
-@pytest.fixture(autouse=True)
-def _ops(cuda):
+@pytest.fixture(autouse=True, params=[0, 2], ids=["core128", "core256"])
+def _ops(cuda, request):
+    """Every conv test runs on both GEMM cores: the 128-row register-staged one and the 256-row DMA
+    one (forced for every shape it applies to; the default picks it where its tiles fill the chip)."""
     global ops
     ops = torch.ops.tfd
+    old = ops.conv_gemm_core(request.param)
+    yield
+    ops.conv_gemm_core(old)
 
 
 def rb(t):  # round to bf16 and back (the kernels' operand precision)

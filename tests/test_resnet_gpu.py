@@ -261,6 +261,9 @@ def test_rccl_comm_outlives_its_python_object(cuda):
     is gone too."""
     from tensorflow_distributed_amd.models.resnet import ResNet
 
+    import gc
+
+    gc.collect()  # earlier tests' communicators retire now, not in the middle of this test
     comm = torch.classes.tfd.RcclComm(torch.classes.tfd.RcclComm.unique_id(), 1, 0, cuda.index)
     before = torch.classes.tfd.RcclComm.retired_count()
     m = ResNet(18, num_classes=16, device=cuda, seed=5, width=16)
@@ -277,8 +280,6 @@ def test_rccl_comm_outlives_its_python_object(cuda):
         out = m.train_step(x, lab, lr=0.01)
     master = m.fp.master
     del m, comm
-    import gc
-
     gc.collect()  # the model's layers point back at it (reference cycles)
     assert torch.classes.tfd.RcclComm.retired_count() == before + 1
     for _ in range(3):
