@@ -39,23 +39,52 @@ ConvShape shape_of(const at::Tensor& x, const at::Tensor& w, int64_t stride, int
   return c;
 }
 
-at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad) {
+// Folded BN input (BnReluIn): mean, invstd, gamma, beta all given (fp32 [C]) or none
+struct Act {
+  BnReluIn in{};
+  bool on = false;
+  const BnReluIn* ptr() const { return on ? &in : nullptr; }
+};
+Act act_of(const c10::optional<at::Tensor>& mean, const c10::optional<at::Tensor>& invstd,
+           const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta, int C) {
+  Act a;
+  const int n = (int)mean.has_value() + (int)invstd.has_value() + (int)gamma.has_value() + (int)beta.has_value();
+  if (n == 0) return a;
+  TORCH_CHECK(n == 4, "conv: a folded BN input needs mean, invstd, gamma and beta");
+  for (const auto* t : {&*mean, &*invstd, &*gamma, &*beta}) {
+    check_f32(*t, "bn");
+    TORCH_CHECK(t->numel() == C, "conv: folded BN vectors must have C elements");
+  }
+  TORCH_CHECK(C <= kBnReluMaxC, "conv: folded BN input with C > ", kBnReluMaxC);
+  a.in = BnReluIn{fp(*mean), fp(*invstd), fp(*gamma), fp(*beta)};
+  a.on = true;
+  return a;
+}
+
+at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                      const c10::optional<at::Tensor>& mean, const c10::optional<at::Tensor>& invstd,
+                      const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta) {
   check_bf16(x, "x", 4);
   check_bf16(w, "w", 4);
   const ConvShape c = shape_of(x, w, stride, pad);
+  const Act a = act_of(mean, invstd, gamma, beta, c.C);
   auto y = at::empty({c.N, c.Ho(), c.Wo(), c.K}, x.options());
-  conv_fwd(c, bp(x), bp(w), bp(y), cur());
+  conv_fwd(c, bp(x), bp(w), bp(y), cur(), a.ptr());
   return y;
 }
 
 std::tuple<at::Tensor, at::Tensor> conv2d_fwd_stats(const at::Tensor& x, const at::Tensor& w, int64_t stride,
-                                                    int64_t pad) {
+                                                    int64_t pad, const c10::optional<at::Tensor>& mean,
+                                                    const c10::optional<at::Tensor>& invstd,
+                                                    const c10::optional<at::Tensor>& gamma,
+                                                    const c10::optional<at::Tensor>& beta) {
   check_bf16(x, "x", 4);
   check_bf16(w, "w", 4);
   const ConvShape c = shape_of(x, w, stride, pad);
+  const Act a = act_of(mean, invstd, gamma, beta, c.C);
   auto y = at::empty({c.N, c.Ho(), c.Wo(), c.K}, x.options());
-  auto part = at::empty({conv_fwd_stats_rows(c), 2, c.K}, x.options().dtype(at::kFloat));
-  conv_fwd_stats(c, bp(x), bp(w), bp(y), fp(part), cur());
+  auto part = at::empty({conv_fwd_stats_rows(c, a.on), 2, c.K}, x.options().dtype(at::kFloat));
+  conv_fwd_stats(c, bp(x), bp(w), bp(y), fp(part), cur(), a.ptr());
   return {y, part};
 }
 
@@ -119,7 +148,9 @@ std::tuple<at::Tensor, at::Tensor> conv2d_dgrad_bn(const at::Tensor& dy, const a
   return {x, part};
 }
 
-void conv2d_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, int64_t stride, int64_t pad, bool zeroed) {
+void conv2d_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, int64_t stride, int64_t pad, bool zeroed,
+                  const c10::optional<at::Tensor>& mean, const c10::optional<at::Tensor>& invstd,
+                  const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta) {
   check_bf16(x, "x", 4);
   check_bf16(dy, "dy", 4);
   check_f32(dw, "dw");
@@ -128,7 +159,8 @@ void conv2d_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, int6
   const ConvShape c = shape_of(x, wfake, stride, pad);
   TORCH_CHECK(dy.size(0) == c.N && dy.size(1) == c.Ho() && dy.size(2) == c.Wo() && dy.size(3) == c.K,
               "wgrad: dy shape mismatch");
-  conv_wgrad(c, bp(x), bp(dy), fp(dw), conv_wgrad_splits(c), cur(), zeroed);
+  const Act a = act_of(mean, invstd, gamma, beta, c.C);
+  conv_wgrad(c, bp(x), bp(dy), fp(dw), conv_wgrad_splits(c, a.on), cur(), zeroed, a.ptr());
 }
 
 at::Tensor gemm_nt_op(const at::Tensor& a, const at::Tensor& bt) {
@@ -207,6 +239,22 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& y, const
   bn_forward(bp(y), fp(gamma), fp(beta), res ? bp(*res) : nullptr, relu ? 1 : 0, bp(out), fp(mean), fp(invstd), rm, rv,
              (float)momentum, (float)eps, M, C, fp(part), cur(), mb);
   return {out, mean, invstd};
+}
+
+// training-mode statistics only (the BN of a folded conv input: its consumer applies it while staging)
+std::tuple<at::Tensor, at::Tensor> bn_stats(const at::Tensor& y, const at::Tensor& partials, at::Tensor running_mean,
+                                            at::Tensor running_var, double momentum, double eps) {
+  check_bf16(y, "y", -1);
+  check_f32(partials, "partials");
+  const int C = (int)y.size(-1);
+  TORCH_CHECK(partials.dim() == 3 && partials.size(1) == 2 && partials.size(2) == C, "bn_stats: partials [nblk,2,C]");
+  auto f = y.options().dtype(at::kFloat);
+  auto mean = at::empty({C}, f), invstd = at::empty({C}, f);
+  float* rm = running_mean.defined() && running_mean.numel() ? fp(running_mean) : nullptr;
+  float* rv = running_var.defined() && running_var.numel() ? fp(running_var) : nullptr;
+  bn_stats_partials(fp(mean), fp(invstd), rm, rv, (float)momentum, (float)eps, (int)(y.numel() / C), C, fp(partials),
+                    (int)partials.size(0), cur());
+  return {mean, invstd};
 }
 
 std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dout, const at::Tensor& out, const at::Tensor& y,
@@ -315,16 +363,20 @@ at::Tensor pad_channels_op(const at::Tensor& x, int64_t cout) {
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(tfd, m) {
-  m.def("conv2d_fwd(Tensor x, Tensor w, int stride, int pad) -> Tensor");
+  m.def("conv2d_fwd(Tensor x, Tensor w, int stride, int pad, Tensor? mean=None, Tensor? invstd=None, "
+        "Tensor? gamma=None, Tensor? beta=None) -> Tensor");
   m.impl("conv2d_fwd", c10::DispatchKey::CUDA, &conv2d_fwd);
-  m.def("conv2d_fwd_stats(Tensor x, Tensor w, int stride, int pad) -> (Tensor, Tensor)");
+  m.def("conv2d_fwd_stats(Tensor x, Tensor w, int stride, int pad, Tensor? mean=None, Tensor? invstd=None, "
+        "Tensor? gamma=None, Tensor? beta=None) -> (Tensor, Tensor)");
   m.impl("conv2d_fwd_stats", c10::DispatchKey::CUDA, &conv2d_fwd_stats);
   m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc=None) -> Tensor");
   m.impl("conv2d_dgrad", c10::DispatchKey::CUDA, &conv2d_dgrad);
   m.def("conv2d_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc, Tensor y, Tensor mean, "
         "Tensor invstd, Tensor gamma, Tensor? beta, Tensor? mask, bool relu) -> (Tensor, Tensor)");
   m.impl("conv2d_dgrad_bn", c10::DispatchKey::CUDA, &conv2d_dgrad_bn);
-  m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad, bool zeroed=False) -> ()");
+  m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad, bool zeroed=False, Tensor? mean=None, "
+        "Tensor? invstd=None, Tensor? gamma=None, Tensor? beta=None) -> ()");
+  m.def("bn_relu_max_channels() -> int", []() -> int64_t { return kBnReluMaxC; });
   m.impl("conv2d_wgrad", c10::DispatchKey::CUDA, &conv2d_wgrad);
   m.def("conv_gemm_core(int mode) -> int", [](int64_t mode) -> int64_t { return conv_gemm_core((int)mode); });
   m.def("gemm_nt(Tensor a, Tensor bt) -> Tensor");
@@ -339,6 +391,9 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
         "Tensor(b!) running_var, float momentum, float eps, Tensor? partials=None, Tensor(c!)? mask=None) -> "
         "(Tensor, Tensor, Tensor)");
   m.impl("bn_fwd", c10::DispatchKey::CUDA, &bn_fwd);
+  m.def("bn_stats(Tensor y, Tensor partials, Tensor(a!) running_mean, Tensor(b!) running_var, float momentum, "
+        "float eps) -> (Tensor, Tensor)");
+  m.impl("bn_stats", c10::DispatchKey::CUDA, &bn_stats);
   m.def("bn_bwd(Tensor dout, Tensor out, Tensor y, Tensor gamma, Tensor mean, Tensor invstd, bool relu, "
         "bool want_dres, Tensor(a!) dgamma, Tensor(b!) dbeta, Tensor? beta=None, Tensor? mask=None, "
         "Tensor? partials=None) -> (Tensor, Tensor)");

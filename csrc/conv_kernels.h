@@ -16,13 +16,22 @@ struct ConvShape {
   int Wo() const { return (W + 2 * pad - S) / stride + 1; }
 };
 
-void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, hipStream_t st);
+// Forward BN fold: the conv input is relu(bn(x)) of the producing layer (training-mode statistics
+// mean / invstd, affine gamma / beta, all fp32 [C]), applied by the operand loader while it stages x --
+// the normalised activation is never materialised. C <= kBnReluMaxC. nullptr: x is the input as is.
+constexpr int kBnReluMaxC = 512;
+struct BnReluIn {
+  const float *mean, *invstd, *gamma, *beta;
+};
+void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, hipStream_t st,
+              const BnReluIn* act = nullptr);
 // conv forward that also emits the batch-norm statistics of its (bf16) output: part is fp32
-// [conv_fwd_stats_rows(c)][2][K] (per-row-block sums and sums of squares), consumed by
-// bn_forward_partials -- the forward BN then never re-reads the conv output for its statistics
-int conv_fwd_stats_rows(const ConvShape& c);
+// [conv_fwd_stats_rows(c, folded)][2][K] (per-row-block sums and sums of squares), consumed by
+// bn_forward_partials / bn_stats_partials -- the forward BN then never re-reads the conv output for
+// its statistics
+int conv_fwd_stats_rows(const ConvShape& c, bool folded = false);
 void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
-                    hipStream_t st);
+                    hipStream_t st, const BnReluIn* act = nullptr);
 // add (optional, must not alias dx): dx = add + dgrad in the epilogue -- the residual-join sum of
 // two gradient paths without a separate add kernel
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
@@ -45,9 +54,10 @@ void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, ui
 // dw: fp32 [R*S*C][K]; overwritten (zeroed first when split)
 // zeroed: dw is known to be zero already (the model zeroes its flat gradient buffer once per
 // step), so split-K needs no per-layer memset
+// act: x is the pre-BN input of a folded conv (see BnReluIn), the X operand is rebuilt while staging
 void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float* dw, int splits, hipStream_t st,
-                bool zeroed = false);
-int conv_wgrad_splits(const ConvShape& c);
+                bool zeroed = false, const BnReluIn* act = nullptr);
+int conv_wgrad_splits(const ConvShape& c, bool folded = false);
 
 void linear_fwd(const uint16_t* x, const uint16_t* w, const float* bias, float* y, int M, int Kin, int N,
                 hipStream_t st);
@@ -74,6 +84,10 @@ void bn_forward_partials(const uint16_t* y, const float* gamma, const float* bet
                          uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var,
                          float momentum, float eps, int M, int C, const float* partials, int nblk, hipStream_t st,
                          uint8_t* mask_bits = nullptr);
+// statistics only (mean / invstd + running stats) from conv_fwd_stats partials: the BN of a folded
+// conv input, whose normalisation is applied by the consumer's loader (BnReluIn)
+void bn_stats_partials(float* mean, float* invstd, float* running_mean, float* running_var, float momentum, float eps,
+                       int M, int C, const float* partials, int nrows, hipStream_t st);
 // dout -> dy (through relu/bn), writes dgamma/dbeta (fp32, overwritten) and, when dres != null, the
 // gradient of the residual input (== gradient after the relu mask).
 // beta != nullptr (only valid when the forward had no residual): the relu mask is recomputed from y

@@ -101,11 +101,26 @@ __device__ __forceinline__ bf16x8 frag_tr16(const bf16* p0, const bf16* p1) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// Operand transforms: a loader that declares `static constexpr int XF_BYTES` still travels
+// global -> registers -> LDS, but gload keeps a per-chunk tag (v = ld.load(mn, k, tag)) and the LDS
+// store writes ld.xform(v, tag, table) instead of v; ld.stage(table) fills the loader's XF_BYTES-byte
+// LDS table (placed after the operand images) once per block, before the first store. Used by the
+// conv loaders that apply the producing layer's batch norm + relu while staging their input
+// (csrc/kernels/conv_nhwc.hip BnRelu).
+template <class L, class = void>
+struct LoaderXF {
+  static constexpr int BYTES = 0;
+};
+template <class L>
+struct LoaderXF<L, std::void_t<decltype(L::XF_BYTES)>> {
+  static constexpr int BYTES = L::XF_BYTES;
+};
+
 template <int BM, int BN, int BK, class LA, class LB>
 struct GemmSmem {
   using TA = LdsTile<BM, BK, LA::KC>;
   using TB = LdsTile<BN, BK, LB::KC>;
-  static constexpr int BYTES = 2 * (TA::ELEMS + TB::ELEMS) * 2;
+  static constexpr int BYTES = 2 * (TA::ELEMS + TB::ELEMS) * 2 + LoaderXF<LA>::BYTES + LoaderXF<LB>::BYTES;
 };
 
 // One workgroup computes the BM x BN tile at (m0, n0) over k in [kbeg, kend).
@@ -130,26 +145,31 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
   constexpr int CA = (TA::CHUNKS + NT - 1) / NT;
   constexpr int CB = (TB::CHUNKS + NT - 1) / NT;
+  constexpr bool XA = LoaderXF<LA>::BYTES > 0, XB = LoaderXF<LB>::BYTES > 0;
   bf16* As0 = smem;
   bf16* As1 = smem + TA::ELEMS;
   bf16* Bs0 = smem + 2 * TA::ELEMS;
   bf16* Bs1 = Bs0 + TB::ELEMS;
+  char* xtab_a = reinterpret_cast<char*>(smem + 2 * (TA::ELEMS + TB::ELEMS));
+  char* xtab_b = xtab_a + LoaderXF<LA>::BYTES;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   uint4 ra[RS][CA], rb[RS][CB];
+  [[maybe_unused]] int ta[RS][CA], tb[RS][CB];  // transform tags (XA / XB loaders only)
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto gload = [&](int k0, uint4 (&xa)[CA], uint4 (&xb)[CB]) {
+  auto gload = [&](int k0, uint4 (&xa)[CA], uint4 (&xb)[CB], int (&ga)[CA], int (&gb)[CB]) {
 #pragma unroll
     for (int c = 0; c < CA; ++c) {
       const int idx = tid + c * NT;
       if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
         const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 8;
-        if constexpr (LA::KC) xa[c] = la(m0 + row, k0 + col);
-        else xa[c] = la(m0 + col, k0 + row);
+        const int mn = LA::KC ? m0 + row : m0 + col, k = LA::KC ? k0 + col : k0 + row;
+        if constexpr (XA) xa[c] = la.load(mn, k, ga[c]);
+        else xa[c] = la(mn, k);
       }
     }
 #pragma unroll
@@ -157,18 +177,22 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
       const int idx = tid + c * NT;
       if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
         const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 8;
-        if constexpr (LB::KC) xb[c] = lb(n0 + row, k0 + col);
-        else xb[c] = lb(n0 + col, k0 + row);
+        const int mn = LB::KC ? n0 + row : n0 + col, k = LB::KC ? k0 + col : k0 + row;
+        if constexpr (XB) xb[c] = lb.load(mn, k, gb[c]);
+        else xb[c] = lb(mn, k);
       }
     }
   };
-  auto sstore = [&](bf16* As, bf16* Bs, const uint4 (&xa)[CA], const uint4 (&xb)[CB]) {
+  auto sstore = [&](bf16* As, bf16* Bs, const uint4 (&xa)[CA], const uint4 (&xb)[CB], const int (&ga)[CA],
+                    const int (&gb)[CB]) {
 #pragma unroll
     for (int c = 0; c < CA; ++c) {
       const int idx = tid + c * NT;
       if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
         const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 8;
-        *reinterpret_cast<uint4*>(As + TA::at(row, col)) = xa[c];
+        uint4 v = xa[c];
+        if constexpr (XA) v = la.xform(v, ga[c], xtab_a);
+        *reinterpret_cast<uint4*>(As + TA::at(row, col)) = v;
       }
     }
 #pragma unroll
@@ -176,8 +200,18 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
       const int idx = tid + c * NT;
       if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
         const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 8;
-        *reinterpret_cast<uint4*>(Bs + TB::at(row, col)) = xb[c];
+        uint4 v = xb[c];
+        if constexpr (XB) v = lb.xform(v, gb[c], xtab_b);
+        *reinterpret_cast<uint4*>(Bs + TB::at(row, col)) = v;
       }
+    }
+  };
+  // transform tables: built while the first tiles' loads are in flight, visible before the first store
+  auto stage_tables = [&]() {
+    if constexpr (XA || XB) {
+      if constexpr (XA) la.stage(xtab_a);
+      if constexpr (XB) lb.stage(xtab_b);
+      __syncthreads();
     }
   };
   auto compute = [&](const bf16* As, const bf16* Bs) {
@@ -198,14 +232,15 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
   const int nk = (kend - kbeg + BK - 1) / BK;
   if constexpr (RS == 1) {
     if (nk > 0) {
-      gload(kbeg, ra[0], rb[0]);
-      sstore(As0, Bs0, ra[0], rb[0]);
+      gload(kbeg, ra[0], rb[0], ta[0], tb[0]);
+      stage_tables();
+      sstore(As0, Bs0, ra[0], rb[0], ta[0], tb[0]);
       __syncthreads();
       for (int t = 0; t < nk; ++t) {
         const bool odd = t & 1;
-        if (t + 1 < nk) gload(kbeg + (t + 1) * BK, ra[0], rb[0]);
+        if (t + 1 < nk) gload(kbeg + (t + 1) * BK, ra[0], rb[0], ta[0], tb[0]);
         compute(odd ? As1 : As0, odd ? Bs1 : Bs0);
-        if (t + 1 < nk) sstore(odd ? As0 : As1, odd ? Bs0 : Bs1, ra[0], rb[0]);
+        if (t + 1 < nk) sstore(odd ? As0 : As1, odd ? Bs0 : Bs1, ra[0], rb[0], ta[0], tb[0]);
         __syncthreads();
       }
     }
@@ -215,17 +250,20 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
     if (nk > 0) {
 #pragma unroll
       for (int u = 0; u < RS; ++u)
-        if (u < nk) gload(kbeg + u * BK, ra[u], rb[u]);
-      sstore(As0, Bs0, ra[0], rb[0]);
+        if (u < nk) gload(kbeg + u * BK, ra[u], rb[u], ta[u], tb[u]);
+      stage_tables();
+      sstore(As0, Bs0, ra[0], rb[0], ta[0], tb[0]);
       __syncthreads();
       for (int t0 = 0; t0 < nk; t0 += RS) {
 #pragma unroll
         for (int u = 0; u < RS; ++u) {
           const int t = t0 + u;
           if (t < nk) {
-            if (t + RS < nk) gload(kbeg + (t + RS) * BK, ra[u], rb[u]);
+            if (t + RS < nk) gload(kbeg + (t + RS) * BK, ra[u], rb[u], ta[u], tb[u]);
             compute((t & 1) ? As1 : As0, (t & 1) ? Bs1 : Bs0);
-            if (t + 1 < nk) sstore((t & 1) ? As0 : As1, (t & 1) ? Bs0 : Bs1, ra[(u + 1) % RS], rb[(u + 1) % RS]);
+            if (t + 1 < nk)
+              sstore((t & 1) ? As0 : As1, (t & 1) ? Bs0 : Bs1, ra[(u + 1) % RS], rb[(u + 1) % RS], ta[(u + 1) % RS],
+                     tb[(u + 1) % RS]);
             __syncthreads();
           }
         }
@@ -234,21 +272,22 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
   } else {
     // LDS[t&1] holds tile t; register set (t+1)&1 holds tile t+1; tile t+2 loads into set t&1.
     if (nk > 0) {
-      gload(kbeg, ra[0], rb[0]);
-      if (nk > 1) gload(kbeg + BK, ra[1], rb[1]);
-      sstore(As0, Bs0, ra[0], rb[0]);
+      gload(kbeg, ra[0], rb[0], ta[0], tb[0]);
+      if (nk > 1) gload(kbeg + BK, ra[1], rb[1], ta[1], tb[1]);
+      stage_tables();
+      sstore(As0, Bs0, ra[0], rb[0], ta[0], tb[0]);
       __syncthreads();
       for (int t = 0; t < nk; t += 2) {
         // even step: compute LDS0 (tile t), regs1 = tile t+1, refill regs0 with tile t+2
-        if (t + 2 < nk) gload(kbeg + (t + 2) * BK, ra[0], rb[0]);
+        if (t + 2 < nk) gload(kbeg + (t + 2) * BK, ra[0], rb[0], ta[0], tb[0]);
         compute(As0, Bs0);
-        if (t + 1 < nk) sstore(As1, Bs1, ra[1], rb[1]);
+        if (t + 1 < nk) sstore(As1, Bs1, ra[1], rb[1], ta[1], tb[1]);
         __syncthreads();
         if (t + 1 >= nk) break;
         // odd step: compute LDS1 (tile t+1), regs0 = tile t+2, refill regs1 with tile t+3
-        if (t + 3 < nk) gload(kbeg + (t + 3) * BK, ra[1], rb[1]);
+        if (t + 3 < nk) gload(kbeg + (t + 3) * BK, ra[1], rb[1], ta[1], tb[1]);
         compute(As1, Bs1);
-        if (t + 2 < nk) sstore(As0, Bs0, ra[0], rb[0]);
+        if (t + 2 < nk) sstore(As0, Bs0, ra[0], rb[0], ta[0], tb[0]);
         __syncthreads();
       }
     }
@@ -285,6 +324,7 @@ __device__ __forceinline__ void gemm_block_oneshot(const LA& la, const LB& lb, c
   using TA = LdsTile<BM, BK, LA::KC>;
   using TB = LdsTile<BN, BK, LB::KC>;
   static_assert(BK % 32 == 0 && BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "tile shape");
+  static_assert(LoaderXF<LA>::BYTES == 0 && LoaderXF<LB>::BYTES == 0, "operand transforms: gemm_mainloop only");
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
   constexpr int CA = (TA::CHUNKS + NT - 1) / NT;
   constexpr int CB = (TB::CHUNKS + NT - 1) / NT;

@@ -20,7 +20,7 @@
 #include "../conv_kernels.h"
 #include "../gemm.h"
 #include "../gemm256.h"
-#include "../bn_totals.h"
+#include "../bn_affine.h"
 
 namespace tfd {
 namespace {
@@ -81,6 +81,7 @@ struct DenseX {
     const bool ok = mn < mn_lim && k < k_lim;
     return boff(KC ? (uint32_t)mn * ld + k : (uint32_t)k * ld + mn, ok);
   }
+  __device__ __forceinline__ int chan(int mn, int k) const { return KC ? k : mn; }  // [pixel][channel] operands
   TFD_LOADER_CALL
 };
 
@@ -97,6 +98,7 @@ struct FwdA {
     const bool ok = m < g.M && k < g.KD && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
     return boff((uint32_t)((n * g.H + h) * g.W + w) * g.C + c, ok);
   }
+  __device__ __forceinline__ int chan(int m, int k) const { return k - g.c.div(k) * g.C; }
   TFD_LOADER_CALL
 };
 
@@ -195,7 +197,51 @@ struct WgradA {
     const bool ok = t < g.M && m < g.KD && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
     return boff((uint32_t)((n * g.H + h) * g.W + w) * g.C + c, ok);
   }
+  __device__ __forceinline__ int chan(int t, int m) const { return t - g.c.div(t) * g.C; }
   TFD_LOADER_CALL
+};
+
+// ---- the producing layer's batch norm + relu, applied while staging (the forward BN fold) ----
+// A conv whose input is relu(bn(y)) of a single-consumer batch norm reads y itself and stages
+// relu(fmaf(y, sc, sh)) rounded to bf16 (bn_affine constants) -- bit for bit the bn_apply_kernel
+// output, which is then never written: one full read + write pass per such BN disappears, and the
+// weight gradient of the same conv rebuilds its X operand the same way. Chunks the loader zero-fills
+// (padding taps, tails) stay zero (tag -1). The per-channel (sc, sh) pairs live in an LDS table the
+// block builds once (gemm_mainloop's LoaderXF hook); C <= kBnReluMaxC.
+struct BnReluArgs {
+  const float *mean, *invstd, *gamma, *beta;
+  int C;
+};
+template <class L>
+struct BnRelu : L {
+  static constexpr int XF_BYTES = kBnReluMaxC * 8;
+  BnReluArgs bn;
+  __device__ __forceinline__ void stage(char* tab) const {
+    float2* t = reinterpret_cast<float2*>(tab);
+    for (int c = threadIdx.x; c < bn.C; c += blockDim.x) {
+      float sc, sh;
+      bn_affine(bn.mean[c], bn.invstd[c], bn.gamma[c], bn.beta[c], sc, sh);
+      t[c] = make_float2(sc, sh);
+    }
+  }
+  __device__ __forceinline__ uint4 load(int mn, int k, int& tag) const {
+    const uint32_t o = this->off(mn, k);
+    tag = o == kBufOOB ? -1 : this->chan(mn, k);
+    return rsrc_ld(this->rsrc(), o);
+  }
+  __device__ __forceinline__ uint4 xform(uint4 v, int tag, const char* tab) const {
+    const float4* t = reinterpret_cast<const float4*>(tab) + (max(tag, 0) >> 1);  // (sc, sh) x 2 per float4
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 p = t[i];
+      const float a = fmaxf(fmaf(__uint_as_float(w[i] << 16), p.x, p.y), 0.f);
+      const float b = fmaxf(fmaf(__uint_as_float(w[i] & 0xFFFF0000u), p.z, p.w), 0.f);
+      o[i] = tag < 0 ? 0u : pack_bf2(a, b);
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+  }
 };
 
 // ---- epilogues ----
@@ -319,7 +365,7 @@ template <int BM, int BN, int WM, int WN, bool ADD, bool STATS, class RM = RowId
 __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], char* smem, uint16_t* __restrict__ y,
                                              const uint16_t* __restrict__ add, int M, int N, int m0, int n0,
                                              float* __restrict__ part, RM rowmap = RM{}, uint32_t ybytes = 0,
-                                             int* tcnt = nullptr, int tG = 0, float* tot = nullptr, BS bs = BS{}) {
+                                             BS bs = BS{}) {
   using E = LdsEpi<BM, BN, WM, WN>;
   constexpr bool BSTAT = BS::MODE >= 0;
   static_assert(!(STATS && BSTAT), "one statistics kind per epilogue");
@@ -368,8 +414,7 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
       bmu[k] = bs.mean[nc + k];
       bis[k] = bs.invstd[nc + k];
       if constexpr (BS::MODE == 2) {
-        bsc[k] = bis[k] * bs.gamma[nc + k];
-        bsh[k] = bs.beta[nc + k] - bmu[k] * bsc[k];
+        bn_affine(bmu[k], bis[k], bs.gamma[nc + k], bs.beta[nc + k], bsc[k], bsh[k]);
       }
     }
   }
@@ -443,18 +488,9 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
       float a = 0.f, b = 0.f;
 #pragma unroll 8
       for (int g = 0; g < E::RG; ++g) { a += cs[g * BN + col]; b += cs[(E::RG + g) * BN + col]; }
-      if (tcnt) {  // handed to the last arriver in this launch: write-through stores
-        tot_store(part + (size_t)blockIdx.y * 2 * N + nn, a);
-        tot_store(part + (size_t)blockIdx.y * 2 * N + N + nn, b);
-      } else {
-        part[(size_t)blockIdx.y * 2 * N + nn] = a;
-        part[(size_t)blockIdx.y * 2 * N + N + nn] = b;
-      }
+      part[(size_t)blockIdx.y * 2 * N + nn] = a;
+      part[(size_t)blockIdx.y * 2 * N + N + nn] = b;
     }
-    // column totals in this launch (bn_totals.h): no separate BN finalize pass
-    if (tcnt)
-      totals_last_arriver<E::NT>(part, gridDim.y, blockIdx.y, N, n0, min(BN, N - n0), tG,
-                                 tcnt + blockIdx.x * kTotCntPerTile, tot, tot + N, reinterpret_cast<int*>(smem));
   }
 }
 
@@ -515,7 +551,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_bnb_kernel(LA la,
   gemm_mainloop<BM, BN, CBK, 2, 2, LA, LB, conv_rs<BM, BN>()>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
                                                        (bf16*)smem_raw, acc);
   lds_epilogue<BM, BN, 2, 2, ADD, false, RowId, BS>(acc, smem_raw, y, add, M, N, blockIdx.y * BM, blockIdx.x * BN, part,
-                                                    RowId{}, 0u, nullptr, 0, nullptr, bs);
+                                                    RowId{}, 0u, bs);
 }
 
 // Forward conv + BN statistics: the block's column partials (sum, sum of squares over its BM rows)
@@ -523,7 +559,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_bnb_kernel(LA la,
 // forward BN needs no separate pass over the conv output. Fixed reduction order (deterministic).
 template <int BM, int BN, class LA, class LB>
 __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB lb, uint16_t* y, int M, int N, int KD,
-                                                         float* part, int* tcnt, int tG, float* tot) {
+                                                         float* part) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   constexpr int WM = 2, WN = 2, WTN = BN / WN, TN = WTN / 16;
 #if TFD_CONV_LDS_EPI
@@ -531,10 +567,8 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB
   f32x4 acc[BM / 32][BN / 32];
   gemm_mainloop<BM, BN, CBK, WM, WN, LA, LB, conv_rs<BM, BN>()>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
                                                          (bf16*)smem_raw, acc);
-  lds_epilogue<BM, BN, WM, WN, false, true>(acc, smem_raw, y, nullptr, M, N, blockIdx.y * BM, blockIdx.x * BN, part,
-                                            RowId{}, 0u, tcnt, tG, tot);
+  lds_epilogue<BM, BN, WM, WN, false, true>(acc, smem_raw, y, nullptr, M, N, blockIdx.y * BM, blockIdx.x * BN, part);
 #else
-  (void)tcnt; (void)tG; (void)tot;
   float s[TN], q[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { s[j] = 0.f; q[j] = 0.f; }
@@ -585,8 +619,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void dgrad_phase_kernel(DgradPha
                                                                          la.g.KD, (bf16*)smem_raw, acc);
   const uint32_t xbytes = (uint32_t)la.g.N * la.g.H * la.g.W * la.g.C * 2u;
   lds_epilogue<BM, BN, 2, 2, ADD, false, PhaseRows, BS>(acc, smem_raw, dx, add, la.g.M, la.g.C, blockIdx.y * BM,
-                                                       blockIdx.x * BN, part, PhaseRows{la.g}, xbytes, nullptr, 0,
-                                                       nullptr, bs);
+                                                       blockIdx.x * BN, part, PhaseRows{la.g}, xbytes, bs);
 }
 
 // pixels of tap-less phases (a 1x1 stride-2 conv leaves 3 of 4 input pixels without a tap):
@@ -648,12 +681,7 @@ void launch_gemm_stats(const LA& la, const LB& lb, uint16_t* y, int M, int N, in
     attr = true;
   }
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, 1);
-  // column totals go to part row grid.y (conv_fwd_stats_rows counts it)
-  const bool tot = TFD_CONV_LDS_EPI && bn_totals_enabled();
-  if (tot && (int)grid.x > kTotMaxTiles) throw std::runtime_error("conv_fwd_stats: too many column tiles for the totals");
-  gemm_stats_kernel<BM, BN, LA, LB><<<grid, 256, sm, st>>>(la, lb, y, M, N, KD, part, tot ? bn_ticket_slot() : nullptr,
-                                                          tot ? bn_totals_group((int)grid.y) : 0,
-                                                          tot ? part + (size_t)grid.y * 2 * N : nullptr);
+  gemm_stats_kernel<BM, BN, LA, LB><<<grid, 256, sm, st>>>(la, lb, y, M, N, KD, part);
 }
 
 // same tile choice as dispatch(): 128x128 when that fills the chip
@@ -768,7 +796,7 @@ long g256_tiles(int M, int N) { return (long)((M + 255) / 256) * ((N + g256_bn(N
 // everywhere, 14.37 with the 256-row core wherever it had >= 256 tiles, 19.6 with it everywhere.
 bool use_g256(int M, int N) {
   const int mode = g256_mode();
-  if (mode == 0 || N % 8 || bn_totals_enabled()) return false;
+  if (mode == 0 || N % 8) return false;
   return mode == 2 || (N >= 1024 && g256_tiles(M, N) >= 32);
 }
 
@@ -808,8 +836,7 @@ __device__ __forceinline__ void g256_epilogue(f32x16 (&acc)[C::TM][C::TN], char*
       bmu[k] = bs.mean[nc + k];
       bis[k] = bs.invstd[nc + k];
       if constexpr (BS::MODE == 2) {
-        bsc[k] = bis[k] * bs.gamma[nc + k];
-        bsh[k] = bs.beta[nc + k] - bmu[k] * bsc[k];
+        bn_affine(bmu[k], bis[k], bs.gamma[nc + k], bs.beta[nc + k], bsc[k], bsh[k]);
       }
     }
   }
@@ -1013,10 +1040,22 @@ void g256_launch_wgrad(const SA& sa, const DenseX<false>& sb, float* dw, int M, 
 
 }  // namespace
 
-void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, hipStream_t st) {
+static BnReluArgs bn_relu_args(const ConvShape& c, const BnReluIn* act) {
+  if (c.C > kBnReluMaxC) throw std::runtime_error("conv: folded BN input with C > kBnReluMaxC");
+  return BnReluArgs{act->mean, act->invstd, act->gamma, act->beta, c.C};
+}
+
+void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, hipStream_t st,
+              const BnReluIn* act) {
   const int M = c.N * c.Ho() * c.Wo(), KD = c.R * c.S * c.C;
   StoreBf16 epi{y, M, c.K};
   DenseX<false> lb{w, c.K, c.K, KD};
+  if (act) {  // the 128-row core: its loaders stage through registers, where the transform happens
+    const BnReluArgs a = bn_relu_args(c, act);
+    if (is_pointwise(c)) dispatch_bf16(BnRelu<DenseX<true>>{{x, c.C, M, c.C}, a}, lb, y, nullptr, M, c.K, KD, st);
+    else dispatch_bf16(BnRelu<FwdA>{{x, make_geo(c, M, KD)}, a}, lb, y, nullptr, M, c.K, KD, st);
+    return;
+  }
   if (use_g256(M, c.K)) {  // A = im2col(X) (KC), B = HWIO weight (MNC)
     if (is_pointwise(c)) g256_launch_bf16<true, false, false, false>(DenseX<true>{x, c.C, M, c.C}, lb, y, nullptr, M, c.K, KD, nullptr, st);
     else g256_launch_bf16<true, false, false, false>(FwdA{x, make_geo(c, M, KD)}, lb, y, nullptr, M, c.K, KD, nullptr, st);
@@ -1033,18 +1072,17 @@ void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t
   }
 }
 
-int conv_fwd_stats_rows(const ConvShape& c) {  // row blocks (+ the totals row, see launch_gemm_stats)
+int conv_fwd_stats_rows(const ConvShape& c, bool folded) {  // row blocks of the partials
   const int M = c.N * c.Ho() * c.Wo();
-  if (use_g256(M, c.K)) return (M + 255) / 256;
-  const int rows = TFD_CONV_LDS_EPI ? out_tile_rows(M, c.K) : (use_big_tiles(M, c.K) ? (M + 127) / 128 : (M + 63) / 64);
-  return rows + (TFD_CONV_LDS_EPI && bn_totals_enabled() ? 1 : 0);
+  if (!folded && use_g256(M, c.K)) return (M + 255) / 256;
+  return TFD_CONV_LDS_EPI ? out_tile_rows(M, c.K) : (use_big_tiles(M, c.K) ? (M + 127) / 128 : (M + 63) / 64);
 }
 
 void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
-                    hipStream_t st) {
+                    hipStream_t st, const BnReluIn* act) {
   const int M = c.N * c.Ho() * c.Wo(), KD = c.R * c.S * c.C;
   DenseX<false> lb{w, c.K, c.K, KD};
-  if (use_g256(M, c.K)) {
+  if (!act && use_g256(M, c.K)) {
     if (is_pointwise(c)) g256_launch_bf16<true, false, false, true>(DenseX<true>{x, c.C, M, c.C}, lb, y, nullptr, M, c.K, KD, part, st);
     else g256_launch_bf16<true, false, false, true>(FwdA{x, make_geo(c, M, KD)}, lb, y, nullptr, M, c.K, KD, part, st);
     return;
@@ -1056,8 +1094,15 @@ void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, ui
     else if (t == OT128x64) launch_gemm_stats<128, 64, LA, DenseX<false>>(la, lb, y, M, c.K, KD, part, st);
     else launch_gemm_stats<64, 64, LA, DenseX<false>>(la, lb, y, M, c.K, KD, part, st);
   };
-  if (is_pointwise(c)) go(DenseX<true>{x, c.C, M, c.C});
-  else go(FwdA{x, make_geo(c, M, KD)});
+  if (act) {
+    const BnReluArgs a = bn_relu_args(c, act);
+    if (is_pointwise(c)) go(BnRelu<DenseX<true>>{{x, c.C, M, c.C}, a});
+    else go(BnRelu<FwdA>{{x, make_geo(c, M, KD)}, a});
+  } else if (is_pointwise(c)) {
+    go(DenseX<true>{x, c.C, M, c.C});
+  } else {
+    go(FwdA{x, make_geo(c, M, KD)});
+  }
 }
 
 template <class Epi>
@@ -1264,8 +1309,8 @@ static int g256_wgrad_splits(const ConvShape& c) {
   int s = (int)std::max<long>(1, 256 / std::max<long>(1, tiles));
   return std::min(s, std::max(1, P / 4096));
 }
-int conv_wgrad_splits(const ConvShape& c) {
-  if (use_g256_wgrad(c)) return g256_wgrad_splits(c);
+int conv_wgrad_splits(const ConvShape& c, bool folded) {
+  if (!folded && use_g256_wgrad(c)) return g256_wgrad_splits(c);
   // enough (tile x split) blocks to fill the chip; each split keeps >= TFD_WGRAD_MINPX pixels of K
   const int P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
   const WgTile t = wgrad_tile(c);
@@ -1287,11 +1332,17 @@ static void wgrad_launch(const ConvShape& c, const LA& la, const DenseX<false>& 
 }
 
 void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float* dw, int splits, hipStream_t st,
-                bool zeroed) {
+                bool zeroed, const BnReluIn* act) {
   const int P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
   if (splits > 1 && !zeroed) (void)hipMemsetAsync(dw, 0, (size_t)MT * c.K * sizeof(float), st);
   AccF32 epi{dw, MT, c.K, splits > 1 ? 1 : 0};
   DenseX<false> lb{dy, c.K, c.K, P};
+  if (act) {
+    const BnReluArgs a = bn_relu_args(c, act);
+    if (is_pointwise(c)) wgrad_launch(c, BnRelu<DenseX<false>>{{x, c.C, c.C, P}, a}, lb, epi, MT, P, splits, st);
+    else wgrad_launch(c, BnRelu<WgradA>{{x, make_geo(c, MT, P)}, a}, lb, epi, MT, P, splits, st);
+    return;
+  }
   if (use_g256_wgrad(c)) {  // A = im2col(X)^T, B = dY: both MNC
     if (is_pointwise(c)) g256_launch_wgrad(DenseX<false>{x, c.C, c.C, P}, lb, dw, MT, c.K, P, splits, st);
     else g256_launch_wgrad(WgradA{x, make_geo(c, MT, P)}, lb, dw, MT, c.K, P, splits, st);

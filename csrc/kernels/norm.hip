@@ -8,17 +8,12 @@
 #include "../common.h"
 #include "../conv_kernels.h"
 #include "../gemm.h"  // buf_ld
-#include "../bn_totals.h"
+#include "../bn_affine.h"
 
-// 1: statistics / BN parameter gradients summed in the producing launch by last-arriver tickets
-// (csrc/bn_totals.h) instead of the bn_final launch. Correct (tests pass with it on) but measured
-// SLOWER (ResNet-50 b128 13.98 -> 17.60 ms/step, profiles/resnet50_bn_totals_ab_r2.log): the
-// hand-off words must be read with write-through/sc1 loads (~2 us round trips to the Infinity
-// Cache) and the last group's reduction is a serial tail after every other block has finished --
-// 60-70 us per BN, against a 5-7 us finalize launch. Kept as the documented negative result.
-#ifndef TFD_BN_TOTALS
-#define TFD_BN_TOTALS 0
-#endif
+// (Round 2 measured a variant that summed the statistics in the producing launch by last-arriver
+// tickets instead of the bn_final launch: ResNet-50 b128 13.98 -> 17.60 ms/step, the hand-off words
+// need write-through / sc1 round trips and the last group's reduction is a serial tail after every
+// other block -- profiles/resnet50_bn_totals_ab_r2.log. Removed in round 4.)
 
 namespace tfd {
 namespace {
@@ -96,11 +91,9 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(const uint16_t* __restri
                                                         const float* __restrict__ invstd,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int M, int C, int tpr,
-                                                        int rg, int rb, float* __restrict__ part, int* tcnt, int tG,
-                                                        float* __restrict__ tot_a, float* __restrict__ tot_b,
+                                                        int rg, int rb, float* __restrict__ part,
                                                         const uint8_t* __restrict__ mbits) {
   __shared__ float red[2][NT][8];
-  __shared__ int tflag;
   const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
   const uint32_t nbytes = (uint32_t)M * (uint32_t)C * 2u;
   float sa[8], sb[8], mu[8], is[8], sc[8], sh[8];
@@ -111,10 +104,7 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(const uint16_t* __restri
     for (int j = 0; j < 8; ++j) {
       mu[j] = mean[c0 + j];
       is[j] = invstd[c0 + j];
-      if (MASK == 2) {
-        sc[j] = is[j] * gamma[c0 + j];
-        sh[j] = beta[c0 + j] - mu[j] * sc[j];
-      }
+      if (MASK == 2) bn_affine(mu[j], is[j], gamma[c0 + j], beta[c0 + j], sc[j], sh[j]);
     }
   }
   const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
@@ -180,15 +170,9 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(const uint16_t* __restri
   }
   if (g == 0) {
     float* pa = part + (size_t)blockIdx.x * 2 * C;
-    if (tcnt) {  // handed to the last arriver in this launch: write-through stores
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { tot_store(pa + c0 + j, sa[j]); tot_store(pa + C + c0 + j, sb[j]); }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { pa[c0 + j] = sa[j]; pa[C + c0 + j] = sb[j]; }
-    }
+    for (int j = 0; j < 8; ++j) { pa[c0 + j] = sa[j]; pa[C + c0 + j] = sb[j]; }
   }
-  if (tcnt) totals_last_arriver<NT>(part, gridDim.x, blockIdx.x, C, 0, C, tG, tcnt, tot_a, tot_b, &tflag);
 }
 
 // per-channel finalize, block = 32 channels x 32 partial-row groups (1024 threads: coalesced 128-B
@@ -243,58 +227,19 @@ __global__ __launch_bounds__(FIN_NT) void bn_final_kernel(int mode, const float*
 // row group); its 8 channels' constants stay in registers for every row it touches; RU rows' loads
 // per batch are issued before the first use (branch-free buffer loads, see bn_partial_kernel).
 // HAS_RES / RELU are compile-time so no load sits under a branch.
-// Totals mode (tot != nullptr: [2][C] column sums and sums of squares from the producing launch):
-// every block derives mean / invstd itself -- the finalize math of bn_final_kernel mode 0 -- and
-// block 0 stores them (saved for the backward) and updates the running statistics.
-struct BnTot {
-  const float* tot;
-  float eps, momentum;
-  float *mean, *invstd, *rmean, *rvar;
-};
-__device__ __forceinline__ void bn_stats_from_totals(const BnTot& b, int M, int C, int c0, bool store, float (&mu)[8],
-                                                     float (&is)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = c0 + j;
-    mu[j] = b.tot[c] / (float)M;
-    const float var = fmaxf(b.tot[C + c] / (float)M - mu[j] * mu[j], 0.f);
-    is[j] = rsqrtf(var + b.eps);
-    if (store) {
-      b.mean[c] = mu[j];
-      b.invstd[c] = is[j];
-      if (b.rmean) {
-        b.rmean[c] = b.rmean[c] * b.momentum + mu[j] * (1.f - b.momentum);
-        b.rvar[c] = b.rvar[c] * b.momentum + var * ((float)M / (float)max(M - 1, 1)) * (1.f - b.momentum);
-      }
-    }
-  }
-}
 template <bool HAS_RES, bool RELU>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, const float* __restrict__ mean,
                                                       const float* __restrict__ invstd,
                                                       const uint16_t* __restrict__ res,
                                                       uint16_t* __restrict__ out, int M, int C, int tpr, int rg, int rb,
-                                                      BnTot bt, uint8_t* __restrict__ mbits) {
+                                                      uint8_t* __restrict__ mbits) {
   const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
   if (g >= rg) return;
   const uint32_t nbytes = (uint32_t)M * (uint32_t)C * 2u;
   float sc[8], sh[8];
-  if (bt.tot) {
-    float mu[8], is[8];
-    bn_stats_from_totals(bt, M, C, c0, blockIdx.x == 0 && g == 0, mu, is);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sc[j] = is[j] * gamma[c0 + j];
-      sh[j] = beta[c0 + j] - mu[j] * sc[j];
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sc[j] = invstd[c0 + j] * gamma[c0 + j];
-      sh[j] = beta[c0 + j] - mean[c0 + j] * sc[j];
-    }
-  }
+  for (int j = 0; j < 8; ++j) bn_affine(mean[c0 + j], invstd[c0 + j], gamma[c0 + j], beta[c0 + j], sc[j], sh[j]);
   const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
   for (int rbase = r0 + g; rbase < r1; rbase += RU * rg) {
     uint4 Y[RU], Q[RU];
@@ -354,10 +299,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __rest
     k1[j] = gamma[c] * is;
     k2[j] = -k1[j] * is * dgamma[c] * invM;
     k3[j] = -k1[j] * (dbeta[c] * invM - mean[c] * is * dgamma[c] * invM);
-    if (MASK == 2) {
-      sc[j] = is * gamma[c];  // the forward's bn_apply constants (mask from y)
-      sh[j] = beta[c] - mean[c] * sc[j];
-    }
+    if (MASK == 2) bn_affine(mean[c], is, gamma[c], beta[c], sc[j], sh[j]);  // the forward's constants (mask from y)
   }
   const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
   for (int rbase = r0 + g; rbase < r1; rbase += RU * rg) {
@@ -571,83 +513,46 @@ inline int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64
 
 void launch_apply(const uint16_t* y, const float* gamma, const float* beta, const float* mean, const float* invstd,
                   const uint16_t* res, int relu, uint16_t* out, int M, int C, const RowSplit& r, hipStream_t st,
-                  BnTot bt = BnTot{nullptr, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr}, uint8_t* mb = nullptr) {
-  if (res && relu) bn_apply_kernel<true, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, bt, mb);
-  else if (res) bn_apply_kernel<true, false><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, bt, mb);
-  else if (relu) bn_apply_kernel<false, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, bt, mb);
-  else bn_apply_kernel<false, false><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, bt, mb);
-}
-
-// group size of the two-level ticket reduction: ~sqrt(rows) rows per group, <= kTotMaxGroups groups
-int tot_group(int nrows) {
-  int g = 8;
-  while (g * g < nrows) ++g;
-  while ((nrows + g - 1) / g > kTotMaxGroups) ++g;
-  return g;
+                  uint8_t* mb = nullptr) {
+  if (res && relu) bn_apply_kernel<true, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, mb);
+  else if (res) bn_apply_kernel<true, false><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, mb);
+  else if (relu) bn_apply_kernel<false, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, mb);
+  else bn_apply_kernel<false, false><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, mb);
 }
 
 }  // namespace
 
-int* bn_ticket_slot() {
-  static int* ws[64] = {nullptr};
-  static unsigned next[64] = {0};
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (dev < 0 || dev >= 64) throw std::runtime_error("bn_ticket_slot: device index");
-  if (!ws[dev]) {
-    const size_t bytes = (size_t)kTotSlots * kTotMaxTiles * kTotCntPerTile * sizeof(int);
-    if (hipMalloc(&ws[dev], bytes) != hipSuccess || hipMemset(ws[dev], 0, bytes) != hipSuccess ||
-        hipDeviceSynchronize() != hipSuccess)
-      throw std::runtime_error("bn_ticket_slot: workspace allocation failed");
-  }
-  return ws[dev] + (size_t)(next[dev]++ % kTotSlots) * kTotMaxTiles * kTotCntPerTile;
-}
-
-bool bn_totals_enabled() { return TFD_BN_TOTALS != 0; }
-int bn_totals_group(int nrows) { return tot_group(nrows); }
-
 int bn_partials_size(int M, int C) {
   const RowSplit r = row_split(M, C);
-  return (r.nblk + 1) * 2 * C;  // + the totals row
+  return r.nblk * 2 * C;
 }
 
 void bn_forward(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
                 uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var, float momentum,
                 float eps, int M, int C, float* partials, hipStream_t st, uint8_t* mask_bits) {
   const RowSplit r = row_split(M, C);
-  if (TFD_BN_TOTALS) {
-    float* tot = partials + (size_t)r.nblk * 2 * C;
-    bn_partial_kernel<0, 0><<<r.nblk, NT, 0, st>>>(y, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, C, r.tpr,
-                                                   r.rg, r.rb, partials, bn_ticket_slot(), tot_group(r.nblk), tot,
-                                                   tot + C, nullptr);
-    launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st,
-                 BnTot{tot, eps, momentum, mean, invstd, running_mean, running_var}, mask_bits);
-    return;
-  }
   bn_partial_kernel<0, 0><<<r.nblk, NT, 0, st>>>(y, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, C, r.tpr,
-                                                 r.rg, r.rb, partials, nullptr, 0, nullptr, nullptr, nullptr);
+                                                 r.rg, r.rb, partials, nullptr);
   bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, r.nblk, M, C, eps, momentum, mean, invstd,
                                                 running_mean, running_var);
-  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st,
-               BnTot{nullptr, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr}, mask_bits);
+  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st, mask_bits);
 }
 
-// partials: [nrows][2][C] from conv_fwd_stats; with TFD_BN_TOTALS its last row holds the column totals
+// partials: [nrows][2][C] from conv_fwd_stats
 void bn_forward_partials(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
                          uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var,
                          float momentum, float eps, int M, int C, const float* partials, int nrows, hipStream_t st,
                          uint8_t* mask_bits) {
   const RowSplit r = row_split(M, C);
-  if (TFD_BN_TOTALS) {
-    launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st,
-                 BnTot{partials + (size_t)(nrows - 1) * 2 * C, eps, momentum, mean, invstd, running_mean, running_var},
-                 mask_bits);
-    return;
-  }
   bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, nrows, M, C, eps, momentum, mean, invstd,
                                                 running_mean, running_var);
-  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st,
-               BnTot{nullptr, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr}, mask_bits);
+  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st, mask_bits);
+}
+
+void bn_stats_partials(float* mean, float* invstd, float* running_mean, float* running_var, float momentum, float eps,
+                       int M, int C, const float* partials, int nrows, hipStream_t st) {
+  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, nrows, M, C, eps, momentum, mean, invstd,
+                                                running_mean, running_var);
 }
 
 void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* beta,
@@ -658,16 +563,10 @@ void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, c
   // mask_bits given: the forward's relu bits, `out` is not read
   const int mask = !relu ? 0 : (mask_bits ? 3 : (beta ? 2 : 1));
 #define TFD_BN_BWD(MK)                                                                                          \
-  if (TFD_BN_TOTALS) {  /* dbeta / dgamma summed by the partial kernel's last arrivers */                      \
-    bn_partial_kernel<1, MK><<<r.nblk, NT, 0, st>>>(y, dout, out, mean, invstd, gamma, beta, M, C, r.tpr, r.rg,   \
-                                                    r.rb, partials, bn_ticket_slot(), tot_group(r.nblk), dbeta,  \
-                                                    dgamma, mask_bits);                                          \
-  } else {                                                                                                      \
-    bn_partial_kernel<1, MK><<<r.nblk, NT, 0, st>>>(y, dout, out, mean, invstd, gamma, beta, M, C, r.tpr, r.rg,   \
-                                                    r.rb, partials, nullptr, 0, nullptr, nullptr, mask_bits);    \
-    bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,\
-                                                  nullptr);                                                     \
-  }                                                                                                             \
+  bn_partial_kernel<1, MK><<<r.nblk, NT, 0, st>>>(y, dout, out, mean, invstd, gamma, beta, M, C, r.tpr, r.rg,     \
+                                                  r.rb, partials, mask_bits);                                    \
+  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,  \
+                                                nullptr);                                                       \
   bn_bwd_apply_kernel<MK><<<r.nblk, NT, 0, st>>>(dout, out, y, gamma, beta, mean, invstd, dbeta, dgamma, dy, dres, M, \
                                                  C, r.tpr, r.rg, r.rb, 1.f / (float)M, mask_bits);
   if (mask == 0) { TFD_BN_BWD(0) }

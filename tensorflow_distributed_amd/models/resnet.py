@@ -266,6 +266,64 @@ class _Conv(torch.autograd.Function):
         return dx, None, None
 
 
+class _BNReluConv(torch.autograd.Function):
+    """relu(bn(y)) -> conv with the batch norm applied by the conv's operand loader (the forward BN
+    fold, ``conv2d_fwd(..., mean, invstd, gamma, beta)``): the normalised activation is never written.
+    The BN here is a residual-free relu BN whose output has this conv as its only consumer (a
+    bottleneck's bn1 -> conv2 and bn2 -> conv3, a basic block's bn1 -> conv2). Its statistics come
+    from the producing conv's epilogue partials (``bn_stats``: the finalize only, no apply pass); the
+    backward rebuilds the conv's X operand the same way in the weight-gradient loader, takes the
+    BN-backward partials from the dgrad epilogue (relu mask recomputed from y) and runs the BN
+    backward -- the unfused _BN + _Conv pair, minus one full read + write of the activation per BN.
+    Bit-identical forward (same bn_affine constants, same fmaf + relu + rounding)."""
+
+    @staticmethod
+    def forward(ctx, y, token, part, bn, conv):
+        o = _ops()
+        mean, invstd = o.bn_stats(y, part, bn.rmean, bn.rvar, bn.momentum, bn.eps)
+        bn.fwd_state = (y, mean, invstd, None, True, False)
+        ctx.bn, ctx.conv = bn, conv
+        ctx.save_for_backward(y, mean, invstd)
+        act = (mean, invstd, bn.gamma(), bn.beta())
+        if conv.model.bn_stats:
+            out, p2 = o.conv2d_fwd_stats(y, conv.w(), conv.stride, conv.pad, *act)
+            ctx.mark_non_differentiable(p2)
+            ctx.set_materialize_grads(False)
+            return out, p2
+        return o.conv2d_fwd(y, conv.w(), conv.stride, conv.pad, *act)
+
+    @staticmethod
+    def backward(ctx, dout, *_dpart):
+        y, mean, invstd = ctx.saved_tensors
+        bn, L = ctx.bn, ctx.conv
+        o = _ops()
+        dout = dout.contiguous()
+        o.conv2d_wgrad(y, dout, L.g(), L.stride, L.pad, L.model.grads_zeroed, mean, invstd, bn.gamma(), bn.beta())
+        L.model.reducer.mark_ready(L.name)
+        if _bn_stats_fusable(L, bn):  # the BN output's gradient + its backward statistics partials
+            dbn = _dgrad_bn(dout, L, list(y.shape), None, bn)
+        else:
+            dbn = o.conv2d_dgrad(dout, L.w(), list(y.shape), L.stride, L.pad)
+        part, bn.bwd_part = bn.bwd_part, None
+        bn.fwd_state = None
+        # relu mask recomputed from y (beta given); `out` is never read
+        dy, _ = o.bn_bwd(dbn, y, y, bn.gamma(), mean, invstd, True, False, bn.g_gamma(), bn.g_beta(), bn.beta(), None,
+                         part)
+        L.model.reducer.mark_ready(bn.name + "/gamma")
+        L.model.reducer.mark_ready(bn.name + "/beta")
+        return dy, None, None, None, None
+
+
+_FOLD_MAX_C = None
+
+
+def _fold_max_c() -> int:
+    global _FOLD_MAX_C
+    if _FOLD_MAX_C is None:
+        _FOLD_MAX_C = int(_ops().bn_relu_max_channels())
+    return _FOLD_MAX_C
+
+
 class _BN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, res, layer, relu, part=None):
@@ -379,6 +437,15 @@ class ConvLayer:
     def __call__(self, x):
         return _Conv.apply(x, self.model.token, self)
 
+    def after_bn(self, bn, yp):
+        """This conv applied to relu(bn(y)) where ``yp`` is the (y, partials) pair of the producing
+        conv: folded when the model allows it (ResNet(fold_bn=True)), else bn then conv."""
+        m = self.model
+        if m.fold_bn and m.mask_from_y and isinstance(yp, tuple) and bn.c <= _fold_max_c():
+            y, part = yp
+            return _BNReluConv.apply(y, m.token, part, bn, self)
+        return self(bn(yp))
+
 
 class BNLayer:
     def __init__(self, model, name, c, zero_init=False):
@@ -441,7 +508,7 @@ class ResNet:
 
     def __init__(self, depth: int = 50, num_classes: int = 1000, device=None, seed: int = 0, width: int = 64,
                  zero_init_residual: bool = True, fuse_joins: bool = True, bn_stats: bool = True,
-                 bn_bwd_stats: bool = True):
+                 bn_bwd_stats: bool = True, fold_bn: bool = True):
         kind, blocks = self.CFG[depth]
         if num_classes % 8 or width % 8:
             raise ValueError("num_classes and width must be multiples of 8 (16-byte MFMA operand chunks)")
@@ -465,6 +532,9 @@ class ResNet:
         self.mask_from_y = True
         # residual BN keeps its relu mask as bits for the backward instead of re-reading the output
         self.relu_bits = True
+        # single-consumer relu BNs applied inside the consuming conv's operand loader (_BNReluConv);
+        # False keeps the separate bn_apply pass (the test oracle)
+        self.fold_bn = fold_bn
         cin = width
         exp = 4 if kind == "bottleneck" else 1
         prev_out_bn = None  # the BN that produced the current block input (None: the stem's maxpool)
@@ -529,18 +599,19 @@ class ResNet:
         x = self.stem_bn(self.stem(x))
         x = _MaxPool.apply(x, 3, 2, 1)
         for blk in self.blocks:
-            sc = x
-            if "cd" in blk:
-                sc = blk["bd"](blk["cd"](x), relu=False)
-            if self.kind == "basic":
-                h = blk["b1"](blk["c1"](x))
-                x = blk["b2"](blk["c2"](h), relu=True, res=sc)
-            else:
-                h = blk["b1"](blk["c1"](x))
-                h = blk["b2"](blk["c2"](h))
-                x = blk["b3"](blk["c3"](h), relu=True, res=sc)
+            x = self.block_forward(blk, x)
         x = _AvgPool.apply(x)
         return self.fc(x)
+
+    def block_forward(self, blk, x):
+        sc = x
+        if "cd" in blk:
+            sc = blk["bd"](blk["cd"](x), relu=False)
+        h = blk["c2"].after_bn(blk["b1"], blk["c1"](x))
+        if self.kind == "basic":
+            return blk["b2"](h, relu=True, res=sc)
+        h = blk["c3"].after_bn(blk["b2"], h)
+        return blk["b3"](h, relu=True, res=sc)
 
     def loss(self, x, labels):
         logits = self.forward(x)

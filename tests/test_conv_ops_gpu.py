@@ -99,6 +99,46 @@ def test_conv_fwd_stats_feeds_bn(cuda, N, H, W, C, K, R, st, pad):
     assert relerr(o1, o0) < 1e-2
 
 
+# forward BN fold: padded 3x3 (zero taps must stay zero after the affine + relu), strided 3x3,
+# 1x1, a channel count that is not a multiple of the 64-wide K tile, 128x128 / 128x64 output tiles
+@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", [(2, 9, 7, 16, 24, 3, 1, 1), (2, 10, 10, 16, 32, 3, 2, 1),
+                                               (3, 8, 8, 40, 16, 1, 1, 0), (48, 28, 28, 64, 128, 1, 1, 0),
+                                               (48, 28, 28, 32, 64, 3, 1, 1), (4, 14, 14, 512, 64, 3, 1, 1)])
+def test_conv_folded_bn_input_is_bit_identical(cuda, N, H, W, C, K, R, st, pad):
+    """conv2d_fwd / conv2d_fwd_stats / conv2d_wgrad with the input's batch norm + relu applied by the
+    operand loader (mean, invstd, gamma, beta passed) against the same ops on bn_fwd's materialised
+    output: bit-identical outputs, statistics partials and weight gradients."""
+    torch.manual_seed(7)
+    ops.conv_gemm_core(0)  # the folded form always takes the 128-row core (the fixture restores the mode)
+    y = rb(torch.randn(N, H, W, C) * 2 + 0.3).to(cuda, torch.bfloat16)
+    w = rb(torch.randn(R, R, C, K) * 0.2).to(cuda, torch.bfloat16)
+    g, b = (torch.rand(C) + 0.5).to(cuda), torch.randn(C).to(cuda)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    out, mean, invstd = ops.bn_fwd(y, g, b, None, True, rm, rv, 0.9, 1e-5)
+    assert (out.float() == 0).any() and (out.float() > 0).any()  # the relu acts
+    act = (mean, invstd, g, b)
+    y0 = ops.conv2d_fwd(out, w, st, pad)
+    assert torch.equal(ops.conv2d_fwd(y, w, st, pad, *act), y0)
+    y1, p1 = ops.conv2d_fwd_stats(out, w, st, pad)
+    y2, p2 = ops.conv2d_fwd_stats(y, w, st, pad, *act)
+    assert torch.equal(y2, y1) and torch.equal(y2, y0) and torch.equal(p2, p1)
+    dy = rb(torch.randn(N, y0.shape[1], y0.shape[2], K)).to(cuda, torch.bfloat16)
+    dw0, dw1 = torch.zeros(R, R, C, K, device=cuda), torch.zeros(R, R, C, K, device=cuda)
+    ops.conv2d_wgrad(out, dy, dw0, st, pad, True)
+    ops.conv2d_wgrad(y, dy, dw1, st, pad, True, *act)
+    torch.testing.assert_close(dw1, dw0, rtol=1e-5, atol=1e-5)  # split-K atomics: order may differ
+    # bn_stats: the finalize alone, same statistics and running-stat update as bn_fwd
+    rm2, rv2 = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    yk, pk = ops.conv2d_fwd_stats(y, w, st, pad)
+    m3, i3 = ops.bn_stats(yk, pk, rm2, rv2, 0.9, 1e-5)
+    rm3, rv3 = torch.zeros(K, device=cuda), torch.ones(K, device=cuda)
+    _, m4, i4 = ops.bn_fwd(yk, torch.ones(K, device=cuda), torch.zeros(K, device=cuda), None, False, rm3, rv3, 0.9, 1e-5,
+                           pk)
+    assert torch.equal(m3, m4) and torch.equal(i3, i4) and torch.equal(rm2, rm3) and torch.equal(rv2, rv3)
+    with pytest.raises(RuntimeError):
+        ops.conv2d_fwd(y, w, st, pad, mean, invstd, g, None)
+
+
 def test_linear(cuda):
     torch.manual_seed(1)
     M, Kin, N = 24, 64, 40
@@ -166,8 +206,7 @@ def test_batchnorm_train(cuda, relu, res):
 @pytest.mark.parametrize("M,C", [(100000, 64), (20000, 520)])
 def test_batchnorm_totals_many_groups(cuda, M, C):
     """Large M (1024 partial rows): statistics and dgamma/dbeta against fp64 sums, bit-identical when
-    repeated (fixed summation order) -- with TFD_BN_TOTALS=1 builds this covers the two-level
-    last-arriver reduction (32 groups, csrc/bn_totals.h)."""
+    repeated (fixed summation order)."""
     torch.manual_seed(6)
     y = rb(torch.randn(M, C) * 2 + 0.5)
     g, b = torch.rand(C) + 0.5, torch.randn(C)

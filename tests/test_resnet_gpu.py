@@ -95,12 +95,7 @@ def test_resnet_block_forward_backward(cuda, depth, bi, hw):
     cin = m.fp.by_name[blk["c1"].name].shape[2]
     x = torch.randn(4, hw, hw, cin).to(torch.bfloat16).float()
     xn = x.to(cuda, torch.bfloat16).requires_grad_(True)
-    sc = blk["bd"](blk["cd"](xn), relu=False) if "cd" in blk else xn
-    if m.kind == "basic":
-        out = blk["b2"](blk["c2"](blk["b1"](blk["c1"](xn))), relu=True, res=sc)
-    else:
-        t = blk["b2"](blk["c2"](blk["b1"](blk["c1"](xn))))
-        out = blk["b3"](blk["c3"](t), relu=True, res=sc)
+    out = m.block_forward(blk, xn)
     g = torch.randn(out.shape).to(torch.bfloat16).float()
     out.backward(g.to(cuda, torch.bfloat16))
     torch.cuda.synchronize()
@@ -325,3 +320,40 @@ def test_bn_bwd_stats_in_dgrad_epilogue(cuda, depth, monkeypatch):
     rel = ((g1 - g0).norm() / g0.norm()).item()
     assert rel < 1e-2, rel
     assert ("from_y", False) in kinds and ("bits", True) in kinds, kinds
+
+
+@pytest.mark.parametrize("depth", [18, 50])
+def test_folded_bn_matches_unfused(cuda, depth):
+    """The forward BN fold (single-consumer relu BNs applied inside the consuming conv's operand
+    loader, _BNReluConv) against the separate bn_apply pass (fold_bn=False, the oracle): the same loss,
+    running statistics and parameter gradients -- bit for bit (same constants, same rounding; only
+    split-K weight-gradient atomics could reorder fp32 adds)."""
+    from tensorflow_distributed_amd.models import resnet as R
+
+    calls = []
+    orig = R._BNReluConv.forward
+
+    def spy(ctx, *a):
+        calls.append(1)
+        return orig(ctx, *a)
+
+    torch.manual_seed(depth + 1)
+    x = torch.randn(4, 32, 32, 3, device=cuda)
+    lab = torch.randint(0, 16, (4,), dtype=torch.int32, device=cuda)
+    out = []
+    for fold in (False, True):
+        m = R.ResNet(depth, num_classes=16, device=cuda, seed=3, width=16, zero_init_residual=False, fold_bn=fold)
+        R._BNReluConv.forward = staticmethod(spy) if fold else staticmethod(orig)
+        try:
+            m.fp.grad.zero_()
+            loss, _ = m.loss(x, lab)
+            loss.backward()
+        finally:
+            R._BNReluConv.forward = staticmethod(orig)
+        torch.cuda.synchronize()
+        out.append((loss.item(), m.fp.grad.clone(), torch.cat([torch.cat([b.rmean, b.rvar]) for b in m.bns])))
+    nfold = len(m.blocks) * (1 if depth == 18 else 2)
+    assert len(calls) == nfold, (len(calls), nfold)
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][2], out[1][2])
+    torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-5, atol=1e-6)
