@@ -128,7 +128,7 @@ def test_conv_folded_bn_input_is_bit_identical(cuda, N, H, W, C, K, R, st, pad):
     ops.conv2d_wgrad(y, dy, dw1, st, pad, True, *act)
     torch.testing.assert_close(dw1, dw0, rtol=1e-5, atol=1e-5)  # split-K atomics: order may differ
     # bn_stats: the finalize alone, same statistics and running-stat update as bn_fwd
-    rm2, rv2 = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    rm2, rv2 = torch.zeros(K, device=cuda), torch.ones(K, device=cuda)
     yk, pk = ops.conv2d_fwd_stats(y, w, st, pad)
     m3, i3 = ops.bn_stats(yk, pk, rm2, rv2, 0.9, 1e-5)
     rm3, rv3 = torch.zeros(K, device=cuda), torch.ones(K, device=cuda)
