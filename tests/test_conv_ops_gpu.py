@@ -126,7 +126,7 @@ def test_conv_folded_bn_input_is_bit_identical(cuda, N, H, W, C, K, R, st, pad):
     dw0, dw1 = torch.zeros(R, R, C, K, device=cuda), torch.zeros(R, R, C, K, device=cuda)
     ops.conv2d_wgrad(out, dy, dw0, st, pad, True)
     ops.conv2d_wgrad(y, dy, dw1, st, pad, True, *act)
-    torch.testing.assert_close(dw1, dw0, rtol=1e-5, atol=1e-5)  # split-K atomics: order may differ
+    assert relerr(dw1, dw0) < 1e-5  # split-K atomics: the fp32 add order may differ
     # bn_stats: the finalize alone, same statistics and running-stat update as bn_fwd
     rm2, rv2 = torch.zeros(K, device=cuda), torch.ones(K, device=cuda)
     yk, pk = ops.conv2d_fwd_stats(y, w, st, pad)
