@@ -50,7 +50,7 @@ def main(argv=None):
     ap.add_argument("--bn_bwd_stats", type=int, default=1, help="1: batch-norm backward statistics summed in the "
                     "epilogue of the dgrad that produces the BN's gradient (no separate partial pass)")
     ap.add_argument("--fold_bn", type=int, default=1, help="1: single-consumer relu batch norms applied inside the "
-                    "consuming conv's operand loader (no bn_apply pass; 0: the separate pass)")
+                    "consuming conv's operand loader (no bn_apply pass; 0: the separate pass; 2: 1x1 consumers only)")
     ap.add_argument("--lr", type=float, default=0.1)
     argv = list(sys.argv[1:] if argv is None else argv)
     a = ap.parse_args(argv)
@@ -70,7 +70,7 @@ def main(argv=None):
     spawn.check_world(a.gpus, ctx.world)
     dev = ctx.device
     m = ResNet(a.depth, num_classes=1000, device=dev, seed=0, fuse_joins=bool(a.fuse_joins),
-               bn_stats=bool(a.bn_stats), bn_bwd_stats=bool(a.bn_bwd_stats), fold_bn=bool(a.fold_bn))
+               bn_stats=bool(a.bn_stats), bn_bwd_stats=bool(a.bn_bwd_stats), fold_bn=a.fold_bn)
     m.mask_from_y = bool(a.mask_from_y)
     m.relu_bits = bool(a.relu_bits)
     comm, transport = None, "none"

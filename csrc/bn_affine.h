@@ -6,12 +6,29 @@
 // applied bit for bit.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stdint.h>
 
 namespace tfd {
 
 __device__ __forceinline__ void bn_affine(float mean, float invstd, float gamma, float beta, float& sc, float& sh) {
   sc = invstd * gamma;
   sh = fmaf(-mean, sc, beta);
+}
+
+// relu(y * sc + sh) of two bf16 values packed in a dword (low half = the lower channel), as packed
+// math: v_pk_fma_f32, one v_cvt_pk_bf16_f32 (RNE), and the relu as v_pk_max_i16 against 0 on the
+// rounded bf16 bits (a negative bf16 is a negative int16; -0 -> +0) -- equal to rounding fmaxf(z, 0)
+// for every non-NaN z. bn_apply_kernel and the folded conv loaders both use it, so the two forms
+// of a relu BN output agree bit for bit.
+typedef float bn_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bn_bf16x2 __attribute__((ext_vector_type(2)));
+typedef short bn_s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t bn_relu2(uint32_t w, bn_f32x2 sc, bn_f32x2 sh) {
+  const bn_f32x2 y = {__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u)};
+  const bn_f32x2 z = __builtin_elementwise_fma(y, sc, sh);
+  bn_s16x2 b = __builtin_bit_cast(bn_s16x2, __builtin_convertvector(z, bn_bf16x2));
+  b = __builtin_elementwise_max(b, (bn_s16x2){0, 0});
+  return __builtin_bit_cast(uint32_t, b);
 }
 
 }  // namespace tfd

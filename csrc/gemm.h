@@ -102,9 +102,10 @@ __device__ __forceinline__ bf16x8 frag_tr16(const bf16* p0, const bf16* p1) {
 }
 
 // Operand transforms: a loader that declares `static constexpr int XF_BYTES` still travels
-// global -> registers -> LDS, but gload keeps a per-chunk tag (v = ld.load(mn, k, tag)) and the LDS
-// store writes ld.xform(v, tag, table) instead of v; ld.stage(table) fills the loader's XF_BYTES-byte
-// LDS table (placed after the operand images) once per block, before the first store. Used by the
+// global -> registers -> LDS, but gload keeps a per-chunk tag (v = ld.load(mn, k, tag)) and before
+// the LDS store ld.xform(v[], tag[], table) rewrites the thread's chunks of the K-tile in place;
+// ld.stage(table) fills the loader's XF_BYTES-byte LDS table (placed after the operand images) once
+// per block, before the first store. Used by the
 // conv loaders that apply the producing layer's batch norm + relu while staging their input
 // (csrc/kernels/conv_nhwc.hip BnRelu).
 template <class L, class = void>
@@ -183,16 +184,25 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
       }
     }
   };
+  // a transform sees all of the thread's chunks at once: they share the LDS column `col` (the asserts),
+  // so a per-channel transform looks its constants up once per K-tile
+  static_assert(!XA || (CA * NT == TA::CHUNKS && NT % TA::CH_PER_ROW == 0), "XF layout (A)");
+  static_assert(!XB || (CB * NT == TB::CHUNKS && NT % TB::CH_PER_ROW == 0), "XF layout (B)");
   auto sstore = [&](bf16* As, bf16* Bs, const uint4 (&xa)[CA], const uint4 (&xb)[CB], const int (&ga)[CA],
                     const int (&gb)[CB]) {
+    uint4 va[CA], vb[CB];
+#pragma unroll
+    for (int c = 0; c < CA; ++c) va[c] = xa[c];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) vb[c] = xb[c];
+    if constexpr (XA) la.xform(va, ga, xtab_a);
+    if constexpr (XB) lb.xform(vb, gb, xtab_b);
 #pragma unroll
     for (int c = 0; c < CA; ++c) {
       const int idx = tid + c * NT;
       if (CA * NT == TA::CHUNKS || idx < TA::CHUNKS) {
         const int row = idx / TA::CH_PER_ROW, col = (idx % TA::CH_PER_ROW) * 8;
-        uint4 v = xa[c];
-        if constexpr (XA) v = la.xform(v, ga[c], xtab_a);
-        *reinterpret_cast<uint4*>(As + TA::at(row, col)) = v;
+        *reinterpret_cast<uint4*>(As + TA::at(row, col)) = va[c];
       }
     }
 #pragma unroll
@@ -200,9 +210,7 @@ __device__ __forceinline__ void gemm_mainloop(const LA& la, const LB& lb, int m0
       const int idx = tid + c * NT;
       if (CB * NT == TB::CHUNKS || idx < TB::CHUNKS) {
         const int row = idx / TB::CH_PER_ROW, col = (idx % TB::CH_PER_ROW) * 8;
-        uint4 v = xb[c];
-        if constexpr (XB) v = lb.xform(v, gb[c], xtab_b);
-        *reinterpret_cast<uint4*>(Bs + TB::at(row, col)) = v;
+        *reinterpret_cast<uint4*>(Bs + TB::at(row, col)) = vb[c];
       }
     }
   };

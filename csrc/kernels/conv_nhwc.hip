@@ -216,12 +216,14 @@ template <class L>
 struct BnRelu : L {
   static constexpr int XF_BYTES = kBnReluMaxC * 8;
   BnReluArgs bn;
+  // table: [C/2] x {sc[2i], sc[2i+1], sh[2i], sh[2i+1]} (one float4 per channel pair: bn_relu2 operands)
   __device__ __forceinline__ void stage(char* tab) const {
-    float2* t = reinterpret_cast<float2*>(tab);
-    for (int c = threadIdx.x; c < bn.C; c += blockDim.x) {
-      float sc, sh;
-      bn_affine(bn.mean[c], bn.invstd[c], bn.gamma[c], bn.beta[c], sc, sh);
-      t[c] = make_float2(sc, sh);
+    float4* t = reinterpret_cast<float4*>(tab);
+    for (int i = threadIdx.x; 2 * i < bn.C; i += blockDim.x) {
+      float4 e;
+      bn_affine(bn.mean[2 * i], bn.invstd[2 * i], bn.gamma[2 * i], bn.beta[2 * i], e.x, e.z);
+      bn_affine(bn.mean[2 * i + 1], bn.invstd[2 * i + 1], bn.gamma[2 * i + 1], bn.beta[2 * i + 1], e.y, e.w);
+      t[i] = e;
     }
   }
   __device__ __forceinline__ uint4 load(int mn, int k, int& tag) const {
@@ -229,18 +231,24 @@ struct BnRelu : L {
     tag = o == kBufOOB ? -1 : this->chan(mn, k);
     return rsrc_ld(this->rsrc(), o);
   }
-  __device__ __forceinline__ uint4 xform(uint4 v, int tag, const char* tab) const {
-    const float4* t = reinterpret_cast<const float4*>(tab) + (max(tag, 0) >> 1);  // (sc, sh) x 2 per float4
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint32_t o[4];
+  // all N chunks of a thread share one 8-channel group (gemm_mainloop asserts the layout), so the
+  // group's constants are read once per K-tile: 4 ds_read_b128, then 24 VALU per chunk
+  template <int N>
+  __device__ __forceinline__ void xform(uint4 (&v)[N], const int (&tag)[N], const char* tab) const {
+    int ch = tag[0];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float4 p = t[i];
-      const float a = fmaxf(fmaf(__uint_as_float(w[i] << 16), p.x, p.y), 0.f);
-      const float b = fmaxf(fmaf(__uint_as_float(w[i] & 0xFFFF0000u), p.z, p.w), 0.f);
-      o[i] = tag < 0 ? 0u : pack_bf2(a, b);
+    for (int c = 1; c < N; ++c) ch = max(ch, tag[c]);
+    const float4* t = reinterpret_cast<const float4*>(tab) + (max(ch, 0) >> 1);
+    const float4 t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+      uint4 o;
+      o.x = bn_relu2(v[c].x, (bn_f32x2){t0.x, t0.y}, (bn_f32x2){t0.z, t0.w});
+      o.y = bn_relu2(v[c].y, (bn_f32x2){t1.x, t1.y}, (bn_f32x2){t1.z, t1.w});
+      o.z = bn_relu2(v[c].z, (bn_f32x2){t2.x, t2.y}, (bn_f32x2){t2.z, t2.w});
+      o.w = bn_relu2(v[c].w, (bn_f32x2){t3.x, t3.y}, (bn_f32x2){t3.z, t3.w});
+      v[c] = tag[c] < 0 ? make_uint4(0u, 0u, 0u, 0u) : o;
     }
-    return make_uint4(o[0], o[1], o[2], o[3]);
   }
 };
 

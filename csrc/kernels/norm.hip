@@ -251,17 +251,25 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int r = rbase + u * rg;
-      float v[8], q[8];
-      unpack8(Y[u], v);
-      if (HAS_RES) unpack8(Q[u], q);
+      uint4 o;
+      if constexpr (RELU && !HAS_RES) {  // the folded conv loaders' form (bn_relu2), bit for bit
+        o.x = bn_relu2(Y[u].x, (bn_f32x2){sc[0], sc[1]}, (bn_f32x2){sh[0], sh[1]});
+        o.y = bn_relu2(Y[u].y, (bn_f32x2){sc[2], sc[3]}, (bn_f32x2){sh[2], sh[3]});
+        o.z = bn_relu2(Y[u].z, (bn_f32x2){sc[4], sc[5]}, (bn_f32x2){sh[4], sh[5]});
+        o.w = bn_relu2(Y[u].w, (bn_f32x2){sc[6], sc[7]}, (bn_f32x2){sh[6], sh[7]});
+      } else {
+        float v[8], q[8];
+        unpack8(Y[u], v);
+        if (HAS_RES) unpack8(Q[u], q);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float z = fmaf(v[j], sc[j], sh[j]);
-        if (HAS_RES) z += q[j];
-        v[j] = RELU ? fmaxf(z, 0.f) : z;
+        for (int j = 0; j < 8; ++j) {
+          float z = fmaf(v[j], sc[j], sh[j]);
+          if (HAS_RES) z += q[j];
+          v[j] = RELU ? fmaxf(z, 0.f) : z;
+        }
+        o = pack8(v);
       }
       if (r < r1) {
-        const uint4 o = pack8(v);
         *reinterpret_cast<uint4*>(out + (size_t)r * C + c0) = o;
         if (RELU && mbits) {  // bit j: the stored bf16 output of channel c0 + j is > 0
           const uint32_t w[4] = {o.x, o.y, o.z, o.w};

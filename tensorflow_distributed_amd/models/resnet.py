@@ -441,7 +441,8 @@ class ConvLayer:
         """This conv applied to relu(bn(y)) where ``yp`` is the (y, partials) pair of the producing
         conv: folded when the model allows it (ResNet(fold_bn=True)), else bn then conv."""
         m = self.model
-        if m.fold_bn and m.mask_from_y and isinstance(yp, tuple) and bn.c <= _fold_max_c():
+        scope = int(m.fold_bn)  # 0 off, 1 every eligible conv, 2 1x1 consumers only
+        if scope and (scope != 2 or self.k == 1) and m.mask_from_y and isinstance(yp, tuple) and bn.c <= _fold_max_c():
             y, part = yp
             return _BNReluConv.apply(y, m.token, part, bn, self)
         return self(bn(yp))
@@ -508,7 +509,7 @@ class ResNet:
 
     def __init__(self, depth: int = 50, num_classes: int = 1000, device=None, seed: int = 0, width: int = 64,
                  zero_init_residual: bool = True, fuse_joins: bool = True, bn_stats: bool = True,
-                 bn_bwd_stats: bool = True, fold_bn: bool = True):
+                 bn_bwd_stats: bool = True, fold_bn: int = 1):
         kind, blocks = self.CFG[depth]
         if num_classes % 8 or width % 8:
             raise ValueError("num_classes and width must be multiples of 8 (16-byte MFMA operand chunks)")
@@ -533,8 +534,9 @@ class ResNet:
         # residual BN keeps its relu mask as bits for the backward instead of re-reading the output
         self.relu_bits = True
         # single-consumer relu BNs applied inside the consuming conv's operand loader (_BNReluConv);
-        # False keeps the separate bn_apply pass (the test oracle)
-        self.fold_bn = fold_bn
+        # False / 0 keeps the separate bn_apply pass (the test oracle); 2: only into 1x1 consumers (a
+        # 3x3 consumer's im2col loader re-applies the transform to every input element 9 times)
+        self.fold_bn = int(fold_bn)
         cin = width
         exp = 4 if kind == "bottleneck" else 1
         prev_out_bn = None  # the BN that produced the current block input (None: the stem's maxpool)
