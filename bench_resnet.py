@@ -49,7 +49,7 @@ def main(argv=None):
                     "epilogue (0: autograd adds; measured faster, see resnet.GradJoin)")
     ap.add_argument("--bn_bwd_stats", type=int, default=1, help="1: batch-norm backward statistics summed in the "
                     "epilogue of the dgrad that produces the BN's gradient (no separate partial pass)")
-    ap.add_argument("--fold_bn", type=int, default=1, help="1: single-consumer relu batch norms applied inside the "
+    ap.add_argument("--fold_bn", type=int, default=0, help="1: single-consumer relu batch norms applied inside the "
                     "consuming conv's operand loader (no bn_apply pass; 0: the separate pass; 2: 1x1 consumers only)")
     ap.add_argument("--lr", type=float, default=0.1)
     argv = list(sys.argv[1:] if argv is None else argv)

@@ -509,7 +509,7 @@ class ResNet:
 
     def __init__(self, depth: int = 50, num_classes: int = 1000, device=None, seed: int = 0, width: int = 64,
                  zero_init_residual: bool = True, fuse_joins: bool = True, bn_stats: bool = True,
-                 bn_bwd_stats: bool = True, fold_bn: int = 1):
+                 bn_bwd_stats: bool = True, fold_bn: int = 0):
         kind, blocks = self.CFG[depth]
         if num_classes % 8 or width % 8:
             raise ValueError("num_classes and width must be multiples of 8 (16-byte MFMA operand chunks)")
@@ -533,9 +533,10 @@ class ResNet:
         self.mask_from_y = True
         # residual BN keeps its relu mask as bits for the backward instead of re-reading the output
         self.relu_bits = True
-        # single-consumer relu BNs applied inside the consuming conv's operand loader (_BNReluConv);
-        # False / 0 keeps the separate bn_apply pass (the test oracle); 2: only into 1x1 consumers (a
-        # 3x3 consumer's im2col loader re-applies the transform to every input element 9 times)
+        # 1: single-consumer relu BNs applied inside the consuming conv's operand loader (_BNReluConv);
+        # 2: only into 1x1 consumers (a 3x3 consumer's im2col loader re-applies the transform to every
+        # input element 9 times); 0 (default): the separate bn_apply pass -- measured no slower than
+        # either fold on ResNet-50 b128 (13.79 vs 14.15 / 13.83 ms, profiles/resnet50_bn_fold_ab_r4.log)
         self.fold_bn = int(fold_bn)
         cin = width
         exp = 4 if kind == "bottleneck" else 1
