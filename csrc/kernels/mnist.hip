@@ -566,76 +566,125 @@ __device__ __forceinline__ void out_grad_block(const MnistStepArgs& a, int blk, 
 }
 
 // ---------------- K10 fc1 dW (+bias row): [3137][1024] = [P2;1]^T dH ----------------
-struct OnesRowMC {  // operand (mn, k) = X[k][mn] for mn < mn_real, 1 for mn == mn_real (k < k_lim)
+// fp32 into the flat gradient buffer, or (bf16 wire format) bf16 straight into the all-reduce /
+// optimizer operand -- the rounding a separate cast pass would do.
+// [P2_all; 1]^T as the KC = false A operand: (mn, k) = P2_all[k][mn] for mn < 3136, the bias
+// "ones row" at mn == 3136 (a chunk {1, 0, ..., 0}), zeros past K.
+struct OnesRowBuf {
   static constexpr bool KC = false;
   const uint16_t* __restrict__ x;
-  int ld, mn_real, k_lim;
+  int k_lim;
+  uint32_t nbytes;
   __device__ __forceinline__ uint4 operator()(int mn, int k) const {
-    if (k >= k_lim) return zero4();
-    if (mn + 8 <= mn_real) return *reinterpret_cast<const uint4*>(x + (size_t)k * ld + mn);
-    uint16_t t[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = mn + j;
-      t[j] = c < mn_real ? x[(size_t)k * ld + c] : (c == mn_real ? (uint16_t)0x3F80 : (uint16_t)0);
-    }
-    return *reinterpret_cast<uint4*>(t);
+    const uint4 v = buf_ld(x, nbytes, (uint32_t)k * FEAT + mn, k < k_lim && mn < FEAT);
+    return (mn == FEAT && k < k_lim) ? make_uint4(0x3F80u, 0u, 0u, 0u) : v;
   }
 };
-// fc1 dW rows [3137][1024]: fp32 into the flat gradient buffer, or (DP, bf16 wire format) bf16
-// straight into the all-reduce operand -- the rounding the separate cast pass used to do.
-struct GradEpi {
-  float* __restrict__ out;
-  uint16_t* __restrict__ outbf;
-  int ld, M, N;
-  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
-    if (n >= N) return;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (m4 + r >= M) continue;
-      const size_t o = (size_t)(m4 + r) * ld + n;
-      if (outbf) outbf[o] = f2bf_bits(v[r]);
-      else out[o] = v[r];
-    }
-  }
-};
+static_assert(FEAT % 8 == 0, "the ones row starts a fresh 8-element chunk");
+
 constexpr int FDW_BM = 64, FDW_BN = 64, FDW_BK = FDW_BK_;
+// fc1 dW tile epilogue through LDS: the fp32 accumulators go to a [64][68] float image, then every
+// thread stores whole 16-B pieces of rows (8 bf16, or 4 fp32 twice) -- a wave writes 1 KiB of row
+// bytes per instruction. The round-3 fragment-order epilogue wrote 2-B (4-B) scalars in 32-B row
+// pieces per instruction: 6.4 MB of bf16 gradient as 200 K partial-line writes per step.
+constexpr int FDW_PITCH = FDW_BN + 4;
+__device__ __forceinline__ void fc1_dw_store(f32x4 (&acc)[2][2], float* cs, float* out, uint16_t* outbf, int m0,
+                                             int n0, int M) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cs[(wm * 32 + 16 * i + 4 * (lane >> 4) + r) * FDW_PITCH + wn * 32 + 16 * j + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+#pragma unroll
+  for (int q = tid; q < FDW_BM * FDW_BN / 8; q += 256) {
+    const int row = q >> 3, ch = q & 7, m = m0 + row;
+    if (m >= M) continue;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + row * FDW_PITCH + ch * 8);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * FDW_PITCH + ch * 8 + 4);
+    const size_t o = (size_t)m * HID + n0 + ch * 8;
+    if (outbf) {
+      *reinterpret_cast<uint4*>(outbf + o) =
+          make_uint4(pack_bf2(lo[0], lo[1]), pack_bf2(lo[2], lo[3]), pack_bf2(hi[0], hi[1]), pack_bf2(hi[2], hi[3]));
+    } else {
+      *reinterpret_cast<f32x4*>(out + o) = lo;
+      *reinterpret_cast<f32x4*>(out + o + 4) = hi;
+    }
+  }
+}
+template <class LA, class LB>
+__device__ __forceinline__ void fc1_dw_tile(const MnistStepArgs& a, const LA& la, const LB& lb, int m0, int n0, int K,
+                                            bf16* smem) {
+  f32x4 acc[2][2];
+  gemm_mainloop<FDW_BM, FDW_BN, FDW_BK, 2, 2, LA, LB, GEMM_RS>(la, lb, m0, n0, 0, K, smem, acc);  // ends with a barrier
+  fc1_dw_store(acc, reinterpret_cast<float*>(smem), a.grad + OFF_WD1, a.gbf_a ? a.gbf_a + OFF_WD1 : nullptr, m0, n0,
+               FEAT + 1);
+}
 __device__ __forceinline__ void fc1_dw_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
-  OnesRowMC la{a.p2, FEAT, FEAT, a.B};
+  OnesRowBuf la{a.p2, a.B, (uint32_t)((int64_t)a.B * FEAT * 2)};
   DenseLoader<false> lb{a.dh, HID, HID, a.B};
-  GradEpi epi{a.grad + OFF_WD1, a.gbf_a ? a.gbf_a + OFF_WD1 : nullptr, HID, FEAT + 1, HID};
-  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), GEMM_RS>(la, lb, epi, by * FDW_BM, bx * FDW_BN, 0, a.B, smem);
+  fc1_dw_tile(a, la, lb, by * FDW_BM, bx * FDW_BN, a.B, smem);
 }
 
 // ---------------- K10 fc1 dX + K11 MaxPoolGrad + ReluGrad -> dz2 (dense, conv2 pre-act grad) --------
-struct UnpoolEpi {
-  const uint16_t* __restrict__ p2;
-  const uint8_t* __restrict__ idx2;
-  uint16_t* __restrict__ dz2;
-  int B;
-  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
-    if (n >= FEAT) return;
-    const int pp = n >> 6, c = n & 63, ph = pp / 7, pw = pp - ph * 7;
+// dX tile = BM batch rows x BN features of ONE pooled pixel pp (a 64-wide tile is all 64 channels,
+// a 32-wide one half of them). Epilogue through LDS: the fp32 tile goes to a [BM][BN + 4] float
+// image; thread (row b, 8-channel chunk cc) loads p2 (relu output, 16 B) and idx2 (argmax, 8 B)
+// chunks once, forms g = p2 > 0 ? dX : 0 in bf16, and writes the 2x2 unpool window as four whole
+// 16-B chunks of dz2 rows (the argmax position gets g, the other three zeros). The fragment-order
+// epilogue it replaces made 16 scattered 2-B stores and 1-2 B loads per lane and value group.
+constexpr int FDX_BM = 32, FDX_BN = 64, FDX_BK = FDX_BK_, FDX_BN2 = 32;
+template <int BN>
+__device__ __forceinline__ void fc1_dx_unpool_store(const MnistStepArgs& a, f32x4 (&acc)[FDX_BM / 32][BN / 32],
+                                                    float* cs, int m0, int n0) {
+  constexpr int PITCH = BN + 4, CPR = BN / 8;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  constexpr int WTM = FDX_BM / 2, WTN = BN / 2;
+  const int b = tid / CPR, cc = tid % CPR, m = m0 + b;
+  const bool live = b < FDX_BM && m < a.B;
+  // the relu / argmax chunks are issued before the accumulator is staged
+  const size_t xo = (size_t)(live ? m : 0) * FEAT + n0 + cc * 8;
+  const uint4 pv = *reinterpret_cast<const uint4*>(a.p2 + xo);
+  const uint2 iv = *reinterpret_cast<const uint2*>(a.idx2 + xo);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = m4 + r;
-      if (b >= B) continue;
-      const size_t o = (size_t)b * FEAT + n;
-      const float g = p2[o] != 0 ? v[r] : 0.f;  // relu output > 0
-      const int w = idx2[o];
-      const uint16_t gb = f2bf_bits(g);
+  for (int i = 0; i < WTM / 16; ++i)
 #pragma unroll
-      for (int wi = 0; wi < 4; ++wi) {
-        const int oh = 2 * ph + (wi >> 1), ow = 2 * pw + (wi & 1);
-        dz2[((size_t)(b * 14 + oh) * 14 + ow) * 64 + c] = (wi == w) ? gb : (uint16_t)0;
-      }
-    }
+    for (int j = 0; j < WTN / 16; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cs[(wm * WTM + 16 * i + 4 * (lane >> 4) + r) * PITCH + wn * WTN + 16 * j + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  if (!live) return;
+  const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + b * PITCH + cc * 8);
+  const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + b * PITCH + cc * 8 + 4);
+  const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+  uint32_t g[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t p = (pw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+    g[j] = p != 0 ? (uint32_t)f2bf_bits(v[j]) : 0u;  // relu output > 0 (it is >= 0)
   }
-};
+  const int pp = n0 >> 6, c0 = (n0 & 63) + cc * 8, ph = pp / 7, pwx = pp - ph * 7;
+  const uint32_t iw[2] = {iv.x, iv.y};
+#pragma unroll
+  for (int wi = 0; wi < 4; ++wi) {
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t i0 = (iw[q >> 1] >> (16 * (q & 1))) & 0xFFu, i1 = (iw[q >> 1] >> (16 * (q & 1) + 8)) & 0xFFu;
+      o[q] = (i0 == (uint32_t)wi ? g[2 * q] : 0u) | (i1 == (uint32_t)wi ? g[2 * q + 1] << 16 : 0u);
+    }
+    const int oh = 2 * ph + (wi >> 1), ow = 2 * pwx + (wi & 1);
+    *reinterpret_cast<uint4*>(a.dz2 + ((size_t)(m * 14 + oh) * 14 + ow) * 64 + c0) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
 // fc1 dX tile width: 64 (196 blocks at B = 128) inside the fused fc backward, where the dX tiles
 // share the launch with ~800 dW tiles; 32 (392 blocks) when dX runs alone (DP step, part 2), where
 // 196 blocks left a quarter of the CUs idle (A/B: one GPU 64 better by 1.3 us, DP 32 better by 1.5)
-constexpr int FDX_BM = 32, FDX_BN = 64, FDX_BK = FDX_BK_, FDX_BN2 = 32;
 // register stages of the long-K (1024) fc1 dX blocks: 1 with BK 128 (8 K-steps; RS 2 +1.3 us/step);
 // dX alone (DP): 2 (-0.3 us, profiles/ab_fc1_dx_tiles_r2.log)
 constexpr int FDX_RS = 1, FDX_RS_ALONE = 2;
@@ -643,8 +692,10 @@ template <int BN = FDX_BN, int RS = FDX_RS>
 __device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   DenseLoader<true> la{a.dh, HID, a.B, HID};
   DenseLoader<true> lb{a.pbf + OFF_WD1, HID, FEAT, HID};
-  UnpoolEpi epi{a.p2, a.idx2, a.dz2, a.B};
-  gemm_block<FDX_BM, BN, FDX_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), RS>(la, lb, epi, by * FDX_BM, bx * BN, 0, HID, smem);
+  f32x4 acc[FDX_BM / 32][BN / 32];
+  gemm_mainloop<FDX_BM, BN, FDX_BK, 2, 2, decltype(la), decltype(lb), RS>(la, lb, by * FDX_BM, bx * BN, 0, HID, smem,
+                                                                          acc);  // ends with a barrier
+  fc1_dx_unpool_store<BN>(a, acc, reinterpret_cast<float*>(smem), by * FDX_BM, bx * BN);
 }
 
 // K8 + K10: every fc-layer gradient in ONE launch (horizontal fusion of three independent
@@ -717,19 +768,6 @@ struct RankRowsMC {
     return buf_ld(x, nbytes, (uint32_t)(r * rs + (int64_t)(k - r * B) * ld + mn), k < k_lim && mn < mn_lim);
   }
 };
-// [P2_all; 1]^T as the KC = false A operand: (mn, k) = P2_all[k][mn] for mn < 3136, the bias
-// "ones row" at mn == 3136 (a chunk {1, 0, ..., 0}), zeros past K.
-struct OnesRowBuf {
-  static constexpr bool KC = false;
-  const uint16_t* __restrict__ x;
-  int k_lim;
-  uint32_t nbytes;
-  __device__ __forceinline__ uint4 operator()(int mn, int k) const {
-    const uint4 v = buf_ld(x, nbytes, (uint32_t)k * FEAT + mn, k < k_lim && mn < FEAT);
-    return (mn == FEAT && k < k_lim) ? make_uint4(0x3F80u, 0u, 0u, 0u) : v;
-  }
-};
-static_assert(FEAT % 8 == 0, "the ones row starts a fresh 8-element chunk");
 
 // Output layer [1025][10] = [Hd;1]^T dlogits over the W*B gathered rows: a block owns 16 rows m
 // (lane r = t & 15) x 16 row groups (q = t >> 4) of the K range, so even W = 8 leaves 64 rows per
@@ -808,9 +846,7 @@ __global__ __launch_bounds__(256) void fc_grad_sfb(MnistStepArgs a) {
   const int WB = a.sfb_world * a.B;
   OnesRowBuf la{a.sfb_p2, WB, (uint32_t)((int64_t)WB * FEAT * 2)};
   RankRowsMC lb{a.sfb_dr, HID, HID, WB, a.B, a.sfb_rs, (uint32_t)((int64_t)a.sfb_world * a.sfb_rs * 2)};
-  GradEpi epi{a.grad + OFF_WD1, a.gbf_a ? a.gbf_a + OFF_WD1 : nullptr, HID, FEAT + 1, HID};
-  gemm_block<FDW_BM, FDW_BN, FDW_BK, 2, 2, decltype(la), decltype(lb), decltype(epi), GEMM_RS>(
-      la, lb, epi, (id / FDW_GX) * FDW_BM, (id % FDW_GX) * FDW_BN, 0, WB, (bf16*)smem_raw);
+  fc1_dw_tile(a, la, lb, (id / FDW_GX) * FDW_BM, (id % FDW_GX) * FDW_BN, WB, (bf16*)smem_raw);
 }
 
 // ---------------- K13 (LDS-staged): conv2 dgrad + conv1 relu/pool-mask epilogue ----------------
@@ -1402,8 +1438,10 @@ void mnist_forward_fc(const MnistStepArgs& a, bool train, hipStream_t s) {
 
 void mnist_backward_a(const MnistStepArgs& a, hipStream_t s, int part) {
   const int B = a.B;
-  constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowMC, DenseLoader<false>>::BYTES;
+  constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowBuf, DenseLoader<false>>::BYTES;
+  static_assert(sm_dw >= FDW_BM * FDW_PITCH * 4, "fc1 dW staging image fits the GEMM's LDS");
   constexpr int sm_dx = GemmSmem<FDX_BM, FDX_BN, FDX_BK, DenseLoader<true>, DenseLoader<true>>::BYTES;
+  static_assert(sm_dx >= FDX_BM * (FDX_BN + 4) * 4, "fc1 dX staging image fits the GEMM's LDS");
   const int sm_og = (B * NCLS + 4 * OUTG_ROWS * NCLS) * 4;
   const int sm = std::max(std::max(sm_dw, sm_dx), sm_og);
   set_smem<fc1_bwd>(sm);
