@@ -22,6 +22,7 @@
 #include "../common.h"
 
 #include "../gemm.h"
+#include "../gemm256.h"  // kc_slot, make_rsrc, DenseSrc (the fc1 dX DMA ring)
 #include "../mnist_layout.h"
 #include "../tfd_kernels.h"
 
@@ -688,6 +689,74 @@ __device__ __forceinline__ void fc1_dx_unpool_store(const MnistStepArgs& a, f32x
 // register stages of the long-K (1024) fc1 dX blocks: 1 with BK 128 (8 K-steps; RS 2 +1.3 us/step);
 // dX alone (DP): 2 (-0.3 us, profiles/ab_fc1_dx_tiles_r2.log)
 constexpr int FDX_RS = 1, FDX_RS_ALONE = 2;
+#ifndef TFD_FDX_DMA  // 1: the fused fc backward's dX tiles on the DMA ring (fc1_dx_block_dma)
+#define TFD_FDX_DMA 1
+#endif
+// fc1 dX inside the fused fc backward: K = 1024 as 16 steps of 64 on a 4-stage LDS ring filled by
+// the buffer-load-to-LDS DMA (3 stages in flight behind the MFMAs, no VGPR staging). With the register
+// pipeline (gemm_mainloop, BK 128, RS 1) every one of 8 K steps waited a full memory round trip:
+// fc1 dX alone measured 10.3 us for 0.82 GFLOP over a 6.4 MB W1 (profiles/diag_fc1bwd_conv2bwd_r3.txt).
+// LDS images: KC [rows][64 bf16], slot s of row r holds chunk s ^ ((r >> 1) & 7) (kc_slot: the 16 rows
+// of a 16x16x32 fragment read hit 16 distinct 16-B bank groups). Waves: 2 x 2 of 16 x 32 outputs.
+constexpr int FDXD_BK = 64, FDXD_S = 4;
+constexpr int FDXD_A = FDX_BM * FDXD_BK * 2, FDXD_B = FDX_BN * FDXD_BK * 2, FDXD_STAGE = FDXD_A + FDXD_B;
+constexpr int FDXD_SMEM = FDXD_S * FDXD_STAGE;  // 48 KiB
+constexpr int FDXD_NK = HID / FDXD_BK;
+static_assert(FDX_BM == 32 && FDX_BN == 64 && FDXD_NK >= FDXD_S, "fc1 dX DMA ring geometry");
+__device__ __forceinline__ void fdxd_stage(const DenseKC& sa, const DenseKC& sb, char* img, int m0, int n0, int k0,
+                                           int w, int l) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  {  // A: 32 rows = 4 wave instructions (one per wave)
+    const int row = w * 8 + (l >> 3);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(sa.rsrc(), (__attribute__((address_space(3))) void*)(img + w * 1024), 16,
+                                             sa.off(m0 + row, k0 + kc_slot(row, l & 7) * 8), 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // B: 64 rows = 8 wave instructions (two per wave)
+    const int ins = 2 * w + i, row = ins * 8 + (l >> 3);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(sb.rsrc(), (__attribute__((address_space(3))) void*)(img + FDXD_A + ins * 1024),
+                                             16, sb.off(n0 + row, k0 + kc_slot(row, l & 7) * 8), 0, 0, 0);
+  }
+#else
+  (void)sa; (void)sb; (void)img; (void)m0; (void)n0; (void)k0; (void)w; (void)l;
+#endif
+}
+__device__ __forceinline__ void fc1_dx_block_dma(const MnistStepArgs& a, int bx, int by, char* smem) {
+  const DenseKC sa{a.dh, HID, a.B, HID};
+  const DenseKC sb{a.pbf + OFF_WD1, HID, FEAT, HID};
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int m0 = by * FDX_BM, n0 = bx * FDX_BN;
+  f32x4 acc[1][2] = {{f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}}};
+#pragma unroll
+  for (int s = 0; s < FDXD_S - 1; ++s) fdxd_stage(sa, sb, smem + s * FDXD_STAGE, m0, n0, s * FDXD_BK, w, l);
+  for (int t = 0; t < FDXD_NK; ++t) {
+    // stage t has landed once at most the stages issued after it (3 wave instructions each) are pending
+    const int after = min(FDXD_S - 2, FDXD_NK - 1 - t);
+    if (after == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage t visible to every wave; every wave is done with stage t - 1's slot
+    if (t + FDXD_S - 1 < FDXD_NK)
+      fdxd_stage(sa, sb, smem + ((t + FDXD_S - 1) % FDXD_S) * FDXD_STAGE, m0, n0, (t + FDXD_S - 1) * FDXD_BK, w, l);
+    const char* As = smem + (t % FDXD_S) * FDXD_STAGE;
+    const char* Bs = As + FDXD_A;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = 4 * ks + (l >> 4);
+      const int ra = 16 * wm + (l & 15);
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + ra * 128 + (kc_slot(ra, ch) << 4));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int rb = 32 * wn + 16 * j + (l & 15);
+        const bf16x8 bf = *reinterpret_cast<const bf16x8*>(Bs + rb * 128 + (kc_slot(rb, ch) << 4));
+        acc[0][j] = mfma16x16x32(af, bf, acc[0][j]);
+      }
+    }
+  }
+  __syncthreads();  // the ring is dead: the epilogue reuses it
+  fc1_dx_unpool_store<FDX_BN>(a, acc, reinterpret_cast<float*>(smem), m0, n0);
+}
+
 template <int BN = FDX_BN, int RS = FDX_RS>
 __device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   DenseLoader<true> la{a.dh, HID, a.B, HID};
@@ -736,7 +805,8 @@ __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int pa
     if (id < n_dx) {
       int bx, by;
       fdx_tile(id, FDX_GX, gy, bx, by);
-      fc1_dx_block(a, bx, by, (bf16*)smem_raw);
+      if (TFD_FDX_DMA) fc1_dx_block_dma(a, bx, by, smem_raw);
+      else fc1_dx_block(a, bx, by, (bf16*)smem_raw);
       return;
     }
     id -= n_dx;
@@ -1443,7 +1513,7 @@ void mnist_backward_a(const MnistStepArgs& a, hipStream_t s, int part) {
   constexpr int sm_dx = GemmSmem<FDX_BM, FDX_BN, FDX_BK, DenseLoader<true>, DenseLoader<true>>::BYTES;
   static_assert(sm_dx >= FDX_BM * (FDX_BN + 4) * 4, "fc1 dX staging image fits the GEMM's LDS");
   const int sm_og = (B * NCLS + 4 * OUTG_ROWS * NCLS) * 4;
-  const int sm = std::max(std::max(sm_dw, sm_dx), sm_og);
+  const int sm = std::max(std::max(sm_dw, part == 2 || !TFD_FDX_DMA ? sm_dx : FDXD_SMEM), sm_og);
   set_smem<fc1_bwd>(sm);
   const int n_dx = FDX_GX * ((B + FDX_BM - 1) / FDX_BM);
   const int nb = part == 2 ? FDX_GX2 * ((B + FDX_BM - 1) / FDX_BM) : FDW_GX * FDW_GY + (part == 0 ? n_dx : 0) + OUTG_BLOCKS;

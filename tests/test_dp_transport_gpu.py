@@ -170,14 +170,14 @@ def test_dp_schedules_captured_equal_eager(cuda, mode, sfb, zero):
 
 @pytest.mark.parametrize("mode", ["rccl", "ipc"])
 def test_forced_dp_world1_captured_steps_track_fused(cuda, mode):
-    """Two eager + two graph-replayed steps (captured collectives) with dropout and Adam: same
-    update direction as the fused one-GPU step (Adam's m/sqrt(v) amplifies the bf16 wire rounding
-    where |g| ~ 0, so compare directions, not bits)."""
+    """Two eager + two graph-replayed steps (captured collectives) with dropout, SGD: the same
+    parameters as the fused one-GPU step with bf16-rounded local gradients, element by element (SGD:
+    the update is the gradient -- Adam's m/sqrt(v) would amplify any wire rounding where |g| ~ 0)."""
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
-        params, (ref, dp) = _engines_on_dataset(cuda, 2)
+        params, (ref, dp) = _engines_on_dataset(cuda, 2, sgd=True)
         ref.set_local_bf16_grads(1)
         tr = attach_engine(dp, 0, 1, cuda, mode=mode, force_dp=True)
         for _ in range(2):
@@ -190,9 +190,13 @@ def test_forced_dp_world1_captured_steps_track_fused(cuda, mode):
     torch.cuda.synchronize()
     assert int(dp.step_tensor().item()) == int(ref.step_tensor().item()) == 4
     tr.check()
-    d0, d1 = ref.params() - params, dp.params() - params
-    cos = torch.nn.functional.cosine_similarity(d0, d1, dim=0).item()
-    assert cos > 0.99, cos
+    d0, d1 = (ref.params() - params).cpu(), (dp.params() - params).cpu()
+    for k, r in M.dict_from_flat(d0).items():
+        d = M.dict_from_flat(d1)[k]
+        tol = 1e-2 * r.abs() + 2e-3 * r.abs().max()
+        bad = (d - r).abs() > tol
+        assert not bad.any(), (f"{k}: {int(bad.sum())}/{r.numel()} elements off; worst {(d - r).abs().max().item():.3e} "
+                               f"vs max|r| {r.abs().max().item():.3e}")
     assert torch.equal(dp.params_bf16(), dp.params().to(torch.bfloat16))
     tr.close()
 

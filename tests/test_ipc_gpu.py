@@ -60,7 +60,31 @@ def test_ipc_allreduce_multiprocess_one_gpu(cuda, world, n):
         assert torch.allclose(outs[2], torch.full((n,), float(tot * world ** 2)))
 
 
-def _engine_dp_worker(rank, world, B, steps, sfb=False, zero=False):
+LR_SGD = 0.05
+
+
+def _set_opt(eng, sgd):
+    if sgd:
+        eng.set_momentum(LR_SGD, 0.0, False)
+    else:
+        eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+
+
+def _close_elementwise(got, ref, what, rel=1.5e-2, absmax=4e-3):
+    """Per tensor of the flat layout: |got - ref| <= rel |ref| + absmax max|ref| for EVERY element
+    (bf16 wire rounding of the per-rank gradients, fp32 sums in a different order)."""
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+
+    gd, rd = M.dict_from_flat(got), M.dict_from_flat(ref)
+    for k in rd:
+        r, d = rd[k].float(), gd[k].float()
+        tol = rel * r.abs() + absmax * r.abs().max()
+        bad = (d - r).abs() > tol
+        assert not bad.any(), (f"{what} {k}: {int(bad.sum())}/{r.numel()} elements off; worst |d-r| "
+                               f"{(d - r).abs().max().item():.3e} vs max|r| {r.abs().max().item():.3e}")
+
+
+def _engine_dp_worker(rank, world, B, steps, sfb=False, zero=False, sgd=False):
     from tensorflow_distributed_amd.models import mnist_cnn as M
     from tensorflow_distributed_amd.parallel.ipc import make_ipc_comm
 
@@ -68,7 +92,7 @@ def _engine_dp_worker(rank, world, B, steps, sfb=False, zero=False):
     dev = torch.device("cuda", 0)
     comm = make_ipc_comm(rank, world, 0, M.TOTAL)
     eng = torch.classes.tfd.MnistEngine(B, 0, 1.0, 5, rank)
-    eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+    _set_opt(eng, sgd)
     eng.set_ipc(comm, 1 << 30, True)
     if sfb:
         eng.set_fc_sfb(True)
@@ -98,20 +122,22 @@ def _engine_dp_worker(rank, world, B, steps, sfb=False, zero=False):
     return out
 
 
-@pytest.mark.parametrize("world,sfb", [(2, False), (2, True), (4, True)])
-def test_engine_dp_over_ipc_matches_single_rank_big_batch(cuda, world, sfb):
-    """DP=N (N processes sharing the GPU, IPC transport, captured graph) == DP=1 with N*B; with
-    sfb the fc gradients come from the all-gathered factors instead of an all-reduce."""
+@pytest.mark.parametrize("world,sfb,zero", [(2, False, False), (2, True, False), (4, True, True)])
+def test_engine_dp_over_ipc_matches_single_rank_big_batch(cuda, world, sfb, zero):
+    """DP=N (N processes sharing the GPU, IPC transport, captured graph; sfb: fc gradients from the
+    all-gathered factors; zero: ZeRO-1 fc1 shards, the N >= 4 default) == DP=1 with N*B over three SGD
+    steps, element by element (SGD: the update is the gradient, no m/sqrt(v) amplification of the
+    bf16 wire rounding where |g| ~ 0)."""
     from tensorflow_distributed_amd.models import mnist_cnn as M
 
     B, steps = 32, 3
-    res = run_ranks(_engine_dp_worker, world, B, steps, sfb, timeout=300)
+    res = run_ranks(_engine_dp_worker, world, B, steps, sfb, zero, True, timeout=300)
     for p, st, e, w in res:
         assert e == 0 and w == world and st == steps
         assert torch.equal(p, res[0][0]), "replicas diverged"
     p0 = res[0][0]
     eng = torch.classes.tfd.MnistEngine(world * B, 0, 1.0, 5, 0)
-    eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+    _set_opt(eng, True)
     g = torch.Generator().manual_seed(7)
     x = torch.rand(steps, world * B, 784, generator=g)
     y = torch.randint(0, 10, (steps, world * B), generator=g, dtype=torch.int32)
@@ -125,13 +151,11 @@ def test_engine_dp_over_ipc_matches_single_rank_big_batch(cuda, world, sfb):
             eng.train_step()
     torch.cuda.synchronize()
     ref = eng.params().cpu()
-    d = p0 - M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()})
-    dr = ref - M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()})
-    cos = torch.nn.functional.cosine_similarity(d, dr, dim=0).item()
-    assert cos > 0.99, cos  # bf16 gradient all-reduce vs one big-batch step: same update direction
+    init = M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()})
+    _close_elementwise(p0 - init, ref - init, "3-step update", rel=3e-2, absmax=6e-3)
 
 
-def _engine_dp_grads_worker(rank, world, B, sfb):
+def _engine_dp_grads_worker(rank, world, B, sfb, zero=False):
     from tensorflow_distributed_amd.models import mnist_cnn as M
     from tensorflow_distributed_amd.parallel.ipc import make_ipc_comm
 
@@ -139,10 +163,12 @@ def _engine_dp_grads_worker(rank, world, B, sfb):
     dev = torch.device("cuda", 0)
     comm = make_ipc_comm(rank, world, 0, M.TOTAL)
     eng = torch.classes.tfd.MnistEngine(B, 0, 1.0, 5, rank)
-    eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+    _set_opt(eng, True)
     eng.set_ipc(comm, 1 << 30, True)
     if sfb:
         eng.set_fc_sfb(True)
+    if zero:
+        eng.set_zero(True)
     g = torch.Generator().manual_seed(11)
     x = torch.rand(world * B, 784, generator=g)
     y = torch.randint(0, 10, (world * B,), generator=g, dtype=torch.int32)
@@ -153,24 +179,32 @@ def _engine_dp_grads_worker(rank, world, B, sfb):
         eng.feed_x().copy_(x[rank * B:(rank + 1) * B].to(dev))
         eng.feed_y().copy_(y[rank * B:(rank + 1) * B].to(dev))
         eng.train_step()
+        grads = eng.grads_bf16().float().cpu()  # the summed gradients the optimizer read
+        eng.sync_params()  # ZeRO: every rank's updated fc1 shard
     torch.cuda.synchronize()
-    out = eng.grads_bf16().float().cpu(), comm.error()  # the summed gradients the optimizer read
+    out = grads, eng.params().cpu(), comm.error()
     comm.close()
     return out
 
 
-@pytest.mark.parametrize("sfb", [False, True])
-def test_engine_dp_reduced_grads_elementwise(cuda, sfb):
-    """The gradient every rank's optimizer consumes after one DP=2 step (bf16 wire: per-rank mean
+@pytest.mark.parametrize("world,sfb,zero", [(2, False, False), (2, True, False), (4, True, False), (4, True, True)])
+def test_engine_dp_reduced_grads_elementwise(cuda, world, sfb, zero):
+    """The gradient every rank's optimizer consumes after one DP=N step (bf16 wire: per-rank mean
     gradients cast to bf16, summed in fp32 in rank order, stored bf16; with sfb the fc gradients
-    are one GEMM over both ranks' gathered factors) equals 2x the DP=1 gradient of the 2B batch,
-    element by element within bf16 rounding."""
+    are one GEMM over all ranks' gathered factors; with zero -- the N >= 4 default -- each rank's
+    optimizer reads only its fc1 shard, compared shard by shard) equals N x the DP=1 gradient of the
+    N*B batch element by element within bf16 rounding, and the post-step parameters (one SGD step,
+    shards gathered) equal the DP=1 step's."""
     from tensorflow_distributed_amd.models import mnist_cnn as M
 
-    world, B = 2, 32
-    res = run_ranks(_engine_dp_grads_worker, world, B, sfb, timeout=300)
-    assert all(e == 0 for _, e in res)
-    assert torch.equal(res[0][0], res[1][0]), "ranks consumed different gradients"
+    B = 32
+    res = run_ranks(_engine_dp_grads_worker, world, B, sfb, zero, timeout=300)
+    assert all(e == 0 for _, _, e in res)
+    assert all(torch.equal(p, res[0][1]) for _, p, _ in res), "replicas diverged"
+    w1, b1 = M.OFFSETS["wd1"], M.OFFSETS["bd1"]
+    shard = (b1 - w1) // world
+    if not zero:
+        assert all(torch.equal(g, res[0][0]) for g, _, _ in res), "ranks consumed different gradients"
     eng = torch.classes.tfd.MnistEngine(world * B, 0, 1.0, 5, 0)
     g = torch.Generator().manual_seed(11)
     x = torch.rand(world * B, 784, generator=g)
@@ -185,14 +219,19 @@ def test_engine_dp_reduced_grads_elementwise(cuda, sfb):
         eng.backward_a()
         eng.backward_b()
     torch.cuda.synchronize()
-    ref = M.dict_from_flat(eng.grads().cpu() * world)  # per-rank means summed = world x the 2B mean
-    got = M.dict_from_flat(res[0][0])
-    for k in ref:
-        r, d = ref[k].float(), got[k].float()
-        tol = 1.5e-2 * r.abs() + 4e-3 * r.abs().max()
-        bad = (d - r).abs() > tol
-        assert not bad.any(), (f"{k}: {int(bad.sum())}/{r.numel()} elements off; worst |d-r| "
-                               f"{(d - r).abs().max().item():.3e} vs max|r| {r.abs().max().item():.3e}")
+    gref = eng.grads().cpu()
+    ref = gref * world  # per-rank means summed = world x the N*B mean
+    for rk, (g, p, _) in enumerate(res):
+        if zero:  # the optimizer of rank rk reads the conv region, its fc1 shard and the tail only
+            lo, hi = w1 + rk * shard, w1 + (rk + 1) * shard
+            g = torch.cat([g[:w1], torch.zeros(lo - w1), g[lo:hi], torch.zeros(b1 - hi), g[b1:]])
+            r = torch.cat([ref[:w1], torch.zeros(lo - w1), ref[lo:hi], torch.zeros(b1 - hi), ref[b1:]])
+        else:
+            r = ref
+        _close_elementwise(g, r, f"rank {rk} reduced gradient")
+    init = M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()})
+    # one SGD step with the 1/N scale: (init - p) / lr is the N*B mean gradient
+    _close_elementwise((init - res[0][1]) / LR_SGD, gref, "post-step parameters")
 
 
 def _resnet_dp_worker(rank, world, steps):
