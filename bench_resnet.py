@@ -38,6 +38,8 @@ def main(argv=None):
     ap.add_argument("--bucket_candidates", default="2,4,8,16,25")
     ap.add_argument("--probe_steps", type=int, default=10, help="timed steps per bucket-size probe")
     ap.add_argument("--probe_warmup", type=int, default=3)
+    ap.add_argument("--small_ipc_mb", type=float, default=1.0, help="gradient buckets of at most this many MB "
+                    "(bf16 wire) take the IPC one-shot all-reduce beside RCCL (N > 1; 0: every bucket on RCCL)")
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--bn_stats", type=int, default=1, help="1: batch-norm statistics summed in the conv "
                     "forward epilogue (no separate statistics pass over the conv output)")
@@ -73,11 +75,16 @@ def main(argv=None):
                bn_stats=bool(a.bn_stats), bn_bwd_stats=bool(a.bn_bwd_stats), fold_bn=a.fold_bn)
     m.mask_from_y = bool(a.mask_from_y)
     m.relu_bits = bool(a.relu_bits)
-    comm, transport = None, "none"
+    comm, transport, small = None, "none", None
     if ctx.world > 1:
         if ctx.comm is not None:  # one rank per GPU: RCCL over xGMI
             comm, transport = ctx.comm, "rccl"
             comm.broadcast(m.fp.master, 0)
+            from tensorflow_distributed_amd.parallel.transport import small_bucket_ipc
+
+            small = small_bucket_ipc(ctx.rank, ctx.world, dev, comm, int(a.small_ipc_mb * (1 << 20)))
+            if small is not None:
+                transport = "rccl+ipc(small buckets)"
         elif ctx.shared_device:  # ranks share a GPU (RCCL refuses that): the IPC transport
             from tensorflow_distributed_amd.parallel.ipc import IpcCollectives, make_ipc_comm
 
@@ -96,7 +103,7 @@ def main(argv=None):
     def configure(mb):
         """Reducer with ``mb``-MB buckets, two eager steps, the step captured; returns run(k)."""
         if comm is not None:
-            m.set_comm(comm, mb)
+            m.set_comm(comm, mb, small=small, small_mb=a.small_ipc_mb)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for _ in range(2):
@@ -175,17 +182,19 @@ def main(argv=None):
             "config": {"model": f"resnet{a.depth} v1.5 NHWC", "global_batch": ctx.world * a.batch_size,
                        "per_gpu_batch": a.batch_size, "seq_len": None, "parallelism": f"dp{ctx.world}",
                        "dp_transport": transport,
-                       "bucket_mb": bucket_mb,
+                       "bucket_mb": bucket_mb, "small_bucket_mb": a.small_ipc_mb if small is not None else None,
+                       "small_buckets": m.reducer.small_buckets if small is not None else 0,
                        "bucket_schedule": {"source": source, "candidates_ms_per_step": (
                            {k: round(v, 4) for k, v in probe_ms.items()} if probe_ms else None)},
                        "optimizer": "sgd-momentum 0.9 wd 1e-4",
                        "hipgraph": not a.eager, "fuse_joins": bool(a.fuse_joins), "bn_stats": bool(a.bn_stats),
                        "mask_from_y": bool(a.mask_from_y), "relu_bits": bool(a.relu_bits),
-                       "bn_bwd_stats": bool(a.bn_bwd_stats)}}), flush=True)
-    if transport == "ipc":
-        if comm.ipc.error():
-            raise RuntimeError("IPC collective barrier timed out: replicas may have diverged")
-        comm.ipc.close()
+                       "bn_bwd_stats": bool(a.bn_bwd_stats), "fold_bn": a.fold_bn}}), flush=True)
+    for c in (comm if transport == "ipc" else None, small):
+        if c is not None:
+            if c.ipc.error():
+                raise RuntimeError("IPC collective barrier timed out: replicas may have diverged")
+            c.ipc.close()
     ctx.shutdown()
     if not topo["replicas_identical"]:
         print("error: DP replicas diverged (parameter digests differ across ranks)", file=sys.stderr)

@@ -98,13 +98,17 @@ class BucketReducer:
     comm stream the moment its last parameter gradient has been written (backward overlap)."""
 
     def __init__(self, fp: FlatParams, comm=None, bucket_bytes: int = 8 << 20, bf16: bool = False,
-                 force_dp: bool = False):
+                 force_dp: bool = False, small=None, small_bytes: int = 0):
         """``force_dp``: run the DP schedule (comm stream, per-bucket bf16 casts and collectives,
         1/N in the optimizer) even when the communicator has ONE rank -- the exact multi-GPU code
         path, rehearsed on a one-GPU box over a real world-1 RcclComm (MnistEngine.set_force_dp's
-        analogue)."""
+        analogue). ``small``: a second communicator (the IPC one-shot all-reduce,
+        parallel/ipc.IpcCollectives) for buckets of at most ``small_bytes`` wire bytes -- latency-bound
+        tails where RCCL's ring pays 2(N-1) link hops for a few hundred KB."""
         self.fp = fp
         self.comm = comm
+        self.small = small
+        self.small_bytes = small_bytes
         self.world = comm.world() if comm is not None else 1
         dp = comm is not None and (self.world > 1 or force_dp)
         self.buckets: List[Tuple[int, int]] = []
@@ -123,6 +127,9 @@ class BucketReducer:
         for s in fp.specs:
             self.need[self.bucket_of[s.name]] += 1
         self.count = [0] * len(self.buckets)
+        self.bucket_comm = [small if (small is not None and (hi - lo) * elt <= small_bytes) else comm
+                            for lo, hi in self.buckets]
+        self.small_buckets = sum(1 for c in self.bucket_comm if c is small and small is not None)
         self.stream = torch.cuda.Stream(fp.device) if dp else None
         self.events = []
         self.launched = 0
@@ -144,11 +151,12 @@ class BucketReducer:
             with torch.cuda.stream(self.stream):
                 self.stream.wait_event(ev)
                 lo, hi = self.buckets[b]
+                c = self.bucket_comm[b]
                 if self.bf16:
                     self.gbf[lo:hi].copy_(self.fp.grad[lo:hi])
-                    self.comm.all_reduce(self.gbf[lo:hi], "sum")
+                    c.all_reduce(self.gbf[lo:hi], "sum")
                 else:
-                    self.comm.all_reduce(self.fp.grad[lo:hi], "sum")
+                    c.all_reduce(self.fp.grad[lo:hi], "sum")
             self.launched += 1
 
     def finish(self):
@@ -590,8 +598,12 @@ class ResNet:
     def num_params(self) -> int:
         return sum(s.numel for s in self.specs)
 
-    def set_comm(self, comm, bucket_mb: float = 8.0, bf16_grads: bool = True, force_dp: bool = False):
-        self.reducer = BucketReducer(self.fp, comm, int(bucket_mb * (1 << 20)), bf16=bf16_grads, force_dp=force_dp)
+    def set_comm(self, comm, bucket_mb: float = 8.0, bf16_grads: bool = True, force_dp: bool = False, small=None,
+                 small_mb: float = 1.0):
+        """Bucketed gradient all-reduce over ``comm``; buckets of at most ``small_mb`` MB of wire bytes
+        go through ``small`` (the IPC one-shot communicator) when one is given."""
+        self.reducer = BucketReducer(self.fp, comm, int(bucket_mb * (1 << 20)), bf16=bf16_grads, force_dp=force_dp,
+                                     small=small, small_bytes=int(small_mb * (1 << 20)))
 
     def forward(self, x_nhwc_f32: torch.Tensor) -> torch.Tensor:
         for j in self.joins:

@@ -115,6 +115,36 @@ def ipc_gather_self_check(ipc, comm, shards, device: torch.device, group=None) -
     return ok
 
 
+def small_bucket_ipc(rank: int, world: int, device: torch.device, comm, max_bytes: int, group=None, log=None,
+                     force: bool = False):
+    """IPC one-shot all-reduce for a bucket reducer's small buckets (bf16 wire, <= ``max_bytes``),
+    beside an RCCL communicator: created, self-checked against ``comm`` (RCCL) on every rank, and
+    kept only when every rank agrees (``IpcCollectives``), else None -- the small buckets then stay on
+    RCCL. ``force``: also at world 1 (the one-GPU rehearsal of this path)."""
+    from .ipc import IpcCollectives, make_ipc_comm
+
+    log = log or (lambda m: print(m, file=sys.stderr))
+    if max_bytes <= 0 or (world <= 1 and not force):
+        return None
+    cap = max(1024, (max_bytes + 3) // 4)  # fp32 elements of staging (a bf16 bucket uses half)
+    ipc, ok = None, 0
+    try:
+        ipc = make_ipc_comm(rank, world, device.index or 0, cap, group=group, max_blocks=64)
+    except Exception as e:  # pragma: no cover - depends on the node's IPC support
+        log(f"# small-bucket ipc setup failed: {e!r}")
+    if ipc is not None:
+        ok = int(ipc_self_check(ipc, comm, min(cap, 65536), device, group))
+    flags = torch.tensor([1 - ok], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=group)
+    if int(flags.item()) == 0:
+        return IpcCollectives(ipc)
+    log("# small-bucket ipc self-check failed; every bucket stays on RCCL")
+    if ipc is not None:
+        ipc.close()
+    return None
+
+
 def _gather_shards(eng, world: int, cap: int, sfb: bool, zero: bool):
     """Shard sizes (bf16 elements) of the all-gathers that will run through an IPC staging of
     ``cap`` fp32 elements (MnistEngine::ipc_gathers)."""

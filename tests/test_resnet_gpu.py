@@ -191,7 +191,7 @@ def test_resnet_graph_capture(cuda):
     assert all(v == v for v in vals) and vals[-1] < vals[0] + 1.0
 
 
-def _rccl_bucketed_worker(rank, world, bf16):
+def _rccl_bucketed_worker(rank, world, bf16, small_ipc=False):
     import torch
 
     from tensorflow_distributed_amd import _native
@@ -204,12 +204,21 @@ def _rccl_bucketed_worker(rank, world, bf16):
     comm = torch.classes.tfd.RcclComm(uid, 1, 0, cuda.index)
     x = torch.randn(8, 32, 32, 3, device=cuda)
     lab = torch.randint(0, 16, (8,), dtype=torch.int32, device=cuda)
+    small = None
+    if small_ipc:  # buckets <= 24 KB over the IPC one-shot all-reduce, the rest over RCCL
+        from tensorflow_distributed_amd.parallel.transport import small_bucket_ipc
+
+        small = small_bucket_ipc(0, 1, cuda, comm, 24 << 10, force=True)
+        assert small is not None
     ms = []
     for dp in (False, True):
         m = ResNet(18, num_classes=16, device=cuda, seed=5, width=16)
         if dp:
-            m.set_comm(comm, bucket_mb=0.05, bf16_grads=bf16, force_dp=True)
+            m.set_comm(comm, bucket_mb=0.05, bf16_grads=bf16, force_dp=True, small=small, small_mb=24 / 1024)
             assert m.reducer.stream is not None and len(m.reducer.buckets) > 3
+            if small_ipc:
+                assert 0 < m.reducer.small_buckets < len(m.reducer.buckets), (m.reducer.small_buckets,
+                                                                               len(m.reducer.buckets))
         elif bf16:  # the reference step reads its gradients rounded to bf16, as the wire delivers them
             fp = m.fp
             m.reducer.reduced_grads = lambda fp=fp: fp.grad.to(torch.bfloat16)
@@ -234,8 +243,8 @@ def _rccl_bucketed_worker(rank, world, bf16):
     return int(bad.numel()), names[:8], bool(torch.isfinite(p1).all().item())
 
 
-@pytest.mark.parametrize("bf16", [False, True])
-def test_resnet_rccl_bucketed_world1_equals_no_comm(cuda, bf16):
+@pytest.mark.parametrize("bf16,small_ipc", [(False, False), (True, False), (True, True)])
+def test_resnet_rccl_bucketed_world1_equals_no_comm(cuda, bf16, small_ipc):
     """The ResNet DP path (BucketReducer: comm stream, per-bucket collectives launched from inside
     the backward, 1/N in the fused SGD) forced at world 1 over a REAL RcclComm, eager and captured
     in a CUDA graph: the world-1 sum is the identity, so the parameters equal the no-communicator
@@ -244,8 +253,9 @@ def test_resnet_rccl_bucketed_world1_equals_no_comm(cuda, bf16):
 
     Runs in the suite's process again (round 3 moved it to a fresh one after an in-suite segfault in
     CUDAGraph.replay): RcclComm's destructor no longer destroys a communicator that an earlier
-    test's still-alive captured graph used (see test_rccl_comm_outlives_its_python_object)."""
-    n_bad, names, finite = _rccl_bucketed_worker(0, 1, bf16)
+    test's still-alive captured graph used (see test_rccl_comm_outlives_its_python_object).
+    small_ipc: the small buckets ride the IPC one-shot all-reduce beside RCCL (a world-1 IpcComm)."""
+    n_bad, names, finite = _rccl_bucketed_worker(0, 1, bf16, small_ipc)
     assert finite
     assert n_bad == 0, f"{n_bad} parameters differ (first in {names})"
 
