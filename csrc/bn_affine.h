@@ -15,8 +15,9 @@ __device__ __forceinline__ void bn_affine(float mean, float invstd, float gamma,
   sh = fmaf(-mean, sc, beta);
 }
 
-// relu(y * sc + sh) of two bf16 values packed in a dword (low half = the lower channel), as packed
-// math: v_pk_fma_f32, one v_cvt_pk_bf16_f32 (RNE), and the relu as v_pk_max_i16 against 0 on the
+// relu(y * sc + sh) of two bf16 values packed in a dword (low half = the lower channel): two fmas
+// (one v_pk_fma_f32 where the build allows packed fp32; this library's build does not, see
+// docs/DESIGN.md §6), one v_cvt_pk_bf16_f32 (RNE), and the relu as v_pk_max_i16 against 0 on the
 // rounded bf16 bits (a negative bf16 is a negative int16; -0 -> +0) -- equal to rounding fmaxf(z, 0)
 // for every non-NaN z. bn_apply_kernel and the folded conv loaders both use it, so the two forms
 // of a relu BN output agree bit for bit.
