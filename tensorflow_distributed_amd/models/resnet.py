@@ -190,14 +190,14 @@ class GradJoin:
         self.seen, self.acc = 0, None
 
     def arrive(self, g=None, conv=None):
-        """``g``: a finished gradient; or ``conv=(dy, layer, xshape)``: compute it as a dgrad.
+        """``g``: a finished gradient; or ``conv=(dy, layer, xshape, fwd_id)``: compute it as a dgrad.
         Returns the total for the last arrival, else None."""
         self.seen += 1
         last = self.seen == self.n
         if conv is not None:
-            dy, L, xs = conv
-            if last and _bn_stats_fusable(L, self.bn):  # the sum is the BN's whole dout
-                g = _dgrad_bn(dy, L, xs, self.acc, self.bn)
+            dy, L, xs, fid = conv
+            if last and _bn_stats_fusable(L, self.bn, fid):  # the sum is the BN's whole dout
+                g = _dgrad_bn(dy, L, xs, self.acc, self.bn, fid)
             elif self.acc is not None:
                 g = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad, self.acc)
             else:
@@ -215,7 +215,7 @@ class GradJoin:
 _BN_STATS_STRIDED = os.environ.get("TFD_BN_STATS_STRIDED", "1") != "0"
 
 
-def _bn_stats_fusable(L, bn) -> bool:
+def _bn_stats_fusable(L, bn, fid) -> bool:
     """Can conv ``L``'s dgrad (the whole dout of batch norm ``bn``) emit that BN's backward
     statistics partials (``conv2d_dgrad_bn``)? Stride-1 dgrads and strided ones whose output phases all
     have taps (3x3 stride 2, by phase GEMMs), and a BN whose relu mask the epilogue
@@ -223,20 +223,23 @@ def _bn_stats_fusable(L, bn) -> bool:
     (residual-free BN with ``mask_from_y``)."""
     if bn is None or not L.model.bn_bwd_stats or bn.fwd_state is None:
         return False
+    if bn.fwd_state[6] != fid:  # the BN state is another forward's (a second forward before this backward)
+        return False
     if L.stride != 1 and (L.k < L.stride or not _BN_STATS_STRIDED):  # tap-less phases (1x1 stride 2)
         return False
-    _, _, _, mask, relu, has_res = bn.fwd_state
+    _, _, _, mask, relu, has_res, _ = bn.fwd_state
     return (not relu) or mask is not None or (not has_res and L.model.mask_from_y)
 
 
-def _dgrad_bn(dy, L, xs, acc, bn):
+def _dgrad_bn(dy, L, xs, acc, bn, fid):
     """dX of conv ``L`` (+ ``acc``) with BN ``bn``'s backward partials summed in the same epilogue;
-    the partials wait on the BN layer for its backward (which then skips its own partial pass)."""
-    y, mean, invstd, mask, relu, has_res = bn.fwd_state
+    the partials wait on the BN layer for its backward (which then skips its own partial pass),
+    tagged with the forward they belong to."""
+    y, mean, invstd, mask, relu, has_res, _ = bn.fwd_state
     beta = bn.beta() if (relu and mask is None) else None
     g, part = _ops().conv2d_dgrad_bn(dy, L.w(), xs, L.stride, L.pad, acc, y, mean, invstd, bn.gamma(), beta, mask,
                                      relu)
-    bn.bwd_part = part
+    bn.bwd_part = (part, fid)
     return g
 
 
@@ -248,6 +251,7 @@ class _Conv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, token, layer):
         ctx.layer = layer
+        ctx.fwd_id = layer.model.fwd_id
         ctx.save_for_backward(x)
         if layer.model.bn_stats:
             y, part = _ops().conv2d_fwd_stats(x, layer.w(), layer.stride, layer.pad)
@@ -266,12 +270,22 @@ class _Conv(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             if L.in_join is not None:
-                dx = L.in_join.arrive(conv=(dy, L, list(x.shape)))
-            elif _bn_stats_fusable(L, L.in_bn):  # this conv is the BN output's only consumer
-                dx = _dgrad_bn(dy, L, list(x.shape), None, L.in_bn)
+                dx = L.in_join.arrive(conv=(dy, L, list(x.shape), ctx.fwd_id))
+            elif _bn_stats_fusable(L, L.in_bn, ctx.fwd_id):  # this conv is the BN output's only consumer
+                dx = _dgrad_bn(dy, L, list(x.shape), None, L.in_bn, ctx.fwd_id)
             else:
                 dx = _ops().conv2d_dgrad(dy, L.w(), list(x.shape), L.stride, L.pad)
         return dx, None, None
+
+
+def _take_bwd_part(bn, fid):
+    """The BN-backward partials a dgrad epilogue left for ``bn`` -- only if they belong to the
+    forward ``fid`` (else None: bn_bwd runs its own partial pass). Clears the layer's state when it
+    is this forward's (its consumers' dgrads have run)."""
+    tagged, bn.bwd_part = bn.bwd_part, None
+    if bn.fwd_state is not None and bn.fwd_state[6] == fid:
+        bn.fwd_state = None
+    return tagged[0] if tagged is not None and tagged[1] == fid else None
 
 
 class _BNReluConv(torch.autograd.Function):
@@ -289,8 +303,9 @@ class _BNReluConv(torch.autograd.Function):
     def forward(ctx, y, token, part, bn, conv):
         o = _ops()
         mean, invstd = o.bn_stats(y, part, bn.rmean, bn.rvar, bn.momentum, bn.eps)
-        bn.fwd_state = (y, mean, invstd, None, True, False)
-        ctx.bn, ctx.conv = bn, conv
+        fid = conv.model.fwd_id
+        bn.fwd_state = (y, mean, invstd, None, True, False, fid)
+        ctx.bn, ctx.conv, ctx.fwd_id = bn, conv, fid
         ctx.save_for_backward(y, mean, invstd)
         act = (mean, invstd, bn.gamma(), bn.beta())
         if conv.model.bn_stats:
@@ -308,12 +323,11 @@ class _BNReluConv(torch.autograd.Function):
         dout = dout.contiguous()
         o.conv2d_wgrad(y, dout, L.g(), L.stride, L.pad, L.model.grads_zeroed, mean, invstd, bn.gamma(), bn.beta())
         L.model.reducer.mark_ready(L.name)
-        if _bn_stats_fusable(L, bn):  # the BN output's gradient + its backward statistics partials
-            dbn = _dgrad_bn(dout, L, list(y.shape), None, bn)
+        if _bn_stats_fusable(L, bn, ctx.fwd_id):  # the BN output's gradient + its backward statistics partials
+            dbn = _dgrad_bn(dout, L, list(y.shape), None, bn, ctx.fwd_id)
         else:
             dbn = o.conv2d_dgrad(dout, L.w(), list(y.shape), L.stride, L.pad)
-        part, bn.bwd_part = bn.bwd_part, None
-        bn.fwd_state = None
+        part = _take_bwd_part(bn, ctx.fwd_id)
         # relu mask recomputed from y (beta given); `out` is never read
         dy, _ = o.bn_bwd(dbn, y, y, bn.gamma(), mean, invstd, True, False, bn.g_gamma(), bn.g_beta(), bn.beta(), None,
                          part)
@@ -343,8 +357,9 @@ class _BN(torch.autograd.Function):
             mask = torch.empty(y.numel() // y.shape[-1], y.shape[-1] // 8, dtype=torch.uint8, device=y.device)
         out, mean, invstd = _ops().bn_fwd(*args, part, mask)
         ctx.layer, ctx.relu, ctx.has_res = layer, relu, res is not None
-        # for the consuming conv's dgrad epilogue (conv2d_dgrad_bn): this step's forward state
-        layer.fwd_state = (y, mean, invstd, mask, relu, res is not None)
+        ctx.fwd_id = layer.model.fwd_id
+        # for the consuming conv's dgrad epilogue (conv2d_dgrad_bn): this forward's state, tagged
+        layer.fwd_state = (y, mean, invstd, mask, relu, res is not None, ctx.fwd_id)
         ctx.save_for_backward(y, out if mask is None else mask, mean, invstd)
         ctx.bits = mask is not None
         return out
@@ -359,8 +374,7 @@ class _BN(torch.autograd.Function):
         mask = out_or_mask if ctx.bits else None
         out = y if ctx.bits else out_or_mask  # not read when a mask (bits or from y) is given
         args = (dout.contiguous(), out, y, L.gamma(), mean, invstd, ctx.relu, ctx.has_res, L.g_gamma(), L.g_beta())
-        part, L.bwd_part = L.bwd_part, None  # partials from the dgrad that produced dout, if it made them
-        L.fwd_state = None  # its consumers' dgrads have run
+        part = _take_bwd_part(L, ctx.fwd_id)  # partials from the dgrad that produced dout, if it made them
         dy, dres = _ops().bn_bwd(*args, beta, mask, part)
         L.model.reducer.mark_ready(L.name + "/gamma")
         L.model.reducer.mark_ready(L.name + "/beta")
@@ -461,8 +475,8 @@ class BNLayer:
         self.model, self.name, self.c = model, name, c
         self.momentum, self.eps = 0.9, 1e-5
         self.res_join = None  # GradJoin of the residual input (identity shortcut)
-        self.fwd_state = None  # (y, mean, invstd, relu bits, relu, has_res) of this step's forward
-        self.bwd_part = None  # backward statistics partials left by the dgrad that produced dout
+        self.fwd_state = None  # (y, mean, invstd, relu bits, relu, has_res, fwd_id) of the latest forward
+        self.bwd_part = None  # (partials, fwd_id) left by the dgrad that produced dout
         model.specs.append(PSpec(name + "/gamma", (c,), "zeros" if zero_init else "ones"))
         model.specs.append(PSpec(name + "/beta", (c,), "zeros"))
         model.bns.append(self)
@@ -593,6 +607,7 @@ class ResNet:
             bn.rvar = torch.ones(bn.c, device=self.device)
         self.reducer = BucketReducer(self.fp)
         self.token = torch.zeros((), device=self.device, requires_grad=True)
+        self.fwd_id = 0
 
     @property
     def num_params(self) -> int:
@@ -606,6 +621,7 @@ class ResNet:
                                      small=small, small_bytes=int(small_mb * (1 << 20)))
 
     def forward(self, x_nhwc_f32: torch.Tensor) -> torch.Tensor:
+        self.fwd_id += 1  # tags the BN states this forward leaves for its own backward
         for j in self.joins:
             j.reset()
         for bn in self.bns:

@@ -308,9 +308,9 @@ def test_bn_bwd_stats_in_dgrad_epilogue(cuda, depth, monkeypatch):
     kinds = []
     orig = R._dgrad_bn
 
-    def spy(dy, L, xs, acc, bn):
+    def spy(dy, L, xs, acc, bn, fid):
         kinds.append(("bits" if bn.fwd_state[3] is not None else "from_y", acc is not None))
-        return orig(dy, L, xs, acc, bn)
+        return orig(dy, L, xs, acc, bn, fid)
 
     monkeypatch.setattr(R, "_dgrad_bn", spy)
     torch.manual_seed(depth)
@@ -367,3 +367,28 @@ def test_folded_bn_matches_unfused(cuda, depth):
     assert out[0][0] == out[1][0]
     assert torch.equal(out[0][2], out[1][2])
     torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-5, atol=1e-6)
+
+
+def test_second_forward_before_backward_keeps_bn_state_per_forward(cuda):
+    """Two train-mode forwards, then the FIRST one's backward: the BN-backward statistics the dgrad
+    epilogues would take from the layers' saved forward state belong to the second forward, so the
+    tagged state must be refused (the BN backward runs its own partial pass) -- the gradients equal
+    a clean forward + backward of the first batch."""
+    from tensorflow_distributed_amd.models.resnet import ResNet
+
+    torch.manual_seed(21)
+    x1 = torch.randn(4, 32, 32, 3, device=cuda)
+    x2 = torch.randn(4, 32, 32, 3, device=cuda) * 3 + 1
+    lab = torch.randint(0, 16, (4,), dtype=torch.int32, device=cuda)
+    grads = []
+    for second in (False, True):
+        m = ResNet(50, num_classes=16, device=cuda, seed=3, width=16, zero_init_residual=False)
+        m.fp.grad.zero_()
+        l1, _ = m.loss(x1, lab)
+        if second:
+            m.loss(x2, lab)  # its graph is dropped; its BN states overwrite the layers' ones
+        l1.backward()
+        torch.cuda.synchronize()
+        grads.append(m.fp.grad.clone())
+    rel = ((grads[1] - grads[0]).norm() / grads[0].norm()).item()
+    assert rel < 1e-2, rel
