@@ -684,14 +684,11 @@ __device__ __forceinline__ void fc1_dx_unpool_store(const MnistStepArgs& a, f32x
   }
 }
 // fc1 dX tile width: 64 (196 blocks at B = 128) inside the fused fc backward, where the dX tiles
-// share the launch with ~800 dW tiles; 32 (392 blocks) when dX runs alone (DP step, part 2), where
-// 196 blocks left a quarter of the CUs idle (A/B: one GPU 64 better by 1.3 us, DP 32 better by 1.5)
-// register stages of the long-K (1024) fc1 dX blocks: 1 with BK 128 (8 K-steps; RS 2 +1.3 us/step);
-// dX alone (DP): 2 (-0.3 us, profiles/ab_fc1_dx_tiles_r2.log)
+// share the launch with ~800 dW tiles (fc1_dx_block_dma); 32 (392 blocks) when dX runs alone (DP
+// step, part 2: the register pipeline below), where 196 blocks left a quarter of the CUs idle (A/B:
+// one GPU 64 better by 1.3 us, DP 32 better by 1.5). Register stages of the dX-alone blocks: 2
+// (-0.3 us, profiles/ab_fc1_dx_tiles_r2.log)
 constexpr int FDX_RS = 1, FDX_RS_ALONE = 2;
-#ifndef TFD_FDX_DMA  // 1: the fused fc backward's dX tiles on the DMA ring (fc1_dx_block_dma)
-#define TFD_FDX_DMA 1
-#endif
 // fc1 dX inside the fused fc backward: K = 1024 as 16 steps of 64 on a 4-stage LDS ring filled by
 // the buffer-load-to-LDS DMA (3 stages in flight behind the MFMAs, no VGPR staging). With the register
 // pipeline (gemm_mainloop, BK 128, RS 1) every one of 8 K steps waited a full memory round trip:
@@ -805,8 +802,7 @@ __global__ __launch_bounds__(256) void fc1_bwd(MnistStepArgs a, int n_dx, int pa
     if (id < n_dx) {
       int bx, by;
       fdx_tile(id, FDX_GX, gy, bx, by);
-      if (TFD_FDX_DMA) fc1_dx_block_dma(a, bx, by, smem_raw);
-      else fc1_dx_block(a, bx, by, (bf16*)smem_raw);
+      fc1_dx_block_dma(a, bx, by, smem_raw);
       return;
     }
     id -= n_dx;
@@ -1513,7 +1509,7 @@ void mnist_backward_a(const MnistStepArgs& a, hipStream_t s, int part) {
   constexpr int sm_dx = GemmSmem<FDX_BM, FDX_BN, FDX_BK, DenseLoader<true>, DenseLoader<true>>::BYTES;
   static_assert(sm_dx >= FDX_BM * (FDX_BN + 4) * 4, "fc1 dX staging image fits the GEMM's LDS");
   const int sm_og = (B * NCLS + 4 * OUTG_ROWS * NCLS) * 4;
-  const int sm = std::max(std::max(sm_dw, part == 2 || !TFD_FDX_DMA ? sm_dx : FDXD_SMEM), sm_og);
+  const int sm = std::max(std::max(sm_dw, part == 2 ? sm_dx : FDXD_SMEM), sm_og);
   set_smem<fc1_bwd>(sm);
   const int n_dx = FDX_GX * ((B + FDX_BM - 1) / FDX_BM);
   const int nb = part == 2 ? FDX_GX2 * ((B + FDX_BM - 1) / FDX_BM) : FDW_GX * FDW_GY + (part == 0 ? n_dx : 0) + OUTG_BLOCKS;
