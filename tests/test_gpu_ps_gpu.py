@@ -7,6 +7,7 @@ import json
 import os
 import re
 
+import numpy as np
 import pytest
 import torch
 
@@ -126,3 +127,40 @@ def test_gpu_ps_async_and_backup_workers_and_speedup(cuda, tmp_path):
     rb, _ = _run_cluster(tmp_path, "backup", ["--replicas_to_aggregate=2"], workers=3, steps=12)
     outb = "".join(rb["outputs"].values())
     assert "synchronous updates" in outb
+
+
+@pytest.mark.parametrize("opt", ["adam", "momentum"])
+def test_gpu_ps_restore_matches_host_ps_restore(cuda, tmp_path, opt):
+    """Checkpoint under the GPU parameter server, then restore it into fresh clusters: one with the
+    GPU ps (OP_INIT with host slot tensors, GpuPsShard.load_state, the pull_state checkpoint read;
+    momentum's 'accum' slot renamed 'm' on the way in) and one with the host ps. Both restored
+    clusters stop at once (train_steps below the restored step) and write their final checkpoint,
+    which must hold exactly the saved params, optimizer slots and global step."""
+    import shutil
+
+    from tensorflow_distributed_amd.training import checkpoint as C
+
+    base = ["--sync_replicas=False", f"--optimizer={opt}"]
+    _run_cluster(tmp_path, "saved", base, steps=12)
+    saved_dir = os.path.join(tmp_path, "saved")
+    def latest(d):
+        path = C.read_checkpoint_state(d)["model_checkpoint_path"]
+        return path if os.path.isabs(path) else os.path.join(d, path)
+
+    saved = C.load_bundle(latest(saved_dir))
+    gs = int(np.asarray(saved["global_step"]).item())
+    assert gs >= 12
+    outs = {}
+    for name, extra in (("gpu", []), ("host", ["--ps_on_gpu=False"])):
+        d = os.path.join(tmp_path, name)
+        shutil.copytree(saved_dir, d)
+        _run_cluster(tmp_path, name, base + extra, steps=1)
+        path = latest(d)
+        assert os.path.dirname(os.path.abspath(path)) == os.path.abspath(d), path  # its own final save
+        outs[name] = C.load_bundle(path)
+    for name, got in outs.items():
+        assert sorted(got) == sorted(saved), (name, sorted(got), sorted(saved))
+        for k, v in saved.items():
+            assert np.array_equal(np.asarray(got[k]), np.asarray(v)), (name, k)
+    slot_keys = [k for k in saved if "/" in k]
+    assert slot_keys, sorted(saved)  # the optimizer slots are in the checkpoint and were compared
