@@ -26,7 +26,7 @@ def test_mnist_kernels_have_no_ab_switches():
     src = open(os.path.join(ROOT, "csrc", "kernels", "mnist.hip")).read()
     switches = set(re.findall(r"#if(?:n?def)?\s+!?\(?(TFD_\w+)", src))
     assert switches <= {"TFD_STAMP"}, switches
-    assert len(src.splitlines()) < 1600
+    assert len(src.splitlines()) < 1700
 
 
 def test_removed_engine_paths_stay_removed():
