@@ -8,9 +8,8 @@
 //                    in registers into a zero-bordered LDS image, then conv2 as a whole-image
 //                    implicit GEMM from LDS with the same pooled epilogue.
 //   fc1_fwd          K4 (split-K MFMA GEMM, each split's K range in one memory round trip; fp32
-//                    slabs, reduced by the tile's last split block).
-//   fc1_fwd tail     K4 finish + K5 dropout (Philox) + the tile's K6 partials (last split block per tile)
-//   head_kernel      K6 finish + K7 + K8(dX) + K9 fused per batch row.
+//                    slabs, reduced by the head kernel).
+//   head_kernel      K4 finish + K5 dropout (Philox) + K6 + K7 + K8(dX) + K9 fused per batch row.
 //   fc1_bwd          K8 dW/db + K10 dW (+ bias row) and dX with the MaxPoolGrad + ReluGrad unpool
 //                    epilogue (K11), one launch.
 //   conv2_bwd_lds    K14 (+K12 bias row) wgrad slabs and K13 dgrad with conv1's relu/pool-mask
@@ -377,10 +376,7 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
   C12_STAMP(6);
 }
 
-// ---------------- K3: fc1 forward, split-K slabs, finished by the tile's last split block -----------
-// The slab stores are write-through (agent-scope relaxed atomic stores: sc1), so the tile's last
-// arriving split block can read them wherever the splits ran (fc1_tail).
-typedef __attribute__((address_space(1))) float fc1_gf32;
+// ---------------- K3: fc1 forward, split-K slabs ----------------
 struct SlabEpi {
   float* __restrict__ out;
   int ld, M, N;
@@ -388,89 +384,14 @@ struct SlabEpi {
     if (n >= N) return;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (m4 + r < M)
-        __hip_atomic_store((fc1_gf32*)(out + (size_t)(m4 + r) * ld + n), v[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (m4 + r < M) out[(size_t)(m4 + r) * ld + n] = v[r];
   }
 };
 constexpr int FC1_BM = 64, FC1_BN = 64, FC1_BK = FC1_BK_;
 constexpr int FC1_SPLITS = 7;  // 3136 = 7 * 448; each split's whole K range staged in one memory round trip
 constexpr int FC1_NKT = FEAT / FC1_SPLITS / FC1_BK;  // K-tiles per split
 static_assert(FC1_NKT * FC1_BK * FC1_SPLITS == FEAT, "fc1 split-K must tile K exactly");
-// K4 finish + K5 dropout + the fc1 tile's share of K6, by the LAST of the tile's split blocks (a
-// ticket per tile): the 7 slab tiles summed in split order (bit-identical to a separate reduction),
-// + bias, relu, dropout (Philox, keyed like the round-3 head) -> hd (bf16), and the tile's partial
-// logits over its 64 hidden units -> plog[tile column][row][10]. Workgroups are dealt to the 8 XCDs
-// round-robin by id and a tile's split blocks are ids x + 16 y + 32 z, so they share an XCD: the
-// ticket word also counts arrivals per XCC (3 bits each), and when all splits ran on the last
-// arriver's XCC its reads hit that XCD's L2 (sc0); otherwise they go to memory (sc1), which the
-// write-through slab stores reached before their block's ticket -- correct wherever the blocks ran.
-// Thread t: hidden units n0 + 4 (t & 15) .. + 3 of rows m0 + (t >> 4) + 16 p, p < 4.
-constexpr int FC1_TAIL_ROWS = 4;
-__device__ __forceinline__ void fc1_tail(const MnistStepArgs& a, int bx, int by, int train, bool local) {
-  const int t = threadIdx.x, g = t & 15, rl = t >> 4;
-  const int n = bx * FC1_BN + 4 * g;
-  const float kp = train ? a.keep_prob : 1.0f;
-  const f32x4 bias = *reinterpret_cast<const f32x4*>(a.p32 + OFF_BD1 + n);
-  f32x4 sl[FC1_TAIL_ROWS][FC1_SPLITS];
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.fc1_slab, (uint32_t)((int64_t)FC1_SPLITS * a.B * HID * 4));
-#pragma unroll
-  for (int p = 0; p < FC1_TAIL_ROWS; ++p) {
-    const int m = by * FC1_BM + rl + 16 * p;
-#pragma unroll
-    for (int z = 0; z < FC1_SPLITS; ++z) {
-      const uint32_t off = m < a.B ? (uint32_t)(((size_t)z * a.B + m) * HID + n) * 4u : kBufOOB;
-      const i32x4v v = local ? __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 1)     // sc0: L2
-                             : __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);   // sc1: memory
-      sl[p][z] = __builtin_bit_cast(f32x4, v);
-    }
-  }
-  float w2[4][NCLS];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int c = 0; c < NCLS; ++c) w2[j][c] = (a.p32 + OFF_OUT)[(size_t)(n + j) * NCLS + c];
-#pragma unroll
-  for (int p = 0; p < FC1_TAIL_ROWS; ++p) {
-    const int m = by * FC1_BM + rl + 16 * p;
-    f32x4 h = bias;
-#pragma unroll
-    for (int z = 0; z < FC1_SPLITS; ++z) h += sl[p][z];
-    float scale[4];
-    if (kp < 1.0f) {
-      const int64_t st = *a.step;
-      Philox4 r = philox4x32_10((uint32_t)(m * 256 + (n >> 2)), (uint32_t)st, (uint32_t)(st >> 32), a.rank, a.seed,
-                                0x5EED1234u);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) scale[j] = (u01(r.v[j]) < kp) ? (1.0f / kp) : 0.f;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) scale[j] = 1.f;
-    }
-    float hd[4], lp[NCLS];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) hd[j] = fmaxf(h[j], 0.f) * scale[j];
-#pragma unroll
-    for (int c = 0; c < NCLS; ++c) {
-      float v = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v = fmaf(hd[j], w2[j][c], v);
-      lp[c] = v;
-    }
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1)  // the 16 lanes of row m (fixed order: deterministic)
-#pragma unroll
-      for (int c = 0; c < NCLS; ++c) lp[c] += __shfl_xor(lp[c], o, 16);
-    if (m < a.B) {
-      *reinterpret_cast<uint2*>(a.hd + (size_t)m * HID + n) = make_uint2(pack_bf2(hd[0], hd[1]), pack_bf2(hd[2], hd[3]));
-      if (g == 0) {
-        float* pl = a.fc1_plog + ((size_t)bx * a.B + m) * NCLS;
-#pragma unroll
-        for (int c = 0; c < NCLS; ++c) pl[c] = lp[c];
-      }
-    }
-  }
-}
-__global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper, int train) {
+__global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DenseLoader<true> la{a.p2, FEAT, a.B, FEAT};
   DenseLoader<false> lb{a.pbf + OFF_WD1, HID, HID, FEAT};
@@ -478,22 +399,6 @@ __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper, int tr
   SlabEpi epi{a.fc1_slab + (size_t)z * a.B * HID, HID, a.B, HID};
   const int kb = z * kper;
   gemm_block_oneshot<FC1_BM, FC1_BN, FC1_BK, FC1_NKT, 2, 2>(la, lb, epi, blockIdx.y * FC1_BM, blockIdx.x * FC1_BN, kb, (bf16*)smem_raw);
-  // ticket: every thread's write-through slab stores complete, then one arrival (+1 for the count,
-  // +1 in this XCC's 3-bit field at bit 8 + 3 xcc)
-  __shared__ int tk;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-  if (threadIdx.x == 0) {
-    const int xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 7;  // HW_REG_XCC_ID
-    const int old = __hip_atomic_fetch_add(a.fc1_ticket + tile, 1 + (1 << (8 + 3 * xcc)), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    const int now = old + 1 + (1 << (8 + 3 * xcc));
-    tk = (now & 0xFF) == (int)gridDim.z ? 1 + (((now >> (8 + 3 * xcc)) & 7) == (int)gridDim.z) : 0;
-    if (tk) __hip_atomic_store(a.fc1_ticket + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next step
-  }
-  __syncthreads();
-  if (tk) fc1_tail(a, blockIdx.x, blockIdx.y, train, tk == 2);
 }
 
 // ---------------- K4-K9 head: reduce slabs, bias, relu, dropout, FC10, softmax-xent, bwd ----------
@@ -502,36 +407,70 @@ __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper, int tr
   do {                                                                                                   \
     if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[4 * a.B * 8 + blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
   } while (0)
-// K6 finish + K7 softmax-xent + K8 dh: one 256-thread block per batch row (thread t: hidden units
-// 4t .. 4t+3). Logits = the 16 fc1 tiles' partials (fc1_tail) + the bias; dh = dl W2^T through the
-// relu / dropout mask, which hd carries (hd != 0 <=> kept and h > 0; dh = d / keep_prob there).
+template <int CTRL, int RMASK, int BMASK, int N>
+__device__ __forceinline__ void dpp_add(float (&x)[N]) {  // x += x[DPP source lane]; masked-off lanes add 0
+#pragma unroll
+  for (int c = 0; c < N; ++c)
+    x[c] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x[c]), CTRL, RMASK, BMASK, true));
+}
 __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   HEAD_STAMP(0);
-  const int row = blockIdx.x, t = threadIdx.x;
+  const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n0 = 4 * t;
+#define HEAD_W(j, c) (a.p32 + OFF_OUT)[(size_t)(n0 + (j)) * NCLS + (c)]
   if (a.t_out && row == 0 && t == 0) *a.t_out = *a.step + 1;
+  // the label's dependent chain (step -> perm -> label) starts first, hidden behind the fc1 math
   const int lbl = batch_label(a, row);
-  __shared__ float lg[NCLS];
-  const uint2 hw = *reinterpret_cast<const uint2*>(a.hd + (size_t)row * HID + n0);
-  float w2[4][NCLS];
+  f32x4 h = *reinterpret_cast<const f32x4*>(a.p32 + OFF_BD1 + n0);
+  {  // all split-K slab loads in flight together (compile-time count: no per-load branches)
+    f32x4 p[FC1_SPLITS];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+    for (int s = 0; s < FC1_SPLITS; ++s) p[s] = *reinterpret_cast<const f32x4*>(a.fc1_slab + ((size_t)s * a.B + row) * HID + n0);
 #pragma unroll
-    for (int c = 0; c < NCLS; ++c) w2[j][c] = (a.p32 + OFF_OUT)[(size_t)(n0 + j) * NCLS + c];
-  if (t < NCLS) {
-    float pv[HID / FC1_BN];
+    for (int s = 0; s < FC1_SPLITS; ++s) h += p[s];
+  }
+  HEAD_STAMP(1);
+  float hd[4], scale[4];
+  const float kp = train ? a.keep_prob : 1.0f;
+  if (kp < 1.0f) {
+    const int64_t st = *a.step;
+    Philox4 r = philox4x32_10((uint32_t)(row * 256 + t), (uint32_t)st, (uint32_t)(st >> 32), a.rank, a.seed,
+                              0x5EED1234u);
 #pragma unroll
-    for (int x = 0; x < HID / FC1_BN; ++x) pv[x] = a.fc1_plog[(x * a.B + row) * NCLS + t];  // 32-bit index math
-    float v = a.p32[OFF_BOUT + t];
+    for (int j = 0; j < 4; ++j) scale[j] = (u01(r.v[j]) < kp) ? (1.0f / kp) : 0.f;
+  } else {
 #pragma unroll
-    for (int x = 0; x < HID / FC1_BN; ++x) v += pv[x];
-    lg[t] = v;
+    for (int j = 0; j < 4; ++j) scale[j] = 1.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) hd[j] = fmaxf(h[j], 0.f) * scale[j];
+  // logits partials
+  float lp[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) lp[c] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) lp[c] = fmaf(hd[j], HEAD_W(j, c), lp[c]);
+  }
+  HEAD_STAMP(2);
+  __shared__ float red[4][NCLS];
+  // DPP wave sums (quad swaps, row shifts, row broadcasts: no LDS round trips) of the 10 partials,
+  // interleaved; the wave total lands in lane 63
+  dpp_add<0xB1, 0xF, 0xF>(lp);   // quad_perm [1,0,3,2]
+  dpp_add<0x4E, 0xF, 0xF>(lp);   // quad_perm [2,3,0,1]
+  dpp_add<0x114, 0xF, 0xE>(lp);  // row_shr:4, banks 1-3
+  dpp_add<0x118, 0xF, 0xC>(lp);  // row_shr:8, banks 2-3
+  dpp_add<0x142, 0xA, 0xF>(lp);  // row_bcast:15 into rows 1, 3
+  dpp_add<0x143, 0xC, 0xF>(lp);  // row_bcast:31 into rows 2, 3
+  if (lane == 63) {
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) red[wv][c] = lp[c];
   }
   __syncthreads();
-  HEAD_STAMP(1);
   float logit[NCLS];
 #pragma unroll
-  for (int c = 0; c < NCLS; ++c) logit[c] = lg[c];
+  for (int c = 0; c < NCLS; ++c) logit[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + a.p32[OFF_BOUT + c];
   float mx = logit[0];
   int am = 0;
 #pragma unroll
@@ -541,30 +480,34 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
 #pragma unroll
   for (int c = 0; c < NCLS; ++c) se += __expf(logit[c] - mx);
   const float lse = mx + __logf(se);
+  HEAD_STAMP(3);
   if (t == 0) {
     a.loss_row[row] = lse - logit[lbl];
     a.correct_row[row] = (am == lbl) ? 1.f : 0.f;
   }
   if (!train) return;
   const float invB = 1.0f / (float)a.B;
-  const float inv_kp = a.keep_prob < 1.0f ? 1.0f / a.keep_prob : 1.0f;
   float dl[NCLS];
 #pragma unroll
   for (int c = 0; c < NCLS; ++c) dl[c] = (__expf(logit[c] - lse) - (c == lbl ? 1.f : 0.f)) * invB;
 #pragma unroll
   for (int c = 0; c < NCLS; ++c)
     if (t == c) a.dlogits[row * NCLS + c] = dl[c];
-  const uint32_t hb[4] = {hw.x & 0xFFFFu, hw.x >> 16, hw.y & 0xFFFFu, hw.y >> 16};
+  uint32_t hdw[2], dhw[2];
   float dhv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float d = 0.f;
 #pragma unroll
-    for (int c = 0; c < NCLS; ++c) d = fmaf(dl[c], w2[j][c], d);
-    dhv[j] = hb[j] != 0 ? d * inv_kp : 0.f;
+    for (int c = 0; c < NCLS; ++c) d = fmaf(dl[c], HEAD_W(j, c), d);
+    dhv[j] = (h[j] > 0.f) ? d * scale[j] : 0.f;
   }
-  *reinterpret_cast<uint2*>(a.dh + (size_t)row * HID + n0) = make_uint2(pack_bf2(dhv[0], dhv[1]), pack_bf2(dhv[2], dhv[3]));
-  HEAD_STAMP(2);
+#undef HEAD_W
+  hdw[0] = pack_bf2(hd[0], hd[1]); hdw[1] = pack_bf2(hd[2], hd[3]);
+  dhw[0] = pack_bf2(dhv[0], dhv[1]); dhw[1] = pack_bf2(dhv[2], dhv[3]);
+  *reinterpret_cast<uint2*>(a.hd + (size_t)row * HID + n0) = make_uint2(hdw[0], hdw[1]);
+  *reinterpret_cast<uint2*>(a.dh + (size_t)row * HID + n0) = make_uint2(dhw[0], dhw[1]);
+  HEAD_STAMP(4);
 }
 
 // ---------------- K8 output layer dW/db: [1025][10] = [Hd;1]^T dlogits ----------------
@@ -1554,9 +1497,7 @@ void mnist_forward_fc(const MnistStepArgs& a, bool train, hipStream_t s) {
     set_smem<fc1_fwd>(sm);
     const int kper = (FEAT + a.fc1_splits - 1) / a.fc1_splits;
     dim3 g(HID / FC1_BN, (B + FC1_BM - 1) / FC1_BM, a.fc1_splits);
-    if (!a.fc1_ticket || !a.fc1_plog || (int)(g.x * g.y) > kMnistFc1Tiles || FC1_SPLITS >= 8)
-      throw std::runtime_error("mnist_forward_fc: fc1 ticket / partial-logit workspace missing or too small");
-    fc1_fwd<<<g, 256, sm, s>>>(a, kper, train ? 1 : 0);
+    fc1_fwd<<<g, 256, sm, s>>>(a, kper);
   }
   head_kernel<<<B, 256, 0, s>>>(a, train ? 1 : 0);
 }

@@ -57,8 +57,6 @@ class MnistEngine : public torch::CustomClassHolder {
     p2_ = at::empty({B_, FEAT}, bf);
     idx2_ = at::empty({B_, FEAT}, u8);
     fc1_slab_ = at::empty({fc1_splits_, B_, HID}, f32);
-    fc1_ticket_ = at::zeros({kMnistFc1Tiles}, f32.dtype(at::kInt));
-    fc1_plog_ = at::empty({HID / 64, B_, NCLS}, f32);
     hd_ = at::empty({B_, HID}, bf);
     dh_ = at::empty({B_, HID}, bf);
     dlogits_ = at::empty({B_, NCLS}, f32);
@@ -1085,8 +1083,6 @@ class MnistEngine : public torch::CustomClassHolder {
     a.p2 = (uint16_t*)p2_.data_ptr();
     a.idx2 = (uint8_t*)idx2_.data_ptr();
     a.fc1_slab = (float*)fc1_slab_.data_ptr();
-    a.fc1_ticket = (int*)fc1_ticket_.data_ptr();
-    a.fc1_plog = (float*)fc1_plog_.data_ptr();
     a.hd = (uint16_t*)hd_.data_ptr();
     a.dh = (uint16_t*)dh_.data_ptr();
     a.dlogits = (float*)dlogits_.data_ptr();
@@ -1136,7 +1132,6 @@ class MnistEngine : public torch::CustomClassHolder {
   int64_t ipc_small_ = 0;
   bool ipc_gather_ = true;
   at::Tensor params_, pbf_, grad_, m_, v_, gbf_, step_, tnext_;
-  at::Tensor fc1_ticket_, fc1_plog_;
   at::Tensor p1_, idx1_, p2_, idx2_, fc1_slab_, hd_, dh_, dlogits_, loss_row_, correct_row_, dz2_, dp1m_, wg2_slab_,
       wg1_slab_, xbuf_, ybuf_;
   at::Tensor data_, labels_, perm_, rows_, xpre_, ypre_, dbg_;

@@ -33,8 +33,6 @@ struct MnistStepArgs {
   uint16_t* p1;  uint8_t* idx1;   // [B][14][14][32]
   uint16_t* p2;  uint8_t* idx2;   // [B][3136]
   float* fc1_slab;                // [fc1_splits][B][1024]
-  int* fc1_ticket;                // [kMnistFc1Tiles] zeroed once; each fc1 tile's last split block resets its word
-  float* fc1_plog;                // [16][B][10] partial logits of the 16 fc1 column tiles
   uint16_t* hd;  uint16_t* dh;    // [B][1024]
   float* dlogits;                 // [B][10]
   float* loss_row; float* correct_row;  // [B]
@@ -68,7 +66,6 @@ struct MnistStepArgs {
   int sfb_by_lo, sfb_by_hi;
 };
 
-constexpr int kMnistFc1Tiles = 1024;  // fc1 forward tiles (16 x ceil(B / 64)) the ticket array covers
 int mnist_fc1_splits(int B);
 int mnist_wg2_splits(int B);
 void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s);        // conv1, conv2, fc1, head
