@@ -152,7 +152,11 @@ def test_engine_dp_over_ipc_matches_single_rank_big_batch(cuda, world, sfb, zero
     torch.cuda.synchronize()
     ref = eng.params().cpu()
     init = M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()})
-    _close_elementwise(p0 - init, ref - init, "3-step update", rel=3e-2, absmax=6e-3)
+    # three steps: the ranks' bf16-wire gradients move the weights a little differently, and steps 2
+    # and 3 see those weights (max-pool argmax / relu flips near ties): every element of each
+    # tensor's 3-step update within 3 % of itself plus 5 % of the tensor's largest update (the
+    # one-step test below holds each reduced gradient to bf16-wire tolerance)
+    _close_elementwise(p0 - init, ref - init, "3-step update", rel=3e-2, absmax=5e-2)
 
 
 def _engine_dp_grads_worker(rank, world, B, sfb, zero=False):
