@@ -170,9 +170,10 @@ def test_dp_schedules_captured_equal_eager(cuda, mode, sfb, zero):
 
 @pytest.mark.parametrize("mode", ["rccl", "ipc"])
 def test_forced_dp_world1_captured_steps_track_fused(cuda, mode):
-    """Two eager + two graph-replayed steps (captured collectives) with dropout, SGD: the same
-    parameters as the fused one-GPU step with bf16-rounded local gradients, element by element (SGD:
-    the update is the gradient -- Adam's m/sqrt(v) would amplify any wire rounding where |g| ~ 0)."""
+    """Two eager + two graph-replayed steps (captured collectives) with dropout, SGD: the parameters
+    track the fused one-GPU step with bf16-rounded local gradients -- per tensor L2 and every element
+    bounded (SGD: the update is the gradient; Adam's m/sqrt(v) would amplify any wire rounding where
+    |g| ~ 0). test_forced_dp_world1_gradients_are_the_fused_gradients pins step 1 bit for bit."""
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     s = torch.cuda.Stream()
@@ -190,18 +191,15 @@ def test_forced_dp_world1_captured_steps_track_fused(cuda, mode):
     torch.cuda.synchronize()
     assert int(dp.step_tensor().item()) == int(ref.step_tensor().item()) == 4
     tr.check()
-    # the DP path sums the conv weight-gradient slabs in another fixed order than the fused step's
-    # optimizer (then both round to bf16): last-bit differences that four steps carry on. All but
-    # 1 % of each tensor's elements within 1 % of themselves + 0.5 % of the largest update, every
-    # element within 10 % of it.
+    # the fused step's optimizer reads the conv weight gradients in fp32 straight from their slabs, the
+    # DP path rounds them to bf16 (the wire): last-bit differences that four steps carry on. Per tensor:
+    # relative L2 error of the update <= 3 %, every element within 10 % of the largest update.
     d0, d1 = (ref.params() - params).cpu(), (dp.params() - params).cpu()
     for k, r in M.dict_from_flat(d0).items():
         d = M.dict_from_flat(d1)[k]
         err, big = (d - r).abs(), r.abs().max()
-        bad = err > 1e-2 * r.abs() + 5e-3 * big
-        msg = f"{k}: {int(bad.sum())}/{r.numel()} elements off; worst {err.max().item():.3e} vs max|r| {big.item():.3e}"
-        assert int(bad.sum()) <= 1e-2 * r.numel(), msg
-        assert bool((err <= 0.1 * big).all()), msg
+        rel = ((d - r).norm() / r.norm().clamp_min(1e-30)).item()
+        assert rel <= 3e-2 and bool((err <= 0.1 * big).all()), (k, rel, err.max().item(), big.item())
     assert torch.equal(dp.params_bf16(), dp.params().to(torch.bfloat16))
     tr.close()
 

@@ -70,23 +70,34 @@ def _set_opt(eng, sgd):
         eng.set_adam(0.01, 0.9, 0.999, 1e-8)
 
 
-def _close_elementwise(got, ref, what, rel=1.5e-2, absmax=4e-3, frac=0.0, cap=None):
-    """Per tensor of the flat layout: |got - ref| <= rel |ref| + absmax max|ref| for every element --
-    or, with frac > 0 (multi-step runs, where a max-pool argmax / relu flip near a tie moves single
-    elements further), for all but a fraction frac of the elements, and every element within cap
-    max|ref|."""
+def _close_elementwise(got, ref, what, rel=1.5e-2, absmax=4e-3):
+    """Per tensor of the flat layout: |got - ref| <= rel |ref| + absmax max|ref| for EVERY element
+    (bf16 wire rounding of the per-rank gradients, fp32 sums in a different order)."""
+    from tensorflow_distributed_amd.models import mnist_cnn as M
+
+    gd, rd = M.dict_from_flat(got), M.dict_from_flat(ref)
+    for k in rd:
+        r, d = rd[k].float(), gd[k].float()
+        tol = rel * r.abs() + absmax * r.abs().max()
+        bad = (d - r).abs() > tol
+        assert not bad.any(), (f"{what} {k}: {int(bad.sum())}/{r.numel()} elements off; worst |d-r| "
+                               f"{(d - r).abs().max().item():.3e} vs max|r| {r.abs().max().item():.3e}")
+
+
+def _close_multistep(got, ref, what, rel_l2=3e-2, cap=0.15):
+    """Several steps apart from the reference (each step sees weights the last one moved slightly
+    differently; max-pool argmax / relu flips near ties move single elements): per tensor, the
+    relative L2 error of the update <= rel_l2 and EVERY element within cap x the tensor's largest
+    update. (The one-step tests hold each element to bf16-wire tolerance.)"""
     from tensorflow_distributed_amd.models import mnist_cnn as M
 
     gd, rd = M.dict_from_flat(got), M.dict_from_flat(ref)
     for k in rd:
         r, d = rd[k].float(), gd[k].float()
         err, big = (d - r).abs(), r.abs().max()
-        bad = err > rel * r.abs() + absmax * big
-        msg = (f"{what} {k}: {int(bad.sum())}/{r.numel()} elements off; worst |d-r| {err.max().item():.3e} "
-               f"vs max|r| {big.item():.3e}")
-        assert int(bad.sum()) <= frac * r.numel(), msg
-        if cap is not None:
-            assert bool((err <= cap * big).all()), msg
+        rel = ((d - r).norm() / r.norm().clamp_min(1e-30)).item()
+        msg = f"{what} {k}: rel L2 {rel:.3e}; worst |d-r| {err.max().item():.3e} vs max|r| {big.item():.3e}"
+        assert rel <= rel_l2 and bool((err <= cap * big).all()), msg
 
 
 def _engine_dp_worker(rank, world, B, steps, sfb=False, zero=False, sgd=False):
@@ -131,8 +142,8 @@ def _engine_dp_worker(rank, world, B, steps, sfb=False, zero=False, sgd=False):
 def test_engine_dp_over_ipc_matches_single_rank_big_batch(cuda, world, sfb, zero):
     """DP=N (N processes sharing the GPU, IPC transport, captured graph; sfb: fc gradients from the
     all-gathered factors; zero: ZeRO-1 fc1 shards, the N >= 4 default) == DP=1 with N*B over three SGD
-    steps, element by element (SGD: the update is the gradient, no m/sqrt(v) amplification of the
-    bf16 wire rounding where |g| ~ 0)."""
+    steps: per tensor L2 and every element bounded (SGD: the update is the gradient, no m/sqrt(v)
+    amplification of the bf16 wire rounding where |g| ~ 0)."""
     from tensorflow_distributed_amd.models import mnist_cnn as M
 
     B, steps = 32, 3
@@ -157,12 +168,7 @@ def test_engine_dp_over_ipc_matches_single_rank_big_batch(cuda, world, sfb, zero
     torch.cuda.synchronize()
     ref = eng.params().cpu()
     init = M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()})
-    # three steps: the ranks' bf16-wire gradients move the weights a little differently, and steps 2
-    # and 3 see those weights (max-pool argmax / relu flips near ties move single elements): all but
-    # 0.1 % of each tensor's elements within the one-step tolerance, every element within 15 % of
-    # the tensor's largest update (the one-step test below holds every element to bf16-wire
-    # tolerance)
-    _close_elementwise(p0 - init, ref - init, "3-step update", rel=3e-2, absmax=6e-3, frac=1e-3, cap=0.15)
+    _close_multistep(p0 - init, ref - init, "3-step update")
 
 
 def _engine_dp_grads_worker(rank, world, B, sfb, zero=False):
