@@ -84,7 +84,7 @@ def _close_elementwise(got, ref, what, rel=1.5e-2, absmax=4e-3):
                                f"{(d - r).abs().max().item():.3e} vs max|r| {r.abs().max().item():.3e}")
 
 
-def _close_multistep(got, ref, what, rel_l2=3e-2, cap=0.15):
+def _close_multistep(got, ref, what, rel_l2=8e-2, cap=0.15):
     """Several steps apart from the reference (each step sees weights the last one moved slightly
     differently; max-pool argmax / relu flips near ties move single elements): per tensor, the
     relative L2 error of the update <= rel_l2 and EVERY element within cap x the tensor's largest
