@@ -51,6 +51,8 @@ def main(argv=None):
                     "epilogue (0: autograd adds; measured faster, see resnet.GradJoin)")
     ap.add_argument("--bn_bwd_stats", type=int, default=1, help="1: batch-norm backward statistics summed in the "
                     "epilogue of the dgrad that produces the BN's gradient (no separate partial pass)")
+    ap.add_argument("--masked_join", type=int, default=1, help="1: identity-shortcut gradients reach the joining "
+                    "conv's dgrad epilogue as (dout, relu bits), the residual BN backward writes no dres tensor")
     ap.add_argument("--fold_bn", type=int, default=0, help="1: single-consumer relu batch norms applied inside the "
                     "consuming conv's operand loader (no bn_apply pass; 0: the separate pass; 2: 1x1 consumers only)")
     ap.add_argument("--lr", type=float, default=0.1)
@@ -75,6 +77,7 @@ def main(argv=None):
                bn_stats=bool(a.bn_stats), bn_bwd_stats=bool(a.bn_bwd_stats), fold_bn=a.fold_bn)
     m.mask_from_y = bool(a.mask_from_y)
     m.relu_bits = bool(a.relu_bits)
+    m.masked_join = bool(a.masked_join)
     comm, transport, small = None, "none", None
     if ctx.world > 1:
         if ctx.comm is not None:  # one rank per GPU: RCCL over xGMI
@@ -189,7 +192,7 @@ def main(argv=None):
                        "optimizer": "sgd-momentum 0.9 wd 1e-4",
                        "hipgraph": not a.eager, "fuse_joins": bool(a.fuse_joins), "bn_stats": bool(a.bn_stats),
                        "mask_from_y": bool(a.mask_from_y), "relu_bits": bool(a.relu_bits),
-                       "bn_bwd_stats": bool(a.bn_bwd_stats), "fold_bn": a.fold_bn}}), flush=True)
+                       "bn_bwd_stats": bool(a.bn_bwd_stats), "fold_bn": a.fold_bn, "masked_join": bool(a.masked_join)}}), flush=True)
     for c in (comm if transport == "ipc" else None, small):
         if c is not None:
             if c.ipc.error():

@@ -88,8 +88,19 @@ std::tuple<at::Tensor, at::Tensor> conv2d_fwd_stats(const at::Tensor& x, const a
   return {y, part};
 }
 
+// acc_bits: acc is a residual BN's dout, the add is dout masked by that BN's forward relu bits
+const uint8_t* acc_bits_of(const c10::optional<at::Tensor>& acc_bits, const c10::optional<at::Tensor>& acc,
+                           at::IntArrayRef xshape) {
+  if (!acc_bits.has_value()) return nullptr;
+  TORCH_CHECK(acc.has_value(), "dgrad: acc_bits needs acc");
+  const int64_t C = xshape.back(), M = acc->numel() / C;
+  TORCH_CHECK(acc_bits->is_cuda() && acc_bits->scalar_type() == at::kByte && acc_bits->is_contiguous() &&
+                  acc_bits->numel() == M * (C / 8), "dgrad: acc_bits must be uint8 [M, C/8] relu bits");
+  return acc_bits->data_ptr<uint8_t>();
+}
+
 at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, at::IntArrayRef xshape, int64_t stride, int64_t pad,
-                        const c10::optional<at::Tensor>& acc) {
+                        const c10::optional<at::Tensor>& acc, const c10::optional<at::Tensor>& acc_bits) {
   check_bf16(dy, "dy", 4);
   check_bf16(w, "w", 4);
   TORCH_CHECK(xshape.size() == 4, "xshape [N,H,W,C]");
@@ -100,7 +111,7 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, at::IntArrayR
   }
   const ConvShape c = shape_of(x, w, stride, pad);
   TORCH_CHECK(dy.size(1) == c.Ho() && dy.size(2) == c.Wo() && dy.size(3) == c.K, "dgrad: dy shape mismatch");
-  conv_dgrad(c, bp(dy), bp(w), bp(x), cur(), acc.has_value() ? bp(*acc) : nullptr);
+  conv_dgrad(c, bp(dy), bp(w), bp(x), cur(), acc.has_value() ? bp(*acc) : nullptr, acc_bits_of(acc_bits, acc, xshape));
   return x;
 }
 
@@ -111,7 +122,8 @@ std::tuple<at::Tensor, at::Tensor> conv2d_dgrad_bn(const at::Tensor& dy, const a
                                                    int64_t stride, int64_t pad, const c10::optional<at::Tensor>& acc,
                                                    const at::Tensor& y, const at::Tensor& mean, const at::Tensor& invstd,
                                                    const at::Tensor& gamma, const c10::optional<at::Tensor>& beta,
-                                                   const c10::optional<at::Tensor>& mask, bool relu) {
+                                                   const c10::optional<at::Tensor>& mask, bool relu,
+                                                   const c10::optional<at::Tensor>& acc_bits) {
   check_bf16(dy, "dy", 4);
   check_bf16(w, "w", 4);
   check_bf16(y, "y", 4);
@@ -144,7 +156,8 @@ std::tuple<at::Tensor, at::Tensor> conv2d_dgrad_bn(const at::Tensor& dy, const a
     }
   }
   auto part = at::empty({conv_dgrad_bn_rows(c), 2, C}, dy.options().dtype(at::kFloat));
-  conv_dgrad_bn(c, bp(dy), bp(w), bp(x), cur(), acc.has_value() ? bp(*acc) : nullptr, b, fp(part));
+  conv_dgrad_bn(c, bp(dy), bp(w), bp(x), cur(), acc.has_value() ? bp(*acc) : nullptr, b, fp(part),
+                acc_bits_of(acc_bits, acc, xshape));
   return {x, part};
 }
 
@@ -369,10 +382,11 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.def("conv2d_fwd_stats(Tensor x, Tensor w, int stride, int pad, Tensor? mean=None, Tensor? invstd=None, "
         "Tensor? gamma=None, Tensor? beta=None) -> (Tensor, Tensor)");
   m.impl("conv2d_fwd_stats", c10::DispatchKey::CUDA, &conv2d_fwd_stats);
-  m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc=None) -> Tensor");
+  m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc=None, Tensor? acc_bits=None) "
+        "-> Tensor");
   m.impl("conv2d_dgrad", c10::DispatchKey::CUDA, &conv2d_dgrad);
   m.def("conv2d_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc, Tensor y, Tensor mean, "
-        "Tensor invstd, Tensor gamma, Tensor? beta, Tensor? mask, bool relu) -> (Tensor, Tensor)");
+        "Tensor invstd, Tensor gamma, Tensor? beta, Tensor? mask, bool relu, Tensor? acc_bits=None) -> (Tensor, Tensor)");
   m.impl("conv2d_dgrad_bn", c10::DispatchKey::CUDA, &conv2d_dgrad_bn);
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad, bool zeroed=False, Tensor? mean=None, "
         "Tensor? invstd=None, Tensor? gamma=None, Tensor? beta=None) -> ()");

@@ -34,8 +34,11 @@ void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, ui
                     hipStream_t st, const BnReluIn* act = nullptr);
 // add (optional, must not alias dx): dx = add + dgrad in the epilogue -- the residual-join sum of
 // two gradient paths without a separate add kernel
+// add_bits (stride 1, with add): add is a residual BN's dout and add_bits its forward relu bits
+// ([M][C/8]): the epilogue adds dout masked by the bits -- the dres that BN's backward then need not
+// write
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                const uint16_t* add = nullptr);
+                const uint16_t* add = nullptr, const uint8_t* add_bits = nullptr);
 // dgrad whose epilogue also emits the backward statistics partials of the batch norm whose output
 // was this conv's input (its dout is the dgrad output): part fp32 [conv_dgrad_bn_rows(c)][2][C] of
 // per-row-block sums of d and d * (y - mean) * invstd, d = dout through the BN's relu mask -- what
@@ -50,7 +53,7 @@ struct BnBwdStats {
 bool conv_dgrad_bn_supported(const ConvShape& c);
 int conv_dgrad_bn_rows(const ConvShape& c);
 void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                   const uint16_t* add, const BnBwdStats& b, float* part);
+                   const uint16_t* add, const BnBwdStats& b, float* part, const uint8_t* add_bits = nullptr);
 // dw: fp32 [R*S*C][K]; overwritten (zeroed first when split)
 // zeroed: dw is known to be zero already (the model zeroes its flat gradient buffer once per
 // step), so split-K needs no per-layer memset

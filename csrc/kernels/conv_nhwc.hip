@@ -329,6 +329,26 @@ struct StoreBf16Stats {
   }
 };
 
+// Residual-join add operand of a bf16-output epilogue: x[m][n] bf16, or -- bits != nullptr -- the
+// gradient through a residual batch norm's relu, x = that BN's dout and bits = the forward's relu
+// bits ([M][N/8] bytes): the masked dout is exactly the dres bn_bwd would have written (a bf16 value
+// or zero), so the BN backward skips that full-tensor write (ResNet identity shortcuts).
+struct AddSrc {
+  const uint16_t* x = nullptr;
+  const uint8_t* bits = nullptr;
+  __host__ __device__ AddSrc() {}
+  __host__ __device__ AddSrc(const uint16_t* p) : x(p) {}  // NOLINT: plain add operand
+  __host__ __device__ AddSrc(const uint16_t* p, const uint8_t* b) : x(p), bits(b) {}
+};
+__device__ __forceinline__ uint4 add_masked(uint4 q, uint32_t bits) {  // bit j keeps element j
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    o[k] = ((bits >> (2 * k)) & 1u ? w[k] & 0xFFFFu : 0u) | ((bits >> (2 * k + 1)) & 1u ? w[k] & 0xFFFF0000u : 0u);
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // ---- LDS-staged epilogue (bf16 outputs) ----
 // The fragment-order epilogues above store 2 B per lane in 4 row-strided 32-B pieces per wave
 // instruction, and AddStoreBf16 serialises its scalar residual loads on memory latency (the
@@ -371,7 +391,7 @@ struct BnB {
 };
 template <int BM, int BN, int WM, int WN, bool ADD, bool STATS, class RM = RowId, class BS = NoBnB>
 __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], char* smem, uint16_t* __restrict__ y,
-                                             const uint16_t* __restrict__ add, int M, int N, int m0, int n0,
+                                             AddSrc add, int M, int N, int m0, int n0,
                                              float* __restrict__ part, RM rowmap = RM{}, uint32_t ybytes = 0,
                                              BS bs = BS{}) {
   using E = LdsEpi<BM, BN, WM, WN>;
@@ -383,6 +403,7 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
   const int n = n0 + cc * 8;
   if (ybytes == 0) ybytes = (uint32_t)M * (uint32_t)N * 2u;
   uint4 q[E::CH];
+  [[maybe_unused]] uint32_t qb[E::CH];
   uint32_t orow[E::CH];
 #pragma unroll
   for (int c = 0; c < E::CH; ++c) orow[c] = rowmap(m0 + g0 + c * E::RG);
@@ -390,7 +411,9 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
 #pragma unroll
     for (int c = 0; c < E::CH; ++c) {
       const int m = m0 + g0 + c * E::RG;
-      q[c] = buf_ld(add, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, m < M && n < N);
+      const bool ok = m < M && n < N;
+      q[c] = buf_ld(add.x, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, ok);
+      if (add.bits) qb[c] = ok ? add.bits[(size_t)orow[c] * (N / 8) + n / 8] : 0u;
     }
   }
   float* cs = reinterpret_cast<float*>(smem);
@@ -439,6 +462,7 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
     const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * E::PITCH + cc * 8 + 4);
     float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     if constexpr (ADD) {
+      if (add.bits) q[c] = add_masked(q[c], qb[c]);
       const uint32_t w[4] = {q[c].x, q[c].y, q[c].z, q[c].w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -541,7 +565,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_kernel(LA la, LB lb, E
 
 // bf16-output GEMM with the LDS-staged epilogue: Y = A B (+ add), no split-K.
 template <int BM, int BN, class LA, class LB, bool ADD>
-__global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_kernel(LA la, LB lb, uint16_t* y, const uint16_t* add,
+__global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_kernel(LA la, LB lb, uint16_t* y, AddSrc add,
                                                                       int M, int N, int KD) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   f32x4 acc[BM / 32][BN / 32];
@@ -552,7 +576,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_kernel(LA la, LB 
 
 // dgrad (+ add) whose epilogue also emits the BN-backward partials of its output (BnB above)
 template <int BM, int BN, class LA, class LB, bool ADD, class BS>
-__global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_bnb_kernel(LA la, LB lb, uint16_t* y, const uint16_t* add,
+__global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_bnb_kernel(LA la, LB lb, uint16_t* y, AddSrc add,
                                                                           int M, int N, int KD, float* part, BS bs) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   f32x4 acc[BM / 32][BN / 32];
@@ -619,7 +643,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB
 // offset per phase by the caller, so the phases' row blocks stack)
 template <int BM, int BN, bool ADD, class BS = NoBnB>
 __global__ __launch_bounds__(256) TFD_CONV_ATTR void dgrad_phase_kernel(DgradPhaseA la, DgradPhaseB lb, uint16_t* dx,
-                                                                        const uint16_t* add, float* part = nullptr,
+                                                                        AddSrc add, float* part = nullptr,
                                                                         BS bs = BS{}) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   f32x4 acc[BM / 32][BN / 32];
@@ -651,7 +675,7 @@ constexpr int stats_smem() {
 }
 
 template <int BM, int BN, class LA, class LB, bool ADD>
-void launch_gemm_bf16(const LA& la, const LB& lb, uint16_t* y, const uint16_t* add, int M, int N, int KD,
+void launch_gemm_bf16(const LA& la, const LB& lb, uint16_t* y, AddSrc add, int M, int N, int KD,
                       hipStream_t st) {
   constexpr int sm = stats_smem<BM, BN, LA, LB>();
   static bool attr = false;
@@ -665,7 +689,7 @@ void launch_gemm_bf16(const LA& la, const LB& lb, uint16_t* y, const uint16_t* a
 }
 
 template <int BM, int BN, class LA, class LB, bool ADD, class BS>
-void launch_gemm_bf16_bnb(const LA& la, const LB& lb, uint16_t* y, const uint16_t* add, int M, int N, int KD, float* part,
+void launch_gemm_bf16_bnb(const LA& la, const LB& lb, uint16_t* y, AddSrc add, int M, int N, int KD, float* part,
                           const BS& bs, hipStream_t st) {
   constexpr int sm = stats_smem<BM, BN, LA, LB>();
   static bool attr = false;
@@ -735,9 +759,9 @@ void dispatch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int KD, 
 
 // bf16-output GEMM (optionally + add), same tile choice as dispatch()
 template <class LA, class LB>
-void dispatch_bf16(const LA& la, const LB& lb, uint16_t* y, const uint16_t* add, int M, int N, int KD, hipStream_t st) {
+void dispatch_bf16(const LA& la, const LB& lb, uint16_t* y, AddSrc add, int M, int N, int KD, hipStream_t st) {
   const OutTile t = out_tile(M, N);
-  if (add) {
+  if (add.x) {
     if (t == OT128) launch_gemm_bf16<128, 128, LA, LB, true>(la, lb, y, add, M, N, KD, st);
     else if (t == OT128x64) launch_gemm_bf16<128, 64, LA, LB, true>(la, lb, y, add, M, N, KD, st);
     else launch_gemm_bf16<64, 64, LA, LB, true>(la, lb, y, add, M, N, KD, st);
@@ -749,10 +773,10 @@ void dispatch_bf16(const LA& la, const LB& lb, uint16_t* y, const uint16_t* add,
 }
 
 template <class LA, class LB, class BS>
-void dispatch_bf16_bnb(const LA& la, const LB& lb, uint16_t* y, const uint16_t* add, int M, int N, int KD, float* part,
+void dispatch_bf16_bnb(const LA& la, const LB& lb, uint16_t* y, AddSrc add, int M, int N, int KD, float* part,
                        const BS& bs, hipStream_t st) {
   const OutTile t = out_tile(M, N);
-  if (add) {
+  if (add.x) {
     if (t == OT128) launch_gemm_bf16_bnb<128, 128, LA, LB, true>(la, lb, y, add, M, N, KD, part, bs, st);
     else if (t == OT128x64) launch_gemm_bf16_bnb<128, 64, LA, LB, true>(la, lb, y, add, M, N, KD, part, bs, st);
     else launch_gemm_bf16_bnb<64, 64, LA, LB, true>(la, lb, y, add, M, N, KD, part, bs, st);
@@ -824,7 +848,7 @@ struct G256Epi {
 };
 template <class C, bool ADD, bool STATS, class RM, class BS>
 __device__ __forceinline__ void g256_epilogue(f32x16 (&acc)[C::TM][C::TN], char* smem, uint16_t* __restrict__ y,
-                                              const uint16_t* __restrict__ add, int M, int N, int m0, int n0,
+                                              AddSrc add, int M, int N, int m0, int n0,
                                               float* __restrict__ part, RM rowmap, uint32_t ybytes, BS bs) {
   using E = G256Epi<C::BN>;
   constexpr bool BSTAT = BS::MODE >= 0;
@@ -854,13 +878,16 @@ __device__ __forceinline__ void g256_epilogue(f32x16 (&acc)[C::TM][C::TN], char*
     const int mb = m0 + 128 * h;
     uint32_t orow[E::CH];
     [[maybe_unused]] uint4 q[E::CH], yq[E::CH];
-    [[maybe_unused]] uint32_t mbits[E::CH];
+    [[maybe_unused]] uint32_t mbits[E::CH], qb[E::CH];
 #pragma unroll
     for (int c = 0; c < E::CH; ++c) {
       const int m = mb + g0 + c * E::RG;
       orow[c] = rowmap(m);
       const bool ok = m < M && n < N;
-      if constexpr (ADD) q[c] = buf_ld(add, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, ok);
+      if constexpr (ADD) {
+        q[c] = buf_ld(add.x, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, ok);
+        if (add.bits) qb[c] = ok ? add.bits[(size_t)orow[c] * (N / 8) + n / 8] : 0u;
+      }
       if constexpr (BSTAT) {
         yq[c] = buf_ld(bs.y, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, ok);
         if constexpr (BS::MODE == 3) mbits[c] = ok ? bs.bits[(size_t)orow[c] * (N / 8) + n / 8] : 0u;
@@ -884,6 +911,7 @@ __device__ __forceinline__ void g256_epilogue(f32x16 (&acc)[C::TM][C::TN], char*
       const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * E::PITCH + cc * 8 + 4);
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       if constexpr (ADD) {
+        if (add.bits) q[c] = add_masked(q[c], qb[c]);
         const uint32_t wq[4] = {q[c].x, q[c].y, q[c].z, q[c].w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -956,7 +984,7 @@ constexpr int g256_smem() {
 // bf16-output conv GEMM: part (STATS / BnB) gets one row per 256-row tile at part + tile_m * 2N
 template <int BN, bool AKC, bool BKC, class SA, class SB, bool ADD, bool STATS, class RM, class BS>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void g256_conv_kernel(
-    SA sa, SB sb, uint16_t* y, const uint16_t* add, int M, int N, int KD, float* part, RM rm, uint32_t ybytes, BS bs,
+    SA sa, SB sb, uint16_t* y, AddSrc add, int M, int N, int KD, float* part, RM rm, uint32_t ybytes, BS bs,
     int tiles_m, int tiles_n) {
   using C = G256<BN, G256WM<BN>::v, AKC, BKC>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -971,7 +999,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // (plain template launchers, no generic lambdas: instantiating the kernel template from a host
 // lambda made hipcc's host pass reject the device-only DMA builtin inside it)
 template <int BN, bool AKC, bool BKC, bool ADD, bool STATS, class SA, class SB, class RM, class BS>
-void g256_launch_bf16_bn(const SA& sa, const SB& sb, uint16_t* y, const uint16_t* add, int M, int N, int KD, float* part,
+void g256_launch_bf16_bn(const SA& sa, const SB& sb, uint16_t* y, AddSrc add, int M, int N, int KD, float* part,
                          hipStream_t st, RM rm, uint32_t ybytes, BS bs) {
   auto* k = &g256_conv_kernel<BN, AKC, BKC, SA, SB, ADD, STATS, RM, BS>;
   static bool attr = false;
@@ -984,7 +1012,7 @@ void g256_launch_bf16_bn(const SA& sa, const SB& sb, uint16_t* y, const uint16_t
   k<<<tm * tn, 512, g256_smem<BN>(), st>>>(sa, sb, y, add, M, N, KD, part, rm, ybytes, bs, tm, tn);
 }
 template <bool AKC, bool BKC, bool ADD, bool STATS, class SA, class SB, class RM = RowId, class BS = NoBnB>
-void g256_launch_bf16(const SA& sa, const SB& sb, uint16_t* y, const uint16_t* add, int M, int N, int KD, float* part,
+void g256_launch_bf16(const SA& sa, const SB& sb, uint16_t* y, AddSrc add, int M, int N, int KD, float* part,
                       hipStream_t st, RM rm = RM{}, uint32_t ybytes = 0, BS bs = BS{}) {
   const int bn = g256_bn(N);
   if (bn == 256) g256_launch_bf16_bn<256, AKC, BKC, ADD, STATS>(sa, sb, y, add, M, N, KD, part, st, rm, ybytes, bs);
@@ -1199,8 +1227,11 @@ static int dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t*
 }
 
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                const uint16_t* add) {
+                const uint16_t* add, const uint8_t* add_bits) {
   const int M = c.N * c.H * c.W;
+  if (add_bits && (!add || c.stride != 1 || !TFD_CONV_LDS_EPI))
+    throw std::runtime_error("conv_dgrad: a relu-masked add operand needs a stride-1 dgrad");
+  const AddSrc aa{add, add_bits};
   if (TFD_CONV_LDS_EPI && TFD_DGRAD_PHASES && c.stride > 1) {
     dgrad_strided(c, dy, w, dx, add, st);
     return;
@@ -1208,8 +1239,8 @@ void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint1
   if (use_g256(M, c.C)) {  // A = dY gather, B = W as [C][(r,s,k)]: both KC
     const int KD = c.R * c.S * c.K;
     auto go = [&](const auto& la, const auto& lb) {
-      if (add) g256_launch_bf16<true, true, true, false>(la, lb, dx, add, M, c.C, KD, nullptr, st);
-      else g256_launch_bf16<true, true, false, false>(la, lb, dx, add, M, c.C, KD, nullptr, st);
+      if (add) g256_launch_bf16<true, true, true, false>(la, lb, dx, aa, M, c.C, KD, nullptr, st);
+      else g256_launch_bf16<true, true, false, false>(la, lb, dx, aa, M, c.C, KD, nullptr, st);
     };
     if (is_pointwise(c)) {
       go(DenseX<true>{dy, c.K, M, c.K}, DenseX<true>{w, c.K, c.C, c.K});
@@ -1224,10 +1255,10 @@ void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint1
     if (is_pointwise(c)) {
       DenseX<true> la{dy, c.K, M, c.K};
       DenseX<true> lb{w, c.K, c.C, c.K};
-      dispatch_bf16(la, lb, dx, add, M, c.C, KD, st);
+      dispatch_bf16(la, lb, dx, aa, M, c.C, KD, st);
     } else {
       Geo g = make_geo(c, M, KD);
-      dispatch_bf16(DgradA{dy, g}, DgradB{w, g}, dx, add, M, c.C, KD, st);
+      dispatch_bf16(DgradA{dy, g}, DgradB{w, g}, dx, aa, M, c.C, KD, st);
     }
     return;
   }
@@ -1254,16 +1285,19 @@ int conv_dgrad_bn_rows(const ConvShape& c) {
 }
 
 void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                   const uint16_t* add, const BnBwdStats& b, float* part) {
+                   const uint16_t* add, const BnBwdStats& b, float* part, const uint8_t* add_bits) {
   if (!conv_dgrad_bn_supported(c)) throw std::runtime_error("conv_dgrad_bn: unsupported conv (C % 8, tap-less phases)");
+  if (add_bits && (!add || c.stride != 1))
+    throw std::runtime_error("conv_dgrad_bn: a relu-masked add operand needs a stride-1 dgrad");
+  const AddSrc aa{add, add_bits};
   const int M = c.N * c.H * c.W, KD = c.R * c.S * c.K;
   auto go = [&](const auto& bs) {
     if (c.stride > 1) {
       dgrad_strided(c, dy, w, dx, add, st, part, bs);
     } else if (use_g256(M, c.C)) {
       auto g2 = [&](const auto& la, const auto& lb) {
-        if (add) g256_launch_bf16<true, true, true, false>(la, lb, dx, add, M, c.C, KD, part, st, RowId{}, 0u, bs);
-        else g256_launch_bf16<true, true, false, false>(la, lb, dx, add, M, c.C, KD, part, st, RowId{}, 0u, bs);
+        if (add) g256_launch_bf16<true, true, true, false>(la, lb, dx, aa, M, c.C, KD, part, st, RowId{}, 0u, bs);
+        else g256_launch_bf16<true, true, false, false>(la, lb, dx, aa, M, c.C, KD, part, st, RowId{}, 0u, bs);
       };
       if (is_pointwise(c)) g2(DenseX<true>{dy, c.K, M, c.K}, DenseX<true>{w, c.K, c.C, c.K});
       else {
@@ -1271,10 +1305,10 @@ void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, ui
         g2(DgradA{dy, g}, DgradB{w, g});
       }
     } else if (is_pointwise(c)) {
-      dispatch_bf16_bnb(DenseX<true>{dy, c.K, M, c.K}, DenseX<true>{w, c.K, c.C, c.K}, dx, add, M, c.C, KD, part, bs, st);
+      dispatch_bf16_bnb(DenseX<true>{dy, c.K, M, c.K}, DenseX<true>{w, c.K, c.C, c.K}, dx, aa, M, c.C, KD, part, bs, st);
     } else {
       Geo g = make_geo(c, M, KD);
-      dispatch_bf16_bnb(DgradA{dy, g}, DgradB{w, g}, dx, add, M, c.C, KD, part, bs, st);
+      dispatch_bf16_bnb(DgradA{dy, g}, DgradB{w, g}, dx, aa, M, c.C, KD, part, bs, st);
     }
   };
   if (b.mode == 0) go(BnB<0>{b.y, b.mean, b.invstd, b.gamma, b.beta, b.bits});

@@ -187,22 +187,41 @@ class GradJoin:
         self.reset()
 
     def reset(self):
-        self.seen, self.acc = 0, None
+        self.seen, self.acc, self.bits = 0, None, None
 
-    def arrive(self, g=None, conv=None):
-        """``g``: a finished gradient; or ``conv=(dy, layer, xshape, fwd_id)``: compute it as a dgrad.
-        Returns the total for the last arrival, else None."""
+    def arrive(self, g=None, conv=None, masked=None):
+        """``g``: a finished gradient; ``conv=(dy, layer, xshape, fwd_id)``: compute it as a dgrad;
+        ``masked=(dout, relu_bits)``: the residual BN's gradient through its relu, never materialised
+        -- the conv arriving after it adds dout masked by the bits in its dgrad epilogue
+        (``acc_bits``), the dres write the BN backward skipped. Returns the total for the last
+        arrival, else None."""
         self.seen += 1
         last = self.seen == self.n
+        if masked is not None:
+            if last or self.acc is not None:  # not the usual order: materialise the masked gradient
+                dout, bits = masked
+                C = dout.shape[-1]
+                keep = ((bits.view(-1, C // 8).unsqueeze(-1) >> torch.arange(8, device=bits.device, dtype=torch.uint8)) & 1)
+                g = dout * keep.reshape(dout.shape).to(dout.dtype)
+                masked = None
+            else:
+                self.acc, self.bits = masked
+                return None
         if conv is not None:
             dy, L, xs, fid = conv
+            bits, self.bits = self.bits, None
             if last and _bn_stats_fusable(L, self.bn, fid):  # the sum is the BN's whole dout
-                g = _dgrad_bn(dy, L, xs, self.acc, self.bn, fid)
+                g = _dgrad_bn(dy, L, xs, self.acc, self.bn, fid, bits)
             elif self.acc is not None:
-                g = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad, self.acc)
+                g = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad, self.acc, bits)
             else:
                 g = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad)
         elif self.acc is not None:
+            if self.bits is not None:  # a second plain gradient after a masked one: materialise the latter
+                dout, bits = self.acc, self.bits
+                C = dout.shape[-1]
+                keep = ((bits.view(-1, C // 8).unsqueeze(-1) >> torch.arange(8, device=bits.device, dtype=torch.uint8)) & 1)
+                self.acc, self.bits = dout * keep.reshape(dout.shape).to(dout.dtype), None
             g = self.acc.add_(g)
         self.acc = g
         if last:
@@ -231,14 +250,14 @@ def _bn_stats_fusable(L, bn, fid) -> bool:
     return (not relu) or mask is not None or (not has_res and L.model.mask_from_y)
 
 
-def _dgrad_bn(dy, L, xs, acc, bn, fid):
+def _dgrad_bn(dy, L, xs, acc, bn, fid, acc_bits=None):
     """dX of conv ``L`` (+ ``acc``) with BN ``bn``'s backward partials summed in the same epilogue;
     the partials wait on the BN layer for its backward (which then skips its own partial pass),
     tagged with the forward they belong to."""
     y, mean, invstd, mask, relu, has_res, _ = bn.fwd_state
     beta = bn.beta() if (relu and mask is None) else None
     g, part = _ops().conv2d_dgrad_bn(dy, L.w(), xs, L.stride, L.pad, acc, y, mean, invstd, bn.gamma(), beta, mask,
-                                     relu)
+                                     relu, acc_bits)
     bn.bwd_part = (part, fid)
     return g
 
@@ -373,12 +392,18 @@ class _BN(torch.autograd.Function):
         beta = L.beta() if (ctx.relu and not ctx.has_res and L.model.mask_from_y) else None
         mask = out_or_mask if ctx.bits else None
         out = y if ctx.bits else out_or_mask  # not read when a mask (bits or from y) is given
-        args = (dout.contiguous(), out, y, L.gamma(), mean, invstd, ctx.relu, ctx.has_res, L.g_gamma(), L.g_beta())
+        dout = dout.contiguous()
+        # identity shortcut with relu bits: the join's conv adds dout masked by the bits in its dgrad
+        # epilogue, so the residual gradient is never written (GradJoin.arrive(masked=...))
+        masked = ctx.has_res and L.res_join is not None and mask is not None and L.model.masked_join
+        args = (dout, out, y, L.gamma(), mean, invstd, ctx.relu, ctx.has_res and not masked, L.g_gamma(), L.g_beta())
         part = _take_bwd_part(L, ctx.fwd_id)  # partials from the dgrad that produced dout, if it made them
         dy, dres = _ops().bn_bwd(*args, beta, mask, part)
         L.model.reducer.mark_ready(L.name + "/gamma")
         L.model.reducer.mark_ready(L.name + "/beta")
-        if ctx.has_res and L.res_join is not None:
+        if masked:
+            dres = L.res_join.arrive(masked=(dout, mask))
+        elif ctx.has_res and L.res_join is not None:
             dres = L.res_join.arrive(dres)
         return dy, (dres if ctx.has_res else None), None, None, None
 
@@ -560,6 +585,9 @@ class ResNet:
         # input element 9 times); 0 (default): the separate bn_apply pass -- measured no slower than
         # either fold on ResNet-50 b128 (13.79 vs 14.15 / 13.83 ms, profiles/resnet50_bn_fold_ab_r4.log)
         self.fold_bn = int(fold_bn)
+        # identity-shortcut gradient as (dout, relu bits) added in the joining conv's dgrad epilogue
+        # instead of a dres tensor written by the residual BN's backward (GradJoin.arrive(masked=))
+        self.masked_join = True
         cin = width
         exp = 4 if kind == "bottleneck" else 1
         prev_out_bn = None  # the BN that produced the current block input (None: the stem's maxpool)

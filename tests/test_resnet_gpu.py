@@ -308,9 +308,9 @@ def test_bn_bwd_stats_in_dgrad_epilogue(cuda, depth, monkeypatch):
     kinds = []
     orig = R._dgrad_bn
 
-    def spy(dy, L, xs, acc, bn, fid):
+    def spy(dy, L, xs, acc, bn, fid, acc_bits=None):
         kinds.append(("bits" if bn.fwd_state[3] is not None else "from_y", acc is not None))
-        return orig(dy, L, xs, acc, bn, fid)
+        return orig(dy, L, xs, acc, bn, fid, acc_bits)
 
     monkeypatch.setattr(R, "_dgrad_bn", spy)
     torch.manual_seed(depth)
@@ -392,3 +392,41 @@ def test_second_forward_before_backward_keeps_bn_state_per_forward(cuda):
         grads.append(m.fp.grad.clone())
     rel = ((grads[1] - grads[0]).norm() / grads[0].norm()).item()
     assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize("depth", [18, 50])
+def test_masked_join_matches_materialised_dres(cuda, depth):
+    """Identity-shortcut gradients handed to the joining conv's dgrad epilogue as (dout, relu bits)
+    (masked_join, the residual BN backward writes no dres) against the materialised dres tensor
+    (the oracle): the masked dout is exactly the bf16 dres, so loss and every gradient are bit-equal.
+    The masked operand must actually reach a dgrad epilogue."""
+    from tensorflow_distributed_amd.models import resnet as R
+
+    seen = []
+    orig = R.GradJoin.arrive
+
+    def spy(self, g=None, conv=None, masked=None):
+        if masked is not None:
+            seen.append(1)
+        return orig(self, g, conv, masked)
+
+    torch.manual_seed(depth + 7)
+    x = torch.randn(4, 32, 32, 3, device=cuda)
+    lab = torch.randint(0, 16, (4,), dtype=torch.int32, device=cuda)
+    out = []
+    for on in (False, True):
+        m = R.ResNet(depth, num_classes=16, device=cuda, seed=5, width=16, zero_init_residual=False)
+        m.masked_join = on
+        R.GradJoin.arrive = spy
+        try:
+            m.fp.grad.zero_()
+            loss, _ = m.loss(x, lab)
+            loss.backward()
+        finally:
+            R.GradJoin.arrive = orig
+        torch.cuda.synchronize()
+        out.append((loss.item(), m.fp.grad.clone()))
+    assert seen, "no identity-shortcut gradient took the masked path"
+    assert out[0][0] == out[1][0]
+    assert torch.isfinite(out[1][1]).all()
+    torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-5, atol=1e-6)
