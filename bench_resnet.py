@@ -53,6 +53,9 @@ def main(argv=None):
                     "epilogue of the dgrad that produces the BN's gradient (no separate partial pass)")
     ap.add_argument("--masked_join", type=int, default=1, help="1: identity-shortcut gradients reach the joining "
                     "conv's dgrad epilogue as (dout, relu bits), the residual BN backward writes no dres tensor")
+    ap.add_argument("--bn_slots", type=int, default=-1, help="BN statistics partials: S > 0 fp32 atomics into S "
+                    "zeroed slots, finalized inside the apply passes (no bn_final launches); 0 per-block rows + "
+                    "bn_final (fixed order); -1 the library default")
     ap.add_argument("--fold_bn", type=int, default=0, help="1: single-consumer relu batch norms applied inside the "
                     "consuming conv's operand loader (no bn_apply pass; 0: the separate pass; 2: 1x1 consumers only)")
     ap.add_argument("--lr", type=float, default=0.1)
@@ -73,6 +76,8 @@ def main(argv=None):
     ctx = D.init_from_env(use_gpu=True)
     spawn.check_world(a.gpus, ctx.world)
     dev = ctx.device
+    if a.bn_slots >= 0:
+        torch.ops.tfd.set_bn_part_slots(a.bn_slots)
     m = ResNet(a.depth, num_classes=1000, device=dev, seed=0, fuse_joins=bool(a.fuse_joins),
                bn_stats=bool(a.bn_stats), bn_bwd_stats=bool(a.bn_bwd_stats), fold_bn=a.fold_bn)
     m.mask_from_y = bool(a.mask_from_y)
@@ -192,7 +197,8 @@ def main(argv=None):
                        "optimizer": "sgd-momentum 0.9 wd 1e-4",
                        "hipgraph": not a.eager, "fuse_joins": bool(a.fuse_joins), "bn_stats": bool(a.bn_stats),
                        "mask_from_y": bool(a.mask_from_y), "relu_bits": bool(a.relu_bits),
-                       "bn_bwd_stats": bool(a.bn_bwd_stats), "fold_bn": a.fold_bn, "masked_join": bool(a.masked_join)}}), flush=True)
+                       "bn_bwd_stats": bool(a.bn_bwd_stats), "fold_bn": a.fold_bn, "masked_join": bool(a.masked_join),
+                       "bn_slots": int(torch.ops.tfd.bn_part_slots())}}), flush=True)
     for c in (comm if transport == "ipc" else None, small):
         if c is not None:
             if c.ipc.error():

@@ -61,6 +61,21 @@ Act act_of(const c10::optional<at::Tensor>& mean, const c10::optional<at::Tensor
   return a;
 }
 
+// A statistics-partials buffer [rows][2][C]: the caller's (slot mode: zeroed by the caller, the
+// ResNet model's per-forward arena) or a fresh one (zero-filled in slot mode).
+at::Tensor part_buffer(const c10::optional<at::Tensor>& given, int64_t rows, int64_t C, const at::TensorOptions& o,
+                       const char* what) {
+  if (given.has_value()) {
+    TORCH_CHECK(given->is_cuda() && given->scalar_type() == at::kFloat && given->is_contiguous() && given->dim() == 3 &&
+                    given->size(0) == rows && given->size(1) == 2 && given->size(2) == C &&
+                    reinterpret_cast<uintptr_t>(given->data_ptr()) % 16 == 0,
+                what, ": partials buffer must be contiguous 16-B aligned fp32 [", rows, ", 2, ", C, "]");
+    return *given;
+  }
+  auto f = o.dtype(at::kFloat);
+  return bn_slots() > 0 ? at::zeros({rows, 2, C}, f) : at::empty({rows, 2, C}, f);
+}
+
 at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
                       const c10::optional<at::Tensor>& mean, const c10::optional<at::Tensor>& invstd,
                       const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta) {
@@ -77,13 +92,14 @@ std::tuple<at::Tensor, at::Tensor> conv2d_fwd_stats(const at::Tensor& x, const a
                                                     int64_t pad, const c10::optional<at::Tensor>& mean,
                                                     const c10::optional<at::Tensor>& invstd,
                                                     const c10::optional<at::Tensor>& gamma,
-                                                    const c10::optional<at::Tensor>& beta) {
+                                                    const c10::optional<at::Tensor>& beta,
+                                                    const c10::optional<at::Tensor>& part_out) {
   check_bf16(x, "x", 4);
   check_bf16(w, "w", 4);
   const ConvShape c = shape_of(x, w, stride, pad);
   const Act a = act_of(mean, invstd, gamma, beta, c.C);
   auto y = at::empty({c.N, c.Ho(), c.Wo(), c.K}, x.options());
-  auto part = at::empty({conv_fwd_stats_rows(c, a.on), 2, c.K}, x.options().dtype(at::kFloat));
+  auto part = part_buffer(part_out, conv_fwd_stats_rows(c, a.on), c.K, x.options(), "conv2d_fwd_stats");
   conv_fwd_stats(c, bp(x), bp(w), bp(y), fp(part), cur(), a.ptr());
   return {y, part};
 }
@@ -123,7 +139,8 @@ std::tuple<at::Tensor, at::Tensor> conv2d_dgrad_bn(const at::Tensor& dy, const a
                                                    const at::Tensor& y, const at::Tensor& mean, const at::Tensor& invstd,
                                                    const at::Tensor& gamma, const c10::optional<at::Tensor>& beta,
                                                    const c10::optional<at::Tensor>& mask, bool relu,
-                                                   const c10::optional<at::Tensor>& acc_bits) {
+                                                   const c10::optional<at::Tensor>& acc_bits,
+                                                   const c10::optional<at::Tensor>& part_out) {
   check_bf16(dy, "dy", 4);
   check_bf16(w, "w", 4);
   check_bf16(y, "y", 4);
@@ -155,7 +172,7 @@ std::tuple<at::Tensor, at::Tensor> conv2d_dgrad_bn(const at::Tensor& dy, const a
       b.mode = 2;
     }
   }
-  auto part = at::empty({conv_dgrad_bn_rows(c), 2, C}, dy.options().dtype(at::kFloat));
+  auto part = part_buffer(part_out, conv_dgrad_bn_rows(c), C, dy.options(), "conv2d_dgrad_bn");
   conv_dgrad_bn(c, bp(dy), bp(w), bp(x), cur(), acc.has_value() ? bp(*acc) : nullptr, b, fp(part),
                 acc_bits_of(acc_bits, acc, xshape));
   return {x, part};
@@ -248,7 +265,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& y, const
                         (int)partials->size(0), cur(), mb);
     return {out, mean, invstd};
   }
-  auto part = at::empty({bn_partials_size(M, C)}, f);
+  auto part = at::empty({bn_partials_size(M, C)}, f);  // the partial pass's rows
   bn_forward(bp(y), fp(gamma), fp(beta), res ? bp(*res) : nullptr, relu ? 1 : 0, bp(out), fp(mean), fp(invstd), rm, rv,
              (float)momentum, (float)eps, M, C, fp(part), cur(), mb);
   return {out, mean, invstd};
@@ -379,14 +396,16 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.def("conv2d_fwd(Tensor x, Tensor w, int stride, int pad, Tensor? mean=None, Tensor? invstd=None, "
         "Tensor? gamma=None, Tensor? beta=None) -> Tensor");
   m.impl("conv2d_fwd", c10::DispatchKey::CUDA, &conv2d_fwd);
+  // part_out: the caller's partials buffer (slot mode: zeroed), returned as the second output
   m.def("conv2d_fwd_stats(Tensor x, Tensor w, int stride, int pad, Tensor? mean=None, Tensor? invstd=None, "
-        "Tensor? gamma=None, Tensor? beta=None) -> (Tensor, Tensor)");
+        "Tensor? gamma=None, Tensor? beta=None, Tensor? part_out=None) -> (Tensor, Tensor)");
   m.impl("conv2d_fwd_stats", c10::DispatchKey::CUDA, &conv2d_fwd_stats);
   m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc=None, Tensor? acc_bits=None) "
         "-> Tensor");
   m.impl("conv2d_dgrad", c10::DispatchKey::CUDA, &conv2d_dgrad);
   m.def("conv2d_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc, Tensor y, Tensor mean, "
-        "Tensor invstd, Tensor gamma, Tensor? beta, Tensor? mask, bool relu, Tensor? acc_bits=None) -> (Tensor, Tensor)");
+        "Tensor invstd, Tensor gamma, Tensor? beta, Tensor? mask, bool relu, Tensor? acc_bits=None, "
+        "Tensor? part_out=None) -> (Tensor, Tensor)");
   m.impl("conv2d_dgrad_bn", c10::DispatchKey::CUDA, &conv2d_dgrad_bn);
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad, bool zeroed=False, Tensor? mean=None, "
         "Tensor? invstd=None, Tensor? gamma=None, Tensor? beta=None) -> ()");
@@ -411,6 +430,14 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.def("bn_bwd(Tensor dout, Tensor out, Tensor y, Tensor gamma, Tensor mean, Tensor invstd, bool relu, "
         "bool want_dres, Tensor(a!) dgamma, Tensor(b!) dbeta, Tensor? beta=None, Tensor? mask=None, "
         "Tensor? partials=None) -> (Tensor, Tensor)");
+  // rows of a statistics-partials buffer in slot mode (TFD_BN_SLOTS; 0: one row per producer block)
+  m.def("bn_part_slots() -> int", []() -> int64_t { return bn_slots(); });
+  // switch the mode (between steps only; returns the previous one) -- the bit-exact tests take row mode
+  m.def("set_bn_part_slots(int slots) -> int", [](int64_t s) -> int64_t {
+    const int old = bn_slots();
+    set_bn_slots((int)s);
+    return old;
+  });
   m.impl("bn_bwd", c10::DispatchKey::CUDA, &bn_bwd);
   m.def("bn_infer(Tensor y, Tensor gamma, Tensor beta, Tensor rm, Tensor rv, float eps, bool relu) -> Tensor");
   m.impl("bn_infer", c10::DispatchKey::CUDA, &bn_infer_op);

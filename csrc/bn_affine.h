@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "conv_kernels.h"  // TFD_BN_SLOTS
+
 namespace tfd {
 
 __device__ __forceinline__ void bn_affine(float mean, float invstd, float gamma, float beta, float& sc, float& sh) {
@@ -30,6 +32,30 @@ __device__ __forceinline__ uint32_t bn_relu2(uint32_t w, bn_f32x2 sc, bn_f32x2 s
   bn_s16x2 b = __builtin_bit_cast(bn_s16x2, __builtin_convertvector(z, bn_bf16x2));
   b = __builtin_elementwise_max(b, (bn_s16x2){0, 0});
   return __builtin_bit_cast(uint32_t, b);
+}
+
+// The statistics-partials mode (bn_slots(), see conv_kernels.h) as each kernel TU's own device copy:
+// internal linkage, so conv_nhwc.hip and norm.hip each hold one, uploaded by set_bn_slots.
+static __device__ int g_bn_slots_dev = TFD_BN_SLOTS;
+static inline hipError_t bn_slots_upload(int s) { return hipMemcpyToSymbol(HIP_SYMBOL(g_bn_slots_dev), &s, sizeof(int)); }
+
+// Row of a [rows][2][N] statistics-partials buffer that producer row block `row` writes: the block
+// itself (row mode), or slot row % S (slot mode).
+__device__ __forceinline__ int bn_part_row(int row) {
+  const int sl = g_bn_slots_dev;
+  return sl > 0 ? row % sl : row;
+}
+// One producer block's column sums (a, b) of channel n: a plain store into its row, or fp32 atomic
+// adds into its slot of a zeroed buffer.
+__device__ __forceinline__ void put_bn_part(float* part, int row, int N, int n, float a, float b) {
+  float* p = part + (size_t)bn_part_row(row) * 2 * N;
+  if (g_bn_slots_dev > 0) {
+    atomicAdd(p + n, a);
+    atomicAdd(p + N + n, b);
+  } else {
+    p[n] = a;
+    p[N + n] = b;
+  }
 }
 
 }  // namespace tfd

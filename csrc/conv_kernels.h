@@ -74,7 +74,26 @@ int conv_gemm_core(int mode);
 void gemm_nt_bf16(const uint16_t* a, const uint16_t* bt, uint16_t* c, int M, int N, int K, hipStream_t st);
 
 // ---- batch norm (training mode, per-channel over the M = N*H*W rows of a [M][C] bf16 tensor) ----
-// partials: fp32 workspace of bn_partials_size(M, C) floats.
+// Statistics partials ([rows][2][C] fp32: per-channel sums of a and b over row blocks -- y and y^2
+// forward, d and d*xhat backward). Slot mode, bn_slots() = S > 0: every producer (the conv
+// epilogues, the partial pass) ADDS its row block's column sums into slot (row block % S) with fp32
+// atomics, so a buffer has S rows and MUST BE ZEROED before its producer runs (the ResNet model
+// zeroes one arena per forward); the apply passes then finalize the statistics inline from the S
+// slots -- no bn_final launch between producer and apply (106 per ResNet-50 step). S only spreads
+// same-address atomics. The fp32 sums' order is then not fixed (like the split-K weight gradients).
+// Row mode, S = 0: one row per producer block (fixed order, bit-reproducible) reduced by
+// bn_final_kernel -- what the bit-exact race tests select (set_bn_slots(0)). Default TFD_BN_SLOTS.
+// Switch only between steps (no captured graph or queued kernel may span a change).
+#ifndef TFD_BN_SLOTS
+#define TFD_BN_SLOTS 4
+#endif
+int bn_slots();
+void set_bn_slots(int s);
+// per-TU device copies of the mode (conv_nhwc.hip / norm.hip), set by set_bn_slots
+void bn_slots_upload_conv(int s);
+void bn_slots_upload_norm(int s);
+// partials: fp32 workspace of bn_partials_size(M, C) floats for the partial pass (one row per block
+// in either mode; only producer epilogues use the slots).
 int bn_partials_size(int M, int C);
 // mean/invstd [C]; running stats updated with `momentum` (TF decay semantics: r = r*m + x*(1-m)).
 void bn_forward(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,

@@ -520,8 +520,7 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
       float a = 0.f, b = 0.f;
 #pragma unroll 8
       for (int g = 0; g < E::RG; ++g) { a += cs[g * BN + col]; b += cs[(E::RG + g) * BN + col]; }
-      part[(size_t)blockIdx.y * 2 * N + nn] = a;
-      part[(size_t)blockIdx.y * 2 * N + N + nn] = b;
+      put_bn_part(part, blockIdx.y, N, nn, a, b);
     }
   }
 }
@@ -632,8 +631,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int w = 0; w < WM; ++w) { a += red[(w * BN + c) * 2]; b += red[(w * BN + c) * 2 + 1]; }
-    part[(size_t)blockIdx.y * 2 * N + n] = a;
-    part[(size_t)blockIdx.y * 2 * N + N + n] = b;
+    put_bn_part(part, blockIdx.y, N, n, a, b);
   }
 #endif
 }
@@ -969,8 +967,7 @@ __device__ __forceinline__ void g256_epilogue(f32x16 (&acc)[C::TM][C::TN], char*
       float a = 0.f, b = 0.f;
 #pragma unroll 8
       for (int g = 0; g < E::RG; ++g) { a += cs[g * C::BN + col]; b += cs[(E::RG + g) * C::BN + col]; }
-      part[nn] = a;
-      part[N + nn] = b;
+      put_bn_part(part, 0, N, nn, a, b);  // part: already the tile's row (or slot), see g256_conv_kernel
     }
   }
 }
@@ -981,7 +978,8 @@ constexpr int g256_smem() {
   return C::SMEM > G256Epi<BN>::BYTES ? C::SMEM : G256Epi<BN>::BYTES;
 }
 
-// bf16-output conv GEMM: part (STATS / BnB) gets one row per 256-row tile at part + tile_m * 2N
+// bf16-output conv GEMM: part (STATS / BnB) gets one row per 256-row tile at part + tile_m * 2N (slot
+// mode: added into slot tile_m % TFD_BN_SLOTS)
 template <int BN, bool AKC, bool BKC, class SA, class SB, bool ADD, bool STATS, class RM, class BS>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void g256_conv_kernel(
     SA sa, SB sb, uint16_t* y, AddSrc add, int M, int N, int KD, float* part, RM rm, uint32_t ybytes, BS bs,
@@ -993,7 +991,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   f32x16 acc[C::TM][C::TN];
   g256_mainloop<C>(sa, sb, tm * 256, tn * BN, 0, KD, smem_raw, acc);
   g256_epilogue<C, ADD, STATS, RM, BS>(acc, smem_raw, y, add, M, N, tm * 256, tn * BN,
-                                       part ? part + (size_t)tm * 2 * N : nullptr, rm, ybytes, bs);
+                                       part ? part + (size_t)bn_part_row(tm) * 2 * N : nullptr, rm, ybytes, bs);
 }
 
 // (plain template launchers, no generic lambdas: instantiating the kernel template from a host
@@ -1108,7 +1106,12 @@ void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t
   }
 }
 
+void bn_slots_upload_conv(int s) {
+  if (bn_slots_upload(s) != hipSuccess) throw std::runtime_error("set_bn_slots: device symbol upload failed");
+}
+
 int conv_fwd_stats_rows(const ConvShape& c, bool folded) {  // row blocks of the partials
+  if (bn_slots() > 0) return bn_slots();
   const int M = c.N * c.Ho() * c.Wo();
   if (!folded && use_g256(M, c.K)) return (M + 255) / 256;
   return TFD_CONV_LDS_EPI ? out_tile_rows(M, c.K) : (use_big_tiles(M, c.K) ? (M + 127) / 128 : (M + 63) / 64);
@@ -1198,7 +1201,8 @@ static int dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t*
       g.hpwp = FastDiv(g.Hp * g.Wp); g.wp = FastDiv(g.Wp); g.k = FastDiv(c.K); g.nsd = FastDiv(g.ns);
       DgradPhaseA la{dy, g};
       DgradPhaseB lb{w, g, c.S};
-      float* pp = part ? part + (size_t)rows * 2 * c.C : nullptr;
+      // slot mode: every phase adds into the same slots
+      float* pp = part ? part + (bn_slots() > 0 ? (size_t)0 : (size_t)rows * 2 * c.C) : nullptr;
       if (use_g256(g.M, c.C)) {
         rows += (g.M + 255) / 256;
         const uint32_t xbytes = (uint32_t)((int64_t)c.N * c.H * c.W * c.C * 2);
@@ -1274,6 +1278,7 @@ bool conv_dgrad_bn_supported(const ConvShape& c) {
 }
 static int bf16_out_rows(int M, int N) { return use_g256(M, N) ? (M + 255) / 256 : out_tile_rows(M, N); }
 int conv_dgrad_bn_rows(const ConvShape& c) {
+  if (bn_slots() > 0) return bn_slots();
   if (c.stride == 1) return bf16_out_rows(c.N * c.H * c.W, c.C);
   int rows = 0;
   for (int ph = 0; ph < c.stride; ++ph)

@@ -168,7 +168,7 @@ __global__ __launch_bounds__(NT) void bn_partial_kernel(const uint16_t* __restri
       for (int j = 0; j < 8; ++j) { sa[j] += red[0][q * tpr + ch][j]; sb[j] += red[1][q * tpr + ch][j]; }
     }
   }
-  if (g == 0) {
+  if (g == 0) {  // always one row per block (the partial pass is followed by bn_final in either mode)
     float* pa = part + (size_t)blockIdx.x * 2 * C;
 #pragma unroll
     for (int j = 0; j < 8; ++j) { pa[c0 + j] = sa[j]; pa[C + c0 + j] = sb[j]; }
@@ -223,31 +223,122 @@ __global__ __launch_bounds__(FIN_NT) void bn_final_kernel(int mode, const float*
   }
 }
 
+// Inline finalize (slot mode, bn_slots() > 0): the apply passes read the S slot sums of a zeroed
+// [S][2][C] buffer that the producer filled with atomics, instead of waiting on a bn_final launch.
+// Threads g == 0 (one per 8-channel chunk) sum the slots of their chunk, hand the block's per-channel
+// constants to the other row groups through LDS; block 0 also writes the statistics out (mean /
+// invstd + running stats forward, dbeta / dgamma backward) with bn_final_kernel's formulas.
+struct BnFin {
+  const float* part;  // [slots][2][C]
+  int slots;
+  float eps, momentum;
+  float *o0, *o1;       // forward: mean, invstd; backward: dbeta, dgamma (written by block 0)
+  float *rmean, *rvar;  // forward running statistics (optional)
+};
+constexpr int FIN_MAXC = 2048;
+constexpr int FIN_MAXS = 8;  // slot counts the inline finalize takes (set_bn_slots bounds it)
+// Stage 1 (before the barrier): row group g < G = min(rg, S) sums slots g, g + G, ... of its thread's
+// 8 channels and parks the pair in LDS [G][2][C] (rg * C = 2048, so at most 16 KB); stage 2 (after
+// it): every thread sums the G parked pairs of its channels. Fixed order, so every block of the
+// launch forms bit-identical statistics.
+__device__ __forceinline__ void fin_stage(const BnFin& f, int C, int c0, int g, int rg, float* lds) {
+  const int G = min(rg, f.slots);
+  if (g >= G) return;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, b0 = a0, b1 = a0;
+  for (int q = g; q < f.slots; q += G) {
+    const f32x4* pa = reinterpret_cast<const f32x4*>(f.part + (size_t)q * 2 * C + c0);
+    const f32x4* pb = reinterpret_cast<const f32x4*>(f.part + (size_t)q * 2 * C + C + c0);
+    a0 += pa[0];
+    a1 += pa[1];
+    b0 += pb[0];
+    b1 += pb[1];
+  }
+  f32x4* la = reinterpret_cast<f32x4*>(lds + (size_t)g * 2 * C + c0);
+  f32x4* lb = reinterpret_cast<f32x4*>(lds + (size_t)g * 2 * C + C + c0);
+  la[0] = a0;
+  la[1] = a1;
+  lb[0] = b0;
+  lb[1] = b1;
+}
+__device__ __forceinline__ void fin_sums(const BnFin& f, int C, int c0, int rg, const float* lds, float (&a)[8],
+                                         float (&b)[8]) {
+  const int G = min(rg, f.slots);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { a[j] = 0.f; b[j] = 0.f; }
+  for (int q = 0; q < G; ++q) {
+    const f32x4* la = reinterpret_cast<const f32x4*>(lds + (size_t)q * 2 * C + c0);
+    const f32x4* lb = reinterpret_cast<const f32x4*>(lds + (size_t)q * 2 * C + C + c0);
+    const f32x4 a0 = la[0], a1 = la[1], b0 = lb[0], b1 = lb[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a[j] += a0[j];
+      a[4 + j] += a1[j];
+      b[j] += b0[j];
+      b[4 + j] += b1[j];
+    }
+  }
+}
+
 // Elementwise passes walk the same row split as the partial kernel: thread = (8-channel chunk,
 // row group); its 8 channels' constants stay in registers for every row it touches; RU rows' loads
 // per batch are issued before the first use (branch-free buffer loads, see bn_partial_kernel).
 // HAS_RES / RELU are compile-time so no load sits under a branch.
-template <bool HAS_RES, bool RELU>
+template <bool HAS_RES, bool RELU, bool FIN = false>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict__ y, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, const float* __restrict__ mean,
                                                       const float* __restrict__ invstd,
                                                       const uint16_t* __restrict__ res,
                                                       uint16_t* __restrict__ out, int M, int C, int tpr, int rg, int rb,
-                                                      uint8_t* __restrict__ mbits) {
+                                                      uint8_t* __restrict__ mbits, BnFin fin = BnFin{}) {
   const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
-  if (g >= rg) return;
   const uint32_t nbytes = (uint32_t)M * (uint32_t)C * 2u;
-  float sc[8], sh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bn_affine(mean[c0 + j], invstd[c0 + j], gamma[c0 + j], beta[c0 + j], sc[j], sh[j]);
   const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
-  for (int rbase = r0 + g; rbase < r1; rbase += RU * rg) {
-    uint4 Y[RU], Q[RU];
+  uint4 Y[RU], Q[RU];
+  auto load = [&](int rs) {
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
-      Y[u] = row_ld(y, nbytes, rbase + u * rg, r1, C, c0);
-      if (HAS_RES) Q[u] = row_ld(res, nbytes, rbase + u * rg, r1, C, c0);
+      Y[u] = row_ld(y, nbytes, rs + u * rg, r1, C, c0);
+      if (HAS_RES) Q[u] = row_ld(res, nbytes, rs + u * rg, r1, C, c0);
     }
+  };
+  int rbase = r0 + g;
+  float sc[8], sh[8];
+  if constexpr (FIN) {
+    // the finalize's operands (gamma, beta, the slot sums) and the block's first row batch are in
+    // flight together: one memory latency before the barrier
+    float gm[8], bt[8];
+    __shared__ float fl[FIN_MAXC * 2];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { gm[j] = gamma[c0 + j]; bt[j] = beta[c0 + j]; }
+    fin_stage(fin, C, c0, g, rg, fl);
+    if (g < rg) load(rbase);
+    __syncthreads();
+    if (g >= rg) return;
+    float a[8], b[8];
+    fin_sums(fin, C, c0, rg, fl, a, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      const float mu = a[j] / (float)M;
+      const float var = fmaxf(b[j] / (float)M - mu * mu, 0.f);
+      const float is = rsqrtf(var + fin.eps);
+      if (blockIdx.x == 0 && g == 0) {
+        fin.o0[c] = mu;
+        fin.o1[c] = is;
+        if (fin.rmean) {
+          fin.rmean[c] = fin.rmean[c] * fin.momentum + mu * (1.f - fin.momentum);
+          fin.rvar[c] = fin.rvar[c] * fin.momentum + var * ((float)M / (float)max(M - 1, 1)) * (1.f - fin.momentum);
+        }
+      }
+      bn_affine(mu, is, gm[j], bt[j], sc[j], sh[j]);
+    }
+  } else {
+    if (g >= rg) return;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bn_affine(mean[c0 + j], invstd[c0 + j], gamma[c0 + j], beta[c0 + j], sc[j], sh[j]);
+    load(rbase);
+  }
+  for (; rbase < r1; rbase += RU * rg) {
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int r = rbase + u * rg;
@@ -280,11 +371,12 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict
         }
       }
     }
+    if (rbase + RU * rg < r1) load(rbase + RU * rg);
   }
 }
 
 // MASK: 0 no relu, 1 mask = out > 0, 2 mask recomputed from y
-template <int MASK>
+template <int MASK, bool FIN = false>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __restrict__ dout,
                                                           const uint16_t* __restrict__ out, const uint16_t* __restrict__ y,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -293,34 +385,65 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __rest
                                                           const float* __restrict__ dgamma,
                                                           uint16_t* __restrict__ dy, uint16_t* __restrict__ dres,
                                                           int M, int C, int tpr, int rg, int rb, float invM,
-                                                          const uint8_t* __restrict__ mbits) {
+                                                          const uint8_t* __restrict__ mbits, BnFin fin = BnFin{}) {
   const int t = threadIdx.x, ch = t % tpr, g = t / tpr, c0 = ch * 8;
-  if (g >= rg) return;
   const uint32_t nbytes = (uint32_t)M * (uint32_t)C * 2u;
-  // dy = k1 * dz + k2 * y + k3 with k1 = gamma*invstd, k2 = -k1*invstd*dgamma/M,
-  // k3 = -k1*(dbeta/M - mean*invstd^2*dgamma/M)
-  float k1[8], k2[8], k3[8], sc[8], sh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = c0 + j;
-    const float is = invstd[c];
-    k1[j] = gamma[c] * is;
-    k2[j] = -k1[j] * is * dgamma[c] * invM;
-    k3[j] = -k1[j] * (dbeta[c] * invM - mean[c] * is * dgamma[c] * invM);
-    if (MASK == 2) bn_affine(mean[c], is, gamma[c], beta[c], sc[j], sh[j]);  // the forward's constants (mask from y)
-  }
   const int r0 = blockIdx.x * rb, r1 = min(M, r0 + rb);
-  for (int rbase = r0 + g; rbase < r1; rbase += RU * rg) {
-    uint4 D[RU], Y[RU], O[RU];
-    uint32_t MB[RU];
+  uint4 D[RU], Y[RU], O[RU];
+  uint32_t MB[RU];
+  auto load = [&](int rs) {
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
-      const int r = rbase + u * rg;
+      const int r = rs + u * rg;
       D[u] = row_ld(dout, nbytes, r, r1, C, c0);
       Y[u] = row_ld(y, nbytes, r, r1, C, c0);
       if (MASK == 1) O[u] = row_ld(out, nbytes, r, r1, C, c0);
       if (MASK == 3) MB[u] = mask_byte(mbits, r, r1, tpr, ch);
     }
+  };
+  int rbase = r0 + g;
+  float db[8], dg[8];
+  // the per-channel operands, issued before any wait (the FIN barrier included)
+  float gm[8], is8[8], mu8[8], bt8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    gm[j] = gamma[c0 + j];
+    is8[j] = invstd[c0 + j];
+    mu8[j] = mean[c0 + j];
+    if (MASK == 2) bt8[j] = beta[c0 + j];
+  }
+  if constexpr (FIN) {  // dbeta / dgamma from the slot sums (block 0 writes them out)
+    __shared__ float fl[FIN_MAXC * 2];
+    fin_stage(fin, C, c0, g, rg, fl);
+    if (g < rg) load(rbase);  // the first batch is in flight while the sums are read
+    __syncthreads();
+    if (g >= rg) return;
+    fin_sums(fin, C, c0, rg, fl, db, dg);
+    if (blockIdx.x == 0 && g == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        fin.o0[c0 + j] = db[j];
+        fin.o1[c0 + j] = dg[j];
+      }
+    }
+  } else {
+    if (g >= rg) return;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { db[j] = dbeta[c0 + j]; dg[j] = dgamma[c0 + j]; }
+    load(rbase);
+  }
+  // dy = k1 * dz + k2 * y + k3 with k1 = gamma*invstd, k2 = -k1*invstd*dgamma/M,
+  // k3 = -k1*(dbeta/M - mean*invstd^2*dgamma/M)
+  float k1[8], k2[8], k3[8], sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float is = is8[j];
+    k1[j] = gm[j] * is;
+    k2[j] = -k1[j] * is * dg[j] * invM;
+    k3[j] = -k1[j] * (db[j] * invM - mu8[j] * is * dg[j] * invM);
+    if (MASK == 2) bn_affine(mu8[j], is, gm[j], bt8[j], sc[j], sh[j]);  // the forward's constants (mask from y)
+  }
+  for (; rbase < r1; rbase += RU * rg) {
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int r = rbase + u * rg;
@@ -346,6 +469,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const uint16_t* __rest
         *reinterpret_cast<uint4*>(dy + o) = pack8(w);
       }
     }
+    if (rbase + RU * rg < r1) load(rbase + RU * rg);
   }
 }
 
@@ -521,40 +645,109 @@ inline int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64
 
 void launch_apply(const uint16_t* y, const float* gamma, const float* beta, const float* mean, const float* invstd,
                   const uint16_t* res, int relu, uint16_t* out, int M, int C, const RowSplit& r, hipStream_t st,
-                  uint8_t* mb = nullptr) {
-  if (res && relu) bn_apply_kernel<true, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, mb);
-  else if (res) bn_apply_kernel<true, false><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, mb);
-  else if (relu) bn_apply_kernel<false, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, mb);
-  else bn_apply_kernel<false, false><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, mb);
+                  uint8_t* mb = nullptr, const BnFin* fin = nullptr) {
+#define TFD_BN_APPLY(R, U)                                                                                          \
+  if (fin)                                                                                                        \
+    bn_apply_kernel<R, U, true><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg,  \
+                                                       r.rb, mb, *fin);                                           \
+  else                                                                                                            \
+    bn_apply_kernel<R, U><<<r.nblk, NT, 0, st>>>(y, gamma, beta, mean, invstd, res, out, M, C, r.tpr, r.rg, r.rb, mb);
+  if (res && relu) { TFD_BN_APPLY(true, true) }
+  else if (res) { TFD_BN_APPLY(true, false) }
+  else if (relu) { TFD_BN_APPLY(false, true) }
+  else { TFD_BN_APPLY(false, false) }
+#undef TFD_BN_APPLY
+}
+
+template <int MK>
+void launch_bwd_apply(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma,
+                      const float* beta, const float* mean, const float* invstd, uint16_t* dy, uint16_t* dres,
+                      float* dgamma, float* dbeta, int M, int C, const RowSplit& r, hipStream_t st,
+                      const uint8_t* mb, const BnFin* fin) {
+  if (fin)
+    bn_bwd_apply_kernel<MK, true><<<r.nblk, NT, 0, st>>>(dout, out, y, gamma, beta, mean, invstd, dbeta, dgamma, dy, dres,
+                                                         M, C, r.tpr, r.rg, r.rb, 1.f / (float)M, mb, *fin);
+  else
+    bn_bwd_apply_kernel<MK><<<r.nblk, NT, 0, st>>>(dout, out, y, gamma, beta, mean, invstd, dbeta, dgamma, dy, dres, M, C,
+                                                   r.tpr, r.rg, r.rb, 1.f / (float)M, mb);
+}
+
+// backward: bn_final over the partial rows, then the apply pass; slots (a slot-mode buffer of nrows
+// slots from a dgrad epilogue): the apply pass finalizes inline
+void backward_apply(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma, const float* beta,
+                    const float* mean, const float* invstd, int relu, uint16_t* dy, uint16_t* dres, float* dgamma,
+                    float* dbeta, int M, int C, const float* partials, int nrows, hipStream_t st,
+                    const uint8_t* mask_bits, bool slots) {
+  const RowSplit r = row_split(M, C);
+  // beta given (no residual in the forward): the relu mask is recomputed from y, `out` is not read;
+  // mask_bits given: the forward's relu bits, `out` is not read
+  const int mask = !relu ? 0 : (mask_bits ? 3 : (beta ? 2 : 1));
+  BnFin f{partials, nrows, 0.f, 0.f, dbeta, dgamma, nullptr, nullptr};
+  const BnFin* fin = slots ? &f : nullptr;
+  if (!fin)
+    bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, nrows, M, C, 0.f, 0.f, dbeta, dgamma, nullptr, nullptr);
+  if (mask == 0) launch_bwd_apply<0>(dout, out, y, gamma, beta, mean, invstd, dy, dres, dgamma, dbeta, M, C, r, st, mask_bits, fin);
+  else if (mask == 1) launch_bwd_apply<1>(dout, out, y, gamma, beta, mean, invstd, dy, dres, dgamma, dbeta, M, C, r, st, mask_bits, fin);
+  else if (mask == 2) launch_bwd_apply<2>(dout, out, y, gamma, beta, mean, invstd, dy, dres, dgamma, dbeta, M, C, r, st, mask_bits, fin);
+  else launch_bwd_apply<3>(dout, out, y, gamma, beta, mean, invstd, dy, dres, dgamma, dbeta, M, C, r, st, mask_bits, fin);
 }
 
 }  // namespace
 
-int bn_partials_size(int M, int C) {
+static int g_bn_slots = TFD_BN_SLOTS;
+int bn_slots() { return g_bn_slots; }
+void bn_slots_upload_norm(int s) {
+  if (bn_slots_upload(s) != hipSuccess) throw std::runtime_error("set_bn_slots: device symbol upload failed");
+}
+void set_bn_slots(int s) {
+  if (s < 0 || s > FIN_MAXS) throw std::runtime_error("set_bn_slots: 0 (row mode) or 1..8 slots");
+  if (s == g_bn_slots) return;
+  bn_slots_upload_norm(s);
+  bn_slots_upload_conv(s);
+  g_bn_slots = s;
+}
+
+int bn_partials_size(int M, int C) {  // the partial pass's rows (row layout in either mode)
   const RowSplit r = row_split(M, C);
   return r.nblk * 2 * C;
 }
 
+namespace {
+void forward_apply(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
+                   uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var, float momentum,
+                   float eps, int M, int C, const float* partials, int nrows, hipStream_t st, uint8_t* mask_bits,
+                   bool slots) {
+  const RowSplit r = row_split(M, C);
+  if (slots) {
+    const BnFin f{partials, nrows, eps, momentum, mean, invstd, running_mean, running_var};
+    launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st, mask_bits, &f);
+    return;
+  }
+  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, nrows, M, C, eps, momentum, mean, invstd,
+                                                running_mean, running_var);
+  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st, mask_bits);
+}
+}  // namespace
+
+// partials from conv_fwd_stats: [nrows][2][C] rows (row mode) or zeroed slots filled by atomics (slot mode)
+void bn_forward_partials(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
+                         uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var,
+                         float momentum, float eps, int M, int C, const float* partials, int nrows, hipStream_t st,
+                         uint8_t* mask_bits) {
+  forward_apply(y, gamma, beta, residual, relu, out, mean, invstd, running_mean, running_var, momentum, eps, M, C,
+                partials, nrows, st, mask_bits, bn_slots() > 0);
+}
+
+// the partial pass writes one row per block in either mode (its blocks all end together, so slot
+// atomics there serialised into a tail: ResNet-50 bn_partial 46 -> 92 us), then bn_final
 void bn_forward(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
                 uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var, float momentum,
                 float eps, int M, int C, float* partials, hipStream_t st, uint8_t* mask_bits) {
   const RowSplit r = row_split(M, C);
   bn_partial_kernel<0, 0><<<r.nblk, NT, 0, st>>>(y, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, C, r.tpr,
                                                  r.rg, r.rb, partials, nullptr);
-  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, r.nblk, M, C, eps, momentum, mean, invstd,
-                                                running_mean, running_var);
-  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st, mask_bits);
-}
-
-// partials: [nrows][2][C] from conv_fwd_stats
-void bn_forward_partials(const uint16_t* y, const float* gamma, const float* beta, const uint16_t* residual, int relu,
-                         uint16_t* out, float* mean, float* invstd, float* running_mean, float* running_var,
-                         float momentum, float eps, int M, int C, const float* partials, int nrows, hipStream_t st,
-                         uint8_t* mask_bits) {
-  const RowSplit r = row_split(M, C);
-  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(0, partials, nrows, M, C, eps, momentum, mean, invstd,
-                                                running_mean, running_var);
-  launch_apply(y, gamma, beta, mean, invstd, residual, relu, out, M, C, r, st, mask_bits);
+  forward_apply(y, gamma, beta, residual, relu, out, mean, invstd, running_mean, running_var, momentum, eps, M, C,
+                partials, r.nblk, st, mask_bits, false);
 }
 
 void bn_stats_partials(float* mean, float* invstd, float* running_mean, float* running_var, float momentum, float eps,
@@ -567,38 +760,25 @@ void bn_backward(const uint16_t* dout, const uint16_t* out, const uint16_t* y, c
                  const float* mean, const float* invstd, int relu, uint16_t* dy, uint16_t* dres, float* dgamma,
                  float* dbeta, int M, int C, float* partials, hipStream_t st, const uint8_t* mask_bits) {
   const RowSplit r = row_split(M, C);
-  // beta given (no residual in the forward): the relu mask is recomputed from y, `out` is not read;
-  // mask_bits given: the forward's relu bits, `out` is not read
   const int mask = !relu ? 0 : (mask_bits ? 3 : (beta ? 2 : 1));
-#define TFD_BN_BWD(MK)                                                                                          \
-  bn_partial_kernel<1, MK><<<r.nblk, NT, 0, st>>>(y, dout, out, mean, invstd, gamma, beta, M, C, r.tpr, r.rg,     \
-                                                  r.rb, partials, mask_bits);                                    \
-  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, r.nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr,  \
-                                                nullptr);                                                       \
-  bn_bwd_apply_kernel<MK><<<r.nblk, NT, 0, st>>>(dout, out, y, gamma, beta, mean, invstd, dbeta, dgamma, dy, dres, M, \
-                                                 C, r.tpr, r.rg, r.rb, 1.f / (float)M, mask_bits);
-  if (mask == 0) { TFD_BN_BWD(0) }
-  else if (mask == 1) { TFD_BN_BWD(1) }
-  else if (mask == 2) { TFD_BN_BWD(2) }
-  else { TFD_BN_BWD(3) }
-#undef TFD_BN_BWD
+#define TFD_BN_PART(MK)                                                                                       \
+  bn_partial_kernel<1, MK><<<r.nblk, NT, 0, st>>>(y, dout, out, mean, invstd, gamma, beta, M, C, r.tpr, r.rg, \
+                                                  r.rb, partials, mask_bits);
+  if (mask == 0) { TFD_BN_PART(0) }
+  else if (mask == 1) { TFD_BN_PART(1) }
+  else if (mask == 2) { TFD_BN_PART(2) }
+  else { TFD_BN_PART(3) }
+#undef TFD_BN_PART
+  backward_apply(dout, out, y, gamma, beta, mean, invstd, relu, dy, dres, dgamma, dbeta, M, C, partials, r.nblk, st,
+                 mask_bits, false);
 }
 
 void bn_backward_partials(const uint16_t* dout, const uint16_t* out, const uint16_t* y, const float* gamma,
                           const float* beta, const float* mean, const float* invstd, int relu, uint16_t* dy,
                           uint16_t* dres, float* dgamma, float* dbeta, int M, int C, const float* partials, int nblk,
                           hipStream_t st, const uint8_t* mask_bits) {
-  const RowSplit r = row_split(M, C);
-  const int mask = !relu ? 0 : (mask_bits ? 3 : (beta ? 2 : 1));
-  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, st>>>(1, partials, nblk, M, C, 0.f, 0.f, dbeta, dgamma, nullptr, nullptr);
-#define TFD_BN_BWDP(MK)                                                                                          \
-  bn_bwd_apply_kernel<MK><<<r.nblk, NT, 0, st>>>(dout, out, y, gamma, beta, mean, invstd, dbeta, dgamma, dy, dres, M, \
-                                                 C, r.tpr, r.rg, r.rb, 1.f / (float)M, mask_bits);
-  if (mask == 0) { TFD_BN_BWDP(0) }
-  else if (mask == 1) { TFD_BN_BWDP(1) }
-  else if (mask == 2) { TFD_BN_BWDP(2) }
-  else { TFD_BN_BWDP(3) }
-#undef TFD_BN_BWDP
+  backward_apply(dout, out, y, gamma, beta, mean, invstd, relu, dy, dres, dgamma, dbeta, M, C, partials, nblk, st,
+                 mask_bits, bn_slots() > 0);
 }
 
 void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,

@@ -257,7 +257,7 @@ def _dgrad_bn(dy, L, xs, acc, bn, fid, acc_bits=None):
     y, mean, invstd, mask, relu, has_res, _ = bn.fwd_state
     beta = bn.beta() if (relu and mask is None) else None
     g, part = _ops().conv2d_dgrad_bn(dy, L.w(), xs, L.stride, L.pad, acc, y, mean, invstd, bn.gamma(), beta, mask,
-                                     relu, acc_bits)
+                                     relu, acc_bits, part_out=bn.acc_b)
     bn.bwd_part = (part, fid)
     return g
 
@@ -273,7 +273,7 @@ class _Conv(torch.autograd.Function):
         ctx.fwd_id = layer.model.fwd_id
         ctx.save_for_backward(x)
         if layer.model.bn_stats:
-            y, part = _ops().conv2d_fwd_stats(x, layer.w(), layer.stride, layer.pad)
+            y, part = _ops().conv2d_fwd_stats(x, layer.w(), layer.stride, layer.pad, part_out=layer.acc)
             ctx.mark_non_differentiable(part)
             ctx.set_materialize_grads(False)  # no zero-filled gradient for `part` in the backward
             return y, part
@@ -328,7 +328,7 @@ class _BNReluConv(torch.autograd.Function):
         ctx.save_for_backward(y, mean, invstd)
         act = (mean, invstd, bn.gamma(), bn.beta())
         if conv.model.bn_stats:
-            out, p2 = o.conv2d_fwd_stats(y, conv.w(), conv.stride, conv.pad, *act)
+            out, p2 = o.conv2d_fwd_stats(y, conv.w(), conv.stride, conv.pad, *act, part_out=conv.acc)
             ctx.mark_non_differentiable(p2)
             ctx.set_materialize_grads(False)
             return out, p2
@@ -467,13 +467,50 @@ class _SoftmaxXent(torch.autograd.Function):
         return dl.float() * dloss, None  # dl already carries the 1/N of the mean
 
 
+class StatArena:
+    """Batch-norm statistics slots in slot mode (``bn_part_slots() = S > 0``, csrc/conv_kernels.h):
+    the producer epilogues of BN statistics -- a conv's forward epilogue (``conv2d_fwd_stats``) and a
+    dgrad's BN-backward epilogue (``conv2d_dgrad_bn``) -- add their tiles' column sums into an
+    [S, 2, C] buffer with fp32 atomics, and the BN apply pass finalizes inline: no bn_final launch
+    between them. The buffers must start at zero, so they are slices of one arena zeroed once per
+    forward (one fill) instead of a fill per buffer. Each slice has one producer per forward /
+    backward (a conv's output slots; the slots of the dgrad producing a BN's dout), so a second forward
+    before a backward (whose BN states are refused, see _bn_stats_fusable) cannot mix sums. BNs
+    without such a producer keep bn_fwd / bn_bwd's own partial pass (row layout + bn_final).
+    S = 0 (row mode): no arena, the ops allocate per-tile partial rows that bn_final reduces."""
+
+    def __init__(self, model):
+        self.slots = int(_ops().bn_part_slots())
+        self.buf = None
+        if not self.slots:
+            return
+        S = self.slots
+        layout = []  # (owner, attr, C)
+        for L in model.convs:
+            layout.append((L, "acc", L.cout))
+        for bn in model.bns:
+            layout.append((bn, "acc_b", bn.c))
+        sizes = [(S * 2 * c + 63) // 64 * 64 for _, _, c in layout]  # 256-B aligned slices
+        self.buf = torch.zeros(sum(sizes), dtype=torch.float32, device=model.device)
+        off = 0
+        for (owner, attr, c), n in zip(layout, sizes):
+            setattr(owner, attr, self.buf[off:off + S * 2 * c].view(S, 2, c))
+            off += n
+
+    def zero(self):
+        if self.buf is not None:
+            self.buf.zero_()
+
+
 # ----------------------------------------------------------------------------- layers
 class ConvLayer:
     def __init__(self, model, name, cin, cout, k, stride, pad):
-        self.model, self.name, self.stride, self.pad, self.k = model, name, stride, pad, k
+        self.model, self.name, self.stride, self.pad, self.k, self.cout = model, name, stride, pad, k, cout
+        self.acc = None  # statistics-partials slots of this conv's output (StatArena), None: row mode
         self.in_join = None  # GradJoin of this conv's input (residual block inputs)
         self.in_bn = None  # the BN whose output is this conv's only input consumer (BN-backward stats)
         model.specs.append(PSpec(name, (k, k, cin, cout), "he", fan_in=k * k * cin))
+        model.convs.append(self)
 
     def w(self):
         return self.model.fp.w(self.name)
@@ -502,6 +539,8 @@ class BNLayer:
         self.res_join = None  # GradJoin of the residual input (identity shortcut)
         self.fwd_state = None  # (y, mean, invstd, relu bits, relu, has_res, fwd_id) of the latest forward
         self.bwd_part = None  # (partials, fwd_id) left by the dgrad that produced dout
+        # statistics-partials slots of the dgrad epilogue that produces this BN's dout (StatArena)
+        self.acc_b = None
         model.specs.append(PSpec(name + "/gamma", (c,), "zeros" if zero_init else "ones"))
         model.specs.append(PSpec(name + "/beta", (c,), "zeros"))
         model.bns.append(self)
@@ -564,6 +603,7 @@ class ResNet:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.specs: List[PSpec] = []
         self.bns: List[BNLayer] = []
+        self.convs: List[ConvLayer] = []
         self.stem = ConvLayer(self, "conv1", 8, width, 7, 2, 3)
         self.stem_bn = BNLayer(self, "bn1", width)
         self.blocks = []
@@ -634,6 +674,7 @@ class ResNet:
             bn.rmean = torch.zeros(bn.c, device=self.device)
             bn.rvar = torch.ones(bn.c, device=self.device)
         self.reducer = BucketReducer(self.fp)
+        self.stats = StatArena(self)
         self.token = torch.zeros((), device=self.device, requires_grad=True)
         self.fwd_id = 0
 
@@ -654,6 +695,7 @@ class ResNet:
             j.reset()
         for bn in self.bns:
             bn.fwd_state, bn.bwd_part = None, None
+        self.stats.zero()
         x = _ops().pad_channels(x_nhwc_f32, 8)
         x = self.stem_bn(self.stem(x))
         x = _MaxPool.apply(x, 3, 2, 1)
