@@ -69,7 +69,7 @@ def main(argv=None):
     import torch
 
     from tensorflow_distributed_amd import _native
-    from tensorflow_distributed_amd.models.resnet import ResNet
+    from tensorflow_distributed_amd.models.resnet import ResNet, retain_graph
     from tensorflow_distributed_amd.parallel import dist as D
 
     _native.require()
@@ -107,6 +107,7 @@ def main(argv=None):
     x = torch.randn(a.batch_size, a.image, a.image, 3, device=dev, generator=g)
     y = torch.randint(0, 1000, (a.batch_size,), device=dev, generator=g, dtype=torch.int32)
     s = torch.cuda.Stream(dev)
+    pool = torch.cuda.graph_pool_handle()  # every captured step (probes + the timed one) shares it
 
     def configure(mb):
         """Reducer with ``mb``-MB buckets, two eager steps, the step captured; returns run(k)."""
@@ -125,8 +126,9 @@ def main(argv=None):
                 return out
             return run, None
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, pool=pool):
             out_static = m.train_step(x, y, lr=a.lr)
+        retain_graph(graph)  # never destroyed while the process runs (models/resnet.py retain_graph)
 
         def run(k):
             for _ in range(k):

@@ -93,6 +93,33 @@ class FlatParams:
 
 
 # ----------------------------------------------------------------------------- bucketed reducer
+_RETAINED_GRAPHS: List["torch.cuda.CUDAGraph"] = []
+
+
+def retain_graph(g) -> None:
+    """Keep a captured CUDA graph alive until the process exits. On this stack (ROCm 7, PyTorch 2.10)
+    destroying a torch CUDAGraph captured over the two-stream DP step (the reducer's comm stream
+    forked off and joined back inside the capture) and then carrying on corrupted the host heap:
+    glibc aborts ("corrupted size vs. prev_size", "double free") a few reducer rebuilds later, in
+    1-49 capture/replay/destroy cycles over RCCL or IPC, never in 120 cycles without a graph nor in
+    80 with every graph kept (scripts/debug/rn_configure_loop.py). Callers that capture several
+    step graphs (bench_resnet.py's bucket probes) retain each one and share one memory pool between
+    them, so the kept graphs cost no extra memory."""
+    _RETAINED_GRAPHS.append(g)
+
+
+_EVENT_POOL: Dict[int, List[torch.cuda.Event]] = {}
+
+
+def _reducer_events(device, n: int) -> List["torch.cuda.Event"]:
+    """The first ``n`` events of the device's process-lifetime pool (grown on demand)."""
+    idx = torch.device(device).index or 0
+    pool = _EVENT_POOL.setdefault(idx, [])
+    while len(pool) < n:
+        pool.append(torch.cuda.Event())
+    return pool[:n]
+
+
 class BucketReducer:
     """Contiguous gradient buckets of ~``bucket_bytes``; a bucket's all-reduce is launched on the
     comm stream the moment its last parameter gradient has been written (backward overlap)."""
@@ -131,6 +158,13 @@ class BucketReducer:
                             for lo, hi in self.buckets]
         self.small_buckets = sum(1 for c in self.bucket_comm if c is small and small is not None)
         self.stream = torch.cuda.Stream(fp.device) if dp else None
+        # one event per bucket for the compute -> comm stream hand-off, from a pool that is never freed:
+        # an event recorded while a step is captured belongs to the captured graph, which may outlive
+        # this reducer (a fresh torch.cuda.Event per call was freed right after its record + wait:
+        # with a graph captured over such events, the host heap got corrupted within a few dozen
+        # reducer rebuilds, scripts/debug/rn_configure_loop.py)
+        ev = _reducer_events(fp.device, len(self.buckets) + 1) if dp else [None]
+        self.bucket_events, self.join_event = ev[:-1], ev[-1]
         self.events = []
         self.launched = 0
         # bf16 wire format halves the all-reduce bytes; the optimizer reads the bf16 sums directly
@@ -146,7 +180,7 @@ class BucketReducer:
         b = self.bucket_of[name]
         self.count[b] += 1
         if self.count[b] == self.need[b] and self.stream is not None:
-            ev = torch.cuda.Event()
+            ev = self.bucket_events[b]
             ev.record(torch.cuda.current_stream(self.fp.device))
             with torch.cuda.stream(self.stream):
                 self.stream.wait_event(ev)
@@ -160,8 +194,10 @@ class BucketReducer:
             self.launched += 1
 
     def finish(self):
-        if self.stream is not None:
-            torch.cuda.current_stream(self.fp.device).wait_stream(self.stream)
+        if self.stream is not None:  # the join event from the pool too (wait_stream makes a temporary one)
+            ev = self.join_event
+            ev.record(self.stream)
+            torch.cuda.current_stream(self.fp.device).wait_event(ev)
 
     def reduced_grads(self) -> torch.Tensor:
         return self.gbf if self.bf16 else self.fp.grad
