@@ -204,6 +204,10 @@ class BucketReducer:
 
 
 # ----------------------------------------------------------------------------- autograd ops
+# A/B switch: TFD_JOIN_DEFER=0 computes a join's first conv arrival at once (GradJoin.arrive)
+_JOIN_DEFER = os.environ.get("TFD_JOIN_DEFER", "1") != "0"
+
+
 class GradJoin:
     """Sum of the gradients that reach one activation over several paths (a residual block's input
     feeds the first conv and the shortcut), without autograd's separate elementwise add: the
@@ -223,47 +227,69 @@ class GradJoin:
         self.reset()
 
     def reset(self):
-        self.seen, self.acc, self.bits = 0, None, None
+        self.seen, self.acc, self.bits, self.deferred = 0, None, None, None
+
+    @staticmethod
+    def _unmask(dout, bits):
+        """dout through the relu bits, as a tensor (the masked operand's explicit form)."""
+        C = dout.shape[-1]
+        keep = ((bits.view(-1, C // 8).unsqueeze(-1) >> torch.arange(8, device=bits.device, dtype=torch.uint8)) & 1)
+        return dout * keep.reshape(dout.shape).to(dout.dtype)
+
+    def _add(self, g):
+        if self.acc is None:
+            self.acc = g
+            return
+        if self.bits is not None:  # a parked masked gradient meets a plain one: materialise it
+            self.acc, self.bits = self._unmask(self.acc, self.bits), None
+        self.acc = self.acc.add_(g)
 
     def arrive(self, g=None, conv=None, masked=None):
         """``g``: a finished gradient; ``conv=(dy, layer, xshape, fwd_id)``: compute it as a dgrad;
         ``masked=(dout, relu_bits)``: the residual BN's gradient through its relu, never materialised
-        -- the conv arriving after it adds dout masked by the bits in its dgrad epilogue
+        -- a conv arriving after it adds dout masked by the bits in its dgrad epilogue
         (``acc_bits``), the dres write the BN backward skipped. Returns the total for the last
-        arrival, else None."""
+        arrival, else None.
+
+        A conv whose dgrad can carry the BN-backward statistics (``_bn_stats_fusable``) arriving
+        first is deferred and run last, after the other arrival: then its epilogue sees the whole
+        dout and the BN backward needs no partial pass -- whichever order autograd delivers the two
+        paths in (a downsample block's strided 1x1 shortcut dgrad, which cannot carry them, used to
+        arrive last at 4 joins per ResNet-50 step)."""
         self.seen += 1
         last = self.seen == self.n
+        if (_JOIN_DEFER and not last and conv is not None and self.deferred is None and self.acc is None
+                and _bn_stats_fusable(conv[1], self.bn, conv[3])):
+            self.deferred = conv
+            return None
+        fuse_now = last and self.deferred is None
+        # fold this arrival into (acc, bits)
         if masked is not None:
-            if last or self.acc is not None:  # not the usual order: materialise the masked gradient
-                dout, bits = masked
-                C = dout.shape[-1]
-                keep = ((bits.view(-1, C // 8).unsqueeze(-1) >> torch.arange(8, device=bits.device, dtype=torch.uint8)) & 1)
-                g = dout * keep.reshape(dout.shape).to(dout.dtype)
-                masked = None
+            if self.acc is None and (not last or self.deferred is not None):
+                self.acc, self.bits = masked  # consumed by a later (or the deferred) dgrad's epilogue
             else:
-                self.acc, self.bits = masked
-                return None
-        if conv is not None:
+                self._add(self._unmask(*masked))
+        elif conv is not None:
             dy, L, xs, fid = conv
             bits, self.bits = self.bits, None
-            if last and _bn_stats_fusable(L, self.bn, fid):  # the sum is the BN's whole dout
-                g = _dgrad_bn(dy, L, xs, self.acc, self.bn, fid, bits)
+            if fuse_now and _bn_stats_fusable(L, self.bn, fid):  # the sum is the BN's whole dout
+                self.acc = _dgrad_bn(dy, L, xs, self.acc, self.bn, fid, bits)
             elif self.acc is not None:
-                g = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad, self.acc, bits)
+                self.acc = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad, self.acc, bits)
             else:
-                g = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad)
-        elif self.acc is not None:
-            if self.bits is not None:  # a second plain gradient after a masked one: materialise the latter
-                dout, bits = self.acc, self.bits
-                C = dout.shape[-1]
-                keep = ((bits.view(-1, C // 8).unsqueeze(-1) >> torch.arange(8, device=bits.device, dtype=torch.uint8)) & 1)
-                self.acc, self.bits = dout * keep.reshape(dout.shape).to(dout.dtype), None
-            g = self.acc.add_(g)
-        self.acc = g
-        if last:
-            self.acc = None
-            return g
-        return None
+                self.acc = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad)
+        elif g is not None:
+            self._add(g)
+        if not last:
+            return None
+        if self.deferred is not None:  # the deferred conv last: its epilogue sums the statistics
+            dy, L, xs, fid = self.deferred
+            bits, self.bits = self.bits, None
+            out = _dgrad_bn(dy, L, xs, self.acc, self.bn, fid, bits)
+        else:
+            out = self.acc if self.bits is None else self._unmask(self.acc, self.bits)
+        self.acc, self.bits, self.deferred = None, None, None
+        return out
 
 
 # A/B switch: TFD_BN_STATS_STRIDED=0 keeps the strided (phase) dgrads out of the BN-statistics fusion

@@ -371,7 +371,11 @@ def test_bn_bwd_stats_in_dgrad_epilogue(cuda, row_mode, depth, monkeypatch):
     g0, g1 = out[0][1], out[1][1]
     assert torch.isfinite(g1).all()
     rel = ((g1 - g0).norm() / g0.norm()).item()
-    assert rel < 1e-2, rel
+    # the fused path also sums each residual join in another order (GradJoin defers the conv that
+    # carries the statistics), so bf16 roundings differ; train-mode BN over these tiny batches
+    # amplifies that to 0.8-1.6 % relative at depth 18 / 50 -- as much as the order change alone gives
+    # at 8 x 64^2 images without any deferral (scripts/debug/bn_bwd_stats_rel.py)
+    assert rel < 3e-2, rel
     assert ("from_y", False) in kinds and ("bits", True) in kinds, kinds
 
 
@@ -436,7 +440,10 @@ def test_second_forward_before_backward_keeps_bn_state_per_forward(cuda):
         torch.cuda.synchronize()
         grads.append(m.fp.grad.clone())
     rel = ((grads[1] - grads[0]).norm() / grads[0].norm()).item()
-    assert rel < 1e-2, rel
+    # the refused states also turn off GradJoin's deferral, so the joins sum in another order: the
+    # tiny-batch amplification of bf16 rounding (see test_bn_bwd_stats_in_dgrad_epilogue) bounds this
+    # at a few %; a wrong forward's statistics would be off by far more (x2 is scaled and shifted)
+    assert rel < 3e-2, rel
 
 
 @pytest.mark.parametrize("depth", [18, 50])
