@@ -53,6 +53,8 @@ def main(argv=None):
                     "epilogue of the dgrad that produces the BN's gradient (no separate partial pass)")
     ap.add_argument("--masked_join", type=int, default=1, help="1: identity-shortcut gradients reach the joining "
                     "conv's dgrad epilogue as (dout, relu bits), the residual BN backward writes no dres tensor")
+    ap.add_argument("--fuse_stem_pool", type=int, default=1, help="1: the stem's bn + relu + max pool in one pass "
+                    "(the BN output is never written)")
     ap.add_argument("--bn_slots", type=int, default=-1, help="BN statistics partials: S > 0 fp32 atomics into S "
                     "zeroed slots, finalized inside the apply passes (no bn_final launches); 0 per-block rows + "
                     "bn_final (fixed order); -1 the library default")
@@ -83,6 +85,7 @@ def main(argv=None):
     m.mask_from_y = bool(a.mask_from_y)
     m.relu_bits = bool(a.relu_bits)
     m.masked_join = bool(a.masked_join)
+    m.fuse_stem_pool = bool(a.fuse_stem_pool)
     comm, transport, small = None, "none", None
     if ctx.world > 1:
         if ctx.comm is not None:  # one rank per GPU: RCCL over xGMI
@@ -200,6 +203,7 @@ def main(argv=None):
                        "hipgraph": not a.eager, "fuse_joins": bool(a.fuse_joins), "bn_stats": bool(a.bn_stats),
                        "mask_from_y": bool(a.mask_from_y), "relu_bits": bool(a.relu_bits),
                        "bn_bwd_stats": bool(a.bn_bwd_stats), "fold_bn": a.fold_bn, "masked_join": bool(a.masked_join),
+                       "fuse_stem_pool": bool(a.fuse_stem_pool),
                        "bn_slots": int(torch.ops.tfd.bn_part_slots())}}), flush=True)
     for c in (comm if transport == "ipc" else None, small):
         if c is not None:

@@ -344,6 +344,29 @@ std::tuple<at::Tensor, at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k,
   return {y, am};
 }
 
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_relu_maxpool_op(
+    const at::Tensor& y, const at::Tensor& gamma, const at::Tensor& beta, at::Tensor running_mean, at::Tensor running_var,
+    double momentum, double eps, const at::Tensor& partials, int64_t k, int64_t st, int64_t pad) {
+  check_bf16(y, "y", 4);
+  check_f32(gamma, "gamma");
+  check_f32(beta, "beta");
+  check_f32(partials, "partials");
+  const int N = (int)y.size(0), H = (int)y.size(1), W = (int)y.size(2), C = (int)y.size(3);
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && k <= 3 && y.numel() < (1ll << 30), "bn_relu_maxpool: C % 8, C <= 2048, k <= 3");
+  TORCH_CHECK(partials.dim() == 3 && partials.size(1) == 2 && partials.size(2) == C, "bn_relu_maxpool: partials [rows,2,C]");
+  const int Ho = (H + 2 * (int)pad - (int)k) / (int)st + 1, Wo = (W + 2 * (int)pad - (int)k) / (int)st + 1;
+  auto out = at::empty({N, Ho, Wo, C}, y.options());
+  auto am = at::empty({N, Ho, Wo, C}, y.options().dtype(at::kByte));
+  auto f = y.options().dtype(at::kFloat);
+  auto mean = at::empty({C}, f), invstd = at::empty({C}, f);
+  float* rm = running_mean.defined() && running_mean.numel() ? fp(running_mean) : nullptr;
+  float* rv = running_var.defined() && running_var.numel() ? fp(running_var) : nullptr;
+  bn_relu_maxpool(bp(y), fp(gamma), fp(beta), fp(mean), fp(invstd), rm, rv, (float)momentum, (float)eps, fp(partials),
+                  (int)partials.size(0), bp(out), am.data_ptr<uint8_t>(), N, H, W, C, (int)k, (int)st, (int)pad, Ho, Wo,
+                  cur());
+  return {out, am, mean, invstd};
+}
+
 at::Tensor maxpool2d_bwd(const at::Tensor& dy, const at::Tensor& am, at::IntArrayRef xshape, int64_t k, int64_t st,
                          int64_t pad) {
   check_bf16(dy, "dy", 4);
@@ -443,6 +466,9 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.impl("bn_infer", c10::DispatchKey::CUDA, &bn_infer_op);
   m.def("maxpool2d_fwd(Tensor x, int k, int stride, int pad) -> (Tensor, Tensor)");
   m.impl("maxpool2d_fwd", c10::DispatchKey::CUDA, &maxpool2d_fwd);
+  m.def("bn_relu_maxpool(Tensor y, Tensor gamma, Tensor beta, Tensor(a!) running_mean, Tensor(b!) running_var, "
+        "float momentum, float eps, Tensor partials, int k, int stride, int pad) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.impl("bn_relu_maxpool", c10::DispatchKey::CUDA, &bn_relu_maxpool_op);
   m.def("maxpool2d_bwd(Tensor dy, Tensor argmax, int[] xshape, int k, int stride, int pad) -> Tensor");
   m.impl("maxpool2d_bwd", c10::DispatchKey::CUDA, &maxpool2d_bwd);
   m.def("avgpool_fwd(Tensor x) -> Tensor");

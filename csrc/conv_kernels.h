@@ -126,6 +126,14 @@ void bn_backward_partials(const uint16_t* dout, const uint16_t* out, const uint1
 void bn_infer(const uint16_t* y, const float* gamma, const float* beta, const float* rmean, const float* rvar,
               float eps, int relu, uint16_t* out, int M, int C, hipStream_t st);
 
+// the stem's training-mode relu(bn(y)) + max pool in one pass (the BN output is never written):
+// statistics from conv_fwd_stats partials (finalized inline in slot mode), mean / invstd / running
+// stats as bn_forward_partials; out / argmax exactly those of bn_forward_partials + maxpool_fwd
+void bn_relu_maxpool(const uint16_t* y, const float* gamma, const float* beta, float* mean, float* invstd,
+                     float* running_mean, float* running_var, float momentum, float eps, const float* partials,
+                     int nrows, uint16_t* out, uint8_t* argmax, int N, int H, int W, int C, int k, int st, int pad,
+                     int Ho, int Wo, hipStream_t s);
+
 // ---- pooling / head ----
 void maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* argmax, int N, int H, int W, int C, int k, int st, int pad,
                  int Ho, int Wo, hipStream_t s);

@@ -529,6 +529,164 @@ __global__ __launch_bounds__(NT) void maxpool_fwd_kernel(const uint16_t* __restr
 }
 
 // gather form: every input element sums the output windows whose argmax points at it
+// The stem's relu(bn(y)) -> max pool in one pass: the BN output (the largest activation of a ResNet,
+// 112x112x64 per image) is never written or re-read. Thread = (8-channel chunk, row group) as in the
+// apply passes, so the inline finalize (FIN, slot mode) is bn_apply_kernel's; each thread then walks
+// pooled pixels grid-stride. A window's KMAX^2 16-B loads are issued together (range-checked buffer
+// loads, no branch); every tap goes through bn_relu2 -- bn_apply's packed form, bit for bit -- before
+// the max, so output and argmax equal bn_apply + maxpool_fwd_kernel's (strict >, taps in r, s order).
+constexpr int POOL_KMAX = 3;
+template <bool FIN>
+__global__ __launch_bounds__(NT) void bn_relu_maxpool_kernel(const uint16_t* __restrict__ y, const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd, uint16_t* __restrict__ out,
+                                                             uint8_t* __restrict__ am, int N, int H, int W, int C, int k,
+                                                             int st, int pad, int Ho, int Wo, BnFin fin) {
+  const int tpr = C / 8, t = threadIdx.x, ch = t % tpr, g = t / tpr, rg = NT / tpr, c0 = ch * 8;
+  const int M = N * H * W;
+  bn_f32x2 sc2[4], sh2[4];
+  float sc[8], sh[8];
+  if constexpr (FIN) {
+    __shared__ float fl[FIN_MAXC * 2];
+    float gm[8], bt[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { gm[j] = gamma[c0 + j]; bt[j] = beta[c0 + j]; }
+    fin_stage(fin, C, c0, g, rg, fl);
+    __syncthreads();
+    if (g >= rg) return;
+    float a[8], b[8];
+    fin_sums(fin, C, c0, rg, fl, a, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      const float mu = a[j] / (float)M;
+      const float var = fmaxf(b[j] / (float)M - mu * mu, 0.f);
+      const float is = rsqrtf(var + fin.eps);
+      if (blockIdx.x == 0 && g == 0) {
+        fin.o0[c] = mu;
+        fin.o1[c] = is;
+        if (fin.rmean) {
+          fin.rmean[c] = fin.rmean[c] * fin.momentum + mu * (1.f - fin.momentum);
+          fin.rvar[c] = fin.rvar[c] * fin.momentum + var * ((float)M / (float)max(M - 1, 1)) * (1.f - fin.momentum);
+        }
+      }
+      bn_affine(mu, is, gm[j], bt[j], sc[j], sh[j]);
+    }
+  } else {
+    if (g >= rg) return;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bn_affine(mean[c0 + j], invstd[c0 + j], gamma[c0 + j], beta[c0 + j], sc[j], sh[j]);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    sc2[q] = (bn_f32x2){sc[2 * q], sc[2 * q + 1]};
+    sh2[q] = (bn_f32x2){sh[2 * q], sh[2 * q + 1]};
+  }
+  const uint32_t ybytes = (uint32_t)M * (uint32_t)C * 2u;
+  // blocks walk output rows (n, ho), the row groups its pixels: no per-pixel integer division
+  for (int row = blockIdx.x; row < N * Ho; row += gridDim.x) {
+   const int n = row / Ho, ho = row - n * Ho;
+   for (int wo = g; wo < Wo; wo += rg) {
+    const int64_t px = (int64_t)row * Wo + wo;
+    uint4 v[POOL_KMAX * POOL_KMAX];
+    bool ok[POOL_KMAX * POOL_KMAX];
+#pragma unroll
+    for (int r = 0; r < POOL_KMAX; ++r)
+#pragma unroll
+      for (int s = 0; s < POOL_KMAX; ++s) {
+        const int h = ho * st - pad + r, w = wo * st - pad + s;
+        const bool in = r < k && s < k && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        ok[r * POOL_KMAX + s] = in;
+        v[r * POOL_KMAX + s] = buf_ld(y, ybytes, ((uint32_t)(n * H + h) * (uint32_t)W + (uint32_t)w) * (uint32_t)C + c0, in);
+      }
+    float best[8];
+    uint8_t arg[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; }
+#pragma unroll
+    for (int r = 0; r < POOL_KMAX; ++r)
+#pragma unroll
+      for (int s = 0; s < POOL_KMAX; ++s) {
+        if (!ok[r * POOL_KMAX + s]) continue;
+        const uint4 q = v[r * POOL_KMAX + s];
+        const uint32_t o[4] = {bn_relu2(q.x, sc2[0], sh2[0]), bn_relu2(q.y, sc2[1], sh2[1]), bn_relu2(q.z, sc2[2], sh2[2]),
+                               bn_relu2(q.w, sc2[3], sh2[3])};
+        float f[8];
+        unpack8(make_uint4(o[0], o[1], o[2], o[3]), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (f[j] > best[j]) { best[j] = f[j]; arg[j] = (uint8_t)(r * k + s); }
+      }
+    const size_t oi = (size_t)px * C + c0;
+    *reinterpret_cast<uint4*>(out + oi) = pack8(best);
+    const uint32_t lo = arg[0] | arg[1] << 8 | arg[2] << 16 | (uint32_t)arg[3] << 24;
+    const uint32_t hi = arg[4] | arg[5] << 8 | arg[6] << 16 | (uint32_t)arg[7] << 24;
+    *reinterpret_cast<uint2*>(am + oi) = make_uint2(lo, hi);
+   }
+  }
+}
+
+// Max-pool backward at most 2x2 windows per input pixel (ceil(k / st) <= 2: the ResNet stem's 3x3/2)
+// with every window's dy / argmax loads issued together (range-checked buffer loads), and -- STATS --
+// the backward statistics of the relu BN in front of the pool summed on the way (bn_partial_kernel<1,
+// 2>'s math: d = dx through the relu mask recomputed from y, sums of d and d * xhat), so that BN's
+// backward needs no partial pass over dx and y. Thread = (8-channel chunk, row group), walking input
+// pixels grid-stride; windows in maxpool_bwd_kernel's order, so dx is the same bit for bit.
+// Max-pool backward for at most 2x2 windows per input pixel (ceil(k / st) <= 2: the ResNet stem's
+// 3x3/2): blocks walk input rows (n, h) -- no per-pixel division by runtime sizes -- and a pixel's
+// window loads (dy, argmax) are issued together as range-checked buffer loads, so no load waits
+// behind a branch. Windows in maxpool_bwd_kernel's order: the same dx bit for bit. ResNet-50 stem
+// (128 x 112 x 112 x 64): 109 -> 84-88 us. (Summing the stem BN's backward statistics here as well
+// measured 150-158 us in row mode and 173-273 in slot mode against 87 + the 79-us partial pass:
+// not kept, scripts/debug/pool_probe.py.)
+__global__ __launch_bounds__(NT) void maxpool2_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ am,
+                                                          uint16_t* __restrict__ dx, int N, int H, int W, int C, int k,
+                                                          int st, int pad, int Ho, int Wo) {
+  const int tpr = C / 8, t = threadIdx.x, ch = t % tpr, g = t / tpr, rg = NT / tpr, c0 = ch * 8;
+  if (g >= rg) return;
+  const uint32_t dybytes = (uint32_t)N * Ho * Wo * C * 2u, ambytes = dybytes / 2u;
+  for (int row = blockIdx.x; row < N * H; row += gridDim.x) {
+    const int n = row / H, h = row - n * H;
+    const int ho_lo = max(0, (h + pad - k + st) / st), ho_hi = min(Ho - 1, (h + pad) / st);
+    for (int w = g; w < W; w += rg) {
+      const int wo_lo = max(0, (w + pad - k + st) / st), wo_hi = min(Wo - 1, (w + pad) / st);
+      uint4 G[2][2];
+      uint2 A[2][2];
+      int tap[2][2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int ho = ho_lo + a, wo = wo_lo + b, r = h + pad - ho * st, s = w + pad - wo * st;
+          const bool ok = ho <= ho_hi && wo <= wo_hi && r >= 0 && r < k && s >= 0 && s < k;
+          tap[a][b] = ok ? r * k + s : -1;
+          const uint32_t o = ((uint32_t)(n * Ho + ho) * (uint32_t)Wo + (uint32_t)wo) * (uint32_t)C + (uint32_t)c0;
+          G[a][b] = buf_ld(dy, dybytes, o, ok);
+          // the chunk's 8 argmax bytes (a 16-B load whose upper half is ignored; the range check
+          // zero-fills a last chunk's overhang)
+          const uint4 q = buf_ld(reinterpret_cast<const uint16_t*>(am), ambytes, o / 2u, ok);
+          A[a][b] = make_uint2(q.x, q.y);
+        }
+      float acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if (tap[a][b] < 0) continue;
+          float gv[8];
+          unpack8(G[a][b], gv);
+          const uint8_t* ab = reinterpret_cast<const uint8_t*>(&A[a][b]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (ab[j] == (uint8_t)tap[a][b]) acc[j] += gv[j];
+        }
+      *reinterpret_cast<uint4*>(dx + ((size_t)row * W + w) * C + c0) = pack8(acc);
+    }
+  }
+}
+
 __global__ __launch_bounds__(NT) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ am,
                                                          uint16_t* __restrict__ dx, int N, int H, int W, int C, int k,
                                                          int st, int pad, int Ho, int Wo) {
@@ -795,8 +953,31 @@ void maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* argmax, int N, int H, 
 
 void maxpool_bwd(const uint16_t* dy, const uint8_t* argmax, uint16_t* dx, int N, int H, int W, int C, int k, int st,
                  int pad, int Ho, int Wo, hipStream_t s) {
+  if ((k + st - 1) / st <= 2) {  // every window's loads in flight together
+    const int grid = std::max(1, std::min(8192, N * H));
+    maxpool2_bwd_kernel<<<grid, NT, 0, s>>>(dy, argmax, dx, N, H, W, C, k, st, pad, Ho, Wo);
+    return;
+  }
   const int64_t total = (int64_t)N * H * W * (C / 8);
   maxpool_bwd_kernel<<<(int)((total + NT - 1) / NT), NT, 0, s>>>(dy, argmax, dx, N, H, W, C, k, st, pad, Ho, Wo);
+}
+
+void bn_relu_maxpool(const uint16_t* y, const float* gamma, const float* beta, float* mean, float* invstd,
+                     float* running_mean, float* running_var, float momentum, float eps, const float* partials,
+                     int nrows, uint16_t* out, uint8_t* argmax, int N, int H, int W, int C, int k, int st, int pad,
+                     int Ho, int Wo, hipStream_t s) {
+  if (k > POOL_KMAX || C % 8 || C > 2048) throw std::runtime_error("bn_relu_maxpool: k <= 3, C % 8 == 0, C <= 2048");
+  const int grid = std::max(1, std::min(2048, N * Ho));  // blocks walk output rows
+  if (bn_slots() > 0) {
+    const BnFin f{partials, nrows, eps, momentum, mean, invstd, running_mean, running_var};
+    bn_relu_maxpool_kernel<true><<<grid, NT, 0, s>>>(y, gamma, beta, mean, invstd, out, argmax, N, H, W, C, k, st, pad,
+                                                     Ho, Wo, f);
+    return;
+  }
+  bn_final_kernel<<<(C + 31) / 32, FIN_NT, 0, s>>>(0, partials, nrows, N * H * W, C, eps, momentum, mean, invstd,
+                                               running_mean, running_var);
+  bn_relu_maxpool_kernel<false><<<grid, NT, 0, s>>>(y, gamma, beta, mean, invstd, out, argmax, N, H, W, C, k, st, pad, Ho,
+                                                    Wo, BnFin{});
 }
 
 void avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s) {

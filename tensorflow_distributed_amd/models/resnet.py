@@ -485,6 +485,37 @@ class _MaxPool(torch.autograd.Function):
         return _ops().maxpool2d_bwd(dy.contiguous(), am, xs, k, st, pad), None, None, None
 
 
+class _BNReluMaxPool(torch.autograd.Function):
+    """The stem's relu(bn(y)) -> max pool in one pass (``bn_relu_maxpool``): the BN output, the
+    largest activation of the network, is never written nor read back. Same output and argmax as
+    _BN + _MaxPool bit for bit. The backward is theirs (maxpool2d_bwd, then bn_bwd with the relu mask
+    recomputed from y; folding the statistics into the pool's backward measured no faster,
+    csrc/kernels/norm.hip maxpool2_bwd_kernel)."""
+
+    @staticmethod
+    def forward(ctx, y, part, bn, k, st, pad):
+        o = _ops()
+        out, am, mean, invstd = o.bn_relu_maxpool(y, bn.gamma(), bn.beta(), bn.rmean, bn.rvar, bn.momentum, bn.eps, part,
+                                                  k, st, pad)
+        ctx.bn, ctx.cfg = bn, (list(y.shape), k, st, pad)
+        ctx.save_for_backward(y, mean, invstd, am)
+        ctx.mark_non_differentiable(am)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, mean, invstd, am = ctx.saved_tensors
+        bn = ctx.bn
+        xs, k, st, pad = ctx.cfg
+        o = _ops()
+        dpre = o.maxpool2d_bwd(dout.contiguous(), am, xs, k, st, pad)
+        dy, _ = o.bn_bwd(dpre, y, y, bn.gamma(), mean, invstd, True, False, bn.g_gamma(), bn.g_beta(), bn.beta(), None,
+                         None)
+        bn.model.reducer.mark_ready(bn.name + "/gamma")
+        bn.model.reducer.mark_ready(bn.name + "/beta")
+        return dy, None, None, None, None, None
+
+
 class _AvgPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
@@ -690,6 +721,8 @@ class ResNet:
         # identity-shortcut gradient as (dout, relu bits) added in the joining conv's dgrad epilogue
         # instead of a dres tensor written by the residual BN's backward (GradJoin.arrive(masked=))
         self.masked_join = True
+        # the stem's bn + relu + max pool as one pass (_BNReluMaxPool): its BN output is never written
+        self.fuse_stem_pool = True
         cin = width
         exp = 4 if kind == "bottleneck" else 1
         prev_out_bn = None  # the BN that produced the current block input (None: the stem's maxpool)
@@ -759,8 +792,11 @@ class ResNet:
             bn.fwd_state, bn.bwd_part = None, None
         self.stats.zero()
         x = _ops().pad_channels(x_nhwc_f32, 8)
-        x = self.stem_bn(self.stem(x))
-        x = _MaxPool.apply(x, 3, 2, 1)
+        yp = self.stem(x)
+        if self.fuse_stem_pool and isinstance(yp, tuple):  # (y, statistics partials) from a stats conv
+            x = _BNReluMaxPool.apply(yp[0], yp[1], self.stem_bn, 3, 2, 1)
+        else:
+            x = _MaxPool.apply(self.stem_bn(yp), 3, 2, 1)
         for blk in self.blocks:
             x = self.block_forward(blk, x)
         x = _AvgPool.apply(x)

@@ -305,3 +305,41 @@ def test_gemm256_nt_matches_fp32(cuda, M, N, K):
     C = torch.ops.tfd.gemm_nt(A, Bt).float()
     ref = A.float() @ Bt.float().t()
     torch.testing.assert_close(C, ref.bfloat16().float(), rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("N,H,W,C", [(2, 16, 16, 64), (3, 15, 13, 32), (8, 112, 112, 64)])
+def test_bn_relu_maxpool_equals_bn_then_pool(cuda, bn_mode, N, H, W, C):
+    """The stem's fused relu(bn(y)) -> 3x3/2 max pool (bn_relu_maxpool) against bn_fwd + maxpool2d_fwd
+    from the same conv-epilogue partials: output and argmax bit for bit, the same statistics and running
+    stats (row mode: bit for bit; slot mode: both finalize the same slot sums)."""
+    torch.manual_seed(9)
+    x = rb(torch.randn(N, H, W, 8)).to(cuda, torch.bfloat16)
+    w = rb(torch.randn(3, 3, 8, C) * 0.3).to(cuda, torch.bfloat16)
+    y, part = ops.conv2d_fwd_stats(x, w, 1, 1)
+    g, b = (torch.rand(C) + 0.5).to(cuda), torch.randn(C).to(cuda)
+    rm0, rv0 = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    rm1, rv1 = rm0.clone(), rv0.clone()
+    bo, m0, i0 = ops.bn_fwd(y, g, b, None, True, rm0, rv0, 0.9, 1e-5, part)
+    p0, a0 = ops.maxpool2d_fwd(bo, 3, 2, 1)
+    p1, a1, m1, i1 = ops.bn_relu_maxpool(y, g, b, rm1, rv1, 0.9, 1e-5, part, 3, 2, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(p1, p0) and torch.equal(a1, a0)
+    for u, v in ((m1, m0), (i1, i0), (rm1, rm0), (rv1, rv0)):
+        assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("N,H,W,C,k,st,pad", [(2, 16, 16, 64, 3, 2, 1), (3, 15, 13, 32, 3, 2, 1), (8, 112, 112, 64, 3, 2, 1),
+                                            (2, 9, 11, 16, 2, 2, 0), (2, 10, 10, 8, 3, 3, 1), (2, 8, 8, 16, 3, 1, 1)])
+def test_maxpool_bwd_matches_torch(cuda, N, H, W, C, k, st, pad):
+    """Max-pool backward (the row-walking 2x2-window kernel where ceil(k / stride) <= 2, the generic
+    one else) against torch's max_pool2d backward on the same bf16 input."""
+    torch.manual_seed(11)
+    x = rb(torch.randn(N, H, W, C))
+    y, am = ops.maxpool2d_fwd(x.to(cuda, torch.bfloat16), k, st, pad)
+    xr = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    yr = F.max_pool2d(xr, k, st, pad)
+    assert torch.equal(y.cpu().float().permute(0, 3, 1, 2), yr.detach())
+    dy = rb(torch.randn_like(yr))
+    yr.backward(dy)
+    dx = ops.maxpool2d_bwd(dy.permute(0, 2, 3, 1).contiguous().to(cuda, torch.bfloat16), am, [N, H, W, C], k, st, pad)
+    assert relerr(dx.cpu().permute(0, 3, 1, 2), xr.grad) < 1e-2
