@@ -160,6 +160,16 @@ void IpcComm::all_reduce(const at::Tensor& t, double scale) {
   all_reduce_raw(t.data_ptr(), bf, t.data_ptr(), bf, t.numel(), scale, c10::hip::getCurrentHIPStream().stream());
 }
 
+void IpcComm::all_reduce_into(const at::Tensor& in, const at::Tensor& out, double scale) {
+  for (const at::Tensor* t : {&in, &out}) {
+    TORCH_CHECK(t->is_cuda() && t->is_contiguous(), "IpcComm.all_reduce_into: contiguous GPU tensors");
+    TORCH_CHECK(t->scalar_type() == at::kFloat || t->scalar_type() == at::kBFloat16, "IpcComm: fp32/bf16 only");
+  }
+  TORCH_CHECK(in.numel() == out.numel(), "IpcComm.all_reduce_into: in and out sizes differ");
+  all_reduce_raw(in.data_ptr(), in.scalar_type() == at::kBFloat16, out.data_ptr(), out.scalar_type() == at::kBFloat16,
+                 in.numel(), scale, c10::hip::getCurrentHIPStream().stream());
+}
+
 void IpcComm::reduce_scatter_raw(const void* in, bool in_bf16, void* out, bool out_bf16, int64_t shard, double scale,
                                  hipStream_t s) {
   TORCH_CHECK(opened_ || world_ == 1, "IpcComm: open() the peer handles first");
@@ -234,6 +244,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("open", &IpcComm::open)
       .def("close", &IpcComm::close)
       .def("all_reduce", &IpcComm::all_reduce)
+      .def("all_reduce_into", &IpcComm::all_reduce_into)
       .def("reduce_scatter", &IpcComm::reduce_scatter)
       .def("all_gather", &IpcComm::all_gather)
       .def("error", &IpcComm::error)

@@ -14,6 +14,9 @@ class IpcComm : public torch::CustomClassHolder {
   void open(const at::Tensor& all_handles);  // [world, 128]: open every peer's export
   void close();
   void all_reduce(const at::Tensor& t, double scale);  // in place, current HIP stream
+  // out = scale * sum over ranks of in (fp32 / bf16 each, same numel; the staging keeps in's format):
+  // e.g. fp32 gradients in, the bf16 sums out -- the wire cast fused into the collective
+  void all_reduce_into(const at::Tensor& in, const at::Tensor& out, double scale);
   // in: fp32/bf16 -> fp32 staging -> reduced sum * scale -> out (fp32/bf16); n <= capacity
   void all_reduce_raw(const void* in, bool in_bf16, void* out, bool out_bf16, int64_t n, double scale,
                       hipStream_t s);

@@ -186,7 +186,10 @@ class BucketReducer:
                 self.stream.wait_event(ev)
                 lo, hi = self.buckets[b]
                 c = self.bucket_comm[b]
-                if self.bf16:
+                if self.bf16 and hasattr(c, "all_reduce_into"):
+                    # the IPC one-shot reads the fp32 gradients and writes the bf16 sums: no cast pass
+                    c.all_reduce_into(self.fp.grad[lo:hi], self.gbf[lo:hi], "sum")
+                elif self.bf16:
                     self.gbf[lo:hi].copy_(self.fp.grad[lo:hi])
                     c.all_reduce(self.gbf[lo:hi], "sum")
                 else:

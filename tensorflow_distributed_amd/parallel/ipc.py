@@ -74,3 +74,10 @@ class IpcCollectives:
         if op not in ("sum", "avg", "mean"):
             raise ValueError(f"IpcCollectives: unsupported op {op}")
         self.ipc.all_reduce(t, 1.0 if op == "sum" else 1.0 / self.ipc.world())
+
+    def all_reduce_into(self, src, dst, op: str = "sum") -> None:
+        """dst = the ranks' sum of src (dtypes may differ: fp32 gradients in, the bf16 wire sums out --
+        the cast a bucket otherwise pays as a separate pass before its collective)."""
+        if op not in ("sum", "avg", "mean"):
+            raise ValueError(f"IpcCollectives: unsupported op {op}")
+        self.ipc.all_reduce_into(src, dst, 1.0 if op == "sum" else 1.0 / self.ipc.world())

@@ -27,6 +27,12 @@ def _ar_worker(rank, world, n):
     comm.all_reduce(tb, 0.5)
     torch.cuda.synchronize()
     outs.append(tb.float().cpu())
+    # fp32 in, bf16 out (the ResNet reducer's fused wire cast): the fp32 sum, rounded once
+    src = base * (rank + 1) + 0.25
+    dst = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    comm.all_reduce_into(src, dst, 1.0)
+    torch.cuda.synchronize()
+    outs.append(dst.float().cpu())
     s = torch.cuda.Stream()
     g = torch.cuda.CUDAGraph()
     x = torch.ones(n, device=dev) * (rank + 1)
@@ -55,9 +61,11 @@ def test_ipc_allreduce_multiprocess_one_gpu(cuda, world, n):
         assert torch.equal(outs[0], base * tot)
         ref_bf = sum((base * (r + 1)).to(torch.bfloat16).float() for r in range(world)) * 0.5
         torch.testing.assert_close(outs[1], ref_bf.to(torch.bfloat16).float(), rtol=1e-2, atol=1e-2)
+        ref_into = sum(base * (r + 1) + 0.25 for r in range(world))
+        assert torch.equal(outs[2], ref_into.to(torch.bfloat16).float())
         # three replays of an in-place all-reduce: x -> x * tot each time, starting from rank+1 per rank
         # (first replay sums (1..world), later replays multiply the identical value by world)
-        assert torch.allclose(outs[2], torch.full((n,), float(tot * world ** 2)))
+        assert torch.allclose(outs[3], torch.full((n,), float(tot * world ** 2)))
 
 
 LR_SGD = 0.05
