@@ -18,7 +18,6 @@ from __future__ import annotations
 import argparse
 import os
 import signal
-import socket
 import subprocess
 import sys
 import threading
@@ -29,9 +28,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from .parallel.spawn import free_port as _free_port  # below the ephemeral range (see there)
+
+    return _free_port()
 
 
 class Proc:

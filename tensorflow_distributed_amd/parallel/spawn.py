@@ -26,6 +26,21 @@ SELF_LAUNCH_ENV = "TFD_SELF_LAUNCHED"
 
 
 def free_port() -> int:
+    """A port that binds now, taken BELOW the kernel's ephemeral range (Linux 32768-60999): a port
+    from bind(0) is released and only bound again by the child a moment later, and in between an
+    outgoing connection (another job's Gloo or TCPStore client) may take it as its local port --
+    EADDRINUSE in a launched task. Ports under 32768 are never handed out that way."""
+    import random
+
+    rng = random.SystemRandom()
+    for _ in range(64):
+        port = rng.randrange(20000, 32000)
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]

@@ -1,15 +1,14 @@
 """Helpers to run a function in N gloo processes on 127.0.0.1 (CPU distributed tests)."""
 import os
-import socket
 import traceback
 
 import torch.multiprocessing as mp
 
 
 def free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from tensorflow_distributed_amd.parallel.spawn import free_port as _free_port  # below the ephemeral range
+
+    return _free_port()
 
 
 def _to_plain(x):
