@@ -6,6 +6,7 @@
 #include <torch/library.h>
 
 #include <tuple>
+#include <vector>
 
 #include "../conv_kernels.h"
 
@@ -115,19 +116,29 @@ const uint8_t* acc_bits_of(const c10::optional<at::Tensor>& acc_bits, const c10:
   return acc_bits->data_ptr<uint8_t>();
 }
 
+// acc_sub2: acc is [N, ceil(H/2), ceil(W/2), C], added at the even pixels (AddSrc)
+void check_acc(const at::Tensor& acc, at::IntArrayRef xshape, bool sub2, const char* what) {
+  check_bf16(acc, "acc", 4);
+  if (sub2) {
+    const std::vector<int64_t> s2{xshape[0], (xshape[1] + 1) / 2, (xshape[2] + 1) / 2, xshape[3]};
+    TORCH_CHECK(acc.sizes() == at::IntArrayRef(s2), what, ": a stride-2 acc must be [N, ceil(H/2), ceil(W/2), C]");
+  } else {
+    TORCH_CHECK(acc.sizes() == xshape, what, ": acc shape must equal xshape");
+  }
+}
+
 at::Tensor conv2d_dgrad(const at::Tensor& dy, const at::Tensor& w, at::IntArrayRef xshape, int64_t stride, int64_t pad,
-                        const c10::optional<at::Tensor>& acc, const c10::optional<at::Tensor>& acc_bits) {
+                        const c10::optional<at::Tensor>& acc, const c10::optional<at::Tensor>& acc_bits, bool acc_sub2) {
   check_bf16(dy, "dy", 4);
   check_bf16(w, "w", 4);
   TORCH_CHECK(xshape.size() == 4, "xshape [N,H,W,C]");
   auto x = at::empty(xshape, dy.options());
-  if (acc.has_value()) {  // dx = acc + dgrad
-    check_bf16(*acc, "acc", 4);
-    TORCH_CHECK(acc->sizes() == xshape, "dgrad: acc shape must equal xshape");
-  }
+  TORCH_CHECK(!acc_sub2 || acc.has_value(), "dgrad: acc_sub2 needs acc");
+  if (acc.has_value()) check_acc(*acc, xshape, acc_sub2, "dgrad");  // dx = acc + dgrad
   const ConvShape c = shape_of(x, w, stride, pad);
   TORCH_CHECK(dy.size(1) == c.Ho() && dy.size(2) == c.Wo() && dy.size(3) == c.K, "dgrad: dy shape mismatch");
-  conv_dgrad(c, bp(dy), bp(w), bp(x), cur(), acc.has_value() ? bp(*acc) : nullptr, acc_bits_of(acc_bits, acc, xshape));
+  conv_dgrad(c, bp(dy), bp(w), bp(x), cur(), acc.has_value() ? bp(*acc) : nullptr, acc_bits_of(acc_bits, acc, xshape),
+             acc_sub2);
   return x;
 }
 
@@ -140,16 +151,14 @@ std::tuple<at::Tensor, at::Tensor> conv2d_dgrad_bn(const at::Tensor& dy, const a
                                                    const at::Tensor& gamma, const c10::optional<at::Tensor>& beta,
                                                    const c10::optional<at::Tensor>& mask, bool relu,
                                                    const c10::optional<at::Tensor>& acc_bits,
-                                                   const c10::optional<at::Tensor>& part_out) {
+                                                   const c10::optional<at::Tensor>& part_out, bool acc_sub2) {
   check_bf16(dy, "dy", 4);
   check_bf16(w, "w", 4);
   check_bf16(y, "y", 4);
   TORCH_CHECK(xshape.size() == 4 && y.sizes() == xshape, "dgrad_bn: y must have the conv input's shape");
   auto x = at::empty(xshape, dy.options());
-  if (acc.has_value()) {
-    check_bf16(*acc, "acc", 4);
-    TORCH_CHECK(acc->sizes() == xshape, "dgrad_bn: acc shape must equal xshape");
-  }
+  TORCH_CHECK(!acc_sub2 || acc.has_value(), "dgrad_bn: acc_sub2 needs acc");
+  if (acc.has_value()) check_acc(*acc, xshape, acc_sub2, "dgrad_bn");
   const ConvShape c = shape_of(x, w, stride, pad);
   TORCH_CHECK(dy.size(1) == c.Ho() && dy.size(2) == c.Wo() && dy.size(3) == c.K, "dgrad_bn: dy shape mismatch");
   TORCH_CHECK(conv_dgrad_bn_supported(c), "dgrad_bn: unsupported conv (C % 8, or a strided dgrad with tap-less phases)");
@@ -174,7 +183,7 @@ std::tuple<at::Tensor, at::Tensor> conv2d_dgrad_bn(const at::Tensor& dy, const a
   }
   auto part = part_buffer(part_out, conv_dgrad_bn_rows(c), C, dy.options(), "conv2d_dgrad_bn");
   conv_dgrad_bn(c, bp(dy), bp(w), bp(x), cur(), acc.has_value() ? bp(*acc) : nullptr, b, fp(part),
-                acc_bits_of(acc_bits, acc, xshape));
+                acc_sub2 ? nullptr : acc_bits_of(acc_bits, acc, xshape), acc_sub2);
   return {x, part};
 }
 
@@ -423,12 +432,12 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.def("conv2d_fwd_stats(Tensor x, Tensor w, int stride, int pad, Tensor? mean=None, Tensor? invstd=None, "
         "Tensor? gamma=None, Tensor? beta=None, Tensor? part_out=None) -> (Tensor, Tensor)");
   m.impl("conv2d_fwd_stats", c10::DispatchKey::CUDA, &conv2d_fwd_stats);
-  m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc=None, Tensor? acc_bits=None) "
-        "-> Tensor");
+  m.def("conv2d_dgrad(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc=None, Tensor? acc_bits=None, "
+        "bool acc_sub2=False) -> Tensor");
   m.impl("conv2d_dgrad", c10::DispatchKey::CUDA, &conv2d_dgrad);
   m.def("conv2d_dgrad_bn(Tensor dy, Tensor w, int[] xshape, int stride, int pad, Tensor? acc, Tensor y, Tensor mean, "
         "Tensor invstd, Tensor gamma, Tensor? beta, Tensor? mask, bool relu, Tensor? acc_bits=None, "
-        "Tensor? part_out=None) -> (Tensor, Tensor)");
+        "Tensor? part_out=None, bool acc_sub2=False) -> (Tensor, Tensor)");
   m.impl("conv2d_dgrad_bn", c10::DispatchKey::CUDA, &conv2d_dgrad_bn);
   m.def("conv2d_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad, bool zeroed=False, Tensor? mean=None, "
         "Tensor? invstd=None, Tensor? gamma=None, Tensor? beta=None) -> ()");

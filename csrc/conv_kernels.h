@@ -37,8 +37,10 @@ void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, ui
 // add_bits (stride 1, with add): add is a residual BN's dout and add_bits its forward relu bits
 // ([M][C/8]): the epilogue adds dout masked by the bits -- the dres that BN's backward then need not
 // write
+// add_sub2 (stride 1, with add): add is [N][ceil(H/2)][ceil(W/2)][C], added at the even (h, w)
+// pixels only -- a downsample block's 1x1 stride-2 shortcut dgrad computed on its own grid
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                const uint16_t* add = nullptr, const uint8_t* add_bits = nullptr);
+                const uint16_t* add = nullptr, const uint8_t* add_bits = nullptr, bool add_sub2 = false);
 // dgrad whose epilogue also emits the backward statistics partials of the batch norm whose output
 // was this conv's input (its dout is the dgrad output): part fp32 [conv_dgrad_bn_rows(c)][2][C] of
 // per-row-block sums of d and d * (y - mean) * invstd, d = dout through the BN's relu mask -- what
@@ -53,7 +55,8 @@ struct BnBwdStats {
 bool conv_dgrad_bn_supported(const ConvShape& c);
 int conv_dgrad_bn_rows(const ConvShape& c);
 void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                   const uint16_t* add, const BnBwdStats& b, float* part, const uint8_t* add_bits = nullptr);
+                   const uint16_t* add, const BnBwdStats& b, float* part, const uint8_t* add_bits = nullptr,
+                   bool add_sub2 = false);
 // dw: fp32 [R*S*C][K]; overwritten (zeroed first when split)
 // zeroed: dw is known to be zero already (the model zeroes its flat gradient buffer once per
 // step), so split-K needs no per-layer memset

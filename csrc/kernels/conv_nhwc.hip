@@ -333,13 +333,24 @@ struct StoreBf16Stats {
 // gradient through a residual batch norm's relu, x = that BN's dout and bits = the forward's relu
 // bits ([M][N/8] bytes): the masked dout is exactly the dres bn_bwd would have written (a bf16 value
 // or zero), so the BN backward skips that full-tensor write (ResNet identity shortcuts).
+// sub_w != 0: x lives on the stride-2 grid [N][Ho][Wo][C] of the output's [N][sub_h][sub_w] pixels --
+// a downsample block's 1x1 stride-2 shortcut dgrad, whose other three phases are zero -- and is added
+// at the even (h, w) pixels only (abytes: its size), so those zeros are never written nor read.
 struct AddSrc {
   const uint16_t* x = nullptr;
   const uint8_t* bits = nullptr;
+  uint32_t sub_w = 0, sub_h = 0, sub_wo = 0, sub_ho = 0, abytes = 0;
   __host__ __device__ AddSrc() {}
   __host__ __device__ AddSrc(const uint16_t* p) : x(p) {}  // NOLINT: plain add operand
   __host__ __device__ AddSrc(const uint16_t* p, const uint8_t* b) : x(p), bits(b) {}
 };
+// row of the add operand for output row `row`; clears ok where a stride-2 operand has no value
+__device__ __forceinline__ uint32_t add_row(const AddSrc& a, uint32_t row, bool& ok) {
+  if (!a.sub_w) return row;
+  const uint32_t w = row % a.sub_w, hw = row / a.sub_w, h = hw % a.sub_h, img = hw / a.sub_h;
+  ok = ok && !(w & 1u) && !(h & 1u);
+  return (img * a.sub_ho + (h >> 1)) * a.sub_wo + (w >> 1);
+}
 __device__ __forceinline__ uint4 add_masked(uint4 q, uint32_t bits) {  // bit j keeps element j
   const uint32_t w[4] = {q.x, q.y, q.z, q.w};
   uint32_t o[4];
@@ -412,7 +423,9 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
     for (int c = 0; c < E::CH; ++c) {
       const int m = m0 + g0 + c * E::RG;
       const bool ok = m < M && n < N;
-      q[c] = buf_ld(add.x, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, ok);
+      bool aok = ok;
+      const uint32_t ar = add_row(add, orow[c], aok);
+      q[c] = buf_ld(add.x, add.abytes ? add.abytes : ybytes, ar * (uint32_t)N + (uint32_t)n, aok);
       if (add.bits) qb[c] = ok ? add.bits[(size_t)orow[c] * (N / 8) + n / 8] : 0u;
     }
   }
@@ -883,7 +896,9 @@ __device__ __forceinline__ void g256_epilogue(f32x16 (&acc)[C::TM][C::TN], char*
       orow[c] = rowmap(m);
       const bool ok = m < M && n < N;
       if constexpr (ADD) {
-        q[c] = buf_ld(add.x, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, ok);
+        bool aok = ok;
+        const uint32_t ar = add_row(add, orow[c], aok);
+        q[c] = buf_ld(add.x, add.abytes ? add.abytes : ybytes, ar * (uint32_t)N + (uint32_t)n, aok);
         if (add.bits) qb[c] = ok ? add.bits[(size_t)orow[c] * (N / 8) + n / 8] : 0u;
       }
       if constexpr (BSTAT) {
@@ -1230,12 +1245,25 @@ static int dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t*
   return rows;
 }
 
+static AddSrc make_add(const ConvShape& c, const uint16_t* add, const uint8_t* add_bits, bool add_sub2) {
+  AddSrc a{add, add_bits};
+  if (add_sub2) {  // the operand is on the stride-2 grid of this dgrad's output (see AddSrc)
+    a.sub_w = (uint32_t)c.W;
+    a.sub_h = (uint32_t)c.H;
+    a.sub_wo = (uint32_t)((c.W + 1) / 2);
+    a.sub_ho = (uint32_t)((c.H + 1) / 2);
+    a.abytes = (uint32_t)((int64_t)c.N * a.sub_ho * a.sub_wo * c.C * 2);
+  }
+  return a;
+}
+
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                const uint16_t* add, const uint8_t* add_bits) {
+                const uint16_t* add, const uint8_t* add_bits, bool add_sub2) {
   const int M = c.N * c.H * c.W;
-  if (add_bits && (!add || c.stride != 1 || !TFD_CONV_LDS_EPI))
-    throw std::runtime_error("conv_dgrad: a relu-masked add operand needs a stride-1 dgrad");
-  const AddSrc aa{add, add_bits};
+  if ((add_bits || add_sub2) && (!add || c.stride != 1 || !TFD_CONV_LDS_EPI))
+    throw std::runtime_error("conv_dgrad: a relu-masked or stride-2 add operand needs a stride-1 dgrad");
+  if (add_bits && add_sub2) throw std::runtime_error("conv_dgrad: one add-operand form at a time");
+  const AddSrc aa = make_add(c, add, add_bits, add_sub2);
   if (TFD_CONV_LDS_EPI && TFD_DGRAD_PHASES && c.stride > 1) {
     dgrad_strided(c, dy, w, dx, add, st);
     return;
@@ -1290,11 +1318,12 @@ int conv_dgrad_bn_rows(const ConvShape& c) {
 }
 
 void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
-                   const uint16_t* add, const BnBwdStats& b, float* part, const uint8_t* add_bits) {
+                   const uint16_t* add, const BnBwdStats& b, float* part, const uint8_t* add_bits, bool add_sub2) {
   if (!conv_dgrad_bn_supported(c)) throw std::runtime_error("conv_dgrad_bn: unsupported conv (C % 8, tap-less phases)");
-  if (add_bits && (!add || c.stride != 1))
-    throw std::runtime_error("conv_dgrad_bn: a relu-masked add operand needs a stride-1 dgrad");
-  const AddSrc aa{add, add_bits};
+  if ((add_bits || add_sub2) && (!add || c.stride != 1))
+    throw std::runtime_error("conv_dgrad_bn: a relu-masked or stride-2 add operand needs a stride-1 dgrad");
+  if (add_bits && add_sub2) throw std::runtime_error("conv_dgrad_bn: one add-operand form at a time");
+  const AddSrc aa = make_add(c, add, add_bits, add_sub2);
   const int M = c.N * c.H * c.W, KD = c.R * c.S * c.K;
   auto go = [&](const auto& bs) {
     if (c.stride > 1) {

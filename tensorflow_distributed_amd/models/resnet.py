@@ -209,6 +209,8 @@ class BucketReducer:
 # ----------------------------------------------------------------------------- autograd ops
 # A/B switch: TFD_JOIN_DEFER=0 computes a join's first conv arrival at once (GradJoin.arrive)
 _JOIN_DEFER = os.environ.get("TFD_JOIN_DEFER", "1") != "0"
+# A/B switch: TFD_JOIN_SUB2=0 writes a 1x1 stride-2 shortcut dgrad on the full grid (zeros included)
+_JOIN_SUB2 = os.environ.get("TFD_JOIN_SUB2", "1") != "0"
 
 
 class GradJoin:
@@ -231,6 +233,19 @@ class GradJoin:
 
     def reset(self):
         self.seen, self.acc, self.bits, self.deferred = 0, None, None, None
+        self.sub = None  # full [N, H, W, C] when acc is a stride-2 shortcut dgrad on its own grid
+
+    @staticmethod
+    def _sub2(L) -> bool:
+        """A 1x1 stride-2 unpadded conv: its dgrad is nonzero at the even pixels only."""
+        return _JOIN_SUB2 and L.k == 1 and L.stride == 2 and L.pad == 0
+
+    def _expand(self):
+        """Materialise a parked stride-2 gradient on the full grid (an unusual arrival order)."""
+        if self.sub is not None:
+            full = torch.zeros(self.sub, dtype=self.acc.dtype, device=self.acc.device)
+            full[:, ::2, ::2, :] = self.acc
+            self.acc, self.sub = full, None
 
     @staticmethod
     def _unmask(dout, bits):
@@ -243,9 +258,30 @@ class GradJoin:
         if self.acc is None:
             self.acc = g
             return
+        self._expand()
         if self.bits is not None:  # a parked masked gradient meets a plain one: materialise it
             self.acc, self.bits = self._unmask(self.acc, self.bits), None
         self.acc = self.acc.add_(g)
+
+    def _conv_into_acc(self, dy, L, xs, fid, fuse):
+        """acc <- this conv's dgrad (+ acc): with the BN statistics in its epilogue when ``fuse``; a
+        stride-2 parked acc rides the epilogue only of a stride-1 dgrad."""
+        bits, self.bits = self.bits, None
+        if self.sub is not None and L.stride != 1:
+            self._expand()
+        sub2 = self.sub is not None
+        if fuse:
+            self.acc = _dgrad_bn(dy, L, xs, self.acc, self.bn, fid, bits, sub2)
+        elif self.acc is not None:
+            self.acc = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad, self.acc, bits, sub2)
+        elif self._sub2(L):  # nothing to add yet: the shortcut dgrad on its own grid, parked
+            N, H, W, C = xs
+            self.acc = _ops().conv2d_dgrad(dy, L.w(), [N, (H + 1) // 2, (W + 1) // 2, C], 1, 0)
+            self.sub = list(xs)
+            return
+        else:
+            self.acc = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad)
+        self.sub = None
 
     def arrive(self, g=None, conv=None, masked=None):
         """``g``: a finished gradient; ``conv=(dy, layer, xshape, fwd_id)``: compute it as a dgrad;
@@ -274,24 +310,18 @@ class GradJoin:
                 self._add(self._unmask(*masked))
         elif conv is not None:
             dy, L, xs, fid = conv
-            bits, self.bits = self.bits, None
-            if fuse_now and _bn_stats_fusable(L, self.bn, fid):  # the sum is the BN's whole dout
-                self.acc = _dgrad_bn(dy, L, xs, self.acc, self.bn, fid, bits)
-            elif self.acc is not None:
-                self.acc = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad, self.acc, bits)
-            else:
-                self.acc = _ops().conv2d_dgrad(dy, L.w(), xs, L.stride, L.pad)
+            # the sum is the BN's whole dout when this is the last arrival
+            self._conv_into_acc(dy, L, xs, fid, fuse_now and _bn_stats_fusable(L, self.bn, fid))
         elif g is not None:
             self._add(g)
         if not last:
             return None
         if self.deferred is not None:  # the deferred conv last: its epilogue sums the statistics
             dy, L, xs, fid = self.deferred
-            bits, self.bits = self.bits, None
-            out = _dgrad_bn(dy, L, xs, self.acc, self.bn, fid, bits)
-        else:
-            out = self.acc if self.bits is None else self._unmask(self.acc, self.bits)
-        self.acc, self.bits, self.deferred = None, None, None
+            self._conv_into_acc(dy, L, xs, fid, True)
+        self._expand()
+        out = self.acc if self.bits is None else self._unmask(self.acc, self.bits)
+        self.acc, self.bits, self.deferred, self.sub = None, None, None, None
         return out
 
 
@@ -315,14 +345,14 @@ def _bn_stats_fusable(L, bn, fid) -> bool:
     return (not relu) or mask is not None or (not has_res and L.model.mask_from_y)
 
 
-def _dgrad_bn(dy, L, xs, acc, bn, fid, acc_bits=None):
+def _dgrad_bn(dy, L, xs, acc, bn, fid, acc_bits=None, acc_sub2=False):
     """dX of conv ``L`` (+ ``acc``) with BN ``bn``'s backward partials summed in the same epilogue;
     the partials wait on the BN layer for its backward (which then skips its own partial pass),
     tagged with the forward they belong to."""
     y, mean, invstd, mask, relu, has_res, _ = bn.fwd_state
     beta = bn.beta() if (relu and mask is None) else None
     g, part = _ops().conv2d_dgrad_bn(dy, L.w(), xs, L.stride, L.pad, acc, y, mean, invstd, bn.gamma(), beta, mask,
-                                     relu, acc_bits, part_out=bn.acc_b)
+                                     relu, acc_bits, part_out=bn.acc_b, acc_sub2=acc_sub2)
     bn.bwd_part = (part, fid)
     return g
 

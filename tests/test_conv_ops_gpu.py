@@ -343,3 +343,25 @@ def test_maxpool_bwd_matches_torch(cuda, N, H, W, C, k, st, pad):
     yr.backward(dy)
     dx = ops.maxpool2d_bwd(dy.permute(0, 2, 3, 1).contiguous().to(cuda, torch.bfloat16), am, [N, H, W, C], k, st, pad)
     assert relerr(dx.cpu().permute(0, 3, 1, 2), xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,C,K", [(2, 14, 14, 64, 32), (3, 9, 7, 32, 16), (16, 28, 28, 256, 128)])
+def test_dgrad_with_stride2_add_operand(cuda, N, H, W, C, K):
+    """conv2d_dgrad / conv2d_dgrad_bn with acc_sub2: a [N, ceil(H/2), ceil(W/2), C] operand added at the
+    even pixels equals adding its zero-filled full-grid form (the 1x1 stride-2 shortcut dgrad)."""
+    torch.manual_seed(12)
+    dy = rb(torch.randn(N, H, W, K)).to(cuda, torch.bfloat16)
+    w = rb(torch.randn(1, 1, C, K) * 0.2).to(cuda, torch.bfloat16)
+    comp = rb(torch.randn(N, (H + 1) // 2, (W + 1) // 2, C)).to(cuda, torch.bfloat16)
+    full = torch.zeros(N, H, W, C, device=cuda, dtype=torch.bfloat16)
+    full[:, ::2, ::2, :] = comp
+    ref = ops.conv2d_dgrad(dy, w, [N, H, W, C], 1, 0, full)
+    got = ops.conv2d_dgrad(dy, w, [N, H, W, C], 1, 0, comp, None, True)
+    assert torch.equal(got, ref)
+    y = rb(torch.randn(N, H, W, C)).to(cuda, torch.bfloat16)
+    mean, invstd = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    g = torch.ones(C, device=cuda)
+    r0, p0 = ops.conv2d_dgrad_bn(dy, w, [N, H, W, C], 1, 0, full, y, mean, invstd, g, None, None, False)
+    r1, p1 = ops.conv2d_dgrad_bn(dy, w, [N, H, W, C], 1, 0, comp, y, mean, invstd, g, None, None, False, None, None, True)
+    assert torch.equal(r1, r0)
+    torch.testing.assert_close(p1.sum(0), p0.sum(0), rtol=1e-4, atol=1e-3)

@@ -351,9 +351,9 @@ def test_bn_bwd_stats_in_dgrad_epilogue(cuda, row_mode, depth, monkeypatch):
     kinds = []
     orig = R._dgrad_bn
 
-    def spy(dy, L, xs, acc, bn, fid, acc_bits=None):
+    def spy(dy, L, xs, acc, bn, fid, acc_bits=None, acc_sub2=False):
         kinds.append(("bits" if bn.fwd_state[3] is not None else "from_y", acc is not None))
-        return orig(dy, L, xs, acc, bn, fid, acc_bits)
+        return orig(dy, L, xs, acc, bn, fid, acc_bits, acc_sub2)
 
     monkeypatch.setattr(R, "_dgrad_bn", spy)
     torch.manual_seed(depth)
@@ -513,3 +513,40 @@ def test_bn_slot_mode_matches_row_mode(cuda, depth):
     g0, g1 = out[0][1], out[1][1]
     assert torch.isfinite(g1).all()
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("depth", [18, 50])
+def test_stride2_shortcut_gradient_on_its_own_grid(cuda, row_mode, depth, monkeypatch):
+    """A downsample block's 1x1 stride-2 shortcut dgrad computed on its own (stride-2) grid and added
+    at the even pixels inside the joining conv's dgrad epilogue (acc_sub2) against the full-grid
+    dgrad with its zero phases written (TFD_JOIN_SUB2=0): the same loss, and gradients equal up to the
+    fp32 order of the shortcut GEMM (bf16 roundings amplified through train-mode BN); the stride-2 form
+    must actually be used."""
+    from tensorflow_distributed_amd.models import resnet as R
+
+    used = []
+    orig = R._dgrad_bn
+
+    def spy(dy, L, xs, acc, bn, fid, acc_bits=None, acc_sub2=False):
+        used.append(acc_sub2)
+        return orig(dy, L, xs, acc, bn, fid, acc_bits, acc_sub2)
+
+    monkeypatch.setattr(R, "_dgrad_bn", spy)
+    torch.manual_seed(depth + 3)
+    x = torch.randn(4, 64, 64, 3, device=cuda)
+    lab = torch.randint(0, 16, (4,), dtype=torch.int32, device=cuda)
+    out = []
+    for sub in (False, True):
+        monkeypatch.setattr(R, "_JOIN_SUB2", sub)
+        m = R.ResNet(depth, num_classes=16, device=cuda, seed=4, width=16, zero_init_residual=False)
+        m.fp.grad.zero_()
+        loss, _ = m.loss(x, lab)
+        loss.backward()
+        torch.cuda.synchronize()
+        out.append((loss.item(), m.fp.grad.clone()))
+    if depth == 50:  # bottleneck joins end in a stride-1 1x1 dgrad; a basic block's conv1 is strided itself
+        assert any(used), "no join took the stride-2 shortcut operand"
+    assert out[0][0] == out[1][0]
+    g0, g1 = out[0][1], out[1][1]
+    assert torch.isfinite(g1).all()
+    assert ((g1 - g0).norm() / g0.norm()).item() < 3e-2
