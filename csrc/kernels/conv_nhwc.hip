@@ -1178,7 +1178,7 @@ static void conv_dgrad_impl(const ConvShape& c, const uint16_t* dy, const uint16
 #define TFD_DGRAD_PHASES 1
 #endif
 template <int BM, int BN, bool ADD, class BS = NoBnB>
-static void launch_phase(const DgradPhaseA& la, const DgradPhaseB& lb, uint16_t* dx, const uint16_t* add,
+static void launch_phase(const DgradPhaseA& la, const DgradPhaseB& lb, uint16_t* dx, const AddSrc& add,
                          hipStream_t st, float* part = nullptr, const BS& bs = BS{}) {
   constexpr int sm = GemmSmem<BM, BN, CBK, DgradPhaseA, DgradPhaseB>::BYTES > LdsEpi<BM, BN, 2, 2>::BYTES
                          ? GemmSmem<BM, BN, CBK, DgradPhaseA, DgradPhaseB>::BYTES : LdsEpi<BM, BN, 2, 2>::BYTES;
@@ -1194,7 +1194,7 @@ static void launch_phase(const DgradPhaseA& la, const DgradPhaseB& lb, uint16_t*
 // BS != NoBnB: every phase also emits its BN-backward partial rows at part + (rows so far) * 2 * C
 // (callers ensure no phase is tap-less: those pixels would carry no partials). Returns the rows.
 template <class BS = NoBnB>
-static int dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, const uint16_t* add,
+static int dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, const AddSrc& add,
                          hipStream_t st, float* part = nullptr, const BS& bs = BS{}) {
   const int s = c.stride;
   bool empty = false;
@@ -1221,13 +1221,13 @@ static int dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t*
       if (use_g256(g.M, c.C)) {
         rows += (g.M + 255) / 256;
         const uint32_t xbytes = (uint32_t)((int64_t)c.N * c.H * c.W * c.C * 2);
-        if (add) g256_launch_bf16<true, true, true, false>(la, lb, dx, add, g.M, c.C, g.KD, pp, st, PhaseRows{g}, xbytes, bs);
+        if (add.x) g256_launch_bf16<true, true, true, false>(la, lb, dx, add, g.M, c.C, g.KD, pp, st, PhaseRows{g}, xbytes, bs);
         else g256_launch_bf16<true, true, false, false>(la, lb, dx, add, g.M, c.C, g.KD, pp, st, PhaseRows{g}, xbytes, bs);
         continue;
       }
       const OutTile ot = out_tile(g.M, c.C);
       rows += ot == OT64 ? (g.M + 63) / 64 : (g.M + 127) / 128;
-      if (add) {
+      if (add.x) {
         if (ot == OT128) launch_phase<128, 128, true>(la, lb, dx, add, st, pp, bs);
         else if (ot == OT128x64) launch_phase<128, 64, true>(la, lb, dx, add, st, pp, bs);
         else launch_phase<64, 64, true>(la, lb, dx, add, st, pp, bs);
@@ -1239,8 +1239,10 @@ static int dgrad_strided(const ConvShape& c, const uint16_t* dy, const uint16_t*
     }
   if (empty) {
     const int64_t total = (int64_t)c.N * c.H * c.W * (c.C / 8);
-    dgrad_empty_phase_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(dx, add, c.N, c.H, c.W, c.C, s, c.pad, c.R,
-                                                                         c.S);
+    // tap-less phases: the add operand there, or zeros (a stride-2 operand must sit on tap phases)
+    if (add.sub_w && (c.pad % s) != 0) throw std::runtime_error("dgrad: stride-2 add operand over a tap-less phase");
+    dgrad_empty_phase_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(dx, add.sub_w ? nullptr : add.x, c.N, c.H, c.W,
+                                                                         c.C, s, c.pad, c.R, c.S);
   }
   return rows;
 }
@@ -1260,12 +1262,13 @@ static AddSrc make_add(const ConvShape& c, const uint16_t* add, const uint8_t* a
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                 const uint16_t* add, const uint8_t* add_bits, bool add_sub2) {
   const int M = c.N * c.H * c.W;
-  if ((add_bits || add_sub2) && (!add || c.stride != 1 || !TFD_CONV_LDS_EPI))
-    throw std::runtime_error("conv_dgrad: a relu-masked or stride-2 add operand needs a stride-1 dgrad");
+  if (add_bits && (!add || c.stride != 1 || !TFD_CONV_LDS_EPI))
+    throw std::runtime_error("conv_dgrad: a relu-masked add operand needs a stride-1 dgrad");
+  if (add_sub2 && (!add || !TFD_CONV_LDS_EPI)) throw std::runtime_error("conv_dgrad: stride-2 add operand without add");
   if (add_bits && add_sub2) throw std::runtime_error("conv_dgrad: one add-operand form at a time");
   const AddSrc aa = make_add(c, add, add_bits, add_sub2);
   if (TFD_CONV_LDS_EPI && TFD_DGRAD_PHASES && c.stride > 1) {
-    dgrad_strided(c, dy, w, dx, add, st);
+    dgrad_strided(c, dy, w, dx, aa, st);
     return;
   }
   if (use_g256(M, c.C)) {  // A = dY gather, B = W as [C][(r,s,k)]: both KC
@@ -1320,14 +1323,15 @@ int conv_dgrad_bn_rows(const ConvShape& c) {
 void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                    const uint16_t* add, const BnBwdStats& b, float* part, const uint8_t* add_bits, bool add_sub2) {
   if (!conv_dgrad_bn_supported(c)) throw std::runtime_error("conv_dgrad_bn: unsupported conv (C % 8, tap-less phases)");
-  if ((add_bits || add_sub2) && (!add || c.stride != 1))
-    throw std::runtime_error("conv_dgrad_bn: a relu-masked or stride-2 add operand needs a stride-1 dgrad");
+  if (add_bits && (!add || c.stride != 1))
+    throw std::runtime_error("conv_dgrad_bn: a relu-masked add operand needs a stride-1 dgrad");
+  if (add_sub2 && !add) throw std::runtime_error("conv_dgrad_bn: stride-2 add operand without add");
   if (add_bits && add_sub2) throw std::runtime_error("conv_dgrad_bn: one add-operand form at a time");
   const AddSrc aa = make_add(c, add, add_bits, add_sub2);
   const int M = c.N * c.H * c.W, KD = c.R * c.S * c.K;
   auto go = [&](const auto& bs) {
     if (c.stride > 1) {
-      dgrad_strided(c, dy, w, dx, add, st, part, bs);
+      dgrad_strided(c, dy, w, dx, aa, st, part, bs);
     } else if (use_g256(M, c.C)) {
       auto g2 = [&](const auto& la, const auto& lb) {
         if (add) g256_launch_bf16<true, true, true, false>(la, lb, dx, aa, M, c.C, KD, part, st, RowId{}, 0u, bs);

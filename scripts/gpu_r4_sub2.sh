@@ -11,7 +11,7 @@ grep -E "passed|failed" gpurun_out/r4_sub2_tests.log
 for i in 1 2 3; do
   line="run $i"
   for v in 0 1; do
-    r=$(TFD_JOIN_SUB2=$v timeout -k 10 240 python bench_resnet.py --depth 50 --batch_size 128 --steps 20 --warmup 5 2>/dev/null | grep -o '"ms_per_step": [0-9.]*') || { echo "bench sub2=$v failed"; exit 1; }
+    r=$(TFD_JOIN_SUB2=$v timeout -k 10 240 python bench_resnet.py --depth ${DEPTH:-50} --batch_size 128 --steps 20 --warmup 5 2>/dev/null | grep -o '"ms_per_step": [0-9.]*') || { echo "bench sub2=$v failed"; exit 1; }
     line="$line | sub2_$v $r"
   done
   echo "$line" | tee -a gpurun_out/r4_sub2_ab.log

@@ -265,10 +265,9 @@ class GradJoin:
 
     def _conv_into_acc(self, dy, L, xs, fid, fuse):
         """acc <- this conv's dgrad (+ acc): with the BN statistics in its epilogue when ``fuse``; a
-        stride-2 parked acc rides the epilogue only of a stride-1 dgrad."""
+        stride-2 parked acc rides the epilogue (every phase of a strided dgrad maps its rows to the
+        full grid, so the odd pixels simply get no add)."""
         bits, self.bits = self.bits, None
-        if self.sub is not None and L.stride != 1:
-            self._expand()
         sub2 = self.sub is not None
         if fuse:
             self.acc = _dgrad_bn(dy, L, xs, self.acc, self.bn, fid, bits, sub2)

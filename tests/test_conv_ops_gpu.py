@@ -365,3 +365,9 @@ def test_dgrad_with_stride2_add_operand(cuda, N, H, W, C, K):
     r1, p1 = ops.conv2d_dgrad_bn(dy, w, [N, H, W, C], 1, 0, comp, y, mean, invstd, g, None, None, False, None, None, True)
     assert torch.equal(r1, r0)
     torch.testing.assert_close(p1.sum(0), p0.sum(0), rtol=1e-4, atol=1e-3)
+    # a strided 3x3 consumer (phase GEMMs): the odd pixels get no add
+    w3 = rb(torch.randn(3, 3, C, K) * 0.1).to(cuda, torch.bfloat16)
+    dy2 = rb(torch.randn(N, (H + 1) // 2, (W + 1) // 2, K)).to(cuda, torch.bfloat16)
+    ref2 = ops.conv2d_dgrad(dy2, w3, [N, H, W, C], 2, 1, full)
+    got2 = ops.conv2d_dgrad(dy2, w3, [N, H, W, C], 2, 1, comp, None, True)
+    assert torch.equal(got2, ref2)
