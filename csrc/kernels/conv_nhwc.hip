@@ -1373,6 +1373,9 @@ WgTile wgrad_tile(const ConvShape& c) {
 #ifndef TFD_WGRAD_MINPX  // fewest pixels (K of the weight-gradient GEMM) per split
 #define TFD_WGRAD_MINPX 2048
 #endif
+#ifndef TFD_WGRAD_BLOCKS_SMALL  // the same for 64x64 tiles (short-MT 1x1 weight gradients)
+#define TFD_WGRAD_BLOCKS_SMALL 512
+#endif
 #ifndef TFD_WGRAD_BLOCKS  // (tile x split) blocks the split count aims for
 #define TFD_WGRAD_BLOCKS 512
 #endif
@@ -1396,7 +1399,8 @@ int conv_wgrad_splits(const ConvShape& c, bool folded) {
   const WgTile t = wgrad_tile(c);
   const int bm = t == WG64x64 ? 64 : 128, bn = t == WG128x128 ? 128 : 64;
   const long tiles = (long)((MT + bm - 1) / bm) * ((c.K + bn - 1) / bn);
-  int s = (int)std::max<long>(1, TFD_WGRAD_BLOCKS / std::max<long>(1, tiles));
+  const long target = t == WG64x64 ? TFD_WGRAD_BLOCKS_SMALL : TFD_WGRAD_BLOCKS;
+  int s = (int)std::max<long>(1, target / std::max<long>(1, tiles));
   s = std::min(s, std::max(1, P / TFD_WGRAD_MINPX));
   return s;
 }
