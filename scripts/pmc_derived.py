@@ -35,7 +35,7 @@ def parse(path):
             continue
         if cols is None:
             continue
-        name = parts[0]
+        name = line[:40].strip().replace("void ", "")  # fixed-width name column (templates hold spaces)
         nums = parts[-(len(cols) + 1):]
         try:
             d = float(nums[0])
