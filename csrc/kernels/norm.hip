@@ -75,7 +75,10 @@ __device__ __forceinline__ void apply_mask_bits(uint32_t bits, float (&d)[8]) {
 // issued before the first use, through buffer descriptors whose hardware range check zero-fills the
 // rows past the block's chunk (no exec-masked branch around a load, so the loads of a batch are all
 // in flight together). With one row per iteration these kernels waited one memory latency per row.
-constexpr int RU = 4;
+#ifndef TFD_BN_RU  // rows per batch of the BN passes (all their loads issued before the first use)
+#define TFD_BN_RU 4
+#endif
+constexpr int RU = TFD_BN_RU;
 __device__ __forceinline__ uint4 row_ld(const uint16_t* base, uint32_t nbytes, int r, int r1, int C, int c0) {
   return buf_ld(base, nbytes, (uint32_t)r * (uint32_t)C + (uint32_t)c0, r < r1);
 }
