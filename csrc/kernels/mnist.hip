@@ -34,10 +34,7 @@
 constexpr int GEMM_RS = 2;       // register stages of the LDS-staged GEMM core (csrc/gemm.h)
 constexpr int FDX_BK_ = 128;     // fc1 dX K-tile
 constexpr int FDW_BK_ = 64;      // fc1 dW K-tile
-#ifndef TFD_ADAM_U
-#define TFD_ADAM_U 2
-#endif
-constexpr int ADAM_U = TFD_ADAM_U;        // fc-region Adam: strides per lane with all loads issued up front
+constexpr int ADAM_U = 2;        // fc-region Adam: strides per lane with all loads issued up front
 constexpr int FC1_BK_ = 32;      // one-shot fc1: 14 K-tiles of 32 (140 KiB LDS), 0.6 us/step faster than 7 of 64
 
 namespace tfd {
@@ -1357,10 +1354,7 @@ constexpr int MAD_C1F4 = (int)(OFF_WC2 / 4);   // 208
 constexpr int MAD_C2END = (int)(OFF_WD1 / 4);  // 13024
 constexpr int MAD_C1BLK = MAD_C1F4 / 16;       // 13
 constexpr int MAD_C2BLK = (MAD_C2END - MAD_C1F4 + 63) / 64;  // 201
-#ifndef TFD_MAD_FC_BLOCKS
-#define TFD_MAD_FC_BLOCKS 1024
-#endif
-constexpr int MAD_FC_BLOCKS = TFD_MAD_FC_BLOCKS;  // grid-stride blocks of the fc-region Adam
+constexpr int MAD_FC_BLOCKS = 1024;  // grid-stride blocks of the fc-region Adam
 constexpr int MAD_CONV = MAD_C1BLK + MAD_C2BLK;
 static_assert(MAD_C1F4 % 16 == 0, "conv1 region: whole blocks");
 constexpr int MAD_SL = 16;  // slab loads in flight per thread
