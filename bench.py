@@ -32,6 +32,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from tensorflow_distributed_amd.parallel.schedule import MNIST_SCHEDULES as SCH_MNIST_SCHEDULES  # noqa: E402
+
 METRIC = "images/sec (whole node) MNIST CNN DP at 1/2/4/8 MI355X; step-time scaling"  # BASELINE.json
 BASELINE_IMG_PER_S = 52.1  # 120 global steps x 256 images / 590 s (performance:6)
 DATA_DESC = {
@@ -41,15 +43,8 @@ DATA_DESC = {
     "random": "synthetic (device-resident MNIST-shaped 55000x784 uniform noise, random labels; random N(0,1) "
               "init; the model collapses to the label prior)",
 }
-# DP schedules of the bf16 step (N > 1 or --force_dp). "sfb": fc-region gradients by sufficient-
-# factor broadcasting (all-gather the fc factors, 1.33 MB/rank, and form the summed gradient
-# locally); "+zero": ZeRO-1 sharding of the fc1 weight on top; "allreduce": the bucketed bf16
-# gradient all-reduce (6.4 MB fc bucket + IPC one-shot conv bucket).
-SCHEDULES = {
-    "sfb+zero": {"fc_sfb": 1, "zero": 1},
-    "sfb": {"fc_sfb": 1, "zero": 0},
-    "allreduce": {"fc_sfb": 0, "zero": 0},
-}
+# DP schedules of the bf16 step (N > 1 or --force_dp): parallel/schedule.MNIST_SCHEDULES
+SCHEDULES = SCH_MNIST_SCHEDULES
 
 
 def _args(argv):
@@ -79,6 +74,8 @@ def _args(argv):
                     "schedule together with --fc_sfb; -1 = from --schedule)")
     ap.add_argument("--fc_sfb", type=int, default=-1, help="override: 1/0 = sufficient-factor fc gradients on/off "
                     "(-1 = from --schedule)")
+    ap.add_argument("--merge_reduce", type=int, default=-1, help="override with --fc_sfb 1: 1/0 = conv slab reduce "
+                    "inside the SFB GEMM launch on/off (-1 = from --schedule; with --fc_sfb/--zero alone: 1)")
     ap.add_argument("--min_warmup_ms", type=float, default=300.0, help="after --warmup steps, keep replaying "
                     "untimed steps until this much warm-up time has passed (GPU clock ramp; reported in the JSON)")
     ap.add_argument("--graph_steps", type=int, default=20, help="training steps captured per hipGraph "
@@ -119,12 +116,14 @@ def _candidates(a, dp: bool):
         return [None], "single"
     if a.dtype == "fp32":  # fp32 DP all-reduces the whole fp32 buffer (no SFB / ZeRO variants)
         return ["allreduce"], "fp32"
-    if a.fc_sfb >= 0 or a.zero >= 0:  # explicit switches fix the schedule
+    if a.fc_sfb >= 0 or a.zero >= 0 or a.merge_reduce >= 0:  # explicit switches fix the schedule
         sfb = a.fc_sfb != 0
         zero = a.zero == 1
         name = ("sfb+zero" if zero else "sfb") if sfb else ("allreduce" if not zero else None)
         if name is None:
             raise SystemExit("error: --zero 1 needs --fc_sfb 1 (the ZeRO-1 path of this bench rides the SFB step)")
+        if sfb and a.merge_reduce != 0:
+            name += "+mr"
         return [name], "flag"
     if a.schedule != "auto":
         return [a.schedule], "flag"
@@ -148,7 +147,7 @@ class _Job:
         self.a, self.ctx = a, ctx
         dev, rank, world = ctx.device, ctx.rank, ctx.world
         self.sched = sched
-        cfg = SCHEDULES[sched] if sched else {"fc_sfb": 0, "zero": 0}
+        cfg = SCHEDULES[sched] if sched else {"fc_sfb": 0, "zero": 0, "merge_reduce": 0}
         self.zero = bool(cfg["zero"]) and a.dtype == "bf16"
         eng = torch.classes.tfd.MnistEngine(a.batch_size, dev.index, 0.75, a.seed, rank)
         eng.set_adam(a.lr, 0.9, 0.999, 1e-8)
@@ -163,6 +162,7 @@ class _Job:
                                 sfb=bool(cfg["fc_sfb"]) and a.dtype == "bf16", zero=self.zero)
         if self.zero:
             eng.set_zero(True)
+        eng.set_sfb_merge_reduce(bool(cfg["merge_reduce"]))
         self.eng = eng
         self.stream = s = torch.cuda.Stream(dev)
         with torch.cuda.stream(s):

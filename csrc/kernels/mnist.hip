@@ -894,26 +894,6 @@ __device__ __forceinline__ int xcd_grouped_tile(int b, int first, int n) {
   return x * (n >> 3) + ((b - first_x) >> 3);
 }
 
-// [output-layer blocks | fc1 dW (+ bias row) tiles over K = W*B]
-__global__ __launch_bounds__(256) void fc_grad_sfb(MnistStepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  int id = blockIdx.x;
-  if (id < OUTS_BLOCKS) { out_grad_sfb_block(a, id, (float*)smem_raw); return; }
-  // tile rows: all FDW_GY, or (ZeRO shard) [by_lo, by_hi] plus the bias row's tile
-  const bool part = a.sfb_by_hi >= a.sfb_by_lo;
-  const int nby = part ? (a.sfb_by_hi - a.sfb_by_lo + 1) + (a.sfb_by_hi < FDW_GY - 1 ? 1 : 0) : FDW_GY;
-  static_assert(FDW_GX % 8 == 0, "XCD grouping deals whole residue classes");
-  id = xcd_grouped_tile(id, OUTS_BLOCKS, FDW_GX * nby);
-  if (part) {
-    int by = id / FDW_GX + a.sfb_by_lo;
-    if (by > a.sfb_by_hi) by = FDW_GY - 1;  // the bias row (3136) is updated by every rank
-    id = by * FDW_GX + id % FDW_GX;
-  }
-  const int WB = a.sfb_world * a.B;
-  OnesRowBuf la{a.sfb_p2, WB, (uint32_t)((int64_t)WB * FEAT * 2)};
-  RankRowsMC lb{a.sfb_dr, HID, HID, WB, a.B, a.sfb_rs, (uint32_t)((int64_t)a.sfb_world * a.sfb_rs * 2)};
-  fc1_dw_tile(a, la, lb, (id / FDW_GX) * FDW_BM, (id % FDW_GX) * FDW_BN, WB, (bf16*)smem_raw);
-}
 
 // ---------------- K13 (LDS-staged): conv2 dgrad + conv1 relu/pool-mask epilogue ----------------
 // Block = (image b, half h: input rows ih in [7h, 7h + 7)), 512 threads, 140.5 KiB LDS. dz2 rows oh
@@ -1321,13 +1301,12 @@ __global__ __launch_bounds__(256) void gather_next_kernel(MnistStepArgs a) { gat
 // gb > 0: the first gb blocks gather the next step's batch (step number from MnistStepArgs::t_out,
 // written by this step's head kernel, so nothing here reads the step that block gb bumps) -- one
 // launch instead of gather_next_kernel + reduce_conv_grads on the DP path
-__global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a, int gb) {
-  __shared__ float red[256];
-  if ((int)blockIdx.x < gb) {
-    gather_next(a, *a.t_out, blockIdx.x);
+__device__ __forceinline__ void conv_reduce_block(const MnistStepArgs& a, int blk, int gb, float* red) {
+  if (blk < gb) {
+    gather_next(a, *a.t_out, blk);
     return;
   }
-  const int id = blockIdx.x - gb;
+  const int id = blk - gb;
   if (id < RED2_BLOCKS)
     reduce_chunk<64>(a.wg2_slab, a.wg2_splits, 801 * 64, 801 * 64, id * 64, a.grad + OFF_WC2,
                      a.gbf_b ? a.gbf_b + OFF_WC2 : nullptr, red);
@@ -1335,6 +1314,34 @@ __global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a, int gb
     reduce_chunk<16>(a.wg1_slab, 2 * a.B, 832, 832, (id - RED2_BLOCKS) * 16, a.grad + OFF_WC1,
                      a.gbf_b ? a.gbf_b + OFF_WC1 : nullptr, red);
   if (id == 0 && threadIdx.x == 0 && a.step_bump) *a.step_bump += 1;  // see MnistStepArgs::step_bump
+}
+__global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a, int gb) {
+  __shared__ float red[256];
+  conv_reduce_block(a, blockIdx.x, gb, red);
+}
+
+// [nlead: next-batch gather + conv slab-reduce blocks (conv_reduce_block) | output-layer blocks |
+//  fc1 dW (+ bias row) tiles over K = W*B]. nlead > 0 is the merged DP tail: the slab reduce (a
+// latency-bound 5 us launch of its own) runs beside the SFB GEMM's blocks instead of before them.
+__global__ __launch_bounds__(256) void fc_grad_sfb(MnistStepArgs a, int gb, int nlead) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  if ((int)blockIdx.x < nlead) { conv_reduce_block(a, blockIdx.x, gb, (float*)smem_raw); return; }
+  int id = (int)blockIdx.x - nlead;
+  if (id < OUTS_BLOCKS) { out_grad_sfb_block(a, id, (float*)smem_raw); return; }
+  // tile rows: all FDW_GY, or (ZeRO shard) [by_lo, by_hi] plus the bias row's tile
+  const bool part = a.sfb_by_hi >= a.sfb_by_lo;
+  const int nby = part ? (a.sfb_by_hi - a.sfb_by_lo + 1) + (a.sfb_by_hi < FDW_GY - 1 ? 1 : 0) : FDW_GY;
+  static_assert(FDW_GX % 8 == 0, "XCD grouping deals whole residue classes");
+  id = xcd_grouped_tile((int)blockIdx.x, nlead + OUTS_BLOCKS, FDW_GX * nby);
+  if (part) {
+    int by = id / FDW_GX + a.sfb_by_lo;
+    if (by > a.sfb_by_hi) by = FDW_GY - 1;  // the bias row (3136) is updated by every rank
+    id = by * FDW_GX + id % FDW_GX;
+  }
+  const int WB = a.sfb_world * a.B;
+  OnesRowBuf la{a.sfb_p2, WB, (uint32_t)((int64_t)WB * FEAT * 2)};
+  RankRowsMC lb{a.sfb_dr, HID, HID, WB, a.B, a.sfb_rs, (uint32_t)((int64_t)a.sfb_world * a.sfb_rs * 2)};
+  fc1_dw_tile(a, la, lb, (id / FDW_GX) * FDW_BM, (id % FDW_GX) * FDW_BN, WB, (bf16*)smem_raw);
 }
 
 // ---------------- one-GPU optimizer tail: K16 ApplyAdam with the K12/K14/K15 slab reduce fused ----------------
@@ -1543,16 +1550,24 @@ void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_
 
 int64_t mnist_sfb_slot_elems(int B) { return ((int64_t)B * (2 * HID + 2 * NCLS) + 63) / 64 * 64; }
 
-void mnist_fc_grad_sfb(const MnistStepArgs& a, hipStream_t s) {
+void mnist_fc_grad_sfb(const MnistStepArgs& a, hipStream_t s, bool with_reduce) {
   if (a.sfb_world < 1 || !a.sfb_p2 || !a.sfb_dr) throw std::runtime_error("mnist_fc_grad_sfb: no gathered factors");
   constexpr int sm_og = OUTS_ROWS * OUTS_GROUPS * NCLS * 4;
   constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowBuf, RankRowsMC>::BYTES;
   constexpr int sm = sm_dw > sm_og ? sm_dw : sm_og;
+  static_assert(sm >= 256 * 4, "the merged slab-reduce blocks use the launch's LDS as their 256-float stage");
   set_smem<fc_grad_sfb>(sm);
   const bool part = a.sfb_by_hi >= a.sfb_by_lo;
   if (part && (a.sfb_by_lo < 0 || a.sfb_by_hi >= FDW_GY)) throw std::runtime_error("mnist_fc_grad_sfb: tile rows");
   const int nby = part ? (a.sfb_by_hi - a.sfb_by_lo + 1) + (a.sfb_by_hi < FDW_GY - 1 ? 1 : 0) : FDW_GY;
-  fc_grad_sfb<<<OUTS_BLOCKS + FDW_GX * nby, 256, sm, s>>>(a);
+  int gb = 0, nlead = 0;
+  if (with_reduce) {  // the slab reduce's contract (mnist_conv_grad_reduce): gather blocks read t_out
+    if (a.step_bump && a.perm && a.xpre && !a.t_out)
+      throw std::runtime_error("mnist_fc_grad_sfb: the merged gather reads the next step from t_out");
+    gb = (a.step_bump && a.perm && a.xpre) ? a.B : 0;
+    nlead = gb + RED2_BLOCKS + RED1_BLOCKS;
+  }
+  fc_grad_sfb<<<nlead + OUTS_BLOCKS + FDW_GX * nby, 256, sm, s>>>(a, gb, nlead);
 }
 
 void mnist_sfb_tile_rows(int row0, int row1, int* by_lo, int* by_hi) {

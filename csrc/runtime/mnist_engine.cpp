@@ -220,6 +220,10 @@ class MnistEngine : public torch::CustomClassHolder {
     sfb_ = true;
   }
   bool fc_sfb() const { return sfb_active(); }
+  // SFB schedule: run the conv slab reduce inside the SFB GEMM's launch (one kernel boundary and the
+  // reduce's own latency less; the conv bucket's all-reduce moves behind the fc-region optimizer)
+  void set_sfb_merge_reduce(bool on) { merge_tail_ = on; }
+  bool sfb_merge_reduce() const { return merge_tail_; }
   // bf16 elements of the larger of the two per-rank gather shards (IPC staging must hold it)
   int64_t sfb_shard_elems() const { return std::max<int64_t>(B_ * FEAT, mnist_sfb_slot_elems((int)B_)); }
   void set_fused_tail(int64_t on) { fuse_tail_ = on != 0; }
@@ -533,19 +537,32 @@ class MnistEngine : public torch::CustomClassHolder {
     mark(P_BFC, s);
     mnist_backward_b(a, s);
     tag("conv_bwd", s);
-    mnist_conv_grad_reduce(a, s);
-    tag("slab_reduce", s);
-    mark(P_BCONV, s);
-    HIP_OK(hipEventRecord(ev_b_, s));
-    wait(comm_stream_, ev_b_, "ar_conv<-slab_reduce");
-    mark(P_CB0, comm_stream_);
-    reduce_bucket(0, BUCKET_SPLIT, bf);
-    tag("ar_conv", comm_stream_);
-    mark(P_CB1, comm_stream_);
-    HIP_OK(hipEventRecord(ev_done_, comm_stream_));
-    wait(s, ev_ag_, "sfb_gemm<-gather_dr");
-    mnist_fc_grad_sfb(a, s);  // beside the conv bucket's all-reduce
-    tag("sfb_gemm", s);
+    auto ar_conv = [&]() {
+      mark(P_BCONV, s);
+      HIP_OK(hipEventRecord(ev_b_, s));
+      wait(comm_stream_, ev_b_, "ar_conv<-slab_reduce");
+      mark(P_CB0, comm_stream_);
+      reduce_bucket(0, BUCKET_SPLIT, bf);
+      tag("ar_conv", comm_stream_);
+      mark(P_CB1, comm_stream_);
+      HIP_OK(hipEventRecord(ev_done_, comm_stream_));
+    };
+    if (merge_tail_) {
+      // ONE launch for the slab reduce and the SFB GEMM (their blocks side by side); the conv
+      // bucket's all-reduce then runs beside the fc-region optimizer instead of beside the GEMM
+      wait(s, ev_ag_, "sfb_gemm<-gather_dr");
+      mnist_fc_grad_sfb(a, s, true);
+      tag("sfb_gemm", s);
+      tag_alias("slab_reduce");
+      ar_conv();
+    } else {
+      mnist_conv_grad_reduce(a, s);
+      tag("slab_reduce", s);
+      ar_conv();
+      wait(s, ev_ag_, "sfb_gemm<-gather_dr");
+      mnist_fc_grad_sfb(a, s);  // beside the conv bucket's all-reduce
+      tag("sfb_gemm", s);
+    }
     const int64_t* t = (const int64_t*)tnext_.data_ptr();
     // With real peers the conv bucket's all-reduce can outlast the SFB GEMM (at 8 ranks the ZeRO
     // GEMM is ~4 us): the fc-region optimizer (its gradients are local) then runs first and covers
@@ -932,6 +949,12 @@ class MnistEngine : public torch::CustomClassHolder {
   }
   // capture_topology: the graph nodes this operation added (everything new since the last tag; the
   // host issues operations one after another, so the difference is exactly this operation's nodes)
+  // capture_topology: the last operation's nodes under a second label (one launch doing two jobs)
+  void tag_alias(const char* label) {
+    if (!topo_ || topo_tags_.empty()) return;
+    auto nodes = topo_tags_.back().second;
+    topo_tags_.emplace_back(std::string(label) + "@" + std::to_string(topo_step_), std::move(nodes));
+  }
   void tag(const char* label, hipStream_t st) {
     if (!topo_) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -1142,6 +1165,7 @@ class MnistEngine : public torch::CustomClassHolder {
   hipStream_t opt_stream_ = nullptr;  // train_step_dp: the fc-region optimizer
   hipEvent_t ev_opt_a_ = nullptr, ev_start_ = nullptr, ev_ag_ = nullptr;
   bool zero_ = false;
+  bool merge_tail_ = false;
   bool pending_wag_ = false;  // serialized ZeRO: this step's shards not yet all-gathered
   bool wag_issued_ = false;   // ... their all-gather already queued on the comm stream (ev_wag_)
   bool force_dp_ = false;
@@ -1210,6 +1234,8 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def("set_ipc", &MnistEngine::set_ipc)
       .def("set_ipc_gather", &MnistEngine::set_ipc_gather)
       .def("set_zero", &MnistEngine::set_zero)
+      .def("set_sfb_merge_reduce", &MnistEngine::set_sfb_merge_reduce)
+      .def("sfb_merge_reduce", &MnistEngine::sfb_merge_reduce)
       .def("set_fc_sfb", &MnistEngine::set_fc_sfb)
       .def("fc_sfb", &MnistEngine::fc_sfb)
       .def("sfb_shard_elems", &MnistEngine::sfb_shard_elems)

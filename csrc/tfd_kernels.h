@@ -95,7 +95,9 @@ void mnist_adam_fused(const MnistStepArgs& a, const MnistAdamArgs& o, hipStream_
 // products (dW_fc1 = [P2;1]^T dH, dW_out = [Hd;1]^T dlogits), so the all-reduced gradient is ONE
 // GEMM over the all-gathered factors (K = W*B). Writes the summed fc-region gradients (bucket A)
 // like mnist_backward_a part 1 (bf16 into gbf_a when set), identical on every rank.
-void mnist_fc_grad_sfb(const MnistStepArgs& a, hipStream_t s);
+// with_reduce: the same launch also runs mnist_conv_grad_reduce's blocks (next-batch gather + conv
+// slab reduce + step bump; needs t_out like its one-launch form) -- the merged DP tail.
+void mnist_fc_grad_sfb(const MnistStepArgs& a, hipStream_t s, bool with_reduce = false);
 // fc1 dW tile-row range (64 rows per tile row) covering flat fc1 weight rows [row0, row1)
 void mnist_sfb_tile_rows(int row0, int row1, int* by_lo, int* by_hi);
 // bf16 elements of one rank's sfb_dr slot for batch B (dh + hd + dlogits, padded to 64)

@@ -180,6 +180,9 @@ class TorchMnistRunner(MnistRunnerBase):
     def set_phase_timing(self, on: bool = True) -> None:
         pass
 
+    def sync_state(self) -> None:
+        pass  # never sharded
+
     def phase_times(self) -> dict:
         """CPU path: host time of the last Gloo gradient all-reduce (the only timed phase)."""
         ms = getattr(self.comm, "last_ms", None)
@@ -403,6 +406,13 @@ class NativeMnistRunner(MnistRunnerBase):
         self.stream.synchronize()
         self._hstep += 1
         return self.eng.grads(), (float(self.eng.loss_rows().mean().item()) if with_loss else None)
+
+    def sync_state(self) -> None:
+        """ZeRO-1 (``eng.zero()``): every worker gathers the fc1 shards of the fp32 master and the Adam
+        slots, so ``params()`` / ``slot_tensors()`` are whole (a collective: all workers call it)."""
+        with torch.cuda.stream(self.stream):
+            self.eng.sync_params()
+        self.stream.synchronize()
 
     def sync_shadow(self) -> None:
         """Re-derive the bf16 operand shadow from the fp32 master (after a parameter server wrote the

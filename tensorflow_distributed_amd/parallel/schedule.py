@@ -20,6 +20,22 @@ from __future__ import annotations
 import math
 from typing import Callable, Dict, Optional, Sequence, Tuple
 
+# The bf16 MNIST engine's DP schedules (name -> MnistEngine switches), in probe order (ties go to the
+# earlier one). "sfb": fc-region gradients by sufficient-factor broadcasting (all-gather the fc
+# factors, 1.33 MB/rank at B = 128, and form the summed gradient locally); "+zero": ZeRO-1 sharding of
+# the fc1 weight on top; "+mr": the conv slab reduce merged into the SFB GEMM's launch (the conv
+# bucket's all-reduce then hides behind the fc-region optimizer instead of the GEMM); "allreduce": the
+# bucketed bf16 gradient all-reduce (6.4 MB fc bucket + IPC one-shot conv bucket).
+MNIST_SCHEDULES = {
+    "sfb+zero+mr": {"fc_sfb": 1, "zero": 1, "merge_reduce": 1},
+    "sfb+mr": {"fc_sfb": 1, "zero": 0, "merge_reduce": 1},
+    "sfb+zero": {"fc_sfb": 1, "zero": 1, "merge_reduce": 0},
+    "sfb": {"fc_sfb": 1, "zero": 0, "merge_reduce": 0},
+    "allreduce": {"fc_sfb": 0, "zero": 0, "merge_reduce": 0},
+}
+# CPU (Gloo) sync DP: the flat gradient in one all-reduce, or the conv and fc buckets separately
+CPU_SCHEDULES = ("flat", "buckets")
+
 
 def probe(candidates: Sequence[str], run_one: Callable[[str], float], max_over_ranks: Callable[[float], float],
           log: Optional[Callable[[str], None]] = None) -> Dict[str, float]:

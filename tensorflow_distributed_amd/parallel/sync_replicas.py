@@ -58,7 +58,7 @@ class SyncReplicasStepper:
     """One global step of sync DP for a model runner (CPU or native GPU)."""
 
     def __init__(self, runner, worker_rank: int, num_workers: int, replicas_to_aggregate: int,
-                 group=None, straggler_delay_s: Optional[dict] = None):
+                 group=None, straggler_delay_s: Optional[dict] = None, splits=None):
         self.runner = runner
         self.rank = worker_rank
         self.world = num_workers
@@ -68,7 +68,7 @@ class SyncReplicasStepper:
         self.last_contributors = list(range(num_workers))
         native = hasattr(runner, "eng")
         if not native and self.r2a == self.world:
-            runner.comm = GlooGradAverager(group, num_workers)
+            runner.comm = GlooGradAverager(group, num_workers, splits)  # splits: the "buckets" schedule
 
     def step(self, x, y) -> None:
         r = self.runner

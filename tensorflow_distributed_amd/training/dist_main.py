@@ -96,9 +96,15 @@ def define_flags(task_index_default: int = 0, job_name_default: str = "ps") -> N
     f.DEFINE_enum("dp_transport", "auto", ["auto", "rccl", "ipc"], "GPU sync gradient transport: auto = "
                   "peer-to-peer IPC when workers share a GPU (--num_gpus < workers; RCCL refuses that), else "
                   "RCCL over xGMI (+ IPC one-shot for the small conv bucket)")
-    f.DEFINE_boolean("fc_sfb", True, "GPU sync DP: fc-layer gradients by sufficient-factor broadcasting -- "
-                     "all-gather each worker's fc factors (activations + output gradients, 1.33 MB at batch 128) "
-                     "and form the summed fc gradient locally instead of all-reducing it (6.4 MB bf16)")
+    f.DEFINE_string("dp_schedule", "auto", "Sync DP schedule (workers > 1). auto = before training every worker "
+                    "times each candidate for --dp_probe_steps steps and all keep the fastest (max over workers); or "
+                    "a name. GPU bf16: sfb+zero+mr, sfb+mr, sfb+zero, sfb, allreduce (parallel/schedule.py: "
+                    "sufficient-factor fc gradients, ZeRO-1 fc1 sharding, slab reduce merged into the SFB GEMM, "
+                    "bucketed all-reduce); GPU fp32: allreduce; CPU (Gloo): flat, buckets")
+    f.DEFINE_integer("dp_probe_steps", 200, "Timed steps per --dp_schedule=auto candidate (CPU: at most 5)")
+    f.DEFINE_integer("dp_probe_warmup", 30, "Untimed steps before each candidate's timing (CPU: 1)")
+    f.DEFINE_integer("zero_sync_every", 100, "ZeRO-1 schedules: every this many global steps all workers agree "
+                     "whether the chief's checkpoint is due and, if so, gather the sharded fc1 state first")
     f.DEFINE_boolean("phase_timing", False, "GPU: HIP timing events at the step's phase boundaries (forward, fc "
                      "backward, conv backward, optimizer, all-reduce), written to --metrics_file (always on when "
                      "--metrics_file is set on the chief)")
@@ -233,6 +239,121 @@ def _resnet_worker(server, cluster, num_workers: int, is_chief: bool) -> int:
     return 0
 
 
+def _max_over(group, v: float) -> float:
+    import torch.distributed as dist
+
+    t = torch.tensor([float(v)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def dp_candidates(device_type: str, dtype: str):
+    """The sync DP schedules this worker device can run (parallel/schedule.py), in probe order."""
+    from ..parallel import schedule as SCH
+
+    if device_type == "cuda":
+        return list(SCH.MNIST_SCHEDULES) if dtype == "bf16" else ["allreduce"]
+    return list(SCH.CPU_SCHEDULES)
+
+
+def choose_dp_schedule(run_one, rank: int, num_workers: int, device_type: str, group=None, log=None):
+    """(schedule, {candidate: ms/step max over workers} or None, how it was chosen).
+
+    ``--dp_schedule=auto`` with more than one candidate: every worker times every candidate with
+    ``run_one(name)`` (same names, same order), the slowest worker's time counts and all keep the
+    fastest -- the same in-job probe as bench.py (parallel/schedule.py). The reference has one
+    schedule, the PS star (/root/reference/mnist_python_m.py:177,210-233)."""
+    from ..parallel import schedule as SCH
+
+    known = dp_candidates(device_type, FLAGS.dtype)
+    want = FLAGS.dp_schedule
+    if want != "auto":
+        if want not in known:
+            raise ValueError("--dp_schedule=%s: not a %s schedule (known: %s)" % (want, device_type, ", ".join(known)))
+        return want, None, "flag"
+    if num_workers <= 1 or len(known) == 1:
+        return known[0], None, "only"
+    times = SCH.probe(known, run_one, lambda v: _max_over(group, v), log)
+    return SCH.pick(times), times, "probe"
+
+
+def _probe_gpu_schedule(name, mnist, device, num_workers, group, src, comm):
+    """Local ms/step of one GPU DP schedule: a throwaway engine + transport on the worker's device,
+    chief-style init, the device-resident split, --dp_probe_warmup untimed then --dp_probe_steps
+    timed graph replays between barriers. Setup failures are agreed on first (no worker may enter
+    the timing collectives alone)."""
+    import torch.distributed as dist
+
+    from ..models import mnist_cnn as M
+    from ..models.mnist_runner import make_runner
+    from ..parallel.schedule import MNIST_SCHEDULES
+    from ..parallel.transport import attach_engine
+
+    cfg = MNIST_SCHEDULES.get(name, {"fc_sfb": 0, "zero": 0, "merge_reduce": 0})
+    r, tr, err = None, None, None
+    try:
+        r = make_runner(FLAGS.batch_size, _make_optimizer(), device, keep_prob=FLAGS.keep_prob, seed=FLAGS.seed,
+                        rank=FLAGS.task_index, bf16_grads=FLAGS.bf16_grads, use_graph=True, dtype=FLAGS.dtype)
+        tr = attach_engine(r.eng, FLAGS.task_index, num_workers, device, group=group, src=src, mode=FLAGS.dp_transport,
+                           comm=comm, bf16=FLAGS.bf16_grads, sfb=bool(cfg["fc_sfb"]) and FLAGS.dtype == "bf16",
+                           zero=bool(cfg["zero"]))
+        if cfg["zero"]:
+            r.eng.set_zero(True)
+        r.eng.set_sfb_merge_reduce(bool(cfg["merge_reduce"]))
+        r.comm, r.transport = tr.comm, tr
+        r.set_device_dataset(mnist.train.images, mnist.train.labels, seed=FLAGS.seed * 1000 + FLAGS.task_index + 31)
+        r.load_flat(M.flat_from_dict(M.init_params(FLAGS.seed)), {}, 0)
+    except Exception as e:  # noqa: BLE001 - agreed below
+        err = e
+    if _max_over(group, 1.0 if err is not None else 0.0) > 0:
+        if tr is not None:
+            tr.close()
+        raise RuntimeError("schedule probe setup failed on a worker (here: %r)" % (err,))
+    try:
+        r.train_step(None, None)  # eager step + capture of the step graph
+        with torch.cuda.stream(r.stream):
+            r.eng.replay("train", max(1, FLAGS.dp_probe_warmup))
+        torch.cuda.synchronize(device)
+        dist.barrier(group=group)
+        t0 = time.perf_counter()
+        n = max(1, FLAGS.dp_probe_steps)
+        with torch.cuda.stream(r.stream):
+            r.eng.replay("train", n)
+        torch.cuda.synchronize(device)
+        dt = time.perf_counter() - t0
+        tr.check("schedule probe %s" % name)
+    finally:
+        torch.cuda.synchronize(device)
+        dist.barrier(group=group)  # a peer may still read this engine's IPC staging
+        r.eng.drop_graph("train")
+        tr.close()
+        dist.barrier(group=group)
+    return dt * 1e3 / n
+
+
+def _probe_cpu_schedule(name, num_workers, group):
+    """Local ms/step of one Gloo schedule on the CPU runner (random batch, 1 + min(5, steps) steps)."""
+    import torch.distributed as dist
+
+    from ..models import mnist_cnn as M
+    from ..models.mnist_runner import TorchMnistRunner
+    from ..parallel.sync_replicas import GlooGradAverager
+
+    r = TorchMnistRunner(FLAGS.batch_size, _make_optimizer(), FLAGS.keep_prob, FLAGS.seed, FLAGS.task_index)
+    r.load_flat(M.flat_from_dict(M.init_params(FLAGS.seed)), {}, 0)
+    r.comm = GlooGradAverager(group, num_workers, [M.BUCKET_SPLIT] if name == "buckets" else None)
+    g = torch.Generator().manual_seed(FLAGS.task_index + 5)
+    x = torch.rand(FLAGS.batch_size, 784, generator=g)
+    y = torch.randint(0, 10, (FLAGS.batch_size,), generator=g)
+    r.train_step(x, y)
+    dist.barrier(group=group)
+    n = max(1, min(FLAGS.dp_probe_steps, 5))
+    t0 = time.perf_counter()
+    for _ in range(n):
+        r.train_step(x, y)
+    return (time.perf_counter() - t0) * 1e3 / n
+
+
 def main(argv=None) -> int:
     from ..models import mnist_cnn as M
     from ..models.mnist_runner import make_runner
@@ -329,18 +450,47 @@ def main(argv=None) -> int:
     if sync:
         sopt = SyncReplicasOptimizer(opt, replicas_to_aggregate=r2a, total_num_replicas=num_workers).resolve(num_workers)
 
+    # Sync all-reduce DP: which schedule (parallel/schedule.py) -- probed in-job by every worker, or
+    # fixed by --dp_schedule. One RCCL communicator serves every probe and the training run.
+    dp_sched, dp_probe, dp_source, rccl = None, None, None, None
+    allreduce_dp = sync and num_workers > 1 and not backup_ps
+    if allreduce_dp:
+        grp = server.worker_group
+        if device.type == "cuda":
+            from ..parallel.transport import devices_shared, make_rccl
+
+            if FLAGS.dp_transport != "ipc" and not devices_shared(device, num_workers, grp):
+                rccl = make_rccl(FLAGS.task_index, num_workers, device.index or 0, group=grp, src=cluster.num_ps)
+            run_one = lambda name: _probe_gpu_schedule(name, mnist, device, num_workers, grp,  # noqa: E731
+                                                       cluster.num_ps, rccl)
+        else:
+            run_one = lambda name: _probe_cpu_schedule(name, num_workers, grp)  # noqa: E731
+        log = (lambda m: print(m, file=sys.stderr, flush=True)) if is_chief else None
+        dp_sched, dp_probe, dp_source = choose_dp_schedule(run_one, FLAGS.task_index, num_workers, device.type,
+                                                           grp, log)
+        if is_chief:
+            print("Worker %d: DP schedule %s (%s%s)" % (
+                FLAGS.task_index, dp_sched, dp_source,
+                (": " + ", ".join("%s %.4f ms/step" % kv for kv in dp_probe.items())) if dp_probe else ""))
     runner = make_runner(FLAGS.batch_size, opt, device, keep_prob=FLAGS.keep_prob, seed=FLAGS.seed,
                          rank=FLAGS.task_index, comm=None, bf16_grads=FLAGS.bf16_grads,
                          use_graph=FLAGS.use_graph and (sopt is None or not sopt.has_backup_workers or backup_ps),
                          dtype=FLAGS.dtype)
     comm = None
     transport = None
-    if device.type == "cuda" and sync and num_workers > 1 and not backup_ps:
+    zero = False
+    if allreduce_dp and device.type == "cuda":
+        from ..parallel.schedule import MNIST_SCHEDULES
         from ..parallel.transport import attach_engine
 
+        cfg = MNIST_SCHEDULES.get(dp_sched, {"fc_sfb": 0, "zero": 0, "merge_reduce": 0})
+        zero = bool(cfg["zero"]) and FLAGS.dtype == "bf16"
         transport = attach_engine(runner.eng, FLAGS.task_index, num_workers, device, group=server.worker_group,
-                                  src=cluster.num_ps, mode=FLAGS.dp_transport, bf16=FLAGS.bf16_grads,
-                                  sfb=FLAGS.fc_sfb and FLAGS.dtype == "bf16" and FLAGS.model == "mnist_cnn")
+                                  src=cluster.num_ps, mode=FLAGS.dp_transport, comm=rccl, bf16=FLAGS.bf16_grads,
+                                  sfb=bool(cfg["fc_sfb"]) and FLAGS.dtype == "bf16", zero=zero)
+        if zero:
+            runner.eng.set_zero(True)
+        runner.eng.set_sfb_merge_reduce(bool(cfg["merge_reduce"]))
         comm = transport.comm
         runner.comm = comm
         runner.transport = transport
@@ -444,8 +594,12 @@ def main(argv=None) -> int:
     stepper = None
     if sync and not backup_ps:
         stepper = sync_replicas.SyncReplicasStepper(runner, FLAGS.task_index, num_workers, sopt.replicas_to_aggregate,
-                                                    group=server.worker_group, straggler_delay_s=delays)
+                                                    group=server.worker_group, straggler_delay_s=delays,
+                                                    splits=[M.BUCKET_SPLIT] if dp_sched == "buckets" else None)
     metrics = MetricsLogger(FLAGS.metrics_file if is_chief else "")
+    if dp_sched is not None:
+        metrics.log(event="dp_schedule", chosen=dp_sched, source=dp_source,
+                    candidates_ms_per_step=({k: round(v, 5) for k, v in dp_probe.items()} if dp_probe else None))
     phase_timing = FLAGS.phase_timing or (is_chief and bool(FLAGS.metrics_file))
     if phase_timing:
         runner.set_phase_timing(True)
@@ -511,8 +665,24 @@ def main(argv=None) -> int:
             rec.setdefault("allreduce_ms", 0.0 if (not sync or num_workers == 1) else None)
             metrics.log(**rec)
         if FLAGS.check_consistency_every and sync and local_step % FLAGS.check_consistency_every == 0:
+            if zero:
+                runner.sync_state()  # every worker: the fc1 shards -> whole fp32 state
             _check_consistency(runner, server, num_workers)
-        sv.on_step(step)
+        if zero:
+            # the fp32 fc1 master and its Adam slots are sharded over the workers: the chief's timed
+            # checkpoint needs a gather that every worker joins, at agreed global steps
+            save_now = False
+            if step % max(1, FLAGS.zero_sync_every) == 0:
+                due = torch.tensor([1 if sv.save_due() else 0], dtype=torch.int64)
+                import torch.distributed as dist
+
+                dist.all_reduce(due, op=dist.ReduceOp.MAX, group=server.worker_group)
+                save_now = bool(due.item())
+                if save_now:
+                    runner.sync_state()
+            sv.on_step(step, allow_save=save_now)
+        else:
+            sv.on_step(step)
         while is_chief and eval_at and step >= eval_at[0]:
             te = time.time()
             accs = []
@@ -532,6 +702,8 @@ def main(argv=None) -> int:
             os._exit(17)
 
     watchdog.stop()
+    if zero:
+        runner.sync_state()  # whole replicas again: final checksum, eval and the chief's last checkpoint
     if FLAGS.check_consistency_every and sync:
         pp = runner.params().detach().double()
         print("Worker %d: parameter checksum %.17g %.17g" % (FLAGS.task_index, float(pp.sum().item()),

@@ -81,13 +81,19 @@ class Supervisor:
             self._threads.append(t)
 
     # ---- per-step services (training thread) ----
-    def on_step(self, global_step: int, scalars: Optional[dict] = None) -> None:
+    def save_due(self) -> bool:
+        """The chief's checkpoint timer has fired and the save has not happened yet."""
+        return self.is_chief and self._save_due.is_set()
+
+    def on_step(self, global_step: int, scalars: Optional[dict] = None, allow_save: bool = True) -> None:
+        """``allow_save=False`` defers a due checkpoint (the flag stays set): a sharded run saves only at
+        steps where every worker first gathered the shards (dist_main's ZeRO-1 sync points)."""
         if not self.is_chief:
             return
         if self._summary_due.is_set():
             self._summary_due.clear()
             self.write_summary(global_step, scalars)
-        if self._save_due.is_set():
+        if allow_save and self._save_due.is_set():
             self._save_due.clear()
             self.save(global_step)
 

@@ -133,13 +133,16 @@ def test_forced_dp_world1_zero1_tracks_plain_dp(cuda, mode, sfb):
     tr1.close()
 
 
-@pytest.mark.parametrize("mode,sfb,zero", [("rccl", True, False), ("ipc", True, False), ("rccl", True, True),
-                                           ("rccl", False, False), ("rccl", False, True)])
-def test_dp_schedules_captured_equal_eager(cuda, mode, sfb, zero):
-    """Every DP schedule that remains (SFB serialized step, with and without ZeRO-1; bucketed
-    all-reduce step, with and without reduce-scatter ZeRO-1), forced at world 1 over the real
-    communicator: multi-step hipGraphs with captured collectives replay exactly the eager steps --
-    parameters, Adam state and bf16 shadow bit for bit."""
+@pytest.mark.parametrize("mode,sfb,zero,mr", [("rccl", True, False, False), ("ipc", True, False, False),
+                                              ("rccl", True, True, False), ("rccl", True, False, True),
+                                              ("ipc", True, False, True), ("rccl", True, True, True),
+                                              ("rccl", False, False, False), ("rccl", False, True, False)])
+def test_dp_schedules_captured_equal_eager(cuda, mode, sfb, zero, mr):
+    """Every DP schedule that remains (SFB serialized step, with and without ZeRO-1, slab reduce in
+    its own launch or merged into the SFB GEMM's; bucketed all-reduce step, with and without
+    reduce-scatter ZeRO-1), forced at world 1 over the real communicator: multi-step hipGraphs with
+    captured collectives replay exactly the eager steps -- parameters, Adam state and bf16 shadow bit
+    for bit."""
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     s = torch.cuda.Stream()
@@ -150,6 +153,7 @@ def test_dp_schedules_captured_equal_eager(cuda, mode, sfb, zero):
             trs.append(attach_engine(e, 0, 1, cuda, mode=mode, force_dp=True, sfb=sfb))
             if zero:
                 e.set_zero(True)
+            e.set_sfb_merge_reduce(mr)
             e.train_step()
             e.train_step()
         gr.capture_train_steps("t", 3)
@@ -164,6 +168,39 @@ def test_dp_schedules_captured_equal_eager(cuda, mode, sfb, zero):
     assert int(gr.step_tensor().item()) == int(ea.step_tensor().item()) == 8
     assert torch.equal(gr.params(), ea.params()) and torch.equal(gr.adam_v(), ea.adam_v())
     assert torch.equal(gr.params_bf16(), ea.params_bf16())
+    for tr in trs:
+        tr.close()
+
+
+@pytest.mark.parametrize("mode,zero", [("rccl", False), ("ipc", False), ("rccl", True)])
+def test_sfb_merged_reduce_equals_separate(cuda, mode, zero):
+    """The merged DP tail (conv slab reduce + next-batch gather + step bump as leading blocks of the SFB
+    GEMM's launch) against the separate reduce launch: the same blocks compute the same sums in the
+    same order, so five steps (eager and captured) leave parameters, Adam state, bf16 shadow and the
+    step counter bit-identical."""
+    from tensorflow_distributed_amd.parallel.transport import attach_engine
+
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        params, (sep, mer) = _engines_on_dataset(cuda, 2)
+        trs = []
+        for e, mr in ((sep, False), (mer, True)):
+            trs.append(attach_engine(e, 0, 1, cuda, mode=mode, force_dp=True, sfb=True))
+            if zero:
+                e.set_zero(True)
+            e.set_sfb_merge_reduce(mr)
+            assert e.sfb_merge_reduce() == mr
+            for _ in range(2):
+                e.train_step()
+            e.capture_train_steps("t", 3)
+            e.replay("t", 1)
+            e.sync_params()
+    torch.cuda.synchronize()
+    for tr in trs:
+        tr.check()
+    assert int(sep.step_tensor().item()) == int(mer.step_tensor().item()) == 5
+    for get in ("params", "adam_m", "adam_v", "params_bf16"):
+        assert torch.equal(getattr(sep, get)(), getattr(mer, get)()), get
     for tr in trs:
         tr.close()
 
@@ -211,7 +248,7 @@ def test_reference_quickstart_two_workers_share_one_gpu(cuda, tmp_path):
 
     args = ["--num_gpus=1", "--train_steps=12", f"--logdir={tmp_path}", "--synthetic_data", "--eval_batches=1",
             "--data_dir=/nonexistent", "--check_consistency_every=1", "--log_device_placement",
-            f"--metrics_file={tmp_path}/m.jsonl"]
+            f"--metrics_file={tmp_path}/m.jsonl", "--dp_probe_steps=20", "--dp_probe_warmup=5"]
     r = launch.launch(1, 2, args, echo=False, timeout_s=300)
     assert r["ok"], r["outputs"]
     outs = {k.split("#")[0]: v for k, v in r["outputs"].items()}
@@ -224,6 +261,14 @@ def test_reference_quickstart_two_workers_share_one_gpu(cuda, tmp_path):
         sums.append(line.split("checksum")[1].split())
     assert sums[0] == sums[1], sums
     recs = [json.loads(ln) for ln in open(tmp_path / "m.jsonl")]
+    # the workers probed every GPU DP schedule in-job (dist_main --dp_schedule=auto) and kept the fastest
+    from tensorflow_distributed_amd.parallel.schedule import MNIST_SCHEDULES
+
+    sch = [rec for rec in recs if rec.get("event") == "dp_schedule"]
+    assert len(sch) == 1 and sch[0]["source"] == "probe", sch
+    c = sch[0]["candidates_ms_per_step"]
+    assert set(c) == set(MNIST_SCHEDULES) and sch[0]["chosen"] == min(c, key=c.get), sch
+    assert f"Worker 0: DP schedule {sch[0]['chosen']} (probe: " in outs["worker:0"]
     steps = [rec for rec in recs if "step" in rec and "event" not in rec]
     assert len(steps) == 12
     # GPU phase events: the IPC bucket collectives were timed on the comm stream
@@ -269,12 +314,14 @@ def test_bench_self_launches_n_ranks(cuda, n):
     assert r["n_gpus"] == n and r["config"]["parallelism"] == f"dp{n}"
     assert r["comm_world"] == n and len(r["devices"]) == n and r["replicas_identical"], r
     assert r["config"]["global_batch"] == 128 * n and r["value"] > 0
-    # the ranks probed all three DP schedules at this N and timed the fastest
+    # the ranks probed every DP schedule at this N and timed the fastest
     sch = r["schedule"]
     c = sch["candidates_ms_per_step"]
-    assert sch["source"] == "probe" and set(c) == {"sfb+zero", "sfb", "allreduce"}, sch
+    from tensorflow_distributed_amd.parallel.schedule import MNIST_SCHEDULES
+
+    assert sch["source"] == "probe" and set(c) == set(MNIST_SCHEDULES), sch
     assert all(v > 0 for v in c.values()) and sch["chosen"] == min(c, key=c.get), sch
-    assert r["config"]["zero1_fc1"] == (sch["chosen"] == "sfb+zero")
+    assert r["config"]["zero1_fc1"] == sch["chosen"].startswith("sfb+zero")
     assert r["config"]["dp_transport"] == ("ipc+sfb" if "sfb" in sch["chosen"] else "ipc"), r["config"]
 
 

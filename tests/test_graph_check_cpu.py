@@ -32,6 +32,10 @@ class Sim:
         self.last[stream] = i
         self.lines.append(f"tag {label}@{self.step} {i}")
 
+    def alias(self, label):
+        """The last op's node under a second label (MnistEngine::tag_alias: one launch, two jobs)."""
+        self.lines.append(f"tag {label}@{self.step} {self.n - 1}")
+
     def record(self, ev, stream):
         self.ev[ev] = self.last[stream]
 
@@ -40,8 +44,9 @@ class Sim:
             self.pending.setdefault(stream, set()).add(self.ev[ev])
 
 
-def sfb_schedule(sim, steps=2, zero=False, world=2):
-    """train_step_sfb_serial's operation/event order (csrc/runtime/mnist_engine.cpp)."""
+def sfb_schedule(sim, steps=2, zero=False, world=2, merged=False):
+    """train_step_sfb_serial's operation/event order (csrc/runtime/mnist_engine.cpp). merged: the slab
+    reduce runs inside the SFB GEMM's launch (set_sfb_merge_reduce)."""
     pending_wag = False
     for i in range(steps):
         sim.step = i
@@ -65,13 +70,19 @@ def sfb_schedule(sim, steps=2, zero=False, world=2):
         sim.record("ag", "c")
         sim.op("s", "fc1_dx")
         sim.op("s", "conv_bwd")
-        sim.op("s", "slab_reduce")
+        if merged:
+            sim.wait("s", "ag", "sfb_gemm<-gather_dr")
+            sim.op("s", "sfb_gemm")
+            sim.alias("slab_reduce")
+        else:
+            sim.op("s", "slab_reduce")
         sim.record("b", "s")
         sim.wait("c", "b", "ar_conv<-slab_reduce")
         sim.op("c", "ar_conv")
         sim.record("done", "c")
-        sim.wait("s", "ag", "sfb_gemm<-gather_dr")
-        sim.op("s", "sfb_gemm")
+        if not merged:
+            sim.wait("s", "ag", "sfb_gemm<-gather_dr")
+            sim.op("s", "sfb_gemm")
         if world > 1:
             sim.op("s", "opt_fc")
             if zero:
@@ -130,7 +141,8 @@ def allreduce_schedule(sim, steps=2):
 def test_full_schedules_have_no_violations():
     for world in (1, 2):
         for zero in (False, True):
-            assert violations(Topology(sfb_schedule(Sim(), 3, zero, world))) == [], (world, zero)
+            for merged in (False, True):
+                assert violations(Topology(sfb_schedule(Sim(), 3, zero, world, merged))) == [], (world, zero, merged)
     assert violations(Topology(allreduce_schedule(Sim(), 3))) == []
 
 
@@ -138,6 +150,10 @@ def test_dropped_wait_is_reported():
     v = violations(Topology(sfb_schedule(Sim(drop={"sfb_gemm<-gather_dr"}), 2)))
     assert any(x.startswith("gather_dr@0 -> sfb_gemm@0") for x in v), v
     assert any(x.startswith("gather_dr@1 -> sfb_gemm@1") for x in v), v
+    v = violations(Topology(sfb_schedule(Sim(drop={"sfb_gemm<-gather_dr"}), 2, merged=True)))
+    assert any(x.startswith("gather_dr@1 -> sfb_gemm@1") for x in v), v
+    v = violations(Topology(sfb_schedule(Sim(drop={"opt_conv<-ar_conv"}), 2, world=2, merged=True)))
+    assert any(x.startswith("ar_conv@0 -> opt_conv@0") for x in v), v
     v = violations(Topology(sfb_schedule(Sim(drop={"gather_p2<-conv_fwd"}), 2)))
     assert any(x.startswith("conv_fwd@0 -> gather_p2@0") for x in v), v
     v = violations(Topology(sfb_schedule(Sim(drop={"fc_fwd<-wag"}), 3, zero=True, world=2)))

@@ -15,7 +15,8 @@ from dist_util import run_ranks
 
 pytestmark = pytest.mark.gpu
 
-SCHEDULES = {"sfb": (True, False), "sfb+zero": (True, True), "allreduce": (False, False)}
+SCHEDULES = {"sfb": (True, False, False), "sfb+zero": (True, True, False), "sfb+mr": (True, False, True),
+             "sfb+zero+mr": (True, True, True), "allreduce": (False, False, False)}
 
 
 def _engine(cuda, world_rank=0, B=64):
@@ -66,13 +67,14 @@ def test_forced_dp_world1_topology(cuda, sched, mode):
     node at all -- nothing to order -- so only the IPC transport must show a node per collective.)"""
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
-    sfb, zero = SCHEDULES[sched]
+    sfb, zero, mr = SCHEDULES[sched]
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         e = _engine(cuda)
         tr = attach_engine(e, 0, 1, cuda, mode=mode, force_dp=True, sfb=sfb, zero=zero)
         if zero:
             e.set_zero(True)
+        e.set_sfb_merge_reduce(mr)
         e.train_step()
         t, v = _check(e, 3, require_nodes=mode == "ipc")
         assert v == [], (sched, v)
@@ -100,13 +102,14 @@ def _ipc_topology_worker(rank, world, sched):
     _native.require()
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
-    sfb, zero = SCHEDULES[sched]
+    sfb, zero, mr = SCHEDULES[sched]
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         e = _engine(dev, rank)
         tr = attach_engine(e, rank, world, dev, mode="ipc", sfb=sfb, zero=zero)
         if zero:
             e.set_zero(True)
+        e.set_sfb_merge_reduce(mr)
         e.train_step()
         lines = list(e.capture_topology(2))
     torch.cuda.synchronize()

@@ -40,6 +40,30 @@ def test_sync_cluster_reference_lines(tmp_path):
     assert os.path.exists(tmp_path / "trace0.json")
 
 
+def test_sync_cluster_probes_dp_schedule(tmp_path):
+    """--dp_schedule=auto (default) at 2 workers over Gloo: both workers time every CPU candidate
+    before training, the chief prints and logs the choice (the fastest by max over workers), and the
+    run trains with it; a pinned schedule skips the probes."""
+    import json
+
+    mf = tmp_path / "m.jsonl"
+    r = launch.launch(1, 2, ["--train_steps=3", f"--logdir={tmp_path}/a", f"--metrics_file={mf}",
+                             "--dp_probe_steps=2"] + COMMON, echo=False, timeout_s=300)
+    assert r["ok"], r["outputs"]
+    w0 = _out(r, "worker:0")
+    rec = [json.loads(ln) for ln in open(mf) if '"dp_schedule"' in ln]
+    assert len(rec) == 1 and rec[0]["source"] == "probe", rec
+    c = rec[0]["candidates_ms_per_step"]
+    assert set(c) == {"flat", "buckets"} and all(v > 0 for v in c.values()), c
+    assert rec[0]["chosen"] == min(c, key=c.get)
+    assert f"Worker 0: DP schedule {rec[0]['chosen']} (probe: " in w0, w0
+    assert "training step 3 done (global step: 3)" in w0
+    r = launch.launch(1, 2, ["--train_steps=2", f"--logdir={tmp_path}/b", "--dp_schedule=buckets"] + COMMON,
+                      echo=False, timeout_s=300)
+    assert r["ok"], r["outputs"]
+    assert "Worker 0: DP schedule buckets (flag)" in _out(r, "worker:0")
+
+
 def test_async_cluster_two_ps(tmp_path):
     r = launch.launch(2, 2, ["--train_steps=4", "--sync_replicas=False", f"--logdir={tmp_path}"] + COMMON,
                       echo=False, timeout_s=300)

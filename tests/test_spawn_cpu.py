@@ -112,7 +112,7 @@ def test_schedule_pick_takes_max_over_ranks_and_fastest():
 
 
 def test_bench_schedule_flags_resolve():
-    """--schedule NAME and the --fc_sfb/--zero overrides fix the schedule without probes; a one-GPU
+    """--schedule NAME and the --fc_sfb/--zero/--merge_reduce overrides fix the schedule without probes; a one-GPU
     job without --force_dp has no DP schedule at all."""
     sys.path.insert(0, ROOT)
     import bench
@@ -122,5 +122,8 @@ def test_bench_schedule_flags_resolve():
     assert bench._candidates(a, False) == ([None], "single")
     assert bench._candidates(bench._args(["--schedule", "sfb"]), True) == (["sfb"], "flag")
     assert bench._candidates(bench._args(["--fc_sfb", "0", "--zero", "0"]), True) == (["allreduce"], "flag")
-    assert bench._candidates(bench._args(["--fc_sfb", "1", "--zero", "1"]), True) == (["sfb+zero"], "flag")
+    assert bench._candidates(bench._args(["--fc_sfb", "1", "--zero", "1"]), True) == (["sfb+zero+mr"], "flag")
+    assert bench._candidates(bench._args(["--fc_sfb", "1", "--zero", "1", "--merge_reduce", "0"]), True) == \
+        (["sfb+zero"], "flag")
+    assert bench._candidates(bench._args(["--fc_sfb", "1", "--merge_reduce", "1"]), True) == (["sfb+mr"], "flag")
     assert bench._candidates(bench._args(["--candidates", "sfb,allreduce"]), True) == (["sfb", "allreduce"], "probe")
