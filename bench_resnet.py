@@ -58,6 +58,10 @@ def main(argv=None):
     ap.add_argument("--bn_slots", type=int, default=-1, help="BN statistics partials: S > 0 fp32 atomics into S "
                     "zeroed slots, finalized inside the apply passes (no bn_final launches); 0 per-block rows + "
                     "bn_final (fixed order); -1 the library default")
+    ap.add_argument("--deterministic", action="store_true", help="BN statistics in row mode (= --bn_slots 0): every "
+                    "sum of the step in a fixed order, so a run repeats bit for bit (slot mode's fp32 atomics vary the "
+                    "summation order run to run; measured 13.57 vs 13.22 ms/step for ResNet-50 b128, "
+                    "profiles/resnet50_bn_slots_ab_r4.log)")
     ap.add_argument("--fold_bn", type=int, default=0, help="1: single-consumer relu batch norms applied inside the "
                     "consuming conv's operand loader (no bn_apply pass; 0: the separate pass; 2: 1x1 consumers only)")
     ap.add_argument("--lr", type=float, default=0.1)
@@ -78,6 +82,10 @@ def main(argv=None):
     ctx = D.init_from_env(use_gpu=True)
     spawn.check_world(a.gpus, ctx.world)
     dev = ctx.device
+    if a.deterministic:
+        if a.bn_slots > 0:
+            raise SystemExit("error: --deterministic is row mode (--bn_slots 0)")
+        a.bn_slots = 0
     if a.bn_slots >= 0:
         torch.ops.tfd.set_bn_part_slots(a.bn_slots)
     m = ResNet(a.depth, num_classes=1000, device=dev, seed=0, fuse_joins=bool(a.fuse_joins),
@@ -112,10 +120,21 @@ def main(argv=None):
     s = torch.cuda.Stream(dev)
     pool = torch.cuda.graph_pool_handle()  # every captured step (probes + the timed one) shares it
 
+    def agree(err, what):
+        """Every rank learns whether a local step failed on ANY rank before the next collective, so no
+        rank enters the step's collectives (RCCL / IPC / the probes' barriers) alone."""
+        if ctx.max_scalar(1.0 if err is not None else 0.0) > 0:
+            raise RuntimeError(f"{what} failed on at least one rank (here: {err!r})")
+
     def configure(mb):
         """Reducer with ``mb``-MB buckets, two eager steps, the step captured; returns run(k)."""
-        if comm is not None:
-            m.set_comm(comm, mb, small=small, small_mb=a.small_ipc_mb)
+        err = None
+        try:
+            if comm is not None:
+                m.set_comm(comm, mb, small=small, small_mb=a.small_ipc_mb)
+        except Exception as e:  # noqa: BLE001 - agreed below
+            err = e
+        agree(err, f"bucket reducer setup ({mb:g} MB)")
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for _ in range(2):
@@ -128,9 +147,13 @@ def main(argv=None):
                     out = m.train_step(x, y, lr=a.lr)
                 return out
             return run, None
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, pool=pool):
-            out_static = m.train_step(x, y, lr=a.lr)
+        graph, out_static, err = torch.cuda.CUDAGraph(), None, None
+        try:
+            with torch.cuda.graph(graph, pool=pool):
+                out_static = m.train_step(x, y, lr=a.lr)
+        except Exception as e:  # noqa: BLE001 - a capture fails locally (nothing is launched): agreed below
+            err = e
+        agree(err, f"step capture ({mb:g} MB buckets)")
         retain_graph(graph)  # never destroyed while the process runs (models/resnet.py retain_graph)
 
         def run(k):
@@ -204,7 +227,10 @@ def main(argv=None):
                        "mask_from_y": bool(a.mask_from_y), "relu_bits": bool(a.relu_bits),
                        "bn_bwd_stats": bool(a.bn_bwd_stats), "fold_bn": a.fold_bn, "masked_join": bool(a.masked_join),
                        "fuse_stem_pool": bool(a.fuse_stem_pool),
-                       "bn_slots": int(torch.ops.tfd.bn_part_slots())}}), flush=True)
+                       "bn_slots": int(torch.ops.tfd.bn_part_slots()),
+                       "bn_stats_mode": ("row: fixed summation order, bit-reproducible"
+                                         if int(torch.ops.tfd.bn_part_slots()) == 0 else
+                                         "slots: fp32 atomics, summation order varies run to run")}}), flush=True)
     for c in (comm if transport == "ipc" else None, small):
         if c is not None:
             if c.ipc.error():

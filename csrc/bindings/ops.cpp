@@ -39,6 +39,21 @@ void momentum_flat(at::Tensor p, c10::optional<at::Tensor> mom, at::Tensor g, c1
   sgd_apply(a, cur());
 }
 
+void roofline_stream(at::Tensor p, at::Tensor m, at::Tensor v, const at::Tensor& g, at::Tensor pbf,
+                     c10::optional<at::Tensor> x, int64_t blocks, int64_t unroll) {
+  const int64_t n = p.numel();
+  TORCH_CHECK(p.is_cuda() && p.scalar_type() == at::kFloat && p.is_contiguous() && n % 4 == 0, "roofline_stream: p");
+  TORCH_CHECK(m.numel() == n && v.numel() == n && g.numel() == n && pbf.numel() == n, "roofline_stream: sizes");
+  TORCH_CHECK(g.scalar_type() == at::kBFloat16 && pbf.scalar_type() == at::kBFloat16, "roofline_stream: bf16 g / pbf");
+  const int64_t nx = x ? x->numel() : 0;
+  TORCH_CHECK(nx % 4 == 0 && nx <= n && (!x || x->scalar_type() == at::kFloat), "roofline_stream: x");
+  stream_floor((float*)p.data_ptr(), (float*)m.data_ptr(), (float*)v.data_ptr(), (const uint16_t*)g.data_ptr(),
+               (uint16_t*)pbf.data_ptr(), x ? (const float*)x->data_ptr() : nullptr, n / 4, nx / 4, (int)blocks,
+               (int)unroll, cur());
+}
+
+void noop_op(int64_t blocks) { noop_launch((int)blocks, cur()); }
+
 at::Tensor to_bf16(const at::Tensor& x) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat, "to_bf16: fp32 GPU");
   auto xc = x.contiguous();
@@ -57,6 +72,11 @@ TORCH_LIBRARY(tfd, m) {
   m.def("momentum_flat(Tensor(a!) p, Tensor(b!)? mom, Tensor g, Tensor(d!)? pbf, float lr, float momentum, "
         "float weight_decay, bool nesterov, float grad_scale=1.0) -> ()");
   m.impl("momentum_flat", c10::DispatchKey::CUDA, &momentum_flat);
+  m.def("roofline_stream(Tensor(a!) p, Tensor(b!) m, Tensor(c!) v, Tensor g, Tensor(d!) pbf, Tensor? x, int blocks, "
+        "int unroll) -> ()");
+  m.impl("roofline_stream", c10::DispatchKey::CUDA, &roofline_stream);
+  m.def("noop(int blocks) -> ()");
+  m.impl("noop", c10::DispatchKey::CompositeExplicitAutograd, &noop_op);
   m.def("to_bf16(Tensor x) -> Tensor");
   m.impl("to_bf16", c10::DispatchKey::CUDA, &to_bf16);
 }

@@ -34,22 +34,22 @@ __device__ __forceinline__ uint32_t bn_relu2(uint32_t w, bn_f32x2 sc, bn_f32x2 s
   return __builtin_bit_cast(uint32_t, b);
 }
 
-// The statistics-partials mode (bn_slots(), see conv_kernels.h) as each kernel TU's own device copy:
-// internal linkage, so conv_nhwc.hip and norm.hip each hold one, uploaded by set_bn_slots.
-static __device__ int g_bn_slots_dev = TFD_BN_SLOTS;
-static inline hipError_t bn_slots_upload(int s) { return hipMemcpyToSymbol(HIP_SYMBOL(g_bn_slots_dev), &s, sizeof(int)); }
-
-// Row of a [rows][2][N] statistics-partials buffer that producer row block `row` writes: the block
-// itself (row mode), or slot row % S (slot mode).
-__device__ __forceinline__ int bn_part_row(int row) {
-  const int sl = g_bn_slots_dev;
-  return sl > 0 ? row % sl : row;
+// A statistics-partials destination as a kernel argument: the [rows][2][N] buffer and its mode
+// (bn_slots(), see conv_kernels.h) fixed at launch -- so a captured graph keeps the mode it was built
+// with, and every device of a process follows the host setting (there is no device-side copy).
+struct BnPart {
+  float* p = nullptr;
+  int slots = 0;  // 0: row mode (plain stores into row `row`); S > 0: fp32 atomics into slot row % S
+};
+// Row of the buffer that producer row block `row` writes: the block itself (row mode), or row % S.
+__device__ __forceinline__ int bn_part_row(const BnPart& part, int row) {
+  return part.slots > 0 ? row % part.slots : row;
 }
 // One producer block's column sums (a, b) of channel n: a plain store into its row, or fp32 atomic
 // adds into its slot of a zeroed buffer.
-__device__ __forceinline__ void put_bn_part(float* part, int row, int N, int n, float a, float b) {
-  float* p = part + (size_t)bn_part_row(row) * 2 * N;
-  if (g_bn_slots_dev > 0) {
+__device__ __forceinline__ void put_bn_part(const BnPart& part, int row, int N, int n, float a, float b) {
+  float* p = part.p + (size_t)bn_part_row(part, row) * 2 * N;
+  if (part.slots > 0) {
     atomicAdd(p + n, a);
     atomicAdd(p + N + n, b);
   } else {

@@ -92,9 +92,6 @@ void gemm_nt_bf16(const uint16_t* a, const uint16_t* bt, uint16_t* c, int M, int
 #endif
 int bn_slots();
 void set_bn_slots(int s);
-// per-TU device copies of the mode (conv_nhwc.hip / norm.hip), set by set_bn_slots
-void bn_slots_upload_conv(int s);
-void bn_slots_upload_norm(int s);
 // partials: fp32 workspace of bn_partials_size(M, C) floats for the partial pass (one row per block
 // in either mode; only producer epilogues use the slots).
 int bn_partials_size(int M, int C);

@@ -403,7 +403,7 @@ struct BnB {
 template <int BM, int BN, int WM, int WN, bool ADD, bool STATS, class RM = RowId, class BS = NoBnB>
 __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN / 16], char* smem, uint16_t* __restrict__ y,
                                              AddSrc add, int M, int N, int m0, int n0,
-                                             float* __restrict__ part, RM rowmap = RM{}, uint32_t ybytes = 0,
+                                             BnPart part, RM rowmap = RM{}, uint32_t ybytes = 0,
                                              BS bs = BS{}) {
   using E = LdsEpi<BM, BN, WM, WN>;
   constexpr bool BSTAT = BS::MODE >= 0;
@@ -583,13 +583,13 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_kernel(LA la, LB 
   f32x4 acc[BM / 32][BN / 32];
   gemm_mainloop<BM, BN, CBK, 2, 2, LA, LB, conv_rs<BM, BN>()>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
                                                        (bf16*)smem_raw, acc);
-  lds_epilogue<BM, BN, 2, 2, ADD, false>(acc, smem_raw, y, add, M, N, blockIdx.y * BM, blockIdx.x * BN, nullptr);
+  lds_epilogue<BM, BN, 2, 2, ADD, false>(acc, smem_raw, y, add, M, N, blockIdx.y * BM, blockIdx.x * BN, BnPart{});
 }
 
 // dgrad (+ add) whose epilogue also emits the BN-backward partials of its output (BnB above)
 template <int BM, int BN, class LA, class LB, bool ADD, class BS>
 __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_bnb_kernel(LA la, LB lb, uint16_t* y, AddSrc add,
-                                                                          int M, int N, int KD, float* part, BS bs) {
+                                                                          int M, int N, int KD, BnPart part, BS bs) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   f32x4 acc[BM / 32][BN / 32];
   gemm_mainloop<BM, BN, CBK, 2, 2, LA, LB, conv_rs<BM, BN>()>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_bnb_kernel(LA la,
 // forward BN needs no separate pass over the conv output. Fixed reduction order (deterministic).
 template <int BM, int BN, class LA, class LB>
 __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB lb, uint16_t* y, int M, int N, int KD,
-                                                         float* part) {
+                                                         BnPart part) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   constexpr int WM = 2, WN = 2, WTN = BN / WN, TN = WTN / 16;
 #if TFD_CONV_LDS_EPI
@@ -654,7 +654,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB
 // offset per phase by the caller, so the phases' row blocks stack)
 template <int BM, int BN, bool ADD, class BS = NoBnB>
 __global__ __launch_bounds__(256) TFD_CONV_ATTR void dgrad_phase_kernel(DgradPhaseA la, DgradPhaseB lb, uint16_t* dx,
-                                                                        AddSrc add, float* part = nullptr,
+                                                                        AddSrc add, BnPart part = BnPart{},
                                                                         BS bs = BS{}) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   f32x4 acc[BM / 32][BN / 32];
@@ -710,7 +710,8 @@ void launch_gemm_bf16_bnb(const LA& la, const LB& lb, uint16_t* y, AddSrc add, i
     attr = true;
   }
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, 1);
-  gemm_bf16_bnb_kernel<BM, BN, LA, LB, ADD, BS><<<grid, 256, sm, st>>>(la, lb, y, add, M, N, KD, part, bs);
+  gemm_bf16_bnb_kernel<BM, BN, LA, LB, ADD, BS><<<grid, 256, sm, st>>>(la, lb, y, add, M, N, KD, BnPart{part, bn_slots()},
+                                                                        bs);
 }
 
 template <int BM, int BN, class LA, class LB>
@@ -724,7 +725,7 @@ void launch_gemm_stats(const LA& la, const LB& lb, uint16_t* y, int M, int N, in
     attr = true;
   }
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, 1);
-  gemm_stats_kernel<BM, BN, LA, LB><<<grid, 256, sm, st>>>(la, lb, y, M, N, KD, part);
+  gemm_stats_kernel<BM, BN, LA, LB><<<grid, 256, sm, st>>>(la, lb, y, M, N, KD, BnPart{part, bn_slots()});
 }
 
 // same tile choice as dispatch(): 128x128 when that fills the chip
@@ -860,7 +861,7 @@ struct G256Epi {
 template <class C, bool ADD, bool STATS, class RM, class BS>
 __device__ __forceinline__ void g256_epilogue(f32x16 (&acc)[C::TM][C::TN], char* smem, uint16_t* __restrict__ y,
                                               AddSrc add, int M, int N, int m0, int n0,
-                                              float* __restrict__ part, RM rowmap, uint32_t ybytes, BS bs) {
+                                              BnPart part, RM rowmap, uint32_t ybytes, BS bs) {
   using E = G256Epi<C::BN>;
   constexpr bool BSTAT = BS::MODE >= 0;
   static_assert(!(STATS && BSTAT), "one statistics kind per epilogue");
@@ -994,10 +995,10 @@ constexpr int g256_smem() {
 }
 
 // bf16-output conv GEMM: part (STATS / BnB) gets one row per 256-row tile at part + tile_m * 2N (slot
-// mode: added into slot tile_m % TFD_BN_SLOTS)
+// mode: added into slot tile_m % part.slots)
 template <int BN, bool AKC, bool BKC, class SA, class SB, bool ADD, bool STATS, class RM, class BS>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void g256_conv_kernel(
-    SA sa, SB sb, uint16_t* y, AddSrc add, int M, int N, int KD, float* part, RM rm, uint32_t ybytes, BS bs,
+    SA sa, SB sb, uint16_t* y, AddSrc add, int M, int N, int KD, BnPart part, RM rm, uint32_t ybytes, BS bs,
     int tiles_m, int tiles_n) {
   using C = G256<BN, G256WM<BN>::v, AKC, BKC>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -1006,7 +1007,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   f32x16 acc[C::TM][C::TN];
   g256_mainloop<C>(sa, sb, tm * 256, tn * BN, 0, KD, smem_raw, acc);
   g256_epilogue<C, ADD, STATS, RM, BS>(acc, smem_raw, y, add, M, N, tm * 256, tn * BN,
-                                       part ? part + (size_t)bn_part_row(tm) * 2 * N : nullptr, rm, ybytes, bs);
+                                       BnPart{part.p ? part.p + (size_t)bn_part_row(part, tm) * 2 * N : nullptr,
+                                              part.slots}, rm, ybytes, bs);
 }
 
 // (plain template launchers, no generic lambdas: instantiating the kernel template from a host
@@ -1022,7 +1024,7 @@ void g256_launch_bf16_bn(const SA& sa, const SB& sb, uint16_t* y, AddSrc add, in
     attr = true;
   }
   const int tm = (M + 255) / 256, tn = (N + BN - 1) / BN;
-  k<<<tm * tn, 512, g256_smem<BN>(), st>>>(sa, sb, y, add, M, N, KD, part, rm, ybytes, bs, tm, tn);
+  k<<<tm * tn, 512, g256_smem<BN>(), st>>>(sa, sb, y, add, M, N, KD, BnPart{part, bn_slots()}, rm, ybytes, bs, tm, tn);
 }
 template <bool AKC, bool BKC, bool ADD, bool STATS, class SA, class SB, class RM = RowId, class BS = NoBnB>
 void g256_launch_bf16(const SA& sa, const SB& sb, uint16_t* y, AddSrc add, int M, int N, int KD, float* part,
@@ -1121,9 +1123,6 @@ void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t
   }
 }
 
-void bn_slots_upload_conv(int s) {
-  if (bn_slots_upload(s) != hipSuccess) throw std::runtime_error("set_bn_slots: device symbol upload failed");
-}
 
 int conv_fwd_stats_rows(const ConvShape& c, bool folded) {  // row blocks of the partials
   if (bn_slots() > 0) return bn_slots();
@@ -1189,7 +1188,7 @@ static void launch_phase(const DgradPhaseA& la, const DgradPhaseB& lb, uint16_t*
     attr = true;
   }
   dim3 grid((la.g.C + BN - 1) / BN, (la.g.M + BM - 1) / BM, 1);
-  dgrad_phase_kernel<BM, BN, ADD, BS><<<grid, 256, sm, st>>>(la, lb, dx, add, part, bs);
+  dgrad_phase_kernel<BM, BN, ADD, BS><<<grid, 256, sm, st>>>(la, lb, dx, add, BnPart{part, bn_slots()}, bs);
 }
 // BS != NoBnB: every phase also emits its BN-backward partial rows at part + (rows so far) * 2 * C
 // (callers ensure no phase is tap-less: those pixels would carry no partials). Returns the rows.

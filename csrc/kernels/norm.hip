@@ -857,15 +857,9 @@ void backward_apply(const uint16_t* dout, const uint16_t* out, const uint16_t* y
 
 static int g_bn_slots = TFD_BN_SLOTS;
 int bn_slots() { return g_bn_slots; }
-void bn_slots_upload_norm(int s) {
-  if (bn_slots_upload(s) != hipSuccess) throw std::runtime_error("set_bn_slots: device symbol upload failed");
-}
 void set_bn_slots(int s) {
   if (s < 0 || s > FIN_MAXS) throw std::runtime_error("set_bn_slots: 0 (row mode) or 1..8 slots");
-  if (s == g_bn_slots) return;
-  bn_slots_upload_norm(s);
-  bn_slots_upload_conv(s);
-  g_bn_slots = s;
+  g_bn_slots = s;  // read at launch time: every kernel takes the mode as an argument (BnPart, BnFin)
 }
 
 int bn_partials_size(int M, int C) {  // the partial pass's rows (row layout in either mode)

@@ -156,6 +156,48 @@ __global__ void copy_f32_kernel(float* __restrict__ d, const float* __restrict__
   for (int64_t i = (n4 << 2) + i0; i < n; i += stride) d[i] = s[i];
 }
 
+// ---- roofline probes (scripts/debug/roofline_probe.py) ----
+// The optimizer's byte floor: the same traffic as ApplyAdam over a flat buffer -- fp32 p, m, v read
+// and written in place, a bf16 gradient read, the bf16 shadow written (28 B per parameter) -- plus
+// an optional extra fp32 read stream (the conv weight-gradient slabs the one-GPU tail also reads),
+// with no math beyond adds. U float4 per lane in flight (grid-stride by U strides).
+template <int U>
+__global__ __launch_bounds__(kOptThreads) void stream_floor_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                                   float* __restrict__ v, const uint16_t* __restrict__ g,
+                                                                   uint16_t* __restrict__ pbf, const float* __restrict__ x,
+                                                                   int64_t n4, int64_t nx4) {
+  const int64_t stride = (int64_t)gridDim.x * kOptThreads;
+  for (int64_t base = (int64_t)blockIdx.x * kOptThreads + threadIdx.x; base < n4; base += stride * U) {
+    f32x4 pp[U], mm[U], vv[U];
+    uint2 gg[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + u * stride;
+      if (i < n4) {
+        pp[u] = reinterpret_cast<const f32x4*>(p)[i];
+        mm[u] = reinterpret_cast<const f32x4*>(m)[i];
+        vv[u] = reinterpret_cast<const f32x4*>(v)[i];
+        gg[u] = reinterpret_cast<const uint2*>(g)[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + u * stride;
+      if (i < n4) {
+        const float gs = __uint_as_float(gg[u].x << 16);
+        f32x4 q = pp[u] + gs;
+        if (i < nx4) q += reinterpret_cast<const f32x4*>(x)[i];
+        reinterpret_cast<f32x4*>(p)[i] = q;
+        reinterpret_cast<f32x4*>(m)[i] = mm[u] + gs;
+        reinterpret_cast<f32x4*>(v)[i] = vv[u] + gs;
+        reinterpret_cast<uint2*>(pbf)[i] = make_uint2(pack_bf2(q[0], q[1]), pack_bf2(q[2], q[3]));
+      }
+    }
+  }
+}
+// an empty kernel: the dependent-launch boundary floor of a chain of launches
+__global__ void noop_kernel() {}
+
 inline int blocks_for(int64_t n, int per_thread) {
   const int64_t b = (n / per_thread + kOptThreads - 1) / kOptThreads;
   return (int)(b < 1 ? 1 : (b > kOptMaxBlocks ? kOptMaxBlocks : b));
@@ -180,6 +222,15 @@ void adam_apply_ranges(const AdamArgs& a, int nr, const int64_t* beg, const int6
   r.tail_n = n[nr - 1] % 4;
   adam_ranges_kernel<<<blocks_for(r.pre4[nr] * 4, 4), kOptThreads, 0, s>>>(a, r);
 }
+void stream_floor(float* p, float* m, float* v, const uint16_t* g, uint16_t* pbf, const float* x, int64_t n4, int64_t nx4,
+                  int blocks, int unroll, hipStream_t s) {
+  if (blocks < 1) throw std::runtime_error("stream_floor: blocks >= 1");
+  if (unroll == 1) stream_floor_kernel<1><<<blocks, kOptThreads, 0, s>>>(p, m, v, g, pbf, x, n4, nx4);
+  else if (unroll == 2) stream_floor_kernel<2><<<blocks, kOptThreads, 0, s>>>(p, m, v, g, pbf, x, n4, nx4);
+  else if (unroll == 4) stream_floor_kernel<4><<<blocks, kOptThreads, 0, s>>>(p, m, v, g, pbf, x, n4, nx4);
+  else throw std::runtime_error("stream_floor: unroll 1, 2 or 4");
+}
+void noop_launch(int blocks, hipStream_t s) { noop_kernel<<<blocks < 1 ? 1 : blocks, 64, 0, s>>>(); }
 void sgd_apply(const SgdArgs& a, hipStream_t s) {
   sgd_kernel<<<blocks_for(a.n, 1), kOptThreads, 0, s>>>(a);
 }

@@ -152,6 +152,11 @@ struct SgdArgs {
   float* p; float* mom; const float* g; uint16_t* pbf; const uint16_t* gbf; int64_t n;
   float lr, momentum, weight_decay, grad_scale; int nesterov;
 };
+// roofline probes: the optimizer's byte floor (Adam's 28 B/param of traffic, optional extra fp32 read
+// stream of nx4 float4) and an empty launch (scripts/debug/roofline_probe.py)
+void stream_floor(float* p, float* m, float* v, const uint16_t* g, uint16_t* pbf, const float* x, int64_t n4, int64_t nx4,
+                  int blocks, int unroll, hipStream_t s);
+void noop_launch(int blocks, hipStream_t s);
 void sgd_apply(const SgdArgs& a, hipStream_t s);
 void cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
 void cast_bf16_f32(const uint16_t* x, float* y, int64_t n, float scale, hipStream_t s);

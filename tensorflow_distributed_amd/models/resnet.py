@@ -849,6 +849,36 @@ class ResNet:
         loss, correct = _SoftmaxXent.apply(logits, labels)
         return loss, correct
 
+    @torch.no_grad()
+    def evaluate(self, x, labels):
+        """Inference-mode pass (BN with the running statistics, no dropout of state): returns the
+        (sum of per-example losses, number correct) of the batch as floats -- the reference's accuracy
+        op (/root/reference/mnist_python_m.py:206-207,309-320) for this model family."""
+        ops = _ops()
+
+        def bn(y, L, relu, res=None):
+            if res is None:
+                return ops.bn_infer(y, L.gamma(), L.beta(), L.rmean, L.rvar, L.eps, relu)
+            z = ops.bn_infer(y, L.gamma(), L.beta(), L.rmean, L.rvar, L.eps, False).float() + res.float()
+            return (z.relu_() if relu else z).to(torch.bfloat16)
+
+        def conv(h, L):
+            return ops.conv2d_fwd(h, L.w(), L.stride, L.pad)
+
+        h = bn(conv(ops.pad_channels(x, 8), self.stem), self.stem_bn, True)
+        h, _ = ops.maxpool2d_fwd(h, 3, 2, 1)
+        for blk in self.blocks:
+            sc = bn(conv(h, blk["cd"]), blk["bd"], False) if "cd" in blk else h
+            t = bn(conv(h, blk["c1"]), blk["b1"], True)
+            if self.kind == "basic":
+                h = bn(conv(t, blk["c2"]), blk["b2"], True, sc)
+            else:
+                t = bn(conv(t, blk["c2"]), blk["b2"], True)
+                h = bn(conv(t, blk["c3"]), blk["b3"], True, sc)
+        logits = ops.linear_fwd(ops.avgpool_fwd(h), self.fc.w(), self.fc.bias())
+        loss_rows, correct, _ = ops.softmax_xent(logits.contiguous(), labels)
+        return float(loss_rows.float().sum().item()), int(round(float(correct.float().sum().item())))
+
     def train_step(self, x, labels, lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 1e-4):
         """fwd + bwd (bucketed all-reduce overlapped) + fused flat SGD-momentum. Returns loss tensor."""
         self.reducer.reset()
@@ -865,3 +895,67 @@ class ResNet:
         _ops().momentum_flat(self.fp.master, self.fp.momentum, self.reducer.reduced_grads(), self.fp.shadow, lr,
                              momentum, weight_decay, False, scale)
         return loss.detach()
+
+
+class ResNetRunner:
+    """The Supervisor's view of a ResNet (training/supervisor.py, the reference's Supervisor + Saver at
+    /root/reference/mnist_python_m.py:235-253): a global step and TF-named checkpoint tensors in the
+    MNIST runners' layout -- ``global_step``, every parameter under its layer name (conv weights HWIO,
+    fc [in, out]), its SGD-momentum slot as ``<name>/Momentum``, and each batch norm's running
+    statistics as ``<bn>/moving_mean`` / ``<bn>/moving_variance`` (TF's names)."""
+
+    def __init__(self, model: "ResNet"):
+        self.m = model
+        self._step = 0
+        self.ps_client = None
+
+    def global_step(self) -> int:
+        return self._step
+
+    def set_global_step(self, s: int) -> None:
+        self._step = int(s)
+
+    def params(self) -> torch.Tensor:
+        return self.m.fp.master
+
+    def train_step(self, x, labels, lr: float, **kw):
+        loss = self.m.train_step(x, labels, lr=lr, **kw)
+        self._step += 1
+        return loss
+
+    def state_dict_tf(self):
+        from collections import OrderedDict
+
+        import numpy as np
+
+        fp = self.m.fp
+        if fp.device.type == "cuda":
+            torch.cuda.synchronize(fp.device)
+        out = OrderedDict()
+        out["global_step"] = np.array(self._step, dtype=np.int64)
+        master, mom = fp.master.detach().cpu(), fp.momentum.detach().cpu()
+        for s in fp.specs:
+            out[s.name] = fp.view(master, s).numpy().copy()
+            out[s.name + "/Momentum"] = fp.view(mom, s).numpy().copy()
+        for bn in self.m.bns:
+            out[bn.name + "/moving_mean"] = bn.rmean.detach().cpu().numpy().copy()
+            out[bn.name + "/moving_variance"] = bn.rvar.detach().cpu().numpy().copy()
+        return out
+
+    def load_state_dict_tf(self, tensors) -> None:
+        import numpy as np
+
+        fp = self.m.fp
+        master = torch.zeros(fp.total)
+        mom = torch.zeros(fp.total)
+        for s in fp.specs:
+            fp.view(master, s).copy_(torch.from_numpy(np.asarray(tensors[s.name]).reshape(s.shape)))
+            if s.name + "/Momentum" in tensors:
+                fp.view(mom, s).copy_(torch.from_numpy(np.asarray(tensors[s.name + "/Momentum"]).reshape(s.shape)))
+        fp.master.copy_(master.to(fp.device))
+        fp.momentum.copy_(mom.to(fp.device))
+        fp.shadow.copy_(fp.master)
+        for bn in self.m.bns:
+            bn.rmean.copy_(torch.from_numpy(np.asarray(tensors[bn.name + "/moving_mean"])).to(bn.rmean.device))
+            bn.rvar.copy_(torch.from_numpy(np.asarray(tensors[bn.name + "/moving_variance"])).to(bn.rvar.device))
+        self._step = int(np.asarray(tensors.get("global_step", 0)))

@@ -116,6 +116,9 @@ def define_flags(task_index_default: int = 0, job_name_default: str = "ps") -> N
                    "generic bucket reducer (--model resnet*)")
     f.DEFINE_enum("model", "mnist_cnn", ["mnist_cnn", "resnet18", "resnet50"], "Model: the reference CNN, or the "
                   "synthetic-ImageNet ResNet family (BASELINE configs 4-5; trained by bench_resnet.py)")
+    f.DEFINE_integer("image_size", 224, "--model resnet*: synthetic image height = width")
+    f.DEFINE_boolean("bn_deterministic", False, "--model resnet*: batch-norm statistics in row mode (fixed summation "
+                     "order, bit-reproducible runs) instead of slot mode's fp32 atomics (~3 % faster, order varies)")
     f.DEFINE_boolean("ps_on_gpu", True, "Parameter-server modes (async, backup workers) with --num_gpus > 0: each "
                      "ps task keeps its variables, optimizer slots and accumulator on GPU task_index % num_gpus; "
                      "workers push gradients into its GPU mailbox and the ps writes fresh values straight into "
@@ -179,57 +182,105 @@ def _agree_gpu_ps() -> bool:
 
 
 def _resnet_worker(server, cluster, num_workers: int, is_chief: bool) -> int:
-    """``--model resnet18|resnet50``: the same cluster roles and stdout, training the synthetic-
-    ImageNet ResNet family (BASELINE configs 4-5) with synchronous DP -- bucketed bf16 gradient
-    all-reduce (``--bucket_mb``, default 8) overlapped with the backward, fused SGD-momentum (lr =
-    ``--learning_rate``). RCCL between GPUs; the IPC transport when workers share a GPU. Synthetic
-    data: one device-resident random 224x224x3 batch per worker. No checkpointing in this mode."""
+    """``--model resnet18|resnet50``: the same cluster roles, stdout and Supervisor services as the MNIST
+    path, training the synthetic-ImageNet ResNet family (BASELINE configs 4-5) with synchronous DP --
+    bucketed bf16 gradient all-reduce (``--bucket_mb``, default 8) overlapped with the backward, fused
+    SGD-momentum (lr = ``--learning_rate``). RCCL between GPUs; the IPC transport when workers share a
+    GPU. Synthetic data: one device-resident random ``--image_size``^2 x 3 batch per worker.
+
+    Supervisor (/root/reference/mnist_python_m.py:235-253): the chief restores the newest checkpoint
+    in ``--logdir`` or keeps its seeded init, then params, momentum, BN running statistics and the
+    global step go to every worker; timed checkpoints (``--save_model_secs``) in the MNIST layout
+    (models/resnet.ResNetRunner); after training an inference-mode validation pass over
+    ``--eval_batches`` synthetic batches and a final checkpoint."""
     import torch.distributed as dist
 
-    from ..models.resnet import ResNet
+    from ..models.resnet import ResNet, ResNetRunner
     from ..parallel.ipc import IpcCollectives, make_ipc_comm
     from ..parallel.transport import devices_shared, make_rccl
+    from .supervisor import Supervisor
 
     if not FLAGS.sync_replicas or FLAGS.num_gpus <= 0:
         raise ValueError("--model %s: synchronous data parallelism on GPUs only (--num_gpus > 0)" % FLAGS.model)
+    if FLAGS.bn_deterministic:
+        torch.ops.tfd.set_bn_part_slots(0)
     gpu = FLAGS.task_index % FLAGS.num_gpus
     torch.cuda.set_device(gpu)
     device = torch.device("cuda", gpu)
     depth = int(FLAGS.model.replace("resnet", ""))
     m = ResNet(depth, num_classes=1000, device=device, seed=FLAGS.seed)
+    runner = ResNetRunner(m)
     comm = None
+    grp = server.worker_group
     if num_workers > 1:
-        grp = server.worker_group
         if devices_shared(device, num_workers, grp):
             comm = IpcCollectives(make_ipc_comm(FLAGS.task_index, num_workers, gpu, m.fp.total, group=grp))
         else:
             comm = make_rccl(FLAGS.task_index, num_workers, gpu, group=grp, src=cluster.num_ps)
-        host = m.fp.master.detach().cpu()
-        dist.broadcast(host, cluster.num_ps, group=grp)  # chief init -> every worker
-        m.fp.master.copy_(host.to(device))
-        m.fp.shadow.copy_(m.fp.master)
     m.set_comm(comm, FLAGS.bucket_mb or 8.0)
-    g = torch.Generator(device=device).manual_seed(100 + FLAGS.task_index)
-    x = torch.randn(FLAGS.batch_size, 224, 224, 3, device=device, generator=g)
-    y = torch.randint(0, 1000, (FLAGS.batch_size,), device=device, generator=g, dtype=torch.int32)
+
+    def broadcast_fn():  # chief's (restored or seeded) state -> every worker (reference M6)
+        if num_workers <= 1:
+            return
+        for t in [m.fp.master, m.fp.momentum] + [b for bn in m.bns for b in (bn.rmean, bn.rvar)]:
+            host = t.detach().cpu()
+            dist.broadcast(host, cluster.num_ps, group=grp)
+            t.copy_(host.to(device))
+        m.fp.shadow.copy_(m.fp.master)
+        st = torch.tensor([runner.global_step()], dtype=torch.int64)
+        dist.broadcast(st, cluster.num_ps, group=grp)
+        runner.set_global_step(int(st.item()))
+
+    logdir = FLAGS.logdir or tempfile.mkdtemp()
+    sv = Supervisor(is_chief=is_chief, logdir=logdir, runner=runner, init_fn=lambda: None, broadcast_fn=broadcast_fn,
+                    save_model_secs=FLAGS.save_model_secs, save_summaries_secs=FLAGS.save_summaries_secs,
+                    recovery_wait_secs=1)
+    if is_chief:
+        print("Worker %d: Initializing session..." % FLAGS.task_index)
+    else:
+        print("Worker %d: Waiting for session to be initialized..." % FLAGS.task_index)
+    sys.stdout.flush()
+    sv.prepare_or_wait_for_session()
     print("Worker %d: Session initialization complete." % FLAGS.task_index)
+    S = FLAGS.image_size
+    g = torch.Generator(device=device).manual_seed(100 + FLAGS.task_index)
+    x = torch.randn(FLAGS.batch_size, S, S, 3, device=device, generator=g)
+    y = torch.randint(0, 1000, (FLAGS.batch_size,), device=device, generator=g, dtype=torch.int32)
     time_begin = time.time()
     print("Training begins @ %f" % time_begin)
-    step = 0
+    local_step = 0
+    step = runner.global_step()
     while step < FLAGS.train_steps:
-        loss = m.train_step(x, y, lr=FLAGS.learning_rate)
-        step += 1
+        loss = runner.train_step(x, y, lr=FLAGS.learning_rate)
+        step = runner.global_step()
+        local_step += 1
         if not FLAGS.quiet:
             print("%f: Worker %d: training step %d done (global step: %d) loss %.4f" % (
-                time.time(), FLAGS.task_index, step, step, float(loss)))
+                time.time(), FLAGS.task_index, local_step, step, float(loss)))
+        sv.on_step(step)
     torch.cuda.synchronize(device)
     time_end = time.time()
     print("Training ends @ %f" % time_end)
     el = time_end - time_begin
     print("Training elapsed time: %f s" % el)
-    print("Worker %d: %.1f images/sec (this worker)" % (FLAGS.task_index, FLAGS.batch_size * step / max(el, 1e-9)))
+    print("Worker %d: %.1f images/sec (this worker)" % (FLAGS.task_index, FLAGS.batch_size * local_step / max(el, 1e-9)))
+    # validation (reference: 5 x 1000 images, mnist_python_m.py:309-320): synthetic batches of at most
+    # --batch_size images through the inference-mode network (running BN statistics)
+    gv = torch.Generator(device=device).manual_seed(7 + FLAGS.task_index)
+    accs = []
+    nb = min(FLAGS.eval_batch_size, FLAGS.batch_size)
+    for _ in range(FLAGS.eval_batches):
+        vx = torch.randn(nb, S, S, 3, device=device, generator=gv)
+        vy = torch.randint(0, 1000, (nb,), device=device, generator=gv, dtype=torch.int32)
+        _, correct = m.evaluate(vx, vy)
+        print("After %d training step(s)", FLAGS.train_steps)  # verbatim reference line (quirk Q3)
+        print("Accuracy : %f" % (correct / float(nb)))
+        accs.append(correct / float(nb))
+    print("Mean Accuracy : %f" % (sum(accs) / len(accs) if accs else float("nan")))
+    sys.stdout.flush()
     if num_workers > 1:
-        dist.barrier(group=server.worker_group)
+        dist.barrier(group=grp)
+    sv.stop(save=True)
     if isinstance(comm, IpcCollectives):
         if comm.ipc.error():
             raise RuntimeError("IPC collective barrier timed out")

@@ -75,3 +75,45 @@ def test_event_file_roundtrip(tmp_path):
     assert S.read_scalars(w.path) == [(7, "global_step/sec", 3.5), (8, "loss", 0.25), (8, "accuracy", 0.5)]
     recs = list(S.read_records(w.path))
     assert b"brain.Event:2" in recs[0]
+
+
+def test_resnet_supervisor_checkpoint_roundtrip(tmp_path):
+    """The ResNet mode's Supervisor state (models/resnet.ResNetRunner, dist_main --model resnet*) on CPU:
+    params (HWIO convs), SGD-momentum slots, BN running statistics and global_step go through the
+    Saver's V2 bundle in the logdir layout and restore into a freshly initialised model bit for bit;
+    the chief's prepare_or_wait_for_session finds the checkpoint and resumes from its step."""
+    import torch
+
+    from tensorflow_distributed_amd.models.resnet import ResNet, ResNetRunner
+    from tensorflow_distributed_amd.training.checkpoint import latest_checkpoint
+    from tensorflow_distributed_amd.training.supervisor import Supervisor
+
+    cpu = torch.device("cpu")
+    a = ResNetRunner(ResNet(18, num_classes=16, device=cpu, seed=1, width=16))
+    g = torch.Generator().manual_seed(5)
+    a.m.fp.master.copy_(torch.randn(a.m.fp.total, generator=g))
+    a.m.fp.momentum.copy_(torch.randn(a.m.fp.total, generator=g))
+    for bn in a.m.bns:
+        bn.rmean.copy_(torch.randn(bn.c, generator=g))
+        bn.rvar.copy_(torch.rand(bn.c, generator=g) + 0.5)
+    a.set_global_step(17)
+    sd = a.state_dict_tf()
+    assert sd["layer1.0.conv1"].shape == (3, 3, 16, 16) and sd["fc"].shape == (128, 16)
+    assert "layer1.0.bn1/moving_mean" in sd and "layer1.0.conv1/Momentum" in sd
+    sv = Supervisor(is_chief=True, logdir=str(tmp_path), runner=a, init_fn=lambda: None, summary_writer=False)
+    path = sv.save(17)
+    assert latest_checkpoint(str(tmp_path)) == path and path.endswith("model.ckpt-17")
+    b = ResNetRunner(ResNet(18, num_classes=16, device=cpu, seed=2, width=16))
+    inits = []
+    sv2 = Supervisor(is_chief=True, logdir=str(tmp_path), runner=b, init_fn=lambda: inits.append(1),
+                     summary_writer=False, log=lambda *_: None)
+    sv2.prepare_or_wait_for_session()
+    assert sv2.restored_from == path and not inits and b.global_step() == 17
+    fa, fb = a.m.fp, b.m.fp
+    for sp in fa.specs:  # (the flat buffers' 64-element slot padding is not state)
+        for buf in ("master", "momentum"):
+            assert torch.equal(fb.view(getattr(fb, buf), fb.by_name[sp.name]), fa.view(getattr(fa, buf), sp)), sp.name
+        assert torch.equal(fb.w(sp.name), fa.p(sp.name).to(torch.bfloat16)), sp.name
+    for x, y in zip(a.m.bns, b.m.bns):
+        assert torch.equal(x.rmean, y.rmean) and torch.equal(x.rvar, y.rvar)
+    sv2.stop(save=False)

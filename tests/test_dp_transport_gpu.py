@@ -367,14 +367,26 @@ def test_bench_forced_dp_world1_rccl(cuda, sfb, zero):
 
 
 def test_dist_main_resnet18_two_workers_one_gpu(tmp_path):
-    """--model resnet18 through the same cluster roles: sync DP (bucketed all-reduce over IPC,
-    both workers on gpu:0), reference step lines, clean exit."""
+    """--model resnet18 through the same cluster roles: sync DP (bucketed all-reduce over IPC, both
+    workers on gpu:0), reference step lines, the Supervisor's services -- a checkpoint in the logdir,
+    the inference-mode validation lines, and a second run that resumes from the checkpoint's global
+    step -- and a clean exit."""
     from tensorflow_distributed_amd import launch
+    from tensorflow_distributed_amd.training.checkpoint import latest_checkpoint
 
-    args = ["--num_gpus=1", "--model=resnet18", "--train_steps=3", "--batch_size=8", "--bucket_mb=2",
-            "--synthetic_data", "--data_dir=/nonexistent", f"--logdir={tmp_path}"]
-    r = launch.launch(1, 2, args, echo=False, timeout_s=300)
+    args = ["--num_gpus=1", "--model=resnet18", "--batch_size=8", "--bucket_mb=2", "--image_size=64",
+            "--eval_batches=2", "--synthetic_data", "--data_dir=/nonexistent", f"--logdir={tmp_path}"]
+    r = launch.launch(1, 2, args + ["--train_steps=3"], echo=False, timeout_s=300)
     assert r["ok"], r["outputs"]
     for w in ("worker:0", "worker:1"):
         out = "".join(v for k, v in r["outputs"].items() if k.startswith(w + "#"))
         assert "training step 3 done (global step: 3)" in out and "images/sec" in out, out
+        assert out.count("Accuracy : ") == 3 and "Mean Accuracy : " in out, out
+    assert latest_checkpoint(str(tmp_path)).endswith("model.ckpt-3")
+    r = launch.launch(1, 2, args + ["--train_steps=5"], echo=False, timeout_s=300)
+    assert r["ok"], r["outputs"]
+    w0 = "".join(v for k, v in r["outputs"].items() if k.startswith("worker:0#"))
+    w1 = "".join(v for k, v in r["outputs"].items() if k.startswith("worker:1#"))
+    assert "Restored from checkpoint" in w0 and "training step 2 done (global step: 5)" in w0, w0
+    assert "training step 2 done (global step: 5)" in w1, w1
+    assert latest_checkpoint(str(tmp_path)).endswith("model.ckpt-5")
