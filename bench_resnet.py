@@ -75,7 +75,7 @@ def main(argv=None):
     import torch
 
     from tensorflow_distributed_amd import _native
-    from tensorflow_distributed_amd.models.resnet import ResNet, retain_graph
+    from tensorflow_distributed_amd.models.resnet import ResNet
     from tensorflow_distributed_amd.parallel import dist as D
 
     _native.require()
@@ -118,7 +118,7 @@ def main(argv=None):
     x = torch.randn(a.batch_size, a.image, a.image, 3, device=dev, generator=g)
     y = torch.randint(0, 1000, (a.batch_size,), device=dev, generator=g, dtype=torch.int32)
     s = torch.cuda.Stream(dev)
-    pool = torch.cuda.graph_pool_handle()  # every captured step (probes + the timed one) shares it
+    pool = torch.cuda.graph_pool_handle()  # every captured step (probes + the timed one) shares one pool
 
     def agree(err, what):
         """Every rank learns whether a local step failed on ANY rank before the next collective, so no
@@ -134,7 +134,7 @@ def main(argv=None):
                 m.set_comm(comm, mb, small=small, small_mb=a.small_ipc_mb)
         except Exception as e:  # noqa: BLE001 - agreed below
             err = e
-        agree(err, f"bucket reducer setup ({mb:g} MB)")
+        agree(err, f"bucket reducer setup ({mb} MB)")
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for _ in range(2):
@@ -153,8 +153,7 @@ def main(argv=None):
                 out_static = m.train_step(x, y, lr=a.lr)
         except Exception as e:  # noqa: BLE001 - a capture fails locally (nothing is launched): agreed below
             err = e
-        agree(err, f"step capture ({mb:g} MB buckets)")
-        retain_graph(graph)  # never destroyed while the process runs (models/resnet.py retain_graph)
+        agree(err, f"step capture ({mb} MB buckets)")
 
         def run(k):
             for _ in range(k):

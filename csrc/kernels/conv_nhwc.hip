@@ -543,41 +543,25 @@ struct Tile {
   static constexpr int WM = 2, WN = 2, BK = 64;
 };
 
-#ifndef TFD_CONV_RS  // register stages of the conv/dense GEMM core (global-load prefetch depth)
-#define TFD_CONV_RS 1
-#endif
-#ifndef TFD_CONV_RS_SMALL  // register stages for tiles of at most 64x64 (fewer accumulator registers)
-#define TFD_CONV_RS_SMALL TFD_CONV_RS
-#endif
+// One register stage (global-load prefetch depth) and a 64-deep K-tile for every conv GEMM tile: two
+// stages doubled the 128x128 tile's accumulators to 368 VGPR+AGPR (one wave per SIMD, ResNet-50
+// 18.9 -> 21.6 ms), BK = 32 halved the LDS but doubled the barriers (20.8 ms) -- docs/DESIGN.md §5,
+// profiles/resnet_small_tile_rs_ab_r2.log.
 template <int BM, int BN>
-constexpr int conv_rs() { return BM * BN <= 64 * 64 ? TFD_CONV_RS_SMALL : TFD_CONV_RS; }
-#ifndef TFD_CONV_BK  // K-tile of the conv/dense GEMM core (LDS per block: 2 x (BM + BN) x (BK + pad) x 2 B)
-#define TFD_CONV_BK 64
-#endif
-#ifndef TFD_CONV_WPE  // > 0: amdgpu_waves_per_eu lower bound (register budget) of the GEMM kernels
-#define TFD_CONV_WPE 0
-#endif
-#if TFD_CONV_WPE > 0
-#define TFD_CONV_ATTR __attribute__((amdgpu_waves_per_eu(TFD_CONV_WPE)))
-#else
-#define TFD_CONV_ATTR
-#endif
-constexpr int CBK = TFD_CONV_BK;
+constexpr int conv_rs() { return 1; }
+constexpr int CBK = 64;
 template <int BM, int BN, class LA, class LB, class EPI>
-__global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_kernel(LA la, LB lb, EPI epi, int kchunk, int KD) {
+__global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int kchunk, int KD) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int kb = blockIdx.z * kchunk, ke = min(KD, kb + kchunk);
   gemm_block<BM, BN, CBK, 2, 2, LA, LB, EPI, conv_rs<BM, BN>()>(la, lb, epi, blockIdx.y * BM, blockIdx.x * BN, kb, ke,
                                                          (bf16*)smem_raw);
 }
 
-#ifndef TFD_CONV_LDS_EPI  // 1: bf16-output conv GEMMs (fwd, fwd+stats, dgrad) use the LDS-staged epilogue
-#define TFD_CONV_LDS_EPI 1
-#endif
 
 // bf16-output GEMM with the LDS-staged epilogue: Y = A B (+ add), no split-K.
 template <int BM, int BN, class LA, class LB, bool ADD>
-__global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_kernel(LA la, LB lb, uint16_t* y, AddSrc add,
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(LA la, LB lb, uint16_t* y, AddSrc add,
                                                                       int M, int N, int KD) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   f32x4 acc[BM / 32][BN / 32];
@@ -588,7 +572,7 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_kernel(LA la, LB 
 
 // dgrad (+ add) whose epilogue also emits the BN-backward partials of its output (BnB above)
 template <int BM, int BN, class LA, class LB, bool ADD, class BS>
-__global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_bnb_kernel(LA la, LB lb, uint16_t* y, AddSrc add,
+__global__ __launch_bounds__(256) void gemm_bf16_bnb_kernel(LA la, LB lb, uint16_t* y, AddSrc add,
                                                                           int M, int N, int KD, BnPart part, BS bs) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   f32x4 acc[BM / 32][BN / 32];
@@ -602,58 +586,21 @@ __global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_bf16_bnb_kernel(LA la,
 // go to part[blockIdx.y][2][N] -- the [nblk][2][C] layout bn_final_kernel reduces -- so the
 // forward BN needs no separate pass over the conv output. Fixed reduction order (deterministic).
 template <int BM, int BN, class LA, class LB>
-__global__ __launch_bounds__(256) TFD_CONV_ATTR void gemm_stats_kernel(LA la, LB lb, uint16_t* y, int M, int N, int KD,
+__global__ __launch_bounds__(256) void gemm_stats_kernel(LA la, LB lb, uint16_t* y, int M, int N, int KD,
                                                          BnPart part) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  constexpr int WM = 2, WN = 2, WTN = BN / WN, TN = WTN / 16;
-#if TFD_CONV_LDS_EPI
-  (void)TN;
+  constexpr int WM = 2, WN = 2;
   f32x4 acc[BM / 32][BN / 32];
   gemm_mainloop<BM, BN, CBK, WM, WN, LA, LB, conv_rs<BM, BN>()>(la, lb, blockIdx.y * BM, blockIdx.x * BN, 0, KD,
                                                          (bf16*)smem_raw, acc);
   lds_epilogue<BM, BN, WM, WN, false, true>(acc, smem_raw, y, nullptr, M, N, blockIdx.y * BM, blockIdx.x * BN, part);
-#else
-  float s[TN], q[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) { s[j] = 0.f; q[j] = 0.f; }
-  StoreBf16Stats<TN> epi{y, M, N, s, q};
-  gemm_block<BM, BN, CBK, WM, WN, LA, LB, StoreBf16Stats<TN>, conv_rs<BM, BN>()>(la, lb, epi, blockIdx.y * BM,
-                                                                          blockIdx.x * BN, 0, KD, (bf16*)smem_raw);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wm = wid / WN, wn = wid % WN;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {  // the 4 row groups of the MFMA C layout (lane >> 4)
-    s[j] += __shfl_xor(s[j], 16, 64);
-    s[j] += __shfl_xor(s[j], 32, 64);
-    q[j] += __shfl_xor(q[j], 16, 64);
-    q[j] += __shfl_xor(q[j], 32, 64);
-  }
-  __syncthreads();  // the GEMM's LDS tiles are dead: reuse them for the cross-wave sum
-  float* red = reinterpret_cast<float*>(smem_raw);  // [WM][BN][2]
-  if (lane < 16) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * WTN + 16 * j + lane;
-      red[(wm * BN + col) * 2] = s[j];
-      red[(wm * BN + col) * 2 + 1] = q[j];
-    }
-  }
-  __syncthreads();
-  for (int c = tid; c < BN; c += 256) {
-    const int n = blockIdx.x * BN + c;
-    if (n >= N) continue;
-    float a = 0.f, b = 0.f;
-#pragma unroll
-    for (int w = 0; w < WM; ++w) { a += red[(w * BN + c) * 2]; b += red[(w * BN + c) * 2 + 1]; }
-    put_bn_part(part, blockIdx.y, N, n, a, b);
-  }
-#endif
 }
 
 // one phase of a strided dgrad: Y rows scattered to the phase's pixels (+ add)
 // BS (BnB<MODE>): the phase's rows of the BN-backward partials go to part[blockIdx.y] (part is
 // offset per phase by the caller, so the phases' row blocks stack)
 template <int BM, int BN, bool ADD, class BS = NoBnB>
-__global__ __launch_bounds__(256) TFD_CONV_ATTR void dgrad_phase_kernel(DgradPhaseA la, DgradPhaseB lb, uint16_t* dx,
+__global__ __launch_bounds__(256) void dgrad_phase_kernel(DgradPhaseA la, DgradPhaseB lb, uint16_t* dx,
                                                                         AddSrc add, BnPart part = BnPart{},
                                                                         BS bs = BS{}) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -682,7 +629,7 @@ __global__ __launch_bounds__(256) void dgrad_empty_phase_kernel(uint16_t* __rest
 template <int BM, int BN, class LA, class LB>
 constexpr int stats_smem() {
   constexpr int g = GemmSmem<BM, BN, CBK, LA, LB>::BYTES;
-  return TFD_CONV_LDS_EPI && LdsEpi<BM, BN, 2, 2>::BYTES > g ? LdsEpi<BM, BN, 2, 2>::BYTES : g;
+  return LdsEpi<BM, BN, 2, 2>::BYTES > g ? LdsEpi<BM, BN, 2, 2>::BYTES : g;
 }
 
 template <int BM, int BN, class LA, class LB, bool ADD>
@@ -732,15 +679,12 @@ void launch_gemm_stats(const LA& la, const LB& lb, uint16_t* y, int M, int N, in
 bool use_big_tiles(int M, int N) { return (long)((M + 127) / 128) * ((N + 127) / 128) >= 256 && N >= 128; }
 
 // bf16-output tile (fwd, fwd + stats, dgrad): 128x128 when that fills the chip; for a 64-column
-// output (the C = 64 stage of a ResNet) 128x64 when that does, else 64x64. TFD_TALL_TILES=0: no
-// 128x64 (the round-2 first pass).
-#ifndef TFD_TALL_TILES
-#define TFD_TALL_TILES 1
-#endif
+// output (the C = 64 stage of a ResNet) 128x64 when that does, else 64x64 (the 128x64 arm:
+// profiles/resnet_tall_tiles_ab_r2.log, resnet50_tall_tiles_ab_r4.log).
 enum OutTile { OT64, OT128x64, OT128 };
 OutTile out_tile(int M, int N) {
   if (use_big_tiles(M, N)) return OT128;
-  if (TFD_TALL_TILES && N == 64 && (long)((M + 127) / 128) >= 256) return OT128x64;
+  if (N == 64 && (long)((M + 127) / 128) >= 256) return OT128x64;
   return OT64;
 }
 int out_tile_rows(int M, int N) { return out_tile(M, N) == OT64 ? (M + 63) / 64 : (M + 127) / 128; }
@@ -1099,7 +1043,6 @@ static BnReluArgs bn_relu_args(const ConvShape& c, const BnReluIn* act) {
 void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, hipStream_t st,
               const BnReluIn* act) {
   const int M = c.N * c.Ho() * c.Wo(), KD = c.R * c.S * c.C;
-  StoreBf16 epi{y, M, c.K};
   DenseX<false> lb{w, c.K, c.K, KD};
   if (act) {  // the 128-row core: its loaders stage through registers, where the transform happens
     const BnReluArgs a = bn_relu_args(c, act);
@@ -1112,15 +1055,8 @@ void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t
     else g256_launch_bf16<true, false, false, false>(FwdA{x, make_geo(c, M, KD)}, lb, y, nullptr, M, c.K, KD, nullptr, st);
     return;
   }
-  if (is_pointwise(c)) {
-    DenseX<true> la{x, c.C, M, c.C};
-    if (TFD_CONV_LDS_EPI) dispatch_bf16(la, lb, y, nullptr, M, c.K, KD, st);
-    else dispatch(la, lb, epi, M, c.K, KD, 1, st);
-  } else {
-    FwdA la{x, make_geo(c, M, KD)};
-    if (TFD_CONV_LDS_EPI) dispatch_bf16(la, lb, y, nullptr, M, c.K, KD, st);
-    else dispatch(la, lb, epi, M, c.K, KD, 1, st);
-  }
+  if (is_pointwise(c)) dispatch_bf16(DenseX<true>{x, c.C, M, c.C}, lb, y, nullptr, M, c.K, KD, st);
+  else dispatch_bf16(FwdA{x, make_geo(c, M, KD)}, lb, y, nullptr, M, c.K, KD, st);
 }
 
 
@@ -1128,7 +1064,7 @@ int conv_fwd_stats_rows(const ConvShape& c, bool folded) {  // row blocks of the
   if (bn_slots() > 0) return bn_slots();
   const int M = c.N * c.Ho() * c.Wo();
   if (!folded && use_g256(M, c.K)) return (M + 255) / 256;
-  return TFD_CONV_LDS_EPI ? out_tile_rows(M, c.K) : (use_big_tiles(M, c.K) ? (M + 127) / 128 : (M + 63) / 64);
+  return out_tile_rows(M, c.K);
 }
 
 void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t* y, float* part,
@@ -1140,7 +1076,7 @@ void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, ui
     else g256_launch_bf16<true, false, false, true>(FwdA{x, make_geo(c, M, KD)}, lb, y, nullptr, M, c.K, KD, part, st);
     return;
   }
-  const OutTile t = TFD_CONV_LDS_EPI ? out_tile(M, c.K) : (use_big_tiles(M, c.K) ? OT128 : OT64);
+  const OutTile t = out_tile(M, c.K);
   auto go = [&](const auto& la) {
     using LA = std::decay_t<decltype(la)>;
     if (t == OT128) launch_gemm_stats<128, 128, LA, DenseX<false>>(la, lb, y, M, c.K, KD, part, st);
@@ -1173,9 +1109,6 @@ static void conv_dgrad_impl(const ConvShape& c, const uint16_t* dy, const uint16
   }
 }
 
-#ifndef TFD_DGRAD_PHASES  // 1: strided dgrads as one dense GEMM per output phase (dgrad_strided)
-#define TFD_DGRAD_PHASES 1
-#endif
 template <int BM, int BN, bool ADD, class BS = NoBnB>
 static void launch_phase(const DgradPhaseA& la, const DgradPhaseB& lb, uint16_t* dx, const AddSrc& add,
                          hipStream_t st, float* part = nullptr, const BS& bs = BS{}) {
@@ -1261,12 +1194,12 @@ static AddSrc make_add(const ConvShape& c, const uint16_t* add, const uint8_t* a
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                 const uint16_t* add, const uint8_t* add_bits, bool add_sub2) {
   const int M = c.N * c.H * c.W;
-  if (add_bits && (!add || c.stride != 1 || !TFD_CONV_LDS_EPI))
+  if (add_bits && (!add || c.stride != 1))
     throw std::runtime_error("conv_dgrad: a relu-masked add operand needs a stride-1 dgrad");
-  if (add_sub2 && (!add || !TFD_CONV_LDS_EPI)) throw std::runtime_error("conv_dgrad: stride-2 add operand without add");
+  if (add_sub2 && !add) throw std::runtime_error("conv_dgrad: stride-2 add operand without add");
   if (add_bits && add_sub2) throw std::runtime_error("conv_dgrad: one add-operand form at a time");
   const AddSrc aa = make_add(c, add, add_bits, add_sub2);
-  if (TFD_CONV_LDS_EPI && TFD_DGRAD_PHASES && c.stride > 1) {
+  if (c.stride > 1) {  // one dense GEMM per output phase (profiles/resnet50_dgrad_phases_ab_r2.log)
     dgrad_strided(c, dy, w, dx, aa, st);
     return;
   }
@@ -1284,27 +1217,20 @@ void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint1
     }
     return;
   }
-  if (TFD_CONV_LDS_EPI) {
-    const int KD = c.R * c.S * c.K;
-    if (is_pointwise(c)) {
-      DenseX<true> la{dy, c.K, M, c.K};
-      DenseX<true> lb{w, c.K, c.C, c.K};
-      dispatch_bf16(la, lb, dx, aa, M, c.C, KD, st);
-    } else {
-      Geo g = make_geo(c, M, KD);
-      dispatch_bf16(DgradA{dy, g}, DgradB{w, g}, dx, aa, M, c.C, KD, st);
-    }
-    return;
+  const int KD = c.R * c.S * c.K;
+  if (is_pointwise(c)) {
+    dispatch_bf16(DenseX<true>{dy, c.K, M, c.K}, DenseX<true>{w, c.K, c.C, c.K}, dx, aa, M, c.C, KD, st);
+  } else {
+    Geo g = make_geo(c, M, KD);
+    dispatch_bf16(DgradA{dy, g}, DgradB{w, g}, dx, aa, M, c.C, KD, st);
   }
-  if (add) conv_dgrad_impl(c, dy, w, AddStoreBf16{dx, add, M, c.C}, st);
-  else conv_dgrad_impl(c, dy, w, StoreBf16{dx, M, c.C}, st);
 }
 
 // stride 1, or a strided dgrad by output phases none of which is tap-less (every input pixel is in
 // some phase GEMM, e.g. ResNet v1.5's 3x3 stride-2 convs)
 bool conv_dgrad_bn_supported(const ConvShape& c) {
-  if (!TFD_CONV_LDS_EPI || c.C % 8 != 0) return false;
-  return c.stride == 1 || (TFD_DGRAD_PHASES && c.R >= c.stride && c.S >= c.stride);
+  if (c.C % 8 != 0) return false;
+  return c.stride == 1 || (c.R >= c.stride && c.S >= c.stride);
 }
 static int bf16_out_rows(int M, int N) { return use_g256(M, N) ? (M + 255) / 256 : out_tile_rows(M, N); }
 int conv_dgrad_bn_rows(const ConvShape& c) {
@@ -1357,27 +1283,19 @@ void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, ui
 // Weight-gradient tile: dW is [R*S*C][K] with a very long reduction over pixels (split-K), so the
 // block's operand traffic per MFMA decides its speed. 64x64 tiles stream 32 FLOP per staged byte,
 // 128x64 43 and 128x128 64; the wide tiles are used whenever dW has the rows/columns for them
-// (TFD_WGRAD_TILES=0: always 64x64, the round-1 choice).
-#ifndef TFD_WGRAD_TILES
-#define TFD_WGRAD_TILES 1
-#endif
+// (profiles/resnet50_wgrad_tiles_ab_r2.log: the 3x3 weight gradients 24-31 % faster than 64x64).
 enum WgTile { WG64x64, WG128x64, WG128x128 };
 WgTile wgrad_tile(const ConvShape& c) {
   const int MT = c.R * c.S * c.C;
-  if (!TFD_WGRAD_TILES || MT < 128) return WG64x64;
+  if (MT < 128) return WG64x64;
   if (c.K % 128 == 0) return WG128x128;
   return WG128x64;
 }
 
-#ifndef TFD_WGRAD_MINPX  // fewest pixels (K of the weight-gradient GEMM) per split
-#define TFD_WGRAD_MINPX 2048
-#endif
-#ifndef TFD_WGRAD_BLOCKS_SMALL  // the same for 64x64 tiles (short-MT 1x1 weight gradients)
-#define TFD_WGRAD_BLOCKS_SMALL 512
-#endif
-#ifndef TFD_WGRAD_BLOCKS  // (tile x split) blocks the split count aims for
-#define TFD_WGRAD_BLOCKS 512
-#endif
+// split-K of a weight gradient: about kWgradBlocks (tile x split) blocks, each split keeping at least
+// kWgradMinPx pixels of K (1,024: 13.79 vs 13.80 ms, 512: 13.90, profiles/resnet50_wgrad_minpx_ab_r3.log;
+// the 64x64-tile target: profiles/resnet50_wgrad_small_splits_ab_r4.log)
+constexpr int kWgradMinPx = 2048, kWgradBlocks = 512, kWgradBlocksSmall = 512;
 // weight gradients on the 256-row core: mode 2 only (the A/B switch)
 static bool use_g256_wgrad(const ConvShape& c) {
   const int mode = g256_mode(), P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
@@ -1393,14 +1311,14 @@ static int g256_wgrad_splits(const ConvShape& c) {
 }
 int conv_wgrad_splits(const ConvShape& c, bool folded) {
   if (!folded && use_g256_wgrad(c)) return g256_wgrad_splits(c);
-  // enough (tile x split) blocks to fill the chip; each split keeps >= TFD_WGRAD_MINPX pixels of K
+  // enough (tile x split) blocks to fill the chip; each split keeps >= kWgradMinPx pixels of K
   const int P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
   const WgTile t = wgrad_tile(c);
   const int bm = t == WG64x64 ? 64 : 128, bn = t == WG128x128 ? 128 : 64;
   const long tiles = (long)((MT + bm - 1) / bm) * ((c.K + bn - 1) / bn);
-  const long target = t == WG64x64 ? TFD_WGRAD_BLOCKS_SMALL : TFD_WGRAD_BLOCKS;
+  const long target = t == WG64x64 ? kWgradBlocksSmall : kWgradBlocks;
   int s = (int)std::max<long>(1, target / std::max<long>(1, tiles));
-  s = std::min(s, std::max(1, P / TFD_WGRAD_MINPX));
+  s = std::min(s, std::max(1, P / kWgradMinPx));
   return s;
 }
 

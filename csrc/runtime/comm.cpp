@@ -43,38 +43,59 @@ at::Tensor RcclComm::unique_id() {
   return t;
 }
 
-RcclComm::RcclComm(const at::Tensor& uid, int64_t world, int64_t rank, int64_t device)
-    : world_(world), rank_(rank), device_(device) {
-  TORCH_CHECK(uid.numel() == NCCL_UNIQUE_ID_BYTES && uid.scalar_type() == at::kByte, "bad unique id");
-  ncclUniqueId id;
-  auto c = uid.contiguous().cpu();
-  std::memcpy(&id, c.data_ptr(), NCCL_UNIQUE_ID_BYTES);
-  TORCH_CHECK(hipSetDevice((int)device) == hipSuccess, "hipSetDevice failed");
-  rccl_check(ncclCommInitRank(&comm_, (int)world, id, (int)rank), "CommInitRank");
-}
-
-// A collective captured into a hipGraph stays tied to its communicator's resources until that
-// graph is destroyed, and Python frees a job's objects in no fixed order: a communicator dropped
-// before a graph that captured it (a test's locals, a model rebuilt between bucket-size probes)
-// left the later graph teardown / replay working on a destroyed communicator -- the in-suite
-// segfault inside CUDAGraph.replay of round 3 (profiles/pytest_gpu_r3_segv.log). The destructor
-// therefore only retires the handle; retired communicators are destroyed by reap(), which a caller
-// runs once no graph that captured them exists (or never: the process exit releases them).
 namespace {
 std::mutex g_retired_mu;
 std::vector<ncclComm_t>& retired() {
   static auto* v = new std::vector<ncclComm_t>();  // intentionally never destroyed (exit order)
   return *v;
 }
+thread_local bool t_user_object_thread = false;
+// HIP user-object destructor: a captured graph that held a reference is gone
+void release_graph_ref(void* p) {
+  t_user_object_thread = true;
+  delete static_cast<std::shared_ptr<CommHandle>*>(p);
+  t_user_object_thread = false;
+}
 }  // namespace
 
-RcclComm::~RcclComm() {
-  if (comm_) {
+// A collective captured into a hipGraph stays tied to its communicator until that graph is destroyed,
+// and Python frees a job's objects in no fixed order (a test's locals, a model rebuilt between
+// bucket-size probes): a communicator destroyed before a graph that captured it left that graph's
+// replay / teardown on freed resources -- round 3's in-suite segfault in CUDAGraph.replay
+// (profiles/pytest_gpu_r3_segv.log). So the handle is reference-counted: the RcclComm holds one
+// reference and every capture that issues a collective hands one to its graph as a HIP user object
+// (hipUserObjectCreate + hipGraphRetainUserObject; the instantiated graph keeps its graph's user
+// objects). The last holder destroys the communicator -- on the caller's thread directly, or, when
+// the last holder was a graph released on HIP's user-object thread (where no HIP/RCCL call is allowed),
+// through the retired list that the next constructor, destructor or reap() drains.
+CommHandle::~CommHandle() {
+  if (!comm) return;
+  if (t_user_object_thread) {
     std::lock_guard<std::mutex> g(g_retired_mu);
-    retired().push_back(comm_);
-    comm_ = nullptr;
+    retired().push_back(comm);
+  } else {
+    ncclCommDestroy(comm);
   }
 }
+
+RcclComm::RcclComm(const at::Tensor& uid, int64_t world, int64_t rank, int64_t device)
+    : world_(world), rank_(rank), device_(device) {
+  TORCH_CHECK(uid.numel() == NCCL_UNIQUE_ID_BYTES && uid.scalar_type() == at::kByte, "bad unique id");
+  reap();
+  ncclUniqueId id;
+  auto c = uid.contiguous().cpu();
+  std::memcpy(&id, c.data_ptr(), NCCL_UNIQUE_ID_BYTES);
+  TORCH_CHECK(hipSetDevice((int)device) == hipSuccess, "hipSetDevice failed");
+  h_ = std::make_shared<CommHandle>();
+  rccl_check(ncclCommInitRank(&h_->comm, (int)world, id, (int)rank), "CommInitRank");
+}
+
+RcclComm::~RcclComm() {
+  h_.reset();  // destroys the communicator now unless a live captured graph still holds it
+  reap();
+}
+
+int64_t RcclComm::graph_refs() const { return h_ ? (int64_t)h_.use_count() - 1 : 0; }
 
 int64_t RcclComm::reap() {
   std::vector<ncclComm_t> v;
@@ -92,26 +113,42 @@ int64_t RcclComm::retired_count() {
 }
 
 void RcclComm::abort() {
-  if (comm_) {
-    ncclCommAbort(comm_);
-    comm_ = nullptr;
+  if (h_ && h_->comm) {
+    ncclCommAbort(h_->comm);
+    h_->comm = nullptr;
   }
+}
+
+ncclComm_t RcclComm::live(hipStream_t s) {
+  TORCH_CHECK(h_ && h_->comm, "communicator aborted");
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  TORCH_CHECK(hipStreamGetCaptureInfo_v2(s, &st, &id, &g, nullptr, nullptr) == hipSuccess, "capture info");
+  if (st == hipStreamCaptureStatusActive && g) {
+    auto* ref = new std::shared_ptr<CommHandle>(h_);
+    hipUserObject_t obj = nullptr;
+    if (hipUserObjectCreate(&obj, ref, release_graph_ref, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
+      delete ref;
+      TORCH_CHECK(false, "hipUserObjectCreate failed");
+    }
+    TORCH_CHECK(hipGraphRetainUserObject(g, obj, 1, hipGraphUserObjectMove) == hipSuccess,
+                "hipGraphRetainUserObject failed");
+  }
+  return h_->comm;
 }
 
 static hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 void RcclComm::all_reduce_raw(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
-  TORCH_CHECK(comm_, "communicator aborted");
-  rccl_check(ncclAllReduce(buf, buf, count, dt, op, comm_, s), "AllReduce");
+  rccl_check(ncclAllReduce(buf, buf, count, dt, op, live(s), s), "AllReduce");
 }
 void RcclComm::reduce_scatter_raw(const void* in, void* out, size_t recvcount, ncclDataType_t dt, ncclRedOp_t op,
                                   hipStream_t s) {
-  TORCH_CHECK(comm_, "communicator aborted");
-  rccl_check(ncclReduceScatter(in, out, recvcount, dt, op, comm_, s), "ReduceScatter");
+  rccl_check(ncclReduceScatter(in, out, recvcount, dt, op, live(s), s), "ReduceScatter");
 }
 void RcclComm::all_gather_raw(const void* in, void* out, size_t sendcount, ncclDataType_t dt, hipStream_t s) {
-  TORCH_CHECK(comm_, "communicator aborted");
-  rccl_check(ncclAllGather(in, out, sendcount, dt, comm_, s), "AllGather");
+  rccl_check(ncclAllGather(in, out, sendcount, dt, live(s), s), "AllGather");
 }
 
 void RcclComm::all_reduce(const at::Tensor& t, const std::string& op) {
@@ -127,17 +164,16 @@ void RcclComm::all_gather(const at::Tensor& in, const at::Tensor& out) {
   all_gather_raw(in.data_ptr(), out.data_ptr(), in.numel(), rccl_dtype(in), cur_stream());
 }
 void RcclComm::broadcast(const at::Tensor& t, int64_t root) {
-  TORCH_CHECK(comm_, "communicator aborted");
-  rccl_check(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), rccl_dtype(t), (int)root, comm_, cur_stream()),
-             "Broadcast");
+  hipStream_t s = cur_stream();
+  rccl_check(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), rccl_dtype(t), (int)root, live(s), s), "Broadcast");
 }
 void RcclComm::send(const at::Tensor& t, int64_t peer) {
-  TORCH_CHECK(comm_, "communicator aborted");
-  rccl_check(ncclSend(t.data_ptr(), t.numel(), rccl_dtype(t), (int)peer, comm_, cur_stream()), "Send");
+  hipStream_t s = cur_stream();
+  rccl_check(ncclSend(t.data_ptr(), t.numel(), rccl_dtype(t), (int)peer, live(s), s), "Send");
 }
 void RcclComm::recv(const at::Tensor& t, int64_t peer) {
-  TORCH_CHECK(comm_, "communicator aborted");
-  rccl_check(ncclRecv(t.data_ptr(), t.numel(), rccl_dtype(t), (int)peer, comm_, cur_stream()), "Recv");
+  hipStream_t s = cur_stream();
+  rccl_check(ncclRecv(t.data_ptr(), t.numel(), rccl_dtype(t), (int)peer, live(s), s), "Recv");
 }
 
 }  // namespace tfd

@@ -1196,6 +1196,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
       .def_static("unique_id", &RcclComm::unique_id)
       .def_static("reap", &RcclComm::reap)
       .def_static("retired_count", &RcclComm::retired_count)
+      .def("graph_refs", &RcclComm::graph_refs)
       .def("world", &RcclComm::world)
       .def("rank", &RcclComm::rank)
       .def("all_reduce", &RcclComm::all_reduce)

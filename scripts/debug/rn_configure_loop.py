@@ -1,5 +1,14 @@
 """bench_resnet's probe flow in ONE process: reducer rebuilt (set_comm), two eager steps, the step
-captured and replayed, the graph dropped -- repeated. comm: none | ipc1 (a world-1 IpcComm, forced DP)."""
+captured and replayed, the graph dropped -- repeated. comm: none | ipc1 (a world-1 IpcComm, forced DP)
+| rccl1 (a world-1 RcclComm) | stub1 (a torch-op stand-in for the collective: copy / in-place scale).
+TFD_LOOP_FP32=1: fp32 wire (in-place all_reduce instead of the bf16 all_reduce_into).
+Bisection of the host-heap corruption (round 5): TFD_LOOP_NOSTREAM=1 drops the reducer's comm stream
+(no event hand-offs, no side-stream work); TFD_LOOP_DEFER=1 keeps the side stream but issues every
+bucket's hand-off (event record, stream wait, collective) from the main thread after backward()
+instead of from inside the autograd engine's backward thread; TFD_LOOP_SPLIT=1 records each bucket's
+ready event inside backward (the overlap point on the compute stream) but issues the side-stream wait and
+the collective from the main thread after backward()."""
+import os
 import sys
 
 import torch
@@ -16,6 +25,67 @@ slots = int(sys.argv[3]) if len(sys.argv) > 3 else -1
 masked = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 if slots >= 0:
     torch.ops.tfd.set_bn_part_slots(slots)
+if os.environ.get("TFD_LOOP_SPLIT") == "1":
+    from tensorflow_distributed_amd.models import resnet as _R
+
+    _orig_finish2 = _R.BucketReducer.finish
+
+    def _mark_ready2(self, name):
+        b = self.bucket_of[name]
+        self.count[b] += 1
+        if self.count[b] == self.need[b] and self.stream is not None:
+            self.bucket_events[b].record(torch.cuda.current_stream(self.fp.device))
+            self.__dict__.setdefault("_pending", []).append(b)
+
+    def _finish2(self):
+        for b in self.__dict__.pop("_pending", []):
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(self.bucket_events[b])
+                lo, hi = self.buckets[b]
+                c = self.bucket_comm[b]
+                if self.bf16 and hasattr(c, "all_reduce_into"):
+                    c.all_reduce_into(self.fp.grad[lo:hi], self.gbf[lo:hi], "sum")
+                elif self.bf16:
+                    self.gbf[lo:hi].copy_(self.fp.grad[lo:hi])
+                    c.all_reduce(self.gbf[lo:hi], "sum")
+                else:
+                    c.all_reduce(self.fp.grad[lo:hi], "sum")
+            self.launched += 1
+        _orig_finish2(self)
+
+    _R.BucketReducer.mark_ready = _mark_ready2
+    _R.BucketReducer.finish = _finish2
+if os.environ.get("TFD_LOOP_DEFER") == "1":
+    from tensorflow_distributed_amd.models import resnet as _R
+
+    _orig_finish = _R.BucketReducer.finish
+
+    def _mark_ready(self, name):
+        b = self.bucket_of[name]
+        self.count[b] += 1
+        if self.count[b] == self.need[b] and self.stream is not None:
+            self.__dict__.setdefault("_pending", []).append(b)
+
+    def _finish(self):
+        for b in self.__dict__.pop("_pending", []):
+            ev = self.bucket_events[b]
+            ev.record(torch.cuda.current_stream(self.fp.device))
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(ev)
+                lo, hi = self.buckets[b]
+                c = self.bucket_comm[b]
+                if self.bf16 and hasattr(c, "all_reduce_into"):
+                    c.all_reduce_into(self.fp.grad[lo:hi], self.gbf[lo:hi], "sum")
+                elif self.bf16:
+                    self.gbf[lo:hi].copy_(self.fp.grad[lo:hi])
+                    c.all_reduce(self.gbf[lo:hi], "sum")
+                else:
+                    c.all_reduce(self.fp.grad[lo:hi], "sum")
+            self.launched += 1
+        _orig_finish(self)
+
+    _R.BucketReducer.mark_ready = _mark_ready
+    _R.BucketReducer.finish = _finish
 dev = torch.device("cuda", 0)
 m = ResNet(18, num_classes=1000, device=dev, seed=0)
 m.masked_join = bool(masked)
@@ -25,6 +95,18 @@ if mode == "ipc1":
     from tensorflow_distributed_amd.parallel.ipc import IpcCollectives, make_ipc_comm
 
     comm = IpcCollectives(make_ipc_comm(0, 1, 0, m.fp.total))
+elif mode == "stub1":
+    class _Stub:  # the collective as plain torch ops on the caller's (comm) stream
+        def world(self):
+            return 1
+
+        def all_reduce(self, t, op="sum"):
+            t.mul_(1.0)
+
+        def all_reduce_into(self, src, dst, op="sum"):
+            dst.copy_(src)
+
+    comm = _Stub()
 elif mode == "rccl1":
     uid = torch.classes.tfd.RcclComm.unique_id()
     comm = torch.classes.tfd.RcclComm(uid, 1, 0, 0)
@@ -37,7 +119,9 @@ y = torch.randint(0, 1000, (8,), device=dev, generator=g, dtype=torch.int32)
 s = torch.cuda.Stream(dev)
 for it in range(iters):
     if comm is not None:
-        m.set_comm(comm, [0.5, 2.0][it % 2], force_dp=True)
+        m.set_comm(comm, [0.5, 2.0][it % 2], force_dp=True, bf16_grads=os.environ.get("TFD_LOOP_FP32") != "1")
+        if os.environ.get("TFD_LOOP_NOSTREAM") == "1":
+            m.reducer.stream = None
     s.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(s):
         for _ in range(2):

@@ -93,21 +93,6 @@ class FlatParams:
 
 
 # ----------------------------------------------------------------------------- bucketed reducer
-_RETAINED_GRAPHS: List["torch.cuda.CUDAGraph"] = []
-
-
-def retain_graph(g) -> None:
-    """Keep a captured CUDA graph alive until the process exits. On this stack (ROCm 7, PyTorch 2.10)
-    destroying a torch CUDAGraph captured over the two-stream DP step (the reducer's comm stream
-    forked off and joined back inside the capture) and then carrying on corrupted the host heap:
-    glibc aborts ("corrupted size vs. prev_size", "double free") a few reducer rebuilds later, in
-    1-49 capture/replay/destroy cycles over RCCL or IPC, never in 120 cycles without a graph nor in
-    80 with every graph kept (scripts/debug/rn_configure_loop.py). Callers that capture several
-    step graphs (bench_resnet.py's bucket probes) retain each one and share one memory pool between
-    them, so the kept graphs cost no extra memory."""
-    _RETAINED_GRAPHS.append(g)
-
-
 _EVENT_POOL: Dict[int, List[torch.cuda.Event]] = {}
 
 
@@ -158,14 +143,13 @@ class BucketReducer:
                             for lo, hi in self.buckets]
         self.small_buckets = sum(1 for c in self.bucket_comm if c is small and small is not None)
         self.stream = torch.cuda.Stream(fp.device) if dp else None
-        # one event per bucket for the compute -> comm stream hand-off, from a pool that is never freed:
-        # an event recorded while a step is captured belongs to the captured graph, which may outlive
-        # this reducer (a fresh torch.cuda.Event per call was freed right after its record + wait:
-        # with a graph captured over such events, the host heap got corrupted within a few dozen
-        # reducer rebuilds, scripts/debug/rn_configure_loop.py)
+        # one event per bucket for the compute -> comm stream hand-off, from a per-device pool (no event
+        # objects created or freed per reducer / per step; the host-heap corruption they were once
+        # suspected of was the autograd-thread issuance fixed in mark_ready)
         ev = _reducer_events(fp.device, len(self.buckets) + 1) if dp else [None]
         self.bucket_events, self.join_event = ev[:-1], ev[-1]
         self.events = []
+        self.ready: List[int] = []  # buckets whose ready event is recorded, collective not yet issued
         self.launched = 0
         # bf16 wire format halves the all-reduce bytes; the optimizer reads the bf16 sums directly
         self.bf16 = bf16 and self.stream is not None
@@ -174,31 +158,52 @@ class BucketReducer:
     def reset(self):
         self.count = [0] * len(self.buckets)
         self.events = []
+        self.ready = []
         self.launched = 0
 
     def mark_ready(self, name: str):
+        """Called from inside backward (the autograd engine's thread): a bucket whose last gradient
+        just landed only records its ready event on the compute stream -- the point its collective
+        will wait for. The side-stream work itself is issued by finish() on the caller's thread.
+
+        Issuing it here instead (stream switch, wait, collective launch on the autograd thread)
+        corrupted the host heap once a CUDA graph captured over it was destroyed: glibc aborts
+        ("free(): invalid pointer", segfaults) within 1-30 capture / replay / destroy cycles, with
+        the IPC collective, RCCL or a plain torch-op stand-in alike, never with the hand-offs issued
+        from the main thread (80 cycles each) nor without the side stream; a torch-only twin issuing
+        the same stream/event pattern from the main thread was clean too (scripts/debug/heap_twin.py,
+        scripts/debug/rn_configure_loop.py, profiles/heap_bisect_r5.log). The overlap is unchanged:
+        the collective still waits only for its bucket's event, recorded at the same point of the
+        backward."""
         b = self.bucket_of[name]
         self.count[b] += 1
         if self.count[b] == self.need[b] and self.stream is not None:
-            ev = self.bucket_events[b]
-            ev.record(torch.cuda.current_stream(self.fp.device))
-            with torch.cuda.stream(self.stream):
-                self.stream.wait_event(ev)
-                lo, hi = self.buckets[b]
-                c = self.bucket_comm[b]
-                if self.bf16 and hasattr(c, "all_reduce_into"):
-                    # the IPC one-shot reads the fp32 gradients and writes the bf16 sums: no cast pass
-                    c.all_reduce_into(self.fp.grad[lo:hi], self.gbf[lo:hi], "sum")
-                elif self.bf16:
-                    self.gbf[lo:hi].copy_(self.fp.grad[lo:hi])
-                    c.all_reduce(self.gbf[lo:hi], "sum")
-                else:
-                    c.all_reduce(self.fp.grad[lo:hi], "sum")
-            self.launched += 1
+            self.bucket_events[b].record(torch.cuda.current_stream(self.fp.device))
+            self.ready.append(b)
+
+    def _launch(self, b: int):
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(self.bucket_events[b])
+            lo, hi = self.buckets[b]
+            c = self.bucket_comm[b]
+            if self.bf16 and hasattr(c, "all_reduce_into"):
+                # the IPC one-shot reads the fp32 gradients and writes the bf16 sums: no cast pass
+                c.all_reduce_into(self.fp.grad[lo:hi], self.gbf[lo:hi], "sum")
+            elif self.bf16:
+                self.gbf[lo:hi].copy_(self.fp.grad[lo:hi])
+                c.all_reduce(self.gbf[lo:hi], "sum")
+            else:
+                c.all_reduce(self.fp.grad[lo:hi], "sum")
+        self.launched += 1
 
     def finish(self):
-        if self.stream is not None:  # the join event from the pool too (wait_stream makes a temporary one)
-            ev = self.join_event
+        """After backward, on the caller's thread: every ready bucket's collective on the comm stream (in
+        readiness order, each behind its own event), then the join back into the compute stream."""
+        if self.stream is not None:
+            for b in self.ready:
+                self._launch(b)
+            self.ready = []
+            ev = self.join_event  # from the pool too (wait_stream makes a temporary one)
             ev.record(self.stream)
             torch.cuda.current_stream(self.fp.device).wait_event(ev)
 
