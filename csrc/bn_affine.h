@@ -8,7 +8,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "conv_kernels.h"  // TFD_BN_SLOTS
 
 namespace tfd {
 

@@ -85,11 +85,11 @@ void gemm_nt_bf16(const uint16_t* a, const uint16_t* bt, uint16_t* c, int M, int
 // slots -- no bn_final launch between producer and apply (106 per ResNet-50 step). S only spreads
 // same-address atomics. The fp32 sums' order is then not fixed (like the split-K weight gradients).
 // Row mode, S = 0: one row per producer block (fixed order, bit-reproducible) reduced by
-// bn_final_kernel -- what the bit-exact race tests select (set_bn_slots(0)). Default TFD_BN_SLOTS.
-// Switch only between steps (no captured graph or queued kernel may span a change).
-#ifndef TFD_BN_SLOTS
-#define TFD_BN_SLOTS 4
-#endif
+// bn_final_kernel -- what the bit-exact race tests and --deterministic runs select (set_bn_slots(0)).
+// The mode is read at launch and passed to every kernel (BnPart / BnFin arguments), so a captured
+// graph keeps the mode it was built with. S = 4 by default (S = 1 15.4, 2 13.37, 4 and 8 13.22,
+// 16 13.70 ms/step for ResNet-50 b128, profiles/resnet50_bn_slots_ab_r4.log).
+constexpr int kBnSlotsDefault = 4;
 int bn_slots();
 void set_bn_slots(int s);
 // partials: fp32 workspace of bn_partials_size(M, C) floats for the partial pass (one row per block

@@ -44,13 +44,10 @@ __device__ __forceinline__ void epi_call(const EPI& epi, int m4, int n, const f3
 //  KC = false: [BK][MN] with the 16-B chunk index of row k XORed by swz_chunk(k) (no pad): the 8
 //              rows k = kk + 8g + q (g < 2, q < 4) of one tr-read lane group cover 8 disjoint 8-bank
 //              windows (pad 16 mapped rows k and k + 8 to the same banks: 2-way on every read).
-// TFD_LDS_SWZ=0 restores the padded round-2 images.
-#ifndef TFD_LDS_SWZ
-#define TFD_LDS_SWZ 1
-#endif
+// (measured: ResNet-50 -0.6 %, the MNIST step neutral -- profiles/ab_gemm_lds_swz_r3.log)
 template <int CPR>
 __device__ __forceinline__ int swz_chunk(int k) {
-  if constexpr (!TFD_LDS_SWZ || (CPR & (CPR - 1)) != 0 || CPR < 4) return 0;
+  if constexpr ((CPR & (CPR - 1)) != 0 || CPR < 4) return 0;
   else if constexpr (CPR >= 16) return (2 * (k & 1) + 4 * ((k >> 1) & 1) + 8 * ((k >> 3) & 1)) & (CPR - 1);
   else if constexpr (CPR == 8) return 2 * ((k >> 1) & 1) + 4 * ((k >> 3) & 1);
   else return 2 * ((k >> 3) & 1);
@@ -58,8 +55,8 @@ __device__ __forceinline__ int swz_chunk(int k) {
 template <int MN, int BK, bool KC>
 struct LdsTile {
   static constexpr int CH_PER_ROW = KC ? BK / 8 : MN / 8; // 16-byte chunks per LDS row
-  static constexpr bool SWZ = !KC && TFD_LDS_SWZ && (CH_PER_ROW & (CH_PER_ROW - 1)) == 0 && CH_PER_ROW >= 4;
-  static constexpr int PAD = KC ? (TFD_LDS_SWZ ? 16 : 8) : (SWZ ? 0 : 16);  // elements
+  static constexpr bool SWZ = !KC && (CH_PER_ROW & (CH_PER_ROW - 1)) == 0 && CH_PER_ROW >= 4;
+  static constexpr int PAD = KC ? 16 : (SWZ ? 0 : 16);  // elements
   static constexpr int ROW = KC ? (BK + PAD) : (MN + PAD);
   static constexpr int ELEMS = KC ? MN * ROW : BK * ROW;
   static constexpr int CHUNKS = MN * BK / 8;

@@ -43,11 +43,9 @@ __device__ __forceinline__ float read_frag_f(const float* lds, int r0, int kk, i
 
 // C tile (m0, n0) over k in [kbeg, kend); WM x WN waves; epilogue epi(m4, n, f32x4 rows m4..m4+3).
 // RS = register stages: RS = 2 issues the global loads of K-tile t+2 while tile t+1 still waits in
-// registers (two K-iterations of latency cover instead of one).
-#ifndef TFD_F32_RS
-#define TFD_F32_RS 2
-#endif
-template <int BM, int BN, int BK, int WM, int WN, class LA, class LB, class EPI, int RS = TFD_F32_RS>
+// registers (two K-iterations of latency cover instead of one): 268 -> 190 us/step for the fp32 MNIST
+// step; 3-4 stages no better (profiles/mnist_fp32_gemm_ab_r2.log).
+template <int BM, int BN, int BK, int WM, int WN, class LA, class LB, class EPI, int RS = 2>
 __device__ __forceinline__ void gemm_block_f32(const LA& la, const LB& lb, const EPI& epi, int m0, int n0, int kbeg,
                                                int kend, float* smem) {
   constexpr int NT = 64 * WM * WN;

@@ -762,17 +762,12 @@ bool is_pointwise(const ConvShape& c) { return c.R == 1 && c.S == 1 && c.stride 
 // Block tile 256 x BN (BN = 256 / 128 / 64 by the output width), 8 waves, 32x32x16 MFMA, operands
 // DMA'd into LDS through the same loaders (their off() / rsrc()). Forward: A = im2col(X) (KC), B = the
 // HWIO weight (MNC, transposed fragment reads); dgrad: A = dY gather, B = W as [C][(r,s,k)] (both KC);
-// weight gradient: A = im2col(X)^T, B = dY (both MNC). TFD_G256 (read at the first launch): 0 = the
-// 128-row core everywhere, 1 (default) = this core where its tiles fill the chip, 2 = wherever it
-// applies -- the switch the per-layer A/B (scripts/debug/gemm_probe.py) runs on.
-int g256_mode_v = -1;
-int g256_mode() {
-  if (g256_mode_v < 0) {
-    const char* e = std::getenv("TFD_G256");
-    g256_mode_v = e ? std::atoi(e) : 1;
-  }
-  return g256_mode_v;
-}
+// weight gradient: A = im2col(X)^T, B = dY (both MNC). The core choice (conv_gemm_core(), the op
+// tfd::conv_gemm_core that the per-layer probe scripts/debug/gemm_probe.py and the numerics tests
+// switch): 0 = the 128-row core everywhere, 1 (default) = this core where its tiles fill the chip with
+// >= 1024-channel bf16 outputs, 2 = wherever it applies (profiles/resnet50_core_ab_r4.log).
+int g256_mode_v = 1;  // conv_gemm_core(): 0 / 1 (default) / 2, see above
+int g256_mode() { return g256_mode_v; }
 int g256_bn(int N) { return N >= 256 ? 256 : (N >= 128 ? 128 : 64); }
 long g256_tiles(int M, int N) { return (long)((M + 255) / 256) * ((N + g256_bn(N) - 1) / g256_bn(N)); }
 // Mode 1 takes the 256-row core only where the per-layer A/B measured it faster

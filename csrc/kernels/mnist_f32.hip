@@ -136,10 +136,7 @@ struct PoolEpiF {
     idx2[o] = (uint8_t)am;
   }
 };
-#ifndef TFD_F_BK  // K-tile of the fp32 GEMM blocks
-#define TFD_F_BK 32
-#endif
-constexpr int F_BK = TFD_F_BK;
+constexpr int F_BK = 32;  // K-tile of the fp32 GEMM blocks (64 measured no better, profiles/mnist_fp32_gemm_ab_r2.log)
 __global__ __launch_bounds__(256) void f32_conv2_fwd(MnistF32Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int M = a.B * 196;

@@ -75,10 +75,9 @@ __device__ __forceinline__ void apply_mask_bits(uint32_t bits, float (&d)[8]) {
 // issued before the first use, through buffer descriptors whose hardware range check zero-fills the
 // rows past the block's chunk (no exec-masked branch around a load, so the loads of a batch are all
 // in flight together). With one row per iteration these kernels waited one memory latency per row.
-#ifndef TFD_BN_RU  // rows per batch of the BN passes (all their loads issued before the first use)
-#define TFD_BN_RU 4
-#endif
-constexpr int RU = TFD_BN_RU;
+// rows per batch of the BN passes, all their loads issued before the first use (2 and 8 measured no
+// better, profiles/resnet50_bn_ru_ab_r4.log)
+constexpr int RU = 4;
 __device__ __forceinline__ uint4 row_ld(const uint16_t* base, uint32_t nbytes, int r, int r1, int C, int c0) {
   return buf_ld(base, nbytes, (uint32_t)r * (uint32_t)C + (uint32_t)c0, r < r1);
 }
@@ -855,7 +854,7 @@ void backward_apply(const uint16_t* dout, const uint16_t* out, const uint16_t* y
 
 }  // namespace
 
-static int g_bn_slots = TFD_BN_SLOTS;
+static int g_bn_slots = kBnSlotsDefault;
 int bn_slots() { return g_bn_slots; }
 void set_bn_slots(int s) {
   if (s < 0 || s > FIN_MAXS) throw std::runtime_error("set_bn_slots: 0 (row mode) or 1..8 slots");

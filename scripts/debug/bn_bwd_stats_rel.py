@@ -27,4 +27,4 @@ for depth in (18, 50):
             torch.cuda.synchronize()
             out.append(m.fp.grad.clone())
         rel = ((out[1] - out[0]).norm() / out[0].norm()).item()
-        print(f"defer={os.environ.get('TFD_JOIN_DEFER', '1')} depth {depth} B {B} hw {hw}: rel {rel:.4f}", flush=True)
+        print(f"defer={R._JOIN_DEFER} depth {depth} B {B} hw {hw}: rel {rel:.4f}", flush=True)

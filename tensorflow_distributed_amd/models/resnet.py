@@ -212,10 +212,14 @@ class BucketReducer:
 
 
 # ----------------------------------------------------------------------------- autograd ops
-# A/B switch: TFD_JOIN_DEFER=0 computes a join's first conv arrival at once (GradJoin.arrive)
-_JOIN_DEFER = os.environ.get("TFD_JOIN_DEFER", "1") != "0"
-# A/B switch: TFD_JOIN_SUB2=0 writes a 1x1 stride-2 shortcut dgrad on the full grid (zeros included)
-_JOIN_SUB2 = os.environ.get("TFD_JOIN_SUB2", "1") != "0"
+# GradJoin defers a first-arriving conv whose dgrad can carry the BN-backward statistics (13.335 ->
+# 13.25 ms, profiles/resnet50_join_defer_ab_r4.log); False = compute it at once -- the oracle form the
+# tests and scripts/debug/bn_bwd_stats_rel.py compare against (module attribute, not a run-time switch)
+_JOIN_DEFER = True
+# a 1x1 stride-2 shortcut dgrad stays on its own grid, added at the even pixels by the joining dgrad's
+# epilogue (13.12 -> 13.04 ms, profiles/resnet50_shortcut_sub2_ab_r4.log); False = the full-grid
+# dgrad with its zero phases written -- test_stride2_shortcut_gradient_on_its_own_grid's oracle
+_JOIN_SUB2 = True
 
 
 class GradJoin:
@@ -329,8 +333,8 @@ class GradJoin:
         return out
 
 
-# A/B switch: TFD_BN_STATS_STRIDED=0 keeps the strided (phase) dgrads out of the BN-statistics fusion
-_BN_STATS_STRIDED = os.environ.get("TFD_BN_STATS_STRIDED", "1") != "0"
+# strided (phase) dgrads carry BN-backward statistics too (profiles/resnet50_bn_stats_strided_ab_r3.log)
+_BN_STATS_STRIDED = True
 
 
 def _bn_stats_fusable(L, bn, fid) -> bool:

@@ -33,3 +33,29 @@ def test_removed_engine_paths_stay_removed():
     eng = open(os.path.join(ROOT, "csrc", "runtime", "mnist_engine.cpp")).read()
     for name in ("set_fc_adam", "set_conv_unfused", "pbf_alt", "mnist_backward_a_adam"):
         assert name not in eng, name
+
+
+def test_generic_library_has_no_ab_switches():
+    """The generic conv / GEMM / BN library and the fp32 MNIST path carry no compile-time A/B arms
+    (VERDICT r4 item 8): every arm that lost its logged A/B was deleted, the winners are plain code
+    with the evidence cited beside it. Code-generating macros (TFD_BN_APPLY, TFD_BN_PART,
+    TFD_LOADER_CALL) are not switches."""
+    names = ["conv_nhwc.hip", "norm.hip", "gemm256.hip", "mnist_f32.hip", "optim.hip"]
+    srcs = [os.path.join(ROOT, "csrc", "kernels", n) for n in names]
+    srcs += [os.path.join(ROOT, "csrc", n) for n in ("gemm.h", "gemm256.h", "gemm_f32.h", "conv_kernels.h", "bn_affine.h")]
+    found = {}
+    for p in srcs:
+        src = open(p).read()
+        sw = set(re.findall(r"#if(?:n?def)?\s+!?\(?(TFD_\w+)", src))
+        if sw:
+            found[os.path.basename(p)] = sorted(sw)
+    assert not found, found
+
+
+def test_resnet_model_reads_no_ab_environment_variables():
+    """The ResNet model's former TFD_JOIN_DEFER / TFD_JOIN_SUB2 / TFD_BN_STATS_STRIDED environment
+    arms are module constants now (the tests flip them as oracles); no TFD_* variable steers it."""
+    src = open(os.path.join(ROOT, "tensorflow_distributed_amd", "models", "resnet.py")).read()
+    assert not re.search(r"environ(?:\.get)?\(?\[?[\"']TFD_", src)
+    conv = open(os.path.join(ROOT, "csrc", "kernels", "conv_nhwc.hip")).read()
+    assert "getenv" not in conv
