@@ -62,6 +62,9 @@ def main(argv=None):
                     "sum of the step in a fixed order, so a run repeats bit for bit (slot mode's fp32 atomics vary the "
                     "summation order run to run; measured 13.57 vs 13.22 ms/step for ResNet-50 b128, "
                     "profiles/resnet50_bn_slots_ab_r4.log)")
+    ap.add_argument("--conv_halo", type=int, default=-1, help="3x3 stride-1 convs on LDS halo tiles (csrc/conv_halo.h): "
+                    "0 off (im2col gather), 1 where measured faster (the library default), 2 every eligible shape; "
+                    "-1 the library default")
     ap.add_argument("--fold_bn", type=int, default=0, help="1: single-consumer relu batch norms applied inside the "
                     "consuming conv's operand loader (no bn_apply pass; 0: the separate pass; 2: 1x1 consumers only)")
     ap.add_argument("--lr", type=float, default=0.1)
@@ -88,6 +91,8 @@ def main(argv=None):
         a.bn_slots = 0
     if a.bn_slots >= 0:
         torch.ops.tfd.set_bn_part_slots(a.bn_slots)
+    if a.conv_halo >= 0:
+        torch.ops.tfd.conv_halo_mode(a.conv_halo)
     m = ResNet(a.depth, num_classes=1000, device=dev, seed=0, fuse_joins=bool(a.fuse_joins),
                bn_stats=bool(a.bn_stats), bn_bwd_stats=bool(a.bn_bwd_stats), fold_bn=a.fold_bn)
     m.mask_from_y = bool(a.mask_from_y)
@@ -227,6 +232,7 @@ def main(argv=None):
                        "bn_bwd_stats": bool(a.bn_bwd_stats), "fold_bn": a.fold_bn, "masked_join": bool(a.masked_join),
                        "fuse_stem_pool": bool(a.fuse_stem_pool),
                        "bn_slots": int(torch.ops.tfd.bn_part_slots()),
+                       "conv_halo": int(torch.ops.tfd.conv_halo_mode(-1)),
                        "bn_stats_mode": ("row: fixed summation order, bit-reproducible"
                                          if int(torch.ops.tfd.bn_part_slots()) == 0 else
                                          "slots: fp32 atomics, summation order varies run to run")}}), flush=True)

@@ -73,6 +73,9 @@ void linear_wgrad(const uint16_t* x, const uint16_t* dy, float* dw, int M, int K
 // chip (default; env TFD_G256 at the first call), 2 = the 256-row core wherever it applies. Returns the
 // previous mode; -1 only queries. (A/B switch for tests and the per-layer probe.)
 int conv_gemm_core(int mode);
+// 3x3 stride-1 convs on LDS halo tiles: 0 off, 1 (default) maps >= 14 wide, 2 every eligible shape;
+// returns the previous mode (-1: query only)
+int conv_halo_mode(int mode);
 // C[M][N] bf16 = A[M][K] . Bt[N][K]^T on the 256 x 256 core (csrc/kernels/gemm256.hip)
 void gemm_nt_bf16(const uint16_t* a, const uint16_t* bt, uint16_t* c, int M, int N, int K, hipStream_t st);
 

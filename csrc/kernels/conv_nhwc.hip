@@ -380,7 +380,9 @@ struct LdsEpi {
   static constexpr int BYTES = BM * PITCH * 4;
   static_assert(BM * CPR % NT == 0 && NT % CPR == 0, "whole chunks per thread");
 };
-// GEMM row m -> output row (identity; the strided-dgrad phase GEMMs scatter to every st-th pixel)
+// GEMM row m -> output row (identity; the strided-dgrad phase GEMMs scatter to every st-th pixel; the
+// halo-tile convs map tile rows to pixels and mark those past the image edge kNoRow: not stored)
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 struct RowId {
   __device__ __forceinline__ uint32_t operator()(int m) const { return (uint32_t)m; }
 };
@@ -422,7 +424,7 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
 #pragma unroll
     for (int c = 0; c < E::CH; ++c) {
       const int m = m0 + g0 + c * E::RG;
-      const bool ok = m < M && n < N;
+      const bool ok = m < M && n < N && orow[c] != kNoRow;
       bool aok = ok;
       const uint32_t ar = add_row(add, orow[c], aok);
       q[c] = buf_ld(add.x, add.abytes ? add.abytes : ybytes, ar * (uint32_t)N + (uint32_t)n, aok);
@@ -448,7 +450,7 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
 #pragma unroll
     for (int c = 0; c < E::CH; ++c) {
       const int m = m0 + g0 + c * E::RG;
-      const bool ok = m < M && n < N;
+      const bool ok = m < M && n < N && orow[c] != kNoRow;
       yq[c] = buf_ld(bs.y, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, ok);
       if constexpr (BS::MODE == 3) mbits[c] = ok ? bs.bits[(size_t)orow[c] * (N / 8) + n / 8] : 0u;
     }
@@ -484,7 +486,7 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
       }
     }
     const uint4 o = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
-    if (m < M && n < N) {
+    if (m < M && n < N && orow[c] != kNoRow) {
       *reinterpret_cast<uint4*>(y + (size_t)orow[c] * N + n) = o;
       if constexpr (STATS) {
         const uint32_t w[4] = {o.x, o.y, o.z, o.w};
@@ -537,6 +539,8 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
     }
   }
 }
+
+#include "../conv_halo.h"
 
 template <int BM, int BN>
 struct Tile {
@@ -781,6 +785,52 @@ bool use_g256(int M, int N) {
   const int mode = g256_mode();
   if (mode == 0 || N % 8) return false;
   return mode == 2 || (N >= 1024 && g256_tiles(M, N) >= 32);
+}
+
+// ---- 3x3 stride-1 convs on LDS halo tiles (csrc/conv_halo.h) ----
+// conv_halo_mode(): 0 = off (the im2col gather everywhere), 1 (default) = forward and stride-1 dgrad of
+// the 3x3 stride-1 pad-1 convs where the per-layer probe measured the halo tiles faster -- maps at least
+// 32 pixels wide (ResNet-50 stage 1, 56 x 56 x 64: fwd 74.2 -> 64.5 us, dgrad 76.8 -> 62.8 us); on the
+// 28- and 14-wide maps an 8 x 16 tile leaves 23 % of its rows past the image edge and the gather wins
+// (profiles/halo_probe_r5.log) -- 2 = every eligible shape (tests, probes).
+int g_halo_mode = 1;
+bool use_halo(const ConvShape& c, int cin, int cout) {
+  if (g_halo_mode == 0 || c.R != 3 || c.S != 3 || c.stride != 1 || c.pad != 1) return false;
+  if (cin % HL_CK || cout % 64) return false;
+  return g_halo_mode == 2 || c.W >= 32;
+}
+HaloGeo halo_geo(const ConvShape& c, bool dgrad) {
+  HaloGeo g;
+  g.N = c.N; g.H = c.H; g.W = c.W;
+  g.Cin = dgrad ? c.K : c.C;
+  g.Cout = dgrad ? c.C : c.K;
+  g.tx = (c.W + HL_TW - 1) / HL_TW;
+  g.ty = (c.H + HL_TH - 1) / HL_TH;
+  g.mtiles = c.N * g.tx * g.ty;
+  const uint32_t px = (uint32_t)c.N * (uint32_t)c.H * (uint32_t)c.W;
+  g.xbytes = px * (uint32_t)g.Cin * 2u;
+  g.ybytes = px * (uint32_t)g.Cout * 2u;
+  g.wbytes = 9u * (uint32_t)c.C * (uint32_t)c.K * 2u;
+  return g;
+}
+template <int BN, bool DG, bool ADD, bool STATS, class BS>
+void halo_launch_bn(const uint16_t* x, const uint16_t* w, uint16_t* y, const HaloGeo& g, const AddSrc& add, float* part,
+                    const BS& bs, hipStream_t st) {
+  constexpr int sm = HaloSmem<BN>::BYTES;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_halo_kernel<BN, DG, ADD, STATS, BS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+    attr = true;
+  }
+  conv3x3_halo_kernel<BN, DG, ADD, STATS, BS><<<dim3(g.Cout / BN, g.mtiles), 256, sm, st>>>(
+      x, w, y, g, add, BnPart{part, bn_slots()}, bs);
+}
+template <bool DG, bool ADD, bool STATS, class BS = NoBnB>
+void halo_launch(const uint16_t* x, const uint16_t* w, uint16_t* y, const HaloGeo& g, const AddSrc& add, float* part,
+                 hipStream_t st, const BS& bs = BS{}) {
+  if (g.Cout % 128 == 0) halo_launch_bn<128, DG, ADD, STATS, BS>(x, w, y, g, add, part, bs, st);
+  else halo_launch_bn<64, DG, ADD, STATS, BS>(x, w, y, g, add, part, bs, st);
 }
 
 template <int BN> struct G256WM { static constexpr int v = BN == 256 ? 2 : 4; };
@@ -1045,6 +1095,10 @@ void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t
     else dispatch_bf16(BnRelu<FwdA>{{x, make_geo(c, M, KD)}, a}, lb, y, nullptr, M, c.K, KD, st);
     return;
   }
+  if (use_halo(c, c.C, c.K)) {
+    halo_launch<false, false, false>(x, w, y, halo_geo(c, false), AddSrc{}, nullptr, st);
+    return;
+  }
   if (use_g256(M, c.K)) {  // A = im2col(X) (KC), B = HWIO weight (MNC)
     if (is_pointwise(c)) g256_launch_bf16<true, false, false, false>(DenseX<true>{x, c.C, M, c.C}, lb, y, nullptr, M, c.K, KD, nullptr, st);
     else g256_launch_bf16<true, false, false, false>(FwdA{x, make_geo(c, M, KD)}, lb, y, nullptr, M, c.K, KD, nullptr, st);
@@ -1058,6 +1112,7 @@ void conv_fwd(const ConvShape& c, const uint16_t* x, const uint16_t* w, uint16_t
 int conv_fwd_stats_rows(const ConvShape& c, bool folded) {  // row blocks of the partials
   if (bn_slots() > 0) return bn_slots();
   const int M = c.N * c.Ho() * c.Wo();
+  if (!folded && use_halo(c, c.C, c.K)) return halo_geo(c, false).mtiles;
   if (!folded && use_g256(M, c.K)) return (M + 255) / 256;
   return out_tile_rows(M, c.K);
 }
@@ -1066,6 +1121,10 @@ void conv_fwd_stats(const ConvShape& c, const uint16_t* x, const uint16_t* w, ui
                     hipStream_t st, const BnReluIn* act) {
   const int M = c.N * c.Ho() * c.Wo(), KD = c.R * c.S * c.C;
   DenseX<false> lb{w, c.K, c.K, KD};
+  if (!act && use_halo(c, c.C, c.K)) {
+    halo_launch<false, false, true>(x, w, y, halo_geo(c, false), AddSrc{}, part, st);
+    return;
+  }
   if (!act && use_g256(M, c.K)) {
     if (is_pointwise(c)) g256_launch_bf16<true, false, false, true>(DenseX<true>{x, c.C, M, c.C}, lb, y, nullptr, M, c.K, KD, part, st);
     else g256_launch_bf16<true, false, false, true>(FwdA{x, make_geo(c, M, KD)}, lb, y, nullptr, M, c.K, KD, part, st);
@@ -1198,6 +1257,11 @@ void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint1
     dgrad_strided(c, dy, w, dx, aa, st);
     return;
   }
+  if (use_halo(c, c.K, c.C)) {
+    if (add) halo_launch<true, true, false>(dy, w, dx, halo_geo(c, true), aa, nullptr, st);
+    else halo_launch<true, false, false>(dy, w, dx, halo_geo(c, true), aa, nullptr, st);
+    return;
+  }
   if (use_g256(M, c.C)) {  // A = dY gather, B = W as [C][(r,s,k)]: both KC
     const int KD = c.R * c.S * c.K;
     auto go = [&](const auto& la, const auto& lb) {
@@ -1230,6 +1294,7 @@ bool conv_dgrad_bn_supported(const ConvShape& c) {
 static int bf16_out_rows(int M, int N) { return use_g256(M, N) ? (M + 255) / 256 : out_tile_rows(M, N); }
 int conv_dgrad_bn_rows(const ConvShape& c) {
   if (bn_slots() > 0) return bn_slots();
+  if (c.stride == 1 && use_halo(c, c.K, c.C)) return halo_geo(c, true).mtiles;
   if (c.stride == 1) return bf16_out_rows(c.N * c.H * c.W, c.C);
   int rows = 0;
   for (int ph = 0; ph < c.stride; ++ph)
@@ -1252,6 +1317,10 @@ void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, ui
   auto go = [&](const auto& bs) {
     if (c.stride > 1) {
       dgrad_strided(c, dy, w, dx, aa, st, part, bs);
+    } else if (use_halo(c, c.K, c.C)) {
+      using BSt = std::decay_t<decltype(bs)>;
+      if (add) halo_launch<true, true, false, BSt>(dy, w, dx, halo_geo(c, true), aa, part, st, bs);
+      else halo_launch<true, false, false, BSt>(dy, w, dx, halo_geo(c, true), aa, part, st, bs);
     } else if (use_g256(M, c.C)) {
       auto g2 = [&](const auto& la, const auto& lb) {
         if (add) g256_launch_bf16<true, true, true, false>(la, lb, dx, aa, M, c.C, KD, part, st, RowId{}, 0u, bs);
@@ -1353,6 +1422,11 @@ void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float
   }
 }
 
+int conv_halo_mode(int mode) {  // -1: query
+  const int old = g_halo_mode;
+  if (mode >= 0) g_halo_mode = mode;
+  return old;
+}
 int conv_gemm_core(int mode) {  // -1: query
   const int old = g256_mode();
   if (mode >= 0) g256_mode_v = mode;

@@ -8,15 +8,19 @@ pytestmark = pytest.mark.gpu
 ops = None
 
 
-@pytest.fixture(autouse=True, params=[0, 2], ids=["core128", "core256"])
+@pytest.fixture(autouse=True, params=[(0, 0), (2, 0), (1, 2)], ids=["core128", "core256", "halo"])
 def _ops(cuda, request):
-    """Every conv test runs on both GEMM cores: the 128-row register-staged one and the 256-row DMA
-    one (forced for every shape it applies to; the default picks it where its tiles fill the chip)."""
+    """Every conv test runs on every GEMM path: the 128-row register-staged core and the 256-row DMA
+    core with the im2col gather (each forced for every shape it applies to; the default picks the
+    256-row core where its tiles fill the chip), and the LDS halo-tile kernel (csrc/conv_halo.h) for
+    every 3x3 stride-1 conv with 64-channel multiples, narrow maps included."""
     global ops
     ops = torch.ops.tfd
-    old = ops.conv_gemm_core(request.param)
+    core, halo = request.param
+    old = ops.conv_gemm_core(core), ops.conv_halo_mode(halo)
     yield
-    ops.conv_gemm_core(old)
+    ops.conv_gemm_core(old[0])
+    ops.conv_halo_mode(old[1])
 
 
 @pytest.fixture(params=[0, 4], ids=["rowmode", "slots4"])
@@ -58,8 +62,14 @@ CONVS = [  # N, H, W, C, K, R, stride, pad
 # (48, 28, 28, 128, ...): its dgrad (M = 37632, C = 128) takes the 128x128 tiles of the LDS-staged
 # epilogue; (48, 28, 28, 64, 64): 128x64 output tiles for fwd and dgrad; (48, 56, 56, 64, 64, s2): the
 # strided phase dgrad on 128x64 tiles
-@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS + [(48, 28, 28, 128, 32, 3, 1, 1), (48, 28, 28, 64, 64, 3, 1, 1),
-                                                   (48, 56, 56, 64, 64, 3, 2, 1)])
+# halo-tile shapes (3x3 s1, 64-channel multiples): partial tiles in both directions with 128-wide
+# output tiles, three input-channel chunks, a 7-wide map (halo mode 2), C != K both ways
+HALO = [(2, 20, 36, 64, 128, 3, 1, 1), (2, 9, 23, 192, 64, 3, 1, 1), (3, 7, 7, 128, 64, 3, 1, 1),
+        (2, 16, 16, 64, 192, 3, 1, 1)]
+
+
+@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS + HALO + [(48, 28, 28, 128, 32, 3, 1, 1), (48, 28, 28, 64, 64, 3, 1, 1),
+                                                          (48, 56, 56, 64, 64, 3, 2, 1)])
 def test_conv_fwd_dgrad_wgrad(cuda, N, H, W, C, K, R, st, pad):
     torch.manual_seed(0)
     x = rb(torch.randn(N, H, W, C))
@@ -89,7 +99,7 @@ def test_conv_fwd_dgrad_wgrad(cuda, N, H, W, C, K, R, st, pad):
     assert relerr(dw2.cpu(), wr.grad.permute(2, 3, 1, 0)) < 1e-3
 
 
-@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS + [(8, 28, 28, 64, 256, 1, 1, 0), (48, 28, 28, 32, 64, 3, 1, 1)])
+@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS + HALO + [(8, 28, 28, 64, 256, 1, 1, 0), (48, 28, 28, 32, 64, 3, 1, 1)])
 def test_conv_fwd_stats_feeds_bn(cuda, bn_mode, N, H, W, C, K, R, st, pad):
     """conv2d_fwd_stats: same output as conv2d_fwd, and per-row-block sums of the stored bf16 output
     that bn_fwd(partials=...) turns into the same normalisation as its own statistics pass. The
@@ -128,7 +138,8 @@ def test_conv_folded_bn_input_is_bit_identical(cuda, bn_mode, N, H, W, C, K, R, 
     operand loader (mean, invstd, gamma, beta passed) against the same ops on bn_fwd's materialised
     output: bit-identical outputs, statistics partials and weight gradients."""
     torch.manual_seed(7)
-    ops.conv_gemm_core(0)  # the folded form always takes the 128-row core (the fixture restores the mode)
+    ops.conv_gemm_core(0)  # the folded form always takes the 128-row core with the im2col gather
+    ops.conv_halo_mode(0)  # (the fixture restores both modes)
     y = rb(torch.randn(N, H, W, C) * 2 + 0.3).to(cuda, torch.bfloat16)
     w = rb(torch.randn(R, R, C, K) * 0.2).to(cuda, torch.bfloat16)
     g, b = (torch.rand(C) + 0.5).to(cuda), torch.randn(C).to(cuda)
