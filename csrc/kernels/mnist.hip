@@ -1320,19 +1320,25 @@ __global__ __launch_bounds__(256) void reduce_conv_grads(MnistStepArgs a, int gb
   conv_reduce_block(a, blockIdx.x, gb, red);
 }
 
-// [nlead: next-batch gather + conv slab-reduce blocks (conv_reduce_block) | output-layer blocks |
-//  fc1 dW (+ bias row) tiles over K = W*B]. nlead > 0 is the merged DP tail: the slab reduce (a
+// [output-layer blocks | fc1 dW (+ bias row) tiles over K = W*B | nlead: next-batch gather + conv
+// slab-reduce blocks (conv_reduce_block)]. nlead > 0 is the merged DP tail: the slab reduce (a
 // latency-bound 5 us launch of its own) runs beside the SFB GEMM's blocks instead of before them.
 __global__ __launch_bounds__(256) void fc_grad_sfb(MnistStepArgs a, int gb, int nlead) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  if ((int)blockIdx.x < nlead) { conv_reduce_block(a, blockIdx.x, gb, (float*)smem_raw); return; }
-  int id = (int)blockIdx.x - nlead;
+  // the GEMM's blocks are dealt first, the short reduce / gather blocks fill in behind them (5 of 6
+  // interleaved pairs 0.1-1 us/step faster than reduce-first, profiles/mnist_dp_kernels_r5.txt)
+  const int b = blockIdx.x, nsfb = (int)gridDim.x - nlead;
+  if (b >= nsfb) {
+    conv_reduce_block(a, b - nsfb, gb, (float*)smem_raw);
+    return;
+  }
+  int id = b;
   if (id < OUTS_BLOCKS) { out_grad_sfb_block(a, id, (float*)smem_raw); return; }
   // tile rows: all FDW_GY, or (ZeRO shard) [by_lo, by_hi] plus the bias row's tile
   const bool part = a.sfb_by_hi >= a.sfb_by_lo;
   const int nby = part ? (a.sfb_by_hi - a.sfb_by_lo + 1) + (a.sfb_by_hi < FDW_GY - 1 ? 1 : 0) : FDW_GY;
   static_assert(FDW_GX % 8 == 0, "XCD grouping deals whole residue classes");
-  id = xcd_grouped_tile((int)blockIdx.x, nlead + OUTS_BLOCKS, FDW_GX * nby);
+  id = xcd_grouped_tile(b, OUTS_BLOCKS, FDW_GX * nby);
   if (part) {
     int by = id / FDW_GX + a.sfb_by_lo;
     if (by > a.sfb_by_hi) by = FDW_GY - 1;  // the bias row (3136) is updated by every rank
