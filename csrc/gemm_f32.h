@@ -8,10 +8,10 @@
 //
 //   Loader::KC = true : operator()(mn, k) returns float4 {X[mn][k..k+3]}  -> LDS [MN][BK + 4]
 //   Loader::KC = false: operator()(mn, k) returns float4 {X[mn..mn+3][k]} -> LDS [BK][MN + 4]
-// Padding 4: with BK = 32 the k-major rows are 36 floats apart, so the 16 row-lanes x 4 k-lanes of
-// a fragment read hit 64 distinct banks; the mn-major rows are read along mn (consecutive lanes).
+// Padding 4 keeps every fragment read conflict-free (read_frag4_f); a KC row stays 16-B aligned.
 #pragma once
 #include "common.h"
+#include "gemm.h"  // buf_ld
 
 namespace tfd {
 
@@ -33,34 +33,56 @@ struct GemmSmemF {
   static constexpr int BYTES = 2 * (LdsTileF<BM, BK, LA::KC>::ELEMS + LdsTileF<BN, BK, LB::KC>::ELEMS) * 4;
 };
 
+// Four K-steps of one operand fragment per read, K permuted inside each 16-deep group: lane group
+// g = lane >> 4 holds k = kq + 4g .. kq + 4g + 3, and MFMA s of the group takes component s, so MFMA s
+// sums k = kq + s + {0, 4, 8, 12} and the four MFMAs together cover the group exactly once (A and B
+// use the same map). KC tiles: one ds_read_b128 per lane ([MN][BK + 4] rows are 144 B apart: the 16
+// rows of a lane group hit 64 distinct banks). !KC tiles: four ds_read_b32 from rows 4 apart; with a
+// row of MN + 4 floats, 4 rows = 16 banks mod 64, so the four lane groups are conflict-free too.
 template <int MN, int BK, bool KC>
-__device__ __forceinline__ float read_frag_f(const float* lds, int r0, int kk, int lane) {
+__device__ __forceinline__ f32x4 read_frag4_f(const float* lds, int r0, int kq, int lane) {
   using L = LdsTileF<MN, BK, KC>;
-  const int i = lane & 15, k = kk + (lane >> 4);
-  if constexpr (KC) return lds[(r0 + i) * L::ROW + k];
-  else return lds[k * L::ROW + r0 + i];
+  const int i = lane & 15, k = kq + 4 * (lane >> 4);
+  if constexpr (KC) {
+    return *reinterpret_cast<const f32x4*>(lds + (r0 + i) * L::ROW + k);
+  } else {
+    const float* p = lds + k * L::ROW + r0 + i;
+    return f32x4{p[0], p[L::ROW], p[2 * L::ROW], p[3 * L::ROW]};
+  }
+}
+
+// Branch-free float4 operand load (raw buffer load; an out-of-range chunk gets an offset past the
+// descriptor, which the hardware range check returns as zeros): no exec-masked branch per load, so the
+// register pipeline keeps the next K-tiles' loads in flight.
+__device__ __forceinline__ f32x4 buf_ld_f4(const float* base, uint32_t nbytes, uint32_t elem_off, bool ok) {
+  const uint4 u = buf_ld(reinterpret_cast<const uint16_t*>(base), nbytes, elem_off * 2u, ok);
+  return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
 }
 
 // C tile (m0, n0) over k in [kbeg, kend); WM x WN waves; epilogue epi(m4, n, f32x4 rows m4..m4+3).
-// RS = register stages: RS = 2 issues the global loads of K-tile t+2 while tile t+1 still waits in
-// registers (two K-iterations of latency cover instead of one): 268 -> 190 us/step for the fp32 MNIST
-// step; 3-4 stages no better (profiles/mnist_fp32_gemm_ab_r2.log).
-template <int BM, int BN, int BK, int WM, int WN, class LA, class LB, class EPI, int RS = 2>
+// Two register stages: the global loads of K-tile t+2 are issued while tile t+1 still waits in
+// registers (two K-iterations of latency cover; 268 -> 190 us/step for the fp32 MNIST step, 3-4 stages
+// no better, profiles/mnist_fp32_gemm_ab_r2.log). The loop body is the pair (t, t+1) with one exit, and
+// the loads are unconditional (loaders zero or range-check past their bounds; loads past kend are
+// never stored): a mid-body exit or per-tile load guards made the compiler shuttle the accumulators
+// between AGPRs and VGPRs every iteration and drain vmcnt before each load batch.
+template <int BM, int BN, int BK, int WM, int WN, class LA, class LB, class EPI>
 __device__ __forceinline__ void gemm_block_f32(const LA& la, const LB& lb, const EPI& epi, int m0, int n0, int kbeg,
                                                int kend, float* smem) {
   constexpr int NT = 64 * WM * WN;
   using TA = LdsTileF<BM, BK, LA::KC>;
   using TB = LdsTileF<BN, BK, LB::KC>;
-  static_assert(BK % 4 == 0 && BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "tile shape");
+  static_assert(BK % 16 == 0 && BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "tile shape");
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
   constexpr int CA = (TA::CHUNKS + NT - 1) / NT;
   constexpr int CB = (TB::CHUNKS + NT - 1) / NT;
-  float* As[2] = {smem, smem + TA::ELEMS};
-  float* Bs[2] = {smem + 2 * TA::ELEMS, smem + 2 * TA::ELEMS + TB::ELEMS};
+  float* const A0 = smem;
+  float* const A1 = smem + TA::ELEMS;
+  float* const B0 = smem + 2 * TA::ELEMS;
+  float* const B1 = smem + 2 * TA::ELEMS + TB::ELEMS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  static_assert(RS >= 1 && RS <= 6, "register stages");
-  f32x4 ra[RS][CA], rb[RS][CB];
+  f32x4 ra0[CA], rb0[CB], ra1[CA], rb1[CB];
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -105,76 +127,49 @@ __device__ __forceinline__ void gemm_block_f32(const LA& la, const LB& lb, const
       }
     }
   };
+  // every fragment of the K-tile is read before the first MFMA (the scheduler otherwise interleaves
+  // each read with a wait right before its MFMAs), and the next loads are pinned at the top of each
+  // half-iteration (sunk below the compute they got one K-tile of latency cover instead of two)
   auto compute = [&](const float* A, const float* Bt) {
+    constexpr int KQ = BK / 16;
+    f32x4 a[KQ][TM], b[KQ][TN];
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 4) {
-      float a[TM], b[TN];
+    for (int q = 0; q < KQ; ++q) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = read_frag_f<BM, BK, LA::KC>(A, wm * WTM + 16 * i, kk, lane);
+      for (int i = 0; i < TM; ++i) a[q][i] = read_frag4_f<BM, BK, LA::KC>(A, wm * WTM + 16 * i, 16 * q, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = read_frag_f<BN, BK, LB::KC>(Bt, wn * WTN + 16 * j, kk, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x4f32(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < TN; ++j) b[q][j] = read_frag4_f<BN, BK, LB::KC>(Bt, wn * WTN + 16 * j, 16 * q, lane);
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x4f32(a[q][i][s], b[q][j][s], acc[i][j]);
   };
   const int nk = (kend - kbeg + BK - 1) / BK;
-  if constexpr (RS == 1) {
-    if (nk > 0) {
-      gload(kbeg, ra[0], rb[0]);
-      sstore(As[0], Bs[0], ra[0], rb[0]);
-      __syncthreads();
-      for (int t = 0; t < nk; ++t) {
-        const int cur = t & 1;
-        if (t + 1 < nk) gload(kbeg + (t + 1) * BK, ra[0], rb[0]);
-        compute(As[cur], Bs[cur]);
-        if (t + 1 < nk) sstore(As[cur ^ 1], Bs[cur ^ 1], ra[0], rb[0]);
-        __syncthreads();
-      }
-    }
-  } else if constexpr (RS > 2) {
-    // register ring: set u = t % RS holds tile t until it is written to LDS at step t-1, then is
-    // refilled with tile t+RS (RS tiles of loads in flight behind the MFMAs)
-    if (nk > 0) {
-#pragma unroll
-      for (int u = 0; u < RS; ++u)
-        if (u < nk) gload(kbeg + u * BK, ra[u], rb[u]);
-      sstore(As[0], Bs[0], ra[0], rb[0]);
-      __syncthreads();
-      for (int t0 = 0; t0 < nk; t0 += RS) {
-#pragma unroll
-        for (int u = 0; u < RS; ++u) {
-          const int t = t0 + u;
-          if (t < nk) {
-            if (t + RS < nk) gload(kbeg + (t + RS) * BK, ra[u], rb[u]);
-            compute(As[t & 1], Bs[t & 1]);
-            if (t + 1 < nk) sstore(As[(t + 1) & 1], Bs[(t + 1) & 1], ra[(u + 1) % RS], rb[(u + 1) % RS]);
-            __syncthreads();
-          }
-        }
-      }
-    }
-  } else {
-    // LDS[t&1] holds tile t; register set (t+1)&1 holds tile t+1; tile t+2 loads into set t&1
-    if (nk > 0) {
-      gload(kbeg, ra[0], rb[0]);
-      if (nk > 1) gload(kbeg + BK, ra[1], rb[1]);
-      sstore(As[0], Bs[0], ra[0], rb[0]);
-      __syncthreads();
-      for (int t = 0; t < nk; t += 2) {
-        if (t + 2 < nk) gload(kbeg + (t + 2) * BK, ra[0], rb[0]);
-        compute(As[0], Bs[0]);
-        if (t + 1 < nk) sstore(As[1], Bs[1], ra[1], rb[1]);
-        __syncthreads();
-        if (t + 1 >= nk) break;
-        if (t + 3 < nk) gload(kbeg + (t + 3) * BK, ra[1], rb[1]);
-        compute(As[1], Bs[1]);
-        if (t + 2 < nk) sstore(As[0], Bs[0], ra[0], rb[0]);
-        __syncthreads();
-      }
-    }
+  // LDS buffer 0 holds even tiles, 1 odd tiles; register set 0 even tiles, set 1 odd tiles
+  gload(kbeg, ra0, rb0);
+  gload(kbeg + BK, ra1, rb1);
+  sstore(A0, B0, ra0, rb0);
+  __syncthreads();
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {
+    gload(kbeg + (t + 2) * BK, ra0, rb0);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(A0, B0);
+    sstore(A1, B1, ra1, rb1);
+    __syncthreads();
+    gload(kbeg + (t + 3) * BK, ra1, rb1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(A1, B1);
+    if (t + 2 < nk) sstore(A0, B0, ra0, rb0);
+    __syncthreads();
   }
+  if (t < nk) compute(A0, B0);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -182,28 +177,18 @@ __device__ __forceinline__ void gemm_block_f32(const LA& la, const LB& lb, const
       epi(m0 + wm * WTM + 16 * i + 4 * (lane >> 4), n0 + wn * WTN + 16 * j + (lane & 15), acc[i][j]);
 }
 
-// Row-major fp32 X[rows][ld]: KC: (mn, k) = X[mn][k]; !KC: (mn, k) = X[k][mn]. Zero past bounds.
+// Row-major fp32 X[rows][ld]: KC: (mn, k) = X[mn][k]; !KC: (mn, k) = X[k][mn]. A chunk is all in or
+// all out (zeros): the caller keeps ld and the chunked bound (k_lim for KC, mn_lim for !KC) multiples
+// of 4.
 template <bool KC_>
 struct DenseLoaderF {
   static constexpr bool KC = KC_;
   const float* __restrict__ x;
   int ld, mn_lim, k_lim;
   __device__ __forceinline__ f32x4 operator()(int mn, int k) const {
-    if constexpr (KC) {
-      if (mn >= mn_lim || k >= k_lim) return zero_f4();
-      if (k + 4 <= k_lim) return *reinterpret_cast<const f32x4*>(x + (size_t)mn * ld + k);
-      f32x4 t;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) t[j] = (k + j < k_lim) ? x[(size_t)mn * ld + k + j] : 0.f;
-      return t;
-    } else {
-      if (k >= k_lim || mn >= mn_lim) return zero_f4();
-      if (mn + 4 <= mn_lim) return *reinterpret_cast<const f32x4*>(x + (size_t)k * ld + mn);
-      f32x4 t;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) t[j] = (mn + j < mn_lim) ? x[(size_t)k * ld + mn + j] : 0.f;
-      return t;
-    }
+    const bool ok = mn < mn_lim && k < k_lim;
+    if constexpr (KC) return buf_ld_f4(x, (uint32_t)mn_lim * (uint32_t)ld * 4u, (uint32_t)mn * (uint32_t)ld + (uint32_t)k, ok);
+    else return buf_ld_f4(x, (uint32_t)k_lim * (uint32_t)ld * 4u, (uint32_t)k * (uint32_t)ld + (uint32_t)mn, ok);
   }
 };
 

@@ -31,14 +31,6 @@ __device__ __forceinline__ int data_row_f(const int* perm, const int64_t* step, 
   return perm[(int)((s * (int64_t)B + b) % (int64_t)n_data)];
 }
 
-// Branch-free float4 operand load (raw buffer load; an out-of-range chunk gets an offset past the
-// descriptor, which the hardware range check returns as zeros) -- csrc/gemm.h buf_ld for fp32: no
-// exec-masked branch per load, so the register pipeline can keep the next K-tile's loads in flight.
-__device__ __forceinline__ f32x4 buf_ld_f4(const float* base, uint32_t nbytes, uint32_t elem_off, bool ok) {
-  const uint4 u = buf_ld(reinterpret_cast<const uint16_t*>(base), nbytes, elem_off * 2u, ok);
-  return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
-}
-
 // ---------------- K1+K3: conv1 + bias + relu + maxpool + argmax (VALU, fp32 out) ----------------
 // Block = (image b, output-channel group of 8); the image is staged into a zero-bordered 32x32 LDS
 // tile; thread pp < 196 computes one pooled pixel's 2x2 window for 8 channels.
@@ -290,17 +282,11 @@ __device__ __forceinline__ void f32_out_grad_block(const MnistF32Args& a, int bl
 struct OnesRowMCF {  // (mn, k) = X[k][mn] for mn < mn_real, 1 for mn == mn_real (k < k_lim); 4 along mn
   static constexpr bool KC = false;
   const float* __restrict__ x;
-  int ld, mn_real, k_lim;
+  int ld, mn_real, k_lim;  // mn_real % 4 == 0: a chunk is all data, the ones chunk, or past the end
   __device__ __forceinline__ f32x4 operator()(int mn, int k) const {
-    if (k >= k_lim) return zero_f4();
-    if (mn + 4 <= mn_real) return *reinterpret_cast<const f32x4*>(x + (size_t)k * ld + mn);
-    f32x4 t;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = mn + j;
-      t[j] = c < mn_real ? x[(size_t)k * ld + c] : (c == mn_real ? 1.f : 0.f);
-    }
-    return t;
+    const f32x4 v = buf_ld_f4(x, (uint32_t)k_lim * (uint32_t)ld * 4u, (uint32_t)k * (uint32_t)ld + (uint32_t)mn,
+                              mn < mn_real && k < k_lim);
+    return mn == mn_real && k < k_lim ? f32x4{1.f, 0.f, 0.f, 0.f} : v;
   }
 };
 struct GradEpiF {
