@@ -88,55 +88,132 @@ __global__ __launch_bounds__(256) void f32_conv1_pool_fwd(MnistF32Args a) {
   *reinterpret_cast<uint2*>(a.idx1 + gp * 32 + cg * 8) = make_uint2((uint32_t)idxw, (uint32_t)(idxw >> 32));
 }
 
-// ---------------- K2+K3: conv2 implicit GEMM (pool-window-major M), pooled epilogue ----------------
-// m = ((b*49 + pp)*4 + win), k = tap*32 + ci: each lane's 4 accumulator rows are one 2x2 window.
-struct Conv2FwdAF {
-  static constexpr bool KC = true;
-  const float* __restrict__ p1;
-  int M;
-  __device__ __forceinline__ f32x4 operator()(int m, int k) const {
-    const int b = m / 196, r = m - b * 196, pp = r >> 2, win = r & 3;
-    const int ph = pp / 7, pw = pp - ph * 7;
-    const int tap = k >> 5, ci0 = k & 31, kh = tap / 5, kw = tap - kh * 5;
-    const int ih = 2 * ph + (win >> 1) + kh - 2, iw = 2 * pw + (win & 1) + kw - 2;
-    const bool ok = m < M && k < 800 && (unsigned)ih < 14u && (unsigned)iw < 14u;
-    const uint32_t nb = (uint32_t)(M / 196) * 14u * 14u * 32u * 4u;
-    return buf_ld_f4(p1, nb, (uint32_t)((b * 14 + ih) * 14 + iw) * 32u + ci0, ok);
+// ---------------- K2+K3: conv2 as a whole-image implicit GEMM from LDS, pooled epilogue ----------------
+// The bf16 step's conv2 structure (csrc/kernels/mnist.hip conv12_fwd_lds) on the fp32 matrix core.
+// Block = (image b, output-channel half nh), 512 threads (8 waves), 2B blocks. The image's 14x14x32
+// fp32 activations are staged ONCE into a zero-bordered, channel-chunk-major LDS image [8 chunks of 4
+// channels][18 rows][24 cols] x 16 B, and the block's half of W2 as [32 n][800 k + 4] (k contiguous):
+// every A and B fragment of the 25-tap K loop is then one ds_read_b128 (read_frag4_f's K permutation:
+// lane group g holds channels 16q + 4g .. + 3 of a tap), with no global re-reads of the 25x-expanded
+// im2col matrix and no barrier inside the K loop (the generic-core version: 392 blocks each re-staging
+// 64-row A and B tiles through LDS 25 times, a barrier per 32-deep K-tile). M = 196 rows in
+// pool-window-major order (13 tiles of 16), N = 32 (2 tiles): 26 fragment tiles, wave w owns tiles
+// f = w + 8j (m = f >> 1, n-tile = f & 1), so the SIMDs (waves w, w + 4) carry 7, 7, 6, 6 tiles.
+// Row stride 24 px = 8 (mod 16) 16-B slots keeps a 16-lane read group of four pool windows on 16
+// distinct slots; W2 rows 804 floats apart (= 36 mod 64 banks) keep the B reads conflict-free.
+constexpr int F2F_W = 24, F2F_PLANE = 18 * F2F_W /*432 slots*/, F2F_WROW = 800 + 4;
+constexpr int F2F_SMEM = (8 * F2F_PLANE * 4 + 32 * F2F_WROW) * 4;  // 55,296 + 102,912 = 158,208 B
+static_assert(F2F_SMEM <= 160 * 1024, "conv2 LDS carve");
+
+template <int NF>
+__device__ __forceinline__ void f32_conv2_taps(const float* img, const float* wt, const int (&abase)[4], int bbase,
+                                               f32x4 (&acc)[4]) {
+  f32x4 a[2][NF], b[2];
+  auto load = [&](int step, int slot) {  // step = tap * 2 + q
+    const int tap = step >> 1, q = step & 1, kh = tap / 5, kw = tap - 5 * kh;
+    const int aoff = ((4 * q) * F2F_PLANE + kh * F2F_W + kw) * 4;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) a[slot][j] = *reinterpret_cast<const f32x4*>(img + abase[j] + aoff);
+    b[slot] = *reinterpret_cast<const f32x4*>(wt + bbase + tap * 32 + 16 * q);
+  };
+  load(0, 0);
+  // step st + 1's reads go out behind step st's first MFMAs (hard scheduling fences: left alone, the
+  // scheduler sinks them below the step's last MFMA and every step starts with an LDS round trip)
+#pragma unroll
+  for (int st = 0; st < 50; ++st) {
+    const int cur = st & 1;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[j] = mfma16x16x4f32(a[cur][j][0], b[cur][0], acc[j]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + 1 < 50) load(st + 1, cur ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 1; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[j] = mfma16x16x4f32(a[cur][j][s], b[cur][s], acc[j]);
   }
-};
-struct PoolEpiF {
-  const float* __restrict__ bias;
-  float* __restrict__ p2;
-  uint8_t* __restrict__ idx2;
-  int M;
-  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
-    if (m4 >= M) return;
-    const int b = m4 / 196, pp = (m4 - b * 196) >> 2;
-    const float bb = bias[n];
-    float mx = v[0] + bb;
+}
+
+__global__ __launch_bounds__(512) void f32_conv2_fwd_lds(MnistF32Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  float* img = reinterpret_cast<float*>(smem_raw);  // [8][18*24] x float4
+  float* wt = img + 8 * F2F_PLANE * 4;               // [32][804]
+  const int b = blockIdx.x >> 1, nh = blockIdx.x & 1, t = threadIdx.x;
+  // 1. the image: every slot of the zero-bordered layout in one pass (border slots load out of range
+  //    of the buffer descriptor -> zeros), and the W2 half: 16-B loads along n, transposed into k rows
+  {
+    const uint32_t pbytes = (uint32_t)a.B * 196u * 32u * 4u;
+    constexpr int NS = (8 * F2F_PLANE + 511) / 512;  // 7
+    f32x4 v[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int i = t + 512 * j, c = i / F2F_PLANE, q = i - c * F2F_PLANE, r = q / F2F_W, x = q - r * F2F_W;
+      const int y = r - 2, xx = x - 2;
+      const bool ok = i < 8 * F2F_PLANE && (unsigned)y < 14u && (unsigned)xx < 14u;
+      v[j] = buf_ld_f4(a.p1, pbytes, (uint32_t)((b * 196 + y * 14 + xx) * 32 + 4 * c), ok);
+    }
+    constexpr int NW = 800 * 8 / 512;  // 12.5 -> 13 (800 k rows x 8 chunks of 4 n)
+    f32x4 w[NW + 1];
+#pragma unroll
+    for (int j = 0; j <= NW; ++j) {
+      const int i = t + 512 * j, k = i >> 3, n4 = (i & 7) * 4;
+      w[j] = buf_ld_f4(a.p32 + OFF_WC2, 800u * 64u * 4u, (uint32_t)(k * 64 + nh * 32 + n4), i < 800 * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int i = t + 512 * j;
+      if (i < 8 * F2F_PLANE) *reinterpret_cast<f32x4*>(img + 4 * i) = v[j];
+    }
+#pragma unroll
+    for (int j = 0; j <= NW; ++j) {
+      const int i = t + 512 * j, k = i >> 3, n4 = (i & 7) * 4;
+      if (i < 800 * 8) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) wt[(n4 + e) * F2F_WROW + k] = w[j][e];
+      }
+    }
+  }
+  __syncthreads();
+  // 2. the 25-tap K loop from LDS
+  const int lane = t & 63, w = t >> 6, g = lane >> 4, i = lane & 15, nt = w & 1;
+  int abase[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int f = w + 8 * j, m = (f >> 1) * 16 + i;
+    int px = 0;
+    if (f < 26 && m < 196) {
+      const int pp = m >> 2, win = m & 3;
+      px = (2 * (pp / 7) + (win >> 1)) * F2F_W + 2 * (pp % 7) + (win & 1);
+    }
+    abase[j] = (g * F2F_PLANE + px) * 4;
+  }
+  const int bbase = (nt * 16 + i) * F2F_WROW + 4 * g;
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = zero_f4();
+  if (w < 2) f32_conv2_taps<4>(img, wt, abase, bbase, acc);
+  else f32_conv2_taps<3>(img, wt, abase, bbase, acc);
+  // 3. bias + relu + 2x2 max pool + argmax in registers: lane's 4 rows are one pool window
+  const int n = nh * 32 + nt * 16 + i;
+  const float bb = a.p32[OFF_BC2 + n];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int f = w + 8 * j, m4 = (f >> 1) * 16 + 4 * g;
+    if (f >= 26 || m4 >= 196) continue;
+    float mx = acc[j][0] + bb;
     int am = 0;
 #pragma unroll
     for (int r = 1; r < 4; ++r) {
-      const float z = v[r] + bb;
+      const float z = acc[j][r] + bb;
       if (z > mx) { mx = z; am = r; }
     }
-    const size_t o = (size_t)b * FEAT + pp * 64 + n;
-    a_store(o, fmaxf(mx, 0.f), am);
+    const size_t o = (size_t)b * FEAT + (m4 >> 2) * 64 + n;
+    a.p2[o] = fmaxf(mx, 0.f);
+    a.idx2[o] = (uint8_t)am;
   }
-  __device__ __forceinline__ void a_store(size_t o, float v, int am) const {
-    p2[o] = v;
-    idx2[o] = (uint8_t)am;
-  }
-};
-constexpr int F_BK = 32;  // K-tile of the fp32 GEMM blocks (64 measured no better, profiles/mnist_fp32_gemm_ab_r2.log)
-__global__ __launch_bounds__(256) void f32_conv2_fwd(MnistF32Args a) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  const int M = a.B * 196;
-  Conv2FwdAF la{a.p1, M};
-  DenseLoaderF<false> lb{a.p32 + OFF_WC2, 64, 64, 800};
-  PoolEpiF epi{a.p32 + OFF_BC2, a.p2, a.idx2, M};
-  gemm_block_f32<64, 64, F_BK, 2, 2>(la, lb, epi, blockIdx.x * 64, 0, 0, 800, (float*)smem_raw);
 }
+
+constexpr int F_BK = 32;  // K-tile of the fp32 GEMM blocks (64: 188 vs 172 us/step, fewer blocks per CU; profiles/mnist_fp32_r5.log)
 
 // ---------------- K4: fc1 forward, split-K slabs (reduced by the head) ----------------
 struct SlabEpiF {
@@ -483,11 +560,8 @@ int mnist_f32_wg2_splits(int B) { return (B * 196 + F_C2W_KPER - 1) / F_C2W_KPER
 void mnist_f32_forward(const MnistF32Args& a, bool train, hipStream_t s) {
   const int B = a.B;
   f32_conv1_pool_fwd<<<4 * B, 256, 0, s>>>(a);
-  {
-    constexpr int sm = GemmSmemF<64, 64, F_BK, Conv2FwdAF, DenseLoaderF<false>>::BYTES;
-    set_smem_f<f32_conv2_fwd>(sm);
-    f32_conv2_fwd<<<(B * 196 + 63) / 64, 256, sm, s>>>(a);
-  }
+  set_smem_f<f32_conv2_fwd_lds>(F2F_SMEM);
+  f32_conv2_fwd_lds<<<2 * B, 512, F2F_SMEM, s>>>(a);
   {
     constexpr int sm = GemmSmemF<64, 64, F_BK, DenseLoaderF<true>, DenseLoaderF<false>>::BYTES;
     set_smem_f<f32_fc1_fwd>(sm);
