@@ -7,7 +7,7 @@
 // (v_mfma_f32_16x16x4_f32, csrc/gemm_f32.h). No bf16 rounding anywhere: gradients match an fp32
 // PyTorch oracle to ~1e-5.
 //
-// Kernel map: f32_conv1_pool_fwd K1+K3; f32_conv2_fwd K2+K3; f32_fc1_fwd K4;
+// Kernel map: f32_conv12_fwd_lds K1+K3+K2+K3; f32_fc1_fwd K4;
 // f32_head K4-finish+K5+K6+K7+K8(dX)+K9; f32_fc1_bwd K8 dW + K10 dW/dX (+K11 unpool epilogue);
 // f32_conv2_bwd K13 (+conv1 ReluGrad/pool-mask epilogue) + K14 (+K12 bias row) slabs;
 // f32_conv1_wgrad K15 (+K12). The slab reduce + optimizer are shared with the bf16 step.
@@ -31,64 +31,7 @@ __device__ __forceinline__ int data_row_f(const int* perm, const int64_t* step, 
   return perm[(int)((s * (int64_t)B + b) % (int64_t)n_data)];
 }
 
-// ---------------- K1+K3: conv1 + bias + relu + maxpool + argmax (VALU, fp32 out) ----------------
-// Block = (image b, output-channel group of 8); the image is staged into a zero-bordered 32x32 LDS
-// tile; thread pp < 196 computes one pooled pixel's 2x2 window for 8 channels.
-__global__ __launch_bounds__(256) void f32_conv1_pool_fwd(MnistF32Args a) {
-  __shared__ float img[32 * 32];
-  __shared__ float w[KTAPS * 8 + 8];
-  const int b = blockIdx.x >> 2, cg = blockIdx.x & 3, t = threadIdx.x;
-  const float* x = a.data + (size_t)data_row_f(a.perm, a.step, a.n_data, a.B, b) * 784;
-  for (int i = t; i < 32 * 32; i += 256) img[i] = 0.f;
-  if (t < KTAPS * 8) w[t] = a.p32[OFF_WC1 + (t >> 3) * C1 + cg * 8 + (t & 7)];
-  else if (t < KTAPS * 8 + 8) w[t] = a.p32[OFF_BC1 + cg * 8 + (t - KTAPS * 8)];
-  __syncthreads();
-  if (t < 196) {
-    const f32x4 v = reinterpret_cast<const f32x4*>(x)[t];
-    const int r = (4 * t) / 28, c = (4 * t) % 28;
-    float* d = img + (r + 2) * 32 + c + 2;
-    d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
-  }
-  __syncthreads();
-  if (t >= 196) return;
-  const int ph = t / 14, pw = t - ph * 14;
-  float patch[6][6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) patch[i][j] = img[(2 * ph + i) * 32 + 2 * pw + j];
-  const size_t gp = (size_t)b * 196 + t;
-  float out[8];
-  uint64_t idxw = 0;
-#pragma unroll 2
-  for (int cc = 0; cc < 8; ++cc) {
-    const float bias = w[KTAPS * 8 + cc];
-    float z[4] = {bias, bias, bias, bias};
-#pragma unroll
-    for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-      for (int kw = 0; kw < 5; ++kw) {
-        const float wt = w[(kh * 5 + kw) * 8 + cc];
-        z[0] = fmaf(patch[kh][kw], wt, z[0]);
-        z[1] = fmaf(patch[kh][kw + 1], wt, z[1]);
-        z[2] = fmaf(patch[kh + 1][kw], wt, z[2]);
-        z[3] = fmaf(patch[kh + 1][kw + 1], wt, z[3]);
-      }
-    float mx = z[0];
-    int am = 0;
-#pragma unroll
-    for (int win = 1; win < 4; ++win)
-      if (z[win] > mx) { mx = z[win]; am = win; }
-    out[cc] = fmaxf(mx, 0.f);
-    idxw |= (uint64_t)am << (8 * cc);
-  }
-  f32x4* op = reinterpret_cast<f32x4*>(a.p1 + gp * 32 + cg * 8);
-  op[0] = f32x4{out[0], out[1], out[2], out[3]};
-  op[1] = f32x4{out[4], out[5], out[6], out[7]};
-  *reinterpret_cast<uint2*>(a.idx1 + gp * 32 + cg * 8) = make_uint2((uint32_t)idxw, (uint32_t)(idxw >> 32));
-}
-
-// ---------------- K2+K3: conv2 as a whole-image implicit GEMM from LDS, pooled epilogue ----------------
+// ---------------- K1+K3+K2+K3: conv1 -> pool -> conv2 (whole-image implicit GEMM from LDS) -> pool ----------------
 // The bf16 step's conv2 structure (csrc/kernels/mnist.hip conv12_fwd_lds) on the fp32 matrix core.
 // Block = (image b, output-channel half nh), 512 threads (8 waves), 2B blocks. The image's 14x14x32
 // fp32 activations are staged ONCE into a zero-bordered, channel-chunk-major LDS image [8 chunks of 4
@@ -134,43 +77,109 @@ __device__ __forceinline__ void f32_conv2_taps(const float* img, const float* wt
   }
 }
 
-__global__ __launch_bounds__(512) void f32_conv2_fwd_lds(MnistF32Args a) {
+// K1+K3 fused in front (f32_conv12_fwd_lds): conv1 + bias + relu + 2x2 pool + argmax on the fp32
+// matrix core, straight into the LDS image conv2 reads (half 0 also writes p1 / idx1 for the
+// backward). Implicit GEMM M = 784 pixels (pool-window-major, m = pp*4 + win), N = 32, K = 25 taps
+// padded to 28: lane group g of MFMA step s takes tap 4s + g, one scalar LDS read of the x image per
+// (m-tile, step), W1 in registers. Each half of an image recomputes conv1 (~686 MFMAs per block,
+// the price of keeping conv2's p1 on chip); the conv2 weight half's loads are issued before it and
+// land behind its arithmetic. The x image and W1 are staged in the W2 region, which is written only
+// after conv1.
+constexpr int F12_XS = 36;  // x image row pitch (floats): zero-bordered 32 x 32 coordinates
+__global__ __launch_bounds__(512) void f32_conv12_fwd_lds(MnistF32Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   float* img = reinterpret_cast<float*>(smem_raw);  // [8][18*24] x float4
   float* wt = img + 8 * F2F_PLANE * 4;               // [32][804]
+  float* xs = wt;                                    // conv1 staging: [32][36] x image,
+  float* w1 = wt + 32 * F12_XS;                      //   [25][32] W1 + [32] bias
   const int b = blockIdx.x >> 1, nh = blockIdx.x & 1, t = threadIdx.x;
-  // 1. the image: every slot of the zero-bordered layout in one pass (border slots load out of range
-  //    of the buffer descriptor -> zeros), and the W2 half: 16-B loads along n, transposed into k rows
+  // 1. loads: x / W1 first (needed first; a wave's vmcnt is in order), then the W2 half, which stays
+  //    in registers until conv1 is done
+  f32x4 xv = zero_f4(), w1v = zero_f4();
+  if (t < 196) xv = reinterpret_cast<const f32x4*>(a.data + (size_t)data_row_f(a.perm, a.step, a.n_data, a.B, b) * 784)[t];
+  else if (t >= 256 && t < 256 + (KTAPS * C1 + C1) / 4) w1v = reinterpret_cast<const f32x4*>(a.p32 + OFF_WC1)[t - 256];
+  constexpr int NW = (800 * 8 + 511) / 512;  // 13 (800 k rows x 8 chunks of 4 n)
+  f32x4 w2v[NW];
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const int i = t + 512 * j, k = i >> 3, n4 = (i & 7) * 4;
+    w2v[j] = buf_ld_f4(a.p32 + OFF_WC2, 800u * 64u * 4u, (uint32_t)(k * 64 + nh * 32 + n4), i < 800 * 8);
+  }
+  // 2. zero the p1 image (its border is conv2's SAME padding) and the x image, then stage x / W1
+  for (int i = t; i < 8 * F2F_PLANE; i += 512) reinterpret_cast<f32x4*>(img)[i] = zero_f4();
+  for (int i = t; i < 32 * F12_XS / 4; i += 512) reinterpret_cast<f32x4*>(xs)[i] = zero_f4();
+  __syncthreads();
+  if (t < 196) {
+    const int r = (4 * t) / 28, c = (4 * t) % 28;
+    float* d = xs + (r + 2) * F12_XS + c + 2;
+    d[0] = xv[0]; d[1] = xv[1]; d[2] = xv[2]; d[3] = xv[3];
+  } else if (t >= 256 && t < 256 + (KTAPS * C1 + C1) / 4) {
+    reinterpret_cast<f32x4*>(w1)[t - 256] = w1v;
+  }
+  __syncthreads();
+  // 3. conv1 on the matrix core; wave w owns M-tiles w, w + 8, ... (<= 7 of 49)
   {
-    const uint32_t pbytes = (uint32_t)a.B * 196u * 32u * 4u;
-    constexpr int NS = (8 * F2F_PLANE + 511) / 512;  // 7
-    f32x4 v[NS];
+    const int lane = t & 63, wv = t >> 6, g = lane >> 4, col = lane & 15;
+    float bw[7][2];
 #pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      const int i = t + 512 * j, c = i / F2F_PLANE, q = i - c * F2F_PLANE, r = q / F2F_W, x = q - r * F2F_W;
-      const int y = r - 2, xx = x - 2;
-      const bool ok = i < 8 * F2F_PLANE && (unsigned)y < 14u && (unsigned)xx < 14u;
-      v[j] = buf_ld_f4(a.p1, pbytes, (uint32_t)((b * 196 + y * 14 + xx) * 32 + 4 * c), ok);
+    for (int st = 0; st < 7; ++st) {
+      const int k = 4 * st + g;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) bw[st][nt] = k < KTAPS ? w1[k * C1 + nt * 16 + col] : 0.f;
     }
-    constexpr int NW = 800 * 8 / 512;  // 12.5 -> 13 (800 k rows x 8 chunks of 4 n)
-    f32x4 w[NW + 1];
+    const float bias0 = w1[KTAPS * C1 + col], bias1 = w1[KTAPS * C1 + 16 + col];
+    int toff[7];
 #pragma unroll
-    for (int j = 0; j <= NW; ++j) {
-      const int i = t + 512 * j, k = i >> 3, n4 = (i & 7) * 4;
-      w[j] = buf_ld_f4(a.p32 + OFF_WC2, 800u * 64u * 4u, (uint32_t)(k * 64 + nh * 32 + n4), i < 800 * 8);
+    for (int st = 0; st < 7; ++st) {
+      const int k = min(4 * st + g, KTAPS - 1), kh = k / 5, kw = k - 5 * kh;
+      toff[st] = kh * F12_XS + kw;
     }
 #pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      const int i = t + 512 * j;
-      if (i < 8 * F2F_PLANE) *reinterpret_cast<f32x4*>(img + 4 * i) = v[j];
-    }
+    for (int ii = 0; ii < 7; ++ii) {
+      const int mt = wv + 8 * ii;
+      if (mt >= 49) break;
+      const int m = mt * 16 + col, pp = m >> 2, win = m & 3;
+      const int pbase = (2 * (pp / 14) + (win >> 1)) * F12_XS + 2 * (pp % 14) + (win & 1);
+      float av[7];
 #pragma unroll
-    for (int j = 0; j <= NW; ++j) {
-      const int i = t + 512 * j, k = i >> 3, n4 = (i & 7) * 4;
-      if (i < 800 * 8) {
+      for (int st = 0; st < 7; ++st) av[st] = xs[pbase + toff[st]];
+      f32x4 z0 = zero_f4(), z1 = zero_f4();
 #pragma unroll
-        for (int e = 0; e < 4; ++e) wt[(n4 + e) * F2F_WROW + k] = w[j][e];
+      for (int st = 0; st < 7; ++st) {
+        z0 = mfma16x16x4f32(av[st], bw[st][0], z0);
+        z1 = mfma16x16x4f32(av[st], bw[st][1], z1);
       }
+      const int pq = mt * 4 + g, ph = pq / 14, pw = pq - ph * 14;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const f32x4 z = nt ? z1 : z0;
+        const float bias = nt ? bias1 : bias0;
+        const int n = nt * 16 + col;
+        float mx = z[0] + bias;
+        int am = 0;
+#pragma unroll
+        for (int r = 1; r < 4; ++r) {
+          const float zz = z[r] + bias;
+          if (zz > mx) { mx = zz; am = r; }
+        }
+        const float v = fmaxf(mx, 0.f);
+        img[((n >> 2) * F2F_PLANE + (ph + 2) * F2F_W + pw + 2) * 4 + (n & 3)] = v;
+        if (nh == 0) {
+          const size_t o = ((size_t)b * 196 + pq) * 32 + n;
+          a.p1[o] = v;
+          a.idx1[o] = (uint8_t)am;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // 4. the W2 half (landed during conv1) into LDS, k rows per output channel
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const int i = t + 512 * j, k = i >> 3, n4 = (i & 7) * 4;
+    if (i < 800 * 8) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wt[(n4 + e) * F2F_WROW + k] = w2v[j][e];
     }
   }
   __syncthreads();
@@ -559,9 +568,8 @@ int mnist_f32_wg2_splits(int B) { return (B * 196 + F_C2W_KPER - 1) / F_C2W_KPER
 
 void mnist_f32_forward(const MnistF32Args& a, bool train, hipStream_t s) {
   const int B = a.B;
-  f32_conv1_pool_fwd<<<4 * B, 256, 0, s>>>(a);
-  set_smem_f<f32_conv2_fwd_lds>(F2F_SMEM);
-  f32_conv2_fwd_lds<<<2 * B, 512, F2F_SMEM, s>>>(a);
+  set_smem_f<f32_conv12_fwd_lds>(F2F_SMEM);
+  f32_conv12_fwd_lds<<<2 * B, 512, F2F_SMEM, s>>>(a);
   {
     constexpr int sm = GemmSmemF<64, 64, F_BK, DenseLoaderF<true>, DenseLoaderF<false>>::BYTES;
     set_smem_f<f32_fc1_fwd>(sm);
