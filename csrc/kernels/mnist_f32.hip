@@ -9,8 +9,8 @@
 //
 // Kernel map: f32_conv12_fwd_lds K1+K3+K2+K3; f32_fc1_fwd K4;
 // f32_head K4-finish+K5+K6+K7+K8(dX)+K9; f32_fc1_bwd K8 dW + K10 dW/dX (+K11 unpool epilogue);
-// f32_conv2_bwd K13 (+conv1 ReluGrad/pool-mask epilogue) + K14 (+K12 bias row) slabs;
-// f32_conv1_wgrad K15 (+K12). The slab reduce + optimizer are shared with the bf16 step.
+// f32_conv2_bwd_lds K13 (+conv1 ReluGrad mask, + the K15/K12 conv1 wgrad tail) + K14 (+K12 bias
+// row) slabs. The slab reduce + optimizer are shared with the bf16 step.
 #include "../common.h"
 
 #include "../gemm.h"  // buf_ld
@@ -432,125 +432,316 @@ __global__ __launch_bounds__(256) void f32_fc1_bwd(MnistF32Args a, int n_dx) {
   gemm_block_f32<64, 64, F_BK, 2, 2>(la, lb, epi, by * 64, bx * 64, 0, a.B, (float*)smem_raw);
 }
 
-// ---------------- K13: conv2 dgrad + conv1 relu/pool-mask epilogue; K14: conv2 wgrad slabs ----------
-struct Conv2DgradAF {  // (m = (b,ih,iw), k = tap*64 + co) = dz2[b][ih-kh+2][iw-kw+2][co]
-  static constexpr bool KC = true;
-  const float* __restrict__ dz2;
-  int M;
-  __device__ __forceinline__ f32x4 operator()(int m, int k) const {
-    const int b = m / 196, r = m - b * 196, ih = r / 14, iw = r - ih * 14;
-    const int tap = k >> 6, co0 = k & 63, kh = tap / 5, kw = tap - kh * 5;
-    const int oh = ih - kh + 2, ow = iw - kw + 2;
-    const bool ok = m < M && k < 1600 && (unsigned)oh < 14u && (unsigned)ow < 14u;
-    const uint32_t nb = (uint32_t)(M / 196) * 14u * 14u * 64u * 4u;
-    return buf_ld_f4(dz2, nb, (uint32_t)((b * 14 + oh) * 14 + ow) * 64u + co0, ok);
-  }
-};
-struct Conv2DgradBF {  // (n = ci, k = tap*64 + co) -> W2[tap][ci][co]
-  static constexpr bool KC = true;
-  const float* __restrict__ w2;
-  __device__ __forceinline__ f32x4 operator()(int n, int k) const {
-    const int tap = k >> 6, co0 = k & 63;
-    return buf_ld_f4(w2, 25u * 32u * 64u * 4u, (uint32_t)(tap * 32 + n) * 64u + co0, n < 32 && k < 1600);
-  }
-};
-struct MaskEpiF {
-  const float* __restrict__ p1;
-  float* __restrict__ dp1m;
-  int M;
-  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
+// ---------------- K13 (LDS-staged): conv2 dgrad + conv1 relu mask, fp32 ----------------
+// The bf16 step's dgrad structure (mnist.hip conv2_dgrad_body) on the fp32 matrix core. Block =
+// (image b, half h: input rows ih in [7h, 7h + 7)), 512 threads. dz2 rows oh in [7h - 2, 7h + 9) are
+// staged ONCE into a zero-bordered channel-chunk-major LDS image [16 chunks of 4 co][11 rows][20
+// cols] x 16 B (planes padded to 224 slots); W2 streams through a double-buffered LDS ring of 5-tap
+// stages ([tap*32 + ci] rows of 64 co, the 16-B chunk c of row r stored at c ^ (r & 15): the 16 rows
+// of a B-fragment read hit 16 distinct bank quads). dX[p][ci] = sum_{tap, co} dz2[p - tap][co]
+// W2[tap][ci][co]: M-tile = one input row (16 lanes = iw 0..15, 14 valid) so the 16 lanes of an A
+// fragment read 16 consecutive slots; N = 32 (2 tiles); K = 1600 in 100 steps of 16 (read_frag4_f's K
+// permutation: lane group g holds co 16q + 4g .. + 3; q = 0..3 per tap).
+// 14 fragment tiles (row m, n-tile nt) = 3.5 per SIMD (SIMD s runs waves s and s + 4): waves 0-3 own
+// rows {w >> 1, (w >> 1) + 2} of n-tile w & 1, waves 4-7 row 4 + ((w - 4) >> 1) plus HALF of row 6's
+// tile w & 1 (co half (w >> 1) & 1: the steps q = 0, 1 or q = 2, 3 of every tap), summed through LDS
+// after the loop -- 1400 MFMAs per SIMD instead of 1600 / 1200 with whole tiles.
+// Replaces the generic-core dgrad that re-read the 25x-expanded im2col matrix through L2 with a
+// barrier per 32-deep K-tile.
+constexpr int F2D_COLS = 20, F2D_PLANE = 224, F2D_TPS = 5, F2D_NST = 25 / F2D_TPS;
+constexpr int F2D_STAGE = F2D_TPS * 32 * 64;                          // floats per W2 stage (40 KB)
+constexpr int F2D_SMEM = 16 * F2D_PLANE * 16 + 2 * F2D_STAGE * 4;      // 57,344 + 81,920 = 139,264 B
+constexpr int F2D_BPT = F2D_STAGE / 4 / 512;                           // 16-B pieces per thread per stage
+static_assert(F2D_TPS * F2D_NST == 25 && F2D_BPT * 512 * 4 == F2D_STAGE, "stage split");
+// the conv1-wgrad tail's own region past the K loop's: the zero-bordered x image [32][32] and the
+// half image's conv1 argmax bytes [98][32], both filled before the K loop
+constexpr int F2D_XOFF = F2D_SMEM, F2D_IOFF = F2D_XOFF + 32 * 32 * 4, F2D_SMEM_T = F2D_IOFF + 98 * 32;
+static_assert(F2D_SMEM_T <= 160 * 1024, "conv2 dgrad LDS carve");
+
+// HALF < 0: both fragment tiles over all K; HALF = 0 / 1: the second tile only over q in {0, 1} / {2, 3}
+template <int HALF>
+__device__ __forceinline__ void f32_dgrad_stage(const float* img, const float* wb, int tap0, const int (&abase)[2],
+                                                int brow, int lane, f32x4 (&acc)[2]) {
+  const int g = lane >> 4, i = lane & 15;
+  f32x4 a[2][2], b[2];
+  auto second = [](int q) { return HALF < 0 || (q >> 1) == HALF; };
+  auto load = [&](int st, int slot) {  // st = local tap * 4 + q
+    const int lt = st >> 2, q = st & 3, tap = tap0 + lt, kh = tap / 5, kw = tap - 5 * kh;
+    const int aoff = ((4 * q) * F2D_PLANE - kh * F2D_COLS - kw) * 4;
+    a[slot][0] = *reinterpret_cast<const f32x4*>(img + abase[0] + aoff);
+    if (second(q)) a[slot][1] = *reinterpret_cast<const f32x4*>(img + abase[1] + aoff);
+    const int row = lt * 32 + brow;
+    b[slot] = *reinterpret_cast<const f32x4*>(wb + row * 64 + (((4 * q + g) ^ i) << 2));
+  };
+  constexpr int NS = F2D_TPS * 4;
+  load(0, 0);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m4 + r;
-      if (m >= M) return;
-      const size_t o = (size_t)m * 32 + n;
-      dp1m[o] = p1[o] > 0.f ? v[r] : 0.f;  // relu output > 0
+  for (int st = 0; st < NS; ++st) {
+    const int cur = st & 1, q = st & 3;
+    acc[0] = mfma16x16x4f32(a[cur][0][0], b[cur][0], acc[0]);
+    if (second(q)) acc[1] = mfma16x16x4f32(a[cur][1][0], b[cur][0], acc[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + 1 < NS) load(st + 1, cur ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 1; s < 4; ++s) {
+      acc[0] = mfma16x16x4f32(a[cur][0][s], b[cur][s], acc[0]);
+      if (second(q)) acc[1] = mfma16x16x4f32(a[cur][1][s], b[cur][s], acc[1]);
     }
   }
-};
-struct Conv2WgradAF {  // (mn = tap*32+ci [800 = ones row], k = pixel): 4 consecutive ci
-  static constexpr bool KC = false;
-  const float* __restrict__ p1;
-  int K;
-  __device__ __forceinline__ f32x4 operator()(int mn, int k) const {
-    const int tap = mn >> 5, ci0 = mn & 31, kh = tap / 5, kw = tap - kh * 5;
-    const int b = k / 196, r = k - b * 196, oh = r / 14, ow = r - oh * 14;
-    const int ih = oh + kh - 2, iw = ow + kw - 2;
-    const bool ok = k < K && mn < 800 && (unsigned)ih < 14u && (unsigned)iw < 14u;
-    const uint32_t nb = (uint32_t)(K / 196) * 14u * 14u * 32u * 4u;
-    const f32x4 v = buf_ld_f4(p1, nb, (uint32_t)((b * 14 + ih) * 14 + iw) * 32u + ci0, ok);
-    // the bias "ones row" (mn == 800): a select, not a branch around the load
-    return mn == 800 && k < K ? f32x4{1.f, 0.f, 0.f, 0.f} : v;
-  }
-};
-constexpr int F_C2W_GX = (801 + 63) / 64;  // 13
-constexpr int F_C2W_KPER = 1024;           // pixels per slab
-__global__ __launch_bounds__(256) void f32_conv2_bwd(MnistF32Args a, int n_dgrad) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  const int id = blockIdx.x;
-  const int M = a.B * 196;
-  if (id < n_dgrad) {
-    Conv2DgradAF la{a.dz2, M};
-    Conv2DgradBF lb{a.p32 + OFF_WC2};
-    MaskEpiF epi{a.p1, a.dp1m, M};
-    gemm_block_f32<64, 32, F_BK, 2, 2>(la, lb, epi, id * 64, 0, 0, 1600, (float*)smem_raw);
-    return;
-  }
-  const int w = id - n_dgrad, bx = w % F_C2W_GX, z = w / F_C2W_GX;
-  Conv2WgradAF la{a.p1, M};
-  DenseLoaderF<false> lb{a.dz2, 64, 64, M};
-  SlabEpiF epi{a.wg2_slab + (size_t)z * 801 * 64, 64, 801, 64};
-  const int kb = z * F_C2W_KPER, ke = min(M, kb + F_C2W_KPER);
-  gemm_block_f32<64, 64, F_BK, 2, 2>(la, lb, epi, bx * 64, 0, kb, ke, (float*)smem_raw);
 }
 
-// ---------------- K15 + K12: conv1 wgrad + bias grad (sparse: only the argmax pixel of a window) -------
-constexpr int F_C1W_HALF = 98;
-__global__ __launch_bounds__(256) void f32_conv1_wgrad(MnistF32Args a) {
-  __shared__ float img[32 * 32];
-  __shared__ __attribute__((aligned(16))) float gs[F_C1W_HALF * 32];
-  __shared__ __attribute__((aligned(16))) uint8_t is[F_C1W_HALF * 32];
-  __shared__ float part[8][26 * 32 + 1];
-  const int b = blockIdx.x >> 1, half = blockIdx.x & 1, t = threadIdx.x, c = t & 31, sub = t >> 5;
-  const float* x = a.data + (size_t)data_row_f(a.perm, a.step, a.n_data, a.B, b) * 784;
-  for (int i = t; i < 32 * 32; i += 256) img[i] = 0.f;
-  const size_t base = ((size_t)b * 196 + half * F_C1W_HALF) * 32;
-  for (int i = t; i < F_C1W_HALF * 32 / 4; i += 256)
-    reinterpret_cast<f32x4*>(gs)[i] = reinterpret_cast<const f32x4*>(a.dp1m + base)[i];
-  for (int i = t; i < F_C1W_HALF * 32 / 16; i += 256)
-    reinterpret_cast<uint4*>(is)[i] = reinterpret_cast<const uint4*>(a.idx1 + base)[i];
+__device__ __forceinline__ float part_at(const char* smem, int q, int k) {
+  return reinterpret_cast<const float*>(smem)[q * (26 * 32 + 1) + k];
+}
+__device__ __forceinline__ void f32_conv2_dgrad_body(const MnistF32Args& a, int bid) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  float* img = reinterpret_cast<float*>(smem_raw);  // [16][224] x float4
+  float* wb0 = img + 16 * F2D_PLANE * 4;             // two [160][64] W2 stages
+  float* wb1 = wb0 + F2D_STAGE;
+  const int b = bid >> 1, h = bid & 1, t = threadIdx.x;
+  const float* w2 = a.p32 + OFF_WC2;
+  f32x4 wr[F2D_BPT];
+  auto gload_w = [&](int stage) {  // piece p = t + 512 j: row p >> 4, LDS chunk p & 15
+#pragma unroll
+    for (int j = 0; j < F2D_BPT; ++j) {
+      const int p = t + 512 * j, row = p >> 4, sl = p & 15;
+      wr[j] = *reinterpret_cast<const f32x4*>(w2 + (size_t)(stage * F2D_TPS * 32 + row) * 64 + ((sl ^ (row & 15)) << 2));
+    }
+  };
+  auto sstore_w = [&](float* dst) {
+#pragma unroll
+    for (int j = 0; j < F2D_BPT; ++j) *reinterpret_cast<f32x4*>(dst + 4 * (t + 512 * j)) = wr[j];
+  };
+  gload_w(0);
+  // the conv1-wgrad tail's global operands, consumed after the K loop (which reads only LDS): the x
+  // image (threads < 196) and this half's argmax bytes (threads 256..451)
+  f32x4 xv = zero_f4();
+  uint4 iv = make_uint4(0u, 0u, 0u, 0u);
+  if (t < 196) xv = reinterpret_cast<const f32x4*>(a.data + (size_t)data_row_f(a.perm, a.step, a.n_data, a.B, b) * 784)[t];
+  else if (t >= 256 && t < 256 + 196) iv = reinterpret_cast<const uint4*>(a.idx1 + ((size_t)b * 196 + h * 98) * 32)[t - 256];
+  float* xs = reinterpret_cast<float*>(smem_raw + F2D_XOFF);
+  uint8_t* is = reinterpret_cast<uint8_t*>(smem_raw + F2D_IOFF);
+  if (t < 256) reinterpret_cast<f32x4*>(xs)[t] = zero_f4();
+  {
+    constexpr int NI = 16 * F2D_PLANE / 512;  // 7
+    const uint32_t zbytes = (uint32_t)a.B * 196u * 64u * 4u;
+    f32x4 v[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int i = t + 512 * j, c = i / F2D_PLANE, q = i - c * F2D_PLANE, rr = q / F2D_COLS, cc = q - rr * F2D_COLS;
+      const int r = rr + 7 * h - 2, col = cc - 2;
+      const bool ok = q < 11 * F2D_COLS && (unsigned)r < 14u && (unsigned)col < 14u;
+      v[j] = buf_ld_f4(a.dz2, zbytes, (uint32_t)(((b * 14 + r) * 14 + col) * 64 + 4 * c), ok);
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) *reinterpret_cast<f32x4*>(img + 4 * (t + 512 * j)) = v[j];
+  }
+  sstore_w(wb0);
   __syncthreads();
-  if (t < 196) {
-    const f32x4 v = reinterpret_cast<const f32x4*>(x)[t];
-    const int r = (4 * t) / 28, q = (4 * t) % 28;
-    float* d = img + (r + 2) * 32 + q + 2;
-    d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+  const int lane = t & 63, w = t >> 6, g = lane >> 4, i = lane & 15, nt = w & 1;
+  // this wave's two rows: waves 0-3 rows w >> 1 and (w >> 1) + 2, waves 4-7 row 4 + ((w - 4) >> 1)
+  // and (half of) row 6
+  const int r0 = w < 4 ? (w >> 1) : 4 + ((w - 4) >> 1), r1 = w < 4 ? (w >> 1) + 2 : 6;
+  const int abase[2] = {(g * F2D_PLANE + (r0 + 4) * F2D_COLS + i + 4) * 4, (g * F2D_PLANE + (r1 + 4) * F2D_COLS + i + 4) * 4};
+  const int brow = nt * 16 + i;
+  // conv1's relu outputs that mask this lane's dX values
+  float p1pre[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      p1pre[j][e] = a.p1[((size_t)b * 196 + (7 * h + (j ? r1 : r0)) * 14 + min(4 * g + e, 13)) * 32 + nt * 16 + i];
+  if (t < 196) {  // x into the zero-bordered image (zeroed before the barrier above)
+    const int r = (4 * t) / 28, c = (4 * t) % 28;
+    float* d = xs + (r + 2) * 32 + c + 2;
+    d[0] = xv[0]; d[1] = xv[1]; d[2] = xv[2]; d[3] = xv[3];
+  } else if (t >= 256 && t < 256 + 196) {
+    reinterpret_cast<uint4*>(is)[t - 256] = iv;
+  }
+  f32x4 acc[2] = {zero_f4(), zero_f4()};
+  const int role = w < 4 ? -1 : ((w >> 1) & 1);
+  for (int stg = 0; stg < F2D_NST; ++stg) {
+    if (stg + 1 < F2D_NST) gload_w(stg + 1);
+    const float* wb = (stg & 1) ? wb1 : wb0;
+    if (role < 0) f32_dgrad_stage<-1>(img, wb, stg * F2D_TPS, abase, brow, lane, acc);
+    else if (role == 0) f32_dgrad_stage<0>(img, wb, stg * F2D_TPS, abase, brow, lane, acc);
+    else f32_dgrad_stage<1>(img, wb, stg * F2D_TPS, abase, brow, lane, acc);
+    if (stg + 1 < F2D_NST) sstore_w((stg & 1) ? wb0 : wb1);
+    __syncthreads();
+  }
+  // row 6: waves 6, 7 (co half 1) park their partial tile, waves 4, 5 (co half 0) add it
+  f32x4* park = reinterpret_cast<f32x4*>(smem_raw);  // the dz2 image is dead
+  if (w >= 6) park[(w - 6) * 64 + lane] = acc[1];
+  __syncthreads();
+  if (w == 4 || w == 5) acc[1] += park[(w - 4) * 64 + lane];
+  // K15 + K12 tail: conv1 weight + bias gradient of this half image. dX through conv1's relu mask
+  // (p1 > 0) is the pooled conv1 gradient; it reaches the conv1 output pixel at its window's argmax
+  // only (MaxPoolGrad), so dW1[kh][kw][c] = sum over the 98 pooled pixels of g * x[argmax pixel + tap].
+  float* gs = wb0;  // [98][32] masked dX (the W2 ring is dead)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (j == 1 && w >= 6) break;
+    const int lr = j ? r1 : r0, ci = nt * 16 + i;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int iw = 4 * g + e;
+      if (iw >= 14) break;
+      gs[(lr * 14 + iw) * 32 + ci] = p1pre[j][e] > 0.f ? acc[j][e] : 0.f;
+    }
   }
   __syncthreads();
-  float acc[26];
+  {
+    const int c = t & 31, sub = t >> 5;  // 16 pixel slices
+    float a1[26];
 #pragma unroll
-  for (int j = 0; j < 26; ++j) acc[j] = 0.f;
-  for (int lp = sub; lp < F_C1W_HALF; lp += 8) {
-    const float g = gs[lp * 32 + c];
-    {  // no zero skip: time must not depend on values (fma(0, x, acc) == acc)
-      const int pp = half * F_C1W_HALF + lp, w = is[lp * 32 + c];
-      const int oh = 2 * (pp / 14) + (w >> 1), ow = 2 * (pp % 14) + (w & 1);
+    for (int k = 0; k < 26; ++k) a1[k] = 0.f;
+    for (int lp = sub; lp < 98; lp += 16) {  // no zero skip: time must not depend on values
+      const float gv = gs[lp * 32 + c];
+      const int pp = h * 98 + lp, wi = is[lp * 32 + c];
+      const int oh = 2 * (pp / 14) + (wi >> 1), ow = 2 * (pp % 14) + (wi & 1);
 #pragma unroll
       for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
-        for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] = fmaf(g, img[(oh + kh) * 32 + ow + kw], acc[kh * 5 + kw]);
-      acc[25] += g;
+        for (int kw = 0; kw < 5; ++kw) a1[kh * 5 + kw] = fmaf(gv, xs[(oh + kh) * 32 + ow + kw], a1[kh * 5 + kw]);
+      a1[25] += gv;
+    }
+    float* part = reinterpret_cast<float*>(smem_raw);  // [16][26*32 + 1] (the dz2 image / park are dead)
+#pragma unroll
+    for (int k = 0; k < 26; ++k) part[sub * (26 * 32 + 1) + k * 32 + c] = a1[k];
+  }
+  __syncthreads();
+  for (int k = t; k < 26 * 32; k += 512) {
+    float sm = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sm += part_at(smem_raw, q, k);
+    a.wg1_slab[(size_t)bid * 832 + k] = sm;
+  }
+}
+
+// ---------------- K14 (LDS-staged): conv2 wgrad (+ K12 bias row), fp32 ----------------
+// The bf16 step's wgrad structure (mnist.hip conv2_wgrad_body). Block = (tap group tg, image pair ip),
+// 512 threads; 4 x 64 = 256 blocks at B = 128. Per image: p1 (14x14x32) into a zero-bordered LDS image
+// [18][18] positions x 48-float channel stride and dz2 (196 x 64) into LDS rows of 80 floats; then
+// dW[tap*32 + ci][co] += sum_px p1[px + tap][ci] dz2[px][co] on the fp32 matrix core: K = the image's
+// 196 pixels (49 MFMA k-steps of 4, lane group g = pixel 4kk + g), so the im2col shift of a tap is a
+// per-lane position offset and every operand is one conflict-free scalar LDS read (16 lanes = 16
+// consecutive channels; the 4 pixel groups land 16 banks apart: strides 48 and 80 = 48 / 16 mod 64
+// per position / pixel). Wave w owns ci-tile w >> 2, co-tile w & 3 and every tap of its group (6, the
+// last 7): one B read feeds 6-7 MFMAs. One fp32 slab per image pair (rows of its tap group; tap group 0
+// also the bias row 800), reduced by the optimizer tail. Image ii + 1's global loads are issued before
+// image ii's MFMAs. Replaces the im2col GEMM that re-read p1 25x through L2.
+constexpr int F2W_NTG = 4, F2W_TPG = 6, F2W_MAXT = 25 - F2W_TPG * (F2W_NTG - 1);  // 7
+constexpr int F2W_IMG = 2, F2W_PW = 18, F2W_CS = 48, F2W_DS = 80;
+constexpr int F2W_IMG_F = F2W_PW * F2W_PW * F2W_CS;        // 15,552 floats
+constexpr int F2W_DZ_F = 196 * F2W_DS;                     // 15,680 floats
+constexpr int F2W_SMEM = (F2W_IMG_F + F2W_DZ_F + 8 * 64) * 4;  // 126,976 B
+static_assert(F2W_SMEM <= F2D_SMEM, "one LDS size for both block kinds of the launch");
+constexpr int F2W_N1 = (196 * 8 + 511) / 512, F2W_N2 = (196 * 16 + 511) / 512;  // 4, 7 float4 per thread
+
+__device__ __forceinline__ void f32_conv2_wgrad_body(const MnistF32Args& a, int bid) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  float* img = reinterpret_cast<float*>(smem_raw);
+  float* dz = img + F2W_IMG_F;
+  float* bred = dz + F2W_DZ_F;  // [8][64]
+  const int tg = bid % F2W_NTG, ip = bid / F2W_NTG, t = threadIdx.x;
+  const int tap0 = tg * F2W_TPG, ntaps = (tg == F2W_NTG - 1) ? F2W_MAXT : F2W_TPG;
+  const int lane = t & 63, w = t >> 6, cit = w >> 2, ct = w & 3, g = lane >> 4, i = lane & 15;
+  f32x4 v1[F2W_N1], v2[F2W_N2];
+  auto gload = [&](int b) {
+    const f32x4* s1 = reinterpret_cast<const f32x4*>(a.p1 + (size_t)b * 196 * 32);
+    const f32x4* s2 = reinterpret_cast<const f32x4*>(a.dz2 + (size_t)b * 196 * 64);
+#pragma unroll
+    for (int j = 0; j < F2W_N1; ++j) { const int k = t + 512 * j; v1[j] = k < 196 * 8 ? s1[k] : zero_f4(); }
+#pragma unroll
+    for (int j = 0; j < F2W_N2; ++j) { const int k = t + 512 * j; v2[j] = k < 196 * 16 ? s2[k] : zero_f4(); }
+  };
+  if (ip * F2W_IMG < a.B) gload(ip * F2W_IMG);
+  // the image border stays zero for every image of the block
+  for (int k = t; k < F2W_PW * F2W_PW; k += 512) {
+    const int r = k / F2W_PW, c = k - r * F2W_PW;
+    if (r < 2 || r >= 16 || c < 2 || c >= 16) {
+      f32x4* d = reinterpret_cast<f32x4*>(img + k * F2W_CS);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = zero_f4();
     }
   }
+  f32x4 acc[F2W_MAXT];
 #pragma unroll
-  for (int j = 0; j < 26; ++j) part[sub][j * 32 + c] = acc[j];
-  __syncthreads();
-  for (int i = t; i < 26 * 32; i += 256) {
-    float s = 0.f;
+  for (int j = 0; j < F2W_MAXT; ++j) acc[j] = zero_f4();
+  float bsum = 0.f;
+  for (int ii = 0; ii < F2W_IMG; ++ii) {
+    const int b = ip * F2W_IMG + ii;
+    if (b >= a.B) break;
+    __syncthreads();  // the previous image's operands are consumed
 #pragma unroll
-    for (int q = 0; q < 8; ++q) s += part[q][i];
-    a.wg1_slab[(size_t)blockIdx.x * 832 + i] = s;
+    for (int j = 0; j < F2W_N1; ++j) {
+      const int k = t + 512 * j;
+      if (k < 196 * 8) {
+        const int px = k >> 3, ch = k & 7, r = px / 14, c = px - r * 14;
+        *reinterpret_cast<f32x4*>(img + ((r + 2) * F2W_PW + c + 2) * F2W_CS + ch * 4) = v1[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < F2W_N2; ++j) {
+      const int k = t + 512 * j;
+      if (k < 196 * 16) *reinterpret_cast<f32x4*>(dz + (k >> 4) * F2W_DS + (k & 15) * 4) = v2[j];
+    }
+    __syncthreads();
+    if (ii + 1 < F2W_IMG && b + 1 < a.B) gload(b + 1);
+    if (tg == 0) {  // bias row: column sums of dz2 (pixel slice t >> 6 of 8)
+      for (int px = t >> 6; px < 196; px += 8) bsum += dz[px * F2W_DS + (t & 63)];
+    }
+    auto operands = [&](int kk, float& bv, float (&av)[F2W_MAXT]) {
+      const int px = 4 * kk + g, oh = px / 14, ow = px - oh * 14;
+      bv = dz[px * F2W_DS + ct * 16 + i];
+      const float* ap = img + (oh * F2W_PW + ow) * F2W_CS + cit * 16 + i;
+#pragma unroll
+      for (int j = 0; j < F2W_MAXT; ++j) {
+        const int tap = tap0 + (j < ntaps ? j : 0), kh = tap / 5, kw = tap - 5 * kh;
+        av[j] = ap[(kh * F2W_PW + kw) * F2W_CS];
+      }
+    };
+    float bv[2], av[2][F2W_MAXT];
+    operands(0, bv[0], av[0]);
+#pragma unroll
+    for (int kk = 0; kk < 49; ++kk) {
+      const int cur = kk & 1;
+      acc[0] = mfma16x16x4f32(av[cur][0], bv[cur], acc[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kk + 1 < 49) operands(kk + 1, bv[cur ^ 1], av[cur ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 1; j < F2W_MAXT; ++j)
+        if (j < ntaps) acc[j] = mfma16x16x4f32(av[cur][j], bv[cur], acc[j]);
+    }
   }
+  float* slab = a.wg2_slab + (size_t)ip * 801 * 64;
+#pragma unroll
+  for (int j = 0; j < F2W_MAXT; ++j) {
+    if (j < ntaps) {
+      const int tap = tap0 + j;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) slab[(size_t)(tap * 32 + cit * 16 + 4 * g + r) * 64 + ct * 16 + i] = acc[j][r];
+    }
+  }
+  if (tg == 0) {
+    bred[(t >> 6) * 64 + (t & 63)] = bsum;
+    __syncthreads();
+    if (t < 64) {
+      float sm = 0.f;
+#pragma unroll
+      for (int sl = 0; sl < 8; ++sl) sm += bred[sl * 64 + t];
+      slab[800 * 64 + t] = sm;
+    }
+  }
+}
+
+// conv2 wgrad (blocks [0, nw)) and dgrad in ONE launch: both consume only dz2, and one LDS size
+// (one block per CU) lets each CU run a dgrad block as soon as its wgrad block is done
+__global__ __launch_bounds__(512) void f32_conv2_bwd_lds(MnistF32Args a, int nw) {
+  if ((int)blockIdx.x < nw) f32_conv2_wgrad_body(a, blockIdx.x);
+  else f32_conv2_dgrad_body(a, blockIdx.x - nw);
 }
 
 template <auto K>
@@ -564,7 +755,7 @@ inline void set_smem_f(int bytes) {
 }  // namespace
 
 int mnist_f32_fc1_splits() { return F_FC1_SPLITS; }
-int mnist_f32_wg2_splits(int B) { return (B * 196 + F_C2W_KPER - 1) / F_C2W_KPER; }
+int mnist_f32_wg2_splits(int B) { return (B + F2W_IMG - 1) / F2W_IMG; }  // one slab per image pair
 
 void mnist_f32_forward(const MnistF32Args& a, bool train, hipStream_t s) {
   const int B = a.B;
@@ -589,15 +780,9 @@ void mnist_f32_backward(const MnistF32Args& a, hipStream_t s) {
     const int n_dx = F_DX_GX * ((B + 31) / 32);
     f32_fc1_bwd<<<F_OUTG_BLOCKS + n_dx + F_DW_GX * F_DW_GY, 256, sm, s>>>(a, n_dx);
   }
-  {
-    constexpr int sm_d = GemmSmemF<64, 32, F_BK, Conv2DgradAF, Conv2DgradBF>::BYTES;
-    constexpr int sm_w = GemmSmemF<64, 64, F_BK, Conv2WgradAF, DenseLoaderF<false>>::BYTES;
-    constexpr int sm = sm_d > sm_w ? sm_d : sm_w;
-    set_smem_f<f32_conv2_bwd>(sm);
-    const int n_dgrad = (B * 196 + 63) / 64;
-    f32_conv2_bwd<<<n_dgrad + F_C2W_GX * a.wg2_splits, 256, sm, s>>>(a, n_dgrad);
-  }
-  f32_conv1_wgrad<<<2 * B, 256, 0, s>>>(a);
+  set_smem_f<f32_conv2_bwd_lds>(F2D_SMEM_T);
+  const int nw = F2W_NTG * a.wg2_splits;
+  f32_conv2_bwd_lds<<<nw + 2 * B, 512, F2D_SMEM_T, s>>>(a, nw);
 }
 
 }  // namespace tfd

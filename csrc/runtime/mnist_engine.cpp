@@ -63,7 +63,6 @@ class MnistEngine : public torch::CustomClassHolder {
     loss_row_ = at::zeros({B_}, f32);
     correct_row_ = at::zeros({B_}, f32);
     dz2_ = at::empty({B_, P1H, P1H, C2}, bf);
-    dp1m_ = at::empty({B_, P1H, P1H, C1}, bf);
     wg2_slab_ = at::empty({wg2_splits_, 801, C2}, f32);
     wg1_slab_ = at::empty({2 * B_, 832}, f32);
     xbuf_ = at::zeros({B_, 784}, f32);
@@ -259,7 +258,6 @@ class MnistEngine : public torch::CustomClassHolder {
       fhd_ = at::empty({B_, HID}, f32);
       fdh_ = at::empty({B_, HID}, f32);
       fdz2_ = at::empty({B_, P1H, P1H, C2}, f32);
-      fdp1m_ = at::empty({B_, P1H, P1H, C1}, f32);
       fslab_ = at::empty({mnist_f32_fc1_splits(), B_, HID}, f32);
       fwg2_ = at::empty({mnist_f32_wg2_splits((int)B_), 801, C2}, f32);
     }
@@ -1072,7 +1070,6 @@ class MnistEngine : public torch::CustomClassHolder {
     f.loss_row = a.loss_row;
     f.correct_row = a.correct_row;
     f.dz2 = (float*)fdz2_.data_ptr();
-    f.dp1m = (float*)fdp1m_.data_ptr();
     f.wg2_slab = (float*)fwg2_.data_ptr();
     f.wg1_slab = a.wg1_slab;
     f.fc1_splits = mnist_f32_fc1_splits();
@@ -1112,7 +1109,6 @@ class MnistEngine : public torch::CustomClassHolder {
     a.loss_row = (float*)loss_row_.data_ptr();
     a.correct_row = (float*)correct_row_.data_ptr();
     a.dz2 = (uint16_t*)dz2_.data_ptr();
-    a.dp1m = (uint16_t*)dp1m_.data_ptr();
     a.wg2_slab = (float*)wg2_slab_.data_ptr();
     a.wg1_slab = (float*)wg1_slab_.data_ptr();
     a.fc1_splits = fc1_splits_;
@@ -1155,10 +1151,10 @@ class MnistEngine : public torch::CustomClassHolder {
   int64_t ipc_small_ = 0;
   bool ipc_gather_ = true;
   at::Tensor params_, pbf_, grad_, m_, v_, gbf_, step_, tnext_;
-  at::Tensor p1_, idx1_, p2_, idx2_, fc1_slab_, hd_, dh_, dlogits_, loss_row_, correct_row_, dz2_, dp1m_, wg2_slab_,
+  at::Tensor p1_, idx1_, p2_, idx2_, fc1_slab_, hd_, dh_, dlogits_, loss_row_, correct_row_, dz2_, wg2_slab_,
       wg1_slab_, xbuf_, ybuf_;
   at::Tensor data_, labels_, perm_, rows_, xpre_, ypre_, dbg_;
-  at::Tensor f1_, f2_, fhd_, fdh_, fdz2_, fdp1m_, fslab_, fwg2_;  // fp32-mode activations / slabs
+  at::Tensor f1_, f2_, fhd_, fdh_, fdz2_, fslab_, fwg2_;  // fp32-mode activations / slabs
   bool fp32_ = false;
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t ev_a_ = nullptr, ev_b_ = nullptr, ev_done_ = nullptr;

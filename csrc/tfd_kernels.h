@@ -37,7 +37,6 @@ struct MnistStepArgs {
   float* dlogits;                 // [B][10]
   float* loss_row; float* correct_row;  // [B]
   uint16_t* dz2;                  // [B][14][14][64]
-  uint16_t* dp1m;                 // [B][14][14][32]
   float* wg2_slab;                // [wg2_splits][801][64]
   float* wg1_slab;                // [2B][832] (one slab per half image)
   int fc1_splits, wg2_splits;
@@ -120,7 +119,6 @@ struct MnistF32Args {
   float* dlogits;              // [B][10]
   float* loss_row; float* correct_row;
   float* dz2;                  // [B][14][14][64]
-  float* dp1m;                 // [B][14][14][32]
   float* wg2_slab;             // [wg2_splits][801][64]
   float* wg1_slab;             // [2B][832]
   int fc1_splits, wg2_splits;
