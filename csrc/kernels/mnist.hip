@@ -1382,7 +1382,7 @@ __device__ __forceinline__ void adam4(const MnistAdamArgs& o, int64_t i, f32x4 g
   reinterpret_cast<f32x4*>(o.p)[i] = p;
   reinterpret_cast<f32x4*>(o.m)[i] = m;
   reinterpret_cast<f32x4*>(o.v)[i] = v;
-  reinterpret_cast<uint2*>(o.pbf)[i] = make_uint2(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]));
+  if (o.pbf) reinterpret_cast<uint2*>(o.pbf)[i] = make_uint2(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]));
 }
 // sum over slabs q, q + QS, ... (< ns) of float4 column x of a [ns][stride4] slab array; MAD_SL loads
 // issued per batch before any add

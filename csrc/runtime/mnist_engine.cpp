@@ -261,6 +261,7 @@ class MnistEngine : public torch::CustomClassHolder {
       fslab_ = at::empty({mnist_f32_fc1_splits(), B_, HID}, f32);
       fwg2_ = at::empty({mnist_f32_wg2_splits((int)B_), 801, C2}, f32);
     }
+    if (fp32_ && !f) sync_shadow();  // the fp32 optimizer tail leaves the bf16 shadow stale
     fp32_ = f;
     if (f) bf16_comm_ = false;
   }
@@ -647,8 +648,10 @@ class MnistEngine : public torch::CustomClassHolder {
     r.wg2_splits = f.wg2_splits;
     r.xpre = nullptr;  // the fp32 kernels read their batch rows through perm/step: no prefetch gather
     if (fused) {
+      // no bf16 shadow: nothing in fp32 mode reads it (set_dtype("bf16") re-derives it), and its
+      // 6.5 MB of writes are 1 us of the bandwidth-bound optimizer tail
       MnistAdamArgs o{(float*)params_.data_ptr(), (float*)m_.data_ptr(), (float*)v_.data_ptr(),
-                      (uint16_t*)pbf_.data_ptr(), (float)lr_, (float)b1_, (float)b2_, (float)eps_,
+                      nullptr, (float)lr_, (float)b1_, (float)b2_, (float)eps_,
                       (const int64_t*)tnext_.data_ptr(), (int64_t*)step_.data_ptr(), nullptr};
       mark(P_BCONV, s);
       mnist_adam_fused(r, o, s, true);

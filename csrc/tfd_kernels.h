@@ -82,7 +82,8 @@ void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s);
 // slab reduction fused in (the conv region takes its gradient straight from the per-block slabs),
 // t = *t (written by the head kernel, MnistStepArgs::t_out), *step bumped once by the kernel.
 struct MnistAdamArgs {
-  float* p; float* m; float* v; uint16_t* pbf;
+  float* p; float* m; float* v;
+  uint16_t* pbf;  // bf16 shadow written beside p; null: none (the fp32 engine reads p itself)
   float lr, beta1, beta2, eps;
   const int64_t* t;
   int64_t* step;

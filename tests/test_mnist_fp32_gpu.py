@@ -141,3 +141,25 @@ def test_fp32_fused_adam_tail_matches_unfused(cuda):
         assert int(eng.step_tensor().item()) == 3
         out.append(eng.params().cpu() - p0)
     assert _relerr(out[1].double(), out[0].double()) < 1e-5
+
+
+def test_fp32_tail_leaves_no_stale_shadow_after_switching_to_bf16(cuda):
+    """The fp32 fused tail writes no bf16 shadow (nothing in fp32 mode reads it); switching the
+    engine back to bf16 must re-derive it from the fp32 master weights."""
+    B = 64
+    eng = _engine(B, cuda, 1.0)
+    eng.set_adam(0.01, 0.9, 0.999, 1e-8)
+    eng.set_fused_tail(1)
+    p0 = M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(3).items()})
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        eng.params().copy_(p0.to(cuda))
+        eng.sync_shadow()
+        for _ in range(2):
+            eng.feed_x().copy_(torch.rand(B, 784, device=cuda))
+            eng.feed_y().copy_(torch.randint(0, 10, (B,), device=cuda, dtype=torch.int32))
+            eng.train_step()
+        eng.set_dtype("bf16")
+    torch.cuda.synchronize()
+    assert not torch.equal(eng.params().cpu(), p0)
+    assert torch.equal(eng.params_bf16().cpu(), eng.params().cpu().to(torch.bfloat16))
