@@ -10,4 +10,4 @@ rm -rf gpurun_out/r5_prof_f32
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_prof_f32 -o run -- python3 bench.py --dtype fp32 --steps 300 --warmup 20 --phases 0 --min_warmup_ms 0 --state_steps 0 > gpurun_out/r5_prof_f32.log 2>&1 || { tail gpurun_out/r5_prof_f32.log; exit 1; }
 db=$(find gpurun_out/r5_prof_f32 -name "*.db" | head -1)
 python scripts/prof_summary.py $db --min-calls 100
-python scripts/prof_timeline.py $db --anchor adam | tail -12
+python scripts/prof_timeline.py $db --anchor mnist_adam | tail -12
