@@ -19,34 +19,49 @@ namespace {
 constexpr int kOptThreads = 256;
 constexpr int kOptMaxBlocks = 2048;
 
+struct AdamItem {
+  f32x4 p, m, v, g;
+};
+__device__ __forceinline__ AdamItem adam_load4(const AdamArgs& a, int64_t i) {
+  AdamItem x;
+  x.p = reinterpret_cast<const f32x4*>(a.p)[i];
+  x.m = reinterpret_cast<const f32x4*>(a.m)[i];
+  x.v = reinterpret_cast<const f32x4*>(a.v)[i];
+  if (a.gbf) {
+    const uint2 gb = reinterpret_cast<const uint2*>(a.gbf)[i];
+    x.g = f32x4{bf2f((uint16_t)(gb.x & 0xFFFF)), bf2f((uint16_t)(gb.x >> 16)), bf2f((uint16_t)(gb.y & 0xFFFF)),
+                bf2f((uint16_t)(gb.y >> 16))};
+  } else {
+    x.g = reinterpret_cast<const f32x4*>(a.g)[i];
+  }
+  return x;
+}
+__device__ __forceinline__ void adam_apply4(const AdamArgs& a, int64_t i, AdamItem x, float lr_t, float c1, float c2) {
+  const f32x4 g = x.g * a.grad_scale;
+  f32x4 p = x.p, m = x.m, v = x.v;
+  m = m + (g - m) * c1;
+  v = v + (g * g - v) * c2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) p[j] -= lr_t * m[j] / (sqrtf(v[j]) + a.eps);
+  reinterpret_cast<f32x4*>(a.p)[i] = p;
+  reinterpret_cast<f32x4*>(a.m)[i] = m;
+  reinterpret_cast<f32x4*>(a.v)[i] = v;
+  if (a.pbf) reinterpret_cast<uint2*>(a.pbf)[i] = make_uint2(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]));
+}
 __global__ __launch_bounds__(kOptThreads) void adam_kernel(AdamArgs a) {
+  // the first item's operands are loaded before t (a dependent load of the step counter) is awaited
+  const int64_t n4 = a.n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * kOptThreads;
+  const int64_t i0 = (int64_t)blockIdx.x * kOptThreads + threadIdx.x;
+  AdamItem x{};
+  if (i0 < n4) x = adam_load4(a, i0);
   const int64_t t = (a.step ? *a.step : 0) + a.t_offset;
   const float b1p = powf(a.beta1, (float)t), b2p = powf(a.beta2, (float)t);
   const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float c1 = 1.f - a.beta1, c2 = 1.f - a.beta2;
-  const int64_t n4 = a.n >> 2;
-  const int64_t stride = (int64_t)gridDim.x * kOptThreads;
-  for (int64_t i = (int64_t)blockIdx.x * kOptThreads + threadIdx.x; i < n4; i += stride) {
-    f32x4 p = reinterpret_cast<f32x4*>(a.p)[i];
-    f32x4 m = reinterpret_cast<f32x4*>(a.m)[i];
-    f32x4 v = reinterpret_cast<f32x4*>(a.v)[i];
-    f32x4 g;
-    if (a.gbf) {
-      const uint2 gb = reinterpret_cast<const uint2*>(a.gbf)[i];
-      g = f32x4{bf2f((uint16_t)(gb.x & 0xFFFF)), bf2f((uint16_t)(gb.x >> 16)), bf2f((uint16_t)(gb.y & 0xFFFF)),
-                bf2f((uint16_t)(gb.y >> 16))};
-    } else {
-      g = reinterpret_cast<const f32x4*>(a.g)[i];
-    }
-    g *= a.grad_scale;
-    m = m + (g - m) * c1;
-    v = v + (g * g - v) * c2;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) p[j] -= lr_t * m[j] / (sqrtf(v[j]) + a.eps);
-    reinterpret_cast<f32x4*>(a.p)[i] = p;
-    reinterpret_cast<f32x4*>(a.m)[i] = m;
-    reinterpret_cast<f32x4*>(a.v)[i] = v;
-    if (a.pbf) reinterpret_cast<uint2*>(a.pbf)[i] = make_uint2(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]));
+  for (int64_t i = i0; i < n4; i += stride) {
+    if (i != i0) x = adam_load4(a, i);
+    adam_apply4(a, i, x, lr_t, c1, c2);
   }
   // scalar tail (n % 4)
   for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * kOptThreads + threadIdx.x; i < a.n; i += stride) {
@@ -64,39 +79,27 @@ struct AdamRanges {
   int64_t beg4[3], pre4[4];  // range starts and prefix sums in float4 units
   int64_t tail_beg, tail_n;  // the last range's n % 4 scalar elements
 };
-__device__ __forceinline__ void adam_elem4(const AdamArgs& a, int64_t i, float lr_t, float c1, float c2) {
-  f32x4 p = reinterpret_cast<f32x4*>(a.p)[i];
-  f32x4 m = reinterpret_cast<f32x4*>(a.m)[i];
-  f32x4 v = reinterpret_cast<f32x4*>(a.v)[i];
-  f32x4 g;
-  if (a.gbf) {
-    const uint2 gb = reinterpret_cast<const uint2*>(a.gbf)[i];
-    g = f32x4{bf2f((uint16_t)(gb.x & 0xFFFF)), bf2f((uint16_t)(gb.x >> 16)), bf2f((uint16_t)(gb.y & 0xFFFF)),
-              bf2f((uint16_t)(gb.y >> 16))};
-  } else {
-    g = reinterpret_cast<const f32x4*>(a.g)[i];
-  }
-  g *= a.grad_scale;
-  m = m + (g - m) * c1;
-  v = v + (g * g - v) * c2;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) p[j] -= lr_t * m[j] / (sqrtf(v[j]) + a.eps);
-  reinterpret_cast<f32x4*>(a.p)[i] = p;
-  reinterpret_cast<f32x4*>(a.m)[i] = m;
-  reinterpret_cast<f32x4*>(a.v)[i] = v;
-  if (a.pbf) reinterpret_cast<uint2*>(a.pbf)[i] = make_uint2(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]));
-}
 // same per-element math as adam_kernel, over a table of ranges (the logical float4 index is mapped
 // to its range by the prefix sums)
 __global__ __launch_bounds__(kOptThreads) void adam_ranges_kernel(AdamArgs a, AdamRanges r) {
+  // the first item's operands are loaded before t (a dependent load of the step counter) is awaited:
+  // for the small conv + output-layer launch of the DP step that is one memory round trip of its ~3
+  const int64_t stride = (int64_t)gridDim.x * kOptThreads;
+  auto phys = [&](int64_t i) {
+    const int k = i < r.pre4[1] ? 0 : (r.nr > 2 && i >= r.pre4[2] ? 2 : 1);
+    return r.beg4[k] + (i - r.pre4[k]);
+  };
+  int64_t i = (int64_t)blockIdx.x * kOptThreads + threadIdx.x;
+  AdamItem x{};
+  if (i < r.pre4[r.nr]) x = adam_load4(a, phys(i));
   const int64_t t = (a.step ? *a.step : 0) + a.t_offset;
   const float b1p = powf(a.beta1, (float)t), b2p = powf(a.beta2, (float)t);
   const float lr_t = a.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float c1 = 1.f - a.beta1, c2 = 1.f - a.beta2;
-  const int64_t stride = (int64_t)gridDim.x * kOptThreads;
-  for (int64_t i = (int64_t)blockIdx.x * kOptThreads + threadIdx.x; i < r.pre4[r.nr]; i += stride) {
-    const int k = i < r.pre4[1] ? 0 : (r.nr > 2 && i >= r.pre4[2] ? 2 : 1);
-    adam_elem4(a, r.beg4[k] + (i - r.pre4[k]), lr_t, c1, c2);
+  for (; i < r.pre4[r.nr]; i += stride) {
+    const int64_t pi = phys(i);
+    if (i != (int64_t)blockIdx.x * kOptThreads + threadIdx.x) x = adam_load4(a, pi);
+    adam_apply4(a, pi, x, lr_t, c1, c2);
   }
   if (blockIdx.x == 0 && threadIdx.x < r.tail_n) {
     const int64_t i = r.tail_beg + threadIdx.x;
