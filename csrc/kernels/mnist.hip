@@ -1371,6 +1371,17 @@ constexpr int MAD_FC_BLOCKS = 1024;  // grid-stride blocks of the fc-region Adam
 constexpr int MAD_CONV = MAD_C1BLK + MAD_C2BLK;
 static_assert(MAD_C1F4 % 16 == 0, "conv1 region: whole blocks");
 constexpr int MAD_SL = 16;  // slab loads in flight per thread
+__device__ __forceinline__ void adam4_pre(const MnistAdamArgs& o, int64_t i, f32x4 p, f32x4 m, f32x4 v, f32x4 g,
+                                          float lr_t, float c1, float c2) {
+  m = m + (g - m) * c1;
+  v = v + (g * g - v) * c2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) p[j] -= lr_t * m[j] / (sqrtf(v[j]) + o.eps);
+  reinterpret_cast<f32x4*>(o.p)[i] = p;
+  reinterpret_cast<f32x4*>(o.m)[i] = m;
+  reinterpret_cast<f32x4*>(o.v)[i] = v;
+  if (o.pbf) reinterpret_cast<uint2*>(o.pbf)[i] = make_uint2(pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]));
+}
 __device__ __forceinline__ void adam4(const MnistAdamArgs& o, int64_t i, f32x4 g, float lr_t, float c1, float c2) {
   f32x4 p = reinterpret_cast<f32x4*>(o.p)[i];
   f32x4 m = reinterpret_cast<f32x4*>(o.m)[i];
@@ -1410,9 +1421,13 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
   const int grid = (int)gridDim.x - gb;
   // grid == MAD_CONV: the conv region only; the last conv2 block bumps the step
   if (grid == MAD_CONV && (int)blockIdx.x - gb == grid - 1 && threadIdx.x == 0) *o.step += 1;
-  const int64_t t = *o.t;
-  const float b1p = powf(o.beta1, (float)t), b2p = powf(o.beta2, (float)t);
-  const float lr_t = o.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  // t (a dependent load of the head's step counter) is awaited only where the update needs it,
+  // after this thread's first operand loads are out (the optimizer's first memory round trip)
+  auto lr_of = [&]() {
+    const int64_t t = *o.t;
+    const float b1p = powf(o.beta1, (float)t), b2p = powf(o.beta2, (float)t);
+    return o.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  };
   const float c1 = 1.f - o.beta1, c2 = 1.f - o.beta2;
   const int bid = (int)blockIdx.x - gb, tid = threadIdx.x;
   if (bid < MAD_CONV) {
@@ -1432,7 +1447,7 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
       const int nq = one ? 16 : 4, qs = one ? 16 : 64;
       f32x4 s = red[x];
       for (int k = 1; k < nq; ++k) s += red[k * qs + x];
-      adam4(o, i, s, lr_t, c1, c2);
+      adam4(o, i, s, lr_of(), c1, c2);
     }
   } else {
     const int64_t i0 = fcb4 + (int64_t)(bid - MAD_CONV) * MAD_NT + tid;  // fcb4: MAD_C2END, or the out layer
@@ -1442,6 +1457,7 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
     // streaming non-temporal loads/stores were +0.9 us: the next step re-reads p/m/v from MALL)
     if (o.gbf) {
       constexpr int U = ADAM_U;
+      const float lr_t = lr_of();
       for (int64_t base = i0; base < TOTAL / 4; base += STRIDE * U) {
         uint2 h[U];
         f32x4 p[U], m[U], v[U];
@@ -1473,7 +1489,18 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
         }
       }
     } else {
-      for (int64_t i = i0; i < TOTAL / 4; i += STRIDE) adam4(o, i, reinterpret_cast<const f32x4*>(a.grad)[i], lr_t, c1, c2);
+      // the first item's p / m / v / g are loaded before t is awaited
+      f32x4 p0 = {}, m0 = {}, v0 = {}, g0 = {};
+      if (i0 < TOTAL / 4) {
+        p0 = reinterpret_cast<const f32x4*>(o.p)[i0];
+        m0 = reinterpret_cast<const f32x4*>(o.m)[i0];
+        v0 = reinterpret_cast<const f32x4*>(o.v)[i0];
+        g0 = reinterpret_cast<const f32x4*>(a.grad)[i0];
+      }
+      const float lr_t = lr_of();
+      if (i0 < TOTAL / 4) adam4_pre(o, i0, p0, m0, v0, g0, lr_t, c1, c2);
+      for (int64_t i = i0 + STRIDE; i < TOTAL / 4; i += STRIDE)
+        adam4(o, i, reinterpret_cast<const f32x4*>(a.grad)[i], lr_t, c1, c2);
     }
     if (bid == grid - 1 && tid == 0) *o.step += 1;  // see MnistAdamArgs
   }
