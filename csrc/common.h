@@ -36,6 +36,24 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// x[c] += x[c] of the DPP source lane (masked-off lanes add 0), N independent values interleaved
+template <int CTRL, int RMASK, int BMASK, int N>
+__device__ __forceinline__ void dpp_add(float (&x)[N]) {
+#pragma unroll
+  for (int c = 0; c < N; ++c)
+    x[c] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x[c]), CTRL, RMASK, BMASK, true));
+}
+// N wave sums at once by DPP (quad swaps, row shifts, row broadcasts: no LDS round trips, unlike
+// the shuffle-based wave_sum); the wave's totals land in lane 63
+template <int N>
+__device__ __forceinline__ void wave_sums_to_lane63(float (&x)[N]) {
+  dpp_add<0xB1, 0xF, 0xF>(x);   // quad_perm [1,0,3,2]
+  dpp_add<0x4E, 0xF, 0xF>(x);   // quad_perm [2,3,0,1]
+  dpp_add<0x114, 0xF, 0xE>(x);  // row_shr:4, banks 1-3
+  dpp_add<0x118, 0xF, 0xC>(x);  // row_shr:8, banks 2-3
+  dpp_add<0x142, 0xA, 0xF>(x);  // row_bcast:15 into rows 1, 3
+  dpp_add<0x143, 0xC, 0xF>(x);  // row_bcast:31 into rows 2, 3
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -407,12 +407,6 @@ __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   do {                                                                                                   \
     if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[4 * a.B * 8 + blockIdx.x * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \
   } while (0)
-template <int CTRL, int RMASK, int BMASK, int N>
-__device__ __forceinline__ void dpp_add(float (&x)[N]) {  // x += x[DPP source lane]; masked-off lanes add 0
-#pragma unroll
-  for (int c = 0; c < N; ++c)
-    x[c] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x[c]), CTRL, RMASK, BMASK, true));
-}
 __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   HEAD_STAMP(0);
   const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -457,12 +451,7 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   __shared__ float red[4][NCLS];
   // DPP wave sums (quad swaps, row shifts, row broadcasts: no LDS round trips) of the 10 partials,
   // interleaved; the wave total lands in lane 63
-  dpp_add<0xB1, 0xF, 0xF>(lp);   // quad_perm [1,0,3,2]
-  dpp_add<0x4E, 0xF, 0xF>(lp);   // quad_perm [2,3,0,1]
-  dpp_add<0x114, 0xF, 0xE>(lp);  // row_shr:4, banks 1-3
-  dpp_add<0x118, 0xF, 0xC>(lp);  // row_shr:8, banks 2-3
-  dpp_add<0x142, 0xA, 0xF>(lp);  // row_bcast:15 into rows 1, 3
-  dpp_add<0x143, 0xC, 0xF>(lp);  // row_bcast:31 into rows 2, 3
+  wave_sums_to_lane63(lp);
   if (lane == 63) {
 #pragma unroll
     for (int c = 0; c < NCLS; ++c) red[wv][c] = lp[c];

@@ -222,7 +222,7 @@ __global__ __launch_bounds__(512) void f32_conv12_fwd_lds(MnistF32Args a) {
   }
 }
 
-constexpr int F_BK = 32;  // K-tile of the fp32 GEMM blocks (64: 188 vs 172 us/step, fewer blocks per CU; profiles/mnist_fp32_r5.log)
+constexpr int F_BK = 32;  // K-tile of the fp32 GEMM blocks (64: 188 vs 172 us/step, fewer blocks per CU; profiles/mnist_fp32_kernels_r5.txt)
 
 // ---------------- K4: fc1 forward, split-K slabs (reduced by the head) ----------------
 struct SlabEpiF {
@@ -285,10 +285,10 @@ __global__ __launch_bounds__(256) void f32_head(MnistF32Args a, int train) {
     for (int c = 0; c < NCLS; ++c) lp[c] = fmaf(hd[j], wr[c], lp[c]);
   }
   __shared__ float red[4][NCLS];
+  wave_sums_to_lane63(lp);  // DPP, interleaved over the 10 classes (was 10 shuffle-based wave sums)
+  if (lane == 63) {
 #pragma unroll
-  for (int c = 0; c < NCLS; ++c) {
-    const float v = wave_sum(lp[c]);
-    if (lane == 0) red[wv][c] = v;
+    for (int c = 0; c < NCLS; ++c) red[wv][c] = lp[c];
   }
   __syncthreads();
   float logit[NCLS];

@@ -972,6 +972,18 @@ class MnistEngine : public torch::CustomClassHolder {
     std::vector<hipGraphNode_t> fresh;
     for (auto nd_ : nodes)
       if (topo_seen_.insert(nd_).second) fresh.push_back(nd_);
+    if (fresh.empty()) {
+      // An operation that captured no node -- a world-1 in-place RCCL collective is a no-op -- gets
+      // a marker: an empty kernel at the operation's place in its stream, with the dependencies the
+      // collective would have had and the same successors. The checker then orders the schedule's
+      // cross-stream waits around every RCCL collective too, not only around the IPC ones.
+      noop_launch(1, st);
+      HIP_OK(hipGraphGetNodes(g, nullptr, &n));
+      nodes.resize(n);
+      HIP_OK(hipGraphGetNodes(g, nodes.data(), &n));
+      for (auto nd_ : nodes)
+        if (topo_seen_.insert(nd_).second) fresh.push_back(nd_);
+    }
     topo_tags_.emplace_back(std::string(label) + "@" + std::to_string(topo_step_), std::move(fresh));
   }
 

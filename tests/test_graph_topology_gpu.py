@@ -63,8 +63,10 @@ def test_one_gpu_step_topology(cuda):
 @pytest.mark.parametrize("sched", list(SCHEDULES))
 def test_forced_dp_world1_topology(cuda, sched, mode):
     """The multi-GPU schedules over a real world-1 communicator: every collective ordered after its
-    producer and before its consumers, 3 steps. (A world-1 in-place RCCL collective may capture no
-    node at all -- nothing to order -- so only the IPC transport must show a node per collective.)"""
+    producer and before its consumers, 3 steps. A world-1 in-place RCCL collective captures no node
+    of its own; the topology capture puts a marker kernel at its place in the comm stream
+    (MnistEngine::tag), so the RCCL schedule's edges are checked like the IPC one's, and dropping one
+    of its cross-stream waits must be caught over both transports."""
     from tensorflow_distributed_amd.parallel.transport import attach_engine
 
     sfb, zero, mr = SCHEDULES[sched]
@@ -76,18 +78,17 @@ def test_forced_dp_world1_topology(cuda, sched, mode):
             e.set_zero(True)
         e.set_sfb_merge_reduce(mr)
         e.train_step()
-        t, v = _check(e, 3, require_nodes=mode == "ipc")
+        t, v = _check(e, 3)
         assert v == [], (sched, v)
         labels = {lb for lb, _, _ in t.tags}
         want = {"gather_p2", "gather_dr", "ar_conv", "sfb_gemm"} if sfb else {"ar_fc", "ar_conv", "opt_fc"}
         assert want <= labels, labels
         if zero:
             assert "wag" in labels
-        if mode == "ipc":  # fault injection: the schedule without one of its cross-stream waits is caught
-            # (over world-1 RCCL the in-place gathers capture no node, so there is nothing to miss)
-            drop = "sfb_gemm<-gather_dr" if sfb else "fc_fwd<-opt_fc"
-            _, v2 = _check(e, 2, drop, require_nodes=False)
-            assert v2, f"dropping {drop} went unnoticed"
+        # fault injection: the schedule without one of its cross-stream waits is caught
+        drop = "sfb_gemm<-gather_dr" if sfb else "fc_fwd<-opt_fc"
+        _, v2 = _check(e, 2, drop)
+        assert v2, f"dropping {drop} went unnoticed"
         e.train_step()  # the engine still runs normally afterwards
     torch.cuda.synchronize()
     tr.check()

@@ -163,3 +163,43 @@ def test_fp32_tail_leaves_no_stale_shadow_after_switching_to_bf16(cuda):
     torch.cuda.synchronize()
     assert not torch.equal(eng.params().cpu(), p0)
     assert torch.equal(eng.params_bf16().cpu(), eng.params().cpu().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("mode", ["rccl", "ipc"])
+def test_fp32_forced_dp_world1_equals_the_unfused_step(cuda, mode):
+    """The fp32 engine's DP schedule (slab reduce, fp32 wire all-reduce over a real world-1
+    communicator, optimizer with 1/N) against the one-GPU step with the unfused optimizer: the same
+    kernels and sums, so three steps leave the parameters and Adam state bit-identical."""
+    from tensorflow_distributed_amd.parallel.transport import attach_engine
+
+    B = 64
+    g = torch.Generator().manual_seed(17)
+    xs = torch.rand(3, B, 784, generator=g)
+    ys = torch.randint(0, 10, (3, B), generator=g, dtype=torch.int32)
+    p0 = M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(8).items()})
+    engs, trs = [], []
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for dp in (False, True):
+            e = _engine(B, cuda, 0.75)
+            e.set_adam(0.01, 0.9, 0.999, 1e-8)
+            e.set_fused_tail(0)
+            if dp:
+                trs.append(attach_engine(e, 0, 1, cuda, mode=mode, force_dp=True, bf16=False))
+            e.params().copy_(p0.to(cuda))
+            e.sync_shadow()
+            for i in range(3):
+                e.feed_x().copy_(xs[i].to(cuda))
+                e.feed_y().copy_(ys[i].to(cuda))
+                e.train_step()
+            engs.append(e)
+    torch.cuda.synchronize()
+    for tr in trs:
+        tr.check()
+    ref, dp = engs
+    assert int(ref.step_tensor().item()) == int(dp.step_tensor().item()) == 3
+    assert not torch.equal(ref.params().cpu(), p0)
+    for get in ("params", "adam_m", "adam_v"):
+        assert torch.equal(getattr(ref, get)(), getattr(dp, get)()), get
+    for tr in trs:
+        tr.close()
