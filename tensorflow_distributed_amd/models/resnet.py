@@ -18,8 +18,6 @@ Execution model (MI355X-first, not a framework-module port):
 """
 from __future__ import annotations
 
-import os
-
 import math
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
@@ -162,9 +160,9 @@ class BucketReducer:
         self.launched = 0
 
     def mark_ready(self, name: str):
-        """Called from inside backward (the autograd engine's thread): a bucket whose last gradient
-        just landed only records its ready event on the compute stream -- the point its collective
-        will wait for. The side-stream work itself is issued by finish() on the caller's thread.
+        """Called from inside backward (ResNet.train_step runs it on the caller's thread): a bucket
+        whose last gradient just landed only records its ready event on the compute stream -- the
+        point its collective will wait for. The side-stream work itself is issued by finish().
 
         Issuing it here instead (stream switch, wait, collective launch on the autograd thread)
         corrupted the host heap once a CUDA graph captured over it was destroyed: glibc aborts
@@ -896,7 +894,13 @@ class ResNet:
         self.grads_zeroed = True
         try:
             loss, _ = self.loss(x, labels)
-            loss.backward()
+            # backward on THIS thread, not the autograd engine's device thread: the bucket hooks
+            # (BucketReducer.mark_ready) record their ready events inside backward, and stream work
+            # issued from the engine's thread into a capture owned by this thread broke the host heap
+            # once the captured graph was destroyed (profiles/heap_bisect_r5.log; the event record
+            # alone still did, about once in 100+ RCCL capture / destroy cycles)
+            with torch.autograd.set_multithreading_enabled(False):  # same speed (profiles/resnet50_backward_thread_ab_r5.log)
+                loss.backward()
         finally:
             self.grads_zeroed = False
         self.reducer.finish()
