@@ -554,12 +554,24 @@ struct Tile {
 template <int BM, int BN>
 constexpr int conv_rs() { return 1; }
 constexpr int CBK = 64;
-template <int BM, int BN, class LA, class LB, class EPI>
+// XR: renumber the blocks so that each XCD runs a run of consecutive (n, m, split) tiles -- dispatch
+// deals block ids round-robin over the 8 XCDs, which puts the n-tiles sharing one A chunk (and the
+// m-tiles sharing one B chunk) on different XCDs, each L2 fetching the chunk from the fabric.
+template <int BM, int BN, class LA, class LB, class EPI, bool XR = false>
 __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int kchunk, int KD) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  const int kb = blockIdx.z * kchunk, ke = min(KD, kb + kchunk);
-  gemm_block<BM, BN, CBK, 2, 2, LA, LB, EPI, conv_rs<BM, BN>()>(la, lb, epi, blockIdx.y * BM, blockIdx.x * BN, kb, ke,
-                                                         (bf16*)smem_raw);
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if constexpr (XR) {
+    const int nx = gridDim.x, ny = gridDim.y, total = nx * ny * gridDim.z;
+    if ((total & 7) == 0) {
+      const int id = bx + nx * (by + ny * bz), l = (id & 7) * (total >> 3) + (id >> 3);
+      bx = l % nx;
+      by = (l / nx) % ny;
+      bz = l / (nx * ny);
+    }
+  }
+  const int kb = bz * kchunk, ke = min(KD, kb + kchunk);
+  gemm_block<BM, BN, CBK, 2, 2, LA, LB, EPI, conv_rs<BM, BN>()>(la, lb, epi, by * BM, bx * BN, kb, ke, (bf16*)smem_raw);
 }
 
 
@@ -693,12 +705,12 @@ OutTile out_tile(int M, int N) {
 }
 int out_tile_rows(int M, int N) { return out_tile(M, N) == OT64 ? (M + 63) / 64 : (M + 127) / 128; }
 
-template <int BM, int BN, class LA, class LB, class EPI>
+template <int BM, int BN, bool XR = false, class LA, class LB, class EPI>
 void launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N, int KD, int splits, hipStream_t st) {
   constexpr int sm = GemmSmem<BM, BN, CBK, LA, LB>::BYTES;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BM, BN, LA, LB, EPI>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BM, BN, LA, LB, EPI, XR>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, sm);
     attr = true;
   }
@@ -706,7 +718,7 @@ void launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K
   int kchunk = ((KD + splits - 1) / splits + CBK - 1) / CBK * CBK;
   splits = (KD + kchunk - 1) / kchunk;
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, splits);
-  gemm_kernel<BM, BN, LA, LB, EPI><<<grid, 256, sm, st>>>(la, lb, epi, kchunk, KD);
+  gemm_kernel<BM, BN, LA, LB, EPI, XR><<<grid, 256, sm, st>>>(la, lb, epi, kchunk, KD);
 }
 
 // pick 128x128 tiles when the problem has enough of them to fill the chip, else 64x64
@@ -1386,13 +1398,18 @@ int conv_wgrad_splits(const ConvShape& c, bool folded) {
   return s;
 }
 
+// Weight gradients run with the per-XCD block renumbering (gemm_kernel<XR>): ResNet-50 b128 12.98 ->
+// 12.82-12.90 ms/step, l1 1x1 64->256 61 -> 44 us, l2 downsample 78 -> 63 us. Measured and not kept
+// (profiles/resnet50_wgrad_ab_r5.log): two register stages, more or fewer splits, an LDS-staged atomic
+// epilogue, 8-wave blocks halving each split's K over two 4-wave groups, the 256-row core with
+// re-tuned splits.
 template <class LA>
 static void wgrad_launch(const ConvShape& c, const LA& la, const DenseX<false>& lb, const AccF32& epi, int MT, int P,
                          int splits, hipStream_t st) {
   switch (wgrad_tile(c)) {
-    case WG128x128: launch_gemm<128, 128>(la, lb, epi, MT, c.K, P, splits, st); break;
-    case WG128x64: launch_gemm<128, 64>(la, lb, epi, MT, c.K, P, splits, st); break;
-    default: launch_gemm<64, 64>(la, lb, epi, MT, c.K, P, splits, st);
+    case WG128x128: launch_gemm<128, 128, true>(la, lb, epi, MT, c.K, P, splits, st); break;
+    case WG128x64: launch_gemm<128, 64, true>(la, lb, epi, MT, c.K, P, splits, st); break;
+    default: launch_gemm<64, 64, true>(la, lb, epi, MT, c.K, P, splits, st);
   }
 }
 

@@ -99,6 +99,23 @@ def test_conv_fwd_dgrad_wgrad(cuda, N, H, W, C, K, R, st, pad):
     assert relerr(dw2.cpu(), wr.grad.permute(2, 3, 1, 0)) < 1e-3
 
 
+@pytest.mark.parametrize("N,H,W,C,K,R,st,pad", [(32, 14, 14, 256, 1024, 1, 1, 0), (64, 7, 7, 512, 2048, 1, 1, 0),
+                                                  (16, 14, 14, 128, 128, 3, 1, 1), (32, 14, 14, 256, 128, 1, 2, 0)])
+def test_conv_wgrad_long_split_k(cuda, N, H, W, C, K, R, st, pad):
+    """Weight gradients of ResNet-50 stage-3/4 shapes: 33-49 K-tiles per split and (tile x split)
+    grids divisible by 8 (the XCD renumbering of the wgrad launch), against the fp32 oracle."""
+    torch.manual_seed(1)
+    x = rb(torch.randn(N, H, W, C))
+    Ho = (H + 2 * pad - R) // st + 1
+    dy = rb(torch.randn(N, Ho, Ho, K))
+    ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2), (K, C, R, R), dy.permute(0, 3, 1, 2),
+                                      stride=st, padding=pad)
+    for zeroed in (False, True):
+        dw = torch.zeros(R, R, C, K, device=cuda)
+        ops.conv2d_wgrad(x.to(cuda, torch.bfloat16), dy.to(cuda, torch.bfloat16), dw, st, pad, zeroed)
+        assert relerr(dw.cpu(), ref.permute(2, 3, 1, 0)) < 1e-5
+
+
 @pytest.mark.parametrize("N,H,W,C,K,R,st,pad", CONVS + HALO + [(8, 28, 28, 64, 256, 1, 1, 0), (48, 28, 28, 32, 64, 3, 1, 1)])
 def test_conv_fwd_stats_feeds_bn(cuda, bn_mode, N, H, W, C, K, R, st, pad):
     """conv2d_fwd_stats: same output as conv2d_fwd, and per-row-block sums of the stored bf16 output
