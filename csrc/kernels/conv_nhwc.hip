@@ -1369,9 +1369,12 @@ WgTile wgrad_tile(const ConvShape& c) {
 }
 
 // split-K of a weight gradient: about kWgradBlocks (tile x split) blocks, each split keeping at least
-// kWgradMinPx pixels of K (1,024: 13.79 vs 13.80 ms, 512: 13.90, profiles/resnet50_wgrad_minpx_ab_r3.log;
-// the 64x64-tile target: profiles/resnet50_wgrad_small_splits_ab_r4.log)
-constexpr int kWgradMinPx = 2048, kWgradBlocks = 512, kWgradBlocksSmall = 512;
+// kWgradMinPx pixels of K (round 3, 2,048: 13.80 ms, 1,024: 13.79, 512: 13.90,
+// profiles/resnet50_wgrad_minpx_ab_r3.log; round 5 with the per-XCD renumbering, 3 interleaved rounds:
+// 1,024 vs 2,048 ResNet-50 12.82-12.85 vs 12.86-12.92 ms, ResNet-18 4.74-4.76 vs 4.83; a 256-block
+// target +0.6 ms, profiles/resnet50_wgrad_ab_r5.log; the 64x64-tile target:
+// profiles/resnet50_wgrad_small_splits_ab_r4.log)
+constexpr int kWgradMinPx = 1024, kWgradBlocks = 512, kWgradBlocksSmall = 512;
 // weight gradients on the 256-row core: mode 2 only (the A/B switch)
 static bool use_g256_wgrad(const ConvShape& c) {
   const int mode = g256_mode(), P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
