@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 VARS=${VARS:-"0 1 2 3 4"}
 for v in $VARS; do
   cp variants/_C_v$v.so tensorflow_distributed_amd/_C.so || exit 1
-  timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_ops_gpu.py -k "wgrad" > gpurun_out/ws_t$v.log 2>&1 || { echo "v$v tests failed"; tail -20 gpurun_out/ws_t$v.log; exit 1; }
+  timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_ops_gpu.py -k "${TESTK:-wgrad}" > gpurun_out/ws_t$v.log 2>&1 || { echo "v$v tests failed"; tail -20 gpurun_out/ws_t$v.log; exit 1; }
 done
 for r in 1 2 3; do
   for v in $VARS; do
