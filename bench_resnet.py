@@ -55,6 +55,8 @@ def main(argv=None):
                     "conv's dgrad epilogue as (dout, relu bits), the residual BN backward writes no dres tensor")
     ap.add_argument("--fuse_stem_pool", type=int, default=1, help="1: the stem's bn + relu + max pool in one pass "
                     "(the BN output is never written)")
+    ap.add_argument("--stem_w2", type=int, default=1, help="1: the stem conv on width-paired input pixels "
+                    "(7x4x8 instead of 7x7x8 MACs per output, models/resnet.py _StemW2); 0: channel-padded input")
     ap.add_argument("--bn_slots", type=int, default=-1, help="BN statistics partials: S > 0 fp32 atomics into S "
                     "zeroed slots, finalized inside the apply passes (no bn_final launches); 0 per-block rows + "
                     "bn_final (fixed order); -1 the library default")
@@ -99,6 +101,7 @@ def main(argv=None):
     m.relu_bits = bool(a.relu_bits)
     m.masked_join = bool(a.masked_join)
     m.fuse_stem_pool = bool(a.fuse_stem_pool)
+    m.stem_w2 = bool(a.stem_w2)
     comm, transport, small = None, "none", None
     if ctx.world > 1:
         if ctx.comm is not None:  # one rank per GPU: RCCL over xGMI
@@ -231,6 +234,7 @@ def main(argv=None):
                        "mask_from_y": bool(a.mask_from_y), "relu_bits": bool(a.relu_bits),
                        "bn_bwd_stats": bool(a.bn_bwd_stats), "fold_bn": a.fold_bn, "masked_join": bool(a.masked_join),
                        "fuse_stem_pool": bool(a.fuse_stem_pool),
+                       "stem_w2": bool(a.stem_w2),
                        "bn_slots": int(torch.ops.tfd.bn_part_slots()),
                        "conv_halo": int(torch.ops.tfd.conv_halo_mode(-1)),
                        "bn_stats_mode": ("row: fixed summation order, bit-reproducible"

@@ -411,6 +411,54 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> softmax_xent_op(const at::Tensor&
   return {loss, corr, dl};
 }
 
+// The width-paired stem (ResNet conv1: 7x7, stride 2, pad 3, 3 input channels). stem_pack pairs
+// horizontally adjacent input pixels into one 8-channel pixel ({p0 c0..2, p1 c0..2, 0, 0}); the filter
+// [R][S'][8][K] holds at channel p*3+c of column s' the original tap s = 2s' + p + pad - 2*pw (pw = (pad+1)/2:
+// s = 2s' + p - 1 at pad 3, tap -1 zero). The conv is then R x S' x 8 with the height stride / pad and width
+// stride 1, left pad pw: 7 x 4 x 8 = 224 MACs per output element instead of 7 x 7 x 8 = 392 over the
+// channel-padded input, and the packed input is half the bytes.
+ConvShape w2_shape(const at::Tensor& xp, const at::Tensor& wp, int64_t stride, int64_t pad) {
+  ConvShape c = shape_of(xp, wp, stride, pad);
+  TORCH_CHECK(c.C == 8 && stride == 2 && pad % 2 == 1, "w2 conv: paired input [N, H, W/2, 8], stride 2, odd pad");
+  c.stride_w = 1;
+  c.pad_w = (int)(pad + 1) / 2;
+  c.wo_out = (2 * c.W + 2 * (int)pad - (2 * c.S - 1)) / (int)stride + 1;
+  return c;
+}
+
+at::Tensor stem_pack_op(const at::Tensor& x) {
+  check_f32(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 3 && x.size(2) % 2 == 0 && x.is_contiguous(),
+              "stem_pack: x must be contiguous fp32 [N, H, W (even), 3]");
+  auto y = at::empty({x.size(0), x.size(1), x.size(2) / 2, 8}, x.options().dtype(at::kBFloat16));
+  stem_pack_w2(fp(x), bp(y), x.numel() / 6, cur());
+  return y;
+}
+
+std::tuple<at::Tensor, at::Tensor> conv2d_fwd_stats_w2(const at::Tensor& xp, const at::Tensor& wp, int64_t stride,
+                                                       int64_t pad, const c10::optional<at::Tensor>& part_out) {
+  check_bf16(xp, "x", 4);
+  check_bf16(wp, "w", 4);
+  const ConvShape c = w2_shape(xp, wp, stride, pad);
+  auto y = at::empty({c.N, c.Ho(), c.Wo(), c.K}, xp.options());
+  auto part = part_buffer(part_out, conv_fwd_stats_rows(c, false), c.K, xp.options(), "conv2d_fwd_stats_w2");
+  conv_fwd_stats(c, bp(xp), bp(wp), bp(y), fp(part), cur(), nullptr);
+  return {y, part};
+}
+
+void conv2d_wgrad_w2(const at::Tensor& xp, const at::Tensor& dy, at::Tensor dwp, int64_t stride, int64_t pad,
+                     bool zeroed) {
+  check_bf16(xp, "x", 4);
+  check_bf16(dy, "dy", 4);
+  check_f32(dwp, "dw");
+  TORCH_CHECK(dwp.dim() == 4, "dw [R,S',8,K]");
+  auto wfake = at::empty({dwp.size(0), dwp.size(1), dwp.size(2), dwp.size(3)}, xp.options().device(at::kCPU));
+  const ConvShape c = w2_shape(xp, wfake, stride, pad);
+  TORCH_CHECK(dy.size(0) == c.N && dy.size(1) == c.Ho() && dy.size(2) == c.Wo() && dy.size(3) == c.K,
+              "wgrad_w2: dy shape mismatch");
+  conv_wgrad(c, bp(xp), bp(dy), fp(dwp), conv_wgrad_splits(c, false), cur(), zeroed, nullptr);
+}
+
 at::Tensor pad_channels_op(const at::Tensor& x, int64_t cout) {
   check_f32(x, "x");
   const int cin = (int)x.size(-1);
@@ -489,6 +537,12 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.impl("softmax_xent", c10::DispatchKey::CUDA, &softmax_xent_op);
   m.def("pad_channels(Tensor x, int cout) -> Tensor");
   m.impl("pad_channels", c10::DispatchKey::CUDA, &pad_channels_op);
+  m.def("stem_pack(Tensor x) -> Tensor");
+  m.impl("stem_pack", c10::DispatchKey::CUDA, &stem_pack_op);
+  m.def("conv2d_fwd_stats_w2(Tensor x, Tensor w, int stride, int pad, Tensor? part_out=None) -> (Tensor, Tensor)");
+  m.impl("conv2d_fwd_stats_w2", c10::DispatchKey::CUDA, &conv2d_fwd_stats_w2);
+  m.def("conv2d_wgrad_w2(Tensor x, Tensor dy, Tensor(a!) dw, int stride, int pad, bool zeroed=False) -> ()");
+  m.impl("conv2d_wgrad_w2", c10::DispatchKey::CUDA, &conv2d_wgrad_w2);
 }
 
 }  // namespace tfd

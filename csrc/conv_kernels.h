@@ -12,8 +12,14 @@ struct ConvShape {
   int N, H, W, C;   // input NHWC
   int K, R, S;      // output channels, filter rows/cols (HWIO filter [R][S][C][K])
   int stride, pad;  // symmetric zero padding
+  // width-only overrides (forward and weight gradient only; the width-paired stem, conv2d_*_w2):
+  // stride_w 0 = stride, pad_w -1 = pad (left pad; the right edge is the input's end), wo_out 0 = derived
+  int stride_w = 0, pad_w = -1, wo_out = 0;
+  int sw() const { return stride_w ? stride_w : stride; }
+  int pw() const { return pad_w >= 0 ? pad_w : pad; }
+  bool w_override() const { return stride_w != 0 || pad_w >= 0 || wo_out != 0; }
   int Ho() const { return (H + 2 * pad - R) / stride + 1; }
-  int Wo() const { return (W + 2 * pad - S) / stride + 1; }
+  int Wo() const { return wo_out ? wo_out : (W + 2 * pw() - S) / sw() + 1; }
 };
 
 // Forward BN fold: the conv input is relu(bn(x)) of the producing layer (training-mode statistics
@@ -148,6 +154,9 @@ void avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStre
 // over N folded in), correct [N]
 void softmax_xent(const float* logits, const int* labels, float* loss_rows, float* correct, uint16_t* dlogits, int N,
                   int K, hipStream_t s);
-void pad_channels(const float* x, uint16_t* y, int P, int Cin, int Cout, hipStream_t s);  // fp32 NHWC -> bf16, zero-pad C
+void pad_channels(const float* x, uint16_t* y, int P, int Cin, int Cout, hipStream_t s);
+// fp32 NHWC [N][H][W][3] -> bf16 [N][H][W/2][8]: each 8-channel pixel holds two horizontally adjacent
+// input pixels' 3 channels, then 2 zeros (the width-paired stem input)
+void stem_pack_w2(const float* x, uint16_t* y, int64_t pairs, hipStream_t s);  // fp32 NHWC -> bf16, zero-pad C
 
 }  // namespace tfd

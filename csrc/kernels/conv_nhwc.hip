@@ -43,6 +43,7 @@ struct FastDiv {
 
 struct Geo {
   int N, H, W, C, K, R, S, st, pad, Ho, Wo;
+  int stw, padw;  // width stride / left pad (= st / pad except for the width-paired stem)
   int M;       // rows of the GEMM
   int KD;      // reduction length
   uint32_t xbytes, ybytes, wbytes;  // buffer-descriptor ranges of input, output(-gradient), filter
@@ -94,7 +95,7 @@ struct FwdA {
   __device__ __forceinline__ uint32_t off(int m, int k) const {
     const int n = g.howo.div(m), r1 = m - n * g.Ho * g.Wo, ho = g.wo.div(r1), wo = r1 - ho * g.Wo;
     const int tap = g.c.div(k), c = k - tap * g.C, r = g.s.div(tap), s = tap - r * g.S;
-    const int h = ho * g.st - g.pad + r, w = wo * g.st - g.pad + s;
+    const int h = ho * g.st - g.pad + r, w = wo * g.stw - g.padw + s;
     const bool ok = m < g.M && k < g.KD && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
     return boff((uint32_t)((n * g.H + h) * g.W + w) * g.C + c, ok);
   }
@@ -193,7 +194,7 @@ struct WgradA {
   __device__ __forceinline__ uint32_t off(int t, int m) const {
     const int tap = g.c.div(t), c = t - tap * g.C, r = g.s.div(tap), s = tap - r * g.S;
     const int n = g.howo.div(m), r1 = m - n * g.Ho * g.Wo, ho = g.wo.div(r1), wo = r1 - ho * g.Wo;
-    const int h = ho * g.st - g.pad + r, w = wo * g.st - g.pad + s;
+    const int h = ho * g.st - g.pad + r, w = wo * g.stw - g.padw + s;
     const bool ok = t < g.M && m < g.KD && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
     return boff((uint32_t)((n * g.H + h) * g.W + w) * g.C + c, ok);
   }
@@ -762,6 +763,7 @@ void dispatch_bf16_bnb(const LA& la, const LB& lb, uint16_t* y, AddSrc add, int 
 Geo make_geo(const ConvShape& c, int M, int KD) {
   Geo g;
   g.N = c.N; g.H = c.H; g.W = c.W; g.C = c.C; g.K = c.K; g.R = c.R; g.S = c.S; g.st = c.stride; g.pad = c.pad;
+  g.stw = c.sw(); g.padw = c.pw();
   g.Ho = c.Ho(); g.Wo = c.Wo();
   g.M = M; g.KD = KD;
   g.howo = FastDiv(g.Ho * g.Wo); g.wo = FastDiv(g.Wo); g.c = FastDiv(g.C); g.k = FastDiv(g.K); g.s = FastDiv(g.S);
@@ -772,7 +774,7 @@ Geo make_geo(const ConvShape& c, int M, int KD) {
   return g;
 }
 
-bool is_pointwise(const ConvShape& c) { return c.R == 1 && c.S == 1 && c.stride == 1 && c.pad == 0; }
+bool is_pointwise(const ConvShape& c) { return c.R == 1 && c.S == 1 && c.stride == 1 && c.pad == 0 && !c.w_override(); }
 
 // ---------------- the conv GEMMs on the 256-row core (csrc/gemm256.h) ----------------
 // Block tile 256 x BN (BN = 256 / 128 / 64 by the output width), 8 waves, 32x32x16 MFMA, operands
@@ -807,7 +809,7 @@ bool use_g256(int M, int N) {
 // (profiles/halo_probe_r5.log) -- 2 = every eligible shape (tests, probes).
 int g_halo_mode = 1;
 bool use_halo(const ConvShape& c, int cin, int cout) {
-  if (g_halo_mode == 0 || c.R != 3 || c.S != 3 || c.stride != 1 || c.pad != 1) return false;
+  if (g_halo_mode == 0 || c.R != 3 || c.S != 3 || c.stride != 1 || c.pad != 1 || c.w_override()) return false;
   if (cin % HL_CK || cout % 64) return false;
   return g_halo_mode == 2 || c.W >= 32;
 }
@@ -1259,6 +1261,7 @@ static AddSrc make_add(const ConvShape& c, const uint16_t* add, const uint8_t* a
 
 void conv_dgrad(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                 const uint16_t* add, const uint8_t* add_bits, bool add_sub2) {
+  if (c.w_override()) throw std::runtime_error("conv dgrad: width overrides are forward / weight-gradient only");
   const int M = c.N * c.H * c.W;
   if (add_bits && (!add || c.stride != 1))
     throw std::runtime_error("conv_dgrad: a relu-masked add operand needs a stride-1 dgrad");
@@ -1319,6 +1322,7 @@ int conv_dgrad_bn_rows(const ConvShape& c) {
 
 void conv_dgrad_bn(const ConvShape& c, const uint16_t* dy, const uint16_t* w, uint16_t* dx, hipStream_t st,
                    const uint16_t* add, const BnBwdStats& b, float* part, const uint8_t* add_bits, bool add_sub2) {
+  if (c.w_override()) throw std::runtime_error("conv dgrad: width overrides are forward / weight-gradient only");
   if (!conv_dgrad_bn_supported(c)) throw std::runtime_error("conv_dgrad_bn: unsupported conv (C % 8, tap-less phases)");
   if (add_bits && (!add || c.stride != 1))
     throw std::runtime_error("conv_dgrad_bn: a relu-masked add operand needs a stride-1 dgrad");

@@ -801,6 +801,17 @@ __global__ __launch_bounds__(NT) void pad_channels_kernel(const float* __restric
   reinterpret_cast<uint4*>(y)[i] = pack8(f);
 }
 
+// one thread per output pixel pair: 6 contiguous floats in, one 16-B chunk out (same rounding as pad_channels)
+__global__ __launch_bounds__(NT) void stem_pack_w2_kernel(const float* __restrict__ x, uint16_t* __restrict__ y,
+                                                          int64_t pairs) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= pairs) return;
+  const float2* p = reinterpret_cast<const float2*>(x + i * 6);
+  const float2 a = p[0], b = p[1], c = p[2];
+  float f[8] = {a.x, a.y, b.x, b.y, c.x, c.y, 0.f, 0.f};
+  reinterpret_cast<uint4*>(y)[i] = pack8(f);
+}
+
 inline int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + NT - 1) / NT)); }
 
 void launch_apply(const uint16_t* y, const float* gamma, const float* beta, const float* mean, const float* invstd,
@@ -988,6 +999,10 @@ void avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStre
 void softmax_xent(const float* logits, const int* labels, float* loss_rows, float* correct, uint16_t* dlogits, int N,
                   int K, hipStream_t s) {
   softmax_xent_kernel<<<N, NT, 0, s>>>(logits, labels, loss_rows, correct, dlogits, N, K);
+}
+
+void stem_pack_w2(const float* x, uint16_t* y, int64_t pairs, hipStream_t s) {
+  stem_pack_w2_kernel<<<(int)((pairs + NT - 1) / NT), NT, 0, s>>>(x, y, pairs);
 }
 
 void pad_channels(const float* x, uint16_t* y, int P, int Cin, int Cout, hipStream_t s) {

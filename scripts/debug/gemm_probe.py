@@ -38,6 +38,8 @@ SHAPES = [
     ("l3.ds.512-1024.s2", 28, 512, 1024, 1, 2),
     ("l4.3x3.512.s2", 14, 512, 512, 3, 2),
     ("l4.ds.1024-2048.s2", 14, 1024, 2048, 1, 2),
+    # the stem: 3 input channels padded to 8 (pad_channels)
+    ("stem.7x7.8-64.s2", 224, 8, 64, 7, 2),
 ]
 
 

@@ -23,6 +23,7 @@ from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 import torch
+import torch.nn.functional as F
 
 ops = None
 
@@ -398,6 +399,53 @@ class _Conv(torch.autograd.Function):
         return dx, None, None
 
 
+def pair_stem_weight(w: torch.Tensor) -> torch.Tensor:
+    """[R, S, 8, K] stem filter (3 real input channels, S odd, pad 3) -> the width-paired filter
+    [R, (S + 1) // 2, 8, K] of ``conv2d_fwd_stats_w2``: channel p*3 + c of column s' is the original tap
+    s = 2s' + p - 1 (tap -1 is zero), channels 6-7 zero."""
+    R, S, _, K = w.shape
+    wz = F.pad(w[:, :, :3, :], (0, 0, 0, 0, 1, 0))  # [R, S + 1, 3, K]: column 0 is the zero tap
+    return F.pad(wz.reshape(R, (S + 1) // 2, 6, K), (0, 0, 0, 2)).contiguous()
+
+
+def unpair_stem_grad(dwp: torch.Tensor, dw: torch.Tensor) -> None:
+    """Write the width-paired filter gradient ``dwp`` [R, S', 8, K] into ``dw`` [R, 2S' - 1, 8, K]
+    (inverse map of ``pair_stem_weight``; the padded input channels 3-7 get zero gradient)."""
+    R, S2, _, K = dwp.shape
+    dw[:, :, :3, :].copy_(dwp[:, :, :6, :].reshape(R, 2 * S2, 3, K)[:, 1:])
+    dw[:, :, 3:, :].zero_()
+
+
+class _StemW2(torch.autograd.Function):
+    """The stem conv (7x7, stride 2, pad 3 over 3 channels) on width-paired input pixels
+    (``stem_pack``): the paired filter covers two input columns per 8-channel chunk, so the implicit
+    GEMM runs 7 x 4 x 8 = 224 MACs per output element instead of 7 x 7 x 8 = 392 over the channel-padded
+    input, and the packed input is half the bytes of the padded one. The weights and their gradient
+    stay in the [7, 7, 8, K] layout of ``ConvLayer`` (checkpoints, optimizer); ``evaluate`` keeps the
+    padded form. Same BN-statistics epilogue as ``_Conv``."""
+
+    @staticmethod
+    def forward(ctx, xp, token, layer):
+        ctx.layer = layer
+        ctx.save_for_backward(xp)
+        y, part = _ops().conv2d_fwd_stats_w2(xp, pair_stem_weight(layer.w()), layer.stride, layer.pad,
+                                             part_out=layer.acc)
+        ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, *_dpart):
+        (xp,) = ctx.saved_tensors
+        L = ctx.layer
+        R, S, _, K = L.g().shape
+        dwp = torch.empty(R, (S + 1) // 2, 8, K, device=dy.device, dtype=torch.float32)
+        _ops().conv2d_wgrad_w2(xp, dy.contiguous(), dwp, L.stride, L.pad, False)
+        unpair_stem_grad(dwp, L.g())
+        L.model.reducer.mark_ready(L.name)
+        return None, None, None
+
+
 def _take_bwd_part(bn, fid):
     """The BN-backward partials a dgrad epilogue left for ``bn`` -- only if they belong to the
     forward ``fid`` (else None: bn_bwd runs its own partial pass). Clears the layer's state when it
@@ -727,7 +775,7 @@ class ResNet:
 
     def __init__(self, depth: int = 50, num_classes: int = 1000, device=None, seed: int = 0, width: int = 64,
                  zero_init_residual: bool = True, fuse_joins: bool = True, bn_stats: bool = True,
-                 bn_bwd_stats: bool = True, fold_bn: int = 0):
+                 bn_bwd_stats: bool = True, fold_bn: int = 0, stem_w2: bool = True):
         kind, blocks = self.CFG[depth]
         if num_classes % 8 or width % 8:
             raise ValueError("num_classes and width must be multiples of 8 (16-byte MFMA operand chunks)")
@@ -762,6 +810,8 @@ class ResNet:
         self.masked_join = True
         # the stem's bn + relu + max pool as one pass (_BNReluMaxPool): its BN output is never written
         self.fuse_stem_pool = True
+        # the stem conv on width-paired input pixels (_StemW2): 7 x 4 x 8 instead of 7 x 7 x 8 MACs per output
+        self.stem_w2 = bool(stem_w2)
         cin = width
         exp = 4 if kind == "bottleneck" else 1
         prev_out_bn = None  # the BN that produced the current block input (None: the stem's maxpool)
@@ -830,8 +880,10 @@ class ResNet:
         for bn in self.bns:
             bn.fwd_state, bn.bwd_part = None, None
         self.stats.zero()
-        x = _ops().pad_channels(x_nhwc_f32, 8)
-        yp = self.stem(x)
+        if self.stem_w2 and self.bn_stats and x_nhwc_f32.shape[2] % 2 == 0:
+            yp = _StemW2.apply(_ops().stem_pack(x_nhwc_f32), self.token, self.stem)
+        else:
+            yp = self.stem(_ops().pad_channels(x_nhwc_f32, 8))
         if self.fuse_stem_pool and isinstance(yp, tuple):  # (y, statistics partials) from a stats conv
             x = _BNReluMaxPool.apply(yp[0], yp[1], self.stem_bn, 3, 2, 1)
         else:

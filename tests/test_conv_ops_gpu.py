@@ -399,3 +399,32 @@ def test_dgrad_with_stride2_add_operand(cuda, N, H, W, C, K):
     ref2 = ops.conv2d_dgrad(dy2, w3, [N, H, W, C], 2, 1, full)
     got2 = ops.conv2d_dgrad(dy2, w3, [N, H, W, C], 2, 1, comp, None, True)
     assert torch.equal(got2, ref2)
+
+
+@pytest.mark.parametrize("N,H,W,K", [(2, 32, 30, 64), (3, 23, 16, 16)])
+def test_width_paired_stem_matches_the_padded_conv(cuda, N, H, W, K):
+    """stem_pack + conv2d_fwd_stats_w2 / conv2d_wgrad_w2 (the ResNet stem, models/resnet.py _StemW2)
+    against the channel-padded 7x7 stride-2 conv on the same bf16 operands: output, BN partials'
+    column sums, and the filter gradient mapped back by unpair_stem_grad."""
+    from tensorflow_distributed_amd.models.resnet import pair_stem_weight, unpair_stem_grad
+    torch.manual_seed(2)
+    x = torch.randn(N, H, W, 3, device=cuda)
+    w = (torch.randn(7, 7, 8, K, device=cuda) * 0.2).to(torch.bfloat16)
+    w[:, :, 3:] = 0
+    xpad = ops.pad_channels(x, 8)
+    xp = ops.stem_pack(x)
+    assert torch.equal(xp.view(N, H, W // 2, 8)[..., :6].reshape(N, H, W, 3), xpad[..., :3])
+    assert torch.equal(xp[..., 6:], torch.zeros_like(xp[..., 6:]))
+    y0, p0 = ops.conv2d_fwd_stats(xpad, w, 2, 3)
+    y1, p1 = ops.conv2d_fwd_stats_w2(xp, pair_stem_weight(w), 2, 3)
+    assert y1.shape == y0.shape
+    assert relerr(y1.float(), y0.float()) < 1e-2
+    torch.testing.assert_close(p1.sum(0), p0.sum(0), rtol=2e-2, atol=2e-2)
+    dy = rb(torch.randn(y0.shape)).to(cuda, torch.bfloat16)
+    dw0 = torch.zeros(7, 7, 8, K, device=cuda)
+    ops.conv2d_wgrad(xpad, dy, dw0, 2, 3)
+    dwp = torch.empty(7, 4, 8, K, device=cuda)
+    ops.conv2d_wgrad_w2(xp, dy, dwp, 2, 3, False)
+    dw1 = torch.full_like(dw0, float("nan"))
+    unpair_stem_grad(dwp, dw1)
+    assert relerr(dw1, dw0) < 1e-5
