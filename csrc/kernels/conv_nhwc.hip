@@ -1420,10 +1420,21 @@ static void wgrad_launch(const ConvShape& c, const LA& la, const DenseX<false>& 
   }
 }
 
+// The split-K accumulator's zero fill as a kernel: a hipMemsetAsync issued into a stream capture here
+// did not clear the buffer on graph replays (the width-paired stem's gradient, zeroed=False, grew to
+// inf from the second replay on: scripts/debug/stem_mode_check.py), so no captured path depends on it.
+__global__ __launch_bounds__(256) void zero_f32_kernel(float* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0.f;
+}
+static void zero_f32(float* p, int64_t n, hipStream_t st) {  // dw may be a 4-B aligned view of a flat buffer
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n + 255) / 256));
+  zero_f32_kernel<<<grid, 256, 0, st>>>(p, n);
+}
+
 void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float* dw, int splits, hipStream_t st,
                 bool zeroed, const BnReluIn* act) {
   const int P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
-  if (splits > 1 && !zeroed) (void)hipMemsetAsync(dw, 0, (size_t)MT * c.K * sizeof(float), st);
+  if (splits > 1 && !zeroed) zero_f32(dw, (int64_t)MT * c.K, st);
   AccF32 epi{dw, MT, c.K, splits > 1 ? 1 : 0};
   DenseX<false> lb{dy, c.K, c.K, P};
   if (act) {

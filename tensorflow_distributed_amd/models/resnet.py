@@ -399,21 +399,25 @@ class _Conv(torch.autograd.Function):
         return dx, None, None
 
 
-def pair_stem_weight(w: torch.Tensor) -> torch.Tensor:
+def pair_stem_weight(w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[R, S, 8, K] stem filter (3 real input channels, S odd, pad 3) -> the width-paired filter
     [R, (S + 1) // 2, 8, K] of ``conv2d_fwd_stats_w2``: channel p*3 + c of column s' is the original tap
-    s = 2s' + p - 1 (tap -1 is zero), channels 6-7 zero."""
+    s = 2s' + p - 1 (tap -1 is zero), channels 6-7 zero. ``out``: a buffer of that shape whose
+    never-written entries (tap -1, channels 6-7) are already zero -- two copies, no allocation."""
     R, S, _, K = w.shape
-    wz = F.pad(w[:, :, :3, :], (0, 0, 0, 0, 1, 0))  # [R, S + 1, 3, K]: column 0 is the zero tap
-    return F.pad(wz.reshape(R, (S + 1) // 2, 6, K), (0, 0, 0, 2)).contiguous()
+    if out is None:
+        out = torch.zeros(R, (S + 1) // 2, 8, K, device=w.device, dtype=w.dtype)
+    out[:, 1:, 0:3].copy_(w[:, 1::2, :3])  # p = 0: taps 1, 3, 5 (column 0 is tap -1)
+    out[:, :, 3:6].copy_(w[:, 0::2, :3])  # p = 1: taps 0, 2, 4, 6
+    return out
 
 
 def unpair_stem_grad(dwp: torch.Tensor, dw: torch.Tensor) -> None:
     """Write the width-paired filter gradient ``dwp`` [R, S', 8, K] into ``dw`` [R, 2S' - 1, 8, K]
     (inverse map of ``pair_stem_weight``; the padded input channels 3-7 get zero gradient)."""
-    R, S2, _, K = dwp.shape
-    dw[:, :, :3, :].copy_(dwp[:, :, :6, :].reshape(R, 2 * S2, 3, K)[:, 1:])
-    dw[:, :, 3:, :].zero_()
+    dw[:, 1::2, :3].copy_(dwp[:, 1:, 0:3])
+    dw[:, 0::2, :3].copy_(dwp[:, :, 3:6])
+    dw[:, :, 3:].zero_()
 
 
 class _StemW2(torch.autograd.Function):
@@ -428,7 +432,11 @@ class _StemW2(torch.autograd.Function):
     def forward(ctx, xp, token, layer):
         ctx.layer = layer
         ctx.save_for_backward(xp)
-        y, part = _ops().conv2d_fwd_stats_w2(xp, pair_stem_weight(layer.w()), layer.stride, layer.pad,
+        if layer.paired_w is None:  # eager warm-up steps allocate, captured steps reuse
+            R, S, C, K = layer.w().shape
+            layer.paired_w = torch.zeros(R, (S + 1) // 2, C, K, device=xp.device, dtype=layer.w().dtype)
+            layer.paired_g = torch.zeros(R, (S + 1) // 2, C, K, device=xp.device, dtype=torch.float32)
+        y, part = _ops().conv2d_fwd_stats_w2(xp, pair_stem_weight(layer.w(), layer.paired_w), layer.stride, layer.pad,
                                              part_out=layer.acc)
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)
@@ -438,10 +446,8 @@ class _StemW2(torch.autograd.Function):
     def backward(ctx, dy, *_dpart):
         (xp,) = ctx.saved_tensors
         L = ctx.layer
-        R, S, _, K = L.g().shape
-        dwp = torch.empty(R, (S + 1) // 2, 8, K, device=dy.device, dtype=torch.float32)
-        _ops().conv2d_wgrad_w2(xp, dy.contiguous(), dwp, L.stride, L.pad, False)
-        unpair_stem_grad(dwp, L.g())
+        _ops().conv2d_wgrad_w2(xp, dy.contiguous(), L.paired_g, L.stride, L.pad, False)
+        unpair_stem_grad(L.paired_g, L.g())
         L.model.reducer.mark_ready(L.name)
         return None, None, None
 
@@ -689,6 +695,7 @@ class ConvLayer:
         self.acc = None  # statistics-partials slots of this conv's output (StatArena), None: row mode
         self.in_join = None  # GradJoin of this conv's input (residual block inputs)
         self.in_bn = None  # the BN whose output is this conv's only input consumer (BN-backward stats)
+        self.paired_w = self.paired_g = None  # the width-paired stem's filter / gradient buffers (_StemW2)
         model.specs.append(PSpec(name, (k, k, cin, cout), "he", fan_in=k * k * cin))
         model.convs.append(self)
 

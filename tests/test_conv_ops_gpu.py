@@ -428,3 +428,26 @@ def test_width_paired_stem_matches_the_padded_conv(cuda, N, H, W, K):
     dw1 = torch.full_like(dw0, float("nan"))
     unpair_stem_grad(dwp, dw1)
     assert relerr(dw1, dw0) < 1e-5
+
+
+def test_captured_split_k_wgrad_zeroes_its_accumulator_on_every_replay(cuda):
+    """conv2d_wgrad(zeroed=False) with split-K clears dw itself; captured in a graph and replayed, every
+    replay must give the eager result (a captured hipMemsetAsync did not clear it on replays)."""
+    torch.manual_seed(4)
+    x = rb(torch.randn(16, 14, 14, 64)).to(cuda, torch.bfloat16)  # 3,136 pixels: split-K
+    dy = rb(torch.randn(16, 14, 14, 128)).to(cuda, torch.bfloat16)
+    ref = torch.zeros(1, 1, 64, 128, device=cuda)
+    ops.conv2d_wgrad(x, dy, ref, 1, 0)
+    dw = torch.full((1, 1, 64, 128), 7.0, device=cuda)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.conv2d_wgrad(x, dy, dw, 1, 0)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.conv2d_wgrad(x, dy, dw, 1, 0)
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert relerr(dw, ref) < 1e-5
