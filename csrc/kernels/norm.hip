@@ -735,6 +735,39 @@ __global__ __launch_bounds__(NT) void avgpool_fwd_kernel(const uint16_t* __restr
   y[i] = f2bf_bits(s / (float)HW);
 }
 
+// 8-channel chunk forms (C % 8 == 0): 16-B loads / stores, the same per-channel sums in the same
+// order and the same rounding as the scalar kernels
+__global__ __launch_bounds__(NT) void avgpool_fwd8_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, int N,
+                                                          int HW, int C8) {
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= N * C8) return;
+  const int n = i / C8, c = i - n * C8;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, v[8];
+  const uint4* p = x + (size_t)n * HW * C8 + c;
+#pragma unroll 7
+  for (int q = 0; q < HW; ++q) {
+    unpack8(p[(size_t)q * C8], v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += v[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = s[j] / (float)HW;
+  y[i] = pack8(s);
+}
+
+__global__ __launch_bounds__(NT) void avgpool_bwd8_kernel(const uint4* __restrict__ dy, uint4* __restrict__ dx, int N,
+                                                          int HW, int C8) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= (int64_t)N * HW * C8) return;
+  const int c = (int)(i % C8);
+  const int n = (int)(i / ((int64_t)HW * C8));
+  float v[8];
+  unpack8(dy[(size_t)n * C8 + c], v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = v[j] / (float)HW;
+  dx[i] = pack8(v);
+}
+
 __global__ __launch_bounds__(NT) void avgpool_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx,
                                                          int N, int HW, int C) {
   const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
@@ -988,10 +1021,21 @@ void bn_relu_maxpool(const uint16_t* y, const float* gamma, const float* beta, f
 }
 
 void avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s) {
+  if (C % 8 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(y) % 16 == 0) {
+    avgpool_fwd8_kernel<<<(N * (C / 8) + NT - 1) / NT, NT, 0, s>>>(reinterpret_cast<const uint4*>(x),
+                                                                   reinterpret_cast<uint4*>(y), N, HW, C / 8);
+    return;
+  }
   avgpool_fwd_kernel<<<(N * C + NT - 1) / NT, NT, 0, s>>>(x, y, N, HW, C);
 }
 
 void avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t s) {
+  if (C % 8 == 0 && reinterpret_cast<uintptr_t>(dy) % 16 == 0 && reinterpret_cast<uintptr_t>(dx) % 16 == 0) {
+    const int64_t chunks = (int64_t)N * HW * (C / 8);
+    avgpool_bwd8_kernel<<<(int)((chunks + NT - 1) / NT), NT, 0, s>>>(reinterpret_cast<const uint4*>(dy),
+                                                                     reinterpret_cast<uint4*>(dx), N, HW, C / 8);
+    return;
+  }
   const int64_t total = (int64_t)N * HW * C;
   avgpool_bwd_kernel<<<(int)((total + NT - 1) / NT), NT, 0, s>>>(dy, dx, N, HW, C);
 }

@@ -451,3 +451,18 @@ def test_captured_split_k_wgrad_zeroes_its_accumulator_on_every_replay(cuda):
         g.replay()
         torch.cuda.synchronize()
         assert relerr(dw, ref) < 1e-5
+
+
+@pytest.mark.parametrize("C", [64, 12])
+def test_avgpool_chunk_and_scalar_forms(cuda, C):
+    """avgpool_fwd / avgpool_bwd: the 8-channel chunk kernels (C % 8 == 0) and the scalar ones (C = 12):
+    forward within bf16 rounding of the fp64 mean, backward exactly bf16(dy / HW) (fp32 divide, RNE)."""
+    torch.manual_seed(5)
+    x = rb(torch.randn(3, 7, 7, C))
+    a = ops.avgpool_fwd(x.to(cuda, torch.bfloat16)).cpu().double()
+    ref = x.double().mean((1, 2))
+    assert (a - ref).abs().max().item() <= 2 ** -7 * ref.abs().max().item() + 1e-6
+    dy = rb(torch.randn(3, C))
+    da = ops.avgpool_bwd(dy.to(cuda, torch.bfloat16), [3, 7, 7, C]).cpu()
+    want = (dy.float() / 49.0).to(torch.bfloat16)[:, None, None, :].expand(3, 7, 7, C)
+    assert torch.equal(da, want)
