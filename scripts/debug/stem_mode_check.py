@@ -56,7 +56,7 @@ def main():
     for stem_w2 in (False, True):
         print(f"eager stem_w2={stem_w2}: {run_eager(stem_w2, x, lab, cuda)}", flush=True)
     for stem_w2 in (False, True):
-        for switch in (False,):
+        for switch in (False, True):
             print(f"stem_w2={stem_w2} switch={switch}: {run(stem_w2, switch, x, lab, cuda)}", flush=True)
     torch.ops.tfd.set_bn_part_slots(old)
 
