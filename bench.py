@@ -103,6 +103,9 @@ def _args(argv):
                     "0: time whatever state the warm-up steps left")
     ap.add_argument("--data", default="strokes", choices=["strokes", "random"], help="device-resident training "
                     "set: learnable class-conditional strokes (default) or uniform noise with random labels")
+    ap.add_argument("--fp32_also", type=int, default=-1, help="after the bf16 headline, time the fp32 step (the "
+                    "reference's precision) with the same protocol and report it under \"fp32\": 1 always, 0 never, "
+                    "-1 at world 1 only")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu", action="store_true", help="plumbing dry-run: fp32 PyTorch CPU runner + Gloo "
@@ -234,6 +237,8 @@ def _probe_once(a, ctx, data, labels, sched) -> float:
         if job is not None:
             job.close()
         raise RuntimeError(f"setup failed on at least one rank (here: {err!r})")
+    _CUR["tr"] = job.tr
+    dt, err = 0.0, None
     try:
         with torch.cuda.stream(job.stream):
             job.run(a.probe_warmup)
@@ -245,9 +250,24 @@ def _probe_once(a, ctx, data, labels, sched) -> float:
         torch.cuda.synchronize(ctx.device)
         dt = time.perf_counter() - t0
         job.tr.check(f"schedule probe {sched}")
-    finally:
-        job.close()
+    except Exception as e:  # noqa: BLE001 - agreed after the teardown barriers
+        err = e
+    job.close()
+    _CUR["tr"] = None
+    # a timed-section failure (an IPC timeout caught by check) on one rank is raised on EVERY rank,
+    # so no rank goes on alone into the next candidate's collectives
+    if ctx.max_scalar(1.0 if err is not None else 0.0) > 0:
+        raise RuntimeError(f"schedule probe {sched} failed on at least one rank (here: {err!r})")
     return dt * 1e3 / max(1, a.probe_steps)
+
+
+_CUR = {"tr": None}  # the live DP transport, for the watchdog's error-word report
+
+
+def _watchdog(rank):
+    from tensorflow_distributed_amd.utils.tracing import PhaseWatchdog
+
+    return PhaseWatchdog(rank, err_fn=lambda: _CUR["tr"].error() if _CUR["tr"] is not None else 0, tag="bench.py")
 
 
 def main(argv=None):
@@ -267,6 +287,8 @@ def main(argv=None):
     from tensorflow_distributed_amd.parallel import dist as D
     from tensorflow_distributed_amd.parallel import schedule as SCH
 
+    wd = _watchdog(int(os.environ.get("RANK", "0")))
+    wd.phase("setup: native library, process group, RCCL/IPC bootstrap, dataset", 600)
     _native.require()
     ctx = D.init_from_env(use_gpu=True)
     world, rank = ctx.world, ctx.rank
@@ -292,17 +314,141 @@ def main(argv=None):
     probe_ms = None
     if source == "probe" and len(cands) > 1:
         log = (lambda m: print(m, file=sys.stderr, flush=True)) if rank == 0 else None
-        probe_ms = SCH.probe(cands, lambda name: _probe_once(a, ctx, data, labels, name), ctx.max_scalar, log)
+
+        def probe_one(name):
+            wd.phase(f"schedule probe {name} (setup, {a.probe_warmup} + {a.probe_steps} steps, teardown)",
+                     180 + 0.05 * (a.probe_warmup + a.probe_steps))
+            return _probe_once(a, ctx, data, labels, name)
+
+        probe_ms = SCH.probe(cands, probe_one, ctx.max_scalar, log)
         sched = SCH.pick(probe_ms)
     else:
         sched = cands[0]
 
+    res = _measure(a, ctx, data, labels, sched, wd, "bf16" if a.dtype == "bf16" else "fp32")
+    job, tr, eng = res["job"], res["job"].tr, res["job"].eng
+    topo = _job_topology(ctx, dev, tr, eng)
+    phases = _phase_breakdown(eng, job.stream, job.graph_mode, world, ctx) if a.phases else None
+    # the phase steps ran on the job's stream: wait for them before reading the state on the default
+    # stream (without this the last step's loss rows could be read mid-write: two runs of the same
+    # binary printed the loss of step N or N - 1)
+    torch.cuda.synchronize(dev)
+    _finish_losses(res)
+    res_g = {k: v for k, v in res.items() if k not in ("job", "loss0_t")}
+    ms = res["dt"] * 1e3 / a.steps
+    img_s = world * B * a.steps / res["dt"]
+    graph_mode, gsteps = job.graph_mode, job.gsteps
+    kind, zero = tr.kind, job.zero
+    tr.close()
+    # The reference's precision (fp32 variables and arithmetic, /root/reference/mnist_python_m.py:185-200)
+    # timed in the same process after the bf16 headline: same steps, warm-up and learning-state
+    # protocol, reported beside it. World 1 by default (--fp32_also -1).
+    fp32 = None
+    if a.dtype == "bf16" and (a.fp32_also == 1 or (a.fp32_also < 0 and world == 1)):
+        job.eng = None
+        del res, job, eng
+        torch.cuda.synchronize(dev)
+        a32 = argparse.Namespace(**vars(a))
+        a32.dtype, a32.lead_steps = "fp32", 0
+        r32 = _measure(a32, ctx, data, labels, "allreduce" if dp else None, wd, "fp32")
+        torch.cuda.synchronize(dev)
+        _finish_losses(r32)
+        fp32 = {"ms_per_step": round(r32["dt"] * 1e3 / a.steps, 5),
+                "images_per_s": round(world * B * a.steps / r32["dt"], 1),
+                "gpu_event_ms_per_step": round(r32["gpu_ms"] / a.steps, 5),
+                "steps": a.steps, "warmup": a.warmup, "warmup_extra_steps": r32["extra"],
+                "train_state": {"global_step": r32["gstep"], "loss_before_timed": round(r32["loss0"], 4),
+                                "loss_after_timed": round(r32["loss1"], 4),
+                                "minibatch_accuracy": round(r32["acc1"], 4)},
+                "schedule": "allreduce" if dp else None,
+                "what": "fp32 operands, fp32 MFMA (v_mfma_f32_16x16x4_f32), fp32 master/Adam: the reference's precision"}
+        r32["job"].tr.close()
+        if rank == 0:
+            print(f"# fp32 (reference precision): {fp32['ms_per_step']:.4f} ms/step, {fp32['images_per_s']:.0f} img/s",
+                  file=sys.stderr)
+    if rank == 0:
+        print(f"# world={world} B/gpu={B} schedule={sched} steps={a.steps} global_step={res_g['gstep']} "
+              f"loss {res_g['loss0']:.3f}->{res_g['loss1']:.3f} acc {res_g['acc1']:.3f} {ms:.4f} ms/step",
+              file=sys.stderr)
+        print(json.dumps({
+            "metric": METRIC,
+            "value": round(img_s, 1),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "warmup_extra_steps": res_g["extra"],
+            "train_state": {"global_step": res_g["gstep"], "loss_before_timed": round(res_g["loss0"], 4),
+                            "loss_after_timed": round(res_g["loss1"], 4),
+                            "minibatch_accuracy": round(res_g["acc1"], 4), "state_steps": a.state_steps},
+            "ms_per_step": round(ms, 5),
+            "gpu_event_ms_per_step": round(res_g["gpu_ms"] / a.steps, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(img_s / BASELINE_IMG_PER_S, 1),
+            "dtype": a.dtype,
+            "data": DATA_DESC[a.data],
+            "phases_ms": phases,
+            "schedule": {"chosen": sched, "source": source,
+                         "candidates_ms_per_step": ({k: round(v, 5) for k, v in probe_ms.items()}
+                                                    if probe_ms else None),
+                         "probe_steps": a.probe_steps if probe_ms else 0},
+            **topo,
+            "fp32": fp32,
+            "config": {
+                "model": "MNIST 2-conv CNN (reference conv_net: conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout0.75-fc10), "
+                         "Adam lr 0.01",
+                "global_batch": world * B,
+                "per_gpu_batch": B,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "grad_allreduce": "fp32" if (a.fp32_grads or a.dtype == "fp32") else "bf16",
+                "hipgraph": graph_mode,
+                "steps_per_graph": gsteps if graph_mode else 0,
+                "dp_transport": kind,
+                "force_dp": bool(a.force_dp),
+                "zero1_fc1": zero,
+                "fc_grads": ("fp32" if a.dtype == "fp32" else
+                             "summed from all-gathered factors (sfb), bf16" if "sfb" in kind else
+                             "bf16" if (a.local_bf16_grads or world > 1) and not a.fp32_grads else "fp32"),
+            },
+        }), flush=True)
+    wd.stop()
+    ctx.shutdown()
+    if not topo["replicas_identical"]:
+        print("error: DP replicas diverged (parameter digests differ across ranks)", file=sys.stderr)
+        return 3
+    return 0
+
+
+def _finish_losses(res):
+    """Host reads of the losses / accuracy / step of a measured job (after its stream is drained)."""
+    eng = res["job"].eng
+    if res["loss0"] is None:
+        res["loss0"] = float(res["loss0_t"].item())
+    res["loss1"] = float(eng.loss_rows().mean().item())
+    res["acc1"] = float(eng.correct_rows().mean().item())  # last timed step's minibatch accuracy (train mode)
+    res["gstep"] = int(eng.step_tensor().item())
+
+
+def _measure(a, ctx, data, labels, sched, wd, label):
+    """Set up one job (engine, transport, graphs) and run the timing protocol on it: ``--state_steps``
+    steps from init (snapshotted), ``--warmup`` + clock-ramp warm-up steps, state restored, then
+    EXACTLY ``--steps`` replayed steps between a barrier + synchronize on both sides; ``dt`` is the
+    max over ranks."""
+    import torch
+
+    dev, rank = ctx.device, ctx.rank
+    wd.phase(f"{label} job setup ({sched}): engine, transport, graph capture", 300)
     lead = max(0, min(a.lead_steps, a.steps - 1)) if not a.eager else 0
     job = _Job(a, ctx, data, labels, sched, a.graph_steps, extra_graph=(a.steps - lead) if lead else 0)
     eng, tr, s, run = job.eng, job.tr, job.stream, job.run
-    graph_mode, gsteps = job.graph_mode, job.gsteps
-    if not graph_mode:
+    _CUR["tr"] = tr
+    wd.phase(f"{label} warm-up ({a.state_steps} state + {a.warmup} steps + {a.min_warmup_ms:.0f} ms)",
+             180 + 0.05 * (a.state_steps + a.warmup) + a.min_warmup_ms / 1e3)
+    if not job.graph_mode:
         lead = 0
+    loss0_t = None
     with torch.cuda.stream(s):
         # The timed steps start from the training state after --state_steps steps (a model that is
         # still learning), not from wherever the clock-ramp warm-up below leaves it: snapshot it now,
@@ -356,6 +502,7 @@ def main(argv=None):
     else:
         loss0 = float(eng.loss_rows().mean().item())
 
+    wd.phase(f"{label} timed region ({a.steps} steps)", 120 + 0.05 * a.steps)
     ctx.barrier()
     torch.cuda.synchronize(dev)
     if a.idle_us > 0:
@@ -383,76 +530,14 @@ def main(argv=None):
         print(f"# timed region: host launch {1e6 * (t_launched - t0):.1f} us, sync wait "
               f"{1e6 * (t_synced - t_launched):.1f} us, barrier {1e6 * (t0 + dt - t_synced):.1f} us", file=sys.stderr)
     _diag_digest("timed", eng, rank)
+    wd.phase(f"{label} report: replica digests, phase breakdown, teardown", 300)
     gpu_ms = ev0.elapsed_time(ev1)  # device time of the same K steps (diagnostic: host/sync overhead = dt - this)
     if job.zero:
         with torch.cuda.stream(s):
             eng.sync_params()
     dt = ctx.max_scalar(dt)
     tr.check("after the timed steps")
-    topo = _job_topology(ctx, dev, tr, eng)
-    phases = _phase_breakdown(eng, s, graph_mode, world, ctx) if a.phases else None
-    # the phase steps ran on stream s: wait for them before reading the state on the default stream
-    # (without this the last step's loss rows could be read mid-write: two runs of the same binary
-    # printed the loss of step N or N - 1)
-    torch.cuda.synchronize(dev)
-    if loss0 is None:
-        loss0 = float(loss0_t.item())
-    loss1 = float(eng.loss_rows().mean().item())
-    acc1 = float(eng.correct_rows().mean().item())  # last timed step's minibatch accuracy (train mode)
-    gstep = int(eng.step_tensor().item())
-    ms = dt * 1e3 / a.steps
-    img_s = world * B * a.steps / dt
-    if rank == 0:
-        print(f"# world={world} B/gpu={B} schedule={sched} steps={a.steps} global_step={gstep} "
-              f"loss {loss0:.3f}->{loss1:.3f} acc {acc1:.3f} {ms:.4f} ms/step", file=sys.stderr)
-        print(json.dumps({
-            "metric": METRIC,
-            "value": round(img_s, 1),
-            "unit": "images/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "warmup_extra_steps": extra,
-            "train_state": {"global_step": gstep, "loss_before_timed": round(loss0, 4),
-                            "loss_after_timed": round(loss1, 4), "minibatch_accuracy": round(acc1, 4),
-                            "state_steps": a.state_steps},
-            "ms_per_step": round(ms, 5),
-            "gpu_event_ms_per_step": round(gpu_ms / a.steps, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(img_s / BASELINE_IMG_PER_S, 1),
-            "dtype": a.dtype,
-            "data": DATA_DESC[a.data],
-            "phases_ms": phases,
-            "schedule": {"chosen": sched, "source": source,
-                         "candidates_ms_per_step": ({k: round(v, 5) for k, v in probe_ms.items()}
-                                                    if probe_ms else None),
-                         "probe_steps": a.probe_steps if probe_ms else 0},
-            **topo,
-            "config": {
-                "model": "MNIST 2-conv CNN (reference conv_net: conv5x5x32-pool-conv5x5x64-pool-fc1024-dropout0.75-fc10), "
-                         "Adam lr 0.01",
-                "global_batch": world * B,
-                "per_gpu_batch": B,
-                "seq_len": None,
-                "parallelism": f"dp{world}",
-                "grad_allreduce": "fp32" if (a.fp32_grads or a.dtype == "fp32") else "bf16",
-                "hipgraph": graph_mode,
-                "steps_per_graph": gsteps if graph_mode else 0,
-                "dp_transport": tr.kind,
-                "force_dp": bool(a.force_dp),
-                "zero1_fc1": job.zero,
-                "fc_grads": ("fp32" if a.dtype == "fp32" else
-                             "summed from all-gathered factors (sfb), bf16" if "sfb" in tr.kind else
-                             "bf16" if (a.local_bf16_grads or world > 1) and not a.fp32_grads else "fp32"),
-            },
-        }), flush=True)
-    tr.close()
-    ctx.shutdown()
-    if not topo["replicas_identical"]:
-        print("error: DP replicas diverged (parameter digests differ across ranks)", file=sys.stderr)
-        return 3
-    return 0
+    return {"job": job, "dt": dt, "gpu_ms": gpu_ms, "extra": extra, "loss0": loss0, "loss0_t": loss0_t}
 
 
 def _diag_digest(where, eng, rank):

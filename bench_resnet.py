@@ -83,6 +83,12 @@ def main(argv=None):
     from tensorflow_distributed_amd.models.resnet import ResNet
     from tensorflow_distributed_amd.parallel import dist as D
 
+    from tensorflow_distributed_amd.utils.tracing import PhaseWatchdog
+
+    live = {"ipc": None}  # the IPC communicator in use, for the watchdog's error-word report
+    wd = PhaseWatchdog(int(os.environ.get("RANK", "0")), tag="bench_resnet.py",
+                       err_fn=lambda: live["ipc"].error() if live["ipc"] is not None else 0)
+    wd.phase("setup: native library, process group, RCCL/IPC bootstrap, model", 600)
     _native.require()
     ctx = D.init_from_env(use_gpu=True)
     spawn.check_world(a.gpus, ctx.world)
@@ -112,10 +118,12 @@ def main(argv=None):
             small = small_bucket_ipc(ctx.rank, ctx.world, dev, comm, int(a.small_ipc_mb * (1 << 20)))
             if small is not None:
                 transport = "rccl+ipc(small buckets)"
+                live["ipc"] = small.ipc
         elif ctx.shared_device:  # ranks share a GPU (RCCL refuses that): the IPC transport
             from tensorflow_distributed_amd.parallel.ipc import IpcCollectives, make_ipc_comm
 
             comm, transport = IpcCollectives(make_ipc_comm(ctx.rank, ctx.world, dev.index, m.fp.total)), "ipc"
+            live["ipc"] = comm.ipc
             host = m.fp.master.detach().cpu()
             ctx.broadcast_tensor_cpu(host, 0)  # chief init -> every rank over Gloo
             m.fp.master.copy_(host.to(dev))
@@ -182,6 +190,8 @@ def main(argv=None):
         snap = [t.clone() for t in (m.fp.master, m.fp.momentum, m.fp.shadow)]
 
         def one(name):
+            wd.phase(f"bucket probe {name} MB (setup, capture, {a.probe_warmup} + {a.probe_steps} steps)",
+                     240 + 2.0 * (a.probe_warmup + a.probe_steps))
             run_p, graph_p = configure(float(name))
             run_p(a.probe_warmup)
             torch.cuda.synchronize(dev)
@@ -200,16 +210,19 @@ def main(argv=None):
             dst.copy_(src)
         del snap
         torch.cuda.synchronize(dev)
+    wd.phase(f"job setup + warm-up ({bucket_mb} MB buckets, {a.warmup} steps)", 240 + 2.0 * a.warmup)
     run, graph = configure(bucket_mb)
     run(a.warmup)
     torch.cuda.synchronize(dev)
     ctx.barrier()
     torch.cuda.synchronize(dev)
+    wd.phase(f"timed region ({a.steps} steps)", 120 + 2.0 * a.steps)
     t0 = time.perf_counter()
     loss = run(a.steps)
     torch.cuda.synchronize(dev)
     ctx.barrier()
     dt = ctx.max_scalar(time.perf_counter() - t0)
+    wd.phase("report: replica digests, teardown", 300)
     img_s = ctx.world * a.batch_size * a.steps / dt
     topo = _topology(ctx, dev, comm, m)
     if ctx.rank == 0:
@@ -245,6 +258,8 @@ def main(argv=None):
             if c.ipc.error():
                 raise RuntimeError("IPC collective barrier timed out: replicas may have diverged")
             c.ipc.close()
+    live["ipc"] = None
+    wd.stop()
     ctx.shutdown()
     if not topo["replicas_identical"]:
         print("error: DP replicas diverged (parameter digests differ across ranks)", file=sys.stderr)

@@ -38,7 +38,7 @@ __device__ __forceinline__ void epi_call(const EPI& epi, int m4, int n, const f3
 }
 
 // LDS images (MI355X LDS: 64 banks x 4 B; ds_read_b128 in 4 groups of 16 lanes, ds_read_b64_tr_b16
-// in 2 groups of 32, scripts/debug/lds_banks.py):
+// in 2 groups of 32, tools/debug/lds_banks.py):
 //  KC = true : [MN][BK + 16] -- the 16 rows of a b128 fragment read land 8 banks apart per row
 //              (pad 8 put rows r and r + 8 on the same banks: 2-way on every read);
 //  KC = false: [BK][MN] with the 16-B chunk index of row k XORed by swz_chunk(k) (no pad): the 8

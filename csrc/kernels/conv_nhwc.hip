@@ -781,7 +781,7 @@ bool is_pointwise(const ConvShape& c) { return c.R == 1 && c.S == 1 && c.stride 
 // DMA'd into LDS through the same loaders (their off() / rsrc()). Forward: A = im2col(X) (KC), B = the
 // HWIO weight (MNC, transposed fragment reads); dgrad: A = dY gather, B = W as [C][(r,s,k)] (both KC);
 // weight gradient: A = im2col(X)^T, B = dY (both MNC). The core choice (conv_gemm_core(), the op
-// tfd::conv_gemm_core that the per-layer probe scripts/debug/gemm_probe.py and the numerics tests
+// tfd::conv_gemm_core that the per-layer probe tools/debug/gemm_probe.py and the numerics tests
 // switch): 0 = the 128-row core everywhere, 1 (default) = this core where its tiles fill the chip with
 // >= 1024-channel bf16 outputs, 2 = wherever it applies (profiles/resnet50_core_ab_r4.log).
 int g256_mode_v = 1;  // conv_gemm_core(): 0 / 1 (default) / 2, see above
@@ -1422,7 +1422,7 @@ static void wgrad_launch(const ConvShape& c, const LA& la, const DenseX<false>& 
 
 // The split-K accumulator's zero fill as a kernel: a hipMemsetAsync issued into a stream capture here
 // did not clear the buffer on graph replays (the width-paired stem's gradient, zeroed=False, grew to
-// inf from the second replay on: scripts/debug/stem_mode_check.py), so no captured path depends on it.
+// inf from the second replay on: tools/debug/stem_mode_check.py), so no captured path depends on it.
 __global__ __launch_bounds__(256) void zero_f32_kernel(float* __restrict__ p, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0.f;
 }

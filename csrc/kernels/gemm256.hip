@@ -1,7 +1,7 @@
 // Dense bf16 GEMM on the 256 x 256 MFMA core (csrc/gemm256.h): C[M][N] = A[M][K] . Bt[N][K]^T,
 // fp32 accumulation, bf16 output. The general-matrix building block behind the ResNet 1x1 layers and
 // the dense layers, and the number VERDICT r3 item 3 asks for (dense 4096^3 >= 1000 TF/s;
-// scripts/debug/gemm_probe.py times it against hipBLASLt through torch.matmul on the same GPU).
+// tools/debug/gemm_probe.py times it against hipBLASLt through torch.matmul on the same GPU).
 #include <stdexcept>
 
 #include "../common.h"

@@ -102,7 +102,7 @@ constexpr int C2F_W = 24, C2F_PLANE = 18 * C2F_W, C2F_WLD = 48;
 // apart inside a group, odd groups shifted by 16 elements. A B-fragment ds_read_b64_tr_b16 has the
 // lanes of K-chunks g = 0, 1 reading rows 8g + q (q < 4; the second read q + 4): with a plain
 // 96-B pitch rows r and r + 8 share banks (2-way, 3.2 K of the conv2 loop's 5.7 K LDS cycles per
-// block); with this layout the 8 rows cover 64 distinct banks (scripts/debug/lds_banks.py). Same
+// block); with this layout the 8 rows cover 64 distinct banks (tools/debug/lds_banks.py). Same
 // footprint as the plain [800][48] layout.
 __device__ __forceinline__ int c2f_wrow(int r) { return (r >> 3) * 384 + (r & 7) * 32 + ((r >> 3) & 1) * 16; }
 constexpr int C2F_WTAP = 4 * 384;  // one tap = 32 rows = 4 groups
@@ -922,7 +922,7 @@ __device__ __forceinline__ int c1w_dz(int px, int c) {  // element offset of dz1
   return px * 32 + (((c >> 3) ^ (2 * ((px >> 3) & 1))) << 3) + (c & 7);
 }
 // timing-stamp builds (TFD_STAMP): thread 0 of dgrad block bid records s_memtime at 8 phase
-// boundaries into dbg[5 * B * 8 + bid * 8 + k] (scripts/debug/stamps.py dgrad)
+// boundaries into dbg[5 * B * 8 + bid * 8 + k] (tools/debug/stamps.py dgrad)
 #define C2D_STAMP(k)                                                                                     \
   do {                                                                                                   \
     if (TFD_STAMP && a.dbg && threadIdx.x == 0) a.dbg[5 * a.B * 8 + bid * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memtime(); \

@@ -640,7 +640,7 @@ __global__ __launch_bounds__(NT) void bn_relu_maxpool_kernel(const uint16_t* __r
 // behind a branch. Windows in maxpool_bwd_kernel's order: the same dx bit for bit. ResNet-50 stem
 // (128 x 112 x 112 x 64): 109 -> 84-88 us. (Summing the stem BN's backward statistics here as well
 // measured 150-158 us in row mode and 173-273 in slot mode against 87 + the 79-us partial pass:
-// not kept, scripts/debug/pool_probe.py.)
+// not kept, tools/debug/pool_probe.py.)
 __global__ __launch_bounds__(NT) void maxpool2_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ am,
                                                           uint16_t* __restrict__ dx, int N, int H, int W, int C, int k,
                                                           int st, int pad, int Ho, int Wo) {

@@ -159,7 +159,7 @@ __global__ void copy_f32_kernel(float* __restrict__ d, const float* __restrict__
   for (int64_t i = (n4 << 2) + i0; i < n; i += stride) d[i] = s[i];
 }
 
-// ---- roofline probes (scripts/debug/roofline_probe.py) ----
+// ---- roofline probes (tools/debug/roofline_probe.py) ----
 // The optimizer's byte floor: the same traffic as ApplyAdam over a flat buffer -- fp32 p, m, v read
 // and written in place, a bf16 gradient read, the bf16 shadow written (28 B per parameter) -- plus
 // an optional extra fp32 read stream (the conv weight-gradient slabs the one-GPU tail also reads),

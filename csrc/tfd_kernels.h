@@ -152,7 +152,7 @@ struct SgdArgs {
   float lr, momentum, weight_decay, grad_scale; int nesterov;
 };
 // roofline probes: the optimizer's byte floor (Adam's 28 B/param of traffic, optional extra fp32 read
-// stream of nx4 float4) and an empty launch (scripts/debug/roofline_probe.py)
+// stream of nx4 float4) and an empty launch (tools/debug/roofline_probe.py)
 void stream_floor(float* p, float* m, float* v, const uint16_t* g, uint16_t* pbf, const float* x, int64_t n4, int64_t nx4,
                   int blocks, int unroll, hipStream_t s);
 void noop_launch(int blocks, hipStream_t s);

@@ -74,7 +74,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         # No packed-fp32 VALU ops (v_pk_fma/mul/add_f32): with them, the SLP-vectorised VALU
         # kernels (conv1, head, wgrad) gave sporadically different results for the same inputs
         # when several processes shared the GPU; without them every stage is bit-reproducible
-        # (scripts/debug/determinism.py, docs/DESIGN.md section 6). TFD_PACKED_FP32=1 (variant
+        # (tools/debug/determinism.py, docs/DESIGN.md section 6). TFD_PACKED_FP32=1 (variant
         # builds only) keeps them for that experiment.
     ] + ([] if os.environ.get("TFD_PACKED_FP32") == "1" else
          ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]) + HIP_EXTRA_FLAGS

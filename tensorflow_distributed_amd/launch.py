@@ -82,7 +82,7 @@ class Proc:
 
 def profiler_prefix(out_dir: str, pmc: str = "") -> List[str]:
     """rocprofv3 command prefix (SURVEY 5.1 ``--profile``): kernel trace + per-kernel stats, or one
-    PMC counter pass (counters of one pass only; see scripts/gpu_pmc.sh for the per-block limits)."""
+    PMC counter pass (counters of one pass only; see scripts/gpu_run.sh pmc= and the per-block limits in docs/DESIGN.md)."""
     if pmc:
         return ["rocprofv3", "--kernel-trace", "--pmc", *pmc.split(","), "-d", out_dir, "-o", "run", "--"]
     return ["rocprofv3", "--kernel-trace", "--stats", "-d", out_dir, "-o", "run", "--"]

@@ -23,7 +23,6 @@ from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 import torch
-import torch.nn.functional as F
 
 ops = None
 
@@ -170,8 +169,8 @@ class BucketReducer:
         ("free(): invalid pointer", segfaults) within 1-30 capture / replay / destroy cycles, with
         the IPC collective, RCCL or a plain torch-op stand-in alike, never with the hand-offs issued
         from the main thread (80 cycles each) nor without the side stream; a torch-only twin issuing
-        the same stream/event pattern from the main thread was clean too (scripts/debug/heap_twin.py,
-        scripts/debug/rn_configure_loop.py, profiles/heap_bisect_r5.log). The overlap is unchanged:
+        the same stream/event pattern from the main thread was clean too (tools/debug/heap_twin.py,
+        tools/debug/rn_configure_loop.py, profiles/heap_bisect_r5.log). The overlap is unchanged:
         the collective still waits only for its bucket's event, recorded at the same point of the
         backward."""
         b = self.bucket_of[name]
@@ -213,7 +212,7 @@ class BucketReducer:
 # ----------------------------------------------------------------------------- autograd ops
 # GradJoin defers a first-arriving conv whose dgrad can carry the BN-backward statistics (13.335 ->
 # 13.25 ms, profiles/resnet50_join_defer_ab_r4.log); False = compute it at once -- the oracle form the
-# tests and scripts/debug/bn_bwd_stats_rel.py compare against (module attribute, not a run-time switch)
+# tests and tools/debug/bn_bwd_stats_rel.py compare against (module attribute, not a run-time switch)
 _JOIN_DEFER = True
 # a 1x1 stride-2 shortcut dgrad stays on its own grid, added at the even pixels by the joining dgrad's
 # epilogue (13.12 -> 13.04 ms, profiles/resnet50_shortcut_sub2_ab_r4.log); False = the full-grid
@@ -1006,9 +1005,13 @@ class ResNetRunner:
         out = OrderedDict()
         out["global_step"] = np.array(self._step, dtype=np.int64)
         master, mom = fp.master.detach().cpu(), fp.momentum.detach().cpu()
+        stem = self.m.stem.name
         for s in fp.specs:
-            out[s.name] = fp.view(master, s).numpy().copy()
-            out[s.name + "/Momentum"] = fp.view(mom, s).numpy().copy()
+            w, mv = fp.view(master, s), fp.view(mom, s)
+            if s.name == stem:  # the kernels' [7, 7, 8, K] channel padding is not saved: TF's [7, 7, 3, K]
+                w, mv = w[:, :, :3, :], mv[:, :, :3, :]
+            out[s.name] = w.numpy().copy()
+            out[s.name + "/Momentum"] = mv.numpy().copy()
         for bn in self.m.bns:
             out[bn.name + "/moving_mean"] = bn.rmean.detach().cpu().numpy().copy()
             out[bn.name + "/moving_variance"] = bn.rvar.detach().cpu().numpy().copy()
@@ -1020,10 +1023,20 @@ class ResNetRunner:
         fp = self.m.fp
         master = torch.zeros(fp.total)
         mom = torch.zeros(fp.total)
+        stem = self.m.stem.name
+
+        def put(dst, arr, s):
+            t = torch.from_numpy(np.asarray(arr))
+            if s.name == stem and t.numel() != dst.numel():  # [7, 7, 3, K] on disk: zero the padded channels
+                dst.zero_()
+                dst[:, :, :t.shape[2], :].copy_(t.reshape(s.shape[0], s.shape[1], -1, s.shape[3]))
+            else:
+                dst.copy_(t.reshape(s.shape))
+
         for s in fp.specs:
-            fp.view(master, s).copy_(torch.from_numpy(np.asarray(tensors[s.name]).reshape(s.shape)))
+            put(fp.view(master, s), tensors[s.name], s)
             if s.name + "/Momentum" in tensors:
-                fp.view(mom, s).copy_(torch.from_numpy(np.asarray(tensors[s.name + "/Momentum"]).reshape(s.shape)))
+                put(fp.view(mom, s), tensors[s.name + "/Momentum"], s)
         fp.master.copy_(master.to(fp.device))
         fp.momentum.copy_(mom.to(fp.device))
         fp.shadow.copy_(fp.master)

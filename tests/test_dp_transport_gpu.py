@@ -248,7 +248,7 @@ def test_reference_quickstart_two_workers_share_one_gpu(cuda, tmp_path):
 
     args = ["--num_gpus=1", "--train_steps=12", f"--logdir={tmp_path}", "--synthetic_data", "--eval_batches=1",
             "--data_dir=/nonexistent", "--check_consistency_every=1", "--log_device_placement",
-            f"--metrics_file={tmp_path}/m.jsonl", "--dp_probe_steps=20", "--dp_probe_warmup=5"]
+            f"--metrics_file={tmp_path}/m.jsonl", "--dp_schedule=auto", "--dp_probe_steps=20", "--dp_probe_warmup=5"]
     r = launch.launch(1, 2, args, echo=False, timeout_s=300)
     assert r["ok"], r["outputs"]
     outs = {k.split("#")[0]: v for k, v in r["outputs"].items()}
@@ -305,12 +305,15 @@ def test_bench_two_ranks_one_gpu_over_ipc(cuda, sfb, zero):
     assert r["comm_world"] == 2 and len(r["devices"]) == 2 and r["replicas_identical"], r
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_bench_self_launches_n_ranks(cuda, n):
     """``bench.py --gpus N`` with no torchrun: the parent spawns the N ranks itself (they share the
-    one GPU here, so DP goes over IPC with sufficient factors), one JSON line, identical replicas."""
+    one GPU here, so DP goes over IPC with sufficient factors), one JSON line, identical replicas.
+    N = 8 runs every world-8 path of the driver's 8-GPU job once: the five schedule probes (SFB over
+    K = 8 x 128, the |wd1| / 8 ZeRO shard, the W = 8 IPC kernels) and the timed job."""
     r = _bench(["--gpus", str(n), "--steps", "20", "--warmup", "5", "--min_warmup_ms", "50", "--probe_steps", "40",
-                "--probe_warmup", "10"], nproc=n, self_launch=True)
+                "--probe_warmup", "10"], nproc=n, self_launch=True, timeout=800)
     assert r["n_gpus"] == n and r["config"]["parallelism"] == f"dp{n}"
     assert r["comm_world"] == n and len(r["devices"]) == n and r["replicas_identical"], r
     assert r["config"]["global_batch"] == 128 * n and r["value"] > 0
@@ -325,13 +328,16 @@ def test_bench_self_launches_n_ranks(cuda, n):
     assert r["config"]["dp_transport"] == ("ipc+sfb" if "sfb" in sch["chosen"] else "ipc"), r["config"]
 
 
-def test_bench_resnet_self_launch_two_ranks_is_real_dp(cuda):
-    """bench_resnet.py --gpus 2 on one GPU: the IPC bucket reducer carries DP (not two independent
-    replicas): both ranks end with bit-identical weights."""
-    r = _bench(["--gpus", "2", "--depth", "18", "--batch_size", "8", "--image", "64", "--steps", "3", "--warmup", "1",
-                "--bucket_candidates", "0.5,2", "--probe_steps", "3", "--probe_warmup", "1"], nproc=2,
-               script="bench_resnet.py", self_launch=True)
-    assert r["n_gpus"] == 2 and r["config"]["dp_transport"] == "ipc" and r["comm_world"] == 2
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("n,depth", [(2, 18), (8, 50)])
+def test_bench_resnet_self_launch_is_real_dp(cuda, n, depth):
+    """bench_resnet.py --gpus N on one GPU: the IPC bucket reducer carries DP (not N independent
+    replicas): every rank ends with bit-identical weights. N = 8 with ResNet-50 is the driver's
+    8-rank bucket reducer (W = 8 IPC all-reduce of every bucket) at a small batch."""
+    r = _bench(["--gpus", str(n), "--depth", str(depth), "--batch_size", "8", "--image", "64", "--steps", "3",
+                "--warmup", "1", "--bucket_candidates", "0.5,2", "--probe_steps", "3", "--probe_warmup", "1"], nproc=n,
+               script="bench_resnet.py", self_launch=True, timeout=800)
+    assert r["n_gpus"] == n and r["config"]["dp_transport"] == "ipc" and r["comm_world"] == n
     assert r["replicas_identical"], r
     bs = r["config"]["bucket_schedule"]
     c = bs["candidates_ms_per_step"]

@@ -31,6 +31,8 @@ def test_sync_cluster_reference_lines(tmp_path):
         assert f"Worker {i}: Session initialization complete." in w
         assert "Training begins @" in w and "Training elapsed time:" in w and "Mean Accuracy :" in w
         assert f"Worker {i}: training step 3 done (global step: 3)" in w
+    # default --dp_schedule=fixed: one schedule per device/dtype, no probes (reproducible runs)
+    assert "Worker 0: DP schedule flat (fixed)" in w0, w0
     assert latest_checkpoint(str(tmp_path)).endswith("model.ckpt-3")
     assert any(f.startswith("events.out.tfevents.") for f in os.listdir(tmp_path))
     import json
@@ -41,14 +43,14 @@ def test_sync_cluster_reference_lines(tmp_path):
 
 
 def test_sync_cluster_probes_dp_schedule(tmp_path):
-    """--dp_schedule=auto (default) at 2 workers over Gloo: both workers time every CPU candidate
+    """--dp_schedule=auto at 2 workers over Gloo: both workers time every CPU candidate
     before training, the chief prints and logs the choice (the fastest by max over workers), and the
     run trains with it; a pinned schedule skips the probes."""
     import json
 
     mf = tmp_path / "m.jsonl"
     r = launch.launch(1, 2, ["--train_steps=3", f"--logdir={tmp_path}/a", f"--metrics_file={mf}",
-                             "--dp_probe_steps=2"] + COMMON, echo=False, timeout_s=300)
+                             "--dp_schedule=auto", "--dp_probe_steps=2"] + COMMON, echo=False, timeout_s=300)
     assert r["ok"], r["outputs"]
     w0 = _out(r, "worker:0")
     rec = [json.loads(ln) for ln in open(mf) if '"dp_schedule"' in ln]
@@ -128,20 +130,24 @@ def test_existing_servers_mode(tmp_path):
                 p.kill()
 
 
-def test_bench_torchrun_cpu_dry_run():
-    """bench.py's multi-rank contract (torchrun env, barrier, max over ranks, one JSON line on rank 0)."""
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_torchrun_cpu_dry_run(n):
+    """bench.py's multi-rank contract (torchrun env, barrier, max over ranks, one JSON line on rank 0),
+    up to the 8 ranks of the driver's 8-GPU job: probes over Gloo, identical replicas."""
     import json
 
     port = launch.free_port()
-    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    env = dict(os.environ, OMP_NUM_THREADS=str(max(1, (os.cpu_count() or 8) // n)))
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu", "--batch_size", "16"],
-                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+                        "--gpus", str(n), "--steps", "2", "--warmup", "1", "--cpu", "--batch_size", "16"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     rec = json.loads(lines[0])
-    assert rec["n_ranks"] == 2 and rec["config"]["global_batch"] == 32 and rec["value"] > 0
+    assert rec["n_ranks"] == n and rec["config"]["global_batch"] == 16 * n and rec["value"] > 0
+    assert rec["replicas_identical"] and set(rec["schedule"]["candidates_ms_per_step"]) == {"flat", "buckets"}
 
 
 def test_performance_table_tool(tmp_path):
@@ -160,6 +166,32 @@ def test_watchdog_exits_nonzero():
             "w = Watchdog(0.5)\ntime.sleep(5)\n" % ROOT)
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert p.returncode == 3 and "watchdog" in p.stderr
+
+
+def test_phase_watchdog_names_rank_phase_and_error_word():
+    """bench.py / bench_resnet.py's rank-side watchdog: a phase past its limit prints the rank, the
+    phase and the transport's error word, then exits non-zero; a finished phase never fires."""
+    code = ("import time,sys; sys.path.insert(0, %r)\n"
+            "from tensorflow_distributed_amd.utils.tracing import PhaseWatchdog\n"
+            "w = PhaseWatchdog(3, err_fn=lambda: 7)\n"
+            "w.phase('setup', 0.3); time.sleep(0.1); w.done(); time.sleep(1.0)\n"
+            "w.phase('timed region (20 steps)', 0.5); time.sleep(10)\n" % ROOT)
+    env = dict(os.environ, TFD_WATCHDOG_SCALE="1")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, env=env)
+    assert p.returncode == 5, p.stderr
+    assert "rank 3 phase 'timed region (20 steps)'" in p.stderr and "ipc error word 7" in p.stderr, p.stderr
+    assert "'setup'" not in p.stderr
+
+
+def test_bn_deterministic_flag_loads_the_library_first():
+    """dist_main --bn_deterministic: in a fresh process nothing has loaded _C.so when the
+    ResNet worker switches the BN statistics mode; the switch must load it and land in row mode."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from tensorflow_distributed_amd.training.dist_main import _set_bn_mode\n"
+            "_set_bn_mode(True)\n"
+            "import torch; print('slots', int(torch.ops.tfd.bn_part_slots()))\n" % ROOT)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "slots 0" in p.stdout, p.stdout + p.stderr
 
 
 def test_log_device_placement_round_robin():

@@ -98,7 +98,7 @@ def test_resnet_end_to_end_loss_and_head(cuda, row_mode, depth):
     """Whole network: loss and the fc gradient agree with the fp32 reference. (Deep gradients are
     checked block by block below: end to end, train-mode BN over tiny M amplifies bf16 rounding --
     a one-ulp change of a batch statistic moves this loss by up to ~2 %
-    (scripts/debug/bn_slot_race.py), so the statistics are summed in row mode's fixed order here;
+    (tools/debug/bn_slot_race.py), so the statistics are summed in row mode's fixed order here;
     slot mode's atomic order is covered by test_bn_slot_mode_matches_row_mode.)"""
     from tensorflow_distributed_amd.models.resnet import ResNet
 
@@ -181,7 +181,7 @@ def block_case(cuda, depth, bi, hw):
 
 
 # Relative-L2 bounds per tensor kind, row mode (fixed-order BN sums); calibrated on the box over every
-# case below (scripts/debug/resnet_oracle_rel.py, profiles/resnet_oracle_rel_r5.txt; row-mode maxima:
+# case below (tools/debug/resnet_oracle_rel.py, profiles/resnet_oracle_rel_r5.txt; row-mode maxima:
 # out 3e-5, dx 2.2e-3, conv dW 5.7e-4, dgamma 5.2e-4, dbeta 5.8e-4), ~5-10x headroom and far below
 # the 5 % a wrong scale of any one tensor gives.
 REL_BOUND = {"out": 1e-3, "dx": 1e-2, "conv": 5e-3, "gamma": 5e-3, "beta": 5e-3}
@@ -434,7 +434,7 @@ def test_bn_bwd_stats_in_dgrad_epilogue(cuda, row_mode, depth, monkeypatch):
     # the fused path also sums each residual join in another order (GradJoin defers the conv that
     # carries the statistics), so bf16 roundings differ; train-mode BN over these tiny batches
     # amplifies that to 0.8-1.6 % relative at depth 18 / 50 -- as much as the order change alone gives
-    # at 8 x 64^2 images without any deferral (scripts/debug/bn_bwd_stats_rel.py)
+    # at 8 x 64^2 images without any deferral (tools/debug/bn_bwd_stats_rel.py)
     assert rel < 3e-2, rel
     assert ("from_y", False) in kinds and ("bits", True) in kinds, kinds
 
