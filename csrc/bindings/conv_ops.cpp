@@ -493,6 +493,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.impl("conv2d_wgrad", c10::DispatchKey::CUDA, &conv2d_wgrad);
   m.def("conv_gemm_core(int mode) -> int", [](int64_t mode) -> int64_t { return conv_gemm_core((int)mode); });
   m.def("conv_halo_mode(int mode) -> int", [](int64_t mode) -> int64_t { return conv_halo_mode((int)mode); });
+  m.def("conv_wgrad_clear_mode(int mode) -> int", [](int64_t mode) -> int64_t { return conv_wgrad_clear_mode((int)mode); });
   m.def("gemm_nt(Tensor a, Tensor bt) -> Tensor");
   m.impl("gemm_nt", c10::DispatchKey::CUDA, &gemm_nt_op);
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias) -> Tensor");

@@ -82,6 +82,10 @@ int conv_gemm_core(int mode);
 // 3x3 stride-1 convs on LDS halo tiles: 0 off, 1 (default) maps >= 14 wide, 2 every eligible shape;
 // returns the previous mode (-1: query only)
 int conv_halo_mode(int mode);
+// how a split-K weight gradient clears its own accumulator (zeroed = false): 0 a fill kernel (default),
+// 1 hipMemsetAsync (tools/debug/memset_capture_probe.py: the diagnosis of the round-5 replay fault);
+// -1 queries. Returns the previous mode.
+int conv_wgrad_clear_mode(int mode);
 // C[M][N] bf16 = A[M][K] . Bt[N][K]^T on the 256 x 256 core (csrc/kernels/gemm256.hip)
 void gemm_nt_bf16(const uint16_t* a, const uint16_t* bt, uint16_t* c, int M, int N, int K, hipStream_t st);
 

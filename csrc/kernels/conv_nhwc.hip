@@ -1431,10 +1431,20 @@ static void zero_f32(float* p, int64_t n, hipStream_t st) {  // dw may be a 4-B 
   zero_f32_kernel<<<grid, 256, 0, st>>>(p, n);
 }
 
+static int g_wgrad_clear = 0;
+int conv_wgrad_clear_mode(int mode) {
+  const int old = g_wgrad_clear;
+  if (mode >= 0) g_wgrad_clear = mode;
+  return old;
+}
+
 void conv_wgrad(const ConvShape& c, const uint16_t* x, const uint16_t* dy, float* dw, int splits, hipStream_t st,
                 bool zeroed, const BnReluIn* act) {
   const int P = c.N * c.Ho() * c.Wo(), MT = c.R * c.S * c.C;
-  if (splits > 1 && !zeroed) zero_f32(dw, (int64_t)MT * c.K, st);
+  if (splits > 1 && !zeroed) {
+    if (g_wgrad_clear == 1) (void)hipMemsetAsync(dw, 0, (size_t)MT * c.K * sizeof(float), st);
+    else zero_f32(dw, (int64_t)MT * c.K, st);
+  }
   AccF32 epi{dw, MT, c.K, splits > 1 ? 1 : 0};
   DenseX<false> lb{dy, c.K, c.K, P};
   if (act) {

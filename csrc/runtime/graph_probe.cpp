@@ -95,6 +95,34 @@ at::Tensor memset_capture_probe(at::Tensor buf, int64_t replays, int64_t clear_m
   return at::tensor(info, at::TensorOptions().dtype(at::kLong));
 }
 
+// The memset nodes of a captured graph (torch.cuda.CUDAGraph(keep_graph=True).raw_cuda_graph()): one row
+// per node [dst, elementSize, width, height, value, dependency count, dependent count]; row 0 holds the
+// graph's node count and kernel-node count.
+at::Tensor graph_memset_nodes(int64_t graph) {
+  hipGraph_t g = reinterpret_cast<hipGraph_t>(graph);
+  size_t nn = 0;
+  GP_OK(hipGraphGetNodes(g, nullptr, &nn));
+  std::vector<hipGraphNode_t> nodes(nn);
+  GP_OK(hipGraphGetNodes(g, nodes.data(), &nn));
+  std::vector<int64_t> rows(7, 0);
+  rows[0] = (int64_t)nn;
+  for (auto nd : nodes) {
+    hipGraphNodeType t;
+    GP_OK(hipGraphNodeGetType(nd, &t));
+    if (t == hipGraphNodeTypeKernel) rows[1]++;
+    if (t != hipGraphNodeTypeMemset) continue;
+    hipMemsetParams prm{};
+    GP_OK(hipGraphMemsetNodeGetParams(nd, &prm));
+    size_t deps = 0, outs = 0;
+    GP_OK(hipGraphNodeGetDependencies(nd, nullptr, &deps));
+    GP_OK(hipGraphNodeGetDependentNodes(nd, nullptr, &outs));
+    const int64_t r[7] = {(int64_t)(uintptr_t)prm.dst, prm.elementSize, (int64_t)prm.width, (int64_t)prm.height,
+                          prm.value, (int64_t)deps, (int64_t)outs};
+    rows.insert(rows.end(), r, r + 7);
+  }
+  return at::tensor(rows, at::TensorOptions().dtype(at::kLong)).view({-1, 7});
+}
+
 // hipMemsetAsync on the caller's current stream (inside a torch.cuda.graph capture: the path the
 // ResNet wgrad took before the fill kernel replaced it)
 void memset_zero_async(at::Tensor buf) {
@@ -110,6 +138,7 @@ void atomic_add_one(at::Tensor buf) {
 TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.def("memset_capture_probe(Tensor buf, int replays, int clear_mode, int capture_mode) -> Tensor",
         &memset_capture_probe);
+  m.def("graph_memset_nodes(int graph) -> Tensor", &graph_memset_nodes);
   m.def("memset_zero_async(Tensor(a!) buf) -> ()");
   m.impl("memset_zero_async", c10::DispatchKey::CUDA, &memset_zero_async);
   m.def("probe_atomic_add_one(Tensor(a!) buf) -> ()");

@@ -27,6 +27,12 @@ import torch
 ops = None
 
 
+# Backward on autograd's device threads (True) or on the caller's thread (False, the library's
+# choice: see ResNet.train_step). A module constant, not a switch: tools/debug/memset_resnet_probe.py
+# flips it to rebuild the round-5 conditions.
+BACKWARD_ON_AUTOGRAD_THREADS = False
+
+
 def _ops():
     global ops
     if ops is None:
@@ -957,7 +963,7 @@ class ResNet:
             # issued from the engine's thread into a capture owned by this thread broke the host heap
             # once the captured graph was destroyed (profiles/heap_bisect_r5.log; the event record
             # alone still did, about once in 100+ RCCL capture / destroy cycles)
-            with torch.autograd.set_multithreading_enabled(False):  # same speed (profiles/resnet50_backward_thread_ab_r5.log)
+            with torch.autograd.set_multithreading_enabled(BACKWARD_ON_AUTOGRAD_THREADS):  # same speed (profiles/resnet50_backward_thread_ab_r5.log)
                 loss.backward()
         finally:
             self.grads_zeroed = False

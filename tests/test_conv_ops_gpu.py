@@ -430,9 +430,20 @@ def test_width_paired_stem_matches_the_padded_conv(cuda, N, H, W, K):
     assert relerr(dw1, dw0) < 1e-5
 
 
-def test_captured_split_k_wgrad_zeroes_its_accumulator_on_every_replay(cuda):
+@pytest.mark.parametrize("clear", [0, 1])
+def test_captured_split_k_wgrad_zeroes_its_accumulator_on_every_replay(cuda, clear):
     """conv2d_wgrad(zeroed=False) with split-K clears dw itself; captured in a graph and replayed, every
-    replay must give the eager result (a captured hipMemsetAsync did not clear it on replays)."""
+    replay must give the eager result. clear 0: the fill kernel (the library's); 1: hipMemsetAsync, the
+    clear the round-5 replay fault was blamed on -- a captured memset node that clears on every replay
+    here and in tools/debug/memset_capture_probe.py / memset_resnet_probe.py (docs/DESIGN.md §8)."""
+    old = ops.conv_wgrad_clear_mode(clear)
+    try:
+        _split_k_replay(cuda)
+    finally:
+        ops.conv_wgrad_clear_mode(old)
+
+
+def _split_k_replay(cuda):
     torch.manual_seed(4)
     x = rb(torch.randn(16, 14, 14, 64)).to(cuda, torch.bfloat16)  # 3,136 pixels: split-K
     dy = rb(torch.randn(16, 14, 14, 128)).to(cuda, torch.bfloat16)
