@@ -13,6 +13,8 @@
 #include "common.h"
 #include "gemm.h"  // buf_ld
 
+#include <type_traits>
+
 namespace tfd {
 
 __device__ __forceinline__ f32x4 mfma16x16x4f32(float a, float b, const f32x4& c) {
@@ -58,6 +60,16 @@ __device__ __forceinline__ f32x4 buf_ld_f4(const float* base, uint32_t nbytes, u
   const uint4 u = buf_ld(reinterpret_cast<const uint16_t*>(base), nbytes, elem_off * 2u, ok);
   return f32x4{__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)};
 }
+
+// An epilogue with `static constexpr bool STAGED = true` gets the whole C tile through LDS instead of
+// fragment by fragment: the accumulators go to a [BM][BN + 4] float image (the operand tiles' LDS,
+// dead after the last K-step), then epi.tile<BM, BN, NT>(img, BN + 4, m0, n0) stores whole 16-B
+// chunks of rows -- a wave instruction writes 1 KiB of row bytes instead of 4-B scalars in 64-B row
+// pieces (the bf16 step's fc epilogues, docs/DESIGN.md §4c).
+template <class E, class = void>
+struct EpiStaged { static constexpr bool value = false; };
+template <class E>
+struct EpiStaged<E, std::void_t<decltype(E::STAGED)>> { static constexpr bool value = E::STAGED; };
 
 // C tile (m0, n0) over k in [kbeg, kend); WM x WN waves; epilogue epi(m4, n, f32x4 rows m4..m4+3).
 // Two register stages: the global loads of K-tile t+2 are issued while tile t+1 still waits in
@@ -170,11 +182,26 @@ __device__ __forceinline__ void gemm_block_f32(const LA& la, const LB& lb, const
     __syncthreads();
   }
   if (t < nk) compute(A0, B0);
+  if constexpr (EpiStaged<EPI>::value) {
+    constexpr int P = BN + 4;
+    static_assert(BM * P <= 2 * (TA::ELEMS + TB::ELEMS), "the C image fits the operand tiles' LDS");
+    __syncthreads();  // every wave's last fragment reads are done
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-      epi(m0 + wm * WTM + 16 * i + 4 * (lane >> 4), n0 + wn * WTN + 16 * j + (lane & 15), acc[i][j]);
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          smem[(wm * WTM + 16 * i + 4 * (lane >> 4) + r) * P + wn * WTN + 16 * j + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    epi.template tile<BM, BN, NT>(smem, P, m0, n0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        epi(m0 + wm * WTM + 16 * i + 4 * (lane >> 4), n0 + wn * WTN + 16 * j + (lane & 15), acc[i][j]);
+  }
 }
 
 // Row-major fp32 X[rows][ld]: KC: (mn, k) = X[mn][k]; !KC: (mn, k) = X[k][mn]. A chunk is all in or

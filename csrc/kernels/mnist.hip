@@ -187,28 +187,34 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
   const int rot = (int)((blockIdx.x * 1031u) % 3200u);  // per-block start: spread L2 channels
   constexpr int NW = (3200 + 255) / 256;
   uint4 vw[NW];
+#pragma unroll
+  for (int j = 0; j < NW; ++j) vw[j] = zero4();  // defined on both roles' paths (else kept in scratch)
   f32x4 xv = f32x4{0.f, 0.f, 0.f, 0.f}, w1v = f32x4{0.f, 0.f, 0.f, 0.f};
   const int u = t - 256;
-  auto load_w2 = [&]() {
+  // Every load below is unconditional (indices clamped; the LDS stores keep the bounds) and the wave
+  // roles branch on a scalar: exec-masked loads merged by a phi made the compiler wait for a load of
+  // the other role's path (waves 0-3 for their first W2 chunk, waves 4-7 for W1 before issuing the x
+  // image) before the first barrier.
+  const bool w2_role = __builtin_amdgcn_readfirstlane(t >> 6) < 4;
+  if (w2_role) {
+    const int tw = t & 255;  // this role's threads are 0..255 (lets the compiler fold j < NW - 1)
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
-      const int i = (t + 256 * j + rot) % 3200;
-      vw[j] = (t + 256 * j < 3200) ? *reinterpret_cast<const uint4*>(wsrc + (i >> 2) * 64 + (i & 3) * 8) : zero4();
+      const int e = tw + 256 * j, i = (min(e, 3199) + rot) % 3200;  // the last chunk of lanes >= 128: a
+      vw[j] = *reinterpret_cast<const uint4*>(wsrc + (i >> 2) * 64 + (i & 3) * 8);  // duplicate, never stored
     }
-  };
-  if (t < 256) {
-    load_w2();
   } else {
-    if (u < (KTAPS * C1 + C1) / 4) w1v = reinterpret_cast<const f32x4*>(a.p32 + OFF_WC1)[u];
+    const int uw = min(u, (KTAPS * C1 + C1) / 4 - 1), ux = min(u, 195);
+    w1v = reinterpret_cast<const f32x4*>(a.p32 + OFF_WC1)[uw];
     // the prefetched image, loaded speculatively beside its tag and the step
     bool hit = false;
     if (a.perm && a.xpre) {
-      if (u < 196) xv = reinterpret_cast<const f32x4*>(a.xpre + (size_t)b * 784)[u];
+      xv = reinterpret_cast<const f32x4*>(a.xpre + (size_t)b * 784)[ux];
       hit = a.rows[a.B] == (int)*a.step;
     }
     if (!hit) {
       const float* x = a.data + (size_t)data_row(a, b) * 784;
-      if (u < 196) xv = reinterpret_cast<const f32x4*>(x)[u];
+      xv = reinterpret_cast<const f32x4*>(x)[ux];
     }
   }
   C12_STAMP(1);
@@ -315,7 +321,7 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
   }
   C12_STAMP(3);
   // 4. the W2 half (landed during conv1) into LDS
-  if (t < 256) {
+  if (w2_role) {
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
       const int i = (t + 256 * j + rot) % 3200;
@@ -351,12 +357,17 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
     base[j] = (g * C2F_PLANE + px) * 8;
   }
   const bf16* wcol = wt + c2f_wrow(8 * g + q) + 4 * p4;  // rows tap*32 + 8g + q (+4)
+  // the conv2 bias loads before the K loop (in the epilogue they were one more memory round trip
+  // after the last MFMA)
+  float bbv[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) bbv[nt] = a.p32[OFF_BC2 + nh * 32 + nt * 16 + (lane & 15)];
   conv2_taps(img, wcol, base, acc);
   C12_STAMP(5);
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
     const int n = nh * 32 + nt * 16 + (lane & 15);
-    const float bb = a.p32[OFF_BC2 + n];
+    const float bb = bbv[nt];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int m4 = (w + 8 * j) * 16 + 4 * g;
@@ -411,23 +422,32 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   HEAD_STAMP(0);
   const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n0 = 4 * t;
-#define HEAD_W(j, c) (a.p32 + OFF_OUT)[(size_t)(n0 + (j)) * NCLS + (c)]
-  if (a.t_out && row == 0 && t == 0) *a.t_out = *a.step + 1;
-  // the label's dependent chain (step -> perm -> label) starts first, hidden behind the fc1 math
-  const int lbl = batch_label(a, row);
+  // Every operand that does not depend on the label is requested first, in one memory round trip:
+  // the split-K slabs, the fc1 bias, this thread's 4 x 10 output-layer weights (160 contiguous bytes)
+  // and the output bias. Then the label chain (step -> tag / prefetched label, or step -> perm ->
+  // label): uniform addresses with no store before them in the kernel, so they are scalar loads that
+  // run beside the vector loads (issued first, the chain's branches held the slab loads back by three
+  // round trips, and the t_out store in front of it made every later load a vector load).
+  f32x4 p[FC1_SPLITS];
+#pragma unroll
+  for (int s = 0; s < FC1_SPLITS; ++s) p[s] = *reinterpret_cast<const f32x4*>(a.fc1_slab + ((size_t)s * a.B + row) * HID + n0);
+  f32x4 wo[NCLS];
+#pragma unroll
+  for (int q = 0; q < NCLS; ++q) wo[q] = reinterpret_cast<const f32x4*>(a.p32 + OFF_OUT + (size_t)n0 * NCLS)[q];
+#define HEAD_W(j, c) wo[((j) * NCLS + (c)) >> 2][((j) * NCLS + (c)) & 3]
+  float bout[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) bout[c] = a.p32[OFF_BOUT + c];
   f32x4 h = *reinterpret_cast<const f32x4*>(a.p32 + OFF_BD1 + n0);
-  {  // all split-K slab loads in flight together (compile-time count: no per-load branches)
-    f32x4 p[FC1_SPLITS];
+  const int64_t st = *a.step;
+  const int lbl = batch_label(a, row);
+  if (a.t_out && row == 0 && t == 0) *a.t_out = st + 1;
 #pragma unroll
-    for (int s = 0; s < FC1_SPLITS; ++s) p[s] = *reinterpret_cast<const f32x4*>(a.fc1_slab + ((size_t)s * a.B + row) * HID + n0);
-#pragma unroll
-    for (int s = 0; s < FC1_SPLITS; ++s) h += p[s];
-  }
+  for (int s = 0; s < FC1_SPLITS; ++s) h += p[s];
   HEAD_STAMP(1);
   float hd[4], scale[4];
   const float kp = train ? a.keep_prob : 1.0f;
   if (kp < 1.0f) {
-    const int64_t st = *a.step;
     Philox4 r = philox4x32_10((uint32_t)(row * 256 + t), (uint32_t)st, (uint32_t)(st >> 32), a.rank, a.seed,
                               0x5EED1234u);
 #pragma unroll
@@ -459,7 +479,7 @@ __global__ __launch_bounds__(256) void head_kernel(MnistStepArgs a, int train) {
   __syncthreads();
   float logit[NCLS];
 #pragma unroll
-  for (int c = 0; c < NCLS; ++c) logit[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + a.p32[OFF_BOUT + c];
+  for (int c = 0; c < NCLS; ++c) logit[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + bout[c];
   float mx = logit[0];
   int am = 0;
 #pragma unroll

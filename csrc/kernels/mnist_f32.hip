@@ -200,11 +200,11 @@ __global__ __launch_bounds__(512) void f32_conv12_fwd_lds(MnistF32Args a) {
   f32x4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = zero_f4();
+  const int n = nh * 32 + nt * 16 + i;
+  const float bb = a.p32[OFF_BC2 + n];  // before the K loop: its latency hides behind the MFMAs
   if (w < 2) f32_conv2_taps<4>(img, wt, abase, bbase, acc);
   else f32_conv2_taps<3>(img, wt, abase, bbase, acc);
   // 3. bias + relu + 2x2 max pool + argmax in registers: lane's 4 rows are one pool window
-  const int n = nh * 32 + nt * 16 + i;
-  const float bb = a.p32[OFF_BC2 + n];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int f = w + 8 * j, m4 = (f >> 1) * 16 + 4 * g;
@@ -225,16 +225,24 @@ __global__ __launch_bounds__(512) void f32_conv12_fwd_lds(MnistF32Args a) {
 constexpr int F_BK = 32;  // K-tile of the fp32 GEMM blocks (64: 188 vs 172 us/step, fewer blocks per CU; profiles/mnist_fp32_kernels_r5.txt)
 
 // ---------------- K4: fc1 forward, split-K slabs (reduced by the head) ----------------
-struct SlabEpiF {
+// Row-major fp32 C (ld, M x N valid, N and ld multiples of 4) stored from the LDS-staged tile: thread
+// i of the block stores 16-B chunks of rows (gemm_block_f32's STAGED epilogue form).
+struct RowsEpiF {
+  static constexpr bool STAGED = true;
   float* __restrict__ out;
   int ld, M, N;
-  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
-    if (n >= N) return;
+  template <int BM, int BN, int NT>
+  __device__ __forceinline__ void tile(const float* img, int P, int m0, int n0) const {
+    constexpr int CPR = BN / 4;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (m4 + r < M) out[(size_t)(m4 + r) * ld + n] = v[r];
+    for (int i = threadIdx.x; i < BM * CPR; i += NT) {
+      const int r = i / CPR, c = (i - r * CPR) * 4, m = m0 + r, n = n0 + c;
+      if (m < M && n < N)
+        *reinterpret_cast<f32x4*>(out + (size_t)m * ld + n) = *reinterpret_cast<const f32x4*>(img + r * P + c);
+    }
   }
 };
+using SlabEpiF = RowsEpiF;
 constexpr int F_FC1_SPLITS = 7;  // 3136 = 7 x 448
 __global__ __launch_bounds__(256) void f32_fc1_fwd(MnistF32Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -251,20 +259,27 @@ __global__ __launch_bounds__(256) void f32_fc1_fwd(MnistF32Args a) {
 __global__ __launch_bounds__(256) void f32_head(MnistF32Args a, int train) {
   const int row = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int n0 = 4 * t;
-  if (a.t_out && row == 0 && t == 0) *a.t_out = *a.step + 1;
-  const int lbl = a.labels[data_row_f(a.perm, a.step, a.n_data, a.B, row)];
+  // the label-independent operands first (slabs, fc1 bias, output-layer weights and bias: one memory
+  // round trip), then the label chain as scalar loads beside them, the t_out store after it (the bf16
+  // head kernel's order, mnist.hip)
+  f32x4 p[F_FC1_SPLITS];
+#pragma unroll
+  for (int s = 0; s < F_FC1_SPLITS; ++s) p[s] = *reinterpret_cast<const f32x4*>(a.fc1_slab + ((size_t)s * a.B + row) * HID + n0);
+  f32x4 wo[NCLS];
+#pragma unroll
+  for (int q = 0; q < NCLS; ++q) wo[q] = reinterpret_cast<const f32x4*>(a.p32 + OFF_OUT + (size_t)n0 * NCLS)[q];
   f32x4 h = *reinterpret_cast<const f32x4*>(a.p32 + OFF_BD1 + n0);
-  {
-    f32x4 p[F_FC1_SPLITS];
+  float bout[NCLS];
 #pragma unroll
-    for (int s = 0; s < F_FC1_SPLITS; ++s) p[s] = *reinterpret_cast<const f32x4*>(a.fc1_slab + ((size_t)s * a.B + row) * HID + n0);
+  for (int c = 0; c < NCLS; ++c) bout[c] = a.p32[OFF_BOUT + c];
+  const int64_t st = *a.step;
+  const int lbl = a.labels[data_row_f(a.perm, a.step, a.n_data, a.B, row)];
+  if (a.t_out && row == 0 && t == 0) *a.t_out = st + 1;
 #pragma unroll
-    for (int s = 0; s < F_FC1_SPLITS; ++s) h += p[s];
-  }
+  for (int s = 0; s < F_FC1_SPLITS; ++s) h += p[s];
   float hd[4], scale[4];
   const float kp = train ? a.keep_prob : 1.0f;
   if (kp < 1.0f) {
-    const int64_t st = *a.step;
     Philox4 r = philox4x32_10((uint32_t)(row * 256 + t), (uint32_t)st, (uint32_t)(st >> 32), a.rank, a.seed, 0x5EED1234u);
 #pragma unroll
     for (int j = 0; j < 4; ++j) scale[j] = (u01(r.v[j]) < kp) ? (1.0f / kp) : 0.f;
@@ -274,15 +289,14 @@ __global__ __launch_bounds__(256) void f32_head(MnistF32Args a, int train) {
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) hd[j] = fmaxf(h[j], 0.f) * scale[j];
-  const float* wout = a.p32 + OFF_OUT;
+#define F32_HEAD_W(j, c) wo[((j) * NCLS + (c)) >> 2][((j) * NCLS + (c)) & 3]
   float lp[NCLS];
 #pragma unroll
   for (int c = 0; c < NCLS; ++c) lp[c] = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float* wr = wout + (size_t)(n0 + j) * NCLS;
 #pragma unroll
-    for (int c = 0; c < NCLS; ++c) lp[c] = fmaf(hd[j], wr[c], lp[c]);
+    for (int c = 0; c < NCLS; ++c) lp[c] = fmaf(hd[j], F32_HEAD_W(j, c), lp[c]);
   }
   __shared__ float red[4][NCLS];
   wave_sums_to_lane63(lp);  // DPP, interleaved over the 10 classes (was 10 shuffle-based wave sums)
@@ -293,7 +307,7 @@ __global__ __launch_bounds__(256) void f32_head(MnistF32Args a, int train) {
   __syncthreads();
   float logit[NCLS];
 #pragma unroll
-  for (int c = 0; c < NCLS; ++c) logit[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + a.p32[OFF_BOUT + c];
+  for (int c = 0; c < NCLS; ++c) logit[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + bout[c];
   float mx = logit[0];
   int am = 0;
 #pragma unroll
@@ -318,12 +332,12 @@ __global__ __launch_bounds__(256) void f32_head(MnistF32Args a, int train) {
   float dhv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float* wr = wout + (size_t)(n0 + j) * NCLS;
     float d = 0.f;
 #pragma unroll
-    for (int c = 0; c < NCLS; ++c) d = fmaf(dl[c], wr[c], d);
+    for (int c = 0; c < NCLS; ++c) d = fmaf(dl[c], F32_HEAD_W(j, c), d);
     dhv[j] = (h[j] > 0.f) ? d * scale[j] : 0.f;
   }
+#undef F32_HEAD_W
   *reinterpret_cast<f32x4*>(a.hd + (size_t)row * HID + n0) = f32x4{hd[0], hd[1], hd[2], hd[3]};
   *reinterpret_cast<f32x4*>(a.dh + (size_t)row * HID + n0) = f32x4{dhv[0], dhv[1], dhv[2], dhv[3]};
 }
@@ -375,35 +389,39 @@ struct OnesRowMCF {  // (mn, k) = X[k][mn] for mn < mn_real, 1 for mn == mn_real
     return mn == mn_real && k < k_lim ? f32x4{1.f, 0.f, 0.f, 0.f} : v;
   }
 };
-struct GradEpiF {
-  float* __restrict__ out;
-  int ld, M, N;
-  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
-    if (n >= N) return;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (m4 + r < M) out[(size_t)(m4 + r) * ld + n] = v[r];
-  }
-};
+using GradEpiF = RowsEpiF;
+// dX tile (BM batch rows x the 64 channels of ONE pooled pixel) -> dz2 through conv2's relu and the
+// 2x2 pool's argmax, from the LDS-staged tile: thread (row b, 4-channel chunk) loads the relu output
+// (16 B) and argmax (4 B) chunks once and writes the window as four whole 16-B chunks of dz2 (the
+// fragment-order form made 16 scattered 4-B stores and 2 x 4 scalar loads per lane and value group).
 struct UnpoolEpiF {
+  static constexpr bool STAGED = true;
   const float* __restrict__ p2;
   const uint8_t* __restrict__ idx2;
   float* __restrict__ dz2;
   int B;
-  __device__ __forceinline__ void operator()(int m4, int n, f32x4 v) const {
-    if (n >= FEAT) return;
-    const int pp = n >> 6, c = n & 63, ph = pp / 7, pw = pp - ph * 7;
+  template <int BM, int BN, int NT>
+  __device__ __forceinline__ void tile(const float* img, int P, int m0, int n0) const {
+    static_assert(BN == 64, "a dX tile is the 64 channels of one pooled pixel");
+    const int pp = n0 >> 6, ph = pp / 7, pw = pp - ph * 7;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = m4 + r;
-      if (b >= B) continue;
-      const size_t o = (size_t)b * FEAT + n;
-      const float g = p2[o] > 0.f ? v[r] : 0.f;  // relu output > 0
-      const int w = idx2[o];
+    for (int i = threadIdx.x; i < BM * 16; i += NT) {
+      const int r = i >> 4, c = (i & 15) * 4, b = m0 + r;
+      if (b >= B || pp >= 49) continue;
+      const size_t o = (size_t)b * FEAT + n0 + c;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * P + c);
+      const f32x4 pv = *reinterpret_cast<const f32x4*>(p2 + o);
+      const uint32_t w4 = *reinterpret_cast<const uint32_t*>(idx2 + o);
+      f32x4 g;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g[k] = pv[k] > 0.f ? v[k] : 0.f;  // relu output > 0
 #pragma unroll
       for (int wi = 0; wi < 4; ++wi) {
+        f32x4 ov;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ov[k] = (int)((w4 >> (8 * k)) & 0xffu) == wi ? g[k] : 0.f;
         const int oh = 2 * ph + (wi >> 1), ow = 2 * pw + (wi & 1);
-        dz2[((size_t)(b * 14 + oh) * 14 + ow) * 64 + c] = (wi == w) ? g : 0.f;
+        *reinterpret_cast<f32x4*>(dz2 + ((size_t)(b * 14 + oh) * 14 + ow) * 64 + c) = ov;
       }
     }
   }
