@@ -59,6 +59,26 @@ __device__ __forceinline__ int data_row(const MnistStepArgs& a, int b) {
   }
   return data_row(a.perm, a.step, a.n_data, a.B, b);
 }
+// data_row split in two: the three independent loads (step, tag, prefetched row) issued early, the
+// choice (and, on a prefetch miss, the dependent perm load) made where the row is used, so the chain
+// costs no wait of its own where it is consumed
+struct RowPre {
+  int64_t step;
+  int tag, row;
+};
+__device__ __forceinline__ RowPre data_row_pre(const MnistStepArgs& a, int b) {
+  RowPre r{0, -1, b};
+  if (a.perm) {
+    r.step = *a.step;
+    if (a.rows) { r.tag = a.rows[a.B]; r.row = a.rows[b]; }
+  }
+  return r;
+}
+__device__ __forceinline__ int data_row_use(const MnistStepArgs& a, const RowPre& r, int b) {
+  if (!a.perm) return b;
+  if (a.rows && r.tag == (int)r.step) return r.row;
+  return a.perm[(int)((r.step * (int64_t)a.B + b) % (int64_t)a.n_data)];
+}
 // gather block b: the batch row b of step `next` into rows / xpre / ypre; block 0 also writes the
 // tag (visibility to the next kernel is the kernel boundary)
 __device__ __forceinline__ void gather_next(const MnistStepArgs& a, int64_t next, int b) {
@@ -955,6 +975,9 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
   const int b = bid >> 1, h = bid & 1, t = threadIdx.x;
   const uint16_t* src = a.dz2 + (size_t)b * 196 * 64;
   const uint16_t* wsrc = a.pbf + OFF_WC2;
+  // the tail's x image row: its loads go out before the staging, whose wait then covers them (as a
+  // chain issued after the staging, two dependent round trips held waves 4-7 at the next barrier)
+  const RowPre xr = data_row_pre(a, b);
   {
     constexpr int CI = 8 * C2D_PLANE, NI = (CI + 511) / 512;  // 1792 chunks -> 4 per thread
     {  // 6400 weight chunks = 100 LDS-DMA wave instructions, 12-13 per wave, all in flight at once
@@ -986,11 +1009,11 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
   // only LDS), so their latency hides behind it: waves 4-7 the x image and the argmax bytes, waves
   // 0-3 the conv1 relu outputs that mask their dX rows
   float xpre[4];
-  uint16_t p1pre[2][2][4];
-  uint8_t ipb[2][2][4];  // the argmax window position of each dX value
+  uint32_t p1pre[2][2][4];  // conv1 relu outputs (bf16 bits) and argmax window positions of the dX
+  uint32_t ipb[2][2][4];    // values, 32-bit so the asm uses below can pin them in VGPRs
   if (kq) {
     const int u = t - 256;
-    const float* xrow = a.data + (size_t)data_row(a, b) * 784;
+    const float* xrow = a.data + (size_t)data_row_use(a, xr, b) * 784;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int i = 4 * u + q, r = i >> 5, c = i & 31;
@@ -1072,6 +1095,15 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
     bf16* dz1 = reinterpret_cast<bf16*>(smem_raw + C2D_Z_OFF);
     bf16* xsh = reinterpret_cast<bf16*>(smem_raw + C2D_XS_OFF);
     if (!kq) {  // dX (+ the parked K half) through conv1's relu mask, scattered to the argmax pixel
+      // the relu / argmax bytes are first touched here: without these empty asm uses the compiler
+      // turned the relu values into compare masks right after their loads, i.e. waves 0-3 waited for
+      // 32 scattered loads before the K loop's barrier instead of behind the K loop
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(p1pre[j][nt][r]), "+v"(ipb[j][nt][r]));
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         if (j == 1 && !two) break;

@@ -573,13 +573,6 @@ __device__ __forceinline__ void f32_conv2_dgrad_body(const MnistF32Args& a, int 
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       p1pre[j][e] = a.p1[((size_t)b * 196 + (7 * h + (j ? r1 : r0)) * 14 + min(4 * g + e, 13)) * 32 + nt * 16 + i];
-  if (t < 196) {  // x into the zero-bordered image (zeroed before the barrier above)
-    const int r = (4 * t) / 28, c = (4 * t) % 28;
-    float* d = xs + (r + 2) * 32 + c + 2;
-    d[0] = xv[0]; d[1] = xv[1]; d[2] = xv[2]; d[3] = xv[3];
-  } else if (t >= 256 && t < 256 + 196) {
-    reinterpret_cast<uint4*>(is)[t - 256] = iv;
-  }
   f32x4 acc[2] = {zero_f4(), zero_f4()};
   const int role = w < 4 ? -1 : ((w >> 1) & 1);
   for (int stg = 0; stg < F2D_NST; ++stg) {
@@ -591,6 +584,21 @@ __device__ __forceinline__ void f32_conv2_dgrad_body(const MnistF32Args& a, int 
     if (stg + 1 < F2D_NST) sstore_w((stg & 1) ? wb0 : wb1);
     __syncthreads();
   }
+  // the tail's x image and argmax bytes into LDS only now (their own regions, untouched by the K
+  // loop): stored before it, the x row's dependent chain (step -> perm -> x) and the relu bytes held
+  // waves 0-3 at the first K stage; the empty asm uses keep the relu compares from being hoisted to
+  // right after their loads for the same reason
+  if (t < 196) {  // x into the zero-bordered image (zeroed before the first barrier)
+    const int r = (4 * t) / 28, c = (4 * t) % 28;
+    float* d = xs + (r + 2) * 32 + c + 2;
+    d[0] = xv[0]; d[1] = xv[1]; d[2] = xv[2]; d[3] = xv[3];
+  } else if (t >= 256 && t < 256 + 196) {
+    reinterpret_cast<uint4*>(is)[t - 256] = iv;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(p1pre[j][e]));
   // row 6: waves 6, 7 (co half 1) park their partial tile, waves 4, 5 (co half 0) add it
   f32x4* park = reinterpret_cast<f32x4*>(smem_raw);  // the dz2 image is dead
   if (w >= 6) park[(w - 6) * 64 + lane] = acc[1];
