@@ -360,6 +360,9 @@ __device__ __forceinline__ void gemm_block_oneshot(const LA& la, const LB& lb, c
       }
     }
   }
+  // every load is issued before the first LDS store: without this fence the scheduler interleaves
+  // them (to save registers) and the staging becomes several round trips
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int t = 0; t < NKT; ++t) {
 #pragma unroll
@@ -445,6 +448,22 @@ struct DenseLoader {
       for (int j = 0; j < 8; ++j) t[j] = (mn + j < mn_lim) ? x[(size_t)k * ld + mn + j] : 0;
       return *reinterpret_cast<uint4*>(t);
     }
+  }
+};
+
+// DenseLoader for shapes whose chunked dimension is a multiple of 8 (k_lim for KC, mn_lim for !KC),
+// so a chunk is all in or all out: one raw buffer load per chunk, out-of-range chunks read as zeros
+// by the hardware range check. No branch: DenseLoader's exec-masked loads merged by a phi made the
+// compiler copy a loaded register (and so drain vmcnt) in the middle of a prologue's load batch.
+template <bool KC_>
+struct DenseLoaderX {
+  static constexpr bool KC = KC_;
+  const uint16_t* __restrict__ x;
+  int ld, mn_lim, k_lim;
+  __device__ __forceinline__ uint4 operator()(int mn, int k) const {
+    const bool ok = mn < mn_lim && k < k_lim;
+    if constexpr (KC) return buf_ld(x, (uint32_t)mn_lim * (uint32_t)ld * 2u, (uint32_t)mn * (uint32_t)ld + (uint32_t)k, ok);
+    else return buf_ld(x, (uint32_t)k_lim * (uint32_t)ld * 2u, (uint32_t)k * (uint32_t)ld + (uint32_t)mn, ok);
   }
 };
 

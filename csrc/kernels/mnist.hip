@@ -424,8 +424,9 @@ constexpr int FC1_NKT = FEAT / FC1_SPLITS / FC1_BK;  // K-tiles per split
 static_assert(FC1_NKT * FC1_BK * FC1_SPLITS == FEAT, "fc1 split-K must tile K exactly");
 __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  DenseLoader<true> la{a.p2, FEAT, a.B, FEAT};
-  DenseLoader<false> lb{a.pbf + OFF_WD1, HID, HID, FEAT};
+  static_assert(FEAT % 8 == 0 && HID % 8 == 0, "whole chunks (DenseLoaderX)");
+  DenseLoaderX<true> la{a.p2, FEAT, a.B, FEAT};
+  DenseLoaderX<false> lb{a.pbf + OFF_WD1, HID, HID, FEAT};
   const int z = blockIdx.z;
   SlabEpi epi{a.fc1_slab + (size_t)z * a.B * HID, HID, a.B, HID};
   const int kb = z * kper;
@@ -655,7 +656,7 @@ __device__ __forceinline__ void fc1_dw_tile(const MnistStepArgs& a, const LA& la
 }
 __device__ __forceinline__ void fc1_dw_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
   OnesRowBuf la{a.p2, a.B, (uint32_t)((int64_t)a.B * FEAT * 2)};
-  DenseLoader<false> lb{a.dh, HID, HID, a.B};
+  DenseLoaderX<false> lb{a.dh, HID, HID, a.B};
   fc1_dw_tile(a, la, lb, by * FDW_BM, bx * FDW_BN, a.B, smem);
 }
 
@@ -785,8 +786,8 @@ __device__ __forceinline__ void fc1_dx_block_dma(const MnistStepArgs& a, int bx,
 
 template <int BN = FDX_BN, int RS = FDX_RS>
 __device__ __forceinline__ void fc1_dx_block(const MnistStepArgs& a, int bx, int by, bf16* smem) {
-  DenseLoader<true> la{a.dh, HID, a.B, HID};
-  DenseLoader<true> lb{a.pbf + OFF_WD1, HID, FEAT, HID};
+  DenseLoaderX<true> la{a.dh, HID, a.B, HID};
+  DenseLoaderX<true> lb{a.pbf + OFF_WD1, HID, FEAT, HID};
   f32x4 acc[FDX_BM / 32][BN / 32];
   gemm_mainloop<FDX_BM, BN, FDX_BK, 2, 2, decltype(la), decltype(lb), RS>(la, lb, by * FDX_BM, bx * BN, 0, HID, smem,
                                                                           acc);  // ends with a barrier
@@ -1573,7 +1574,7 @@ void mnist_forward_conv(const MnistStepArgs& a, hipStream_t s) {
 void mnist_forward_fc(const MnistStepArgs& a, bool train, hipStream_t s) {
   const int B = a.B;
   {
-    constexpr int sm = GemmSmemOneshot<FC1_BM, FC1_BN, FC1_BK, FC1_NKT, DenseLoader<true>, DenseLoader<false>>::BYTES;
+    constexpr int sm = GemmSmemOneshot<FC1_BM, FC1_BN, FC1_BK, FC1_NKT, DenseLoaderX<true>, DenseLoaderX<false>>::BYTES;
     static_assert(sm <= 160 * 1024, "fc1 one-shot LDS");
     set_smem<fc1_fwd>(sm);
     const int kper = (FEAT + a.fc1_splits - 1) / a.fc1_splits;
@@ -1585,9 +1586,9 @@ void mnist_forward_fc(const MnistStepArgs& a, bool train, hipStream_t s) {
 
 void mnist_backward_a(const MnistStepArgs& a, hipStream_t s, int part) {
   const int B = a.B;
-  constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowBuf, DenseLoader<false>>::BYTES;
+  constexpr int sm_dw = GemmSmem<FDW_BM, FDW_BN, FDW_BK, OnesRowBuf, DenseLoaderX<false>>::BYTES;
   static_assert(sm_dw >= FDW_BM * FDW_PITCH * 4, "fc1 dW staging image fits the GEMM's LDS");
-  constexpr int sm_dx = GemmSmem<FDX_BM, FDX_BN, FDX_BK, DenseLoader<true>, DenseLoader<true>>::BYTES;
+  constexpr int sm_dx = GemmSmem<FDX_BM, FDX_BN, FDX_BK, DenseLoaderX<true>, DenseLoaderX<true>>::BYTES;
   static_assert(sm_dx >= FDX_BM * (FDX_BN + 4) * 4, "fc1 dX staging image fits the GEMM's LDS");
   const int sm_og = (B * NCLS + 4 * OUTG_ROWS * NCLS) * 4;
   const int sm = std::max(std::max(sm_dw, part == 2 ? sm_dx : FDXD_SMEM), sm_og);
