@@ -5,7 +5,7 @@
 // the capturing stream, then accumulated with atomics; on graph replays the stem gradient grew to
 // inf, as if the clear did not run (tools/debug/stem_mode_check.py). The engine now clears with a
 // kernel (conv_nhwc.hip zero_f32). This probe captures the same pattern in isolation --
-//     +1 (atomics)  ->  clear  ->  +1 (atomics)
+//     +1 (atomics)  ->  clear  ->  +1 (atomics)      (capture_mode bit 2: clear -> +1, the clear a root node)
 // -- on a caller-given buffer (so a 4-B aligned view of a flat buffer can be tested against a
 // 256-B aligned one), instantiates and replays it, and reports the graph's nodes (type, the memset
 // node's parameters and dependency count) and the buffer after the replays (every element must be
@@ -41,12 +41,13 @@ at::Tensor memset_capture_probe(at::Tensor buf, int64_t replays, int64_t clear_m
   GP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   probe_fill(p, n, 5.f, s);
   GP_OK(hipStreamSynchronize(s));
-  const hipStreamCaptureMode mode = capture_mode == 0 ? hipStreamCaptureModeGlobal
-                                    : capture_mode == 1 ? hipStreamCaptureModeThreadLocal
-                                                        : hipStreamCaptureModeRelaxed;
+  const int cm = (int)(capture_mode & 3);
+  const hipStreamCaptureMode mode = cm == 0 ? hipStreamCaptureModeGlobal
+                                    : cm == 1 ? hipStreamCaptureModeThreadLocal
+                                              : hipStreamCaptureModeRelaxed;
   hipGraph_t g = nullptr;
   GP_OK(hipStreamBeginCapture(s, mode));
-  probe_add_one(p, n, s);
+  if (!(capture_mode & 4)) probe_add_one(p, n, s);  // bit 2: the clear is the graph's root node
   if (clear_mode == 0) GP_OK(hipMemsetAsync(p, 0, n * sizeof(float), s));
   else if (clear_mode == 1) GP_OK(hipMemsetD32Async((hipDeviceptr_t)p, 0, (size_t)n, s));
   else probe_fill(p, n, 0.f, s);

@@ -430,12 +430,17 @@ def test_width_paired_stem_matches_the_padded_conv(cuda, N, H, W, K):
     assert relerr(dw1, dw0) < 1e-5
 
 
-@pytest.mark.parametrize("clear", [0, 1])
+MEMSET_RACE = ("platform: a captured hipMemsetAsync node (a root node, 32 KB) is intermittently not ordered "
+               "before the kernel that depends on it on graph replays -- 2048 of 8192 accumulator elements "
+               "garbage from replay 1 on some boxes, clean on others (profiles/memset_capture_probe_r6.log)")
+
+
+@pytest.mark.parametrize("clear", [0, pytest.param(1, marks=pytest.mark.xfail(strict=False, reason=MEMSET_RACE))])
 def test_captured_split_k_wgrad_zeroes_its_accumulator_on_every_replay(cuda, clear):
     """conv2d_wgrad(zeroed=False) with split-K clears dw itself; captured in a graph and replayed, every
-    replay must give the eager result. clear 0: the fill kernel (the library's); 1: hipMemsetAsync, the
-    clear the round-5 replay fault was blamed on -- a captured memset node that clears on every replay
-    here and in tools/debug/memset_capture_probe.py / memset_resnet_probe.py (docs/DESIGN.md §8)."""
+    replay must give the eager result. clear 0: the fill kernel (the library's); 1: hipMemsetAsync, kept
+    as the platform reproducer (xfail, not strict: it passes on some boxes) -- which is why no capturable
+    path issues a memset (tests/test_source_hygiene_cpu.py, docs/DESIGN.md §8)."""
     old = ops.conv_wgrad_clear_mode(clear)
     try:
         _split_k_replay(cuda)

@@ -59,3 +59,23 @@ def test_resnet_model_reads_no_ab_environment_variables():
     assert not re.search(r"environ(?:\.get)?\(?\[?[\"']TFD_", src)
     conv = open(os.path.join(ROOT, "csrc", "kernels", "conv_nhwc.hip")).read()
     assert "getenv" not in conv
+
+
+def test_no_memset_on_capturable_paths():
+    """A captured hipMemsetAsync node is not reliably ordered before its dependent kernel on graph
+    replays on this platform (profiles/memset_capture_probe_r6.log, docs/DESIGN.md §8): every buffer a
+    captured step clears is cleared by a kernel. Allowed: the GPU parameter server's eager service
+    (its own stream, synchronized right after, never captured), the reproducer itself, and the
+    split-K wgrad's diagnostic clear mode 1 (conv_wgrad_clear_mode, off unless a probe selects it)."""
+    allowed = {("runtime", "gpu_ps.cpp"), ("runtime", "graph_probe.cpp")}
+    bad = []
+    for p in SOURCES:
+        rel = os.path.relpath(p, os.path.join(ROOT, "csrc"))
+        key = tuple(rel.split(os.sep)[-2:])
+        for i, ln in enumerate(open(p), 1):
+            if "hipMemsetAsync" not in ln or ln.strip().startswith("//") or key in allowed:
+                continue
+            if key == ("kernels", "conv_nhwc.hip") and "g_wgrad_clear == 1" in ln:
+                continue
+            bad.append(f"{rel}:{i}: {ln.strip()}")
+    assert not bad, "\n".join(bad)
