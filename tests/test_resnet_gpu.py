@@ -394,7 +394,7 @@ def test_capture_destroy_cycles_keep_the_heap_intact(cuda, mode, cycles):
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, MALLOC_CHECK_="3", MALLOC_PERTURB_="165")
-    p = subprocess.run([sys.executable, os.path.join(root, "scripts", "debug", "rn_configure_loop.py"), mode,
+    p = subprocess.run([sys.executable, os.path.join(root, "tools", "debug", "rn_configure_loop.py"), mode,
                         str(cycles)], capture_output=True, text=True, timeout=280, cwd=root, env=env)
     assert p.returncode == 0 and "done" in p.stdout, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
 
