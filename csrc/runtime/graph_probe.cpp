@@ -124,6 +124,23 @@ at::Tensor graph_memset_nodes(int64_t graph) {
   return at::tensor(rows, at::TensorOptions().dtype(at::kLong)).view({-1, 7});
 }
 
+// Node count of a captured graph per hipGraphNodeType (index = the enum value: 0 kernel, 1 memcpy,
+// 2 memset, 3 host, 4 child graph, 5 empty, 6 wait event, 7 event record, ...).
+at::Tensor graph_node_types(int64_t graph) {
+  hipGraph_t g = reinterpret_cast<hipGraph_t>(graph);
+  size_t nn = 0;
+  GP_OK(hipGraphGetNodes(g, nullptr, &nn));
+  std::vector<hipGraphNode_t> nodes(nn);
+  GP_OK(hipGraphGetNodes(g, nodes.data(), &nn));
+  std::vector<int64_t> counts(16, 0);
+  for (auto nd : nodes) {
+    hipGraphNodeType t;
+    GP_OK(hipGraphNodeGetType(nd, &t));
+    counts[std::min<int>((int)t, 15)]++;
+  }
+  return at::tensor(counts, at::TensorOptions().dtype(at::kLong));
+}
+
 // hipMemsetAsync on the caller's current stream (inside a torch.cuda.graph capture: the path the
 // ResNet wgrad took before the fill kernel replaced it)
 void memset_zero_async(at::Tensor buf) {
@@ -140,6 +157,7 @@ TORCH_LIBRARY_FRAGMENT(tfd, m) {
   m.def("memset_capture_probe(Tensor buf, int replays, int clear_mode, int capture_mode) -> Tensor",
         &memset_capture_probe);
   m.def("graph_memset_nodes(int graph) -> Tensor", &graph_memset_nodes);
+  m.def("graph_node_types(int graph) -> Tensor", &graph_node_types);
   m.def("memset_zero_async(Tensor(a!) buf) -> ()");
   m.impl("memset_zero_async", c10::DispatchKey::CUDA, &memset_zero_async);
   m.def("probe_atomic_add_one(Tensor(a!) buf) -> ()");

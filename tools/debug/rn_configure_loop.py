@@ -132,9 +132,14 @@ for it in range(iters):
         if it % 10 == 0:
             print(f"iter {it} ok", flush=True)
         continue
-    graph = torch.cuda.CUDAGraph()
+    graph = torch.cuda.CUDAGraph(keep_graph=it == 0)
     with torch.cuda.graph(graph):
         out = m.train_step(x, y, lr=0.1)
+    if it == 0:  # what the captured step is made of (kernel / memcpy / memset / event nodes ...)
+        c = torch.ops.tfd.graph_node_types(int(graph.raw_cuda_graph())).tolist()
+        names = ["kernel", "memcpy", "memset", "host", "graph", "empty", "wait_event", "event_record"]
+        print("graph nodes: " + ", ".join(f"{names[i] if i < len(names) else i}={v}" for i, v in enumerate(c) if v),
+              flush=True)
     for _ in range(3):
         graph.replay()
     torch.cuda.synchronize(dev)
