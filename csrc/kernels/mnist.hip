@@ -926,15 +926,18 @@ __device__ __forceinline__ int xcd_grouped_tile(int b, int first, int n) {
 
 
 // ---------------- K13 (LDS-staged): conv2 dgrad + conv1 relu/pool-mask epilogue ----------------
-// Block = (image b, half h: input rows ih in [7h, 7h + 7)), 512 threads, 140.5 KiB LDS. dz2 rows oh
-// in [7h - 2, 7h + 9) are staged into a zero-bordered channel-chunk-major LDS image
-// [8 chunks][11 rows][20 cols] x 16 B (planes padded to 224 px = 256-B multiple) and the whole W2
-// as [tap*32 + ci][co] rows (stride 72): both once, no im2col traffic. dX[p][ci] = sum_{tap,co}
-// dz2[p - tap][co] W2[tap][ci][co]. M-tile = one input row (16 lanes = iw 0..15, 14 valid) so the 16
-// A-fragment lanes read 16 consecutive 16-B slots (conflict-free); N = 32 (2 tiles); K = 1600.
-// Wave w owns M-tiles {w & 3, (w & 3) + 4}, both N-tiles, and taps [0,13) (w < 4) or [13,25):
-// 2 A + 2 B fragment reads per 4 MFMAs; the two K halves are summed through LDS at the end.
+// Block = (image b, half h: input rows ih in [7h, 7h + 7)), 512 threads, 68 KiB LDS. dz2 rows oh
+// in [7h - 2, 7h + 9) are staged once into a zero-bordered channel-chunk-major LDS image
+// [8 chunks][11 rows][20 cols] x 16 B (planes padded to 224 px = 256-B multiple), W2 as
+// [tap*32 + ci][co] rows streams through a two-stage ring; no im2col traffic. dX[p][ci] =
+// sum_{tap,co} dz2[p - tap][co] W2[tap][ci][co]. M-tile = one input row (16 lanes = iw 0..15, 14
+// valid) so the 16 A-fragment lanes read 16 consecutive 16-B slots (conflict-free); N = 32 (2
+// tiles); K = 1600. Wave w owns M-tiles {w & 3, (w & 3) + 4}, both N-tiles, every tap and the co
+// half w >> 2: 2 A + 2 B fragment reads per 4 MFMAs; the two K halves are summed through LDS.
 constexpr int C2D_ROWS = 11, C2D_COLS = 20, C2D_PLANE = 224;
+// threads of a conv2_bwd_lds block (either role): 4 waves, and with both roles' LDS under 80 KB two
+// blocks share a CU, so the launch's 512 blocks are all resident at once
+constexpr int C2B_NT = 256;
 // weight rows (tap, ci) x 64 co, staged by LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no
 // ds_write pass; one wave instruction fills 1 KiB = 8 rows) into an unpadded image whose 16-B chunk
 // c of row r holds global chunk c ^ (r & 7) -- the swizzle is applied to the per-lane SOURCE
@@ -943,7 +946,21 @@ constexpr int C2D_ROWS = 11, C2D_COLS = 20, C2D_PLANE = 224;
 __device__ __forceinline__ const bf16* c2d_w(const bf16* wt, int rr, int ch) {
   return wt + rr * 64 + ((ch ^ (rr & 7)) << 3);
 }
-constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 800 * 64) * 2;  // 131072 B
+// 16-B buffer load at voff + soff bytes (both in range; soff a wave-uniform scalar offset)
+__device__ __forceinline__ uint4 buf_ld_so(const uint16_t* base, uint32_t nbytes, uint32_t voff, uint32_t soff) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)nbytes, 0x00020000);
+  const i32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+  return make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
+}
+// W2 streams through a two-stage LDS ring of C2D_TPS taps (20 KB a stage) instead of staying whole
+// (100 KB): at 69.6 KB two blocks (dgrad or wgrad) share a CU, so the launch's 512 blocks are all
+// resident at once and one block's staging waits overlap the other's MFMA phases
+#ifndef C2D_TPS
+#define C2D_TPS 5
+#endif
+constexpr int C2D_NST = 25 / C2D_TPS, C2D_WSTAGE = C2D_TPS * 32 * 64;  // stages, elements per stage
+static_assert(C2D_NST * C2D_TPS == 25 && C2D_WSTAGE % 512 == 0, "whole W2 stages of 1-KB DMA rows");
+constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 2 * C2D_WSTAGE) * 2;  // 69,632 B
 static_assert(C2D_PLANE * 16 % 256 == 0 && C2D_PLANE >= C2D_ROWS * C2D_COLS, "dz2 plane");
 constexpr int C2D_X_OFF = 8 * C2D_PLANE * 8 * 2;          // 28672: the fused tail's buffers (dead weight region)
 static_assert(4 * 4 * 64 * 16 <= C2D_X_OFF, "park region overlaps the fused tail");
@@ -972,171 +989,167 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
   C2D_STAMP(0);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* img = (bf16*)smem_raw;                           // [8][224][8]
-  bf16* wt = img + 8 * C2D_PLANE * 8;                    // [800][72]
+  bf16* wt = img + 8 * C2D_PLANE * 8;                    // ring: stage s in [s & 1] of [2][C2D_TPS * 32][64]
   const int b = bid >> 1, h = bid & 1, t = threadIdx.x;
   const uint16_t* src = a.dz2 + (size_t)b * 196 * 64;
   const uint16_t* wsrc = a.pbf + OFF_WC2;
   // the tail's x image row: its loads go out before the staging, whose wait then covers them (as a
-  // chain issued after the staging, two dependent round trips held waves 4-7 at the next barrier)
+  // chain issued after the staging, two dependent round trips held the waves at the next barrier)
   const RowPre xr = data_row_pre(a, b);
-  {
-    constexpr int CI = 8 * C2D_PLANE, NI = (CI + 511) / 512;  // 1792 chunks -> 4 per thread
-    {  // 6400 weight chunks = 100 LDS-DMA wave instructions, 12-13 per wave, all in flight at once
-      const int wv = t >> 6, ln = t & 63;
-      for (int ii = wv; ii < 100; ii += 8) {
-        const int p = ii * 64 + ln, rr = p >> 3, sl = p & 7;
-        __builtin_amdgcn_global_load_lds((const void*)(wsrc + rr * 64 + ((sl ^ (rr & 7)) << 3)),
-                                         (__attribute__((address_space(3))) void*)(wt + ii * 64 * 8), 16, 0, 0);
-      }
+  // W2 stage st (taps [st * C2D_TPS, +C2D_TPS): rows tap * 32 + ci) -> ring slot st & 1 by LDS-DMA
+  // (global_load_lds_dwordx4: no VGPR round trip, no ds_write pass; one wave instruction = 8 rows)
+  auto wdma = [&](int st) {
+    constexpr int NI = C2D_WSTAGE / 512;  // wave instructions per stage
+    static_assert(NI % (C2B_NT / 64) == 0, "whole DMA instructions per wave");
+    const int wv = t >> 6, ln = t & 63;
+    const uint16_t* s0 = wsrc + st * C2D_WSTAGE;
+    bf16* d0 = wt + (st & 1) * C2D_WSTAGE;
+#pragma unroll
+    for (int k = 0; k < NI / (C2B_NT / 64); ++k) {
+      const int ii = wv + (C2B_NT / 64) * k, p = ii * 64 + ln, rr = p >> 3, sl = p & 7;
+      __builtin_amdgcn_global_load_lds((const void*)(s0 + rr * 64 + ((sl ^ (rr & 7)) << 3)),
+                                       (__attribute__((address_space(3))) void*)(d0 + ii * 64 * 8), 16, 0, 0);
     }
+  };
+  {
+    constexpr int CI = 8 * C2D_PLANE, NI = CI / C2B_NT;  // 1792 chunks -> 7 per thread
+    static_assert(CI % C2B_NT == 0, "whole image chunks per thread");
+    wdma(0);  // the first two stages of the ring: in flight with the image staging
+    wdma(1);
     uint4 vi[NI];
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      const int i = t + 512 * j, ch = i / C2D_PLANE, px = i - ch * C2D_PLANE;
+      const int i = t + C2B_NT * j, ch = i / C2D_PLANE, px = i - ch * C2D_PLANE;
       const int r = px / C2D_COLS + 7 * h - 2, c = px % C2D_COLS - 2;
-      vi[j] = (i < CI && px < C2D_ROWS * C2D_COLS && (unsigned)r < 14u && (unsigned)c < 14u)
-                  ? *reinterpret_cast<const uint4*>(src + (r * 14 + c) * 64 + ch * 8) : zero4();
+      vi[j] = buf_ld(src, 196 * 64 * 2, (uint32_t)((r * 14 + c) * 64 + ch * 8),
+                     px < C2D_ROWS * C2D_COLS && (unsigned)r < 14u && (unsigned)c < 14u);
     }
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int i = t + 512 * j;
-      if (i < CI) *reinterpret_cast<uint4*>(img + i * 8) = vi[j];
-    }
+    for (int j = 0; j < NI; ++j) *reinterpret_cast<uint4*>(img + (t + C2B_NT * j) * 8) = vi[j];
   }
   C2D_STAMP(1);
-  const int lane = t & 63, w = t >> 6, g = lane >> 4, mt0 = w & 3, kq = w >> 2;
+  const int lane = t & 63, w = t >> 6, g = lane >> 4, mt0 = w;
   const int two = (mt0 + 4 < 7);
   // the conv1-wgrad tail's global operands, issued now and consumed after the K loop (which reads
-  // only LDS), so their latency hides behind it: waves 4-7 the x image and the argmax bytes, waves
-  // 0-3 the conv1 relu outputs that mask their dX rows
+  // only LDS), so their latency hides behind it: the x image, and the conv1 relu outputs and argmax
+  // bytes that mask and place this wave's dX rows
   float xpre[4];
   uint32_t p1pre[2][2][4];  // conv1 relu outputs (bf16 bits) and argmax window positions of the dX
   uint32_t ipb[2][2][4];    // values, 32-bit so the asm uses below can pin them in VGPRs
-  if (kq) {
-    const int u = t - 256;
+  {
     const float* xrow = a.data + (size_t)data_row_use(a, xr, b) * 784;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int i = 4 * u + q, r = i >> 5, c = i & 31;
+      const int i = 4 * t + q, r = i >> 5, c = i & 31;
       xpre[q] = (r >= 2 && r < 30 && c >= 2 && c < 30) ? xrow[(r - 2) * 28 + c - 2] : 0.f;
     }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int x = min(4 * g + r, 13), n = nt * 16 + (lane & 15), ih = 7 * h + min(mt0 + 4 * j, 6);
-          p1pre[j][nt][r] = a.p1[((size_t)b * 196 + ih * 14 + x) * 32 + n];
-          ipb[j][nt][r] = a.idx1[((size_t)b * 196 + ih * 14 + x) * 32 + n];
-        }
   }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int x = min(4 * g + r, 13), n = nt * 16 + (lane & 15), ih = 7 * h + min(mt0 + 4 * j, 6);
+        p1pre[j][nt][r] = a.p1[((size_t)b * 196 + ih * 14 + x) * 32 + n];
+        ipb[j][nt][r] = a.idx1[((size_t)b * 196 + ih * 14 + x) * 32 + n];
+      }
   __syncthreads();
   C2D_STAMP(2);
-  const int iw = lane & 15;
-  int base[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) base[j] = ((mt0 + 4 * j + 4) * C2D_COLS + iw + 4) * 8 + g * C2D_PLANE * 8;
+  const int iw = lane & 15, nl = lane & 15;
   f32x4 acc[2][2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nl = lane & 15;
-  // Fully unrolled, software-pipelined K loop: step st = (tap, co half sk), step st + 1's four
-  // fragments are read while step st's MFMAs run; both M-tiles on every wave (the second tile of
-  // wave 3 reads rows past the image, dropped by the epilogue), and the per-half step count is a
-  // wave-uniform (scalar) branch: the former exec-masked tile branch in a rolled loop waited
-  // lgkmcnt(0) twice per step.
+  // Fully unrolled, software-pipelined K loop: step st = (tap st >> 1, co half st & 1), both M-tiles
+  // (the second tile of wave 3 reads rows past the image, dropped by the epilogue) and both N-tiles;
+  // step st + 1's four fragments are read while step st's MFMAs run. At a stage boundary one barrier
+  // publishes the next W2 stage (its DMA went out a stage earlier) and frees the slot the stage after
+  // it streams into. Per-lane bases sit at the most negative tap shift (kh = kw = 4) and ring slot 0,
+  // so every step's fragment address is a base plus a non-negative constant (the ds_read offset).
   {
-    const int kqu = __builtin_amdgcn_readfirstlane(kq);
-    const int tapb = kqu ? 13 : 0, ns = kqu ? 24 : 26;
+    const bf16* a0 = img + ((mt0 + 4) * C2D_COLS + iw + 4) * 8 + g * C2D_PLANE * 8 - (4 * C2D_COLS + 4) * 8;
+    const bf16* a1 = a0 + 4 * C2D_COLS * 8;
+    const bf16* bw[2][2] = {{c2d_w(wt, nl, g), c2d_w(wt, 16 + nl, g)}, {c2d_w(wt, nl, g + 4), c2d_w(wt, 16 + nl, g + 4)}};
     bf16x8 fb[2][2], fa[2][2];
     auto ld = [&](int st, int slot) {
-      const int tap = tapb + (st >> 1), sk = st & 1;
-      const int kh = tap / 5, kw = tap - kh * 5, coff = -(kh * C2D_COLS + kw) * 8 + sk * 4 * C2D_PLANE * 8;
-      fb[slot][0] = *reinterpret_cast<const bf16x8*>(c2d_w(wt, tap * 32 + nl, g + 4 * sk));
-      fb[slot][1] = *reinterpret_cast<const bf16x8*>(c2d_w(wt, tap * 32 + 16 + nl, g + 4 * sk));
-      fa[slot][0] = *reinterpret_cast<const bf16x8*>(img + base[0] + coff);
-      fa[slot][1] = *reinterpret_cast<const bf16x8*>(img + base[1] + coff);
+      const int tap = st >> 1, sk = st & 1;
+      const int woff = ((tap / C2D_TPS) & 1) * C2D_WSTAGE + (tap % C2D_TPS) * 32 * 64;
+      const int kh = tap / 5, kw = tap - kh * 5, aoff = ((4 - kh) * C2D_COLS + 4 - kw) * 8 + sk * 4 * C2D_PLANE * 8;
+      fb[slot][0] = *reinterpret_cast<const bf16x8*>(bw[sk][0] + woff);
+      fb[slot][1] = *reinterpret_cast<const bf16x8*>(bw[sk][1] + woff);
+      fa[slot][0] = *reinterpret_cast<const bf16x8*>(a0 + aoff);
+      fa[slot][1] = *reinterpret_cast<const bf16x8*>(a1 + aoff);
     };
-    // ns is 24 or 26 (wave-uniform): steps < 24 are unconditional, the last two a scalar branch;
-    // st is a compile-time constant after unrolling, so the fragment slots stay in registers
-    const bool full = ns == 26;
-    if (ns > 0) {
-      ld(0, 0);
+    constexpr int NS = 50, SPS = 2 * C2D_TPS;  // steps, steps per W2 stage
+    ld(0, 0);
 #pragma unroll
-      for (int st = 0; st < 26; ++st) {
-        const int cur = st & 1;
-        if (st + 1 < 24 || (st + 1 < 26 && full)) ld(st + 1, cur ^ 1);
-        if (st < 24 || full) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            acc[j][0] = mfma16x16x32(fa[cur][j], fb[cur][0], acc[j][0]);
-            acc[j][1] = mfma16x16x32(fa[cur][j], fb[cur][1], acc[j][1]);
-          }
+    for (int st = 0; st < NS; ++st) {
+      const int cur = st & 1;
+      if (st + 1 < NS) {
+        if ((st + 1) % SPS == 0) {
+          __syncthreads();
+          if ((st + 1) / SPS + 1 < C2D_NST) wdma((st + 1) / SPS + 1);
         }
+        ld(st + 1, cur ^ 1);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acc[j][0] = mfma16x16x32(fa[cur][j], fb[cur][0], acc[j][0]);
+        acc[j][1] = mfma16x16x32(fa[cur][j], fb[cur][1], acc[j][1]);
       }
     }
   }
-  // sum the two K halves: waves 4..7 park their accumulators in LDS (image region is dead now)
+  // pinned here: wave 3 uses its second M-tile only under a branch (two), and the compiler sank that
+  // tile's 100 MFMAs into it, keeping every step's fragments alive across the loop (400+ spills)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[j][0]), "+v"(acc[j][1]));
   C2D_STAMP(3);
-  __syncthreads();
-  f32x4* park = reinterpret_cast<f32x4*>(smem_raw);  // [4 waves][4 tiles][64 lanes]
-  if (kq) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) park[(mt0 * 4 + j * 2 + nt) * 64 + lane] = acc[j][nt];
-  }
-  for (int i = t; i < (C2D_T_END - C2D_Z_OFF) / 16; i += 512)  // dz1 and the x copies start zero
+  __syncthreads();  // every wave is out of the K loop: the ring region becomes the tail's buffers
+  for (int i = t; i < (C2D_T_END - C2D_Z_OFF) / 16; i += C2B_NT)  // dz1 and the x copies start zero
     reinterpret_cast<uint4*>(smem_raw + C2D_Z_OFF)[i] = zero4();
   __syncthreads();
   C2D_STAMP(4);
   {
     bf16* dz1 = reinterpret_cast<bf16*>(smem_raw + C2D_Z_OFF);
     bf16* xsh = reinterpret_cast<bf16*>(smem_raw + C2D_XS_OFF);
-    if (!kq) {  // dX (+ the parked K half) through conv1's relu mask, scattered to the argmax pixel
-      // the relu / argmax bytes are first touched here: without these empty asm uses the compiler
-      // turned the relu values into compare masks right after their loads, i.e. waves 0-3 waited for
-      // 32 scattered loads before the K loop's barrier instead of behind the K loop
+    // dX through conv1's relu mask, scattered to the argmax pixel. The relu / argmax bytes are first
+    // touched here: without these empty asm uses the compiler turned the relu values into compare
+    // masks right after their loads, i.e. the waves waited for 32 scattered loads before the K loop.
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+      for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(p1pre[j][nt][r]), "+v"(ipb[j][nt][r]));
+        for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(p1pre[j][nt][r]), "+v"(ipb[j][nt][r]));
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if (j == 1 && !two) break;
+    for (int j = 0; j < 2; ++j) {
+      if (j == 1 && !two) break;
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const f32x4 v = acc[j][nt] + park[(mt0 * 4 + j * 2 + nt) * 64 + lane];
-          const int n = nt * 16 + (lane & 15), lr = mt0 + 4 * j;
+      for (int nt = 0; nt < 2; ++nt) {
+        const int n = nt * 16 + (lane & 15), lr = mt0 + 4 * j;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int x = 4 * g + r;
-            if (x >= 14) break;
-            const int wi = ipb[j][nt][r], px = (2 * lr + (wi >> 1)) * 32 + 2 * x + (wi & 1);
-            reinterpret_cast<uint16_t*>(dz1)[c1w_dz(px, n)] = p1pre[j][nt][r] != 0 ? f2bf_bits(v[r]) : (uint16_t)0;
-          }
+        for (int r = 0; r < 4; ++r) {
+          const int x = 4 * g + r;
+          if (x >= 14) break;
+          const int wi = ipb[j][nt][r], px = (2 * lr + (wi >> 1)) * 32 + 2 * x + (wi & 1);
+          reinterpret_cast<uint16_t*>(dz1)[c1w_dz(px, n)] = p1pre[j][nt][r] != 0 ? f2bf_bits(acc[j][nt][r]) : (uint16_t)0;
         }
       }
-    } else {  // x rows 14h .. 14h + 17 of the zero-bordered image, 5 column shifts, bf16
-      const int u = t - 256;
+    }
+    // x rows 14h .. 14h + 17 of the zero-bordered image, 5 column shifts, bf16
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = 4 * u + q, r = i >> 5, c = i & 31, rr = r - 14 * h;
-        if ((unsigned)rr < 18u) {
-          const uint16_t xv = f2bf_bits(xpre[q]);
+    for (int q = 0; q < 4; ++q) {
+      const int i = 4 * t + q, r = i >> 5, c = i & 31, rr = r - 14 * h;
+      if ((unsigned)rr < 18u) {
+        const uint16_t xv = f2bf_bits(xpre[q]);
 #pragma unroll
-          for (int kw = 0; kw < 5; ++kw)
-            if (c >= kw) reinterpret_cast<uint16_t*>(xsh)[(kw * 18 + rr) * 40 + c - kw] = xv;
-        }
+        for (int kw = 0; kw < 5; ++kw)
+          if (c >= kw) reinterpret_cast<uint16_t*>(xsh)[(kw * 18 + rr) * 40 + c - kw] = xv;
       }
     }
     __syncthreads();
     C2D_STAMP(5);
-    const int mi = w & 1, ni = (w >> 1) & 1, kh2 = w >> 2;
+    const int mi = w & 1, ni = w >> 1;  // tap tile (taps 0..15 / 16..31; 25 = bias), channel tile
     const int tap = 16 * mi + (lane & 15), tc = min(tap, 24), tkh = tc / 5, tkw = tc - 5 * tkh;
     const int q = (lane & 15) >> 2, p4 = lane & 3;
     bf16x8 ones, zer;
@@ -1144,38 +1157,32 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
     for (int e = 0; e < 8; ++e) { ones[e] = (bf16)1.0f; zer[e] = (bf16)0.0f; }
     f32x4 c2 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k7 = 0; k7 < 7; ++k7) {
-      const int ks = 7 * kh2 + k7, px0 = ks * 32 + 8 * g, rl = px0 >> 5, col0 = px0 & 31;
+    for (int ks = 0; ks < 14; ++ks) {
+      const int px0 = ks * 32 + 8 * g, rl = px0 >> 5, col0 = px0 & 31;
       bf16x8 af = *reinterpret_cast<const bf16x8*>(xsh + (tkw * 18 + rl + tkh) * 40 + col0);
       if (tap >= 25) af = (tap == 25) ? ones : zer;
       const int row0 = ks * 32 + 8 * g + q, col = 16 * ni + 4 * p4;
       const bf16x8 bfr = frag_tr16(dz1 + c1w_dz(row0, col), dz1 + c1w_dz(row0 + 4, col));
       c2 = mfma16x16x32(af, bfr, c2);
     }
-    f32x4* park2 = reinterpret_cast<f32x4*>(smem_raw);  // the first park is dead (read above)
-    if (kh2) park2[(w & 3) * 64 + lane] = c2;
     C2D_STAMP(6);
-    __syncthreads();
-    if (!kh2) {
-      c2 += park2[(w & 3) * 64 + lane];
-      const int c = 16 * ni + (lane & 15);
+    const int c = 16 * ni + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int to = 16 * mi + 4 * g + r;  // taps 0..24, 25 = bias
-        if (to < 26) a.wg1_slab[(size_t)bid * 832 + to * 32 + c] = c2[r];
-      }
+    for (int r = 0; r < 4; ++r) {
+      const int to = 16 * mi + 4 * g + r;  // taps 0..24, 25 = bias
+      if (to < 26) a.wg1_slab[(size_t)bid * 832 + to * 32 + c] = c2[r];
     }
     C2D_STAMP(7);
   }
 }
 
 // ---------------- K14 (LDS-staged): conv2 wgrad (+ K12 bias row) ----------------
-// Block = (tap group tg, image pair ip), 512 threads; 4 x 64 = 256 blocks at B = 128 (one per CU).
+// Block = (tap group tg, image pair ip), 256 threads; 4 x 64 = 256 blocks at B = 128.
 // Per image: p1 (14x14x32) goes into a zero-bordered LDS image [18][18] x 40 ch and dz2 (196 x 64)
 // into LDS rows [224][72] (pixel rows 196..223 zero); then dW[tap*32 + ci][co] += sum_px
 // p1[px + tap][ci] * dz2[px][co] on MFMA with BOTH fragments read by ds_read_b64_tr_b16 (rows =
 // pixels), so the im2col shift of a tap is just a per-lane row address. Wave w owns ci-tile
-// w >> 2, co-tile w & 3 and every tap of its group. One fp32 slab per image pair (rows of its tap
+// w >> 1, co-tiles 2 (w & 1) and 2 (w & 1) + 1 and every tap of its group. One fp32 slab per image pair (rows of its tap
 // group; tap group 0 also the bias row 800), reduced by the optimizer tail / reduce_conv_grads.
 // Replaces the im2col GEMM that re-read p1 25x through L2 (83 MB -> 19 MB of staging).
 constexpr int C2WL_IMG = 2;      // images per block (= slab count B / C2WL_IMG; 4 x 8 tap groups: +1.7 us)
@@ -1187,7 +1194,7 @@ constexpr int C2WL_CS = 48, C2WL_PW = 18;   // padded image: 18 x 18 positions x
 constexpr int C2WL_DS = 72, C2WL_KP = 224;  // dz2 rows: pixels padded to 7 k-steps of 32
 constexpr int C2WL_IMG_ELEMS = C2WL_PW * C2WL_PW * C2WL_CS;
 constexpr int C2WL_BRED_OFF = (C2WL_IMG_ELEMS + C2WL_KP * C2WL_DS) * 2;
-constexpr int C2WL_SMEM = C2WL_BRED_OFF + 8 * 64 * 4;  // 65408 B: two blocks per CU
+constexpr int C2WL_SMEM = C2WL_BRED_OFF + 4 * 64 * 4;  // 64,384 B
 static_assert(C2WL_BRED_OFF % 16 == 0 && (C2WL_IMG_ELEMS * 2) % 16 == 0, "LDS carve alignment");
 #define C2W_STAMP(k)                                                                                     \
   do {                                                                                                   \
@@ -1198,29 +1205,41 @@ __device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const i
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* img = (bf16*)smem_raw;
   bf16* dz = img + C2WL_IMG_ELEMS;
-  float* bred = reinterpret_cast<float*>(smem_raw + C2WL_BRED_OFF);  // [8][64]
+  float* bred = reinterpret_cast<float*>(smem_raw + C2WL_BRED_OFF);  // [4][64]
   const int tg = bid % C2WL_NTG, ip = bid / C2WL_NTG, t = threadIdx.x;
   const int tap0 = tg * C2WL_TPG, ntaps = (tg == C2WL_NTG - 1) ? 25 - tap0 : C2WL_TPG;
-  const int lane = t & 63, w = t >> 6, h = w >> 2, n = w & 3, g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
-  uint4 v1[2], v2[4];
+  const int lane = t & 63, w = t >> 6, h = w >> 1, n0 = 2 * (w & 1), g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  constexpr int N1 = (784 + C2B_NT - 1) / C2B_NT, N2 = (1568 + C2B_NT - 1) / C2B_NT;  // 16-B chunks per thread
+  uint4 v1[N1], v2[N2];
+  // branch-free buffer loads; chunk j of a thread is 16 t + 4096 j bytes, so the whole chunks share
+  // one offset VGPR with j in the scalar offset (per-j offset VGPRs lived across the MFMA loop and
+  // spilled, and every reload waited for the prefetch in flight), the partial last one range-checked
   auto gload = [&](int b) {
-    const uint4* s1 = reinterpret_cast<const uint4*>(a.p1 + (size_t)b * 196 * 32);
-    const uint4* s2 = reinterpret_cast<const uint4*>(a.dz2 + (size_t)b * 196 * 64);
+    const uint16_t* s1 = a.p1 + (size_t)b * 196 * 32;
+    const uint16_t* s2 = a.dz2 + (size_t)b * 196 * 64;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) { const int i = t + 512 * j; v1[j] = i < 784 ? s1[i] : zero4(); }
+    for (int j = 0; j < N1; ++j) {
+      const int i = t + C2B_NT * j;
+      v1[j] = (C2B_NT * (j + 1) <= 784) ? buf_ld_so(s1, 196 * 32 * 2, 16u * t, 16u * C2B_NT * j)
+                                        : buf_ld(s1, 196 * 32 * 2, 8u * i, i < 784);
+    }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { const int i = t + 512 * j; v2[j] = i < 1568 ? s2[i] : zero4(); }
+    for (int j = 0; j < N2; ++j) {
+      const int i = t + C2B_NT * j;
+      v2[j] = (C2B_NT * (j + 1) <= 1568) ? buf_ld_so(s2, 196 * 64 * 2, 16u * t, 16u * C2B_NT * j)
+                                         : buf_ld(s2, 196 * 64 * 2, 8u * i, i < 1568);
+    }
   };
   if (ip * C2WL_IMG < a.B) gload(ip * C2WL_IMG);  // first image's loads before the LDS zeroing
   // the image border and the dz2 pad rows stay zero for every image of the block
-  for (int i = t; i < C2WL_PW * C2WL_PW; i += 512) {
+  for (int i = t; i < C2WL_PW * C2WL_PW; i += C2B_NT) {
     const int r = i / C2WL_PW, c = i - r * C2WL_PW;
     if (r < 2 || r >= 16 || c < 2 || c >= 16) {
       uint4* d = reinterpret_cast<uint4*>(img + i * C2WL_CS);
       d[0] = zero4(); d[1] = zero4(); d[2] = zero4(); d[3] = zero4();
     }
   }
-  for (int i = t; i < (C2WL_KP - 196) * (C2WL_DS / 8); i += 512) reinterpret_cast<uint4*>(dz + 196 * C2WL_DS)[i] = zero4();
+  for (int i = t; i < (C2WL_KP - 196) * (C2WL_DS / 8); i += C2B_NT) reinterpret_cast<uint4*>(dz + 196 * C2WL_DS)[i] = zero4();
   // padded-image positions of this lane's two tr-read rows (k-slots 32s + 8g + q and +4) per k-step
   int pos[7][2];
 #pragma unroll
@@ -1230,9 +1249,9 @@ __device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const i
       const int k = 32 * s + 8 * g + q + 4 * u;
       pos[s][u] = k < 196 ? (k / 14) * C2WL_PW + (k % 14) : 0;  // pad pixels: dz2 rows are zero
     }
-  f32x4 acc[C2WL_MAXT];
+  f32x4 acc[C2WL_MAXT][2];
 #pragma unroll
-  for (int j = 0; j < C2WL_MAXT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < C2WL_MAXT; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
   // image ii + 1's global loads are issued before image ii's MFMAs, so its staging latency hides
   // under them (one image at a time left the CU idle through each ~37 KB load)
@@ -1241,49 +1260,66 @@ __device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const i
     if (b >= a.B) break;
     __syncthreads();  // the previous image's fragments are consumed
     {
+      int tt = t;  // opaque: the store addresses are recomputed per image, not held across the MFMAs
+      asm volatile("" : "+v"(tt));
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int i = t + 512 * j;
+      for (int j = 0; j < N1; ++j) {
+        const int i = tt + C2B_NT * j;
         if (i < 784) {
           const int px = i >> 2, ch = i & 3, r = px / 14, c = px - r * 14;
           *reinterpret_cast<uint4*>(img + ((r + 2) * C2WL_PW + c + 2) * C2WL_CS + ch * 8) = v1[j];
         }
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int i = t + 512 * j;
+      for (int j = 0; j < N2; ++j) {
+        const int i = tt + C2B_NT * j;
         if (i < 1568) *reinterpret_cast<uint4*>(dz + (i >> 3) * C2WL_DS + (i & 7) * 8) = v2[j];
       }
     }
     __syncthreads();
     C2W_STAMP(1 + 2 * ii);
     if (ii + 1 < C2WL_IMG && b + 1 < a.B) gload(b + 1);
-    if (tg == 0) {  // bias row: column sums of dz2 (pixel slice t >> 6 of 8)
-      for (int px = t >> 6; px < 196; px += 8) bsum += bf2f(dz[px * C2WL_DS + (t & 63)]);
+    if (tg == 0) {  // bias row: column sums of dz2 (pixel slice t >> 6 of 4)
+      static_assert(196 % (C2B_NT / 64) == 0, "whole pixel slices");
+      const bf16* dzc = dz + (t >> 6) * C2WL_DS + (t & 63);
+#pragma unroll 7
+      for (int k = 0; k < 196 / (C2B_NT / 64); ++k) bsum += bf2f(dzc[k * (C2B_NT / 64) * C2WL_DS]);
     }
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
-      const bf16* bp0 = dz + (32 * s + 8 * g + q) * C2WL_DS + 16 * n + 4 * p4;
-      const bf16x8 bfr = frag_tr16(bp0, bp0 + 4 * C2WL_DS);
+      bf16x8 bfr[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16* bp0 = dz + (32 * s + 8 * g + q) * C2WL_DS + 16 * (n0 + u) + 4 * p4;
+        bfr[u] = frag_tr16(bp0, bp0 + 4 * C2WL_DS);
+      }
 #pragma unroll
       for (int j = 0; j < C2WL_MAXT; ++j) {
         if (j < ntaps) {
           const int tap = tap0 + j, toff = (tap / 5) * C2WL_PW + (tap % 5);
           const bf16* a0 = img + (pos[s][0] + toff) * C2WL_CS + 16 * h + 4 * p4;
           const bf16* a1 = img + (pos[s][1] + toff) * C2WL_CS + 16 * h + 4 * p4;
-          acc[j] = mfma16x16x32(frag_tr16(a0, a1), bfr, acc[j]);
+          const bf16x8 af = frag_tr16(a0, a1);
+          acc[j][0] = mfma16x16x32(af, bfr[0], acc[j][0]);
+          acc[j][1] = mfma16x16x32(af, bfr[1], acc[j][1]);
         }
       }
+      __builtin_amdgcn_sched_barrier(0);  // one k-step's fragments live at a time
     }
     C2W_STAMP(2 + 2 * ii);
   }
+#pragma unroll
+  for (int j = 0; j < C2WL_MAXT; ++j) asm volatile("" : "+v"(acc[j][0]), "+v"(acc[j][1]));  // (as the dgrad's)
   float* slab = a.wg2_slab + (size_t)ip * 801 * 64;
 #pragma unroll
   for (int j = 0; j < C2WL_MAXT; ++j) {
     if (j < ntaps) {
       const int tap = tap0 + j;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) slab[(size_t)(tap * 32 + 16 * h + 4 * g + r) * 64 + 16 * n + (lane & 15)] = acc[j][r];
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          slab[(size_t)(tap * 32 + 16 * h + 4 * g + r) * 64 + 16 * (n0 + u) + (lane & 15)] = acc[j][u][r];
     }
   }
   if (tg == 0) {
@@ -1292,17 +1328,18 @@ __device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const i
     if (t < 64) {
       float sm = 0.f;
 #pragma unroll
-      for (int sl = 0; sl < 8; ++sl) sm += bred[sl * 64 + t];
+      for (int sl = 0; sl < C2B_NT / 64; ++sl) sm += bred[sl * 64 + t];
       slab[800 * 64 + t] = sm;
     }
   }
   C2W_STAMP(7);
 }
 
-// conv2 wgrad and dgrad (+ the conv1 wgrad tail) in ONE launch: both consume only dz2, so the
-// dgrad blocks start on each CU as its wgrad block finishes instead of after a kernel boundary
-// (the dgrad's LDS size is the launch's: one block per CU either way). Blocks [0, nw) wgrad.
-__global__ __launch_bounds__(512) void conv2_bwd_lds(MnistStepArgs a, int nw) {
+// conv2 wgrad and dgrad (+ the conv1 wgrad tail) in ONE launch: both consume only dz2. Blocks
+// [0, nw) wgrad, then dgrad; 4-wave blocks at <= 68 KB of LDS and <= 128 VGPRs, two per CU, so all
+// 512 are resident at once and one block's operand waits overlap the other's MFMA / LDS phases
+// (the former 8-wave, 131-KB form ran one block per CU in two serial block waves).
+__global__ __launch_bounds__(C2B_NT, 2) void conv2_bwd_lds(MnistStepArgs a, int nw) {
   if ((int)blockIdx.x < nw) {
     conv2_wgrad_body(a, blockIdx.x);
   } else {
@@ -1604,7 +1641,7 @@ void mnist_backward_b(const MnistStepArgs& a, hipStream_t s) {
   static_assert(C2WL_SMEM <= C2D_SMEM, "conv2_bwd_lds: the dgrad LDS size covers the wgrad blocks");
   set_smem<conv2_bwd_lds>(C2D_SMEM);
   const int nw = C2WL_NTG * a.wg2_splits;
-  conv2_bwd_lds<<<nw + 2 * a.B, 512, C2D_SMEM, s>>>(a, nw);
+  conv2_bwd_lds<<<nw + 2 * a.B, C2B_NT, C2D_SMEM, s>>>(a, nw);
 }
 
 void mnist_conv_grad_reduce(const MnistStepArgs& a, hipStream_t s) {
