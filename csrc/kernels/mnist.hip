@@ -1586,11 +1586,12 @@ __global__ __launch_bounds__(MAD_NT) void mnist_adam_kernel(MnistStepArgs a, Mni
 }
 
 template <auto K>
-inline void set_smem(int bytes) {
-  static bool done = false;
-  if (!done && bytes > 64 * 1024)
+inline void set_smem(int bytes) {  // raise the kernel's dynamic-LDS limit to the largest size asked so far
+  static int limit = 64 * 1024;
+  if (bytes > limit) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(K), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-  done = true;
+    limit = bytes;
+  }
 }
 
 }  // namespace
