@@ -1057,7 +1057,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
   __syncthreads();
   C2D_STAMP(2);
   const int iw = lane & 15, nl = lane & 15;
-  f32x4 acc[2][2];
+  f32x4 acc[2][2];  // this wave's dX tiles (rows mt0, mt0 + 4) x both N-tiles, summed over all of K
 #pragma unroll
   for (int j = 0; j < 2; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   // Fully unrolled, software-pipelined K loop: step st = (tap st >> 1, co half st & 1), both M-tiles
@@ -1177,16 +1177,24 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
 }
 
 // ---------------- K14 (LDS-staged): conv2 wgrad (+ K12 bias row) ----------------
-// Block = (tap group tg, image pair ip), 256 threads; 4 x 64 = 256 blocks at B = 128.
+// Block = (tap group tg, image group ip), 256 threads; 6 x 32 = 192 blocks at B = 128.
 // Per image: p1 (14x14x32) goes into a zero-bordered LDS image [18][18] x 40 ch and dz2 (196 x 64)
 // into LDS rows [224][72] (pixel rows 196..223 zero); then dW[tap*32 + ci][co] += sum_px
 // p1[px + tap][ci] * dz2[px][co] on MFMA with BOTH fragments read by ds_read_b64_tr_b16 (rows =
 // pixels), so the im2col shift of a tap is just a per-lane row address. Wave w owns ci-tile
-// w >> 1, co-tiles 2 (w & 1) and 2 (w & 1) + 1 and every tap of its group. One fp32 slab per image pair (rows of its tap
+// w >> 1, co-tiles 2 (w & 1) and 2 (w & 1) + 1 and every tap of its group. One fp32 slab per image group (rows of its tap
 // group; tap group 0 also the bias row 800), reduced by the optimizer tail / reduce_conv_grads.
 // Replaces the im2col GEMM that re-read p1 25x through L2 (83 MB -> 19 MB of staging).
-constexpr int C2WL_IMG = 2;      // images per block (= slab count B / C2WL_IMG; 4 x 8 tap groups: +1.7 us)
-constexpr int C2WL_NTG = 4;      // tap groups (4: [0,6) [6,12) [12,18) [18,25))
+// Images per block x tap groups (profiles/mnist_conv2_wgrad_grouping_r6.log): 4 x 6 (192 blocks, 32 slabs:
+// the optimizer tail reads 6.6 MB of slabs, not 13.1) 59.0-59.4 us/step; 2 x 4 60.2-60.6; 4 x 8 59.7-60.0.
+#ifndef C2WL_IMG_N
+#define C2WL_IMG_N 4
+#endif
+#ifndef C2WL_NTG_N
+#define C2WL_NTG_N 6
+#endif
+constexpr int C2WL_IMG = C2WL_IMG_N;  // images per block (= slab count B / C2WL_IMG)
+constexpr int C2WL_NTG = C2WL_NTG_N;  // tap groups (6: five of 4 taps, the last 5)
 constexpr int C2WL_TPG = 25 / C2WL_NTG;     // taps per group (the last takes the remainder)
 constexpr int C2WL_MAXT = 25 - C2WL_TPG * (C2WL_NTG - 1);
 constexpr int C2WL_CS = 48, C2WL_PW = 18;   // padded image: 18 x 18 positions x 48-ch stride
@@ -1597,7 +1605,7 @@ inline void set_smem(int bytes) {  // raise the kernel's dynamic-LDS limit to th
 }  // namespace
 
 int mnist_fc1_splits(int B) { (void)B; return FC1_SPLITS; }
-int mnist_wg2_splits(int B) { return (B + C2WL_IMG - 1) / C2WL_IMG; }  // one slab per image pair
+int mnist_wg2_splits(int B) { return (B + C2WL_IMG - 1) / C2WL_IMG; }  // one slab per image group
 
 void mnist_forward(const MnistStepArgs& a, bool train, hipStream_t s) {
   mnist_forward_conv(a, s);
@@ -1637,7 +1645,7 @@ void mnist_backward_a(const MnistStepArgs& a, hipStream_t s, int part) {
 }
 
 void mnist_backward_b(const MnistStepArgs& a, hipStream_t s) {
-  // conv2 wgrad (one slab per image pair), then dgrad + conv1 wgrad, in one launch (a forked wgrad
+  // conv2 wgrad (one slab per image group), then dgrad + conv1 wgrad, in one launch (a forked wgrad
   // stream only contended with dgrad for the CUs: 110 vs 100 us/step, profiles/ab_conv_fork.log)
   static_assert(C2WL_SMEM <= C2D_SMEM, "conv2_bwd_lds: the dgrad LDS size covers the wgrad blocks");
   set_smem<conv2_bwd_lds>(C2D_SMEM);
