@@ -419,7 +419,10 @@ struct SlabEpi {
   }
 };
 constexpr int FC1_BM = 64, FC1_BN = 64, FC1_BK = FC1_BK_;
-constexpr int FC1_SPLITS = 7;  // 3136 = 7 * 448; each split's whole K range staged in one memory round trip
+#ifndef FC1_SPLITS_N
+#define FC1_SPLITS_N 7
+#endif
+constexpr int FC1_SPLITS = FC1_SPLITS_N;  // 3136 = 7 * 448; each split's whole K range staged in one round trip
 constexpr int FC1_NKT = FEAT / FC1_SPLITS / FC1_BK;  // K-tiles per split
 static_assert(FC1_NKT * FC1_BK * FC1_SPLITS == FEAT, "fc1 split-K must tile K exactly");
 __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
