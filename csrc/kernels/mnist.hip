@@ -297,9 +297,11 @@ __global__ __launch_bounds__(512) void conv12_fwd_lds(MnistStepArgs a) {
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
+      for (int jj = 0; jj < 8; ++jj) {  // row 4 read by every lane group, zeroed by a select (an
+        // exec-masked read per element was 10 serial LDS round trips, each with lgkmcnt(0))
+        const float r4 = jj < 5 ? w1[(20 + jj) * C1 + nt * 16 + col] : 0.f;
         bw1[nt][jj] = (bf16)(jj < 5 ? w1[(g * 5 + jj) * C1 + nt * 16 + col] : 0.f);
-        bw2[nt][jj] = (bf16)(jj < 5 && g == 0 ? w1[(20 + jj) * C1 + nt * 16 + col] : 0.f);
+        bw2[nt][jj] = (bf16)(g == 0 ? r4 : 0.f);
       }
     const bf16* x8 = reinterpret_cast<const bf16*>(smem_raw + C12_X8OFF);
     bf16x8 af[MT], af2[MT];

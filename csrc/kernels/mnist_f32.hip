@@ -125,7 +125,10 @@ __global__ __launch_bounds__(512) void f32_conv12_fwd_lds(MnistF32Args a) {
     for (int st = 0; st < 7; ++st) {
       const int k = 4 * st + g;
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) bw[st][nt] = k < KTAPS ? w1[k * C1 + nt * 16 + col] : 0.f;
+      for (int nt = 0; nt < 2; ++nt) {  // clamped read + select: no exec-masked LDS read with its own wait
+        const float wv1 = w1[min(k, KTAPS - 1) * C1 + nt * 16 + col];
+        bw[st][nt] = k < KTAPS ? wv1 : 0.f;
+      }
     }
     const float bias0 = w1[KTAPS * C1 + col], bias1 = w1[KTAPS * C1 + 16 + col];
     int toff[7];
@@ -660,8 +663,14 @@ __device__ __forceinline__ void f32_conv2_dgrad_body(const MnistF32Args& a, int 
 // last 7): one B read feeds 6-7 MFMAs. One fp32 slab per image pair (rows of its tap group; tap group 0
 // also the bias row 800), reduced by the optimizer tail. Image ii + 1's global loads are issued before
 // image ii's MFMAs. Replaces the im2col GEMM that re-read p1 25x through L2.
-constexpr int F2W_NTG = 4, F2W_TPG = 6, F2W_MAXT = 25 - F2W_TPG * (F2W_NTG - 1);  // 7
-constexpr int F2W_IMG = 2, F2W_PW = 18, F2W_CS = 48, F2W_DS = 80;
+#ifndef F2W_NTG_N
+#define F2W_NTG_N 4
+#endif
+#ifndef F2W_IMG_N
+#define F2W_IMG_N 2
+#endif
+constexpr int F2W_NTG = F2W_NTG_N, F2W_TPG = 25 / F2W_NTG, F2W_MAXT = 25 - F2W_TPG * (F2W_NTG - 1);  // 4: 6 / 7
+constexpr int F2W_IMG = F2W_IMG_N, F2W_PW = 18, F2W_CS = 48, F2W_DS = 80;
 constexpr int F2W_IMG_F = F2W_PW * F2W_PW * F2W_CS;        // 15,552 floats
 constexpr int F2W_DZ_F = 196 * F2W_DS;                     // 15,680 floats
 constexpr int F2W_SMEM = (F2W_IMG_F + F2W_DZ_F + 8 * 64) * 4;  // 126,976 B
