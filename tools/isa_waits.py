@@ -6,6 +6,8 @@ merged by a phi, a hoisted compare, a dependent index chain -- shows up before a
 (The round-6 MNIST finds: docs/DESIGN.md §8.)
 
     python tools/isa_waits.py csrc/kernels/mnist.hip [--kernel fc1_fwd] [--lines 400]
+    python tools/isa_waits.py csrc/kernels/mnist.hip --masked   # per kernel: exec-masked loads that wait
+                                                               # inside their branch (each a serial round trip)
 """
 import argparse
 import glob
@@ -27,6 +29,8 @@ def main(argv=None):
     ap.add_argument("src")
     ap.add_argument("--kernel", default="", help="substring of the kernel's mangled name")
     ap.add_argument("--lines", type=int, default=600, help="asm lines scanned per kernel when it has no MFMA")
+    ap.add_argument("--masked", action="store_true", help="count exec-masked branches (s_and_saveexec ... s_or_b64 exec)"
+                    " that hold a load AND a wait: the conv1 weight reads of round 6 were ten of these in a row")
     a = ap.parse_args(argv)
     src = os.path.abspath(a.src)
     with tempfile.TemporaryDirectory() as d:
@@ -36,6 +40,8 @@ def main(argv=None):
         if p.returncode:
             sys.exit(p.stderr[-2000:])
         asm = open(glob.glob(os.path.join(d, "*gfx950*.s"))[0]).read().splitlines()
+    if a.masked:
+        return masked_waits(asm, a.kernel)
     starts = [i for i, ln in enumerate(asm) if re.match(r"^_Z\S+:", ln) and "GLOBAL__N" in ln or
               re.match(r"^_Z\S+:\s", ln)]
     for s in starts:
@@ -55,6 +61,25 @@ def main(argv=None):
             if "load" in t.split()[0]:
                 loads += 1
             print(f"  +{j:5d} [{loads:3d} loads] {t[:90]}")
+
+
+def masked_waits(asm, kernel=""):
+    cur, counts = None, {}
+    for i, ln in enumerate(asm):
+        m = re.match(r"^(_Z\S+):", ln)
+        if m:
+            cur = m.group(1)
+        if cur is None or "s_and_saveexec" not in ln or (kernel and kernel not in cur):
+            continue
+        blk = asm[i:i + 12]
+        end = next((j for j, b in enumerate(blk) if "s_or_b64 exec" in b), None)
+        if end is None:
+            continue
+        inner = "\n".join(blk[:end])
+        if re.search(r"ds_read|global_load|buffer_load", inner) and "s_waitcnt" in inner:
+            counts[cur] = counts.get(cur, 0) + 1
+    for k, v in sorted(counts.items(), key=lambda x: -x[1]):
+        print(f"{v:4d}  {k}")
 
 
 if __name__ == "__main__":
