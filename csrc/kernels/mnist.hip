@@ -421,10 +421,7 @@ struct SlabEpi {
   }
 };
 constexpr int FC1_BM = 64, FC1_BN = 64, FC1_BK = FC1_BK_;
-#ifndef FC1_SPLITS_N
-#define FC1_SPLITS_N 7
-#endif
-constexpr int FC1_SPLITS = FC1_SPLITS_N;  // 3136 = 7 * 448; each split's whole K range staged in one round trip
+constexpr int FC1_SPLITS = 7;  // 3136 = 7 * 448; each split's whole K range in one round trip (14: +0.5 us)
 constexpr int FC1_NKT = FEAT / FC1_SPLITS / FC1_BK;  // K-tiles per split
 static_assert(FC1_NKT * FC1_BK * FC1_SPLITS == FEAT, "fc1 split-K must tile K exactly");
 __global__ __launch_bounds__(256) void fc1_fwd(MnistStepArgs a, int kper) {
@@ -1042,6 +1039,8 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
   uint32_t p1pre[2][2][4];  // conv1 relu outputs (bf16 bits) and argmax window positions of the dX
   uint32_t ipb[2][2][4];    // values, 32-bit so the asm uses below can pin them in VGPRs
   {
+    // (as exec-masked loads each value's bf16 conversion lands in its branch, with vmcnt(0): a
+    // branch-free buffer-load form measured +0.3 us, profiles/mnist_kernels_r6_final.txt)
     const float* xrow = a.data + (size_t)data_row_use(a, xr, b) * 784;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1066,11 +1065,10 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
 #pragma unroll
   for (int j = 0; j < 2; ++j) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   // Fully unrolled, software-pipelined K loop: step st = (tap st >> 1, co half st & 1), both M-tiles
-  // (the second tile of wave 3 reads rows past the image, dropped by the epilogue) and both N-tiles;
-  // step st + 1's four fragments are read while step st's MFMAs run. At a stage boundary one barrier
-  // publishes the next W2 stage (its DMA went out a stage earlier) and frees the slot the stage after
-  // it streams into. Per-lane bases sit at the most negative tap shift (kh = kw = 4) and ring slot 0,
-  // so every step's fragment address is a base plus a non-negative constant (the ds_read offset).
+  // (wave 3's second reads rows past the image, never stored) and both N-tiles; step st + 1's fragments
+  // are read while step st's MFMAs run. A stage boundary's barrier publishes the next W2 stage (DMA'd a
+  // stage earlier) and frees the slot the one after streams into. Bases sit at the most negative tap
+  // shift (kh = kw = 4) and ring slot 0: every address is base + a non-negative constant (ds offset).
   {
     const bf16* a0 = img + ((mt0 + 4) * C2D_COLS + iw + 4) * 8 + g * C2D_PLANE * 8 - (4 * C2D_COLS + 4) * 8;
     const bf16* a1 = a0 + 4 * C2D_COLS * 8;
@@ -1192,14 +1190,8 @@ __device__ __forceinline__ void conv2_dgrad_body(const MnistStepArgs& a, const i
 // Replaces the im2col GEMM that re-read p1 25x through L2 (83 MB -> 19 MB of staging).
 // Images per block x tap groups (profiles/mnist_conv2_wgrad_grouping_r6.log): 4 x 6 (192 blocks, 32 slabs:
 // the optimizer tail reads 6.6 MB of slabs, not 13.1) 59.0-59.4 us/step; 2 x 4 60.2-60.6; 4 x 8 59.7-60.0.
-#ifndef C2WL_IMG_N
-#define C2WL_IMG_N 4
-#endif
-#ifndef C2WL_NTG_N
-#define C2WL_NTG_N 6
-#endif
-constexpr int C2WL_IMG = C2WL_IMG_N;  // images per block (= slab count B / C2WL_IMG)
-constexpr int C2WL_NTG = C2WL_NTG_N;  // tap groups (6: five of 4 taps, the last 5)
+constexpr int C2WL_IMG = 4;  // images per block (= slab count B / C2WL_IMG)
+constexpr int C2WL_NTG = 6;  // tap groups (6: five of 4 taps, the last 5)
 constexpr int C2WL_TPG = 25 / C2WL_NTG;     // taps per group (the last takes the remainder)
 constexpr int C2WL_MAXT = 25 - C2WL_TPG * (C2WL_NTG - 1);
 constexpr int C2WL_CS = 48, C2WL_PW = 18;   // padded image: 18 x 18 positions x 48-ch stride
@@ -1348,10 +1340,9 @@ __device__ __forceinline__ void conv2_wgrad_body(const MnistStepArgs& a, const i
   C2W_STAMP(7);
 }
 
-// conv2 wgrad and dgrad (+ the conv1 wgrad tail) in ONE launch: both consume only dz2. Blocks
-// [0, nw) wgrad, then dgrad; 4-wave blocks at <= 68 KB of LDS and <= 128 VGPRs, two per CU, so all
-// 512 are resident at once and one block's operand waits overlap the other's MFMA / LDS phases
-// (the former 8-wave, 131-KB form ran one block per CU in two serial block waves).
+// conv2 wgrad and dgrad (+ the conv1 wgrad tail) in ONE launch: both consume only dz2. Blocks [0, nw)
+// wgrad, then dgrad; 4-wave blocks at <= 68 KB of LDS, two per CU, all resident at once, so one block's
+// operand waits overlap the other's MFMA / LDS phases (8-wave 131-KB blocks ran in two serial waves).
 __global__ __launch_bounds__(C2B_NT, 2) void conv2_bwd_lds(MnistStepArgs a, int nw) {
   if ((int)blockIdx.x < nw) {
     conv2_wgrad_body(a, blockIdx.x);

@@ -663,14 +663,9 @@ __device__ __forceinline__ void f32_conv2_dgrad_body(const MnistF32Args& a, int 
 // last 7): one B read feeds 6-7 MFMAs. One fp32 slab per image pair (rows of its tap group; tap group 0
 // also the bias row 800), reduced by the optimizer tail. Image ii + 1's global loads are issued before
 // image ii's MFMAs. Replaces the im2col GEMM that re-read p1 25x through L2.
-#ifndef F2W_NTG_N
-#define F2W_NTG_N 4
-#endif
-#ifndef F2W_IMG_N
-#define F2W_IMG_N 2
-#endif
-constexpr int F2W_NTG = F2W_NTG_N, F2W_TPG = 25 / F2W_NTG, F2W_MAXT = 25 - F2W_TPG * (F2W_NTG - 1);  // 4: 6 / 7
-constexpr int F2W_IMG = F2W_IMG_N, F2W_PW = 18, F2W_CS = 48, F2W_DS = 80;
+// 2 images x 4 tap groups: 4 x 4 / 4 x 6 / 4 x 8 / 2 x 6 were +1.6 ... +8.5 us (profiles/mnist_conv2_wgrad_grouping_r6.log)
+constexpr int F2W_NTG = 4, F2W_TPG = 25 / F2W_NTG, F2W_MAXT = 25 - F2W_TPG * (F2W_NTG - 1);  // 6 / 7
+constexpr int F2W_IMG = 2, F2W_PW = 18, F2W_CS = 48, F2W_DS = 80;
 constexpr int F2W_IMG_F = F2W_PW * F2W_PW * F2W_CS;        // 15,552 floats
 constexpr int F2W_DZ_F = 196 * F2W_DS;                     // 15,680 floats
 constexpr int F2W_SMEM = (F2W_IMG_F + F2W_DZ_F + 8 * 64) * 4;  // 126,976 B
