@@ -418,6 +418,11 @@ __device__ __forceinline__ uint4 zero4() { return make_uint4(0u, 0u, 0u, 0u); }
 // load, so the compiler can count loads in flight (register pipelines, RS > 1). nbytes < 2 GiB.
 typedef int i32x4v __attribute__((ext_vector_type(4)));
 constexpr uint32_t kBufOOB = 0xFFFFFFF0u;
+// one byte (relu / mask bits), branch-free: an exec-masked byte load is waited for inside its branch
+__device__ __forceinline__ uint32_t buf_ld_u8(const uint8_t* base, uint32_t nbytes, uint32_t off, bool ok) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)nbytes, 0x00020000);
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, ok ? off : kBufOOB, 0, 0);
+}
 __device__ __forceinline__ uint4 buf_ld(const uint16_t* base, uint32_t nbytes, uint32_t elem_off, bool ok) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)nbytes, 0x00020000);
   const i32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? elem_off * 2u : kBufOOB, 0, 0);

@@ -429,7 +429,7 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
       bool aok = ok;
       const uint32_t ar = add_row(add, orow[c], aok);
       q[c] = buf_ld(add.x, add.abytes ? add.abytes : ybytes, ar * (uint32_t)N + (uint32_t)n, aok);
-      if (add.bits) qb[c] = ok ? add.bits[(size_t)orow[c] * (N / 8) + n / 8] : 0u;
+      if (add.bits) qb[c] = buf_ld_u8(add.bits, ybytes / 16u, orow[c] * (uint32_t)(N / 8) + (uint32_t)(n / 8), ok);
     }
   }
   float* cs = reinterpret_cast<float*>(smem);
@@ -453,7 +453,7 @@ __device__ __forceinline__ void lds_epilogue(f32x4 (&acc)[BM / WM / 16][BN / WN 
       const int m = m0 + g0 + c * E::RG;
       const bool ok = m < M && n < N && orow[c] != kNoRow;
       yq[c] = buf_ld(bs.y, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, ok);
-      if constexpr (BS::MODE == 3) mbits[c] = ok ? bs.bits[(size_t)orow[c] * (N / 8) + n / 8] : 0u;
+      if constexpr (BS::MODE == 3) mbits[c] = buf_ld_u8(bs.bits, ybytes / 16u, orow[c] * (uint32_t)(N / 8) + (uint32_t)(n / 8), ok);
     }
     const int nc = n < N ? n : 0;
 #pragma unroll
@@ -903,11 +903,11 @@ __device__ __forceinline__ void g256_epilogue(f32x16 (&acc)[C::TM][C::TN], char*
         bool aok = ok;
         const uint32_t ar = add_row(add, orow[c], aok);
         q[c] = buf_ld(add.x, add.abytes ? add.abytes : ybytes, ar * (uint32_t)N + (uint32_t)n, aok);
-        if (add.bits) qb[c] = ok ? add.bits[(size_t)orow[c] * (N / 8) + n / 8] : 0u;
+        if (add.bits) qb[c] = buf_ld_u8(add.bits, ybytes / 16u, orow[c] * (uint32_t)(N / 8) + (uint32_t)(n / 8), ok);
       }
       if constexpr (BSTAT) {
         yq[c] = buf_ld(bs.y, ybytes, orow[c] * (uint32_t)N + (uint32_t)n, ok);
-        if constexpr (BS::MODE == 3) mbits[c] = ok ? bs.bits[(size_t)orow[c] * (N / 8) + n / 8] : 0u;
+        if constexpr (BS::MODE == 3) mbits[c] = buf_ld_u8(bs.bits, ybytes / 16u, orow[c] * (uint32_t)(N / 8) + (uint32_t)(n / 8), ok);
       }
     }
     __syncthreads();  // the previous half's chunks (or the mainloop's operands) are consumed
