@@ -83,6 +83,9 @@ def _args(argv):
     ap.add_argument("--lead_steps", type=int, default=0, help="timed region: launch this many one-step graphs "
                     "first, then ONE graph of the remaining steps (the GPU starts on the small launch while the "
                     "host enqueues the big one)")
+    ap.add_argument("--lead_eager", type=int, default=0, help="timed region: launch this many steps as plain "
+                    "kernel launches first, then ONE graph of the remaining steps (the GPU starts on the first "
+                    "kernel while the host writes the graph's packets)")
     ap.add_argument("--spin_sync", type=int, default=0, help="1: after launching the timed steps, poll the end "
                     "event (hipEventQuery) before the closing torch.cuda.synchronize(), so the host notices "
                     "completion without the blocking wait's wake-up latency")
@@ -441,13 +444,15 @@ def _measure(a, ctx, data, labels, sched, wd, label):
     dev, rank = ctx.device, ctx.rank
     wd.phase(f"{label} job setup ({sched}): engine, transport, graph capture", 300)
     lead = max(0, min(a.lead_steps, a.steps - 1)) if not a.eager else 0
-    job = _Job(a, ctx, data, labels, sched, a.graph_steps, extra_graph=(a.steps - lead) if lead else 0)
+    lead_e = max(0, min(a.lead_eager, a.steps - 1)) if not a.eager and not lead else 0
+    job = _Job(a, ctx, data, labels, sched, a.graph_steps,
+               extra_graph=(a.steps - lead - lead_e) if (lead or lead_e) else 0)
     eng, tr, s, run = job.eng, job.tr, job.stream, job.run
     _CUR["tr"] = tr
     wd.phase(f"{label} warm-up ({a.state_steps} state + {a.warmup} steps + {a.min_warmup_ms:.0f} ms)",
              180 + 0.05 * (a.state_steps + a.warmup) + a.min_warmup_ms / 1e3)
     if not job.graph_mode:
-        lead = 0
+        lead = lead_e = 0
     loss0_t = None
     with torch.cuda.stream(s):
         # The timed steps start from the training state after --state_steps steps (a model that is
@@ -514,6 +519,10 @@ def _measure(a, ctx, data, labels, sched, wd, label):
         ev0.record(s)
         if lead:
             eng.replay("train", lead)
+            eng.replay("timed", 1)
+        elif lead_e:
+            for _ in range(lead_e):
+                eng.train_step()
             eng.replay("timed", 1)
         else:
             run(a.steps)
