@@ -965,7 +965,6 @@ static_assert(C2D_NST * C2D_TPS == 25 && C2D_WSTAGE % 512 == 0, "whole W2 stages
 constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 2 * C2D_WSTAGE) * 2;  // 69,632 B
 static_assert(C2D_PLANE * 16 % 256 == 0 && C2D_PLANE >= C2D_ROWS * C2D_COLS, "dz2 plane");
 constexpr int C2D_X_OFF = 8 * C2D_PLANE * 8 * 2;          // 28672: the fused tail's buffers (dead weight region)
-static_assert(4 * 4 * 64 * 16 <= C2D_X_OFF, "park region overlaps the fused tail");
 // The conv1 weight gradient of the tail on the matrix core. dW1[tap][c] =
 // sum_px X[tap][px] dz1[px][c] over the half image's 14 x 28 conv1 output pixels (rows padded to
 // 32, K = 448 = 14 k-steps) with dz1 the unpooled pre-activation gradient (the bf16-rounded pooled

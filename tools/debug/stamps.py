@@ -71,7 +71,7 @@ for k in range(4):
 
 dg = dbg.view(-1, 8).cpu()[5 * B:5 * B + 2 * B]
 if (dg[:, 7] > 0).all():
-    dn = ["issue staging loads", "image LDS stores + barrier", "K loop (MFMA)", "park barrier",
+    dn = ["issue staging loads", "image LDS stores + barrier", "K loop (MFMA)", "barrier + tail LDS zeroing",
           "gsl / x / argmax + barrier", "conv1-wgrad accumulate", "partial reduce + slab store"]
     print("dgrad block span: median", (dg[:, 7] - dg[:, 0]).median().item())
     for k in range(7):
