@@ -963,6 +963,7 @@ __device__ __forceinline__ uint4 buf_ld_so(const uint16_t* base, uint32_t nbytes
 constexpr int C2D_NST = 25 / C2D_TPS, C2D_WSTAGE = C2D_TPS * 32 * 64;  // stages, elements per stage
 static_assert(C2D_NST * C2D_TPS == 25 && C2D_WSTAGE % 512 == 0, "whole W2 stages of 1-KB DMA rows");
 constexpr int C2D_SMEM = (8 * C2D_PLANE * 8 + 2 * C2D_WSTAGE) * 2;  // 69,632 B
+static_assert(2 * C2D_SMEM <= 160 * 1024, "two conv2_bwd_lds blocks share a CU (the launch's point)");
 static_assert(C2D_PLANE * 16 % 256 == 0 && C2D_PLANE >= C2D_ROWS * C2D_COLS, "dz2 plane");
 constexpr int C2D_X_OFF = 8 * C2D_PLANE * 8 * 2;          // 28672: the fused tail's buffers (dead weight region)
 // The conv1 weight gradient of the tail on the matrix core. dW1[tap][c] =
