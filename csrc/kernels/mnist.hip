@@ -34,7 +34,9 @@
 constexpr int GEMM_RS = 2;       // register stages of the LDS-staged GEMM core (csrc/gemm.h)
 constexpr int FDX_BK_ = 128;     // fc1 dX K-tile
 constexpr int FDW_BK_ = 64;      // fc1 dW K-tile
-constexpr int ADAM_U = 2;        // fc-region Adam: strides per lane with all loads issued up front
+// fc-region Adam: strides per lane with all loads issued up front (1: -0.5 us/step against 2 with the
+// round-6 kernels, 4: +0.6; profiles/mnist_conv2_wgrad_grouping_r6.log)
+constexpr int ADAM_U = 1;
 constexpr int FC1_BK_ = 32;      // one-shot fc1: 14 K-tiles of 32 (140 KiB LDS), 0.6 us/step faster than 7 of 64
 
 namespace tfd {
@@ -1450,7 +1452,7 @@ constexpr int MAD_C1F4 = (int)(OFF_WC2 / 4);   // 208
 constexpr int MAD_C2END = (int)(OFF_WD1 / 4);  // 13024
 constexpr int MAD_C1BLK = MAD_C1F4 / 16;       // 13
 constexpr int MAD_C2BLK = (MAD_C2END - MAD_C1F4 + 63) / 64;  // 201
-constexpr int MAD_FC_BLOCKS = 1024;  // grid-stride blocks of the fc-region Adam
+constexpr int MAD_FC_BLOCKS = 1024;  // grid-stride blocks of the fc-region Adam (512 / 2048: within noise)
 constexpr int MAD_CONV = MAD_C1BLK + MAD_C2BLK;
 static_assert(MAD_C1F4 % 16 == 0, "conv1 region: whole blocks");
 constexpr int MAD_SL = 16;  // slab loads in flight per thread
